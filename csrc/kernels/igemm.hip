@@ -1,0 +1,454 @@
+// MFMA implicit-GEMM engine for gfx950: 3x3/1x1 convolutions (forward, data-grad, weight-grad)
+// and dense GEMMs, all on v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+//
+// Why one engine: every hot op of the image-classification path is
+// a GEMM whose operands are either "K-inner" (the reduction index is contiguous in memory: NHWC
+// activations gathered per tap, [N][K] weights) or "K-outer" (the reduction index is the row:
+// weight-grad reductions over pixels, dX = dY·W).  K-inner tiles are staged row-major into a
+// XOR-swizzled LDS image and read with ds_read_b128; K-outer tiles are staged as they sit in
+// memory (coalesced 16-B loads along the non-reduction dim) and transposed for free on the LDS
+// read with ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10).  So conv wgrad and dense
+// dW/dX need no explicit transpose pass, and dgrad reads the forward weights directly with the
+// tap flip folded into the gather.
+//
+// Block = 256 threads = 4 waves (2x2), tile BMxBN, BK = 64; register-staged double-buffered LDS
+// with the async-STAGE split (issue global loads for tile t+1 before the MFMAs of tile t, write
+// LDS after them; one barrier per K-tile).  The MFMA is issued as D = B·A so each lane owns 4
+// consecutive output channels of one output pixel: the epilogue writes 8-byte (bf16) / 16-byte
+// (fp32) vectors straight into the NHWC / [M][N] result, and BatchNorm statistics come out of
+// the accumulators with four lane shuffles (no extra pass over y).
+//
+// Reference parity: replaces the TF/cuDNN conv + dense ops of examples/models/image_classification
+// (TfVgg16.py:115-130, TfFeedForward.py:141-164) and pg_gans `_conv2d`/`_dense`
+// (pg_gans.py:998-1029).  Numerics: fp32 accumulate of bf16 products (tests compare against a
+// PyTorch fp32 reference of the same op).
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+enum OpMode {
+  OP_DENSE_KIN = 0,   // X[i][k], row stride ld                      (weights, dense A)
+  OP_CONV_KIN = 1,    // NHWC gather, tap shift +(kh-1,kw-1)         (conv forward A)
+  OP_CONVT_KIN = 2,   // NHWC gather, tap shift -(kh-1,kw-1)         (conv data-grad A)
+  OP_DENSE_KOUT = 3,  // X[k][i], row stride ld                      (dY in wgrad, W in dX)
+  OP_CONV_KOUT = 4,   // rows = pixels, cols = (tap, c) gathered     (conv weight-grad B)
+  OP_WTAP_KOUT = 5,   // rows = (tap, co), cols = c of W[co][tap][c] (conv data-grad B)
+};
+enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
+enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16,
+             FLAG_LRELU = 32 };
+
+struct IgemmParams {
+  const bf16* A;
+  const bf16* B;
+  void* out;
+  const float* bias;    // [N]
+  float* stats;         // [tilesM*2][2][N] per-wave partial (sum, sumsq) of the fp32 outputs
+  const bf16* gate;     // [M][ldc]: out = gate > 0 ? out : 0 (ReLU backward fused in epilogue)
+  int M, N, K;
+  int lda, ldb, ldc;
+  int H, W, C, taps;    // geometry of the gathered NHWC activation
+  int log2H, log2W, log2C, log2Cb;  // log2Cb: channel count of the tap-major weight rows (dgrad)
+  int P;                // rows of a pixel-indexed K-outer operand
+  int ktPer;            // K-tiles per split (gridDim.z splits)
+  long long slabStride; // elements between split-K slabs
+  int flags;
+  float alpha;          // output scale
+  float slope;          // leaky-relu slope
+};
+
+// ---- LDS images --------------------------------------------------------------------------------
+// K-inner [T][BK] bf16, 128-byte rows, 16-B chunk c of row i lives at chunk (c ^ ((i>>1)&7)):
+// the 16 lanes of each ds_read_b128 lane group hit 16 distinct bank slots.
+RK_DEV int kin_off(int i, int c) { return i * 128 + ((c ^ ((i >> 1) & 7)) << 4); }
+
+// K-outer [BK][T] bf16, T/8 chunks per row; XOR the chunk with a row hash (guide T10 form (b)).
+template <int R>
+RK_DEV int kout_off(int k, int ch) {
+  if constexpr (R == 16) return k * 256 + ((ch ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4);
+  else return k * 128 + ((ch ^ (((k & 3) << 1) | ((k >> 2) & 1))) << 4);
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// Unconditional 16-byte load at base+off (off forced to 0 when !ok) then a bitwise mask: keeps the
+// load unpredicated (no exec branch around it, no per-element vmcnt(0)) and the zero-fill branch-free.
+RK_DEV uint4 masked_load(const bf16* base, long long off, bool ok) {
+  const uint4 v = *(const uint4*)(base + (ok ? off : 0LL));
+  const unsigned m = ok ? 0xffffffffu : 0u;
+  return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+
+template <int MODE, int T>
+struct Operand {
+  static constexpr bool KIN = (MODE == OP_DENSE_KIN || MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN);
+  static constexpr int CH = T * BK / 8 / 256;  // 16-B chunks per thread per K-tile
+  static constexpr int R = T / 8;              // chunks per K-outer row
+  static constexpr int KROWS_PER_PASS = 256 / R;
+
+  const bf16* base;
+  int ldsoff[CH];
+  // K-inner state
+  long long rowoff[CH];
+  int hh[CH], ww[CH];
+  bool rowok[CH];
+  int cchunk;
+  // K-outer state
+  int krow0;
+  int col;
+  bool colok;
+  int dh, dw;  // fixed tap shift (conv K-outer)
+  long long coloff;
+
+  RK_DEV void init(const IgemmParams& p, const bf16* ptr, int ld, int tile0, int extent, int tid) {
+    base = ptr;
+    if constexpr (KIN) {
+      cchunk = tid & 7;
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int r = (tid >> 3) + 32 * i;
+        ldsoff[i] = kin_off(r, cchunk);
+        const int gi = tile0 + r;
+        rowok[i] = gi < extent;
+        const int g = rowok[i] ? gi : 0;
+        if constexpr (MODE == OP_DENSE_KIN) {
+          rowoff[i] = (long long)g * ld;
+          hh[i] = ww[i] = 0;
+        } else {
+          hh[i] = (g >> p.log2W) & (p.H - 1);
+          ww[i] = g & (p.W - 1);
+          rowoff[i] = (long long)g << p.log2C;
+        }
+      }
+    } else {
+      const int ch = tid % R;
+      krow0 = tid / R;
+#pragma unroll
+      for (int i = 0; i < CH; ++i) ldsoff[i] = kout_off<R>(krow0 + KROWS_PER_PASS * i, ch);
+      col = tile0 + ch * 8;
+      colok = col < extent;
+      dh = dw = 0;
+      if constexpr (MODE == OP_CONV_KOUT) {
+        const int tap = col >> p.log2C;
+        colok = colok && tap < p.taps;
+        const int kh = p.taps == 9 ? (tap * 11) >> 5 : 1;  // tap/3 for tap<9
+        const int kw = p.taps == 9 ? tap - 3 * kh : 1;
+        dh = kh - 1;
+        dw = kw - 1;
+        coloff = col & (p.C - 1);
+      } else {
+        coloff = col;
+      }
+    }
+  }
+
+  RK_DEV void load(const IgemmParams& p, int kt, int K, int ld, uint4 (&r)[CH]) const {
+    if constexpr (MODE == OP_DENSE_KIN) {
+      const int k = kt * BK + cchunk * 8;
+      const bool kok = k < K;
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        r[i] = masked_load(base, rowoff[i] + k, kok && rowok[i]);
+      }
+    } else if constexpr (MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN) {
+      const int k = kt * BK + cchunk * 8;
+      const int tap = k >> p.log2C;
+      const int ci = k & (p.C - 1);
+      int dy = 0, dx = 0;
+      if (p.taps == 9) {
+        const int kh = (tap * 11) >> 5;
+        dy = kh - 1;
+        dx = tap - 3 * kh - 1;
+        if constexpr (MODE == OP_CONVT_KIN) { dy = -dy; dx = -dx; }
+      }
+      const bool kok = tap < p.taps;
+      const long long shift = ((long long)(dy * p.W + dx) << p.log2C) + ci;
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int y = hh[i] + dy, x = ww[i] + dx;
+        const bool ok = kok && rowok[i] && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        r[i] = masked_load(base, rowoff[i] + shift, ok);
+      }
+    } else if constexpr (MODE == OP_DENSE_KOUT) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int k = kt * BK + krow0 + KROWS_PER_PASS * i;
+        const bool ok = colok && k < K;
+        r[i] = masked_load(base, coloff + (long long)k * ld, ok);
+      }
+    } else if constexpr (MODE == OP_CONV_KOUT) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int k = kt * BK + krow0 + KROWS_PER_PASS * i;  // pixel index
+        const int h = (k >> p.log2W) & (p.H - 1), w = k & (p.W - 1);
+        const int y = h + dh, x = w + dw;
+        const bool ok = colok && k < K && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        const long long off = ((long long)(k + dh * p.W + dw)) << p.log2C;
+        r[i] = masked_load(base, coloff + off, ok);
+      }
+    } else {  // OP_WTAP_KOUT: row k = tap*Cout + co  ->  W[co][tap][c]
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int k = kt * BK + krow0 + KROWS_PER_PASS * i;
+        const int tap = k >> p.log2Cb, co = k & ((1 << p.log2Cb) - 1);
+        const bool ok = colok && k < K;
+        r[i] = masked_load(base, coloff + (long long)co * ld + (long long)tap * p.N, ok);
+      }
+    }
+  }
+
+  RK_DEV void store(char* lds, const uint4 (&r)[CH]) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *(uint4*)(lds + ldsoff[i]) = r[i];
+  }
+
+  // Fragment of 16 rows (tile-local r0..r0+15) x 32 k (kb..kb+31) for mfma_f32_16x16x32_bf16:
+  // lane l holds X[r0 + (l&15)][kb + 8(l>>4) + j], j = 0..7.
+  static RK_DEV bf16x8 frag(const char* lds, int r0, int kb, int lane) {
+    if constexpr (KIN) {
+      const int i = r0 + (lane & 15);
+      const int c = (kb >> 3) + (lane >> 4);
+      return *(const bf16x8*)(lds + kin_off(i, c));
+    } else {
+      const int g = lane >> 4, ii = lane & 15, q = ii >> 2, pp = ii & 3;
+      const int ch = (r0 >> 3) + (pp >> 1);
+      const int k0 = kb + 8 * g + q;
+      const int a0 = kout_off<R>(k0, ch) + 8 * (pp & 1);
+      const int a1 = kout_off<R>(k0 + 4, ch) + 8 * (pp & 1);
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + a0));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + a1));
+      const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+      bf16x8 f;
+      f[0] = l4[0]; f[1] = l4[1]; f[2] = l4[2]; f[3] = l4[3];
+      f[4] = h4[0]; f[5] = h4[1]; f[6] = h4[2]; f[7] = h4[3];
+      return f;
+    }
+  }
+};
+
+template <int BM, int BN, int AM, int BMODE, int EPI>
+__global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tilesN = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / tilesN, nt = bid - mt * tilesN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kTiles = (p.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * p.ktPer;
+  const int kt1 = min(kTiles, kt0 + p.ktPer);
+
+  Operand<AM, BM> opA;
+  Operand<BMODE, BN> opB;
+  opA.init(p, p.A, p.lda, m0, p.M, tid);
+  opB.init(p, p.B, p.ldb, n0, p.N, tid);
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[Operand<AM, BM>::CH], rb[Operand<BMODE, BN>::CH];
+  if (kt0 < kt1) {
+    opA.load(p, kt0, p.K, p.lda, ra);
+    opB.load(p, kt0, p.K, p.ldb, rb);
+    opA.store(smem, ra);
+    opB.store(smem + A_BYTES, rb);
+  }
+  __syncthreads();
+
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) {
+      opA.load(p, kt + 1, p.K, p.lda, ra);
+      opB.load(p, kt + 1, p.K, p.ldb, rb);
+    }
+    const char* la = smem + cur * (A_BYTES + B_BYTES);
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = Operand<AM, BM>::frag(la, wm * WM + i * 16, ks * 32, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bfr[j] = Operand<BMODE, BN>::frag(lb, wn * WN + j * 16, ks * 32, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* nxt = smem + (cur ^ 1) * (A_BYTES + B_BYTES);
+      opA.store(nxt, ra);
+      opB.store(nxt + A_BYTES, rb);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns out[m][n..n+3] of every (i, j) fragment --------------------------
+  const int mrow = m0 + wm * WM + (lane & 15);
+  const int ncol = n0 + wn * WN + 4 * (lane >> 4);
+  if constexpr (EPI == EPI_BF16) {
+    bf16* C = (bf16*)p.out;
+    float s[NI][4], ss[NI][4];
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[j][e] = ss[j][e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = ncol + j * 16;
+      const bool nok = n < p.N;
+      float b[4] = {0.f, 0.f, 0.f, 0.f};
+      if ((p.flags & FLAG_BIAS) && nok) {
+        const f32x4 bv = *(const f32x4*)(p.bias + n);
+        b[0] = bv[0]; b[1] = bv[1]; b[2] = bv[2]; b[3] = bv[3];
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = mrow + i * 16;
+        if (!(nok && m < p.M)) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] * p.alpha + b[e];
+          s[j][e] += v[e];
+          ss[j][e] += v[e] * v[e];
+        }
+        if (p.flags & FLAG_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (p.flags & FLAG_LRELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope;
+        }
+        if (p.flags & FLAG_GATE) {
+          const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+        *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
+      }
+    }
+    if (p.flags & FLAG_STATS) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = s[j][e], b = ss[j][e];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            a += __shfl_xor(a, o, 64);
+            b += __shfl_xor(b, o, 64);
+          }
+          s[j][e] = a;
+          ss[j][e] = b;
+        }
+      if ((lane & 15) == 0) {
+        float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int n = ncol + j * 16;
+          if (n < p.N) {
+            *(f32x4*)(row + n) = f32x4{s[j][0], s[j][1], s[j][2], s[j][3]};
+            *(f32x4*)(row + p.N + n) = f32x4{ss[j][0], ss[j][1], ss[j][2], ss[j][3]};
+          }
+        }
+      }
+    }
+  } else {
+    float* C = (float*)p.out + (long long)blockIdx.z * p.slabStride;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = ncol + j * 16;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = mrow + i * 16;
+        if (m >= p.M) continue;
+        f32x4 v = acc[i][j] * p.alpha;
+        float* dst = C + (long long)m * p.ldc + n;
+        if (p.flags & FLAG_ACCUM) v += *(const f32x4*)dst;
+        *(f32x4*)dst = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int AM, int BMODE, int EPI>
+int launch_tile(const IgemmParams& p, int splits, hipStream_t st) {
+  const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
+  dim3 grid(tiles, 1, splits);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, AM, BMODE, EPI>), grid, dim3(256), 0, st, p);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+template <int AM, int BMODE, int EPI>
+int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
+  switch (tile) {
+    case 0: return launch_tile<128, 128, AM, BMODE, EPI>(p, splits, st);
+    case 1: return launch_tile<128, 64, AM, BMODE, EPI>(p, splits, st);
+    case 2: return launch_tile<64, 128, AM, BMODE, EPI>(p, splits, st);
+    case 3: return launch_tile<64, 64, AM, BMODE, EPI>(p, splits, st);
+  }
+  return RK_EBADARG;
+}
+
+}  // namespace
+
+// kind: 0 conv-fwd, 1 conv-dgrad, 2 conv-wgrad, 3 dense (A·Bᵀ), 4 dense dX (A·B), 5 dense dW (Aᵀ·B)
+// epi: 0 bf16 out, 1 fp32 out (split-K slabs when splits > 1)
+// tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64
+extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* B, void* C,
+                        const float* bias, float* stats, const void* gate, int M, int N, int K,
+                        int lda, int ldb, int ldc, int H, int W, int Cch, int taps, int Cb,
+                        int splits, long long slabStride, int flags, float alpha, float slope,
+                        void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0) return RK_EBADARG;
+  // K-inner A operands (every kind but the two K-outer x K-outer reductions) need K % 8 == 0
+  if (N % 4 != 0 || (kind != 2 && kind != 5 && K % 8 != 0)) return RK_EUNSUPPORTED;
+  if (taps != 1 && taps != 9) return RK_EBADARG;
+  IgemmParams p{};
+  p.A = (const bf16*)A; p.B = (const bf16*)B; p.out = C; p.bias = bias; p.stats = stats;
+  p.gate = (const bf16*)gate;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.H = H; p.W = W; p.C = Cch; p.taps = taps;
+  p.log2H = rk_log2(H); p.log2W = rk_log2(W); p.log2C = rk_log2(Cch); p.log2Cb = rk_log2(Cb);
+  p.P = M;
+  const int kTiles = rk_cdiv(K, BK);
+  p.ktPer = rk_cdiv(kTiles, splits);
+  p.slabStride = slabStride;
+  p.flags = flags; p.alpha = alpha; p.slope = slope;
+  hipStream_t st = (hipStream_t)stream;
+  const bool conv = kind <= 2;
+  if (conv && (p.log2H < 0 || p.log2W < 0 || p.log2C < 0 || Cch < 8)) return RK_EUNSUPPORTED;
+  if (epi == 0 && splits != 1) return RK_EBADARG;
+  switch (kind) {
+    case 0: if (epi != 0) return RK_EBADARG;
+      return launch_modes<OP_CONV_KIN, OP_DENSE_KIN, EPI_BF16>(tile, p, splits, st);
+    case 1: if (epi != 0 || p.log2Cb < 0) return RK_EUNSUPPORTED;
+      return launch_modes<OP_CONVT_KIN, OP_WTAP_KOUT, EPI_BF16>(tile, p, splits, st);
+    case 2: if (epi != 1) return RK_EBADARG;
+      return launch_modes<OP_DENSE_KOUT, OP_CONV_KOUT, EPI_F32>(tile, p, splits, st);
+    case 3: return epi == 0 ? launch_modes<OP_DENSE_KIN, OP_DENSE_KIN, EPI_BF16>(tile, p, splits, st)
+                            : launch_modes<OP_DENSE_KIN, OP_DENSE_KIN, EPI_F32>(tile, p, splits, st);
+    case 4: return epi == 0 ? launch_modes<OP_DENSE_KIN, OP_DENSE_KOUT, EPI_BF16>(tile, p, splits, st)
+                            : launch_modes<OP_DENSE_KIN, OP_DENSE_KOUT, EPI_F32>(tile, p, splits, st);
+    case 5: if (epi != 1) return RK_EBADARG;
+      return launch_modes<OP_DENSE_KOUT, OP_DENSE_KOUT, EPI_F32>(tile, p, splits, st);
+  }
+  return RK_EBADARG;
+}

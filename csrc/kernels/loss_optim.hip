@@ -1,0 +1,296 @@
+// Loss, optimizer and small streaming kernels for gfx950.
+//
+//  * rk_softmax_xent: fused log-softmax + NLL forward and d(logits) backward in one pass, one wave
+//    per row (64-lane shuffles), optional ignore-index, optional probability output for predict.
+//    Loss and #correct are reduced with a single atomic per wave into device scalars so the whole
+//    training step stays on the GPU (graph-capturable, no host sync per step).
+//  * rk_sgd_step / rk_adam_step: multi-tensor optimizer over ONE flat parameter buffer — fp32
+//    master weights, fp32 grads and state, plus the bf16 compute copy written in the same pass
+//    (so the next forward never needs a separate cast kernel).  16-byte vectors, grid-stride.
+//  * rk_lerp (Gs EMA, pg_gans.py:730-740), rk_nonfinite_count (pg_gans.py:1180-1191),
+//    rk_reduce_slabs (split-K combine), rk_colsum (bias grads), rk_ensemble_mean (predictor).
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits, int ldl,
+                                                           const int* __restrict__ labels, int B, int ncls,
+                                                           int ignore_index, float grad_scale,
+                                                           bf16* __restrict__ dlogits, int ldd,
+                                                           float* __restrict__ probs, float* loss_sum,
+                                                           int* correct, int* counted) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float* lr = logits + (long long)row * ldl;
+  float mx = -INFINITY;
+  int amax = 0;
+  for (int c = lane; c < ncls; c += 64) {
+    const float v = lr[c];
+    if (v > mx) { mx = v; amax = c; }
+  }
+  // wave argmax (first index of the max)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(amax, o, 64);
+    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+  }
+  float se = 0.f;
+  for (int c = lane; c < ncls; c += 64) se += __expf(lr[c] - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  const int y = labels ? labels[row] : -1;
+  const bool valid = labels && y != ignore_index && y >= 0 && y < ncls;
+  if (dlogits) {
+    bf16* dr = dlogits + (long long)row * ldd;
+    for (int c = lane; c < ldd; c += 64) {
+      float g = 0.f;
+      if (valid && c < ncls) g = (__expf(lr[c] - lse) - (c == y ? 1.f : 0.f)) * grad_scale;
+      dr[c] = (bf16)g;
+    }
+  }
+  if (probs) {
+    float* pr = probs + (long long)row * ncls;
+    for (int c = lane; c < ncls; c += 64) pr[c] = __expf(lr[c] - lse);
+  }
+  if (lane == 0 && valid) {
+    if (loss_sum) atomicAdd(loss_sum, lse - lr[y]);
+    if (correct) atomicAdd(correct, amax == y ? 1 : 0);
+    if (counted) atomicAdd(counted, 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, bf16* __restrict__ wb,
+                                                  const float* __restrict__ g, float* __restrict__ mom, long long n,
+                                                  float lr, float momentum, float wd, int nesterov, float gscale,
+                                                  const float* lr_ptr) {
+  const float lrv = lr_ptr ? lr_ptr[0] * lr : lr;
+  const long long n4 = n >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 wv = ((const f32x4*)w)[i];
+    f32x4 gv = ((const f32x4*)g)[i] * gscale + wd * wv;
+    f32x4 d = gv;
+    if (mom) {
+      f32x4 m = ((const f32x4*)mom)[i] * momentum + gv;
+      ((f32x4*)mom)[i] = m;
+      d = nesterov ? gv + momentum * m : m;
+    }
+    wv -= lrv * d;
+    ((f32x4*)w)[i] = wv;
+    if (wb) {
+      bf16x4 o;
+      o[0] = (bf16)wv[0]; o[1] = (bf16)wv[1]; o[2] = (bf16)wv[2]; o[3] = (bf16)wv[3];
+      ((bf16x4*)wb)[i] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* __restrict__ wb,
+                                                   const float* __restrict__ g, float* __restrict__ m,
+                                                   float* __restrict__ v, long long n, float lr, float b1, float b2,
+                                                   float eps, float wd, int decoupled, float c1, float c2,
+                                                   float gscale, const int* skip) {
+  if (skip && skip[0] != 0) return;  // non-finite gradients: skip the update (pg_gans.py:1180-1191)
+  const long long n4 = n >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 wv = ((const f32x4*)w)[i];
+    f32x4 gv = ((const f32x4*)g)[i] * gscale;
+    if (!decoupled) gv += wd * wv;
+    f32x4 mv = ((const f32x4*)m)[i] * b1 + (1.f - b1) * gv;
+    f32x4 vv = ((const f32x4*)v)[i] * b2 + (1.f - b2) * gv * gv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
+    f32x4 upd;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) upd[e] = (mv[e] * c1) / (sqrtf(vv[e] * c2) + eps);
+    if (decoupled) upd += wd * wv;
+    wv -= lr * upd;
+    ((f32x4*)w)[i] = wv;
+    if (wb) {
+      bf16x4 o;
+      o[0] = (bf16)wv[0]; o[1] = (bf16)wv[1]; o[2] = (bf16)wv[2]; o[3] = (bf16)wv[3];
+      ((bf16x4*)wb)[i] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void lerp_kernel(float* __restrict__ dst, const float* __restrict__ src,
+                                                   bf16* __restrict__ dstb, long long n, float t) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    // dst <- src + (dst - src) * t   (tf lerp(a=src, b=dst, t): Gs = lerp(G, Gs, beta))
+    const float s = src[i];
+    const float r = s + (dst[i] - s) * t;
+    dst[i] = r;
+    if (dstb) dstb[i] = (bf16)r;
+  }
+}
+
+__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ x, long long n, int* flag) {
+  int bad = 0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ slab, int S, long long n,
+                                                           float* __restrict__ out, int accumulate, float scale) {
+  const long long n4 = n >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 a = ((const f32x4*)slab)[i];
+    for (int s = 1; s < S; ++s) a += ((const f32x4*)(slab + s * n))[i];
+    a *= scale;
+    if (accumulate) a += ((const f32x4*)out)[i];
+    ((f32x4*)out)[i] = a;
+  }
+}
+
+// column sums of a bf16 [R][C] matrix into fp32 out[C] (bias gradients)
+__global__ __launch_bounds__(256) void colsum_kernel(const bf16* __restrict__ x, int R, int C, int ld,
+                                                     float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int q = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (c < C)
+    for (int r = q; r < R; r += 4) s += (float)x[(long long)r * ld + c];
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && c < C) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    out[c] = accumulate ? out[c] + t : t;
+  }
+}
+
+// mean over models: probs [Wm][Q*C] -> out [Q*C]   (predictor/ensemble.py:10-14 on device)
+__global__ __launch_bounds__(256) void ensemble_mean_kernel(const float* __restrict__ probs, int Wm, long long n,
+                                                            const float* __restrict__ weights, float* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float a = 0.f, ws = 0.f;
+    for (int w = 0; w < Wm; ++w) {
+      const float wt = weights ? weights[w] : 1.f;
+      a += wt * probs[w * n + i];
+      ws += wt;
+    }
+    out[i] = a / ws;
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst,
+                                                            long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = (bf16)src[i];
+}
+
+// uint8/float NCHW images -> bf16 NHWC with channels zero-padded to Cp (input staging, K19):
+// out = (in * scale + shift)
+__global__ __launch_bounds__(256) void pack_nhwc_kernel(const void* __restrict__ src, int is_u8, int N, int C, int H,
+                                                        int W, int Cp, float scale, float shift,
+                                                        bf16* __restrict__ dst) {
+  const long long total = (long long)N * H * W * Cp;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const long long pix = i / Cp;
+    const int w = (int)(pix % W);
+    const long long t = pix / W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float v = 0.f;
+    if (c < C) {
+      const long long si = (((long long)n * C + c) * H + h) * W + w;
+      const float raw = is_u8 ? (float)((const unsigned char*)src)[si] : ((const float*)src)[si];
+      v = raw * scale + shift;
+    }
+    dst[i] = (bf16)v;
+  }
+}
+
+int grid_for(long long work, int cap) {
+  long long g = (work + 255) / 256;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" int rk_softmax_xent(const float* logits, int ldl, const int* labels, int B, int ncls, int ignore_index,
+                               float grad_scale, void* dlogits, int ldd, float* probs, float* loss_sum, int* correct,
+                               int* counted, void* stream) {
+  if (B <= 0) return RK_OK;
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(rk_cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, logits, ldl, labels,
+                     B, ncls, ignore_index, grad_scale, (bf16*)dlogits, ldd, probs, loss_sum, correct, counted);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_sgd_step(float* w, void* wb, const float* g, float* mom, long long n, float lr, float momentum,
+                           float wd, int nesterov, float gscale, const float* lr_ptr, void* stream) {
+  if (n % 4) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4, 4096)), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wb, g, mom,
+                     n, lr, momentum, wd, nesterov, gscale, lr_ptr);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_adam_step(float* w, void* wb, const float* g, float* m, float* v, long long n, float lr, float b1,
+                            float b2, float eps, float wd, int decoupled, float c1, float c2, float gscale,
+                            const int* skip, void* stream) {
+  if (n % 4) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4, 4096)), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wb, g, m,
+                     v, n, lr, b1, b2, eps, wd, decoupled, c1, c2, gscale, skip);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_lerp(float* dst, const float* src, void* dstb, long long n, float t, void* stream) {
+  hipLaunchKernelGGL(lerp_kernel, dim3(grid_for(n, 4096)), dim3(256), 0, (hipStream_t)stream, dst, src, (bf16*)dstb,
+                     n, t);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_nonfinite(const float* x, long long n, int* flag, void* stream) {
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(grid_for(n, 2048)), dim3(256), 0, (hipStream_t)stream, x, n, flag);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_reduce_slabs(const float* slab, int S, long long n, float* out, int accumulate, float scale,
+                               void* stream) {
+  if (n % 4) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(n / 4, 4096)), dim3(256), 0, (hipStream_t)stream, slab, S, n,
+                     out, accumulate, scale);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_colsum(const void* x, int R, int C, int ld, float* out, int accumulate, void* stream) {
+  hipLaunchKernelGGL(colsum_kernel, dim3(rk_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, R, C, ld,
+                     out, accumulate);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_ensemble_mean(const float* probs, int Wm, long long n, const float* weights, float* out,
+                                void* stream) {
+  hipLaunchKernelGGL(ensemble_mean_kernel, dim3(grid_for(n, 2048)), dim3(256), 0, (hipStream_t)stream, probs, Wm, n,
+                     weights, out);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_cast_f32_bf16(const float* src, void* dst, long long n, void* stream) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n, 4096)), dim3(256), 0, (hipStream_t)stream, src, (bf16*)dst,
+                     n);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_pack_nhwc(const void* src, int is_u8, int N, int C, int H, int W, int Cp, float scale, float shift,
+                            void* dst, void* stream) {
+  hipLaunchKernelGGL(pack_nhwc_kernel, dim3(grid_for((long long)N * H * W * Cp, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, src, is_u8, N, C, H, W, Cp, scale, shift, (bf16*)dst);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}

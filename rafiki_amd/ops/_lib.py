@@ -1,0 +1,96 @@
+"""ctypes binding of ``librafiki_kernels.so`` (the hand-written gfx950 HIP kernels).
+
+The library is loaded lazily on first use.  On a GPU process a missing or stale library is a hard
+error (``NativeLibraryError``) — GPU code paths never silently fall back to PyTorch kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from pathlib import Path
+
+_NATIVE = Path(__file__).resolve().parent.parent / "_native"
+KERNEL_LIB = _NATIVE / "librafiki_kernels.so"
+
+_lock = threading.Lock()
+_lib = None
+
+vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
+
+# name -> argtypes (all return int status: 0 ok, <0 error)
+_SIGS = {
+    "rk_igemm": [i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                 i32, i32, i64, i32, f32, f32, vp],
+    "rk_bn_partial_rows": [i64, i32],
+    "rk_channel_stats": [vp, vp, i64, i32, i32, vp],
+    "rk_bn_finalize_fwd": [vp, i32, i32, f64, vp, vp, f32, vp, vp, f32, vp, vp, vp, vp, vp],
+    "rk_bn_eval_coeffs": [i32, vp, vp, vp, vp, f32, vp, vp, vp],
+    "rk_bn_act_fwd": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_bn_finalize_bwd": [vp, i32, i32, f64, vp, vp, vp, vp, vp, vp, i32, vp],
+    "rk_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_softmax_xent": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],
+    "rk_sgd_step": [vp, vp, vp, vp, i64, f32, f32, f32, i32, f32, vp, vp],
+    "rk_adam_step": [vp, vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, f32, f32, vp, vp],
+    "rk_lerp": [vp, vp, vp, i64, f32, vp],
+    "rk_nonfinite": [vp, i64, vp, vp],
+    "rk_reduce_slabs": [vp, i32, i64, vp, i32, f32, vp],
+    "rk_colsum": [vp, i32, i32, i32, vp, i32, vp],
+    "rk_ensemble_mean": [vp, i32, i64, vp, vp, vp],
+    "rk_cast_f32_bf16": [vp, vp, i64, vp],
+    "rk_pack_nhwc": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
+}
+
+_OPTIONAL: set[str] = set()
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def lib():
+    """Return the loaded kernel library (load on first call)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not KERNEL_LIB.exists():
+            raise NativeLibraryError(
+                f"{KERNEL_LIB} is missing: build it with `python -m rafiki_amd._build` "
+                "(the GPU path has no PyTorch fallback)")
+        h = C.CDLL(str(KERNEL_LIB))
+        for name, args in _SIGS.items():
+            try:
+                fn = getattr(h, name)
+            except AttributeError:
+                if name in _OPTIONAL:
+                    continue
+                raise NativeLibraryError(f"{KERNEL_LIB} lacks symbol {name}: rebuild it")
+            fn.argtypes = args
+            fn.restype = C.c_int
+        _lib = h
+        return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except NativeLibraryError:
+        return False
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise KernelError(f"{name} failed with status {rc}")
+
+
+def loaded_path() -> str:
+    return str(KERNEL_LIB)

@@ -1,0 +1,324 @@
+"""Tensor-level wrappers over the gfx950 kernels (no autograd; see ``rafiki_amd.ops.autograd``).
+
+Layout conventions (all device tensors contiguous):
+  * activations  : NHWC bf16 ``[N, H, W, C]`` with C % 8 == 0 (the stem pads RGB to 8 channels)
+  * conv weights : bf16 ``[Cout, kh, kw, Cin]`` (= GEMM B operand ``[N][K]``, K = 9*Cin)
+  * dense weights: bf16 ``[out, in]``
+  * grads of weights and all optimizer state: fp32
+
+Every function launches on ``torch.cuda.current_stream()`` and allocates only through the torch
+caching allocator, so whole training steps can be captured into a hipGraph.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+KIND_CONV_FWD, KIND_CONV_DGRAD, KIND_CONV_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW = range(6)
+FLAG_RELU, FLAG_BIAS, FLAG_STATS, FLAG_GATE, FLAG_ACCUM, FLAG_LRELU = 1, 2, 4, 8, 16, 32
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
+NUM_CU = 256
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def cdiv(a: int, b: int) -> int:
+    return (a + b - 1) // b
+
+
+def pick_tile(M: int, N: int) -> int:
+    """Largest tile that still gives >= 2 blocks per CU without padding waste > 30%."""
+    best, best_blocks = 3, -1
+    for t, (bm, bn) in enumerate(TILES):
+        blocks = cdiv(M, bm) * cdiv(N, bn)
+        waste = (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N)
+        if waste > 1.3 and t != 3:
+            continue
+        if blocks >= 2 * NUM_CU:
+            return t
+        if blocks > best_blocks:
+            best, best_blocks = t, blocks
+    return best
+
+
+def pick_splits(M: int, N: int, K: int, tile: int, target_blocks: int = 2 * NUM_CU, min_ktiles: int = 4) -> int:
+    bm, bn = TILES[tile]
+    tiles = cdiv(M, bm) * cdiv(N, bn)
+    ktiles = cdiv(K, 64)
+    s = max(1, min(cdiv(target_blocks, tiles), ktiles // min_ktiles))
+    # make every split non-empty
+    per = cdiv(ktiles, s)
+    return cdiv(ktiles, per)
+
+
+def igemm(kind, epi, A, B, out, M, N, K, lda=0, ldb=0, ldc=0, *, bias=None, stats=None, gate=None, H=1, W=1,
+          C=8, taps=1, Cb=1, splits=1, slab_stride=0, flags=0, alpha=1.0, slope=0.2, tile=None):
+    if tile is None:
+        tile = pick_tile(M, N)
+    _lib.call("rk_igemm", kind, epi, tile, _p(A), _p(B), _p(out), _p(bias), _p(stats), _p(gate), M, N, K, lda, ldb,
+              ldc, H, W, C, taps, Cb, splits, slab_stride, flags, alpha, slope, _s())
+    return out
+
+
+# ------------------------------------------------------------------------------------------ conv
+def stats_rows(M: int, N: int, tile: Optional[int] = None) -> int:
+    t = pick_tile(M, N) if tile is None else tile
+    return cdiv(M, TILES[t][0]) * 2
+
+
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want_stats=False, act=ACT_NONE,
+             slope=0.2, out=None):
+    """y = conv3x3(x, w) (stride 1, pad 1) [+bias][act]; optional per-channel partial stats."""
+    Nb, H, W, Cin = x.shape
+    Cout = w.shape[0]
+    M, K = Nb * H * W, taps * Cin
+    assert w.numel() == Cout * K, (w.shape, taps, Cin)
+    if out is None:
+        out = torch.empty((Nb, H, W, Cout), device=x.device, dtype=torch.bfloat16)
+    tile = pick_tile(M, Cout)
+    stats = None
+    flags = 0
+    if want_stats:
+        stats = torch.empty((stats_rows(M, Cout, tile), 2, Cout), device=x.device, dtype=torch.float32)
+        flags |= FLAG_STATS
+    if bias is not None:
+        flags |= FLAG_BIAS
+    if act == ACT_RELU:
+        flags |= FLAG_RELU
+    elif act == ACT_LRELU:
+        flags |= FLAG_LRELU
+    igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
+          taps=taps, flags=flags, slope=slope, tile=tile)
+    return (out, stats) if want_stats else out
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, gate=None):
+    Nb, H, W, Cout = dy.shape
+    Cin = w.numel() // (Cout * taps)
+    M, K = Nb * H * W, taps * Cout
+    if out is None:
+        out = torch.empty((Nb, H, W, Cin), device=dy.device, dtype=torch.bfloat16)
+    flags = FLAG_GATE if gate is not None else 0
+    igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, H=H, W=W, C=Cout, taps=taps,
+          Cb=Cout, flags=flags)
+    return out
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, accumulate=False, splits=None):
+    """dW[co][tap][ci] (fp32) = sum over pixels of dy[p][co] * x[shift_tap(p)][ci]."""
+    Nb, H, W, Cout = dy.shape
+    Cin = x.shape[-1]
+    M, N, K = Cout, taps * Cin, Nb * H * W
+    if out is None:
+        out = torch.empty((Cout, N), device=dy.device, dtype=torch.float32)
+    tile = pick_tile(M, N)
+    s = pick_splits(M, N, K, tile) if splits is None else splits
+    if s == 1:
+        igemm(KIND_CONV_WGRAD, 1, dy, x, out, M, N, K, Cout, 0, N, H=H, W=W, C=Cin, taps=taps, splits=1,
+              flags=FLAG_ACCUM if accumulate else 0, tile=tile)
+        return out
+    slab = torch.empty((s, M, N), device=dy.device, dtype=torch.float32)
+    igemm(KIND_CONV_WGRAD, 1, dy, x, slab, M, N, K, Cout, 0, N, H=H, W=W, C=Cin, taps=taps, splits=s,
+          slab_stride=M * N, tile=tile)
+    reduce_slabs(slab, out, accumulate=accumulate)
+    return out
+
+
+# ----------------------------------------------------------------------------------------- dense
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0.2, out_dtype=torch.bfloat16,
+           out=None, alpha=1.0):
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), device=x.device, dtype=out_dtype)
+    flags = (FLAG_BIAS if bias is not None else 0) | (FLAG_RELU if act == ACT_RELU else 0) | (
+        FLAG_LRELU if act == ACT_LRELU else 0)
+    epi = 0 if out.dtype == torch.bfloat16 else 1
+    if epi == 1 and act != ACT_NONE:
+        raise ValueError("fp32 dense output supports no fused activation")
+    if epi == 1 and bias is not None:
+        raise ValueError("fp32 dense output: add bias separately")
+    igemm(KIND_DENSE, epi, x, w, out, M, N, K, x.stride(0), w.stride(0), out.stride(0), bias=bias, flags=flags,
+          slope=slope, alpha=alpha)
+    return out
+
+
+def linear_dx(dy: torch.Tensor, w: torch.Tensor, *, gate=None, out=None):
+    """dx[M][in] = dy[M][out] @ w[out][in]; optional ReLU-backward gate (dx = 0 where gate <= 0)."""
+    M, Nout = dy.shape
+    Nin = w.shape[1]
+    if out is None:
+        out = torch.empty((M, Nin), device=dy.device, dtype=torch.bfloat16)
+    igemm(KIND_DENSE_DX, 0, dy, w, out, M, Nin, Nout, dy.stride(0), w.stride(0), out.stride(0), gate=gate,
+          flags=FLAG_GATE if gate is not None else 0)
+    return out
+
+
+def linear_dw(dy: torch.Tensor, x: torch.Tensor, *, out=None, accumulate=False):
+    """dw[out][in] (fp32) = dy[M][out]^T @ x[M][in]."""
+    M, Nout = dy.shape
+    Nin = x.shape[1]
+    if out is None:
+        out = torch.empty((Nout, Nin), device=dy.device, dtype=torch.float32)
+    tile = pick_tile(Nout, Nin)
+    s = pick_splits(Nout, Nin, M, tile)
+    if s == 1:
+        igemm(KIND_DENSE_DW, 1, dy, x, out, Nout, Nin, M, dy.stride(0), x.stride(0), Nin, splits=1,
+              flags=FLAG_ACCUM if accumulate else 0, tile=tile)
+        return out
+    slab = torch.empty((s, Nout, Nin), device=dy.device, dtype=torch.float32)
+    igemm(KIND_DENSE_DW, 1, dy, x, slab, Nout, Nin, M, dy.stride(0), x.stride(0), Nin, splits=s,
+          slab_stride=Nout * Nin, tile=tile)
+    reduce_slabs(slab, out, accumulate=accumulate)
+    return out
+
+
+# -------------------------------------------------------------------------------------- batchnorm
+def bn_partial_rows(P: int, C: int) -> int:
+    return _lib.lib().rk_bn_partial_rows(P, C)
+
+
+def channel_stats(x2d: torch.Tensor):
+    P, C = x2d.shape
+    rows = bn_partial_rows(P, C)
+    part = torch.empty((rows, 2, C), device=x2d.device, dtype=torch.float32)
+    _lib.call("rk_channel_stats", _p(x2d), _p(part), P, C, rows, _s())
+    return part
+
+
+def bn_finalize_fwd(part, count, gamma, beta, eps, running_mean=None, running_var=None, momentum=0.1, outs=None):
+    R, _, C = part.shape
+    if outs is None:
+        outs = torch.empty((4, C), device=part.device, dtype=torch.float32)
+    mean, rstd, scale, shift = outs[0], outs[1], outs[2], outs[3]
+    _lib.call("rk_bn_finalize_fwd", _p(part), R, C, float(count), _p(gamma), _p(beta), float(eps), _p(running_mean),
+              _p(running_var), float(momentum), _p(mean), _p(rstd), _p(scale), _p(shift), _s())
+    return outs
+
+
+def bn_eval_coeffs(gamma, beta, running_mean, running_var, eps, outs=None):
+    C = running_mean.numel()
+    if outs is None:
+        outs = torch.empty((4, C), device=running_mean.device, dtype=torch.float32)
+    _lib.call("rk_bn_eval_coeffs", C, _p(gamma), _p(beta), _p(running_mean), _p(running_var), float(eps),
+              _p(outs[2]), _p(outs[3]), _s())
+    return outs
+
+
+def bn_act_fwd(y, scale, shift, *, pool=False, act=ACT_RELU, slope=0.2, out=None):
+    Nb, H, W, C = y.shape
+    if out is None:
+        shape = (Nb, H // 2, W // 2, C) if pool else (Nb, H, W, C)
+        out = torch.empty(shape, device=y.device, dtype=torch.bfloat16)
+    _lib.call("rk_bn_act_fwd", _p(y), _p(scale), _p(shift), _p(out), Nb, H, W, C, int(pool), act, float(slope), _s())
+    return out
+
+
+def bn_bwd(dout, y, coeffs, gamma, *, pool=False, act=ACT_RELU, slope=0.2, dgamma=None, dbeta=None, dy=None,
+           accumulate=False):
+    """Backward of out = pool(act(bn(y))).  coeffs = [mean, rstd, scale, shift] rows from forward."""
+    Nb, H, W, C = y.shape
+    P_out = dout.numel() // C
+    rows = bn_partial_rows(P_out, C)
+    part = torch.empty((rows, 2, C), device=y.device, dtype=torch.float32)
+    mean, rstd, scale, shift = coeffs[0], coeffs[1], coeffs[2], coeffs[3]
+    s = _s()
+    _lib.call("rk_bn_bwd_reduce", _p(dout), _p(y), _p(scale), _p(shift), _p(mean), _p(rstd), _p(part), rows, Nb, H,
+              W, C, int(pool), act, float(slope), s)
+    coef = torch.empty((3, C), device=y.device, dtype=torch.float32)
+    _lib.call("rk_bn_finalize_bwd", _p(part), rows, C, float(Nb * H * W), _p(gamma), _p(mean), _p(rstd), _p(dgamma),
+              _p(dbeta), _p(coef), int(accumulate), s)
+    if dy is None:
+        dy = torch.empty_like(y)
+    _lib.call("rk_bn_bwd_apply", _p(dout), _p(y), _p(scale), _p(shift), _p(coef), _p(dy), Nb, H, W, C, int(pool), act,
+              float(slope), s)
+    return dy
+
+
+# ----------------------------------------------------------------------------------- loss / optim
+def softmax_xent(logits, labels, ncls, *, dlogits=None, probs=None, loss_sum=None, correct=None, counted=None,
+                 ignore_index=-100, grad_scale=None):
+    B = logits.shape[0]
+    if grad_scale is None:
+        grad_scale = 1.0 / max(1, B)
+    _lib.call("rk_softmax_xent", _p(logits), logits.stride(0), _p(labels), B, ncls, ignore_index, float(grad_scale),
+              _p(dlogits), 0 if dlogits is None else dlogits.stride(0), _p(probs), _p(loss_sum), _p(correct),
+              _p(counted), _s())
+
+
+def sgd_step(w, g, mom=None, *, wb=None, lr, momentum=0.0, weight_decay=0.0, nesterov=False, grad_scale=1.0,
+             lr_tensor=None):
+    _lib.call("rk_sgd_step", _p(w), _p(wb), _p(g), _p(mom), w.numel(), float(lr), float(momentum),
+              float(weight_decay), int(nesterov), float(grad_scale), _p(lr_tensor), _s())
+
+
+def adam_step(w, g, m, v, *, wb=None, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, decoupled=False,
+              step=1, grad_scale=1.0, skip_flag=None):
+    c1 = 1.0 / (1.0 - beta1 ** step)
+    c2 = 1.0 / (1.0 - beta2 ** step)
+    _lib.call("rk_adam_step", _p(w), _p(wb), _p(g), _p(m), _p(v), w.numel(), float(lr), float(beta1), float(beta2),
+              float(eps), float(weight_decay), int(decoupled), float(c1), float(c2), float(grad_scale),
+              _p(skip_flag), _s())
+
+
+def lerp_(dst, src, t, dst_bf16=None):
+    _lib.call("rk_lerp", _p(dst), _p(src), _p(dst_bf16), dst.numel(), float(t), _s())
+
+
+def nonfinite_flag(x, flag):
+    _lib.call("rk_nonfinite", _p(x), x.numel(), _p(flag), _s())
+
+
+def reduce_slabs(slab, out, *, accumulate=False, scale=1.0):
+    S = slab.shape[0]
+    n = out.numel()
+    _lib.call("rk_reduce_slabs", _p(slab), S, n, _p(out), int(accumulate), float(scale), _s())
+    return out
+
+
+def colsum(x2d, out, *, accumulate=False):
+    R, Cc = x2d.shape
+    _lib.call("rk_colsum", _p(x2d), R, Cc, x2d.stride(0), _p(out), int(accumulate), _s())
+    return out
+
+
+def ensemble_mean(probs, weights=None, out=None):
+    """probs [W, Q, C] fp32 -> mean over W (optionally weighted)."""
+    Wm = probs.shape[0]
+    n = probs[0].numel()
+    if out is None:
+        out = torch.empty(probs.shape[1:], device=probs.device, dtype=torch.float32)
+    _lib.call("rk_ensemble_mean", _p(probs), Wm, n, _p(weights), _p(out), _s())
+    return out
+
+
+def cast_bf16(src, dst):
+    _lib.call("rk_cast_f32_bf16", _p(src), _p(dst), src.numel(), _s())
+    return dst
+
+
+def pack_nhwc(images, cpad=8, scale=1.0, shift=0.0, out=None):
+    """uint8/float32 NCHW -> bf16 NHWC with channels padded to ``cpad``."""
+    Nb, Cc, H, W = images.shape
+    if out is None:
+        out = torch.empty((Nb, H, W, cpad), device=images.device, dtype=torch.bfloat16)
+    is_u8 = 1 if images.dtype == torch.uint8 else 0
+    if not is_u8 and images.dtype != torch.float32:
+        images = images.float()
+    _lib.call("rk_pack_nhwc", _p(images), is_u8, Nb, Cc, H, W, cpad, float(scale), float(shift), _p(out), _s())
+    return out
+
+
+def pad8(n: int) -> int:
+    return int(math.ceil(n / 8.0) * 8)

@@ -1,0 +1,193 @@
+"""Numerics of every hand-written gfx950 kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first, so the reference sees exactly the kernel's operands; the only
+differences left are fp32 accumulation order and the bf16 rounding of outputs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.fixture(scope="module")
+def fn():
+    from rafiki_amd.ops import _lib, functional
+    _lib.lib()  # loud failure if the native library is missing
+    return functional
+
+
+def _nhwc_to_nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _w_to_oihw(w):  # [Cout, 3, 3, Cin] -> [Cout, Cin, 3, 3]
+    return w.permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 64), (2, 16, 16, 8, 64), (3, 4, 4, 128, 256),
+                                            (2, 32, 32, 64, 128), (5, 2, 2, 512, 512)])
+def test_conv_fwd(fn, N, H, W, Cin, Cout):
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    w = (torch.randn(Cout, 3, 3, Cin, device=DEV) / (3 * Cin ** 0.5)).bfloat16()
+    y, stats = fn.conv_fwd(x, w, want_stats=True)
+    ref = F.conv2d(_nhwc_to_nchw(x.float()), _w_to_oihw(w.float()), padding=1).permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-2
+    s = stats.sum(0)
+    assert torch.allclose(s[0], ref.reshape(-1, Cout).sum(0), rtol=1e-3, atol=1e-2 * N * H * W ** 0.5)
+    assert torch.allclose(s[1], (ref ** 2).reshape(-1, Cout).sum(0), rtol=2e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 64), (3, 4, 4, 128, 256), (2, 16, 16, 64, 128)])
+def test_conv_dgrad(fn, N, H, W, Cin, Cout):
+    torch.manual_seed(1)
+    dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    w = (torch.randn(Cout, 3, 3, Cin, device=DEV) / (3 * Cin ** 0.5)).bfloat16()
+    dx = fn.conv_dgrad(dy, w)
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, W), _w_to_oihw(w.float()), _nhwc_to_nchw(dy.float()),
+                                     padding=1).permute(0, 2, 3, 1)
+    assert rel_err(dx, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 64), (2, 16, 16, 8, 64), (3, 4, 4, 128, 256),
+                                            (8, 32, 32, 64, 64)])
+def test_conv_wgrad(fn, N, H, W, Cin, Cout):
+    torch.manual_seed(2)
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    dw = fn.conv_wgrad(dy, x)
+    ref = torch.nn.grad.conv2d_weight(_nhwc_to_nchw(x.float()), (Cout, Cin, 3, 3), _nhwc_to_nchw(dy.float()),
+                                      padding=1).permute(0, 2, 3, 1).reshape(Cout, -1)
+    assert rel_err(dw, ref) < 5e-3
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 2048, 512), (37, 64, 16), (128, 1024, 104), (300, 512, 10 + 6)])
+def test_dense_fwd_bwd(fn, M, K, N):
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=DEV)
+    y = fn.linear(x, w, b, act=fn.ACT_RELU)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    assert rel_err(y, ref) < 1e-2
+    y32 = fn.linear(x, w, out_dtype=torch.float32)
+    assert rel_err(y32, x.float() @ w.float().t()) < 1e-3
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    dx = fn.linear_dx(dy, w)
+    assert rel_err(dx, dy.float() @ w.float()) < 1e-2
+    gate = torch.randn(M, K, device=DEV).bfloat16()
+    dxg = fn.linear_dx(dy, w, gate=gate)
+    assert rel_err(dxg, (dy.float() @ w.float()) * (gate.float() > 0)) < 1e-2
+    dw = fn.linear_dw(dy, x)
+    assert rel_err(dw, dy.float().t() @ x.float()) < 5e-3
+
+
+@pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("N,H,W,C", [(4, 8, 8, 64), (2, 4, 4, 512), (3, 16, 16, 128)])
+def test_bn_relu_pool_fwd_bwd(fn, N, H, W, C, pool):
+    torch.manual_seed(4)
+    y = (torch.randn(N, H, W, C, device=DEV) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    part = fn.channel_stats(y.view(-1, C))
+    coeffs = fn.bn_finalize_fwd(part, N * H * W, gamma, beta, 1e-5, rm, rv, 0.1)
+    out = fn.bn_act_fwd(y, coeffs[2], coeffs[3], pool=pool, act=fn.ACT_RELU)
+    # reference
+    yr = y.float().permute(0, 3, 1, 2).requires_grad_(True)
+    g_ = gamma.clone().requires_grad_(True)
+    b_ = beta.clone().requires_grad_(True)
+    rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    z = F.batch_norm(yr, rm2, rv2, g_, b_, training=True, momentum=0.1, eps=1e-5)
+    a = torch.relu(z)
+    if pool:
+        a = F.max_pool2d(a, 2)
+    ref = a.permute(0, 2, 3, 1)
+    assert rel_err(out, ref) < 1e-2
+    assert torch.allclose(rm, rm2, atol=1e-3) and torch.allclose(rv, rv2, rtol=1e-3, atol=1e-3)
+    dout = torch.randn_like(ref).bfloat16()
+    ref.backward(dout.float())
+    dgamma = torch.zeros(C, device=DEV)
+    dbeta = torch.zeros(C, device=DEV)
+    dy = fn.bn_bwd(dout.contiguous(), y, coeffs, gamma, pool=pool, act=fn.ACT_RELU, dgamma=dgamma, dbeta=dbeta)
+    assert rel_err(dy, yr.grad.permute(0, 2, 3, 1)) < 2e-2
+    assert rel_err(dgamma, g_.grad) < 1e-2
+    assert rel_err(dbeta, b_.grad) < 1e-2
+
+
+def test_softmax_xent(fn):
+    torch.manual_seed(5)
+    B, ncls, ld = 300, 10, 16
+    logits = torch.randn(B, ld, device=DEV) * 3
+    labels = torch.randint(0, ncls, (B,), device=DEV, dtype=torch.int32)
+    dl = torch.empty(B, ld, device=DEV, dtype=torch.bfloat16)
+    loss = torch.zeros(1, device=DEV)
+    correct = torch.zeros(1, device=DEV, dtype=torch.int32)
+    probs = torch.empty(B, ncls, device=DEV)
+    fn.softmax_xent(logits, labels, ncls, dlogits=dl, probs=probs, loss_sum=loss, correct=correct)
+    lr = logits[:, :ncls].clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels.long())
+    ref.backward()
+    assert abs(loss.item() / B - ref.item()) < 1e-4
+    assert rel_err(dl[:, :ncls], lr.grad) < 1e-2
+    assert dl[:, ncls:].float().abs().max().item() == 0
+    assert correct.item() == (lr.argmax(1) == labels).sum().item()
+    assert torch.allclose(probs, torch.softmax(logits[:, :ncls], 1), atol=1e-5)
+
+
+def test_optimizers(fn):
+    torch.manual_seed(6)
+    n = 4096 + 8
+    w = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    wb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    p = torch.nn.Parameter(w.clone())
+    opt = torch.optim.SGD([p], lr=0.1, momentum=0.9, weight_decay=5e-4, nesterov=True)
+    for _ in range(3):
+        p.grad = g.clone()
+        opt.step()
+        fn.sgd_step(w, g, m, wb=wb, lr=0.1, momentum=0.9, weight_decay=5e-4, nesterov=True)
+    assert torch.allclose(w, p.detach(), atol=1e-5)
+    assert torch.equal(wb, w.bfloat16())
+    w2 = torch.randn(n, device=DEV)
+    p2 = torch.nn.Parameter(w2.clone())
+    opt2 = torch.optim.Adam([p2], lr=1e-3, betas=(0.0, 0.99), eps=1e-8)
+    m2, v2 = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    for step in range(1, 4):
+        p2.grad = g.clone()
+        opt2.step()
+        fn.adam_step(w2, g, m2, v2, lr=1e-3, beta1=0.0, beta2=0.99, eps=1e-8, step=step)
+    assert torch.allclose(w2, p2.detach(), atol=1e-6)
+
+
+def test_misc(fn):
+    torch.manual_seed(7)
+    probs = torch.rand(4, 33, 10, device=DEV)
+    assert torch.allclose(fn.ensemble_mean(probs), probs.mean(0), atol=1e-6)
+    a, b = torch.randn(1000, device=DEV), torch.randn(1000, device=DEV)
+    ref = b + (a - b) * 0.99
+    fn.lerp_(a, b, 0.99)
+    assert torch.allclose(a, ref, atol=1e-6)
+    flag = torch.zeros(1, device=DEV, dtype=torch.int32)
+    fn.nonfinite_flag(a, flag)
+    assert flag.item() == 0
+    a[17] = float("nan")
+    fn.nonfinite_flag(a, flag)
+    assert flag.item() == 1
+    x = torch.randn(77, 24, device=DEV).bfloat16()
+    out = torch.empty(24, device=DEV)
+    fn.colsum(x, out)
+    assert torch.allclose(out, x.float().sum(0), atol=1e-3)
+    img = torch.randint(0, 255, (3, 3, 8, 8), device=DEV, dtype=torch.uint8)
+    packed = fn.pack_nhwc(img, 8, 1 / 255.0, 0.0)
+    assert torch.allclose(packed[..., :3].float(), (img.float() / 255).permute(0, 2, 3, 1), atol=4e-3)
+    assert packed[..., 3:].abs().max().item() == 0
