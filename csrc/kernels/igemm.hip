@@ -379,6 +379,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
         const int m = mrow + i * 16;
         if (m >= p.M) continue;
         f32x4 v = acc[i][j] * p.alpha;
+        if (p.flags & FLAG_BIAS) v += *(const f32x4*)(p.bias + n);
         float* dst = C + (long long)m * p.ldc + n;
         if (p.flags & FLAG_ACCUM) v += *(const f32x4*)dst;
         *(f32x4*)dst = v;

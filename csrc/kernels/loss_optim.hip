@@ -90,8 +90,13 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* 
                                                    const float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, long long n, float lr, float b1, float b2,
                                                    float eps, float wd, int decoupled, float c1, float c2,
-                                                   float gscale, const int* skip) {
+                                                   float gscale, const int* skip, const int* step_ptr) {
   if (skip && skip[0] != 0) return;  // non-finite gradients: skip the update (pg_gans.py:1180-1191)
+  if (step_ptr) {  // device-side step counter: bias corrections survive hipGraph replay
+    const float t = (float)step_ptr[0];
+    c1 = 1.f / (1.f - __powf(b1, t));
+    c2 = 1.f / (1.f - __powf(b2, t));
+  }
   const long long n4 = n >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     f32x4 wv = ((const f32x4*)w)[i];
@@ -205,6 +210,8 @@ __global__ __launch_bounds__(256) void pack_nhwc_kernel(const void* __restrict__
   }
 }
 
+__global__ void add_int_kernel(int* p, int v) { if (threadIdx.x == 0) p[0] += v; }
+
 int grid_for(long long work, int cap) {
   long long g = (work + 255) / 256;
   if (g > cap) g = cap;
@@ -235,10 +242,10 @@ extern "C" int rk_sgd_step(float* w, void* wb, const float* g, float* mom, long 
 
 extern "C" int rk_adam_step(float* w, void* wb, const float* g, float* m, float* v, long long n, float lr, float b1,
                             float b2, float eps, float wd, int decoupled, float c1, float c2, float gscale,
-                            const int* skip, void* stream) {
+                            const int* skip, const int* step_ptr, void* stream) {
   if (n % 4) return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4, 4096)), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wb, g, m,
-                     v, n, lr, b1, b2, eps, wd, decoupled, c1, c2, gscale, skip);
+                     v, n, lr, b1, b2, eps, wd, decoupled, c1, c2, gscale, skip, step_ptr);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -291,6 +298,12 @@ extern "C" int rk_pack_nhwc(const void* src, int is_u8, int N, int C, int H, int
                             void* dst, void* stream) {
   hipLaunchKernelGGL(pack_nhwc_kernel, dim3(grid_for((long long)N * H * W * Cp, 8192)), dim3(256), 0,
                      (hipStream_t)stream, src, is_u8, N, C, H, W, Cp, scale, shift, (bf16*)dst);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_add_int(int* p, int v, void* stream) {
+  hipLaunchKernelGGL(add_int_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, p, v);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

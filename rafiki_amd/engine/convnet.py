@@ -1,0 +1,374 @@
+"""Static-graph trainer for BN-ReLU conv nets (VGG-small and friends) on gfx950.
+
+The whole training step — forward, backward, loss, optimizer — is a fixed sequence of hand-written
+kernel launches over pre-planned buffers, captured once into a hipGraph (``torch.cuda.CUDAGraph``
+is hipGraph on ROCm) and replayed per step.  There is no autograd tape and no per-step host work.
+
+Per conv block (conv3x3 -> BatchNorm -> ReLU [-> maxpool2x2]) the step runs
+  fwd : igemm conv (BN partial stats from the accumulators) -> bn finalize -> bn+relu(+pool) apply
+  bwd : bn backward reduce -> finalize (dgamma/dbeta) -> bn backward apply -> conv wgrad (split-K)
+        -> conv dgrad
+then one fused SGD/Adam pass over the flat parameter arena (which also refreshes the bf16 weights).
+
+VGG-small (the BASELINE benchmark architecture; the reference's TfVgg16.py:115-130 is 48x48x3
+VGG16 without BN — SURVEY §7.4 item 8 asks for an explicit definition):
+  input 32x32x3 (zero-padded to 8 channels)
+  [64, 64, M, 128, 128, M, 256, 256, M, 512, 512, M]  conv3x3(pad 1, no bias) + BN + ReLU, M = maxpool 2x2
+  flatten 2x2x512 -> FC 512 + ReLU -> FC num_classes -> softmax cross-entropy
+  = 5.75 M parameters, 0.43 GFLOP forward / image at 32x32 (~1.3 GFLOP / image / train step).
+
+A pure-PyTorch fp32 reference of the same network (``reference_loss``) is the CPU execution path
+and the numerics oracle for GPU tests.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as TF
+
+from ..ops import functional as F
+from .flat import FlatAdam, FlatParams, FlatSGD, init_const, init_kaiming
+
+VGG_SMALL_CFG = (64, 64, 'M', 128, 128, 'M', 256, 256, 'M', 512, 512, 'M')
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+def _is_pow2(n):
+    return n > 0 and (n & (n - 1)) == 0
+
+
+class _BF16Storage(torch.autograd.Function):
+    """Identity whose forward value AND backward gradient are rounded to bf16 — models a tensor
+    the engine stores in bf16 (the activation and its gradient both live in bf16 buffers)."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return t.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+class _BF16Grad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t):
+        return t.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+def _bf16_storage(t):
+    return _BF16Storage.apply(t)
+
+
+def _bf16_grad(t):
+    return _BF16Grad.apply(t)
+
+
+class ConvNetEngine:
+    def __init__(self, num_classes: int = 10, in_channels: int = 3, image_size: int = 32,
+                 cfg: Sequence = VGG_SMALL_CFG, fc_dims: Sequence[int] = (512,), device='cuda', seed: int = 0,
+                 bn_eps: float = 1e-5, bn_momentum: float = 0.1, optimizer: str = 'sgd', lr: float = 0.05,
+                 momentum: float = 0.9, weight_decay: float = 5e-4, nesterov: bool = True,
+                 betas=(0.9, 0.999)):
+        self.device = torch.device(device)
+        self.num_classes, self.in_channels, self.image_size = num_classes, in_channels, image_size
+        self.cin_p = _pad8(in_channels)
+        self.ncls_p = _pad8(num_classes)
+        self.bn_eps, self.bn_momentum = bn_eps, bn_momentum
+        if not _is_pow2(image_size):
+            raise ValueError('image_size must be a power of two (NHWC implicit-GEMM gather)')
+        flat = FlatParams(self.device, seed)
+        self.blocks = []  # (name, cin, cout, pool, H_in)
+        cin, hw, i = self.cin_p, image_size, 0
+        real_cin = in_channels
+        for j, v in enumerate(cfg):
+            if v == 'M':
+                continue
+            pool = j + 1 < len(cfg) and cfg[j + 1] == 'M'
+            name = 'conv{}'.format(i)
+            zero = slice(real_cin, None) if real_cin < cin else None
+            flat.add(name + '.w', (v, 3, 3, cin), init_kaiming(9 * real_cin, zero_in_slice=zero))
+            flat.add(name + '.gamma', (v,), init_const(1.0), decay=False)
+            flat.add(name + '.beta', (v,), init_const(0.0), decay=False)
+            self.blocks.append((name, cin, v, pool, hw))
+            if pool:
+                hw //= 2
+            cin, real_cin, i = v, v, i + 1
+        if hw < 1:
+            raise ValueError('too many pooling stages for image_size {}'.format(image_size))
+        self.feat_hw = hw
+        self.feat_dim = hw * hw * cin
+        self.fcs = []
+        d_in = self.feat_dim
+        for k, d in enumerate(fc_dims):
+            flat.add('fc{}.w'.format(k), (d, d_in), init_kaiming(d_in))
+            flat.add('fc{}.b'.format(k), (d,), init_const(0.0), decay=False)
+            self.fcs.append(('fc{}'.format(k), d_in, d))
+            d_in = d
+        flat.add('out.w', (self.ncls_p, d_in), init_kaiming(d_in, gain=1.0, zero_in_slice=None))
+        flat.add('out.b', (self.ncls_p,), init_const(0.0), decay=False)
+        self.flat = flat.build()
+        with torch.no_grad():  # padded class rows never receive gradient; keep them exactly zero
+            self.flat.w('out.w')[num_classes:].zero_()
+            self.flat.sync_bf16()
+        self.d_last = d_in
+        C = sum(b[2] for b in self.blocks)
+        self.running = torch.zeros((2, C), dtype=torch.float32, device=self.device)
+        self.running[1].fill_(1.0)
+        self._roff = []
+        off = 0
+        for b in self.blocks:
+            self._roff.append(off)
+            off += b[2]
+        if optimizer == 'adam':
+            self.opt = FlatAdam(self.flat, lr, betas=betas, weight_decay=weight_decay, decoupled=True)
+        else:
+            self.opt = FlatSGD(self.flat, lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov)
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.seen = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._graph = None
+        self._graph_batch = None
+        self._static_x = self._static_y = None
+        self._eval_coeffs = None
+
+    # ------------------------------------------------------------------------------- helpers
+    def running_stats(self, bi):
+        o, c = self._roff[bi], self.blocks[bi][2]
+        return self.running[0, o:o + c], self.running[1, o:o + c]
+
+    def flops_per_image(self) -> float:
+        """Forward MACs*2 of the conv + FC layers (train step = 3x)."""
+        fl = 0.0
+        for (_, cin, cout, _, hw) in self.blocks:
+            fl += 2.0 * hw * hw * cout * 9 * cin
+        for (_, di, do) in self.fcs:
+            fl += 2.0 * di * do
+        fl += 2.0 * self.d_last * self.num_classes
+        return fl
+
+    def reset_metrics(self):
+        self.loss_sum.zero_()
+        self.correct.zero_()
+        self.seen.zero_()
+
+    # ----------------------------------------------------------------------------- GPU train
+    def _train_step_gpu(self, x, labels):
+        self._fwd_bwd_gpu(x, labels)
+        self.opt.step()
+
+    def _fwd_bwd_gpu(self, x, labels):
+        """x: [B, H, W, cin_p] bf16 NHWC, labels: [B] int32. Everything stays on-device."""
+        fl = self.flat
+        B = x.shape[0]
+        acts = [x]
+        saved = []
+        h = x
+        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            y, stats = F.conv_fwd(h, fl.wb(name + '.w'), want_stats=True)
+            rm, rv = self.running_stats(bi)
+            coeffs = F.bn_finalize_fwd(stats, B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'), self.bn_eps,
+                                       rm, rv, self.bn_momentum)
+            h = F.bn_act_fwd(y, coeffs[2], coeffs[3], pool=pool, act=F.ACT_RELU)
+            saved.append((y, coeffs))
+            acts.append(h)
+        feat = h.reshape(B, self.feat_dim)
+        fc_in = [feat]
+        z = feat
+        for (name, di, do) in self.fcs:
+            z = F.linear(z, fl.wb(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
+            fc_in.append(z)
+        logits = F.linear(z, fl.wb('out.w'), fl.w('out.b'), out_dtype=torch.float32)
+        dlogits = torch.empty((B, self.ncls_p), dtype=torch.bfloat16, device=self.device)
+        F.softmax_xent(logits, labels, self.num_classes, dlogits=dlogits, loss_sum=self.loss_sum,
+                       correct=self.correct, counted=self.seen)
+        # ---- backward
+        F.linear_dw(dlogits, fc_in[-1], out=fl.g('out.w'))
+        F.colsum(dlogits, fl.g('out.b'))
+        d = dlogits
+        wname = 'out'
+        for k in range(len(self.fcs) - 1, -1, -1):
+            name = self.fcs[k][0]
+            d = F.linear_dx(d, fl.wb(wname + '.w'), gate=fc_in[k + 1])
+            F.linear_dw(d, fc_in[k], out=fl.g(name + '.w'))
+            F.colsum(d, fl.g(name + '.b'))
+            wname = name
+        d = F.linear_dx(d, fl.wb(wname + '.w')).view(B, self.feat_hw, self.feat_hw, -1)
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            name, cin, cout, pool, hw = self.blocks[bi]
+            y, coeffs = saved[bi]
+            dy = F.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), pool=pool, act=F.ACT_RELU,
+                          dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'))
+            F.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
+            if bi > 0:
+                d = F.conv_dgrad(dy, fl.wb(name + '.w'))
+
+    # ------------------------------------------------------------------------ reference path
+    def reference_loss(self, x_nhwc: torch.Tensor, labels: torch.Tensor, params: Optional[dict] = None,
+                       training=True, update_running=False, emulate_bf16=False):
+        """Pure PyTorch fp32 forward of the same network (NCHW internally). Returns (loss, logits).
+
+        ``emulate_bf16`` rounds (straight-through) at exactly the points where the GPU engine stores
+        bf16: weights, conv outputs, block outputs and FC hidden activations — the tight oracle for
+        the kernel path (max-pool argmax routing then agrees with the kernels' bf16 values)."""
+        fl = self.flat
+        P = params if params is not None else {n: fl.w(n) for n in fl.names()}
+        rnd = _bf16_storage if emulate_bf16 else (lambda t: t)
+        rndw = (lambda t: t + (t.bfloat16().float() - t).detach()) if emulate_bf16 else (lambda t: t)
+        h = x_nhwc.float().permute(0, 3, 1, 2)
+        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            w = rndw(P[name + '.w']).permute(0, 3, 1, 2)
+            h = rnd(TF.conv2d(h, w, padding=1))
+            rm, rv = self.running_stats(bi)
+            if training:
+                h = TF.batch_norm(h, rm if update_running else None, rv if update_running else None,
+                                  P[name + '.gamma'], P[name + '.beta'], training=True,
+                                  momentum=self.bn_momentum, eps=self.bn_eps)
+            else:
+                h = TF.batch_norm(h, rm, rv, P[name + '.gamma'], P[name + '.beta'], training=False,
+                                  eps=self.bn_eps)
+            h = torch.relu(h)
+            if pool:
+                h = TF.max_pool2d(h, 2)
+            h = rnd(h)
+        h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)
+        for (name, di, do) in self.fcs:
+            h = rnd(torch.relu(h @ rndw(P[name + '.w']).t() + P[name + '.b']))
+        logits = (h @ rndw(P['out.w']).t() + P['out.b'])[:, :self.num_classes]
+        logits = _bf16_grad(logits) if emulate_bf16 else logits
+        loss = TF.cross_entropy(logits, labels.long()) if labels is not None else None
+        return loss, logits
+
+    def _train_step_cpu(self, x, labels):
+        self._fwd_bwd_cpu(x, labels)
+        self.opt.step()
+
+    def _fwd_bwd_cpu(self, x, labels):
+        fl = self.flat
+        params = {n: fl.w(n).detach().clone().requires_grad_(True) for n in fl.names()}
+        loss, logits = self.reference_loss(x, labels, params, training=True, update_running=True)
+        grads = torch.autograd.grad(loss, [params[n] for n in fl.names()])
+        for n, g in zip(fl.names(), grads):
+            fl.g(n).copy_(g)
+        with torch.no_grad():
+            self.loss_sum += loss.detach() * x.shape[0]
+            self.correct += (logits.argmax(1) == labels.long()).sum().to(torch.int32)
+            self.seen += x.shape[0]
+
+    # --------------------------------------------------------------------------- public API
+    def forward_backward(self, x, labels):
+        """Fill the flat grad buffer (no optimizer step)."""
+        if self.device.type == 'cuda':
+            self._fwd_bwd_gpu(x, labels)
+        else:
+            self._fwd_bwd_cpu(x, labels)
+
+    def train_step(self, x, labels):
+        if self.device.type == 'cuda':
+            self._train_step_gpu(x, labels)
+        else:
+            self._train_step_cpu(x, labels)
+
+    def capture(self, batch_size: int, warmup: int = 2):
+        """Capture one training step on static input buffers into a hipGraph."""
+        if self.device.type != 'cuda':
+            return None
+        self._static_x = torch.zeros((batch_size, self.image_size, self.image_size, self.cin_p),
+                                     dtype=torch.bfloat16, device=self.device)
+        self._static_y = torch.zeros((batch_size,), dtype=torch.int32, device=self.device)
+        # warm the allocator / library outside capture; these steps use zero inputs and are
+        # undone by restoring the parameter state afterwards.
+        snap = [self.flat.master.clone(), self.running.clone()]
+        opt_state = [t.clone() for t in self._opt_tensors()]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._train_step_gpu(self._static_x, self._static_y)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._train_step_gpu(self._static_x, self._static_y)
+        torch.cuda.synchronize()
+        self.flat.master.copy_(snap[0])
+        self.flat.sync_bf16()
+        self.running.copy_(snap[1])
+        for t, v in zip(self._opt_tensors(), opt_state):
+            t.copy_(v)
+        self.reset_metrics()
+        self._graph, self._graph_batch = g, batch_size
+        return g
+
+    def _opt_tensors(self):
+        o = self.opt
+        if isinstance(o, FlatAdam):
+            return [o.m, o.v, o.t]
+        return [o.mom] if o.mom is not None else []
+
+    def step_graph(self, x, labels):
+        """Copy a batch into the static buffers and replay the captured step."""
+        self._static_x.copy_(x)
+        self._static_y.copy_(labels)
+        self._graph.replay()
+
+    # ------------------------------------------------------------------------------ inference
+    def prepare_eval(self):
+        """Fold BN running stats into per-channel scale/shift (inference coefficients)."""
+        fl = self.flat
+        coeffs = []
+        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            rm, rv = self.running_stats(bi)
+            if self.device.type == 'cuda':
+                c = F.bn_eval_coeffs(fl.w(name + '.gamma'), fl.w(name + '.beta'), rm, rv, self.bn_eps)
+            else:
+                r = torch.rsqrt(rv + self.bn_eps)
+                sc = fl.w(name + '.gamma') * r
+                c = torch.stack([rm, r, sc, fl.w(name + '.beta') - rm * sc])
+            coeffs.append(c)
+        self._eval_coeffs = coeffs
+        return coeffs
+
+    @torch.no_grad()
+    def forward_eval(self, x, out_probs=None):
+        """x: [B, H, W, cin_p] bf16 (GPU) or float NHWC (CPU) -> probabilities [B, num_classes] fp32."""
+        if self.device.type != 'cuda':
+            _, logits = self.reference_loss(x, None, training=False)
+            return torch.softmax(logits.float(), 1)
+        if self._eval_coeffs is None:
+            self.prepare_eval()
+        fl = self.flat
+        h = x
+        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            y = F.conv_fwd(h, fl.wb(name + '.w'))
+            c = self._eval_coeffs[bi]
+            h = F.bn_act_fwd(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
+        B = x.shape[0]
+        z = h.reshape(B, self.feat_dim)
+        for (name, di, do) in self.fcs:
+            z = F.linear(z, fl.wb(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
+        logits = F.linear(z, fl.wb('out.w'), fl.w('out.b'), out_dtype=torch.float32)
+        if out_probs is None:
+            out_probs = torch.empty((B, self.num_classes), dtype=torch.float32, device=self.device)
+        F.softmax_xent(logits, None, self.num_classes, probs=out_probs)
+        return out_probs
+
+    # ---------------------------------------------------------------------------- state I/O
+    def state_dict(self):
+        d = self.flat.state_dict()
+        d['__running__'] = self.running.detach().cpu().numpy().copy()
+        return d
+
+    def load_state_dict(self, d):
+        self.flat.load_state_dict(d)
+        if '__running__' in d:
+            self.running.copy_(torch.as_tensor(d['__running__']))
+        self._eval_coeffs = None

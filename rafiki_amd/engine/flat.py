@@ -1,0 +1,221 @@
+"""Flat parameter arena + fused optimizers.
+
+All trainable parameters of a model live in ONE fp32 master buffer (plus a bf16 compute copy and
+an fp32 gradient buffer of the same layout).  Consequences, all deliberate for MI355X:
+  * the optimizer is one streaming kernel over the whole model (multi-tensor for free, §2.4 K9),
+    and it writes the bf16 copy the next forward reads — no separate cast pass;
+  * data-parallel gradient all-reduce is a handful of large contiguous RCCL buckets over the flat
+    grad buffer (``rafiki_amd.parallel.grad_bucket``) instead of one call per tensor
+    (pg_gans.py:1164-1171 does one NCCL all-sum per variable);
+  * a trial's full state is three tensors: cheap to snapshot into the per-GPU HBM param cache.
+
+Parameters with weight decay are laid out first so decay / no-decay are two contiguous ranges.
+Offsets are aligned to 64 elements (256-B fp32 / 128-B bf16 lines).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from ..ops import functional as F
+
+ALIGN = 64
+
+
+@dataclass
+class ParamSpec:
+    name: str
+    shape: Tuple[int, ...]
+    init: Callable[[torch.Tensor, torch.Generator], None]
+    decay: bool = True
+    offset: int = 0
+
+    @property
+    def numel(self):
+        n = 1
+        for s in self.shape:
+            n *= s
+        return n
+
+
+def _align(n):
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def init_normal(std):
+    def f(t, g):
+        t.normal_(0.0, std, generator=g)
+    return f
+
+
+def init_const(v):
+    def f(t, g):
+        t.fill_(v)
+    return f
+
+
+def init_kaiming(fan_in, gain=math.sqrt(2.0), zero_in_slice=None):
+    std = gain / math.sqrt(max(1, fan_in))
+
+    def f(t, g):
+        t.normal_(0.0, std, generator=g)
+        if zero_in_slice is not None:
+            t[..., zero_in_slice] = 0.0
+    return f
+
+
+class FlatParams:
+    def __init__(self, device, seed: int = 0):
+        self.device = torch.device(device)
+        self.seed = seed
+        self.specs: List[ParamSpec] = []
+        self._by_name: Dict[str, ParamSpec] = {}
+        self.master = self.bf16 = self.grad = None
+        self.total = 0
+        self.decay_end = 0
+
+    def add(self, name, shape, init, decay=True):
+        spec = ParamSpec(name, tuple(int(s) for s in shape), init, decay)
+        self.specs.append(spec)
+        self._by_name[name] = spec
+        return spec
+
+    def build(self):
+        ordered = [s for s in self.specs if s.decay] + [s for s in self.specs if not s.decay]
+        off = 0
+        for s in ordered:
+            s.offset = off
+            off += _align(s.numel)
+            if s.decay:
+                self.decay_end = off
+        self.total = _align(max(off, ALIGN))
+        dev = self.device
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        g = torch.Generator(device='cpu')
+        g.manual_seed(self.seed)
+        host = torch.zeros(self.total, dtype=torch.float32)
+        for s in ordered:
+            t = torch.empty(s.shape, dtype=torch.float32)
+            s.init(t, g)
+            host[s.offset:s.offset + s.numel] = t.reshape(-1)
+        self.master.copy_(host)
+        self.bf16 = self.master.to(torch.bfloat16)
+        return self
+
+    # views
+    def _view(self, buf, name):
+        s = self._by_name[name]
+        return buf[s.offset:s.offset + s.numel].view(s.shape)
+
+    def w(self, name):
+        return self._view(self.master, name)
+
+    def wb(self, name):
+        return self._view(self.bf16, name)
+
+    def g(self, name):
+        return self._view(self.grad, name)
+
+    def names(self):
+        return [s.name for s in self.specs]
+
+    def num_params(self):
+        return sum(s.numel for s in self.specs)
+
+    def sync_bf16(self):
+        self.bf16.copy_(self.master)
+
+    def state_dict(self):
+        """{name: float32 numpy array} — picklable, device-independent."""
+        return {s.name: self.w(s.name).detach().float().cpu().numpy().copy() for s in self.specs}
+
+    def load_state_dict(self, d):
+        for s in self.specs:
+            if s.name in d:
+                self.w(s.name).copy_(torch.as_tensor(d[s.name], dtype=torch.float32).reshape(s.shape))
+        self.sync_bf16()
+
+
+class FlatSGD:
+    """SGD (+momentum, +nesterov, decoupled-range weight decay) over a FlatParams arena."""
+
+    def __init__(self, flat: FlatParams, lr, momentum=0.9, weight_decay=5e-4, nesterov=True):
+        self.flat, self.lr, self.momentum, self.wd, self.nesterov = flat, float(lr), float(momentum), float(
+            weight_decay), bool(nesterov)
+        self.mom = torch.zeros_like(flat.master) if momentum > 0 else None
+        # device-side LR multiplier: schedules change it without re-capturing the graph
+        self.lr_scale = torch.ones(1, dtype=torch.float32, device=flat.device)
+
+    def step(self):
+        f = self.flat
+        if f.device.type == 'cuda':
+            ranges = [(0, f.decay_end, self.wd), (f.decay_end, f.total, 0.0)]
+            for a, b, wd in ranges:
+                if b > a:
+                    F.sgd_step(f.master[a:b], f.grad[a:b], None if self.mom is None else self.mom[a:b],
+                               wb=f.bf16[a:b], lr=self.lr, momentum=self.momentum, weight_decay=wd,
+                               nesterov=self.nesterov, lr_tensor=self.lr_scale)
+            return
+        # CPU reference path (same math as sgd_kernel)
+        lr = self.lr * float(self.lr_scale.item())
+        wd = torch.zeros_like(f.master)
+        wd[:f.decay_end] = self.wd
+        g = f.grad + wd * f.master
+        if self.mom is not None:
+            self.mom.mul_(self.momentum).add_(g)
+            d = g + self.momentum * self.mom if self.nesterov else self.mom
+        else:
+            d = g
+        f.master.sub_(lr * d)
+        f.sync_bf16()
+
+    def set_lr_scale(self, s):
+        self.lr_scale.fill_(float(s))
+
+
+class FlatAdam:
+    """Adam / AdamW over a FlatParams arena; step counter lives on the device (graph-safe)."""
+
+    def __init__(self, flat: FlatParams, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False):
+        self.flat, self.lr, self.b1, self.b2, self.eps = flat, float(lr), float(betas[0]), float(betas[1]), float(eps)
+        self.wd, self.decoupled = float(weight_decay), bool(decoupled)
+        self.m = torch.zeros_like(flat.master)
+        self.v = torch.zeros_like(flat.master)
+        self.t = torch.zeros(1, dtype=torch.int32, device=flat.device)
+        self.skip_flag: Optional[torch.Tensor] = None
+
+    def reset_state(self):
+        self.m.zero_()
+        self.v.zero_()
+        self.t.zero_()
+
+    def step(self):
+        f = self.flat
+        if f.device.type == 'cuda':
+            F.add_int_(self.t, 1)
+            for a, b, wd in [(0, f.decay_end, self.wd), (f.decay_end, f.total, 0.0)]:
+                if b > a:
+                    F.adam_step(f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b], wb=f.bf16[a:b], lr=self.lr,
+                                beta1=self.b1, beta2=self.b2, eps=self.eps, weight_decay=wd,
+                                decoupled=self.decoupled, step_tensor=self.t, skip_flag=self.skip_flag)
+            return
+        if self.skip_flag is not None and int(self.skip_flag.item()) != 0:
+            return
+        self.t += 1
+        t = int(self.t.item())
+        wd = torch.zeros_like(f.master)
+        wd[:f.decay_end] = self.wd
+        g = f.grad if self.decoupled else f.grad + wd * f.master
+        self.m.mul_(self.b1).add_((1 - self.b1) * g)
+        self.v.mul_(self.b2).add_((1 - self.b2) * g * g)
+        c1 = 1.0 / (1.0 - self.b1 ** t) if self.b1 > 0 else 1.0
+        c2 = 1.0 / (1.0 - self.b2 ** t)
+        upd = (self.m * c1) / ((self.v * c2).sqrt() + self.eps)
+        if self.decoupled:
+            upd = upd + wd * f.master
+        f.master.sub_(self.lr * upd)
+        f.sync_bf16()

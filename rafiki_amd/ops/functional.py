@@ -147,8 +147,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0
     epi = 0 if out.dtype == torch.bfloat16 else 1
     if epi == 1 and act != ACT_NONE:
         raise ValueError("fp32 dense output supports no fused activation")
-    if epi == 1 and bias is not None:
-        raise ValueError("fp32 dense output: add bias separately")
     igemm(KIND_DENSE, epi, x, w, out, M, N, K, x.stride(0), w.stride(0), out.stride(0), bias=bias, flags=flags,
           slope=slope, alpha=alpha)
     return out
@@ -264,12 +262,18 @@ def sgd_step(w, g, mom=None, *, wb=None, lr, momentum=0.0, weight_decay=0.0, nes
 
 
 def adam_step(w, g, m, v, *, wb=None, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, decoupled=False,
-              step=1, grad_scale=1.0, skip_flag=None):
-    c1 = 1.0 / (1.0 - beta1 ** step)
+              step=1, grad_scale=1.0, skip_flag=None, step_tensor=None):
+    """Adam/AdamW.  ``step_tensor`` (device int32, already incremented) overrides ``step`` so the
+    bias corrections stay right under hipGraph replay."""
+    c1 = 1.0 / (1.0 - beta1 ** step) if beta1 > 0 else 1.0
     c2 = 1.0 / (1.0 - beta2 ** step)
     _lib.call("rk_adam_step", _p(w), _p(wb), _p(g), _p(m), _p(v), w.numel(), float(lr), float(beta1), float(beta2),
               float(eps), float(weight_decay), int(decoupled), float(c1), float(c2), float(grad_scale),
-              _p(skip_flag), _s())
+              _p(skip_flag), _p(step_tensor), _s())
+
+
+def add_int_(t, v=1):
+    _lib.call("rk_add_int", _p(t), int(v), _s())
 
 
 def lerp_(dst, src, t, dst_bf16=None):
