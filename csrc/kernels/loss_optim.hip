@@ -150,6 +150,28 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restri
   }
 }
 
+// Stage-1 parallel row reduction: in [R][W] fp32 -> out [G][W], block (x, g) sums its slice of rows
+// for 256 consecutive columns (coalesced).  Turns the serial "sum thousands of partial rows" tails
+// of BN finalize / split-K combine into a chip-wide pass; stage 2 then reads only G rows.
+__global__ __launch_bounds__(256) void rows_reduce_kernel(const float* __restrict__ in, int R, long long W,
+                                                          float* __restrict__ out) {
+  const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (c >= W) return;
+  const int G = gridDim.y, g = blockIdx.y;
+  const int per = (R + G - 1) / G;
+  const int r0 = g * per, r1 = min(R, r0 + per);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int r = r0;
+  for (; r + 3 < r1; r += 4) {
+    a0 += in[(long long)r * W + c];
+    a1 += in[(long long)(r + 1) * W + c];
+    a2 += in[(long long)(r + 2) * W + c];
+    a3 += in[(long long)(r + 3) * W + c];
+  }
+  for (; r < r1; ++r) a0 += in[(long long)r * W + c];
+  out[(long long)g * W + c] = (a0 + a1) + (a2 + a3);
+}
+
 // column sums of a bf16 [R][C] matrix into fp32 out[C] (bias gradients)
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16* __restrict__ x, int R, int C, int ld,
                                                      float* __restrict__ out, int accumulate) {
@@ -304,6 +326,14 @@ extern "C" int rk_pack_nhwc(const void* src, int is_u8, int N, int C, int H, int
 
 extern "C" int rk_add_int(int* p, int v, void* stream) {
   hipLaunchKernelGGL(add_int_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, p, v);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_rows_reduce(const float* in, int R, long long W, int G, float* out, void* stream) {
+  if (G <= 0 || G > 65535) return RK_EBADARG;
+  dim3 grid((unsigned)((W + 255) / 256), (unsigned)G);
+  hipLaunchKernelGGL(rows_reduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, R, W, out);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -195,7 +195,25 @@ def channel_stats(x2d: torch.Tensor):
     return part
 
 
+def rows_reduce(x2d: torch.Tensor, groups: int) -> torch.Tensor:
+    """[R][W] fp32 -> [groups][W] partial sums (parallel stage 1 of a long row reduction)."""
+    R = x2d.shape[0]
+    W = x2d.numel() // R
+    out = torch.empty((groups,) + tuple(x2d.shape[1:]), device=x2d.device, dtype=torch.float32)
+    _lib.call("rk_rows_reduce", _p(x2d), R, W, groups, _p(out), _s())
+    return out
+
+
+def _shrink_rows(part: torch.Tensor, max_rows: int = 64) -> torch.Tensor:
+    """Cut a [R][2][C] partial-stat table to <= max_rows rows with a parallel pass (~32 rows/block)."""
+    R = part.shape[0]
+    if R <= max_rows:
+        return part
+    return rows_reduce(part, min(max_rows, cdiv(R, 32)))
+
+
 def bn_finalize_fwd(part, count, gamma, beta, eps, running_mean=None, running_var=None, momentum=0.1, outs=None):
+    part = _shrink_rows(part)
     R, _, C = part.shape
     if outs is None:
         outs = torch.empty((4, C), device=part.device, dtype=torch.float32)
@@ -235,6 +253,8 @@ def bn_bwd(dout, y, coeffs, gamma, *, pool=False, act=ACT_RELU, slope=0.2, dgamm
     _lib.call("rk_bn_bwd_reduce", _p(dout), _p(y), _p(scale), _p(shift), _p(mean), _p(rstd), _p(part), rows, Nb, H,
               W, C, int(pool), act, float(slope), s)
     coef = torch.empty((3, C), device=y.device, dtype=torch.float32)
+    part = _shrink_rows(part)
+    rows = part.shape[0]
     _lib.call("rk_bn_finalize_bwd", _p(part), rows, C, float(Nb * H * W), _p(gamma), _p(mean), _p(rstd), _p(dgamma),
               _p(dbeta), _p(coef), int(accumulate), s)
     if dy is None:
@@ -285,6 +305,8 @@ def nonfinite_flag(x, flag):
 
 
 def reduce_slabs(slab, out, *, accumulate=False, scale=1.0):
+    if slab.shape[0] > 16:
+        slab = rows_reduce(slab, min(16, cdiv(slab.shape[0], 16)))
     S = slab.shape[0]
     n = out.numel()
     _lib.call("rk_reduce_slabs", _p(slab), S, n, _p(out), int(accumulate), float(scale), _s())
