@@ -57,6 +57,7 @@ struct IgemmParams {
   int flags;
   float alpha;          // output scale
   float slope;          // leaky-relu slope
+  unsigned long long bytesA, bytesB;  // operand extents for the buffer descriptors (< 2 GiB)
 };
 
 // ---- LDS images --------------------------------------------------------------------------------
@@ -73,13 +74,29 @@ RK_DEV int kout_off(int k, int ch) {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-// Unconditional 16-byte load at base+off (off forced to 0 when !ok) then a bitwise mask: keeps the
-// load unpredicated (no exec branch around it, no per-element vmcnt(0)) and the zero-fill branch-free.
-RK_DEV uint4 masked_load(const bf16* base, long long off, bool ok) {
-  const uint4 v = *(const uint4*)(base + (ok ? off : 0LL));
-  const unsigned m = ok ? 0xffffffffu : 0u;
-  return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+// Operand staging goes through buffer loads: a 128-bit descriptor (built from kernel arguments,
+// so wave-uniform) + a 32-bit byte offset per lane.  Out-of-range offsets (conv halo, tile
+// edges, K tail) are set to OOB and the hardware range check returns zeros — no zero-fill select
+// on the loaded data (that made hipcc wait vmcnt right after every load, serialising global
+// latency into each K-tile) and no 64-bit address arithmetic.  Per-row tap validity for the conv
+// gather is a 9-bit mask computed once per thread, so a K-tile costs ~3 VALU per staged chunk.
+constexpr unsigned OOB = 0x80000000u;
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+RK_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned long long bytes) {
+  const unsigned nrec = bytes >= 0x80000000ull ? 0x80000000u : (unsigned)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec, 0x00020000);
 }
+
+RK_DEV uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// tap t of a 3x3 kernel -> (dy, dx) in {-1,0,1}^2 (times the gather sign s)
+RK_DEV int tap_dy(int t) { return ((t * 11) >> 5) - 1; }
+RK_DEV int tap_dx(int t) { return t - 3 * ((t * 11) >> 5) - 1; }
 
 template <int MODE, int T>
 struct Operand {
@@ -88,22 +105,21 @@ struct Operand {
   static constexpr int R = T / 8;              // chunks per K-outer row
   static constexpr int KROWS_PER_PASS = 256 / R;
 
-  const bf16* base;
+  __amdgpu_buffer_rsrc_t rsrc;
   int ldsoff[CH];
   // K-inner state
-  long long rowoff[CH];
-  int hh[CH], ww[CH];
-  bool rowok[CH];
+  unsigned rowoff[CH];  // byte offset of the row (pixel / matrix row)
+  unsigned tapmask[CH]; // conv: bit t = tap t in bounds for this row; dense: 1 if row valid
   int cchunk;
   // K-outer state
   int krow0;
-  int col;
+  unsigned coloff;
   bool colok;
   int dh, dw;  // fixed tap shift (conv K-outer)
-  long long coloff;
 
-  RK_DEV void init(const IgemmParams& p, const bf16* ptr, int ld, int tile0, int extent, int tid) {
-    base = ptr;
+  RK_DEV void init(const IgemmParams& p, const bf16* ptr, unsigned long long bytes, int ld, int tile0, int extent,
+                   int tid) {
+    rsrc = make_rsrc(ptr, bytes);
     if constexpr (KIN) {
       cchunk = tid & 7;
 #pragma unroll
@@ -111,15 +127,26 @@ struct Operand {
         const int r = (tid >> 3) + 32 * i;
         ldsoff[i] = kin_off(r, cchunk);
         const int gi = tile0 + r;
-        rowok[i] = gi < extent;
-        const int g = rowok[i] ? gi : 0;
+        const bool ok = gi < extent;
         if constexpr (MODE == OP_DENSE_KIN) {
-          rowoff[i] = (long long)g * ld;
-          hh[i] = ww[i] = 0;
+          rowoff[i] = (unsigned)gi * (unsigned)ld * 2u;
+          tapmask[i] = ok ? 1u : 0u;
         } else {
-          hh[i] = (g >> p.log2W) & (p.H - 1);
-          ww[i] = g & (p.W - 1);
-          rowoff[i] = (long long)g << p.log2C;
+          const int h = (gi >> p.log2W) & (p.H - 1), w = gi & (p.W - 1);
+          rowoff[i] = ((unsigned)gi << p.log2C) * 2u;
+          unsigned m = 0;
+          if (p.taps == 1) {
+            m = 1u;
+          } else {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+              int dy = tap_dy(t), dx = tap_dx(t);
+              if constexpr (MODE == OP_CONVT_KIN) { dy = -dy; dx = -dx; }
+              const bool in = (unsigned)(h + dy) < (unsigned)p.H && (unsigned)(w + dx) < (unsigned)p.W;
+              m |= (in ? 1u : 0u) << t;
+            }
+          }
+          tapmask[i] = ok ? m : 0u;
         }
       }
     } else {
@@ -127,19 +154,16 @@ struct Operand {
       krow0 = tid / R;
 #pragma unroll
       for (int i = 0; i < CH; ++i) ldsoff[i] = kout_off<R>(krow0 + KROWS_PER_PASS * i, ch);
-      col = tile0 + ch * 8;
+      const int col = tile0 + ch * 8;
       colok = col < extent;
       dh = dw = 0;
       if constexpr (MODE == OP_CONV_KOUT) {
         const int tap = col >> p.log2C;
         colok = colok && tap < p.taps;
-        const int kh = p.taps == 9 ? (tap * 11) >> 5 : 1;  // tap/3 for tap<9
-        const int kw = p.taps == 9 ? tap - 3 * kh : 1;
-        dh = kh - 1;
-        dw = kw - 1;
-        coloff = col & (p.C - 1);
+        if (p.taps == 9) { dh = tap_dy(tap); dw = tap_dx(tap); }
+        coloff = (unsigned)(col & (p.C - 1)) * 2u;
       } else {
-        coloff = col;
+        coloff = (unsigned)col * 2u;
       }
     }
   }
@@ -150,43 +174,39 @@ struct Operand {
       const bool kok = k < K;
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
-        r[i] = masked_load(base, rowoff[i] + k, kok && rowok[i]);
+        const bool ok = kok && tapmask[i];
+        r[i] = bload(rsrc, ok ? rowoff[i] + (unsigned)k * 2u : OOB);
       }
     } else if constexpr (MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN) {
       const int k = kt * BK + cchunk * 8;
-      const int tap = k >> p.log2C;
+      const int tap = k >> p.log2C;  // >= taps -> no mask bit -> zero
       const int ci = k & (p.C - 1);
       int dy = 0, dx = 0;
       if (p.taps == 9) {
-        const int kh = (tap * 11) >> 5;
-        dy = kh - 1;
-        dx = tap - 3 * kh - 1;
+        dy = tap_dy(tap);
+        dx = tap_dx(tap);
         if constexpr (MODE == OP_CONVT_KIN) { dy = -dy; dx = -dx; }
       }
-      const bool kok = tap < p.taps;
-      const long long shift = ((long long)(dy * p.W + dx) << p.log2C) + ci;
+      const int delta = (((dy * p.W + dx) << p.log2C) + ci) * 2;
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
-        const int y = hh[i] + dy, x = ww[i] + dx;
-        const bool ok = kok && rowok[i] && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-        r[i] = masked_load(base, rowoff[i] + shift, ok);
+        const bool ok = (tapmask[i] >> tap) & 1u;
+        r[i] = bload(rsrc, ok ? (unsigned)((int)rowoff[i] + delta) : OOB);
       }
     } else if constexpr (MODE == OP_DENSE_KOUT) {
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const int k = kt * BK + krow0 + KROWS_PER_PASS * i;
         const bool ok = colok && k < K;
-        r[i] = masked_load(base, coloff + (long long)k * ld, ok);
+        r[i] = bload(rsrc, ok ? coloff + (unsigned)k * (unsigned)ld * 2u : OOB);
       }
     } else if constexpr (MODE == OP_CONV_KOUT) {
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const int k = kt * BK + krow0 + KROWS_PER_PASS * i;  // pixel index
         const int h = (k >> p.log2W) & (p.H - 1), w = k & (p.W - 1);
-        const int y = h + dh, x = w + dw;
-        const bool ok = colok && k < K && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-        const long long off = ((long long)(k + dh * p.W + dw)) << p.log2C;
-        r[i] = masked_load(base, coloff + off, ok);
+        const bool ok = colok && k < K && (unsigned)(h + dh) < (unsigned)p.H && (unsigned)(w + dw) < (unsigned)p.W;
+        r[i] = bload(rsrc, ok ? (((unsigned)(k + dh * p.W + dw)) << p.log2C) * 2u + coloff : OOB);
       }
     } else {  // OP_WTAP_KOUT: row k = tap*Cout + co  ->  W[co][tap][c]
 #pragma unroll
@@ -194,7 +214,7 @@ struct Operand {
         const int k = kt * BK + krow0 + KROWS_PER_PASS * i;
         const int tap = k >> p.log2Cb, co = k & ((1 << p.log2Cb) - 1);
         const bool ok = colok && k < K;
-        r[i] = masked_load(base, coloff + (long long)co * ld + (long long)tap * p.N, ok);
+        r[i] = bload(rsrc, ok ? ((unsigned)co * (unsigned)ld + (unsigned)tap * (unsigned)p.N) * 2u + coloff : OOB);
       }
     }
   }
@@ -228,7 +248,7 @@ struct Operand {
   }
 };
 
-template <int BM, int BN, int AM, int BMODE, int EPI>
+template <int BM, int BN, int AM, int BMODE, int EPI, int PF>
 __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
@@ -246,8 +266,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
 
   Operand<AM, BM> opA;
   Operand<BMODE, BN> opB;
-  opA.init(p, p.A, p.lda, m0, p.M, tid);
-  opB.init(p, p.B, p.ldb, n0, p.N, tid);
+  opA.init(p, p.A, p.bytesA, p.lda, m0, p.M, tid);
+  opB.init(p, p.B, p.bytesB, p.ldb, n0, p.N, tid);
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -255,23 +275,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[Operand<AM, BM>::CH], rb[Operand<BMODE, BN>::CH];
-  if (kt0 < kt1) {
-    opA.load(p, kt0, p.K, p.lda, ra);
-    opB.load(p, kt0, p.K, p.ldb, rb);
-    opA.store(smem, ra);
-    opB.store(smem + A_BYTES, rb);
-  }
-  __syncthreads();
-
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) {
-      opA.load(p, kt + 1, p.K, p.lda, ra);
-      opB.load(p, kt + 1, p.K, p.ldb, rb);
-    }
-    const char* la = smem + cur * (A_BYTES + B_BYTES);
+  auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -286,12 +290,72 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      char* nxt = smem + (cur ^ 1) * (A_BYTES + B_BYTES);
-      opA.store(nxt, ra);
-      opB.store(nxt + A_BYTES, rb);
+  };
+  constexpr int SB = A_BYTES + B_BYTES;  // one LDS stage
+  uint4 ra0[Operand<AM, BM>::CH], rb0[Operand<BMODE, BN>::CH];
+  if constexpr (PF == 1) {
+    // one K-tile in flight: issue t+1 before computing t, write it to LDS after
+    if (kt0 < kt1) {
+      opA.load(p, kt0, p.K, p.lda, ra0);
+      opB.load(p, kt0, p.K, p.ldb, rb0);
+      opA.store(smem, ra0);
+      opB.store(smem + A_BYTES, rb0);
     }
     __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) {
+        opA.load(p, kt + 1, p.K, p.lda, ra0);
+        opB.load(p, kt + 1, p.K, p.ldb, rb0);
+      }
+      compute(smem + cur * SB);
+      if (more) {
+        opA.store(smem + (cur ^ 1) * SB, ra0);
+        opB.store(smem + (cur ^ 1) * SB + A_BYTES, rb0);
+      }
+      __syncthreads();
+    }
+  } else {
+    // two K-tiles in flight through two register sets (static indices: the loop is unrolled by 2):
+    // at the top of step t, LDS stage t&1 holds tile t and register set (t+1)&1 holds tile t+1.
+    uint4 ra1[Operand<AM, BM>::CH], rb1[Operand<BMODE, BN>::CH];
+    if (kt0 < kt1) {
+      opA.load(p, kt0, p.K, p.lda, ra0);
+      opB.load(p, kt0, p.K, p.ldb, rb0);
+      if (kt0 + 1 < kt1) {
+        opA.load(p, kt0 + 1, p.K, p.lda, ra1);
+        opB.load(p, kt0 + 1, p.K, p.ldb, rb1);
+      }
+      opA.store(smem, ra0);
+      opB.store(smem + A_BYTES, rb0);
+    }
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      // even step: compute stage 0, prefetch kt+2 into set 0, publish set 1 (kt+1) to stage 1
+      if (kt + 2 < kt1) {
+        opA.load(p, kt + 2, p.K, p.lda, ra0);
+        opB.load(p, kt + 2, p.K, p.ldb, rb0);
+      }
+      compute(smem);
+      if (kt + 1 < kt1) {
+        opA.store(smem + SB, ra1);
+        opB.store(smem + SB + A_BYTES, rb1);
+      }
+      __syncthreads();
+      if (kt + 1 >= kt1) break;
+      // odd step: compute stage 1, prefetch kt+3 into set 1, publish set 0 (kt+2) to stage 0
+      if (kt + 3 < kt1) {
+        opA.load(p, kt + 3, p.K, p.lda, ra1);
+        opB.load(p, kt + 3, p.K, p.ldb, rb1);
+      }
+      compute(smem + SB);
+      if (kt + 2 < kt1) {
+        opA.store(smem, ra0);
+        opB.store(smem + A_BYTES, rb0);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: lane owns out[m][n..n+3] of every (i, j) fragment --------------------------
@@ -389,21 +453,25 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
 }
 
 template <int BM, int BN, int AM, int BMODE, int EPI>
-int launch_tile(const IgemmParams& p, int splits, hipStream_t st) {
+int launch_tile(const IgemmParams& p, int splits, int pf, hipStream_t st) {
   const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
   dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, AM, BMODE, EPI>), grid, dim3(256), 0, st, p);
+  if (pf == 2)
+    hipLaunchKernelGGL((igemm_kernel<BM, BN, AM, BMODE, EPI, 2>), grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((igemm_kernel<BM, BN, AM, BMODE, EPI, 1>), grid, dim3(256), 0, st, p);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
 template <int AM, int BMODE, int EPI>
 int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
-  switch (tile) {
-    case 0: return launch_tile<128, 128, AM, BMODE, EPI>(p, splits, st);
-    case 1: return launch_tile<128, 64, AM, BMODE, EPI>(p, splits, st);
-    case 2: return launch_tile<64, 128, AM, BMODE, EPI>(p, splits, st);
-    case 3: return launch_tile<64, 64, AM, BMODE, EPI>(p, splits, st);
+  const int pf = (tile >> 4) ? 2 : 1;  // bit 4 of the tile code: two K-tiles in flight
+  switch (tile & 15) {
+    case 0: return launch_tile<128, 128, AM, BMODE, EPI>(p, splits, pf, st);
+    case 1: return launch_tile<128, 64, AM, BMODE, EPI>(p, splits, pf, st);
+    case 2: return launch_tile<64, 128, AM, BMODE, EPI>(p, splits, pf, st);
+    case 3: return launch_tile<64, 64, AM, BMODE, EPI>(p, splits, pf, st);
   }
   return RK_EBADARG;
 }
@@ -412,12 +480,13 @@ int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
 
 // kind: 0 conv-fwd, 1 conv-dgrad, 2 conv-wgrad, 3 dense (A·Bᵀ), 4 dense dX (A·B), 5 dense dW (Aᵀ·B)
 // epi: 0 bf16 out, 1 fp32 out (split-K slabs when splits > 1)
-// tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64
+// tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64; | 16 = two K-tiles in flight (register ring)
 extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* B, void* C,
                         const float* bias, float* stats, const void* gate, int M, int N, int K,
                         int lda, int ldb, int ldc, int H, int W, int Cch, int taps, int Cb,
                         int splits, long long slabStride, int flags, float alpha, float slope,
-                        void* stream) {
+                        long long bytesA, long long bytesB, void* stream) {
+  if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
   if (M <= 0 || N <= 0 || K <= 0 || splits <= 0) return RK_EBADARG;
   // K-inner A operands (every kind but the two K-outer x K-outer reductions) need K % 8 == 0
   if (N % 4 != 0 || (kind != 2 && kind != 5 && K % 8 != 0)) return RK_EUNSUPPORTED;
@@ -433,6 +502,7 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
   p.ktPer = rk_cdiv(kTiles, splits);
   p.slabStride = slabStride;
   p.flags = flags; p.alpha = alpha; p.slope = slope;
+  p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   hipStream_t st = (hipStream_t)stream;
   const bool conv = kind <= 2;
   if (conv && (p.log2H < 0 || p.log2W < 0 || p.log2C < 0 || Cch < 8)) return RK_EUNSUPPORTED;

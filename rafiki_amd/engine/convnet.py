@@ -73,18 +73,33 @@ def _bf16_grad(t):
     return _BF16Grad.apply(t)
 
 
+def _init_fc(fan_in, rows_real, cols_real, gain=math.sqrt(2.0)):
+    """Kaiming-normal over the real [rows_real, cols_real] block; padded rows/cols stay zero forever
+    (zero weights + zero bias -> zero activations -> zero gradients under SGD/Adam)."""
+    std = gain / math.sqrt(max(1, fan_in))
+
+    def f(t, g):
+        t.zero_()
+        t[:rows_real, :cols_real].normal_(0.0, std, generator=g)
+    return f
+
+
 class ConvNetEngine:
     def __init__(self, num_classes: int = 10, in_channels: int = 3, image_size: int = 32,
                  cfg: Sequence = VGG_SMALL_CFG, fc_dims: Sequence[int] = (512,), device='cuda', seed: int = 0,
                  bn_eps: float = 1e-5, bn_momentum: float = 0.1, optimizer: str = 'sgd', lr: float = 0.05,
                  momentum: float = 0.9, weight_decay: float = 5e-4, nesterov: bool = True,
-                 betas=(0.9, 0.999)):
+                 betas=(0.9, 0.999), input_bn: bool = False):
         self.device = torch.device(device)
         self.num_classes, self.in_channels, self.image_size = num_classes, in_channels, image_size
         self.cin_p = _pad8(in_channels)
         self.ncls_p = _pad8(num_classes)
         self.bn_eps, self.bn_momentum = bn_eps, bn_momentum
-        if not _is_pow2(image_size):
+        self.flat_input = not any(v != 'M' for v in cfg)
+        self.input_bn = bool(input_bn)
+        if self.input_bn and not self.flat_input:
+            raise ValueError('input_bn is for fully-connected nets (no conv blocks)')
+        if not self.flat_input and not _is_pow2(image_size):
             raise ValueError('image_size must be a power of two (NHWC implicit-GEMM gather)')
         flat = FlatParams(self.device, seed)
         self.blocks = []  # (name, cin, cout, pool, H_in)
@@ -106,22 +121,30 @@ class ConvNetEngine:
         if hw < 1:
             raise ValueError('too many pooling stages for image_size {}'.format(image_size))
         self.feat_hw = hw
-        self.feat_dim = hw * hw * cin
-        self.fcs = []
-        d_in = self.feat_dim
+        if self.flat_input:
+            self.in_dim = image_size * image_size * in_channels
+            self.feat_dim = _pad8(self.in_dim)
+            real_in = self.in_dim
+        else:
+            self.feat_dim = hw * hw * cin
+            real_in = self.feat_dim
+        if self.input_bn:
+            flat.add('in_bn.gamma', (self.feat_dim,), init_const(1.0), decay=False)
+            flat.add('in_bn.beta', (self.feat_dim,), init_const(0.0), decay=False)
+        self.fcs = []  # (name, d_in_padded, d_padded, d_real)
+        d_in, d_in_real = self.feat_dim, real_in
         for k, d in enumerate(fc_dims):
-            flat.add('fc{}.w'.format(k), (d, d_in), init_kaiming(d_in))
-            flat.add('fc{}.b'.format(k), (d,), init_const(0.0), decay=False)
-            self.fcs.append(('fc{}'.format(k), d_in, d))
-            d_in = d
-        flat.add('out.w', (self.ncls_p, d_in), init_kaiming(d_in, gain=1.0, zero_in_slice=None))
+            dp = _pad8(d)
+            flat.add('fc{}.w'.format(k), (dp, d_in), _init_fc(d_in_real, d, d_in_real))
+            flat.add('fc{}.b'.format(k), (dp,), init_const(0.0), decay=False)
+            self.fcs.append(('fc{}'.format(k), d_in, dp, d))
+            d_in, d_in_real = dp, d
+        flat.add('out.w', (self.ncls_p, d_in), _init_fc(d_in_real, num_classes, d_in_real, gain=1.0))
         flat.add('out.b', (self.ncls_p,), init_const(0.0), decay=False)
         self.flat = flat.build()
-        with torch.no_grad():  # padded class rows never receive gradient; keep them exactly zero
-            self.flat.w('out.w')[num_classes:].zero_()
-            self.flat.sync_bf16()
         self.d_last = d_in
-        C = sum(b[2] for b in self.blocks)
+        self.d_last_real = d_in_real
+        C = sum(b[2] for b in self.blocks) + (self.feat_dim if self.input_bn else 0)
         self.running = torch.zeros((2, C), dtype=torch.float32, device=self.device)
         self.running[1].fill_(1.0)
         self._roff = []
@@ -129,6 +152,7 @@ class ConvNetEngine:
         for b in self.blocks:
             self._roff.append(off)
             off += b[2]
+        self._in_roff = off
         if optimizer == 'adam':
             self.opt = FlatAdam(self.flat, lr, betas=betas, weight_decay=weight_decay, decoupled=True)
         else:
@@ -140,10 +164,14 @@ class ConvNetEngine:
         self._graph_batch = None
         self._static_x = self._static_y = None
         self._eval_coeffs = None
+        self._eval_graphs = {}
 
     # ------------------------------------------------------------------------------- helpers
     def running_stats(self, bi):
-        o, c = self._roff[bi], self.blocks[bi][2]
+        if bi == 'in':
+            o, c = self._in_roff, self.feat_dim
+        else:
+            o, c = self._roff[bi], self.blocks[bi][2]
         return self.running[0, o:o + c], self.running[1, o:o + c]
 
     def flops_per_image(self) -> float:
@@ -151,7 +179,7 @@ class ConvNetEngine:
         fl = 0.0
         for (_, cin, cout, _, hw) in self.blocks:
             fl += 2.0 * hw * hw * cout * 9 * cin
-        for (_, di, do) in self.fcs:
+        for (_, di, do, _) in self.fcs:
             fl += 2.0 * di * do
         fl += 2.0 * self.d_last * self.num_classes
         return fl
@@ -181,10 +209,19 @@ class ConvNetEngine:
             h = F.bn_act_fwd(y, coeffs[2], coeffs[3], pool=pool, act=F.ACT_RELU)
             saved.append((y, coeffs))
             acts.append(h)
+        in_saved = None
+        if self.input_bn:
+            raw = h.reshape(B, 1, 1, self.feat_dim)
+            stats = F.channel_stats(raw.view(B, self.feat_dim))
+            rm, rv = self.running_stats('in')
+            coeffs = F.bn_finalize_fwd(stats, B, fl.w('in_bn.gamma'), fl.w('in_bn.beta'), self.bn_eps, rm, rv,
+                                       self.bn_momentum)
+            h = F.bn_act_fwd(raw, coeffs[2], coeffs[3], pool=False, act=F.ACT_NONE)
+            in_saved = (raw, coeffs)
         feat = h.reshape(B, self.feat_dim)
         fc_in = [feat]
         z = feat
-        for (name, di, do) in self.fcs:
+        for (name, di, do, _) in self.fcs:
             z = F.linear(z, fl.wb(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
             fc_in.append(z)
         logits = F.linear(z, fl.wb('out.w'), fl.w('out.b'), out_dtype=torch.float32)
@@ -202,7 +239,15 @@ class ConvNetEngine:
             F.linear_dw(d, fc_in[k], out=fl.g(name + '.w'))
             F.colsum(d, fl.g(name + '.b'))
             wname = name
-        d = F.linear_dx(d, fl.wb(wname + '.w')).view(B, self.feat_hw, self.feat_hw, -1)
+        if not self.blocks and not self.input_bn:
+            return
+        d = F.linear_dx(d, fl.wb(wname + '.w'))
+        if self.input_bn:
+            raw, coeffs = in_saved
+            F.bn_bwd(d.view(B, 1, 1, self.feat_dim), raw, coeffs, fl.w('in_bn.gamma'), pool=False, act=F.ACT_NONE,
+                     dgamma=fl.g('in_bn.gamma'), dbeta=fl.g('in_bn.beta'))
+            return
+        d = d.view(B, self.feat_hw, self.feat_hw, -1)
         for bi in range(len(self.blocks) - 1, -1, -1):
             name, cin, cout, pool, hw = self.blocks[bi]
             y, coeffs = saved[bi]
@@ -224,7 +269,7 @@ class ConvNetEngine:
         P = params if params is not None else {n: fl.w(n) for n in fl.names()}
         rnd = _bf16_storage if emulate_bf16 else (lambda t: t)
         rndw = (lambda t: t + (t.bfloat16().float() - t).detach()) if emulate_bf16 else (lambda t: t)
-        h = x_nhwc.float().permute(0, 3, 1, 2)
+        h = x_nhwc.float().permute(0, 3, 1, 2) if x_nhwc.dim() == 4 else x_nhwc.float()
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             w = rndw(P[name + '.w']).permute(0, 3, 1, 2)
             h = rnd(TF.conv2d(h, w, padding=1))
@@ -240,8 +285,20 @@ class ConvNetEngine:
             if pool:
                 h = TF.max_pool2d(h, 2)
             h = rnd(h)
-        h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)
-        for (name, di, do) in self.fcs:
+        if self.flat_input:
+            h = x_nhwc.float().reshape(x_nhwc.shape[0], -1)
+            if self.input_bn:
+                rm, rv = self.running_stats('in')
+                if training:
+                    h = TF.batch_norm(h, rm if update_running else None, rv if update_running else None,
+                                      P['in_bn.gamma'], P['in_bn.beta'], training=True, momentum=self.bn_momentum,
+                                      eps=self.bn_eps)
+                else:
+                    h = TF.batch_norm(h, rm, rv, P['in_bn.gamma'], P['in_bn.beta'], training=False, eps=self.bn_eps)
+                h = rnd(h)
+        else:
+            h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)
+        for (name, di, do, _) in self.fcs:
             h = rnd(torch.relu(h @ rndw(P[name + '.w']).t() + P[name + '.b']))
         logits = (h @ rndw(P['out.w']).t() + P['out.b'])[:, :self.num_classes]
         logits = _bf16_grad(logits) if emulate_bf16 else logits
@@ -282,8 +339,7 @@ class ConvNetEngine:
         """Capture one training step on static input buffers into a hipGraph."""
         if self.device.type != 'cuda':
             return None
-        self._static_x = torch.zeros((batch_size, self.image_size, self.image_size, self.cin_p),
-                                     dtype=torch.bfloat16, device=self.device)
+        self._static_x = torch.zeros(self.input_shape(batch_size), dtype=torch.bfloat16, device=self.device)
         self._static_y = torch.zeros((batch_size,), dtype=torch.int32, device=self.device)
         # warm the allocator / library outside capture; these steps use zero inputs and are
         # undone by restoring the parameter state afterwards.
@@ -320,12 +376,45 @@ class ConvNetEngine:
         self._static_y.copy_(labels)
         self._graph.replay()
 
+    # ------------------------------------------------------------------------------ inputs
+    def input_shape(self, batch):
+        if self.flat_input:
+            return (batch, self.feat_dim)
+        return (batch, self.image_size, self.image_size, self.cin_p)
+
+    def prepare_inputs(self, images, scale=1.0 / 127.5, shift=-1.0):
+        """uint8 images [N, H, W] or [N, H, W, C] (host numpy / torch) -> device tensor in this engine's
+        input layout (bf16 NHWC with channels padded to 8, or flat [N, D] padded to 8).  The
+        normalisation (x*scale+shift) and packing run in one gfx950 kernel on the GPU."""
+        t = torch.as_tensor(images)
+        if t.dim() == 3:
+            t = t.unsqueeze(-1)
+        N = t.shape[0]
+        if self.device.type != 'cuda':
+            x = t.float() * scale + shift
+            if self.flat_input:
+                out = torch.zeros((N, self.feat_dim))
+                out[:, :self.in_dim] = x.reshape(N, -1)
+                return out
+            out = torch.zeros((N, self.image_size, self.image_size, self.cin_p))
+            out[..., :x.shape[-1]] = x
+            return out
+        t = t.to(self.device, non_blocking=True)
+        if self.flat_input:
+            nchw = t.reshape(N, -1, 1, 1)
+            return F.pack_nhwc(nchw.contiguous(), self.feat_dim, scale, shift).view(N, self.feat_dim)
+        nchw = t.permute(0, 3, 1, 2).contiguous()
+        return F.pack_nhwc(nchw, self.cin_p, scale, shift)
+
     # ------------------------------------------------------------------------------ inference
     def prepare_eval(self):
         """Fold BN running stats into per-channel scale/shift (inference coefficients)."""
         fl = self.flat
         coeffs = []
-        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+        items = [(bi, b[0]) for bi, b in enumerate(self.blocks)]
+        if self.input_bn:
+            items.append(('in', 'in_bn'))
+        for bi, name in items:
             rm, rv = self.running_stats(bi)
             if self.device.type == 'cuda':
                 c = F.bn_eval_coeffs(fl.w(name + '.gamma'), fl.w(name + '.beta'), rm, rv, self.bn_eps)
@@ -335,31 +424,78 @@ class ConvNetEngine:
                 c = torch.stack([rm, r, sc, fl.w(name + '.beta') - rm * sc])
             coeffs.append(c)
         self._eval_coeffs = coeffs
+        self._eval_graphs = {}
         return coeffs
 
     @torch.no_grad()
+    def _forward_eval_gpu(self, x, out_probs):
+        fl = self.flat
+        h = x
+        B = x.shape[0]
+        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            y = F.conv_fwd(h, fl.wb(name + '.w'))
+            c = self._eval_coeffs[bi]
+            h = F.bn_act_fwd(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
+        if self.input_bn:
+            c = self._eval_coeffs[-1]
+            h = F.bn_act_fwd(h.reshape(B, 1, 1, self.feat_dim), c[2], c[3], pool=False, act=F.ACT_NONE)
+        z = h.reshape(B, self.feat_dim)
+        for (name, di, do, _) in self.fcs:
+            z = F.linear(z, fl.wb(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
+        logits = F.linear(z, fl.wb('out.w'), fl.w('out.b'), out_dtype=torch.float32)
+        F.softmax_xent(logits, None, self.num_classes, probs=out_probs)
+        return out_probs
+
+    @torch.no_grad()
     def forward_eval(self, x, out_probs=None):
-        """x: [B, H, W, cin_p] bf16 (GPU) or float NHWC (CPU) -> probabilities [B, num_classes] fp32."""
+        """x: engine input layout -> probabilities [B, num_classes] fp32."""
         if self.device.type != 'cuda':
             _, logits = self.reference_loss(x, None, training=False)
             return torch.softmax(logits.float(), 1)
         if self._eval_coeffs is None:
             self.prepare_eval()
-        fl = self.flat
-        h = x
-        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
-            y = F.conv_fwd(h, fl.wb(name + '.w'))
-            c = self._eval_coeffs[bi]
-            h = F.bn_act_fwd(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
-        B = x.shape[0]
-        z = h.reshape(B, self.feat_dim)
-        for (name, di, do) in self.fcs:
-            z = F.linear(z, fl.wb(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
-        logits = F.linear(z, fl.wb('out.w'), fl.w('out.b'), out_dtype=torch.float32)
         if out_probs is None:
-            out_probs = torch.empty((B, self.num_classes), dtype=torch.float32, device=self.device)
-        F.softmax_xent(logits, None, self.num_classes, probs=out_probs)
-        return out_probs
+            out_probs = torch.empty((x.shape[0], self.num_classes), dtype=torch.float32, device=self.device)
+        return self._forward_eval_gpu(x, out_probs)
+
+    EVAL_BUCKETS = (1, 8, 32, 128, 512)
+
+    @torch.no_grad()
+    def forward_eval_graphed(self, x):
+        """Inference through hipGraph-captured forwards, one per batch-size bucket (captured lazily,
+        reused for every later request of that bucket).  Returns a view [B, num_classes]."""
+        if self.device.type != 'cuda':
+            return self.forward_eval(x)
+        if self._eval_coeffs is None:
+            self.prepare_eval()
+        B = x.shape[0]
+        bucket = next((b for b in self.EVAL_BUCKETS if b >= B), None)
+        if bucket is None:  # larger than the biggest bucket: chunk it
+            outs = [self.forward_eval_graphed(x[i:i + self.EVAL_BUCKETS[-1]]) for i in
+                    range(0, B, self.EVAL_BUCKETS[-1])]
+            return torch.cat(outs)
+        ent = self._eval_graphs.get(bucket)
+        if ent is None:
+            sx = torch.zeros(self.input_shape(bucket), dtype=torch.bfloat16, device=self.device)
+            so = torch.empty((bucket, self.num_classes), dtype=torch.float32, device=self.device)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._forward_eval_gpu(sx, so)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._forward_eval_gpu(sx, so)
+            ent = self._eval_graphs[bucket] = (g, sx, so)
+        g, sx, so = ent
+        sx[:B].copy_(x)
+        if B < bucket:
+            sx[B:].zero_()
+        g.replay()
+        return so[:B]
+
+    def resident_bytes(self):
+        return self.flat.total * (4 + 2 + 4) + self.running.numel() * 4
 
     # ---------------------------------------------------------------------------- state I/O
     def state_dict(self):

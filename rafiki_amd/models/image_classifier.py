@@ -1,0 +1,157 @@
+"""Shared machinery for the native image-classification models (VGG-small, FeedForward MLP).
+
+A trial uploads its whole train split to HBM once (uint8 -> packed bf16 by one gfx950 kernel),
+captures the training step into a hipGraph and replays it per batch; shuffling and batching are
+device-side index_selects.  evaluate/predict use hipGraph-captured forwards per batch bucket.
+Task I/O contract (reference docs/src/user/tasks.rst:23-63): a query is an HxW (grayscale) or
+HxWxC image as nested lists; a prediction is the list of class probabilities.
+"""
+from __future__ import annotations
+
+import base64
+import io
+import math
+import pickle
+
+import numpy as np
+import torch
+
+from ..engine.convnet import ConvNetEngine
+from ..model import BaseModel, dataset_utils, logger
+from ..parallel.context import current as trial_context
+
+
+class NativeImageClassifier(BaseModel):
+    """Subclasses define ``_engine_kwargs()`` and their knob config."""
+
+    DEFAULT_IMAGE_SIZE = 32
+
+    def __init__(self, **knobs):
+        super().__init__(**knobs)
+        self._knobs = dict(knobs)
+        self._engine = None
+        self._meta = {}
+        self.device = trial_context().device
+
+    # --------------------------------------------------------------------- subclass hooks
+    def _engine_kwargs(self, num_classes, channels, image_size):
+        raise NotImplementedError
+
+    @property
+    def image_size(self):
+        return int(self._knobs.get('image_size', self.DEFAULT_IMAGE_SIZE))
+
+    # ------------------------------------------------------------------------ data helpers
+    def _load(self, uri):
+        ds = dataset_utils.load_dataset_of_image_files(uri, image_size=self.image_size)
+        images, labels = ds.as_arrays()
+        if images.shape[1] != self.image_size or images.shape[2] != self.image_size:
+            images = dataset_utils.resize_as_images(images, self.image_size)
+        return images, labels, ds.classes
+
+    def _build(self, num_classes, channels):
+        kw = self._engine_kwargs(num_classes, channels, self.image_size)
+        self._engine = ConvNetEngine(num_classes=num_classes, in_channels=channels, image_size=self.image_size,
+                                     device=self.device, seed=int(self._knobs.get('seed', 0)), **kw)
+        self._meta = {'num_classes': num_classes, 'channels': channels, 'image_size': self.image_size}
+
+    # ------------------------------------------------------------------------ BaseModel API
+    def train(self, dataset_uri):
+        images, labels, classes = self._load(dataset_uri)
+        channels = 1 if images.ndim == 3 else images.shape[-1]
+        self._build(max(classes, 2), channels)
+        eng = self._engine
+        x_all = eng.prepare_inputs(images)
+        y_all = torch.as_tensor(labels, dtype=torch.int32, device=eng.device)
+        n = x_all.shape[0]
+        bs = int(min(self._knobs.get('batch_size', 128), n))
+        epochs = float(self._knobs.get('epochs', 1))
+        steps_per_epoch = max(1, n // bs)
+        total = max(1, int(math.ceil(epochs * steps_per_epoch)))
+        use_graph = eng.device.type == 'cuda'
+        if use_graph:
+            eng.capture(bs)
+        xb = torch.empty(eng.input_shape(bs), dtype=x_all.dtype, device=eng.device)
+        yb = torch.empty((bs,), dtype=torch.int32, device=eng.device)
+        gen = torch.Generator(device=eng.device) if eng.device.type == 'cuda' else torch.Generator()
+        gen.manual_seed(int(self._knobs.get('seed', 0)))
+        logger.define_loss_plot()
+        logger.define_plot('Train accuracy', ['train_acc'], x_axis='epoch')
+        sched = self._knobs.get('lr_schedule', 'cosine')
+        step = 0
+        epoch = 0
+        while step < total:
+            perm = torch.randperm(n, device=eng.device, generator=gen)
+            eng.reset_metrics()
+            for b in range(steps_per_epoch):
+                if step >= total:
+                    break
+                if hasattr(eng.opt, 'set_lr_scale') and sched == 'cosine':
+                    eng.opt.set_lr_scale(0.5 * (1.0 + math.cos(math.pi * step / total)))
+                idx = perm[b * bs:(b + 1) * bs]
+                torch.index_select(x_all, 0, idx, out=xb)
+                torch.index_select(y_all, 0, idx, out=yb)
+                if use_graph:
+                    eng.step_graph(xb, yb)
+                else:
+                    eng.train_step(xb, yb)
+                step += 1
+            seen = max(1, int(eng.seen.item()))
+            logger.log_loss(loss=float(eng.loss_sum.item()) / seen, epoch=epoch)
+            logger.log(train_acc=float(eng.correct.item()) / seen, epoch=epoch)
+            epoch += 1
+        eng.prepare_eval()
+
+    def _probs(self, images_uint8):
+        eng = self._engine
+        out = []
+        chunk = 4096
+        for i in range(0, len(images_uint8), chunk):
+            x = eng.prepare_inputs(images_uint8[i:i + chunk])
+            out.append(eng.forward_eval_graphed(x).clone() if eng.device.type == 'cuda' else eng.forward_eval(x))
+        return torch.cat(out) if out else torch.zeros((0, self._meta['num_classes']))
+
+    def evaluate(self, dataset_uri):
+        images, labels, _ = self._load(dataset_uri)
+        probs = self._probs(images)
+        pred = probs.argmax(1).cpu().numpy()
+        return float((pred == np.asarray(labels)).mean())
+
+    def _queries_to_images(self, queries):
+        arr = np.asarray(queries)
+        if arr.dtype != np.uint8:
+            arr = np.clip(arr, 0, 255).astype(np.uint8)
+        if arr.ndim == 2:
+            arr = arr[None]
+        if arr.shape[1] != self.image_size or arr.shape[2] != self.image_size:
+            arr = dataset_utils.resize_as_images(arr, self.image_size)
+        ch = self._meta['channels']
+        if ch == 1 and arr.ndim == 4:
+            arr = arr.mean(-1).astype(np.uint8)
+        if ch > 1 and arr.ndim == 3:
+            arr = np.repeat(arr[..., None], ch, -1)
+        return arr
+
+    def predict_proba(self, queries) -> torch.Tensor:
+        """Device tensor [Q, num_classes] (used by the predictor's on-device ensemble)."""
+        return self._probs(self._queries_to_images(queries))
+
+    def predict(self, queries):
+        if len(queries) == 0:
+            return []
+        return self.predict_proba(queries).float().cpu().tolist()
+
+    def dump_parameters(self):
+        return {'meta': dict(self._meta), 'state': self._engine.state_dict(), 'knobs': dict(self._knobs)}
+
+    def load_parameters(self, params):
+        meta = params['meta']
+        self._build(meta['num_classes'], meta['channels'])
+        self._engine.load_state_dict(params['state'])
+        self._engine.prepare_eval()
+
+    def resident_bytes(self):
+        return self._engine.resident_bytes() if self._engine is not None else 0
+
+    def destroy(self):
+        self._engine = None

@@ -1,0 +1,221 @@
+"""POS-tagging models: BigramHmm (count-based bigram HMM + Viterbi) and PyBiLstm (BiLSTM tagger).
+
+Reference: examples/models/pos_tagging/BigramHmm.py:17-187 (counts :73-126, Viterbi :128-187)
+and PyBiLstm.py:19-274 (Embedding -> Dropout -> BiLSTM -> Linear; knobs :24-32).
+
+Task I/O (tasks.rst): a query is a list of tokens, a prediction is a list of integer tags.
+Differences: Viterbi runs vectorised in numpy log-space; the BiLSTM applies cross-entropy to
+logits (the reference applies it to softmax outputs, bug (k)), batches sentences bucketed by
+length, and runs on the trial's device (PyTorch-ROCm LSTM on GPU).
+"""
+import math
+
+import numpy as np
+
+from rafiki_amd.constants import TaskType  # noqa: F401
+from rafiki_amd.model import (BaseModel, CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, dataset_utils,
+                              logger)
+from rafiki_amd.parallel.context import current as trial_context
+
+
+def _accuracy(sents, preds):
+    tot = ok = 0
+    for s, p in zip(sents, preds):
+        for tok, t in zip(s, p):
+            tot += 1
+            ok += int(tok[1] == t)
+    return ok / max(1, tot)
+
+
+class BigramHmm(BaseModel):
+    @staticmethod
+    def get_knob_config():
+        return {'smoothing': FloatKnob(1e-3, 1.0, is_exp=True)}
+
+    def __init__(self, **knobs):
+        super().__init__(**knobs)
+        self._alpha = float(knobs.get('smoothing', 0.01))
+        self._vocab = {}
+        self._log_trans = self._log_emit = self._log_start = None
+
+    def train(self, dataset_uri):
+        ds = dataset_utils.load_dataset_of_corpus(dataset_uri)
+        sents = [ds[i] for i in range(len(ds))]
+        T = ds.tag_num_classes[0]
+        self._vocab = {}
+        for s in sents:
+            for tok in s:
+                self._vocab.setdefault(tok[0], len(self._vocab))
+        V = len(self._vocab) + 1  # last id = unknown word
+        start = np.full(T, self._alpha)
+        trans = np.full((T, T), self._alpha)
+        emit = np.full((T, V), self._alpha)
+        for s in sents:
+            prev = None
+            for tok in s:
+                w, t = self._vocab[tok[0]], tok[1]
+                emit[t, w] += 1
+                if prev is None:
+                    start[t] += 1
+                else:
+                    trans[prev, t] += 1
+                prev = t
+        self._log_start = np.log(start / start.sum())
+        self._log_trans = np.log(trans / trans.sum(1, keepdims=True))
+        self._log_emit = np.log(emit / emit.sum(1, keepdims=True))
+        logger.log('Train accuracy: {}'.format(_accuracy(sents, self._tag([[t[0] for t in s] for s in sents]))))
+
+    def _tag(self, sents_tokens):
+        out = []
+        unk = self._log_emit.shape[1] - 1
+        for toks in sents_tokens:
+            if not toks:
+                out.append([])
+                continue
+            ids = [self._vocab.get(w, unk) for w in toks]
+            score = self._log_start + self._log_emit[:, ids[0]]
+            back = []
+            for w in ids[1:]:
+                cand = score[:, None] + self._log_trans  # [prev, cur]
+                back.append(cand.argmax(0))
+                score = cand.max(0) + self._log_emit[:, w]
+            best = [int(score.argmax())]
+            for bp in reversed(back):
+                best.append(int(bp[best[-1]]))
+            out.append(best[::-1])
+        return out
+
+    def evaluate(self, dataset_uri):
+        ds = dataset_utils.load_dataset_of_corpus(dataset_uri)
+        sents = [ds[i] for i in range(len(ds))]
+        return float(_accuracy(sents, self._tag([[t[0] for t in s] for s in sents])))
+
+    def predict(self, queries):
+        return self._tag(queries)
+
+    def dump_parameters(self):
+        return {'vocab': self._vocab, 'start': self._log_start, 'trans': self._log_trans, 'emit': self._log_emit}
+
+    def load_parameters(self, params):
+        self._vocab = params['vocab']
+        self._log_start, self._log_trans, self._log_emit = params['start'], params['trans'], params['emit']
+
+
+class PyBiLstm(BaseModel):
+    @staticmethod
+    def get_knob_config():
+        return {
+            'epochs': FixedKnob(10),
+            'word_embed_dims': IntegerKnob(16, 128),
+            'word_rnn_hidden_size': IntegerKnob(16, 128),
+            'word_dropout': FloatKnob(1e-3, 2e-1, is_exp=True),
+            'learning_rate': FloatKnob(1e-2, 1e-1, is_exp=True),
+            'batch_size': CategoricalKnob([16, 32, 64, 128]),
+        }
+
+    def __init__(self, **knobs):
+        super().__init__(**knobs)
+        self._knobs = knobs
+        self._net = None
+        self._word_dict = {}
+        self._tag_count = 0
+        self.device = trial_context().device
+
+    def _create(self):
+        import torch
+        import torch.nn as nn
+        k = self._knobs
+        V = len(self._word_dict) + 2  # 0 = pad, 1 = unknown
+
+        class Net(nn.Module):
+            def __init__(s):
+                super().__init__()
+                s.emb = nn.Embedding(V, int(k.get('word_embed_dims', 64)), padding_idx=0)
+                s.drop = nn.Dropout(float(k.get('word_dropout', 0.1)))
+                s.lstm = nn.LSTM(int(k.get('word_embed_dims', 64)), int(k.get('word_rnn_hidden_size', 64)),
+                                 batch_first=True, bidirectional=True)
+                s.out = nn.Linear(2 * int(k.get('word_rnn_hidden_size', 64)), self._tag_count)
+
+            def forward(s, x):
+                h, _ = s.lstm(s.drop(s.emb(x)))
+                return s.out(h)
+
+        return Net().to(self.device)
+
+    def _encode(self, sents_tokens):
+        return [[self._word_dict.get(w, 1) for w in s] for s in sents_tokens]
+
+    def _batches(self, ids, tags, bs, shuffle, rng):
+        import torch
+        order = np.argsort([len(s) for s in ids], kind='stable')  # bucket by length
+        chunks = [order[i:i + bs] for i in range(0, len(order), bs)]
+        if shuffle:
+            rng.shuffle(chunks)
+        for ch in chunks:
+            L = max(1, max(len(ids[i]) for i in ch))
+            x = np.zeros((len(ch), L), np.int64)
+            y = np.full((len(ch), L), -100, np.int64)
+            for r, i in enumerate(ch):
+                x[r, :len(ids[i])] = ids[i]
+                if tags is not None:
+                    y[r, :len(tags[i])] = tags[i]
+            yield ch, torch.from_numpy(x).to(self.device), torch.from_numpy(y).to(self.device)
+
+    def train(self, dataset_uri):
+        import torch
+        import torch.nn.functional as F
+        ds = dataset_utils.load_dataset_of_corpus(dataset_uri)
+        sents = [ds[i] for i in range(len(ds))]
+        self._word_dict = {}
+        for s in sents:
+            for tok in s:
+                self._word_dict.setdefault(tok[0], len(self._word_dict) + 2)
+        self._tag_count = ds.tag_num_classes[0]
+        self._net = self._create()
+        opt = torch.optim.Adam(self._net.parameters(), lr=float(self._knobs.get('learning_rate', 0.05)))
+        ids = self._encode([[t[0] for t in s] for s in sents])
+        tags = [[t[1] for t in s] for s in sents]
+        rng = np.random.default_rng(0)
+        logger.define_loss_plot()
+        for ep in range(int(self._knobs.get('epochs', 10))):
+            self._net.train()
+            tot, n = 0.0, 0
+            for _, x, y in self._batches(ids, tags, int(self._knobs.get('batch_size', 32)), True, rng):
+                logits = self._net(x)
+                loss = F.cross_entropy(logits.reshape(-1, self._tag_count), y.reshape(-1), ignore_index=-100)
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+                tot += float(loss.item())
+                n += 1
+            logger.log_loss(loss=tot / max(1, n), epoch=ep)
+
+    def _predict(self, sents_tokens):
+        import torch
+        self._net.eval()
+        ids = self._encode(sents_tokens)
+        out = [None] * len(ids)
+        with torch.no_grad():
+            for ch, x, _ in self._batches(ids, None, 256, False, None):
+                pred = self._net(x).argmax(-1).cpu().numpy()
+                for r, i in enumerate(ch):
+                    out[i] = [int(t) for t in pred[r, :len(ids[i])]]
+        return out
+
+    def evaluate(self, dataset_uri):
+        ds = dataset_utils.load_dataset_of_corpus(dataset_uri)
+        sents = [ds[i] for i in range(len(ds))]
+        return float(_accuracy(sents, self._predict([[t[0] for t in s] for s in sents])))
+
+    def predict(self, queries):
+        return self._predict(queries)
+
+    def dump_parameters(self):
+        return {'net_state_dict': {k: v.cpu() for k, v in self._net.state_dict().items()},
+                'word_dict': self._word_dict, 'tag_count': self._tag_count}
+
+    def load_parameters(self, params):
+        self._word_dict = params['word_dict']
+        self._tag_count = params['tag_count']
+        self._net = self._create()
+        self._net.load_state_dict(params['net_state_dict'])

@@ -29,6 +29,11 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+def _nbytes(t):
+    """Bytes addressable from t.data_ptr() to the end of its storage (buffer-descriptor extent)."""
+    return t.untyped_storage().nbytes() - t.storage_offset() * t.element_size()
+
+
 def _s():
     return torch.cuda.current_stream().cuda_stream
 
@@ -53,7 +58,7 @@ def pick_tile(M: int, N: int) -> int:
 
 
 def pick_splits(M: int, N: int, K: int, tile: int, target_blocks: int = 2 * NUM_CU, min_ktiles: int = 4) -> int:
-    bm, bn = TILES[tile]
+    bm, bn = TILES[tile & 15]
     tiles = cdiv(M, bm) * cdiv(N, bn)
     ktiles = cdiv(K, 64)
     s = max(1, min(cdiv(target_blocks, tiles), ktiles // min_ktiles))
@@ -67,14 +72,14 @@ def igemm(kind, epi, A, B, out, M, N, K, lda=0, ldb=0, ldc=0, *, bias=None, stat
     if tile is None:
         tile = pick_tile(M, N)
     _lib.call("rk_igemm", kind, epi, tile, _p(A), _p(B), _p(out), _p(bias), _p(stats), _p(gate), M, N, K, lda, ldb,
-              ldc, H, W, C, taps, Cb, splits, slab_stride, flags, alpha, slope, _s())
+              ldc, H, W, C, taps, Cb, splits, slab_stride, flags, alpha, slope, _nbytes(A), _nbytes(B), _s())
     return out
 
 
 # ------------------------------------------------------------------------------------------ conv
 def stats_rows(M: int, N: int, tile: Optional[int] = None) -> int:
     t = pick_tile(M, N) if tile is None else tile
-    return cdiv(M, TILES[t][0]) * 2
+    return cdiv(M, TILES[t & 15][0]) * 2
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want_stats=False, act=ACT_NONE,

@@ -1,0 +1,73 @@
+"""Predictor HTTP service: ``POST /predict {"query": q} -> {"prediction": p}`` (reference
+rafiki/predictor/app.py:23-30) plus ``POST /predict_batch {"queries": [...]}`` (the reference's
+``predict_batch`` TODO, predictor.py:85-87).  Unauthenticated, like the reference.
+
+Run as a service: ``python -m rafiki_amd.predictor.server`` with RAFIKI_INFERENCE_JOB_ID,
+RAFIKI_SERVICE_ID and RAFIKI_SERVICE_PORT in the environment.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import sys
+import traceback
+
+from flask import Flask, jsonify, request
+
+logger = logging.getLogger(__name__)
+
+
+def create_app(predictor):
+    app = Flask('rafiki_amd.predictor')
+    predictor.start()
+
+    @app.errorhandler(Exception)
+    def err(e):
+        return traceback.format_exc(), 500
+
+    @app.route('/')
+    def index():
+        return 'Rafiki Predictor is up.'
+
+    @app.route('/predict', methods=['POST'])
+    def predict():
+        body = request.get_json(silent=True) or {}
+        return jsonify({'prediction': predictor.predict_one(body['query'])})
+
+    @app.route('/predict_batch', methods=['POST'])
+    def predict_batch():
+        body = request.get_json(silent=True) or {}
+        return jsonify({'predictions': predictor.predict(body['queries'])})
+
+    @app.route('/stats', methods=['GET'])
+    def stats():
+        return jsonify({**predictor.stats, 'models': [n for n, _ in predictor.models],
+                        'resident_bytes': predictor.cache.used})
+
+    return app
+
+
+def main():
+    from ..db.database import Database
+    from ..utils.log import configure_logging
+    from .predictor import Predictor
+    sid = os.environ.get('RAFIKI_SERVICE_ID')
+    configure_logging('service-{}-predictor'.format(sid))
+    db = Database()
+    try:
+        predictor = Predictor.from_inference_job(os.environ['RAFIKI_INFERENCE_JOB_ID'], db=db)
+    except Exception:
+        logger.error(traceback.format_exc())
+        if sid:
+            db.mark_service_as_errored(db.get_service(sid))
+        return 1
+    app = create_app(predictor)
+    if sid:
+        db.mark_service_as_running(db.get_service(sid))
+    port = int(os.environ.get('RAFIKI_SERVICE_PORT', '3003'))
+    app.run(host='0.0.0.0', port=port, threaded=True)
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

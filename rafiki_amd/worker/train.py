@@ -1,0 +1,201 @@
+"""TrainWorker: the trial loop of one sub-train-job, run by an SPMD worker group (one rank per GPU).
+
+Reference parity: rafiki/worker/train.py (``TrainWorker.start`` :37-132, ``stop`` :134-148,
+``_train_and_evaluate_model`` :150-186): budget check -> create trial -> propose knobs ->
+train/evaluate -> pickle params to ``<workdir>/params/<trial_id>.model`` -> report score.
+
+MI355X-native redesign:
+  * rank 0 owns the sub-train-job's advisor (GP-EI) and the budget; each round it proposes one knob
+    set per rank and broadcasts them as one packed fp64 tensor over RCCL (gloo on CPU); every rank
+    trains its own trial on its own GPU; (score, ok, seconds) come back by all_gather and rank 0
+    feeds the GP.  No HTTP in the loop, one shared GP posterior, and the budget is decided by one
+    process (fixes the reference's budget race, train.py:50 / SURVEY §5.2);
+  * models that declare ``DATA_PARALLEL = True`` train ONE trial per round on all ranks jointly
+    (bucketed gradient all-reduce inside the model), e.g. the PG-GAN;
+  * a failed trial is marked ERRORED and the loop continues (bounded by ``max_trial_errors``)
+    instead of killing the worker (reference bug (f));
+  * trial log lines go through the DB's batched writer.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import pickle
+import time
+import traceback
+
+import torch
+
+from ..advisor.advisor import make_advisor
+from ..constants import BudgetType, TrialStatus
+from ..model.log import logger as model_logger
+from ..model.model import load_model_class
+from ..parallel import dist as D
+from ..parallel.context import TrialContext, default_device, use_context
+
+logger = logging.getLogger(__name__)
+
+
+class _TrialLogHandler(logging.Handler):
+    def __init__(self, db, trial_id):
+        super().__init__(level=logging.INFO)
+        self.db, self.trial_id = db, trial_id
+
+    def emit(self, record):
+        try:
+            self.db.add_trial_log(self.trial_id, record.getMessage(), record.levelname)
+        except Exception:
+            pass
+
+
+class TrainWorker:
+    def __init__(self, service_id, worker_id, db=None, dist_info: D.DistInfo = None, params_dir=None,
+                 max_trial_errors=3, advisor_type=None, seed=None):
+        from ..config import get_config
+        from ..db.database import Database
+        self._service_id = service_id
+        self._worker_id = worker_id
+        self._db = db or Database()
+        self._dist = dist_info or D.DistInfo()
+        cfg = get_config()
+        self._params_dir = params_dir or os.path.join(cfg.workdir, cfg.params_dir)
+        os.makedirs(self._params_dir, exist_ok=True)
+        self._max_trial_errors = max_trial_errors
+        self._advisor_type = advisor_type
+        self._seed = seed
+        self._trial_id = None
+        self._stop = False
+        self.completed_trials = []
+
+    # ------------------------------------------------------------------------------ main loop
+    def start(self):
+        info = self._dist
+        worker = self._db.get_train_job_worker(self._service_id)
+        if worker is None:
+            raise RuntimeError('no train job worker for service {}'.format(self._service_id))
+        sub = self._db.get_sub_train_job(worker.sub_train_job_id)
+        train_job = self._db.get_train_job(sub.train_job_id)
+        model = self._db.get_model(sub.model_id)
+        budget = train_job.budget or {}
+        max_trials = int(budget.get(BudgetType.MODEL_TRIAL_COUNT, 5))
+        deadline = None
+        if BudgetType.TIME_HOURS in budget:
+            deadline = time.time() + float(budget[BudgetType.TIME_HOURS]) * 3600.0
+        clazz = load_model_class(model.model_file_bytes, model.model_class)
+        knob_config = clazz.get_knob_config()
+        data_parallel = bool(getattr(clazz, 'DATA_PARALLEL', False)) and info.world_size > 1
+        advisor = make_advisor(knob_config, self._advisor_type, self._seed) if info.is_main else None
+        device = default_device()
+        errors = 0
+        while not self._stop:
+            # ---- rank 0 decides this round (budget is enforced by exactly one process)
+            if info.is_main:
+                done = self._db.count_trials_of_sub_train_job(sub.id, [TrialStatus.COMPLETED, TrialStatus.ERRORED])
+                remaining = max(0, max_trials - done)
+                if deadline is not None and time.time() > deadline:
+                    remaining = 0
+                if errors >= self._max_trial_errors:
+                    remaining = 0
+                n_active = min(remaining, 1 if data_parallel else info.world_size)
+                props = advisor.propose_batch(n_active) if n_active > 0 else []
+                padded = props + [props[0] if props else advisor._random_knobs()] * (info.world_size - len(props))
+            else:
+                n_active, padded = 0, None
+            n_active = self._broadcast_int(n_active)
+            if n_active == 0:
+                break
+            proposals = D.broadcast_proposals(info, knob_config, padded) if info.world_size > 1 else padded
+            my = 0 if data_parallel else info.rank
+            active = my < n_active
+            ctx = TrialContext(device=device, dist=info, data_parallel=data_parallel)
+            score, ok, secs = float('nan'), 0.0, 0.0
+            if active:
+                record = (not data_parallel) or info.is_main
+                knobs = proposals[my]
+                t0 = time.time()
+                score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, record)
+                secs = time.time() - t0
+            table = D.gather_floats(info, [score if ok else float('nan'), ok, secs, float(active)])
+            if info.is_main:
+                for r in range(info.world_size):
+                    if table[r, 3] > 0 and (not data_parallel or r == 0):
+                        s = float(table[r, 0])
+                        advisor.feedback(proposals[0 if data_parallel else r], s if table[r, 1] > 0 else None)
+                        errors = errors + 1 if table[r, 1] == 0 else 0
+        if info.is_main:
+            logger.info('sub-train-job %s budget reached', sub.id)
+            self._db.mark_sub_train_job_as_stopped(self._db.get_sub_train_job(sub.id))
+
+    def _broadcast_int(self, v):
+        info = self._dist
+        if info.world_size == 1:
+            return int(v)
+        t = torch.tensor([v], dtype=torch.int64, device=D.comm_device(info))
+        torch.distributed.broadcast(t, src=0)
+        return int(t.item())
+
+    # -------------------------------------------------------------------------------- trial
+    def _run_trial(self, clazz, model, sub, knobs, train_job, ctx, record):
+        trial = None
+        if record:
+            trial = self._db.create_trial(sub.id, model.id, self._worker_id)
+            self._trial_id = trial.id
+            ctx.trial_id = trial.id
+            self._db.mark_trial_as_running(trial, knobs)
+        handler = _TrialLogHandler(self._db, trial.id) if record else None
+        prev_logger = model_logger.get_logger()
+        trial_logger = logging.getLogger('rafiki_amd.trial.{}'.format(trial.id if trial else 'dp'))
+        trial_logger.setLevel(logging.INFO)
+        trial_logger.propagate = False
+        if handler:
+            trial_logger.addHandler(handler)
+        model_logger.set_logger(trial_logger)
+        inst = None
+        try:
+            with use_context(ctx):
+                inst = clazz(**knobs)
+                with model_logger.phase('train'):
+                    inst.train(train_job.train_dataset_uri)
+                with model_logger.phase('evaluate'):
+                    score = float(inst.evaluate(train_job.test_dataset_uri))
+                if not math.isfinite(score):
+                    raise ValueError('non-finite score {}'.format(score))
+                params_path = None
+                if record:
+                    with model_logger.phase('dump_parameters'):
+                        blob = pickle.dumps(inst.dump_parameters())
+                    params_path = os.path.join(self._params_dir, '{}.model'.format(trial.id))
+                    tmp = params_path + '.tmp'
+                    with open(tmp, 'wb') as f:
+                        f.write(blob)
+                    os.replace(tmp, params_path)
+            if record:
+                self._db.mark_trial_as_complete(trial, score, params_path)
+                self.completed_trials.append((trial.id, score))
+            return score, 1.0
+        except Exception:
+            logger.error('trial failed:\n%s', traceback.format_exc())
+            if record and trial is not None:
+                self._db.add_trial_log(trial.id, traceback.format_exc(), 'ERROR')
+                self._db.mark_trial_as_errored(trial)
+            return float('nan'), 0.0
+        finally:
+            if inst is not None:
+                try:
+                    inst.destroy()
+                except Exception:
+                    pass
+            model_logger.set_logger(prev_logger)
+            if handler:
+                trial_logger.removeHandler(handler)
+            self._db.flush_logs()
+            self._trial_id = None
+
+    def stop(self):
+        self._stop = True
+        if self._trial_id is not None:
+            t = self._db.get_trial(self._trial_id)
+            if t is not None and t.status in (TrialStatus.STARTED, TrialStatus.RUNNING):
+                self._db.mark_trial_as_terminated(t)
+        self._db.flush_logs()
