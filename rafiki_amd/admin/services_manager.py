@@ -35,10 +35,10 @@ class ServiceDeploymentError(Exception):
 
 
 class ServicesManager:
-    def __init__(self, db, container_manager: ContainerManager, wait_timeout_s: float = 600.0):
+    def __init__(self, db, container_manager: ContainerManager, wait_timeout_s: float = None):
         self._db = db
         self._cm = container_manager
-        self._wait_timeout_s = wait_timeout_s
+        self._wait_timeout_s = wait_timeout_s or float(os.environ.get("RAFIKI_SERVICE_WAIT_TIMEOUT_S", "600"))
         self._cfg = config.get_config()
 
     # ---------------------------------------------------------------------------- inference
@@ -50,19 +50,20 @@ class ServicesManager:
             self._db.mark_inference_job_as_errored(inference_job)
             raise ServiceDeploymentError('no completed trials to serve')
         try:
-            predictor = self._create_service(ServiceType.PREDICT, PREDICTOR_IMAGE,
-                                             args=['-m', 'rafiki_amd.predictor.server'],
-                                             environment_vars={'RAFIKI_INFERENCE_JOB_ID': inference_job.id},
-                                             container_port=self._cfg.predictor_port,
-                                             gpus=1 if self._gpus_available() else 0)
             workers = []
-            for trial in best_trials:
+            for trial in best_trials:  # rows the predictor reads at start-up exist before it launches
                 svc = self._db.create_service(ServiceType.INFERENCE, type(self._cm).__name__, PREDICTOR_IMAGE, 1, 0)
-                self._db.mark_service_as_deploying(svc, 'in-predictor', predictor.container_service_id, None, None,
-                                                   None, None, {'predictor_service_id': predictor.id})
+                self._db.mark_service_as_deploying(svc, 'in-predictor', None, None, None, None, None, None)
                 self._db.create_inference_job_worker(svc.id, inference_job.id, trial.id)
                 workers.append(svc)
-            self._db.update_inference_job(inference_job, predictor_service_id=predictor.id)
+            predictor = self._create_service(
+                ServiceType.PREDICT, PREDICTOR_IMAGE, args=['-m', 'rafiki_amd.predictor.server'],
+                environment_vars={'RAFIKI_INFERENCE_JOB_ID': inference_job.id},
+                container_port=self._cfg.predictor_port, gpus=1 if self._gpus_available() else 0,
+                before_launch=lambda s: self._db.update_inference_job(inference_job, predictor_service_id=s.id))
+            for w in workers:
+                self._db.update_service_container_info(w, predictor.container_service_id, None, None, None, None,
+                                                       {'predictor_service_id': predictor.id})
             self._wait_until_services_running([predictor])
             for w in workers:
                 self._db.mark_service_as_running(w)
@@ -95,8 +96,9 @@ class ServicesManager:
                 env = {'WORKER_INSTALL_COMMAND': parse_model_install_command(model.dependencies, gpus > 0),
                        'RAFIKI_SUB_TRAIN_JOB_ID': sub.id}
                 svc = self._create_service(ServiceType.TRAIN, model.docker_image, args=['-m', 'rafiki_amd.worker'],
-                                           environment_vars=env, gpus=gpus, replicas=max(1, gpus))
-                self._db.create_train_job_worker(svc.id, sub.id)
+                                           environment_vars=env, gpus=gpus, replicas=max(1, gpus),
+                                           before_launch=lambda s, sub=sub: self._db.create_train_job_worker(
+                                               s.id, sub.id))
                 services.append(svc)
             self._wait_until_services_running(services, accept_stopped=True)
             self.refresh_train_job_status(train_job_id)
@@ -170,22 +172,28 @@ class ServicesManager:
         return bool(ledger and ledger.free)
 
     def _create_service(self, service_type, docker_image, args, environment_vars, container_port=None, gpus=0,
-                        replicas=1):
+                        replicas=1, before_launch=None):
+        """DB row -> (caller's rows) -> DEPLOYING -> launch -> record container info.  Everything the
+        service reads at start-up exists before it is launched, and the launched service is the
+        only writer of its later statuses (RUNNING/STOPPED/ERRORED)."""
         svc = self._db.create_service(service_type, type(self._cm).__name__, docker_image, replicas, gpus)
+        if before_launch is not None:
+            before_launch(svc)
         env = {'RAFIKI_SERVICE_ID': svc.id, 'RAFIKI_SERVICE_TYPE': service_type, 'WORKDIR_PATH': self._cfg.workdir,
                'RAFIKI_DB_PATH': self._db.path, 'PYTHONPATH': os.pathsep.join(p for p in sys.path if p)}
         env.update(environment_vars)
         publish = None
         if container_port is not None:
             publish = (free_port(), container_port)
+        name = 'rafiki-{}-{}'.format(service_type.lower(), svc.id[:8])
+        self._db.mark_service_as_deploying(svc, name, None, None, None, None, None, None)
         try:
-            cs: ContainerService = self._cm.create_service('rafiki-{}-{}'.format(service_type.lower(), svc.id[:8]),
-                                                           docker_image, args, env, None, replicas, publish, gpus)
+            cs: ContainerService = self._cm.create_service(name, docker_image, args, env, None, replicas, publish, gpus)
         except Exception:
             self._db.mark_service_as_errored(svc)
             raise
-        self._db.mark_service_as_deploying(svc, 'rafiki-{}'.format(svc.id[:8]), cs.id, cs.hostname, cs.port,
-                                           self._cfg.admin_host if cs.port else None, cs.port, cs.info)
+        self._db.update_service_container_info(svc, cs.id, cs.hostname, cs.port,
+                                               self._cfg.admin_host if cs.port else None, cs.port, cs.info)
         return svc
 
     def _stop_service(self, service):

@@ -216,20 +216,28 @@ class InProcessManager(ContainerManager):
     def __init__(self, target: Callable[[dict], None]):
         self.target = target
         self._threads: Dict[str, list] = {}
+        self._envs: Dict[str, dict] = {}
         self._ids = itertools.count()
 
     def create_service(self, service_name, docker_image, args, environment_vars, mounts=None, replicas=1,
                        publish_port=None, gpus=0):
         sid = 'inproc-{}'.format(next(self._ids))
         threads = []
-        for r in range(max(1, replicas)):
+        for r in range(max(1, replicas if gpus == 0 else 1)):
             env = dict(environment_vars or {})
             env.update({'RANK': '0', 'WORLD_SIZE': '1', 'LOCAL_RANK': '0'})
+            if publish_port is not None:
+                env['RAFIKI_SERVICE_PORT'] = str(publish_port[0])
             t = threading.Thread(target=self.target, args=(env,), daemon=True, name='{}-{}'.format(service_name, r))
             t.start()
             threads.append(t)
         self._threads[sid] = threads
+        self._envs[sid] = dict(environment_vars or {})
         return ContainerService(sid, '127.0.0.1', publish_port[0] if publish_port else None, {'threads': len(threads)})
 
     def destroy_service(self, service):
         self._threads.pop(service.id, None)
+        env = self._envs.pop(service.id, {})
+        shutdown = getattr(self.target, 'shutdown_service', None)
+        if shutdown is not None and 'RAFIKI_SERVICE_ID' in env:
+            shutdown(env['RAFIKI_SERVICE_ID'])

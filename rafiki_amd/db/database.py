@@ -368,6 +368,13 @@ class Database:
                             ext_hostname=ext_hostname, ext_port=ext_port,
                             container_service_info=container_service_info, status=ServiceStatus.DEPLOYING)
 
+    def update_service_container_info(self, service, container_service_id, hostname, port, ext_hostname, ext_port,
+                                      container_service_info):
+        """Record where a launched service lives without touching its status."""
+        return self._update(service, container_service_id=container_service_id, hostname=hostname, port=port,
+                            ext_hostname=ext_hostname, ext_port=ext_port,
+                            container_service_info=container_service_info)
+
     def mark_service_as_running(self, service):
         return self._update(service, status=ServiceStatus.RUNNING, datetime_stopped=None)
 

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import json
 import logging
+import threading
 import time
 from datetime import datetime
 
@@ -30,7 +31,12 @@ class ModelLogger:
         lg.propagate = False
         if not any(isinstance(h, ModelLoggerDebugHandler) for h in lg.handlers):
             lg.addHandler(ModelLoggerDebugHandler())
-        self._logger = lg
+        self._default = lg
+        self._tls = threading.local()  # workers inject per-thread loggers (several trials per process)
+
+    @property
+    def _logger(self):
+        return getattr(self._tls, 'logger', None) or self._default
 
     def define_loss_plot(self):
         self.define_plot('Loss Over Epochs', ['loss'], x_axis='epoch')
@@ -66,7 +72,8 @@ class ModelLogger:
         return ModelLogger._Timer(self, name)
 
     def set_logger(self, logger):
-        self._logger = logger
+        """Route this thread's model logs to ``logger`` (None restores the stdout debug logger)."""
+        self._tls.logger = None if logger is self._default else logger
 
     def get_logger(self):
         return self._logger

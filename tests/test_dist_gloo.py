@@ -1,0 +1,95 @@
+"""Multi-process (gloo, world_size 2) tests of the RCCL code paths: knob broadcast / score gather and
+the trial-parallel TrainWorker group (rank 0 advisor + budget, one trial per rank per round)."""
+import os
+import socket
+import tempfile
+from contextlib import closing
+
+import pytest
+import torch.multiprocessing as mp
+
+from rafiki_amd.models import model_file
+
+
+def _free_port():
+    with closing(socket.socket(socket.AF_INET, socket.SOCK_STREAM)) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port):
+    os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'RAFIKI_CPU_ONLY': '1'})
+
+
+def _knob_exchange(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rafiki_amd.model import CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob
+    from rafiki_amd.parallel import dist as D
+    info = D.init_distributed(backend='gloo')
+    kc = {'lr': FloatKnob(1e-3, 1.0, is_exp=True), 'n': IntegerKnob(1, 9), 'c': CategoricalKnob(['a', 'b']),
+          'f': FixedKnob(7)}
+    props = [{'lr': 0.01, 'n': 3, 'c': 'b', 'f': 7}, {'lr': 0.5, 'n': 9, 'c': 'a', 'f': 7}] if rank == 0 else None
+    got = D.broadcast_proposals(info, kc, props)
+    table = D.gather_floats(info, [float(rank), got[rank]['n']])
+    mx = D.all_reduce_max(info, float(rank) * 10)
+    with open(os.path.join(out_dir, 'r{}.txt'.format(rank)), 'w') as f:
+        f.write(repr((got, table.tolist(), mx)))
+    D.destroy(info)
+
+
+def test_knob_broadcast_and_gather():
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_knob_exchange, args=(2, port, d), nprocs=2, join=True)
+        for r in range(2):
+            got, table, mx = eval(open(os.path.join(d, 'r{}.txt'.format(r))).read())
+            assert got[1] == {'c': 'a', 'f': 7, 'lr': 0.5, 'n': 9}
+            assert got[0]['c'] == 'b' and got[0]['n'] == 3
+            assert table == [[0.0, 3.0], [1.0, 9.0]]
+            assert mx == 10.0
+
+
+def _setup_db(path, model_name, model_class, task, budget, train_uri, test_uri):
+    from rafiki_amd.db.database import Database
+    from rafiki_amd.utils.auth import hash_password
+    db = Database(path)
+    u = db.create_user('u@x', hash_password('p'), 'ADMIN')
+    with open(model_file(model_name), 'rb') as f:
+        m = db.create_model(u.id, model_class, task, f.read(), model_class, 'img', {}, 'PRIVATE')
+    tj = db.create_train_job(u.id, 'app', 1, task, budget, train_uri, test_uri)
+    sub = db.create_sub_train_job(tj.id, m.id, u.id)
+    svc = db.create_service('TRAIN', 'test', 'img', 2, 0)
+    db.create_train_job_worker(svc.id, sub.id)
+    return db, svc.id, sub.id
+
+
+def _worker_group(rank, world, port, db_path, service_id, workdir):
+    _env(rank, world, port)
+    os.environ['WORKDIR_PATH'] = workdir
+    from rafiki_amd.db.database import Database
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.worker.train import TrainWorker
+    info = D.init_distributed(backend='gloo')
+    w = TrainWorker(service_id, 'w{}'.format(rank), db=Database(db_path), dist_info=info, seed=0)
+    w.start()
+    D.destroy(info)
+
+
+def test_trial_parallel_worker_group_skdt():
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        db_path = os.path.join(d, 'db.sqlite3')
+        db, sid, sub_id = _setup_db(db_path, 'SkDt', 'SkDt', 'IMAGE_CLASSIFICATION', {'MODEL_TRIAL_COUNT': 5},
+                                    'synthetic://image?n=300&size=28&channels=1&classes=5&seed=0',
+                                    'synthetic://image?n=100&size=28&channels=1&classes=5&seed=1')
+        mp.spawn(_worker_group, args=(2, port, db_path, sid, d), nprocs=2, join=True)
+        trials = db.get_trials_of_sub_train_job(sub_id)
+        assert len(trials) == 5  # budget enforced exactly by rank 0 (2 + 2 + 1)
+        assert all(t.status == 'COMPLETED' for t in trials)
+        assert len({t.worker_id for t in trials}) == 2  # both ranks ran trials
+        for t in trials:
+            assert os.path.exists(t.params_file_path) and 0.0 <= t.score <= 1.0
+            logs = db.get_trial_logs(t.id)
+            assert any('phase' in l.line for l in logs)
+        assert db.get_sub_train_job(sub_id).datetime_stopped is not None

@@ -1,0 +1,153 @@
+"""End-to-end over HTTP with the public Client, modeled on the reference's integration suite
+(test/test_users.py, test/test_models.py, test/test_train_jobs.py) plus the serve path it lacks
+(create inference job -> POST /predict).  Services run in-process (InlineServiceRunner), CPU only."""
+import os
+import threading
+import time
+import uuid
+
+import pytest
+from werkzeug.serving import make_server
+
+from rafiki_amd.admin.admin import Admin
+from rafiki_amd.admin.app import create_app
+from rafiki_amd.client import Client, RafikiConnectionError
+from rafiki_amd.constants import TaskType, UserType
+from rafiki_amd.container.container_manager import InProcessManager, free_port
+from rafiki_amd.container.inline import InlineServiceRunner
+from rafiki_amd.db.database import Database
+from rafiki_amd.model.dataset import synthetic_images, write_image_files_zip
+from rafiki_amd.models import model_file
+
+SUPER = ('superadmin@rafiki', 'rafiki')
+
+
+@pytest.fixture(scope='module')
+def stack(tmp_path_factory):
+    d = tmp_path_factory.mktemp('stack')
+    os.environ['WORKDIR_PATH'] = str(d)
+    os.environ['RAFIKI_CPU_ONLY'] = '1'
+    db_path = str(d / 'db.sqlite3')
+    runner = InlineServiceRunner(db_path)
+    admin = Admin(db=Database(db_path), container_manager=InProcessManager(runner))
+    admin.seed()
+    port = free_port()
+    srv = make_server('127.0.0.1', port, create_app(admin), threaded=True)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    imgs, labels = synthetic_images(240, size=28, channels=1, classes=4, seed=0)
+    train = write_image_files_zip(str(d / 'train.zip'), imgs[:180], labels[:180])
+    test = write_image_files_zip(str(d / 'test.zip'), imgs[180:], labels[180:])
+    yield {'port': port, 'train': train, 'test': test, 'admin': admin}
+    srv.shutdown()
+    runner.shutdown()
+
+
+def client(stack, who=SUPER):
+    c = Client(admin_host='127.0.0.1', admin_port=stack['port'])
+    c.login(*who)
+    return c
+
+
+def make_user(stack, user_type):
+    email = '{}@test'.format(uuid.uuid4().hex[:8])
+    client(stack).create_user(email, 'pw', user_type)
+    return client(stack, (email, 'pw')), email
+
+
+def test_users_rbac(stack):
+    admin_c, admin_email = make_user(stack, UserType.ADMIN)
+    dev_c, dev_email = make_user(stack, UserType.MODEL_DEVELOPER)
+    assert any(u['email'] == dev_email for u in admin_c.get_users())
+    with pytest.raises(RafikiConnectionError):
+        dev_c.get_users()
+    with pytest.raises(RafikiConnectionError):  # only superadmin creates admins
+        admin_c.create_user('x{}@t'.format(uuid.uuid4().hex[:6]), 'pw', UserType.ADMIN)
+    admin_c.ban_user(dev_email)
+    with pytest.raises(RafikiConnectionError):
+        client(stack, (dev_email, 'pw'))
+    with pytest.raises(RafikiConnectionError):  # cannot ban yourself
+        admin_c.ban_user(admin_email)
+
+
+def test_models_crud_and_isolation(stack, tmp_path):
+    dev_c, _ = make_user(stack, UserType.MODEL_DEVELOPER)
+    other_c, _ = make_user(stack, UserType.MODEL_DEVELOPER)
+    m = dev_c.create_model('dt_' + uuid.uuid4().hex[:6], TaskType.IMAGE_CLASSIFICATION, model_file('SkDt'), 'SkDt')
+    got = dev_c.get_model(m['id'])
+    assert got['model_class'] == 'SkDt' and got['access_right'] == 'PRIVATE'
+    out = str(tmp_path / 'm.py')
+    dev_c.download_model_file(m['id'], out)
+    assert open(out, 'rb').read() == open(model_file('SkDt'), 'rb').read()
+    assert m['id'] in [x['id'] for x in dev_c.get_available_models(TaskType.IMAGE_CLASSIFICATION)]
+    assert m['id'] not in [x['id'] for x in other_c.get_available_models()]
+    with pytest.raises(RafikiConnectionError):
+        other_c.get_model(m['id'])
+    pub = dev_c.create_model('pub_' + uuid.uuid4().hex[:6], TaskType.IMAGE_CLASSIFICATION, model_file('SkDt'), 'SkDt',
+                             access_right='PUBLIC')
+    assert pub['id'] in [x['id'] for x in other_c.get_available_models()]
+    dev_c.delete_model(m['id'])
+    with pytest.raises(RafikiConnectionError):
+        dev_c.get_model(m['id'])
+
+
+def _wait_stopped(c, app, timeout=300):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        tj = c.get_train_job(app)
+        if tj['status'] in ('STOPPED', 'ERRORED'):
+            return tj
+        time.sleep(0.5)
+    raise TimeoutError(app)
+
+
+def test_train_infer_predict(stack):
+    dev_c, _ = make_user(stack, UserType.MODEL_DEVELOPER)
+    m1 = dev_c.create_model('dt_' + uuid.uuid4().hex[:6], TaskType.IMAGE_CLASSIFICATION, model_file('SkDt'), 'SkDt')
+    m2 = dev_c.create_model('ff_' + uuid.uuid4().hex[:6], TaskType.IMAGE_CLASSIFICATION, model_file('FeedForward'),
+                            'FeedForward')
+    app = 'fashion_' + uuid.uuid4().hex[:6]
+    tj = dev_c.create_train_job(app, TaskType.IMAGE_CLASSIFICATION, stack['train'], stack['test'],
+                                {'MODEL_TRIAL_COUNT': 2, 'GPU_COUNT': 0}, models=[m1['id'], m2['id']])
+    assert tj['app_version'] == 1
+    tj = _wait_stopped(dev_c, app)
+    assert tj['status'] == 'STOPPED', tj
+    assert len(tj['workers']) == 2 and {w['model_name'] for w in tj['workers']} == {m1['name'], m2['name']}
+    trials = dev_c.get_trials_of_train_job(app)
+    assert len(trials) == 4 and all(t['status'] == 'COMPLETED' for t in trials)
+    best = dev_c.get_best_trials_of_train_job(app, max_count=2)
+    assert len(best) == 2 and best[0]['score'] >= best[1]['score']
+    trial = dev_c.get_trial(best[0]['id'])
+    assert trial['model_name'] in (m1['name'], m2['name']) and trial['worker_id']
+    logs = dev_c.get_trial_logs(best[0]['id'])
+    assert logs['metrics'] and 'plots' in logs
+    params = dev_c.get_trial_parameters(best[0]['id'])
+    assert isinstance(params, dict)
+    assert [x['app'] for x in dev_c.get_train_jobs_of_app(app)] == [app]
+    # inference
+    ij = dev_c.create_inference_job(app)
+    assert ij['predictor_host']
+    running = dev_c.get_running_inference_job(app)
+    assert running['status'] == 'RUNNING' and len(running['workers']) == 2
+    q = stack_query = synthetic_images(1, size=28, channels=1, classes=4, seed=5)[0][0].tolist()
+    pred = dev_c.predict(ij['predictor_host'], q)
+    assert len(pred) >= 4 and abs(sum(pred) - 1.0) < 1e-3
+    preds = dev_c.predict_batch(ij['predictor_host'], [stack_query, stack_query])
+    assert len(preds) == 2
+    with pytest.raises(RafikiConnectionError):  # one running inference job per train job
+        dev_c.create_inference_job(app)
+    dev_c.stop_inference_job(app)
+    assert dev_c.get_inference_jobs_of_app(app)[0]['status'] == 'STOPPED'
+    # second train job of the same app auto-increments version
+    tj2 = dev_c.create_train_job(app, TaskType.IMAGE_CLASSIFICATION, stack['train'], stack['test'],
+                                 {'MODEL_TRIAL_COUNT': 1}, models=[m1['id']])
+    assert tj2['app_version'] == 2
+    _wait_stopped(dev_c, app)
+
+
+def test_stop_all_jobs_superadmin_only(stack):
+    dev_c, _ = make_user(stack, UserType.APP_DEVELOPER)
+    with pytest.raises(RafikiConnectionError):
+        dev_c.stop_all_jobs()
+    out = client(stack).stop_all_jobs()
+    assert set(out) == {'train_jobs', 'inference_jobs'}
