@@ -35,6 +35,7 @@ enum OpMode {
   OP_DENSE_KOUT = 3,  // X[k][i], row stride ld                      (dY in wgrad, W in dX)
   OP_CONV_KOUT = 4,   // rows = pixels, cols = (tap, c) gathered     (conv weight-grad B)
   OP_WTAP_KOUT = 5,   // rows = (tap, co), cols = c of W[co][tap][c] (conv data-grad B)
+  OP_CONVUP_KIN = 6,  // NHWC gather from a 2x nearest-upscaled input (fused upscale2d + conv3x3)
 };
 enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
 enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16,
@@ -58,7 +59,17 @@ struct IgemmParams {
   float alpha;          // output scale
   float slope;          // leaky-relu slope
   unsigned long long bytesA, bytesB;  // operand extents for the buffer descriptors (< 2 GiB)
+  float invC;                         // 1/C for non-power-of-two channel counts
 };
+
+// channel arithmetic of the gathered activation: shifts when C is a power of two (every VGG /
+// PG-GAN layer but one), multiply / reciprocal otherwise (the PG-GAN discriminator's 4x4 conv sees
+// 512 + 1 minibatch-stddev channels, padded to 520).  The branch is on a kernel argument (uniform).
+RK_DEV int ch_div(int k, const IgemmParams& p) {
+  return p.log2C >= 0 ? (k >> p.log2C) : (int)(((float)k + 0.5f) * p.invC);
+}
+RK_DEV int ch_mod(int k, int q, const IgemmParams& p) { return p.log2C >= 0 ? (k & (p.C - 1)) : k - q * p.C; }
+RK_DEV unsigned ch_mul(unsigned v, const IgemmParams& p) { return p.log2C >= 0 ? (v << p.log2C) : v * (unsigned)p.C; }
 
 // ---- LDS images --------------------------------------------------------------------------------
 // K-inner [T][BK] bf16, 128-byte rows, 16-B chunk c of row i lives at chunk (c ^ ((i>>1)&7)):
@@ -100,7 +111,8 @@ RK_DEV int tap_dx(int t) { return t - 3 * ((t * 11) >> 5) - 1; }
 
 template <int MODE, int T>
 struct Operand {
-  static constexpr bool KIN = (MODE == OP_DENSE_KIN || MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN);
+  static constexpr bool KIN = (MODE == OP_DENSE_KIN || MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN ||
+                               MODE == OP_CONVUP_KIN);
   static constexpr int CH = T * BK / 8 / 256;  // 16-B chunks per thread per K-tile
   static constexpr int R = T / 8;              // chunks per K-outer row
   static constexpr int KROWS_PER_PASS = 256 / R;
@@ -133,7 +145,15 @@ struct Operand {
           tapmask[i] = ok ? 1u : 0u;
         } else {
           const int h = (gi >> p.log2W) & (p.H - 1), w = gi & (p.W - 1);
-          rowoff[i] = ((unsigned)gi << p.log2C) * 2u;
+          if constexpr (MODE == OP_CONVUP_KIN) {
+            // output pixel (n, h, w) reads input pixel (n, (h+dy)>>1, (w+dx)>>1) of the H/2 x W/2 map
+            const int n = gi >> (p.log2H + p.log2W);
+            const unsigned ip = ((unsigned)n * (unsigned)(p.H >> 1) + (unsigned)(h >> 1)) * (unsigned)(p.W >> 1) +
+                                (unsigned)(w >> 1);
+            rowoff[i] = ch_mul(ip, p) * 2u;
+          } else {
+            rowoff[i] = ch_mul((unsigned)gi, p) * 2u;
+          }
           unsigned m = 0;
           if (p.taps == 1) {
             m = 1u;
@@ -146,6 +166,7 @@ struct Operand {
               m |= (in ? 1u : 0u) << t;
             }
           }
+          if constexpr (MODE == OP_CONVUP_KIN) m |= ((unsigned)(h & 1) << 16) | ((unsigned)(w & 1) << 17);
           tapmask[i] = ok ? m : 0u;
         }
       }
@@ -158,10 +179,10 @@ struct Operand {
       colok = col < extent;
       dh = dw = 0;
       if constexpr (MODE == OP_CONV_KOUT) {
-        const int tap = col >> p.log2C;
+        const int tap = ch_div(col, p);
         colok = colok && tap < p.taps;
         if (p.taps == 9) { dh = tap_dy(tap); dw = tap_dx(tap); }
-        coloff = (unsigned)(col & (p.C - 1)) * 2u;
+        coloff = (unsigned)ch_mod(col, tap, p) * 2u;
       } else {
         coloff = (unsigned)col * 2u;
       }
@@ -179,18 +200,33 @@ struct Operand {
       }
     } else if constexpr (MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN) {
       const int k = kt * BK + cchunk * 8;
-      const int tap = k >> p.log2C;  // >= taps -> no mask bit -> zero
-      const int ci = k & (p.C - 1);
+      const int tap = ch_div(k, p);  // >= taps -> no mask bit -> zero
+      const int ci = ch_mod(k, tap, p);
       int dy = 0, dx = 0;
       if (p.taps == 9) {
         dy = tap_dy(tap);
         dx = tap_dx(tap);
         if constexpr (MODE == OP_CONVT_KIN) { dy = -dy; dx = -dx; }
       }
-      const int delta = (((dy * p.W + dx) << p.log2C) + ci) * 2;
+      const int delta = ((int)ch_mul((unsigned)(dy * p.W + dx), p) + ci) * 2;
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const bool ok = (tapmask[i] >> tap) & 1u;
+        r[i] = bload(rsrc, ok ? (unsigned)((int)rowoff[i] + delta) : OOB);
+      }
+    } else if constexpr (MODE == OP_CONVUP_KIN) {
+      const int k = kt * BK + cchunk * 8;
+      const int tap = ch_div(k, p);
+      const int ci = ch_mod(k, tap, p);
+      const int dy = tap_dy(tap), dx = tap_dx(tap);
+      const int Wi = p.W >> 1;
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const unsigned m = tapmask[i];
+        const bool ok = (m >> tap) & 1u;
+        const int dyi = ((int)((m >> 16) & 1u) + dy) >> 1;  // floor((parity + d) / 2)
+        const int dxi = ((int)((m >> 17) & 1u) + dx) >> 1;
+        const int delta = ((int)ch_mul((unsigned)(dyi * Wi + dxi), p) + ci) * 2;
         r[i] = bload(rsrc, ok ? (unsigned)((int)rowoff[i] + delta) : OOB);
       }
     } else if constexpr (MODE == OP_DENSE_KOUT) {
@@ -206,7 +242,7 @@ struct Operand {
         const int k = kt * BK + krow0 + KROWS_PER_PASS * i;  // pixel index
         const int h = (k >> p.log2W) & (p.H - 1), w = k & (p.W - 1);
         const bool ok = colok && k < K && (unsigned)(h + dh) < (unsigned)p.H && (unsigned)(w + dw) < (unsigned)p.W;
-        r[i] = bload(rsrc, ok ? (((unsigned)(k + dh * p.W + dw)) << p.log2C) * 2u + coloff : OOB);
+        r[i] = bload(rsrc, ok ? ch_mul((unsigned)(k + dh * p.W + dw), p) * 2u + coloff : OOB);
       }
     } else {  // OP_WTAP_KOUT: row k = tap*Cout + co  ->  W[co][tap][c]
 #pragma unroll
@@ -247,6 +283,303 @@ struct Operand {
     }
   }
 };
+
+// ================================================================================================
+// LDS-DMA variant: operands go global -> LDS directly (buffer_load_dwordx4 ... lds), no VGPR
+// staging and no ds_write pass.  The LDS image is lane-linear per wave-instruction (1 KiB), so each
+// lane's SOURCE address is chosen by inverting the XOR swizzle: the bytes that land in LDS slot s
+// are exactly the chunk kin_off/kout_off would have put there, and the frag() readers are unchanged
+// (cdna_hip_programming.md §5.4 rule 21: swizzle the source, keep the destination linear).
+// Out-of-range lanes (conv halo, tile edges, K tail) DMA zeros via the descriptor range check.
+// NST = 3: a ring of three K-tile stages, two tiles in flight, ONE raw s_barrier per K-tile and a
+// counted vmcnt (never __syncthreads(), whose implicit vmcnt(0) would drain the ring).
+// ================================================================================================
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int MODE, int T>
+struct DmaOperand {
+  static constexpr bool KIN = Operand<MODE, T>::KIN;
+  static constexpr int R = T / 8;           // 16-B slots per K-outer row / per K-inner tile column
+  static constexpr int NI = T / 32;         // wave-instructions (1 KiB each) per wave per K-tile
+  __amdgpu_buffer_rsrc_t rsrc;
+  // per (lane, instruction) state, fixed across K-tiles
+  unsigned base[NI];   // K-inner: row byte offset (+ chunk for dense); K-outer: column byte offset
+  unsigned vmask[NI];  // K-inner conv: tap mask; dense: row-valid; K-outer: column-valid
+  int sub[NI];         // K-inner: logical chunk c; K-outer: k-row within the tile
+  int dh[NI], dw[NI];  // K-outer conv: tap shift of this lane's column
+
+  RK_DEV void init(const IgemmParams& p, const bf16* ptr, unsigned long long bytes, int ld, int tile0, int extent,
+                   int wid, int lane) {
+    rsrc = make_rsrc(ptr, bytes);
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int j = wid * NI + q;        // wave-instruction index within the operand tile
+      const int slot = j * 64 + lane;    // 16-B slot this lane's bytes land in
+      if constexpr (KIN) {
+        const int i = slot >> 3;                       // tile row
+        const int c = (slot & 7) ^ ((i >> 1) & 7);     // logical chunk stored at this slot
+        sub[q] = c;
+        const int gi = tile0 + i;
+        const bool ok = gi < extent;
+        if constexpr (MODE == OP_DENSE_KIN) {
+          base[q] = (unsigned)gi * (unsigned)ld * 2u + (unsigned)c * 16u;
+          vmask[q] = ok ? 1u : 0u;
+        } else {
+          const int h = (gi >> p.log2W) & (p.H - 1), w = gi & (p.W - 1);
+          base[q] = ((unsigned)gi << p.log2C) * 2u;
+          unsigned m = 1u;
+          if (p.taps == 9) {
+            m = 0u;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+              int dy = tap_dy(t), dx = tap_dx(t);
+              if constexpr (MODE == OP_CONVT_KIN) { dy = -dy; dx = -dx; }
+              m |= (((unsigned)(h + dy) < (unsigned)p.H && (unsigned)(w + dx) < (unsigned)p.W) ? 1u : 0u) << t;
+            }
+          }
+          vmask[q] = ok ? m : 0u;
+        }
+        dh[q] = dw[q] = 0;
+      } else {
+        const int krow = slot / R;
+        int f;
+        if constexpr (R == 16) f = ((krow & 3) << 2) | ((krow >> 2) & 3);
+        else f = ((krow & 3) << 1) | ((krow >> 2) & 1);
+        const int ch = (slot % R) ^ f;
+        sub[q] = krow;
+        const int col = tile0 + ch * 8;
+        bool ok = col < extent;
+        dh[q] = dw[q] = 0;
+        if constexpr (MODE == OP_CONV_KOUT) {
+          const int tap = col >> p.log2C;
+          ok = ok && tap < p.taps;
+          if (p.taps == 9) { dh[q] = tap_dy(tap); dw[q] = tap_dx(tap); }
+          base[q] = (unsigned)(col & (p.C - 1)) * 2u;
+        } else {
+          base[q] = (unsigned)col * 2u;
+        }
+        vmask[q] = ok ? 1u : 0u;
+      }
+    }
+  }
+
+  // byte offset (or OOB) of this lane's chunk for instruction q of K-tile kt
+  RK_DEV unsigned offset(const IgemmParams& p, int q, int kt, int K, int ld) const {
+    if constexpr (MODE == OP_DENSE_KIN) {
+      const int k = kt * BK + sub[q] * 8;
+      return (vmask[q] && k < K) ? base[q] + (unsigned)(kt * BK) * 2u : OOB;
+    } else if constexpr (MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN) {
+      const int k = kt * BK + sub[q] * 8;
+      const int tap = k >> p.log2C, ci = k & (p.C - 1);
+      int dy = 0, dx = 0;
+      if (p.taps == 9) {
+        dy = tap_dy(tap);
+        dx = tap_dx(tap);
+        if constexpr (MODE == OP_CONVT_KIN) { dy = -dy; dx = -dx; }
+      }
+      const bool ok = (vmask[q] >> tap) & 1u;
+      return ok ? (unsigned)((int)base[q] + ((((dy * p.W + dx) << p.log2C) + ci) * 2)) : OOB;
+    } else if constexpr (MODE == OP_DENSE_KOUT) {
+      const int k = kt * BK + sub[q];
+      return (vmask[q] && k < K) ? base[q] + (unsigned)k * (unsigned)ld * 2u : OOB;
+    } else if constexpr (MODE == OP_CONV_KOUT) {
+      const int k = kt * BK + sub[q];
+      const int h = (k >> p.log2W) & (p.H - 1), w = k & (p.W - 1);
+      const bool ok = vmask[q] && k < K && (unsigned)(h + dh[q]) < (unsigned)p.H &&
+                      (unsigned)(w + dw[q]) < (unsigned)p.W;
+      return ok ? (((unsigned)(k + dh[q] * p.W + dw[q])) << p.log2C) * 2u + base[q] : OOB;
+    } else {  // OP_WTAP_KOUT
+      const int k = kt * BK + sub[q];
+      const int tap = k >> p.log2Cb, co = k & ((1 << p.log2Cb) - 1);
+      return (vmask[q] && k < K) ? ((unsigned)co * (unsigned)ld + (unsigned)tap * (unsigned)p.N) * 2u + base[q]
+                                 : OOB;
+    }
+  }
+
+  RK_DEV void issue(const IgemmParams& p, char* lds_tile, int kt, int K, int ld, int wid) const {
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      char* dst = lds_tile + (wid * NI + q) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)dst, 16, (int)offset(p, q, kt, K, ld), 0, 0, 0);
+    }
+  }
+};
+
+template <int N>
+RK_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+RK_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int AM, int BMODE, int EPI, int NST>
+__global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, SB = A_BYTES + B_BYTES;
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
+  constexpr int L = DmaOperand<AM, BM>::NI + DmaOperand<BMODE, BN>::NI;  // DMA instr / wave / K-tile
+  __shared__ __attribute__((aligned(16))) char smem[NST * SB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tilesN = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / tilesN, nt = bid - mt * tilesN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kTiles = (p.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * p.ktPer;
+  const int kt1 = min(kTiles, kt0 + p.ktPer);
+
+  DmaOperand<AM, BM> opA;
+  DmaOperand<BMODE, BN> opB;
+  opA.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane);
+  opB.init(p, p.B, p.bytesB, p.ldb, n0, p.N, wid, lane);
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt, int stage) {
+    char* st = smem + stage * SB;
+    opA.issue(p, st, kt, p.K, p.lda, wid);
+    opB.issue(p, st + A_BYTES, kt, p.K, p.ldb, wid);
+  };
+  auto compute = [&](const char* la) {
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = Operand<AM, BM>::frag(la, wm * WM + i * 16, ks * 32, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bfr[j] = Operand<BMODE, BN>::frag(lb, wn * WN + j * 16, ks * 32, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (kt0 < kt1) issue(kt0, 0);
+  if (kt0 + 1 < kt1) issue(kt0 + 1, 1);
+  int stage = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    if (kt + 1 < kt1) wait_vmcnt<L>();   // this wave's DMAs of tile kt landed (kt+1 may fly)
+    else wait_vmcnt<0>();
+    raw_barrier();                       // ... and every other wave's
+    if constexpr (NST == 3) {
+      if (kt + 2 < kt1) issue(kt + 2, stage == 0 ? 2 : stage - 1);  // stage of tile kt-1: free
+      compute(smem + stage * SB);
+      stage = stage == 2 ? 0 : stage + 1;
+    } else {
+      compute(smem + stage * SB);
+      raw_barrier();                     // everyone is done reading this stage
+      if (kt + 2 < kt1) issue(kt + 2, stage);
+      stage ^= 1;
+    }
+  }
+  wait_vmcnt<0>();
+
+  // ---- epilogue: lane owns out[m][n..n+3] of every (i, j) fragment --------------------------
+  const int mrow = m0 + wm * WM + (lane & 15);
+  const int ncol = n0 + wn * WN + 4 * (lane >> 4);
+  if constexpr (EPI == EPI_BF16) {
+    bf16* C = (bf16*)p.out;
+    float s[NI][4], ss[NI][4];
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[j][e] = ss[j][e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = ncol + j * 16;
+      const bool nok = n < p.N;
+      float b[4] = {0.f, 0.f, 0.f, 0.f};
+      if ((p.flags & FLAG_BIAS) && nok) {
+        const f32x4 bv = *(const f32x4*)(p.bias + n);
+        b[0] = bv[0]; b[1] = bv[1]; b[2] = bv[2]; b[3] = bv[3];
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = mrow + i * 16;
+        if (!(nok && m < p.M)) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] * p.alpha + b[e];
+          s[j][e] += v[e];
+          ss[j][e] += v[e] * v[e];
+        }
+        if (p.flags & FLAG_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (p.flags & FLAG_LRELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope;
+        }
+        if (p.flags & FLAG_GATE) {
+          const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+        *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
+      }
+    }
+    if (p.flags & FLAG_STATS) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = s[j][e], b = ss[j][e];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            a += __shfl_xor(a, o, 64);
+            b += __shfl_xor(b, o, 64);
+          }
+          s[j][e] = a;
+          ss[j][e] = b;
+        }
+      if ((lane & 15) == 0) {
+        float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int n = ncol + j * 16;
+          if (n < p.N) {
+            *(f32x4*)(row + n) = f32x4{s[j][0], s[j][1], s[j][2], s[j][3]};
+            *(f32x4*)(row + p.N + n) = f32x4{ss[j][0], ss[j][1], ss[j][2], ss[j][3]};
+          }
+        }
+      }
+    }
+  } else {
+    float* C = (float*)p.out + (long long)blockIdx.z * p.slabStride;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = ncol + j * 16;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = mrow + i * 16;
+        if (m >= p.M) continue;
+        f32x4 v = acc[i][j] * p.alpha;
+        if (p.flags & FLAG_BIAS) v += *(const f32x4*)(p.bias + n);
+        float* dst = C + (long long)m * p.ldc + n;
+        if (p.flags & FLAG_ACCUM) v += *(const f32x4*)dst;
+        *(f32x4*)dst = v;
+      }
+    }
+  }
+}
 
 template <int BM, int BN, int AM, int BMODE, int EPI, int PF>
 __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
@@ -456,7 +789,11 @@ template <int BM, int BN, int AM, int BMODE, int EPI>
 int launch_tile(const IgemmParams& p, int splits, int pf, hipStream_t st) {
   const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
   dim3 grid(tiles, 1, splits);
-  if (pf == 2)
+  if (pf == 3)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, AM, BMODE, EPI, 3>), grid, dim3(256), 0, st, p);
+  else if (pf == 4)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, AM, BMODE, EPI, 2>), grid, dim3(256), 0, st, p);
+  else if (pf == 2)
     hipLaunchKernelGGL((igemm_kernel<BM, BN, AM, BMODE, EPI, 2>), grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL((igemm_kernel<BM, BN, AM, BMODE, EPI, 1>), grid, dim3(256), 0, st, p);
@@ -466,7 +803,9 @@ int launch_tile(const IgemmParams& p, int splits, int pf, hipStream_t st) {
 
 template <int AM, int BMODE, int EPI>
 int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
-  const int pf = (tile >> 4) ? 2 : 1;  // bit 4 of the tile code: two K-tiles in flight
+  // tile code: bits 0-3 tile shape; 16 = register ring (2 tiles in flight); 32 = LDS-DMA 3-stage
+  // ring; 64 = LDS-DMA 2-stage
+  const int pf = (tile & 32) ? 3 : (tile & 64) ? 4 : (tile & 16) ? 2 : 1;
   switch (tile & 15) {
     case 0: return launch_tile<128, 128, AM, BMODE, EPI>(p, splits, pf, st);
     case 1: return launch_tile<128, 64, AM, BMODE, EPI>(p, splits, pf, st);
@@ -478,7 +817,8 @@ int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
 
 }  // namespace
 
-// kind: 0 conv-fwd, 1 conv-dgrad, 2 conv-wgrad, 3 dense (A·Bᵀ), 4 dense dX (A·B), 5 dense dW (Aᵀ·B)
+// kind: 0 conv-fwd, 1 conv-dgrad, 2 conv-wgrad, 3 dense (A·Bᵀ), 4 dense dX (A·B), 5 dense dW (Aᵀ·B),
+//       6 fused nearest-upscale(2x) + conv3x3 forward (PG-GAN _upscale2d_conv2d)
 // epi: 0 bf16 out, 1 fp32 out (split-K slabs when splits > 1)
 // tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64; | 16 = two K-tiles in flight (register ring)
 extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* B, void* C,
@@ -504,8 +844,11 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
   p.flags = flags; p.alpha = alpha; p.slope = slope;
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   hipStream_t st = (hipStream_t)stream;
-  const bool conv = kind <= 2;
-  if (conv && (p.log2H < 0 || p.log2W < 0 || p.log2C < 0 || Cch < 8)) return RK_EUNSUPPORTED;
+  const bool conv = kind <= 2 || kind == 6;
+  p.invC = 1.0f / (float)Cch;
+  if (conv && (p.log2H < 0 || p.log2W < 0 || Cch % 8 != 0 || Cch < 8)) return RK_EUNSUPPORTED;
+  // the LDS-DMA operands use shift-only channel arithmetic: other channel counts run register-staged
+  if (conv && p.log2C < 0) tile &= 15 | 16;
   if (epi == 0 && splits != 1) return RK_EBADARG;
   switch (kind) {
     case 0: if (epi != 0) return RK_EBADARG;
@@ -520,6 +863,8 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
                             : launch_modes<OP_DENSE_KIN, OP_DENSE_KOUT, EPI_F32>(tile, p, splits, st);
     case 5: if (epi != 1) return RK_EBADARG;
       return launch_modes<OP_DENSE_KOUT, OP_DENSE_KOUT, EPI_F32>(tile, p, splits, st);
+    case 6: if (epi != 0 || (H & 1) || (W & 1)) return RK_EBADARG;  // H, W = OUTPUT (2x) resolution
+      return launch_modes<OP_CONVUP_KIN, OP_DENSE_KIN, EPI_BF16>(tile & (15 | 16), p, splits, st);
   }
   return RK_EBADARG;
 }

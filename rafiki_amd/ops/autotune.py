@@ -1,0 +1,107 @@
+"""Per-shape kernel-config autotuning for the igemm engine (find-once, replay-forever).
+
+The best (tile shape, staging variant, split-K) differs per layer shape (measured on MI355X with
+scripts/bench_igemm.py: e.g. the LDS-DMA 2-stage ring wins on 16x16/8x8 layers, 64x64 register
+staging on the 4x4x512 layers).  The first time a shape is seen outside hipGraph capture, every
+candidate runs a few times under HIP events and the fastest is cached (in memory and, if
+``RAFIKI_TUNE_CACHE`` points to a file, on disk).  During capture only cached/heuristic configs
+are used, so captured graphs never contain tuning launches.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+
+import torch
+
+_lock = threading.Lock()
+_cache = {}
+_loaded = False
+ENABLED = os.environ.get('RAFIKI_AUTOTUNE', '1') != '0'
+REPS = int(os.environ.get('RAFIKI_AUTOTUNE_REPS', '3'))
+
+
+def _path():
+    return os.environ.get('RAFIKI_TUNE_CACHE', '')
+
+
+def _load():
+    global _loaded
+    if _loaded:
+        return
+    _loaded = True
+    p = _path()
+    if p and os.path.exists(p):
+        try:
+            with open(p) as f:
+                for k, v in json.load(f).items():
+                    _cache[k] = tuple(v)
+        except (OSError, ValueError):
+            pass
+
+
+def _save():
+    p = _path()
+    if not p:
+        return
+    try:
+        tmp = p + '.tmp'
+        with open(tmp, 'w') as f:
+            json.dump({k: list(v) for k, v in _cache.items()}, f)
+        os.replace(tmp, p)
+    except OSError:
+        pass
+
+
+def lookup(key):
+    with _lock:
+        _load()
+        return _cache.get(key)
+
+
+def can_tune():
+    if not ENABLED or not torch.cuda.is_available():
+        return False
+    try:
+        return not torch.cuda.is_current_stream_capturing()
+    except Exception:
+        return False
+
+
+def tune(key, candidates, run):
+    """candidates: list of config tuples; run(cfg) launches the op once.  Returns the best cfg."""
+    hit = lookup(key)
+    if hit is not None:
+        return hit
+    if not can_tune():
+        return candidates[0]
+    best, best_t = candidates[0], float('inf')
+    for cfg in candidates:
+        try:
+            run(cfg)  # warm (also compiles nothing: all variants are prebuilt)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(REPS):
+                run(cfg)
+            e.record()
+            e.synchronize()
+            t = s.elapsed_time(e)
+        except Exception:
+            continue
+        if t < best_t:
+            best, best_t = cfg, t
+    with _lock:
+        _cache[key] = tuple(best)
+        _save()
+    return best
+
+
+def clear():
+    with _lock:
+        _cache.clear()
+
+
+def snapshot():
+    with _lock:
+        return dict(_cache)

@@ -12,6 +12,7 @@ caching allocator, so whole training steps can be captured into a hipGraph.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -23,6 +24,9 @@ FLAG_RELU, FLAG_BIAS, FLAG_STATS, FLAG_GATE, FLAG_ACCUM, FLAG_LRELU = 1, 2, 4, 8
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
 NUM_CU = 256
+# Kernel variant bits OR'ed into the tile code (see rk_igemm): 0 register-staged, 16 register ring,
+# 32 LDS-DMA 3-stage ring, 64 LDS-DMA 2-stage.
+VARIANT = int(os.environ.get('RAFIKI_IGEMM_VARIANT', '0'))
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -67,10 +71,53 @@ def pick_splits(M: int, N: int, K: int, tile: int, target_blocks: int = 2 * NUM_
     return cdiv(ktiles, per)
 
 
+def _tile_candidates(M, N, fixed_bm=None):
+    """Heuristic pick first (used when tuning is impossible), then every shape x staging variant."""
+    first = pick_tile(M, N)
+    if fixed_bm is not None:  # stats partial-row count depends on BM: keep BM fixed for stats outputs
+        shapes = [t for t in range(4) if TILES[t][0] == fixed_bm]
+    else:
+        shapes = list(range(4))
+    out = [(first,)]
+    for t in shapes:
+        for v in (0, 64, 32):
+            c = (t | v,)
+            if c not in out:
+                out.append(c)
+    return out
+
+
+def _split_candidates(M, N, K):
+    t0 = pick_tile(M, N)
+    first = (t0, pick_splits(M, N, K, t0))
+    out = [first]
+    kt = cdiv(K, 64)
+    for t in range(4):
+        for v in (0, 64):
+            for s in (1, 2, 4, 8, 16, 32, 64):
+                if s > kt or (s == 1 and kt > 64):
+                    continue
+                per = cdiv(kt, s)
+                s_eff = cdiv(kt, per)
+                c = (t | v, s_eff)
+                if c not in out:
+                    out.append(c)
+    return out
+
+
+def _tuned(key, candidates, run):
+    from . import autotune
+    if VARIANT or not autotune.ENABLED:
+        return candidates[0]
+    return autotune.tune(key, candidates, run)
+
+
 def igemm(kind, epi, A, B, out, M, N, K, lda=0, ldb=0, ldc=0, *, bias=None, stats=None, gate=None, H=1, W=1,
           C=8, taps=1, Cb=1, splits=1, slab_stride=0, flags=0, alpha=1.0, slope=0.2, tile=None):
     if tile is None:
         tile = pick_tile(M, N)
+    if VARIANT and tile < 16:
+        tile |= VARIANT
     _lib.call("rk_igemm", kind, epi, tile, _p(A), _p(B), _p(out), _p(bias), _p(stats), _p(gate), M, N, K, lda, ldb,
               ldc, H, W, C, taps, Cb, splits, slab_stride, flags, alpha, slope, _nbytes(A), _nbytes(B), _s())
     return out
@@ -103,8 +150,12 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
         flags |= FLAG_RELU
     elif act == ACT_LRELU:
         flags |= FLAG_LRELU
-    igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
-          taps=taps, flags=flags, slope=slope, tile=tile)
+    def run(cfg):
+        igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
+              taps=taps, flags=flags, slope=slope, tile=cfg[0])
+    cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, bool(want_stats)),
+                 _tile_candidates(M, Cout, fixed_bm=TILES[tile][0] if want_stats else None), run)
+    run(cfg)
     return (out, stats) if want_stats else out
 
 
@@ -115,8 +166,11 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, ga
     if out is None:
         out = torch.empty((Nb, H, W, Cin), device=dy.device, dtype=torch.bfloat16)
     flags = FLAG_GATE if gate is not None else 0
-    igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, H=H, W=W, C=Cout, taps=taps,
-          Cb=Cout, flags=flags)
+
+    def run(cfg):
+        igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, H=H, W=W, C=Cout,
+              taps=taps, Cb=Cout, flags=flags, tile=cfg[0])
+    run(_tuned(('cd', M, Cin, K, H, W, Cout, taps), _tile_candidates(M, Cin), run))
     return out
 
 
@@ -127,16 +181,22 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
     M, N, K = Cout, taps * Cin, Nb * H * W
     if out is None:
         out = torch.empty((Cout, N), device=dy.device, dtype=torch.float32)
-    tile = pick_tile(M, N)
-    s = pick_splits(M, N, K, tile) if splits is None else splits
-    if s == 1:
-        igemm(KIND_CONV_WGRAD, 1, dy, x, out, M, N, K, Cout, 0, N, H=H, W=W, C=Cin, taps=taps, splits=1,
-              flags=FLAG_ACCUM if accumulate else 0, tile=tile)
+    def run(cfg):
+        tile, s = cfg
+        if s == 1:
+            igemm(KIND_CONV_WGRAD, 1, dy, x, out, M, N, K, Cout, 0, N, H=H, W=W, C=Cin, taps=taps, splits=1,
+                  flags=FLAG_ACCUM if accumulate else 0, tile=tile)
+            return
+        slab = torch.empty((s, M, N), device=dy.device, dtype=torch.float32)
+        igemm(KIND_CONV_WGRAD, 1, dy, x, slab, M, N, K, Cout, 0, N, H=H, W=W, C=Cin, taps=taps, splits=s,
+              slab_stride=M * N, tile=tile)
+        reduce_slabs(slab, out, accumulate=accumulate)
+    if splits is not None:
+        t0 = pick_tile(M, N)
+        run((t0, splits))
         return out
-    slab = torch.empty((s, M, N), device=dy.device, dtype=torch.float32)
-    igemm(KIND_CONV_WGRAD, 1, dy, x, slab, M, N, K, Cout, 0, N, H=H, W=W, C=Cin, taps=taps, splits=s,
-          slab_stride=M * N, tile=tile)
-    reduce_slabs(slab, out, accumulate=accumulate)
+    cands = _split_candidates(M, N, K)
+    run(_tuned(('cw', M, N, K, H, W, Cin, taps, bool(accumulate)), cands, run) if not accumulate else cands[0])
     return out
 
 

@@ -16,7 +16,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument('--batch', type=int, default=256)
 ap.add_argument('--reps', type=int, default=20)
 ap.add_argument('--passes', default='fwd,dgrad,wgrad')
+ap.add_argument('--variants', default='0,1,2,3,32,33,34,35,64,65,66,67')
 args = ap.parse_args()
+VARIANTS = [int(v) for v in args.variants.split(',')]
 
 LAYERS = [(8, 64, 32), (64, 64, 32), (64, 128, 16), (128, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4),
           (512, 512, 4)]
@@ -50,7 +52,7 @@ for li, (cin, cout, hw) in enumerate(LAYERS):
     line = []
     if 'fwd' in args.passes:
         res = {}
-        for t in (0, 1, 2, 3, 16, 17, 18, 19):
+        for t in VARIANTS:
             stats = torch.empty((F.stats_rows(M, cout, t), 2, cout), device=dev)
             res[t] = timeit(lambda: F.igemm(F.KIND_CONV_FWD, 0, x, w, y, M, cout, 9 * cin, cin, 9 * cin, cout,
                                             stats=stats, H=hw, W=hw, C=cin, taps=9, flags=F.FLAG_STATS, tile=t))
@@ -61,7 +63,7 @@ for li, (cin, cout, hw) in enumerate(LAYERS):
               '  heur=t{}'.format(F.pick_tile(M, cout)))
     if 'dgrad' in args.passes and li > 0:
         res = {}
-        for t in (0, 1, 2, 3, 16, 17, 18, 19):
+        for t in VARIANTS:
             res[t] = timeit(lambda: F.igemm(F.KIND_CONV_DGRAD, 0, dy, w, dx, M, cin, 9 * cout, cout, 9 * cin, cin,
                                             H=hw, W=hw, C=cout, taps=9, Cb=cout, tile=t))
         b = min(res, key=res.get)
@@ -72,7 +74,7 @@ for li, (cin, cout, hw) in enumerate(LAYERS):
     if 'wgrad' in args.passes:
         res = {}
         Mw, Nw, Kw = cout, 9 * cin, M
-        for t in (0, 1, 2, 3, 16, 17, 18, 19):
+        for t in VARIANTS:
             for s in (2, 4, 8, 16, 32):
                 slab = torch.empty((s, Mw, Nw), device=dev)
 
