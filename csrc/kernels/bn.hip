@@ -337,6 +337,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
   }
 }
 
+// odd H or W with 2x2 pooling (VGG16 at 48x48 pools 3x3 -> 1x1): the last row / column belongs to
+// no window (floor mode, as Keras/torch), so its upstream gradient is zero but BN still couples it:
+// dy = k2*y + k3 there.
+__global__ __launch_bounds__(256) void bn_bwd_edge_kernel(const bf16* __restrict__ y, const float* __restrict__ coef,
+                                                          bf16* __restrict__ dy, int N, int H, int W, int C) {
+  const int CC = C >> 3;
+  const int He = H & ~1, We = W & ~1;
+  const long long total = (long long)N * H * W * CC;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int cc = (int)(idx % CC);
+    const long long pix = idx / CC;
+    const int w = (int)(pix % W), h = (int)((pix / W) % H);
+    if (h < He && w < We) continue;
+    float f[8], o[8];
+    unpack8(*(const uint4*)(y + pix * C + cc * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = coef[C + cc * 8 + e] * f[e] + coef[2 * C + cc * 8 + e];
+    *(uint4*)(dy + pix * C + cc * 8) = pack8(o);
+  }
+}
+
 int grid_for(long long work, int per_block, int cap) {
   long long g = (work + per_block - 1) / per_block;
   if (g > cap) g = cap;
@@ -389,7 +411,6 @@ extern "C" int rk_bn_eval_coeffs(int C, const float* gamma, const float* beta, c
 extern "C" int rk_bn_act_fwd(const void* y, const float* scale, const float* shift, void* out, int N, int H, int W,
                              int C, int pool, int act, float slope, void* stream) {
   if (C % 8) return RK_EUNSUPPORTED;
-  if (pool && ((H & 1) || (W & 1))) return RK_EUNSUPPORTED;
   const long long work = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 8);
   hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)y, scale, shift, (bf16*)out, N, H, W, C, pool, act, slope);
@@ -424,5 +445,10 @@ extern "C" int rk_bn_bwd_apply(const void* dout, const void* y, const float* sca
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)dout, (const bf16*)y, scale, shift, coef, (bf16*)dy, N, H, W, C, pool, act, slope);
   RK_LAUNCH_CHECK();
+  if (pool && ((H & 1) || (W & 1))) {
+    hipLaunchKernelGGL(bn_bwd_edge_kernel, dim3(grid_for((long long)N * H * W * (C / 8), 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16*)y, coef, (bf16*)dy, N, H, W, C);
+    RK_LAUNCH_CHECK();
+  }
   return RK_OK;
 }

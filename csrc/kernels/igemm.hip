@@ -59,7 +59,7 @@ struct IgemmParams {
   float alpha;          // output scale
   float slope;          // leaky-relu slope
   unsigned long long bytesA, bytesB;  // operand extents for the buffer descriptors (< 2 GiB)
-  float invC;                         // 1/C for non-power-of-two channel counts
+  float invC, invH, invW;             // reciprocals for non-power-of-two channel / spatial extents
 };
 
 // channel arithmetic of the gathered activation: shifts when C is a power of two (every VGG /
@@ -70,6 +70,18 @@ RK_DEV int ch_div(int k, const IgemmParams& p) {
 }
 RK_DEV int ch_mod(int k, int q, const IgemmParams& p) { return p.log2C >= 0 ? (k & (p.C - 1)) : k - q * p.C; }
 RK_DEV unsigned ch_mul(unsigned v, const IgemmParams& p) { return p.log2C >= 0 ? (v << p.log2C) : v * (unsigned)p.C; }
+// pixel index -> (n, h, w).  Power-of-two maps use shifts; others (VGG16 at 48x48: 48/24/12/6/3) an
+// fp32 reciprocal, exact for pixel indices < 2^22 (checked on the host).
+RK_DEV void pix_nhw(int k, const IgemmParams& p, int& n, int& h, int& w) {
+  if (p.log2H >= 0 && p.log2W >= 0) {
+    w = k & (p.W - 1); h = (k >> p.log2W) & (p.H - 1); n = k >> (p.log2W + p.log2H);
+  } else {
+    const int q = (int)(((float)k + 0.5f) * p.invW);
+    w = k - q * p.W;
+    n = (int)(((float)q + 0.5f) * p.invH);
+    h = q - n * p.H;
+  }
+}
 
 // ---- LDS images --------------------------------------------------------------------------------
 // K-inner [T][BK] bf16, 128-byte rows, 16-B chunk c of row i lives at chunk (c ^ ((i>>1)&7)):
@@ -144,10 +156,10 @@ struct Operand {
           rowoff[i] = (unsigned)gi * (unsigned)ld * 2u;
           tapmask[i] = ok ? 1u : 0u;
         } else {
-          const int h = (gi >> p.log2W) & (p.H - 1), w = gi & (p.W - 1);
+          int n, h, w;
+          pix_nhw(gi, p, n, h, w);
           if constexpr (MODE == OP_CONVUP_KIN) {
             // output pixel (n, h, w) reads input pixel (n, (h+dy)>>1, (w+dx)>>1) of the H/2 x W/2 map
-            const int n = gi >> (p.log2H + p.log2W);
             const unsigned ip = ((unsigned)n * (unsigned)(p.H >> 1) + (unsigned)(h >> 1)) * (unsigned)(p.W >> 1) +
                                 (unsigned)(w >> 1);
             rowoff[i] = ch_mul(ip, p) * 2u;
@@ -240,7 +252,8 @@ struct Operand {
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const int k = kt * BK + krow0 + KROWS_PER_PASS * i;  // pixel index
-        const int h = (k >> p.log2W) & (p.H - 1), w = k & (p.W - 1);
+        int n, h, w;
+        pix_nhw(k, p, n, h, w);
         const bool ok = colok && k < K && (unsigned)(h + dh) < (unsigned)p.H && (unsigned)(w + dw) < (unsigned)p.W;
         r[i] = bload(rsrc, ok ? ch_mul((unsigned)(k + dh * p.W + dw), p) * 2u + coloff : OOB);
       }
@@ -845,10 +858,12 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   hipStream_t st = (hipStream_t)stream;
   const bool conv = kind <= 2 || kind == 6;
-  p.invC = 1.0f / (float)Cch;
-  if (conv && (p.log2H < 0 || p.log2W < 0 || Cch % 8 != 0 || Cch < 8)) return RK_EUNSUPPORTED;
-  // the LDS-DMA operands use shift-only channel arithmetic: other channel counts run register-staged
-  if (conv && p.log2C < 0) tile &= 15 | 16;
+  p.invC = 1.0f / (float)Cch; p.invH = 1.0f / (float)H; p.invW = 1.0f / (float)W;
+  if (conv && (Cch % 8 != 0 || Cch < 8 || H <= 0 || W <= 0)) return RK_EUNSUPPORTED;
+  if (conv && (p.log2H < 0 || p.log2W < 0) && (long long)(kind == 2 ? K : M) + (long long)W * (H + 2) >= (1ll << 22))
+    return RK_EUNSUPPORTED;  // reciprocal pixel decode is exact below 2^22
+  // the LDS-DMA operands use shift-only index arithmetic: other extents run register-staged
+  if (conv && (p.log2C < 0 || p.log2H < 0 || p.log2W < 0)) tile &= 15 | 16;
   if (epi == 0 && splits != 1) return RK_EBADARG;
   switch (kind) {
     case 0: if (epi != 0) return RK_EBADARG;

@@ -99,8 +99,8 @@ class ConvNetEngine:
         self.input_bn = bool(input_bn)
         if self.input_bn and not self.flat_input:
             raise ValueError('input_bn is for fully-connected nets (no conv blocks)')
-        if not self.flat_input and not _is_pow2(image_size):
-            raise ValueError('image_size must be a power of two (NHWC implicit-GEMM gather)')
+        # any image size: power-of-two maps use the shift-decoded (and LDS-DMA) gather, others the
+        # reciprocal-decoded register-staged gather (VGG16 at 48x48: 48/24/12/6/3)
         flat = FlatParams(self.device, seed)
         self.blocks = []  # (name, cin, cout, pool, H_in)
         cin, hw, i = self.cin_p, image_size, 0

@@ -32,6 +32,7 @@ class ParamSpec:
     init: Callable[[torch.Tensor, torch.Generator], None]
     decay: bool = True
     offset: int = 0
+    lr_mult: float = 1.0  # per-parameter LR multiplier (PG-GAN equalized learning rate)
 
     @property
     def numel(self):
@@ -77,8 +78,8 @@ class FlatParams:
         self.total = 0
         self.decay_end = 0
 
-    def add(self, name, shape, init, decay=True):
-        spec = ParamSpec(name, tuple(int(s) for s in shape), init, decay)
+    def add(self, name, shape, init, decay=True, lr_mult=1.0):
+        spec = ParamSpec(name, tuple(int(s) for s in shape), init, decay, lr_mult=float(lr_mult))
         self.specs.append(spec)
         self._by_name[name] = spec
         return spec
@@ -122,6 +123,23 @@ class FlatParams:
 
     def names(self):
         return [s.name for s in self.specs]
+
+    def segments(self, weight_decay: float = 0.0):
+        """Contiguous arena ranges [(a, b, wd, lr_mult)] of equal decay and LR multiplier."""
+        segs = []
+        for s in sorted(self.specs, key=lambda s: s.offset):
+            wd = weight_decay if s.decay else 0.0
+            a, b = s.offset, s.offset + _align(s.numel)
+            if segs and segs[-1][2] == wd and segs[-1][3] == s.lr_mult and segs[-1][1] == a:
+                segs[-1] = (segs[-1][0], b, wd, s.lr_mult)
+            else:
+                segs.append((a, b, wd, s.lr_mult))
+        if segs:
+            segs[-1] = (segs[-1][0], self.total, segs[-1][2], segs[-1][3])
+        return segs
+
+    def param_ranges(self):
+        return [(s.offset, s.numel) for s in self.specs]
 
     def num_params(self):
         return sum(s.numel for s in self.specs)
@@ -195,27 +213,31 @@ class FlatAdam:
 
     def step(self):
         f = self.flat
+        # Equalized LR (pg_gans.py:1006-1013) is applied by re-parameterisation: the arena holds the
+        # EFFECTIVE weights c*w, stepped with lr*c and eps*c — algebraically identical to Adam on w.
+        segs = f.segments(self.wd)
         if f.device.type == 'cuda':
             F.add_int_(self.t, 1)
-            for a, b, wd in [(0, f.decay_end, self.wd), (f.decay_end, f.total, 0.0)]:
+            for a, b, wd, mult in segs:
                 if b > a:
-                    F.adam_step(f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b], wb=f.bf16[a:b], lr=self.lr,
-                                beta1=self.b1, beta2=self.b2, eps=self.eps, weight_decay=wd,
-                                decoupled=self.decoupled, step_tensor=self.t, skip_flag=self.skip_flag)
+                    F.adam_step(f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b], wb=f.bf16[a:b],
+                                lr=self.lr * mult, beta1=self.b1, beta2=self.b2, eps=self.eps * mult,
+                                weight_decay=wd, decoupled=self.decoupled, step_tensor=self.t,
+                                skip_flag=self.skip_flag)
             return
         if self.skip_flag is not None and int(self.skip_flag.item()) != 0:
             return
         self.t += 1
         t = int(self.t.item())
-        wd = torch.zeros_like(f.master)
-        wd[:f.decay_end] = self.wd
-        g = f.grad if self.decoupled else f.grad + wd * f.master
-        self.m.mul_(self.b1).add_((1 - self.b1) * g)
-        self.v.mul_(self.b2).add_((1 - self.b2) * g * g)
         c1 = 1.0 / (1.0 - self.b1 ** t) if self.b1 > 0 else 1.0
         c2 = 1.0 / (1.0 - self.b2 ** t)
-        upd = (self.m * c1) / ((self.v * c2).sqrt() + self.eps)
-        if self.decoupled:
-            upd = upd + wd * f.master
-        f.master.sub_(self.lr * upd)
+        for a, b, wd, mult in segs:
+            w, gr, m, v = f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b]
+            g = gr if self.decoupled else gr + wd * w
+            m.mul_(self.b1).add_((1 - self.b1) * g)
+            v.mul_(self.b2).add_((1 - self.b2) * g * g)
+            upd = (m * c1) / ((v * c2).sqrt() + self.eps * mult)
+            if self.decoupled:
+                upd = upd + wd * w
+            w.sub_(self.lr * mult * upd)
         f.sync_bf16()

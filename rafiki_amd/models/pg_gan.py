@@ -1,0 +1,729 @@
+"""PgGan — Progressive Growing of GANs (WGAN-GP), the IMAGE_GENERATION example model.
+
+Reference: examples/models/image_generation/pg_gans.py (PG_GANs :34-377, G_paper/D_paper :803-989,
+Optimizer :1093-1225, TrainingSchedule :1227-1274, losses :1276-1328).  Same knobs, schedule,
+losses, Gs moving average, optimizer-state reset per level of detail, TFRecord dataset format and
+predict contract ([grid_w, grid_h, n_images] -> JPEG file paths).  Re-designed for MI355X:
+
+* NHWC bf16 activations, fp32 master weights in a flat arena (``engine.flat``); every conv / dense
+  runs on the gfx950 implicit-GEMM MFMA kernels through twice-differentiable autograd Functions
+  (``ops.autograd``) — the gradient penalty's double backward goes through the same kernels;
+* the fused upscale2d+conv3x3 (``Conv0_up``) gathers from the half-resolution input inside the
+  conv kernel (no materialised 2x tensor); the 513-channel minibatch-stddev conv runs on the
+  non-power-of-two channel path (padded to 520);
+* equalized learning rate by re-parameterisation (arena holds c*w, Adam steps with lr*c, eps*c);
+* data parallel (``DATA_PARALLEL = True``): when the worker group has N ranks the trial's minibatch
+  is split across them (pg_gans.py:290-293) and gradients are averaged by bucketed RCCL
+  all-reduces over the flat gradient arena, overlapped with backward
+  (``parallel.grad_bucket``; replaces the per-variable NCCL all-sum at pg_gans.py:1164-1171);
+* the non-finite-gradient guard (pg_gans.py:1180-1191) is a device flag read by the Adam kernel,
+  so no host sync per step;
+* all work at the native resolution of the current level of detail: the reference upsamples G's
+  output to full resolution and D box-filters it back (pg_gans.py:364-369, :1030), an identity
+  for integer LOD that we skip.
+
+evaluate(): the reference downloads the Inception-v3 graph to compute an Inception Score; with no
+network we compute the same statistic (10-split exp(E KL(p(y|x) || p(y))), pg_gans.py:147-164) with
+a classifier trained locally on the evaluation split (its labels if present, otherwise k-means
+pseudo-classes).  The number is therefore NOT comparable to a published Inception Score.
+"""
+from __future__ import annotations
+
+import math
+import os
+import pickle
+import tempfile
+import uuid
+
+import numpy as np
+import torch
+
+from rafiki_amd.constants import TaskType  # noqa: F401
+from rafiki_amd.engine.flat import FlatAdam, FlatParams, init_const, init_normal
+from rafiki_amd.model import BaseModel, CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, logger
+from rafiki_amd.ops import autograd as A
+from rafiki_amd.parallel.context import current as trial_context
+
+
+def _pad8(n):
+    return (int(n) + 7) // 8 * 8
+
+
+# ============================================================================== networks
+class PgNetworks:
+    """G, D (trainable, flat arenas) and Gs (EMA of G) for one resolution/channel configuration."""
+
+    def __init__(self, num_channels=1, resolution=32, label_size=0, fmap_base=8192, fmap_decay=1.0, fmap_max=512,
+                 latent_size=None, mbstd_group_size=4, device='cpu', seed=0):
+        self.num_channels, self.resolution, self.label_size = int(num_channels), int(resolution), int(label_size)
+        self.L = int(np.log2(resolution))
+        assert resolution == 2 ** self.L and resolution >= 4, resolution
+        self.fmap_base, self.fmap_decay, self.fmap_max = fmap_base, fmap_decay, fmap_max
+        self.latent_size = int(latent_size or self.nf(0))
+        self.mbstd_group_size = int(mbstd_group_size)
+        self.device = torch.device(device)
+        self.cpad = _pad8(self.num_channels)
+        self.combo = self.latent_size + self.label_size
+        self.combo_p = _pad8(self.combo)
+        self.dout_p = _pad8(1 + self.label_size)
+        self.G = FlatParams(self.device, seed)
+        self.D = FlatParams(self.device, seed + 1)
+        self._define_G()
+        self._define_D()
+        self.G.build()
+        self.D.build()
+        self.Gs_master = self.G.master.clone()
+        self.Gs_bf16 = self.Gs_master.to(torch.bfloat16)
+        self.g_params = self._leaves(self.G)
+        self.d_params = self._leaves(self.D)
+
+    def nf(self, stage):
+        return min(int(self.fmap_base / (2.0 ** (stage * self.fmap_decay))), self.fmap_max)
+
+    # -- parameter definition (equalized LR: effective weight ~ N(0, std^2), lr multiplier = std)
+    @staticmethod
+    def _w(flat, name, shape, fan_in, gain=math.sqrt(2.0), zero_cols=None, zero_rows=None, bias_shape=None):
+        std = gain / math.sqrt(fan_in)
+
+        def init(t, g):
+            t.normal_(0.0, std, generator=g)
+            if zero_rows is not None:
+                t[zero_rows] = 0.0
+            if zero_cols is not None:
+                t[..., zero_cols] = 0.0
+        flat.add(name + '/weight', shape, init, decay=True, lr_mult=std)
+        flat.add(name + '/bias', bias_shape or (shape[0],), init_const(0.0), decay=False)
+
+    def _define_G(self):
+        G, nc = self.G, self.num_channels
+        n1 = self.nf(1)
+        # 4x4 dense: [16*nf(1), combo_p] (rows laid out (h, w, c) = NHWC), bias per channel
+        self._w(G, '4x4/Dense', (16 * n1, self.combo_p), self.combo, gain=math.sqrt(2) / 4,
+                zero_cols=slice(self.combo, None) if self.combo_p > self.combo else None,
+                bias_shape=(n1,))  # per-channel bias, applied after the NHWC reshape
+        self._w(G, '4x4/Conv', (n1, 9 * n1), 9 * n1)
+        for res in range(3, self.L + 1):
+            cin, cout = self.nf(res - 2), self.nf(res - 1)
+            self._w(G, '%dx%d/Conv0_up' % (2 ** res, 2 ** res), (cout, 9 * cin), 9 * cin)
+            self._w(G, '%dx%d/Conv1' % (2 ** res, 2 ** res), (cout, 9 * cout), 9 * cout)
+        for res in range(2, self.L + 1):
+            c = self.nf(res - 1)
+            self._w(G, 'ToRGB_lod%d' % (self.L - res), (self.cpad, c), c, gain=1.0,
+                    zero_rows=slice(nc, None) if self.cpad > nc else None)
+
+    def _define_D(self):
+        D, nc = self.D, self.num_channels
+        for res in range(2, self.L + 1):
+            c = self.nf(res - 1)
+            self._w(D, 'FromRGB_lod%d' % (self.L - res), (c, self.cpad), nc,
+                    zero_cols=slice(nc, None) if self.cpad > nc else None)
+        for res in range(self.L, 2, -1):
+            c0, c1 = self.nf(res - 1), self.nf(res - 2)
+            self._w(D, '%dx%d/Conv0' % (2 ** res, 2 ** res), (c0, 9 * c0), 9 * c0)
+            self._w(D, '%dx%d/Conv1_down' % (2 ** res, 2 ** res), (c1, 9 * c0), 9 * c0)
+        n1, n0 = self.nf(1), self.nf(0)
+        cm = n1 + 1 if self.mbstd_group_size > 1 else n1
+        cm_p = _pad8(cm)
+        self.mbstd_cp = cm_p
+        # [Cout][tap][Cin_p] with the padded input channels zeroed
+        D.add('4x4/Conv/weight', (n1, 9, cm_p), _zero_tail_init(math.sqrt(2) / math.sqrt(9 * cm), cm),
+              decay=True, lr_mult=math.sqrt(2) / math.sqrt(9 * cm))
+        D.add('4x4/Conv/bias', (n1,), init_const(0.0), decay=False)
+        self._w(D, '4x4/Dense0', (n0, 16 * n1), 16 * n1)
+        self._w(D, '4x4/Dense1', (self.dout_p, n0), n0, gain=1.0,
+                zero_rows=slice(1 + self.label_size, None) if self.dout_p > 1 + self.label_size else None)
+
+    @staticmethod
+    def _leaves(flat):
+        out = {}
+        for s in flat.specs:
+            p = torch.nn.Parameter(flat.w(s.name))
+            p.grad = flat.g(s.name)
+            out[s.name] = p
+        return out
+
+    # -- parameter sources
+    def src_G(self):
+        return _Src(self.g_params, lambda n: self.G.wb(n))
+
+    def src_Gs(self):
+        return _Src({s.name: _view(self.Gs_master, s) for s in self.G.specs},
+                    lambda n: _view(self.Gs_bf16, self.G._by_name[n]))
+
+    def src_D(self):
+        return _Src(self.d_params, lambda n: self.D.wb(n))
+
+    def set_requires_grad(self, params, flag):
+        for p in params.values():
+            p.requires_grad_(flag)
+
+    # -- forward passes ------------------------------------------------------------------
+    def _conv(self, P, name, x, taps=9):
+        w = P.w(name + '/weight')
+        return A.conv2d(x, w.reshape(w.shape[0], -1), P.w(name + '/bias'), taps=taps,
+                        wb=_maybe2d(P.wb(name + '/weight'), w))
+
+    def _upconv(self, P, name, x):
+        w = P.w(name + '/weight')
+        return A.upscale_conv2d(x, w, P.w(name + '/bias'), wb=_maybe2d(P.wb(name + '/weight'), w))
+
+    def _dense(self, P, name, x, bias=True):
+        w = P.w(name + '/weight')
+        return A.dense(x, w, P.w(name + '/bias') if bias else None, wb=P.wb(name + '/weight'))
+
+    def generator(self, P, latents, labels, lod):
+        """latents [N, latent] fp32, labels [N, label_size] -> images NHWC [N, r, r, cpad] (bf16 on GPU)
+        at r = 2 ** (L - floor(lod)), in [-1, 1] drange (pg_gans.py:803-880, 'recursive' structure)."""
+        dt = torch.bfloat16 if self.device.type == 'cuda' else torch.float32
+        lrelu, PN = A.leaky_relu, A.pixel_norm
+        N = latents.shape[0]
+        combo = torch.cat([latents, labels], 1) if self.label_size else latents
+        combo = PN(combo.float())
+        if self.combo_p > self.combo:
+            combo = torch.cat([combo, combo.new_zeros(N, self.combo_p - self.combo)], 1)
+        x = self._dense(P, '4x4/Dense', combo.to(dt), bias=False).reshape(N, 4, 4, self.nf(1))
+        x = PN(lrelu(x + P.w('4x4/Dense/bias').to(dt)))
+        x = PN(lrelu(self._conv(P, '4x4/Conv', x)))
+        cur = self.L - int(math.floor(lod))
+        frac = lod - math.floor(lod)
+        prev = None
+        for res in range(3, cur + 1):
+            prev = x
+            tag = '%dx%d' % (2 ** res, 2 ** res)
+            x = PN(lrelu(self._upconv(P, tag + '/Conv0_up', x)))
+            x = PN(lrelu(self._conv(P, tag + '/Conv1', x)))
+        img = self._conv(P, 'ToRGB_lod%d' % (self.L - cur), x, taps=1)
+        if frac > 0 and cur > 2:
+            lo = A.upscale2d(self._conv(P, 'ToRGB_lod%d' % (self.L - cur + 1), prev, taps=1))
+            img = img + (lo - img) * frac
+        return img
+
+    def discriminator(self, P, img, lod):
+        """img NHWC [N, r, r, cpad] at the current LOD resolution -> (scores [N] fp32, label logits)."""
+        lrelu = A.leaky_relu
+        cur = self.L - int(math.floor(lod))
+        frac = lod - math.floor(lod)
+        x = lrelu(self._conv(P, 'FromRGB_lod%d' % (self.L - cur), img, taps=1))
+        for res in range(cur, 2, -1):
+            tag = '%dx%d' % (2 ** res, 2 ** res)
+            x = lrelu(self._conv(P, tag + '/Conv0', x))
+            x = lrelu(A.downscale2d(self._conv(P, tag + '/Conv1_down', x)))
+            if res == cur and frac > 0:
+                y = lrelu(self._conv(P, 'FromRGB_lod%d' % (self.L - res + 1), A.downscale2d(img), taps=1))
+                x = x + (y - x) * frac
+        if self.mbstd_group_size > 1:
+            x = A.minibatch_stddev(x, self.mbstd_group_size, pad_to=8)
+        x = lrelu(self._conv(P, '4x4/Conv', x))
+        N = x.shape[0]
+        x = lrelu(self._dense(P, '4x4/Dense0', x.reshape(N, -1)))
+        out = self._dense(P, '4x4/Dense1', x).float()
+        return out[:, 0], out[:, 1:1 + self.label_size]
+
+    # -- Gs moving average (pg_gans.py:1247 setup_as_moving_average_of, beta = G_smoothing)
+    def update_Gs(self, beta):
+        if self.device.type == 'cuda':
+            from rafiki_amd.ops import functional as F
+            F.lerp_(self.Gs_master, self.G.master, beta, dst_bf16=self.Gs_bf16)
+        else:
+            self.Gs_master.copy_(self.G.master + (self.Gs_master - self.G.master) * beta)
+            self.Gs_bf16.copy_(self.Gs_master)
+
+    def state(self):
+        return {'G': self.G.state_dict(),
+                'D': self.D.state_dict(),
+                'Gs': {s.name: _view(self.Gs_master, s).detach().cpu().numpy().copy() for s in self.G.specs}}
+
+    def load_state(self, st):
+        self.G.load_state_dict(st['G'])
+        self.D.load_state_dict(st['D'])
+        for s in self.G.specs:
+            if s.name in st['Gs']:
+                _view(self.Gs_master, s).copy_(torch.as_tensor(st['Gs'][s.name]).reshape(s.shape))
+        self.Gs_bf16.copy_(self.Gs_master)
+
+
+def _zero_tail_init(std, real_c):
+    def f(t, g):
+        t.normal_(0.0, std, generator=g)
+        t[..., real_c:] = 0.0
+    return f
+
+
+def _view(buf, spec):
+    return buf[spec.offset:spec.offset + spec.numel].view(spec.shape)
+
+
+def _maybe2d(wb, w):
+    return None if wb is None else wb.reshape(w.shape[0], -1)
+
+
+class _Src:
+    def __init__(self, params, wb_fn):
+        self.params, self.wb_fn = params, wb_fn
+
+    def w(self, name):
+        return self.params[name]
+
+    def wb(self, name):
+        return self.wb_fn(name) if self.params[name].device.type == 'cuda' else None
+
+
+# ============================================================================== schedule
+class TrainingSchedule:
+    """pg_gans.py:1227-1274 (minibatch dicts per minibatch_base, LOD phases, per-GPU caps)."""
+
+    MINIBATCH_DICTS = {
+        4: {4: 128, 8: 128, 16: 128, 32: 64, 64: 32, 128: 16, 256: 8, 512: 4},
+        8: {4: 256, 8: 256, 16: 128, 32: 64, 64: 32, 128: 16, 256: 8},
+        16: {4: 512, 8: 256, 16: 128, 32: 64, 64: 32, 128: 16},
+        32: {4: 512, 8: 256, 16: 128, 32: 64, 64: 32},
+    }
+
+    def __init__(self, cur_nimg, resolution_log2, num_gpus=1, lod_initial_resolution=4, lod_training_kimg=600,
+                 lod_transition_kimg=600, minibatch_base=16, max_minibatch_per_gpu=None, G_lrate=0.001,
+                 D_lrate=0.001):
+        if max_minibatch_per_gpu is None:
+            max_minibatch_per_gpu = {256: 16, 512: 8, 1024: 4}
+        mb_dict = self.MINIBATCH_DICTS.get(int(minibatch_base), {})
+        self.kimg = cur_nimg / 1000.0
+        phase_dur = lod_training_kimg + lod_transition_kimg
+        phase_idx = int(np.floor(self.kimg / phase_dur)) if phase_dur > 0 else 0
+        phase_kimg = self.kimg - phase_idx * phase_dur
+        lod = float(resolution_log2)
+        lod -= np.floor(np.log2(lod_initial_resolution))
+        lod -= phase_idx
+        if lod_transition_kimg > 0:
+            lod -= max(phase_kimg - lod_training_kimg, 0.0) / lod_transition_kimg
+        self.lod = max(float(lod), 0.0)
+        self.resolution = 2 ** (resolution_log2 - int(np.floor(self.lod)))
+        mb = mb_dict.get(self.resolution, int(minibatch_base))
+        mb -= mb % num_gpus
+        if self.resolution in max_minibatch_per_gpu:
+            mb = min(mb, max_minibatch_per_gpu[self.resolution] * num_gpus)
+        self.minibatch = int(mb)
+        self.G_lrate, self.D_lrate = float(G_lrate), float(D_lrate)
+
+
+# ============================================================================== dataset
+def load_gan_dataset(dataset_uri):
+    """TFRecord directory (reference format), IMAGE_FILES zip, or synthetic:// URI ->
+    TFRecordImageDataset-like object with .images[lod] uint8 [N, C, r, r] and .labels."""
+    from rafiki_amd.model import tfrecord as T
+    from rafiki_amd.model import dataset_utils
+    uri = str(dataset_uri)
+    path = uri[7:] if uri.startswith('file://') else uri
+    if os.path.isdir(os.path.expanduser(path)):
+        return T.TFRecordImageDataset(os.path.expanduser(path))
+    ds = dataset_utils.load_dataset_of_image_files(uri)
+    imgs, labels = ds.as_arrays()
+    imgs = np.asarray(imgs)
+    if imgs.ndim == 3:
+        imgs = imgs[:, None]
+    else:
+        imgs = imgs.transpose(0, 3, 1, 2)
+    return _ArrayPyramid(imgs, labels)
+
+
+class _ArrayPyramid:
+    def __init__(self, imgs, labels=None):
+        from rafiki_amd.model.tfrecord import downscale_images
+        R = imgs.shape[-1]
+        self.resolution = R
+        self.resolution_log2 = int(np.log2(R))
+        assert R == 2 ** self.resolution_log2 and imgs.shape[-2] == R, imgs.shape
+        self.shape = [imgs.shape[1], R, R]
+        self.images = {0: imgs.astype(np.uint8)}
+        cur = imgs.astype(np.float32)
+        for lod in range(1, self.resolution_log2 - 1):
+            cur = downscale_images(cur)
+            self.images[lod] = np.rint(cur).clip(0, 255).astype(np.uint8)
+        if labels is not None and len(labels):
+            labels = np.asarray(labels).astype(np.int64)
+            oh = np.zeros((len(labels), int(labels.max()) + 1), np.float32)
+            oh[np.arange(len(labels)), labels] = 1.0
+            self.class_labels = labels
+        else:
+            oh = np.zeros((len(imgs), 0), np.float32)
+            self.class_labels = None
+        self.labels = oh
+        self.label_size = 0  # IMAGE_FILES labels are used for evaluation only (unconditional GAN)
+        self.dynamic_range = [0, 255]
+
+    @property
+    def num_images(self):
+        return int(self.images[0].shape[0])
+
+
+# ============================================================================== model
+class PgGan(BaseModel):
+    DATA_PARALLEL = True
+
+    @staticmethod
+    def get_knob_config():
+        return {
+            'D_repeats': IntegerKnob(1, 3),
+            'minibatch_base': CategoricalKnob([4, 8, 16, 32]),
+            'G_lrate': FloatKnob(1e-3, 3e-3, is_exp=False),
+            'D_lrate': FloatKnob(1e-3, 3e-3, is_exp=False),
+            'lod_initial_resolution': FixedKnob(4),
+            'total_kimg': FixedKnob(2),
+            'lod_training_kimg': FixedKnob(600),
+            'lod_transition_kimg': FixedKnob(600),
+        }
+
+    def __init__(self, **knobs):
+        super().__init__(**knobs)
+        self._knobs = dict(knobs)
+        ctx = trial_context()
+        self.ctx = ctx
+        self.device = ctx.device
+        self.world = ctx.world_size
+        self.rank = ctx.rank
+        self.nets = None
+        self.lod = None
+        self._meta = {}
+        self.seed = int(knobs.get('seed', 1000))
+        self.stats = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _k(self, name, default):
+        return self._knobs.get(name, default)
+
+    def _build(self, shape, label_size):
+        self._meta = dict(num_channels=int(shape[0]), resolution=int(shape[1]), label_size=int(label_size),
+                          fmap_base=int(self._k('fmap_base', 8192)), fmap_max=int(self._k('fmap_max', 512)),
+                          mbstd_group_size=int(self._k('mbstd_group_size', 4)))
+        self.nets = PgNetworks(device=self.device, seed=self.seed, **self._meta)
+        if self.world > 1:
+            import torch.distributed as dist
+            for buf in (self.nets.G.master, self.nets.D.master):
+                dist.broadcast(buf, src=0)
+            self.nets.G.sync_bf16()
+            self.nets.D.sync_bf16()
+            self.nets.Gs_master.copy_(self.nets.G.master)
+            self.nets.Gs_bf16.copy_(self.nets.Gs_master)
+
+    def _reals(self, level_u8, idx, frac):
+        """uint8 [N, C, r, r] (device) rows idx -> NHWC [n, r, r, cpad] in [-1, 1] with LOD fade
+        (pg_gans.py:347-369 process_reals: dynamic range, FadeLOD; UpscaleLOD is the identity here)."""
+        x = level_u8.index_select(0, idx)
+        nets = self.nets
+        if self.device.type == 'cuda' and frac <= 0:
+            from rafiki_amd.ops import functional as F
+            return F.pack_nhwc(x.contiguous(), nets.cpad, 2.0 / 255.0, -1.0)
+        x = x.float() * (2.0 / 255.0) - 1.0
+        if frac > 0:
+            N, C, r, _ = x.shape
+            y = x.reshape(N, C, r // 2, 2, r // 2, 2).mean((3, 5), keepdim=True).expand(N, C, r // 2, 2, r // 2, 2)
+            x = x + (y.reshape(N, C, r, r) - x) * frac
+        x = x.permute(0, 2, 3, 1)
+        if nets.cpad > x.shape[-1]:
+            x = torch.cat([x, x.new_zeros(*x.shape[:3], nets.cpad - x.shape[-1])], -1)
+        dt = torch.bfloat16 if self.device.type == 'cuda' else torch.float32
+        return x.to(dt).contiguous()
+
+    def _slice_images(self, img):
+        return img[..., :self.nets.num_channels]
+
+    # ------------------------------------------------------------------ train
+    def train(self, dataset_uri, **overrides):
+        from rafiki_amd.parallel.grad_bucket import FlatGradAllReduce
+        knobs = dict(self._knobs, **overrides)
+        ds = load_gan_dataset(dataset_uri)
+        if self.nets is None:
+            self._build(ds.shape, ds.label_size)
+        nets, dev = self.nets, self.device
+        total_kimg = float(knobs.get('total_kimg', 2))
+        D_repeats = int(knobs.get('D_repeats', 1))
+        minibatch_repeats = int(knobs.get('minibatch_repeats', 4))
+        G_smoothing = float(knobs.get('G_smoothing', 0.99))
+        sched_kw = dict(lod_initial_resolution=int(knobs.get('lod_initial_resolution', 4)),
+                        lod_training_kimg=float(knobs.get('lod_training_kimg', 600)),
+                        lod_transition_kimg=float(knobs.get('lod_transition_kimg', 600)),
+                        minibatch_base=int(knobs.get('minibatch_base', 16)),
+                        G_lrate=float(knobs.get('G_lrate', 1e-3)), D_lrate=float(knobs.get('D_lrate', 1e-3)))
+        G_opt = FlatAdam(nets.G, sched_kw['G_lrate'], betas=(0.0, 0.99), eps=1e-8)
+        D_opt = FlatAdam(nets.D, sched_kw['D_lrate'], betas=(0.0, 0.99), eps=1e-8)
+        for opt in (G_opt, D_opt):
+            opt.skip_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        g_ar = d_ar = None
+        if self.world > 1:
+            g_ar = FlatGradAllReduce(nets.G.grad, nets.G.param_ranges(), list(nets.g_params.values()), self.world)
+            d_ar = FlatGradAllReduce(nets.D.grad, nets.D.param_ranges(), list(nets.d_params.values()), self.world)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(self.seed * 7919 + self.rank)
+        level_cache = {}
+        labels_all = torch.as_tensor(ds.labels, device=dev)
+        cur_nimg, prev_lod, tick = 0, -1.0, 0
+        logger.define_plot('Losses', ['D_loss', 'G_loss'], x_axis='kimg')
+        logger.define_plot('Scores', ['real_score', 'fake_score', 'grad_norm'], x_axis='kimg')
+        while cur_nimg < total_kimg * 1000:
+            sched = TrainingSchedule(cur_nimg, ds.resolution_log2, num_gpus=self.world, **sched_kw)
+            lod_int = int(math.floor(sched.lod))
+            if lod_int not in level_cache:
+                level_cache.clear()
+                level_cache[lod_int] = torch.as_tensor(ds.images[lod_int]).to(dev)
+            level = level_cache[lod_int]
+            if np.floor(sched.lod) != np.floor(prev_lod) or np.ceil(sched.lod) != np.ceil(prev_lod):
+                G_opt.reset_state()
+                D_opt.reset_state()
+            prev_lod = sched.lod
+            G_opt.lr, D_opt.lr = sched.G_lrate, sched.D_lrate
+            mb = sched.minibatch // self.world
+            if mb % min(nets.mbstd_group_size, mb) != 0:
+                mb -= mb % nets.mbstd_group_size
+            acc = torch.zeros(6, dtype=torch.float32, device=dev)
+            nD = nG = 0
+            for _ in range(minibatch_repeats):
+                for _ in range(D_repeats):
+                    acc[:4] += self._d_step(sched.lod, mb, level, labels_all, gen, D_opt, d_ar)
+                    nets.update_Gs(G_smoothing)
+                    cur_nimg += sched.minibatch
+                    nD += 1
+                acc[4] += self._g_step(sched.lod, mb, labels_all, gen, G_opt, g_ar)
+                nG += 1
+            tick += 1
+            a = acc.cpu().numpy()
+            self.lod = sched.lod
+            self.stats = dict(kimg=cur_nimg / 1000.0, lod=sched.lod, minibatch=sched.minibatch,
+                              D_loss=float(a[0] / nD), real_score=float(a[1] / nD), fake_score=float(a[2] / nD),
+                              grad_norm=float(a[3] / nD), G_loss=float(a[4] / nG))
+            logger.log('tick {}'.format(tick), **self.stats)
+        self.lod = prev_lod if prev_lod >= 0 else 0.0
+        if g_ar is not None:
+            g_ar.remove()
+            d_ar.remove()
+
+    def _latents(self, n, gen):
+        return torch.randn((n, self.nets.latent_size), generator=gen, device=self.device)
+
+    def _rand_labels(self, labels_all, n, gen):
+        if self.nets.label_size == 0:
+            return torch.zeros((n, 0), device=self.device)
+        idx = torch.randint(0, labels_all.shape[0], (n,), generator=gen, device=self.device)
+        return labels_all.index_select(0, idx)
+
+    def _finite_guard(self, flat, opt):
+        opt.skip_flag.zero_()
+        if self.device.type == 'cuda':
+            from rafiki_amd.ops import functional as F
+            F.nonfinite_flag(flat.grad, opt.skip_flag)
+        else:
+            opt.skip_flag.fill_(0 if bool(torch.isfinite(flat.grad).all()) else 1)
+
+    def _d_step(self, lod, mb, level, labels_all, gen, opt, ar, wgan_lambda=10.0, wgan_epsilon=0.001,
+                wgan_target=1.0):
+        """_D_wgangp_acgan (pg_gans.py:1291-1328) + D optimizer step."""
+        nets = self.nets
+        PG, PD = nets.src_G(), nets.src_D()
+        nets.set_requires_grad(nets.g_params, False)
+        nets.set_requires_grad(nets.d_params, True)
+        nets.D.grad.zero_()
+        idx = torch.randint(0, level.shape[0], (mb,), generator=gen, device=self.device)
+        reals = self._reals(level, idx, lod - math.floor(lod))
+        labels = labels_all.index_select(0, idx) if nets.label_size else torch.zeros((mb, 0), device=self.device)
+        with torch.no_grad():
+            fakes = nets.generator(PG, self._latents(mb, gen), labels, lod)
+        real_s, real_l = nets.discriminator(PD, reals, lod)
+        fake_s, fake_l = nets.discriminator(PD, fakes, lod)
+        loss = fake_s - real_s
+        alpha = torch.rand((mb, 1, 1, 1), generator=gen, device=self.device)
+        mixed = (reals.float() + (fakes.float() - reals.float()) * alpha).to(reals.dtype).detach().requires_grad_(True)
+        mixed_s, _ = nets.discriminator(PD, mixed, lod)
+        if ar is not None:
+            ar.begin()
+        (grads,) = torch.autograd.grad(mixed_s.sum(), mixed, create_graph=True)
+        norms = grads.float().square().sum((1, 2, 3)).sqrt()
+        loss = loss + (norms - wgan_target).square() * (wgan_lambda / wgan_target ** 2)
+        loss = loss + real_s.square() * wgan_epsilon
+        if nets.label_size:
+            loss = loss + _softmax_xent(real_l, labels) + _softmax_xent(fake_l, labels)
+        loss.mean().backward()
+        if ar is not None:
+            ar.finish()
+        self._finite_guard(nets.D, opt)
+        opt.step()
+        return torch.stack([loss.mean().detach(), real_s.mean().detach(), fake_s.mean().detach(),
+                            norms.mean().detach()])
+
+    def _g_step(self, lod, mb, labels_all, gen, opt, ar):
+        """_G_wgan_acgan (pg_gans.py:1276-1289) + G optimizer step."""
+        nets = self.nets
+        PG, PD = nets.src_G(), nets.src_D()
+        nets.set_requires_grad(nets.d_params, False)
+        nets.set_requires_grad(nets.g_params, True)
+        nets.G.grad.zero_()
+        labels = self._rand_labels(labels_all, mb, gen)
+        fakes = nets.generator(PG, self._latents(mb, gen), labels, lod)
+        fake_s, fake_l = nets.discriminator(PD, fakes, lod)
+        loss = -fake_s
+        if nets.label_size:
+            loss = loss + _softmax_xent(fake_l, labels)
+        if ar is not None:
+            ar.begin()
+        loss.mean().backward()
+        if ar is not None:
+            ar.finish()
+        self._finite_guard(nets.G, opt)
+        opt.step()
+        nets.set_requires_grad(nets.d_params, True)
+        return loss.mean().detach()
+
+    # ------------------------------------------------------------------ generation
+    @torch.no_grad()
+    def generate(self, n, seed=1000, batch=256, use_Gs=True):
+        """n images uint8 NHWC [n, R, R, C] at full resolution (pg_gans.py:124-136 / Network.run:
+        out_mul=127.5, out_add=127.5, nearest upscale of lower-LOD output)."""
+        nets = self.nets
+        P = nets.src_Gs() if use_Gs else nets.src_G()
+        lod = float(self.lod or 0.0)
+        g = torch.Generator(device=self.device)
+        g.manual_seed(int(seed))
+        outs = []
+        for b in range(0, n, batch):
+            m = min(batch, n - b)
+            lat = torch.randn((m, nets.latent_size), generator=g, device=self.device)
+            lab = torch.zeros((m, nets.label_size), device=self.device)
+            if nets.label_size:
+                lab[torch.arange(m), torch.randint(0, nets.label_size, (m,), generator=g, device=self.device)] = 1.0
+            img = self._slice_images(nets.generator(P, lat, lab, lod)).float()
+            factor = nets.resolution // img.shape[1]
+            if factor > 1:
+                img = A.upscale2d(img, factor)
+            outs.append((img * 127.5 + 127.5).round().clamp(0, 255).to(torch.uint8).cpu())
+        return torch.cat(outs).numpy()
+
+    # ------------------------------------------------------------------ evaluate
+    def evaluate(self, dataset_uri):
+        n = int(self._knobs.get('eval_images', 10000))
+        ds = load_gan_dataset(dataset_uri)
+        real = ds.images[0]  # [N, C, R, R]
+        labels = getattr(ds, 'class_labels', None)
+        if labels is None and ds.labels.shape[1] > 0:
+            labels = ds.labels.argmax(1)
+        if labels is None:
+            labels = _kmeans_labels(real, k=10, seed=0)
+        clf = _train_eval_classifier(real, labels, self.device,
+                                     epochs=int(self._knobs.get('eval_classifier_epochs', 3)))
+        fake = self.generate(n, seed=int(self._knobs.get('eval_seed', 1)))
+        probs = _classify(clf, fake)
+        return float(_inception_score(probs, splits=10))
+
+    # ------------------------------------------------------------------ predict
+    def predict(self, queries):
+        """queries = [grid_w, grid_h, n_images] (pg_gans.py:166-214) -> list of JPEG paths; a list of
+        such triples -> a list of path lists."""
+        if len(queries) and isinstance(queries[0], (list, tuple)):
+            return [self._predict_one(q) for q in queries]
+        return self._predict_one(queries)
+
+    def _predict_one(self, q):
+        from PIL import Image
+        gw, gh, num = int(q[0]), int(q[1]), int(q[2])
+        out_dir = os.environ.get('RAFIKI_OUTPUT_DIR') or os.path.join(tempfile.gettempdir(), 'rafiki_pg_gan')
+        out_dir = os.path.join(out_dir, uuid.uuid4().hex[:12])
+        os.makedirs(out_dir, exist_ok=True)
+        rs = np.random.RandomState(1000)
+        paths = []
+        for i in range(num):
+            cnt = gw * gh
+            imgs = self.generate(cnt, seed=int(rs.randint(1 << 30)))  # [cnt, R, R, C]
+            R, C = imgs.shape[1], imgs.shape[3]
+            grid_w = max(int(np.ceil(np.sqrt(cnt))), 1)
+            grid_h = max((cnt - 1) // grid_w + 1, 1)
+            grid = np.zeros((grid_h * R, grid_w * R, C), np.uint8)
+            for j in range(cnt):
+                x, y = (j % grid_w) * R, (j // grid_w) * R
+                grid[y:y + R, x:x + R] = imgs[j]
+            im = Image.fromarray(grid[..., 0], 'L') if C == 1 else Image.fromarray(grid, 'RGB')
+            p = os.path.abspath(os.path.join(out_dir, 'output%d.jpeg' % i))
+            im.save(p, 'JPEG')
+            paths.append(p)
+        return paths
+
+    # ------------------------------------------------------------------ params
+    def dump_parameters(self):
+        st = self.nets.state()
+        return {'G': pickle.dumps(st['G'], protocol=pickle.HIGHEST_PROTOCOL),
+                'D': pickle.dumps(st['D'], protocol=pickle.HIGHEST_PROTOCOL),
+                'Gs': pickle.dumps(st['Gs'], protocol=pickle.HIGHEST_PROTOCOL),
+                'meta': dict(self._meta, lod=float(self.lod or 0.0))}
+
+    def load_parameters(self, params):
+        meta = dict(params['meta'])
+        self.lod = float(meta.pop('lod', 0.0))
+        self._meta = meta
+        self.nets = PgNetworks(device=self.device, seed=self.seed, **meta)
+        self.nets.load_state({k: pickle.loads(params[k]) for k in ('G', 'D', 'Gs')})
+
+    def destroy(self):
+        self.nets = None
+
+
+# ============================================================================== eval helpers
+def _softmax_xent(logits, onehot):
+    return -(torch.log_softmax(logits.float(), 1) * onehot).sum(1)
+
+
+def _inception_score(probs, splits=10, eps=1e-12):
+    probs = np.asarray(probs, dtype=np.float64)
+    scores = []
+    n = probs.shape[0]
+    for i in range(splits):
+        part = probs[i * n // splits:(i + 1) * n // splits]
+        if len(part) == 0:
+            continue
+        py = part.mean(0, keepdims=True)
+        kl = (part * (np.log(part + eps) - np.log(py + eps))).sum(1).mean()
+        scores.append(np.exp(kl))
+    return float(np.mean(scores))
+
+
+def _kmeans_labels(real, k=10, seed=0, fit_max=20000):
+    """Pseudo-classes for unlabeled evaluation sets: k-means on 8x8 box-filtered images."""
+    from sklearn.cluster import KMeans
+    x = real.astype(np.float32)
+    N, C, R, _ = x.shape
+    f = max(1, R // 8)
+    x = x.reshape(N, C, R // f, f, R // f, f).mean((3, 5)).reshape(N, -1)
+    km = KMeans(n_clusters=min(k, max(2, N // 4)), n_init=3, random_state=seed).fit(x[:fit_max])
+    return km.predict(x)
+
+
+def _train_eval_classifier(real, labels, device, epochs=3):
+    from rafiki_amd.engine.convnet import ConvNetEngine
+    N, C, R, _ = real.shape
+    ncls = int(np.max(labels)) + 1
+    eng = ConvNetEngine(num_classes=max(ncls, 2), in_channels=C, image_size=R, cfg=(32, 'M', 64, 'M', 128, 'M'),
+                        fc_dims=(128,), device=device, seed=0, optimizer='adam', lr=2e-3, weight_decay=0.0)
+    imgs = real.transpose(0, 2, 3, 1)
+    x_all = eng.prepare_inputs(imgs)
+    y_all = torch.as_tensor(np.asarray(labels), dtype=torch.int32, device=eng.device)
+    bs = min(128, N)
+    g = torch.Generator().manual_seed(0)
+    for _ in range(max(1, epochs)):
+        perm = torch.randperm(N, generator=g).to(eng.device)
+        for b in range(0, N - bs + 1, bs):
+            idx = perm[b:b + bs]
+            eng.train_step(x_all.index_select(0, idx), y_all.index_select(0, idx))
+    eng.prepare_eval()
+    return eng
+
+
+def _classify(eng, imgs_nhwc, batch=512):
+    out = []
+    for b in range(0, len(imgs_nhwc), batch):
+        x = eng.prepare_inputs(imgs_nhwc[b:b + batch])
+        out.append(eng.forward_eval(x).float().cpu().numpy())
+    return np.concatenate(out)
+
+
+if __name__ == '__main__':
+    from rafiki_amd.model import test_model_class
+    test_model_class(__file__, 'PgGan', TaskType.IMAGE_GENERATION, {},
+                     'synthetic://image?n=512&size=16&channels=1&classes=4&seed=0',
+                     'synthetic://image?n=256&size=16&channels=1&classes=4&seed=1',
+                     queries=[[2, 2, 1]],
+                     knobs={'D_repeats': 1, 'minibatch_base': 4, 'G_lrate': 1e-3, 'D_lrate': 1e-3,
+                            'lod_initial_resolution': 4, 'total_kimg': 0.5, 'lod_training_kimg': 0.2,
+                            'lod_transition_kimg': 0.2, 'fmap_base': 256, 'fmap_max': 64, 'eval_images': 256})

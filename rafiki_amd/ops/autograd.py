@@ -1,0 +1,306 @@
+"""Twice-differentiable autograd wrappers over the gfx950 conv / dense kernels.
+
+WGAN-GP (pg_gans.py:1305-1315) differentiates the discriminator's input-gradient with respect to
+the discriminator's weights, so every backward here is itself expressed through these Functions
+(SURVEY §7.4 (1)): the three GEMMs of a layer close under differentiation
+
+    y  = conv(x, w)        dx = dgrad(dy, w)      dw = wgrad(x, dy)
+    d(dgrad)/d(dy) = conv(., w)     d(dgrad)/d(w) = wgrad(., dy)
+    d(wgrad)/d(x)  = dgrad(dy, .)   d(wgrad)/d(dy) = conv(x, .)
+
+and the same for dense (x @ w.T, dy @ w, dy.T @ x).  Conventions (see ops.functional):
+activations are NHWC / [M, K] bf16, weights are fp32 masters ``w`` with a bf16 shadow ``wb`` that
+the fused optimizer keeps in sync (pass ``wb=None`` to cast on the fly), weight gradients come out
+of the kernels in fp32 directly (no bf16 round trip on dW).
+
+On CPU tensors every op falls back to plain fp32 PyTorch (F.conv2d / matmul), which torch already
+differentiates twice — that path is the numerics oracle for the GPU tests.  On a GPU tensor the
+native library is mandatory (a missing extension raises, it never silently falls back).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as TF
+
+from . import functional as F
+
+BF16 = torch.bfloat16
+
+
+def _bf(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    return t.detach().to(BF16).contiguous() if t.dtype != BF16 else t.detach().contiguous()
+
+
+def _wshadow(w, wb):
+    return wb if wb is not None else _bf(w)
+
+
+def _needed(ctx, i):
+    """Input i needs a gradient in THIS backward: autograd.grad(..., inputs=[images]) (the WGAN-GP
+    input gradient) must not pay for weight gradients it then drops."""
+    if not ctx.needs_input_grad[i]:
+        return False
+    try:
+        fn = ctx.next_functions[i][0]
+        return fn is None or bool(torch._C._will_engine_execute_node(fn))
+    except Exception:
+        return True
+
+
+def _k(taps):
+    return 3 if taps == 9 else 1
+
+
+# ------------------------------------------------------------------------------- CPU reference
+def _conv_ref(x, w, b, taps):
+    Cout = w.shape[0]
+    Cin = w.numel() // (Cout * taps)
+    k = _k(taps)
+    wt = w.reshape(Cout, k, k, Cin).permute(0, 3, 1, 2)
+    y = TF.conv2d(x.permute(0, 3, 1, 2), wt.to(x.dtype), None if b is None else b.to(x.dtype), padding=k // 2)
+    return y.permute(0, 2, 3, 1)
+
+
+def upscale2d(x, factor=2):
+    """Nearest-neighbour upscale of NHWC (pg_gans.py:1042-1050)."""
+    if factor == 1:
+        return x
+    N, h, w, C = x.shape
+    return x[:, :, None, :, None, :].expand(N, h, factor, w, factor, C).reshape(N, h * factor, w * factor, C)
+
+
+def downscale2d(x, factor=2):
+    """Box-filter downscale of NHWC (pg_gans.py:1062-1067), accumulated in fp32."""
+    if factor == 1:
+        return x
+    N, H, W, C = x.shape
+    y = x.reshape(N, H // factor, factor, W // factor, factor, C).float().mean((2, 4))
+    return y.to(x.dtype)
+
+
+def sumpool2(x):
+    N, H, W, C = x.shape
+    return x.reshape(N, H // 2, 2, W // 2, 2, C).float().sum((2, 4)).to(x.dtype)
+
+
+# ------------------------------------------------------------------------------------- conv
+class ConvFn(torch.autograd.Function):
+    """y = conv_{taps}(x, w) + b   (x NHWC bf16, w fp32 [Cout, taps*Cin] tap-major)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wb, taps):
+        x = x.contiguous()
+        wbs = _wshadow(w, wb)
+        y = F.conv_fwd(x, wbs, taps=taps, bias=None if b is None else b.detach().float().contiguous())
+        ctx.save_for_backward(x, w)
+        ctx.wb, ctx.taps, ctx.has_b = wb, taps, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.to(BF16).contiguous()
+        gx = gw = gb = None
+        if _needed(ctx, 0):
+            gx = ConvDgradFn.apply(gy, w, ctx.wb, ctx.taps)
+        if _needed(ctx, 1):
+            gw = ConvWgradFn.apply(x, gy, ctx.taps)
+        if ctx.has_b and _needed(ctx, 2):
+            gb = gy.float().sum((0, 1, 2))
+        return gx, gw, gb, None, None
+
+
+class ConvDgradFn(torch.autograd.Function):
+    """dx = dgrad(dy, w)  (the transposed conv, tap-flipped gather of the forward weights)."""
+
+    @staticmethod
+    def forward(ctx, gy, w, wb, taps):
+        gy = gy.contiguous()
+        dx = F.conv_dgrad(gy, _wshadow(w, wb), taps=taps)
+        ctx.save_for_backward(gy, w)
+        ctx.wb, ctx.taps = wb, taps
+        return dx
+
+    @staticmethod
+    def backward(ctx, ggx):
+        gy, w = ctx.saved_tensors
+        ggx = ggx.to(BF16).contiguous()
+        g_gy = g_w = None
+        if _needed(ctx, 0):
+            g_gy = ConvFn.apply(ggx, w, None, ctx.wb, ctx.taps)
+        if _needed(ctx, 1):
+            g_w = ConvWgradFn.apply(ggx, gy, ctx.taps)
+        return g_gy, g_w, None, None
+
+
+class ConvWgradFn(torch.autograd.Function):
+    """dw (fp32) = wgrad(x, dy)."""
+
+    @staticmethod
+    def forward(ctx, x, gy, taps):
+        x, gy = x.contiguous(), gy.contiguous()
+        dw = F.conv_wgrad(gy, x, taps=taps)
+        ctx.save_for_backward(x, gy)
+        ctx.taps = taps
+        return dw
+
+    @staticmethod
+    def backward(ctx, ggw):
+        x, gy = ctx.saved_tensors
+        ggw = ggw.contiguous()
+        g_x = g_gy = None
+        if _needed(ctx, 0):
+            g_x = ConvDgradFn.apply(gy, ggw, None, ctx.taps)
+        if _needed(ctx, 1):
+            g_gy = ConvFn.apply(x, ggw, None, None, ctx.taps)
+        return g_x, g_gy, None
+
+
+def conv2d(x, w, b=None, *, taps=9, wb=None):
+    """NHWC conv, stride 1, SAME padding (3x3 when taps == 9, 1x1 when taps == 1)."""
+    if x.device.type != 'cuda':
+        return _conv_ref(x, w, b, taps)
+    return ConvFn.apply(x, w, b, wb, taps)
+
+
+class UpConvFn(torch.autograd.Function):
+    """y = conv3x3(upscale2d(x), w) + b with the upscale fused into the conv gather (forward only;
+    the backward runs on the 2x grid and sum-pools, built from the differentiable Functions)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wb):
+        x = x.contiguous()
+        y = F.conv_up(x, _wshadow(w, wb), bias=None if b is None else b.detach().float().contiguous())
+        ctx.save_for_backward(x, w)
+        ctx.wb, ctx.has_b = wb, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.to(BF16).contiguous()
+        gx = gw = gb = None
+        if _needed(ctx, 0):
+            gx = sumpool2(ConvDgradFn.apply(gy, w, ctx.wb, 9))
+        if _needed(ctx, 1):
+            gw = ConvWgradFn.apply(upscale2d(x).contiguous(), gy, 9)
+        if ctx.has_b and _needed(ctx, 2):
+            gb = gy.float().sum((0, 1, 2))
+        return gx, gw, gb, None
+
+
+def upscale_conv2d(x, w, b=None, *, wb=None):
+    if x.device.type != 'cuda':
+        return _conv_ref(upscale2d(x), w, b, 9)
+    return UpConvFn.apply(x, w, b, wb)
+
+
+def conv2d_downscale2d(x, w, b=None, *, wb=None):
+    """conv3x3 then 2x2 box downscale == the reference's fused 4x4 stride-2 conv (pg_gans.py:1053-1059)."""
+    return downscale2d(conv2d(x, w, b, taps=9, wb=wb))
+
+
+# ------------------------------------------------------------------------------------ dense
+class DenseFn(torch.autograd.Function):
+    """y = x @ w.T + b   (x [M, K] bf16, w fp32 [N, K])."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wb):
+        x = x.contiguous()
+        y = F.linear(x, _wshadow(w, wb), None if b is None else b.detach().float().contiguous())
+        ctx.save_for_backward(x, w)
+        ctx.wb, ctx.has_b = wb, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.to(BF16).contiguous()
+        gx = gw = gb = None
+        if _needed(ctx, 0):
+            gx = DenseDxFn.apply(gy, w, ctx.wb)
+        if _needed(ctx, 1):
+            gw = DenseDwFn.apply(x, gy)
+        if ctx.has_b and _needed(ctx, 2):
+            gb = gy.float().sum(0)
+        return gx, gw, gb, None
+
+
+class DenseDxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gy, w, wb):
+        gy = gy.contiguous()
+        dx = F.linear_dx(gy, _wshadow(w, wb))
+        ctx.save_for_backward(gy, w)
+        ctx.wb = wb
+        return dx
+
+    @staticmethod
+    def backward(ctx, ggx):
+        gy, w = ctx.saved_tensors
+        ggx = ggx.to(BF16).contiguous()
+        g_gy = g_w = None
+        if _needed(ctx, 0):
+            g_gy = DenseFn.apply(ggx, w, None, ctx.wb)
+        if _needed(ctx, 1):
+            g_w = DenseDwFn.apply(ggx, gy)
+        return g_gy, g_w, None
+
+
+class DenseDwFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gy):
+        x, gy = x.contiguous(), gy.contiguous()
+        dw = F.linear_dw(gy, x)
+        ctx.save_for_backward(x, gy)
+        return dw
+
+    @staticmethod
+    def backward(ctx, ggw):
+        x, gy = ctx.saved_tensors
+        ggw = ggw.contiguous()
+        g_x = g_gy = None
+        if _needed(ctx, 0):
+            g_x = DenseDxFn.apply(gy, ggw, None)
+        if _needed(ctx, 1):
+            g_gy = DenseFn.apply(x, ggw, None, None)
+        return g_x, g_gy
+
+
+def dense(x, w, b=None, *, wb=None):
+    if x.device.type != 'cuda':
+        return TF.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
+    return DenseFn.apply(x, w, b, wb)
+
+
+# ---------------------------------------------------------------------------- elementwise glue
+def leaky_relu(x, slope=0.2):
+    """max(x*a, x) (pg_gans.py:987-990); twice differentiable through torch."""
+    return TF.leaky_relu(x, slope)
+
+
+def pixel_norm(x, eps=1e-8):
+    """x * rsqrt(mean_c(x^2) + eps) over the channel (last) axis, fp32 accumulation (pg_gans.py:993-995)."""
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.square().mean(-1, keepdim=True) + eps)).to(x.dtype)
+
+
+def minibatch_stddev(x, group_size=4, pad_to=8):
+    """Append the group-stddev feature map (pg_gans.py:1070-1082) and zero-pad the channel count
+    to a multiple of ``pad_to`` so the following conv can run on the MFMA path (512+1 -> 520)."""
+    N, H, W, C = x.shape
+    g = min(group_size, N)
+    y = x.float().reshape(g, -1, H, W, C)
+    y = y - y.mean(0, keepdim=True)
+    y = (y.square().mean(0) + 1e-8).sqrt()
+    y = y.mean((1, 2, 3))  # [N/g]
+    y = y.reshape(1, -1, 1, 1, 1).expand(g, -1, H, W, 1).reshape(N, H, W, 1).to(x.dtype)
+    extra = (-(C + 1)) % pad_to
+    parts = [x, y]
+    if extra:
+        parts.append(x.new_zeros((N, H, W, extra)))
+    return torch.cat(parts, -1)

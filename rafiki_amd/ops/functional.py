@@ -19,7 +19,7 @@ import torch
 
 from . import _lib
 
-KIND_CONV_FWD, KIND_CONV_DGRAD, KIND_CONV_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW = range(6)
+KIND_CONV_FWD, KIND_CONV_DGRAD, KIND_CONV_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW, KIND_CONV_UP = range(7)
 FLAG_RELU, FLAG_BIAS, FLAG_STATS, FLAG_GATE, FLAG_ACCUM, FLAG_LRELU = 1, 2, 4, 8, 16, 32
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
@@ -157,6 +157,26 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
                  _tile_candidates(M, Cout, fixed_bm=TILES[tile][0] if want_stats else None), run)
     run(cfg)
     return (out, stats) if want_stats else out
+
+
+def conv_up(x: torch.Tensor, w: torch.Tensor, *, bias=None, act=ACT_NONE, slope=0.2, out=None):
+    """y = conv3x3(upscale2d_nearest(x)) [+bias][act] without materialising the 2x input: the gather
+    reads input pixel ((h+dy)>>1, (w+dx)>>1) directly (PG-GAN ``_upscale2d_conv2d``, pg_gans.py:1032-1039)."""
+    Nb, h, w_, Cin = x.shape
+    H, W = 2 * h, 2 * w_
+    Cout = w.shape[0]
+    M, K = Nb * H * W, 9 * Cin
+    assert w.numel() == Cout * K, (w.shape, Cin)
+    if out is None:
+        out = torch.empty((Nb, H, W, Cout), device=x.device, dtype=torch.bfloat16)
+    flags = (FLAG_BIAS if bias is not None else 0) | (FLAG_RELU if act == ACT_RELU else 0) | (
+        FLAG_LRELU if act == ACT_LRELU else 0)
+
+    def run(cfg):
+        igemm(KIND_CONV_UP, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, H=H, W=W, C=Cin, taps=9,
+              flags=flags, slope=slope, tile=cfg[0])
+    run(_tuned(('cu', M, Cout, K, H, W, Cin), [c for c in _tile_candidates(M, Cout) if c[0] < 32], run))
+    return out
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, gate=None):

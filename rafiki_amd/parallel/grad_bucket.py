@@ -1,0 +1,127 @@
+"""Bucketed, backward-overlapped gradient all-reduce over a flat fp32 gradient arena.
+
+Replaces the reference's per-variable ``tf.contrib.nccl.all_sum`` (pg_gans.py:1164-1171: ~25 calls
+per network per step, several of them on tiny bias tensors) with a handful of large RCCL
+all-reduces over contiguous slices of the FlatParams gradient buffer:
+
+* buckets are contiguous ranges of the arena in REVERSE parameter order (backward produces the
+  last layers' gradients first), each ~``bucket_mb`` MiB.  On xGMI a ring all-reduce is bound by
+  one 153 GB/s link per hop, so a 16-32 MiB bucket amortises the ~10-20 us launch/latency to <5%
+  while still giving several buckets to overlap with the remaining backward;
+* a ``register_post_accumulate_grad_hook`` per parameter counts arrivals; when a bucket is
+  complete its all-reduce is launched asynchronously (``async_op=True``) on RCCL's internal
+  stream, overlapping the rest of the backward;
+* ``finish()`` launches whatever did not fire (parameters outside the active graph, e.g. PG-GAN
+  blocks above the current level of detail, still hold zeros and must be reduced to keep the
+  replicas identical) and waits, then applies the 1/world mean (pg_gans.py:1175-1179).
+
+Gradients are summed in fp32 (they live in fp32 in the arena), so the reduction is exact up to
+fp32 association order — identical across ranks, which keeps the replicated Adam states in sync.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+class FlatGradAllReduce:
+    def __init__(self, grad: torch.Tensor, param_ranges: Sequence[Tuple[int, int]], params: Sequence[torch.Tensor],
+                 world_size: int, group=None, bucket_mb: float = 24.0, overlap: bool = True):
+        """grad: flat fp32 buffer; param_ranges[i] = (offset, numel) of params[i] inside it."""
+        self.grad = grad
+        self.world = int(world_size)
+        self.group = group
+        self.overlap = overlap and self.world > 1
+        cap = max(1, int(bucket_mb * (1 << 20)) // 4)
+        order = sorted(range(len(param_ranges)), key=lambda i: -param_ranges[i][0])  # reverse arena order
+        self.buckets: List[Tuple[int, int]] = []
+        self.bucket_of: List[int] = [0] * len(param_ranges)
+        self.bucket_size: List[int] = []
+        lo = hi = None
+        count = 0
+        for i in order:
+            off, n = param_ranges[i]
+            if hi is None:
+                lo, hi, count = off, off + n, 0
+            elif (hi - min(lo, off)) > cap:
+                self.buckets.append((lo, hi))
+                self.bucket_size.append(count)
+                lo, hi, count = off, off + n, 0
+            lo = min(lo, off)
+            hi = max(hi, off + n)
+            self.bucket_of[i] = len(self.buckets)
+            count += 1
+        if hi is not None:
+            self.buckets.append((lo, hi))
+            self.bucket_size.append(count)
+        # close gaps: buckets cover the arena exactly (alignment padding included) so finish() reduces
+        # everything once
+        total = grad.numel()
+        bounds = sorted(self.buckets)
+        fixed = []
+        prev = 0
+        for a, b in bounds:
+            fixed.append((prev, b))
+            prev = b
+        if fixed:
+            fixed[-1] = (fixed[-1][0], total)
+        remap = {old: new for old, new in zip(bounds, fixed)}
+        self.buckets = [remap[b] for b in self.buckets]
+        self._pending = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+        self._hooks = []
+        if self.overlap:
+            for i, p in enumerate(params):
+                if p.requires_grad:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+
+    def _make_hook(self, i):
+        def hook(_p):
+            if not self.active:
+                return
+            b = self.bucket_of[i]
+            self._pending[b] += 1
+            if self._pending[b] == self.bucket_size[b] and not self._launched[b]:
+                self._launch(b)
+        return hook
+
+    active = False
+
+    def begin(self):
+        """Call before the backward whose gradients should be reduced."""
+        self._pending = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+        self.active = self.overlap
+
+    def _launch(self, b):
+        a, e = self.buckets[b]
+        self._launched[b] = True
+        self._works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def finish(self, average: bool = True):
+        self.active = False
+        if self.world <= 1:
+            return
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:
+                self._launch(b)
+        for w in self._works:
+            w.wait()
+        self._works = []
+        if average:
+            self.grad.mul_(1.0 / self.world)
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def broadcast_flat(t: torch.Tensor, src: int = 0, group=None, world_size: int = 1):
+    """Make a replicated flat buffer identical on every rank (initial weights)."""
+    if world_size > 1:
+        dist.broadcast(t, src=src, group=group)

@@ -1,0 +1,51 @@
+"""ctypes bindings of the host C++ runtime (``rafiki_amd/_native/librafiki_runtime.so``).
+
+The runtime is optional on CPU-only dev boxes (pure-Python fallbacks exist for every entry point);
+``available()`` reports whether it was built.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent / "_native" / "librafiki_runtime.so"
+_lock = threading.Lock()
+_lib = None
+_tried = False
+
+_SIGS = {
+    "rt_crc32c": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_longlong]),
+    "rt_masked_crc32c": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_longlong]),
+    "rt_tfrecord_info": (ctypes.c_longlong, [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]),
+    "rt_tfrecord_decode_images": (ctypes.c_longlong,
+                                  [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
+                                   ctypes.c_int]),
+}
+
+
+def lib():
+    global _lib, _tried
+    with _lock:
+        if _lib is None and not _tried:
+            _tried = True
+            if _LIB_PATH.exists():
+                h = ctypes.CDLL(str(_LIB_PATH))
+                for name, (res, args) in _SIGS.items():
+                    fn = getattr(h, name, None)
+                    if fn is None:
+                        continue
+                    fn.restype, fn.argtypes = res, args
+                _lib = h
+        return _lib
+
+
+def available() -> bool:
+    return lib() is not None
+
+
+def reset():
+    """Forget a cached handle (after a rebuild in the same process)."""
+    global _lib, _tried
+    with _lock:
+        _lib, _tried = None, False

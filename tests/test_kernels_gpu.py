@@ -91,7 +91,7 @@ def test_dense_fwd_bwd(fn, M, K, N):
 
 
 @pytest.mark.parametrize("pool", [False, True])
-@pytest.mark.parametrize("N,H,W,C", [(4, 8, 8, 64), (2, 4, 4, 512), (3, 16, 16, 128)])
+@pytest.mark.parametrize("N,H,W,C", [(4, 8, 8, 64), (2, 4, 4, 512), (3, 16, 16, 128), (4, 3, 3, 64), (2, 6, 6, 32)])
 def test_bn_relu_pool_fwd_bwd(fn, N, H, W, C, pool):
     torch.manual_seed(4)
     y = (torch.randn(N, H, W, C, device=DEV) * 2 + 0.5).bfloat16()

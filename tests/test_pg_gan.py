@@ -1,0 +1,225 @@
+"""PG-GAN (IMAGE_GENERATION) on CPU: TFRecord format, schedule, WGAN-GP training, DP over gloo.
+
+Parity notes: the reference's pg_gans.py needs TensorFlow 1.12 (not importable here), so the
+schedule is checked against values derived by hand from pg_gans.py:1227-1274 and the TFRecord
+bytes against the format spec (length/CRC framing + tf.train.Example wire encoding).
+"""
+import os
+import socket
+import tempfile
+from contextlib import closing
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from rafiki_amd.model import tfrecord as T
+
+TINY = dict(D_repeats=1, minibatch_base=4, G_lrate=1e-3, D_lrate=1e-3, lod_initial_resolution=4, total_kimg=0.3,
+            lod_training_kimg=0.1, lod_transition_kimg=0.1, fmap_base=128, fmap_max=32, eval_images=128,
+            minibatch_repeats=1)
+DATA = 'synthetic://image?n=256&size=16&channels=1&classes=4&seed=0'
+
+
+def test_crc32c_known_vector():
+    assert T.crc32c(b'123456789') == 0xE3069283
+    assert T.masked_crc(b'') == ((((0 >> 15) | (0 << 17)) + 0xA282EAD8) & 0xFFFFFFFF)
+
+
+def test_example_roundtrip():
+    payload = T.encode_example({'shape': [3, 8, 8], 'data': bytes(range(192)), 'f': [0.5, 1.5]})
+    ex = T.decode_example(payload)
+    assert ex['shape'] == [3, 8, 8] and ex['data'][0] == bytes(range(192)) and ex['f'] == [0.5, 1.5]
+
+
+def test_tfrecord_dataset_roundtrip(tmp_path):
+    rng = np.random.RandomState(0)
+    imgs = rng.randint(0, 256, (40, 3, 16, 16)).astype(np.uint8)
+    d = str(tmp_path / 'cifar')
+    T.write_tfrecord_dataset(d, imgs, labels=np.arange(40) % 5)
+    names = sorted(os.listdir(d))
+    assert names == ['cifar-r02.tfrecords', 'cifar-r03.tfrecords', 'cifar-r04.tfrecords', 'cifar-rxx.labels']
+    for n in names[:-1]:
+        assert sum(1 for _ in T.iter_records(os.path.join(d, n), verify=True)) == 40
+    ds = T.TFRecordImageDataset(d)
+    order = np.arange(40)
+    np.random.RandomState(123).shuffle(order)
+    assert ds.shape == [3, 16, 16] and ds.label_size == 5 and ds.resolution_log2 == 4
+    assert (ds.images[0] == imgs[order]).all()
+    lod1 = np.rint(T.downscale_images(imgs[order].astype(np.float32))).clip(0, 255).astype(np.uint8)
+    assert (ds.images[1] == lod1).all()
+    assert (ds.labels.argmax(1) == (order % 5)).all()
+
+
+def test_tfrecord_python_fallback_matches_native(tmp_path, monkeypatch):
+    from rafiki_amd import runtime
+    if not runtime.available():
+        pytest.skip('native runtime not built')
+    imgs = np.random.RandomState(1).randint(0, 256, (10, 1, 8, 8)).astype(np.uint8)
+    d = str(tmp_path / 'm')
+    T.write_tfrecord_dataset(d, imgs, shuffle=False)
+    native = T._read_images(os.path.join(d, 'm-r03.tfrecords'))
+    monkeypatch.setattr(runtime, 'lib', lambda: None)
+    py = T._read_images(os.path.join(d, 'm-r03.tfrecords'))
+    assert (native == py).all() and (py == imgs).all()
+
+
+def test_training_schedule():
+    from rafiki_amd.models.pg_gan import TrainingSchedule as S
+    s = S(0, 5, minibatch_base=16)
+    assert s.lod == 3.0 and s.resolution == 4 and s.minibatch == 512
+    s = S(900_000, 5, minibatch_base=4)  # halfway through the first transition
+    assert abs(s.lod - 2.5) < 1e-9 and s.resolution == 8 and s.minibatch == 128
+    s = S(1_200_000, 5, minibatch_base=8, num_gpus=3)
+    assert s.lod == 2.0 and s.minibatch == 255  # 256 - 256 % 3
+    s = S(10_000_000, 5, minibatch_base=32)
+    assert s.lod == 0.0 and s.resolution == 32 and s.minibatch == 64
+
+
+def test_pg_gan_train_eval_predict_cpu(tmp_path, monkeypatch):
+    monkeypatch.setenv('RAFIKI_OUTPUT_DIR', str(tmp_path))
+    from rafiki_amd.models.pg_gan import PgGan
+    m = PgGan(**TINY)
+    m.train(DATA)
+    assert m.lod == 1.0  # 0.3 kimg with 0.1/0.1 phases reaches the 8x8 -> 16x16 level
+    assert all(np.isfinite(v) for v in m.stats.values())
+    score = m.evaluate('synthetic://image?n=128&size=16&channels=1&classes=4&seed=1')
+    assert isinstance(score, float) and 1.0 <= score <= 4.0 + 1e-6
+    params = m.dump_parameters()
+    m2 = PgGan(**TINY)
+    m2.load_parameters(params)
+    a = m.generate(4, seed=3)
+    b = m2.generate(4, seed=3)
+    assert a.shape == (4, 16, 16, 1) and (a == b).all()
+    paths = m2.predict([2, 2, 2])
+    assert len(paths) == 2 and all(os.path.exists(p) and p.endswith('.jpeg') for p in paths)
+
+
+def test_pg_gan_tfrecord_input_and_labels(tmp_path):
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.models.pg_gan import PgGan
+    imgs, labels = synthetic_images(64, size=8, channels=3, classes=3, seed=0)
+    d = str(tmp_path / 'cond')
+    T.write_tfrecord_dataset(d, imgs.transpose(0, 3, 1, 2), labels=labels)
+    m = PgGan(**dict(TINY, total_kimg=0.1))
+    m.train(d)
+    assert m.nets.label_size == 3 and m.nets.num_channels == 3  # AC-GAN label penalty path
+    assert all(np.isfinite(v) for v in m.stats.values())
+
+
+def test_gradient_penalty_double_backward_cpu():
+    """The D-side ops are twice differentiable: d/dw ||dD/dx|| matches finite differences."""
+    from rafiki_amd.models.pg_gan import PgNetworks
+    torch.manual_seed(0)
+    nets = PgNetworks(num_channels=1, resolution=8, fmap_base=64, fmap_max=16, device='cpu', seed=0)
+    P = nets.src_D()
+    x = torch.randn(4, 8, 8, nets.cpad)
+    x[..., 1:] = 0
+
+    def gp():
+        xi = x.clone().requires_grad_(True)
+        s, _ = nets.discriminator(P, xi, 0.0)
+        (g,) = torch.autograd.grad(s.sum(), xi, create_graph=True)
+        return g.square().sum()
+
+    name = '8x8/Conv0/weight'
+    p = nets.d_params[name]
+    p.grad.zero_()
+    gp().backward()
+    ana = p.grad.flatten()[:5].clone()
+    eps = 1e-3
+    num = []
+    flat = p.detach().view(-1)  # aliases the parameter storage
+    for i in range(5):
+        o = flat[i].item()
+        flat[i] = o + eps
+        up = gp().item()
+        flat[i] = o - eps
+        dn = gp().item()
+        flat[i] = o
+        num.append((up - dn) / (2 * eps))
+    num = torch.tensor(num)
+    assert torch.allclose(ana, num, rtol=2e-2, atol=1e-4 * max(1.0, num.abs().max().item())), (ana, num)
+
+
+# ------------------------------------------------------------------------------ DP over gloo
+def _free_port():
+    with closing(socket.socket(socket.AF_INET, socket.SOCK_STREAM)) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port):
+    os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'RAFIKI_CPU_ONLY': '1'})
+
+
+def _bucket_worker(rank, world, port, out_dir):
+    _env(rank, world, port)
+    import torch.distributed as dist
+    from rafiki_amd.engine.flat import FlatParams, init_const
+    from rafiki_amd.parallel.grad_bucket import FlatGradAllReduce
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    flat = FlatParams('cpu')
+    for i in range(6):
+        flat.add('p{}'.format(i), (100 + 37 * i,), init_const(1.0))
+    flat.build()
+    params = []
+    for s in flat.specs:
+        p = torch.nn.Parameter(flat.w(s.name))
+        p.grad = flat.g(s.name)
+        params.append(p)
+    ar = FlatGradAllReduce(flat.grad, flat.param_ranges(), params, world, bucket_mb=0.001)
+    assert len(ar.buckets) > 1
+    ar.begin()
+    loss = sum((p * (rank + 1) * (i + 1)).sum() for i, p in enumerate(params[:4]))  # p4, p5 unused
+    loss.backward()
+    ar.finish()
+    torch.save(flat.grad.clone(), os.path.join(out_dir, 'g{}.pt'.format(rank)))
+    dist.destroy_process_group()
+
+
+def test_flat_grad_allreduce_gloo():
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_bucket_worker, args=(2, port, d), nprocs=2, join=True)
+        g0 = torch.load(os.path.join(d, 'g0.pt'), weights_only=True)
+        g1 = torch.load(os.path.join(d, 'g1.pt'), weights_only=True)
+    assert torch.equal(g0, g1)
+    from rafiki_amd.engine.flat import FlatParams, init_const
+    flat = FlatParams('cpu')
+    for i in range(6):
+        flat.add('p{}'.format(i), (100 + 37 * i,), init_const(1.0))
+    flat.build()
+    for i, s in enumerate(flat.specs):
+        v = g0[s.offset:s.offset + s.numel]
+        expect = (1 + 2) / 2 * (i + 1) if i < 4 else 0.0
+        assert torch.allclose(v, torch.full_like(v, expect)), (i, v[:3])
+
+
+def _dp_worker(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rafiki_amd.models.pg_gan import PgGan
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    info = D.init_distributed(backend='gloo')
+    with use_context(TrialContext(device=torch.device('cpu'), dist=info, data_parallel=True)):
+        m = PgGan(**dict(TINY, total_kimg=0.2))
+        m.train(DATA)
+        torch.save({'G': m.nets.G.master.clone(), 'D': m.nets.D.master.clone(), 'Gs': m.nets.Gs_master.clone(),
+                    'stats': torch.tensor([m.stats['D_loss'], m.stats['G_loss']])},
+                   os.path.join(out_dir, 'r{}.pt'.format(rank)))
+    D.destroy(info)
+
+
+def test_pg_gan_data_parallel_gloo():
+    """2-rank DP: replicas stay bit-identical (same averaged grads, same Adam), shards differ."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dp_worker, args=(2, port, d), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, 'r0.pt'), weights_only=True)
+        r1 = torch.load(os.path.join(d, 'r1.pt'), weights_only=True)
+    for k in ('G', 'D', 'Gs'):
+        assert torch.equal(r0[k], r1[k]), k
+    assert not torch.equal(r0['stats'], r1['stats'])  # each rank saw its own minibatch shard
