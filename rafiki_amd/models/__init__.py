@@ -1,6 +1,7 @@
 """Model zoo: single-file BaseModel classes uploadable through the client.
 
   VggSmall (vgg_small.py)        gfx950 engine, the BASELINE benchmark architecture
+  Vgg16 (vgg16.py)               gfx950 engine, TfVgg16 semantics (48x48x3, Adam)
   FeedForward (feed_forward.py)  gfx950 engine, TfFeedForward semantics
   SkDt, SkSvm (sk_models.py)     scikit-learn on CPU
   BigramHmm, PyBiLstm (pos_tagging.py)
@@ -11,6 +12,7 @@ import os
 MODELS_DIR = os.path.dirname(os.path.abspath(__file__))
 ZOO = {
     'VggSmall': ('vgg_small.py', 'IMAGE_CLASSIFICATION'),
+    'Vgg16': ('vgg16.py', 'IMAGE_CLASSIFICATION'),
     'FeedForward': ('feed_forward.py', 'IMAGE_CLASSIFICATION'),
     'SkDt': ('sk_models.py', 'IMAGE_CLASSIFICATION'),
     'SkSvm': ('sk_models.py', 'IMAGE_CLASSIFICATION'),

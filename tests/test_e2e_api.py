@@ -151,3 +151,11 @@ def test_stop_all_jobs_superadmin_only(stack):
         dev_c.stop_all_jobs()
     out = client(stack).stop_all_jobs()
     assert set(out) == {'train_jobs', 'inference_jobs'}
+
+
+def test_web_ui_served(stack):
+    import requests
+    r = requests.get('http://127.0.0.1:{}/ui'.format(stack['port']), timeout=10)
+    assert r.status_code == 200 and r.headers['Content-Type'].startswith('text/html')
+    for frag in ('/tokens', '/train_jobs', '/trials/', 'plotSvg', 'x_axis'):
+        assert frag in r.text

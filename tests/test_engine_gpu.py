@@ -73,3 +73,33 @@ def test_training_reduces_loss_and_eval():
     _, ref_logits = eng.reference_loss(x, None, training=False)
     ref = torch.softmax(ref_logits, 1)
     assert (probs - ref).abs().max().item() < 5e-2
+
+
+def test_grads_match_reference_non_pow2_vgg16_layout():
+    """48x48 input with VGG16-style pooling to 3x3 -> 1x1 (non-power-of-two gather + odd pool)."""
+    eng = _engine(image_size=48, cfg=(16, 'M', 32, 'M', 32, 'M', 64, 'M', 64, 'M'), fc_dims=(64,))
+    x, y = _batch(32, hw=48, seed=7)
+    eng.forward_backward(x, y)
+    torch.cuda.synchronize()
+    fl = eng.flat
+    params = {n: fl.w(n).detach().clone().requires_grad_(True) for n in fl.names()}
+    loss, _ = eng.reference_loss(x, y, params, training=True, emulate_bf16=True)
+    grads = torch.autograd.grad(loss, [params[n] for n in fl.names()])
+    assert abs(eng.loss_sum.item() / 32 - loss.item()) < 1e-2 * max(1.0, loss.item())
+    for n, g in zip(fl.names(), grads):
+        got = fl.g(n)
+        fro = ((got - g).norm() / g.norm().clamp_min(1e-12)).item()
+        cos = torch.nn.functional.cosine_similarity(got.flatten(), g.flatten(), 0).item()
+        assert fro < 0.12 and cos > 0.99, (n, fro, cos)
+
+
+def test_vgg16_model_trains():
+    import numpy as np
+    from rafiki_amd.models.vgg16 import Vgg16
+    m = Vgg16(epochs=1, learning_rate=1e-3, batch_size=32)
+    m._knobs['epochs'] = 6
+    m.train('synthetic://image?n=512&size=28&channels=1&classes=4&seed=0')
+    acc = m.evaluate('synthetic://image?n=256&size=28&channels=1&classes=4&seed=1')
+    assert acc > 0.5, acc
+    p = m.predict([np.zeros((28, 28), np.uint8).tolist()])
+    assert len(p) == 1 and abs(sum(p[0]) - 1) < 1e-3
