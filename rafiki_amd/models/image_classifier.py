@@ -132,6 +132,18 @@ class NativeImageClassifier(BaseModel):
             arr = np.repeat(arr[..., None], ch, -1)
         return arr
 
+    def input_signature(self):
+        """Models with equal signatures accept the same uint8 image batch (the predictor converts and
+        uploads a request once per signature, not once per model)."""
+        return ('image_u8', self.image_size, self._meta['channels'])
+
+    def queries_to_images(self, queries):
+        return self._queries_to_images(queries)
+
+    def predict_proba_images(self, images) -> torch.Tensor:
+        """uint8 [Q, H, W(, C)] (host or device) at this model's size -> device probabilities [Q, C]."""
+        return self._probs(images)
+
     def predict_proba(self, queries) -> torch.Tensor:
         """Device tensor [Q, num_classes] (used by the predictor's on-device ensemble)."""
         return self._probs(self._queries_to_images(queries))

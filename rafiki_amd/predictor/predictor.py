@@ -138,8 +138,16 @@ class Predictor:
         return ensemble_predictions(preds, self.task)
 
     def _predict_fast(self, queries):
+        return self.predict_proba(queries).cpu().tolist()
+
+    def predict_proba(self, queries):
+        """Ensemble probabilities [Q, C] as a tensor (on the GPU when the models are).
+
+        Queries are decoded to uint8 once per distinct model input signature and uploaded once
+        (pinned, non-blocking); every model then runs its hipGraph-captured bucketed forward on its
+        own HIP stream, and the gfx950 ensemble-mean kernel reduces the [models, Q, C] stack."""
+        import numpy as np
         import torch
-        outs = []
         dev = None
         for name, m in self.models:
             d = getattr(m, 'device', None)
@@ -148,22 +156,44 @@ class Predictor:
                 break
         if dev is None:
             probs = [m.predict_proba(queries) for _, m in self.models]
-            stacked = torch.stack([p.float().cpu() for p in probs])
-            return ensemble_probabilities(stacked).tolist()
+            return ensemble_probabilities(torch.stack([p.float().cpu() for p in probs]))
+        inputs = {}
+        for _, m in self.models:
+            sig_fn = getattr(m, 'input_signature', None)
+            sig = sig_fn() if callable(sig_fn) else None
+            if sig is not None and sig not in inputs:
+                arr = np.ascontiguousarray(m.queries_to_images(queries))
+                host = torch.from_numpy(arr).pin_memory()
+                inputs[sig] = host.to(dev, non_blocking=True)
+        return self.predict_proba_device(inputs, queries)
+
+    def predict_proba_device(self, inputs, queries=None):
+        """inputs: {input_signature: device uint8 batch}.  Models without a signature get ``queries``."""
+        import torch
+        dev = next(iter(inputs.values())).device if inputs else torch.device('cuda')
         if self._streams is None or len(self._streams) != len(self.models):
             self._streams = [torch.cuda.Stream(device=dev) for _ in self.models]
         main = torch.cuda.current_stream(dev)
+        outs = []
         for (name, m), s in zip(self.models, self._streams):
             s.wait_stream(main)
             with torch.cuda.stream(s):
-                outs.append(m.predict_proba(queries))
+                sig_fn = getattr(m, 'input_signature', None)
+                sig = sig_fn() if callable(sig_fn) else None
+                if sig is not None and sig in inputs:
+                    p = m.predict_proba_images(inputs[sig])
+                else:
+                    p = m.predict_proba(queries)
+                outs.append(p)
         for s in self._streams:
             main.wait_stream(s)
+        for p in outs:
+            p.record_stream(main)
         stacked = torch.stack(outs)
         w = None
         if self.weights is not None:
             w = torch.tensor(self.weights, dtype=torch.float32, device=dev)
-        return ensemble_probabilities(stacked, w).cpu().tolist()
+        return ensemble_probabilities(stacked, w)
 
     # ------------------------------------------------------------------- dynamic batching
     def start(self):

@@ -1,0 +1,123 @@
+"""Predictor ensemble QPS benchmark (BASELINE config #4: top-4 trained CNNs batched on 1 MI355X,
+hipGraph forwards).
+
+Four VGG-small models (random init, the BASELINE architecture; weights do not change the cost)
+are loaded into one in-process ``Predictor`` on cuda:0.  Three measurements:
+
+* ``device``: a uint8 query batch already in HBM -> 4 hipGraph-captured forwards on 4 HIP streams
+  -> on-device ensemble mean; QPS per batch size (the serving ceiling of the GPU path);
+* ``api``: ``Predictor.predict(list-of-lists queries)`` — the JSON-shaped path of POST
+  /predict_batch: host decode, one pinned upload, ensemble, ``tolist()``;
+* ``batcher``: C concurrent clients each calling ``predict_one`` (dynamic batcher, max_wait 2 ms)
+  -> QPS and p50/p99 latency — the POST /predict path without HTTP.
+
+Reference analogue: <=128 QPS per inference worker with a >=0.25 s latency floor
+(Redis polling).  Prints one JSON line; ``--out`` also writes it to a file.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def build_models(k, device, classes=10):
+    from rafiki_amd.models.vgg_small import VggSmall
+    models = []
+    for i in range(k):
+        m = VggSmall(epochs=1, learning_rate=0.05, momentum=0.9, weight_decay=5e-4, batch_size=128, width_mult=1.0,
+                     image_size=32, seed=i)
+        m.device = device
+        m._build(classes, 3)
+        m._engine.prepare_eval()
+        models.append(('trial{}'.format(i), m))
+    return models
+
+
+def timed(fn, iters):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--models', type=int, default=4)
+    ap.add_argument('--batches', default='1,8,32,128,512')
+    ap.add_argument('--iters', type=int, default=50)
+    ap.add_argument('--clients', type=int, default=64)
+    ap.add_argument('--seconds', type=float, default=5.0)
+    ap.add_argument('--out', default='')
+    args = ap.parse_args()
+    from rafiki_amd.ops import _lib
+    from rafiki_amd.predictor.predictor import Predictor
+    _lib.lib()
+    dev = torch.device('cuda', 0)
+    models = build_models(args.models, dev)
+    pred = Predictor(models, max_batch=512, max_wait_ms=2.0)
+    rng = np.random.default_rng(0)
+    res = {'metric': 'predictor ensemble QPS (top-{} VGG-small 32x32x3, 1 GPU)'.format(args.models),
+           'n_models': args.models, 'device': {}, 'api': {}, 'dtype': 'bf16', 'data': 'synthetic, random-init'}
+    sig = models[0][1].input_signature()
+    for b in [int(x) for x in args.batches.split(',')]:
+        imgs = torch.from_numpy(rng.integers(0, 256, (b, 32, 32, 3), dtype=np.uint8)).to(dev)
+        inputs = {sig: imgs}
+        for _ in range(3):
+            pred.predict_proba_device(inputs)
+        dt = timed(lambda: pred.predict_proba_device(inputs), args.iters)
+        res['device'][b] = {'qps': round(b * args.iters / dt, 1), 'ms_per_batch': round(1e3 * dt / args.iters, 3)}
+        q = rng.integers(0, 256, (b, 32, 32, 3)).tolist()
+        pred.predict(q)
+        it = max(3, args.iters // 5)
+        dt = timed(lambda: pred.predict(q), it)
+        res['api'][b] = {'qps': round(b * it / dt, 1), 'ms_per_batch': round(1e3 * dt / it, 3)}
+    # dynamic batcher under concurrent single-query clients
+    pred.start()
+    one = rng.integers(0, 256, (32, 32, 3)).tolist()
+    for _ in range(20):
+        pred.predict_one(one)
+    lat, stop = [], threading.Event()
+    lock = threading.Lock()
+
+    def client():
+        mine = []
+        while not stop.is_set():
+            t = time.perf_counter()
+            pred.predict_one(one)
+            mine.append(time.perf_counter() - t)
+        with lock:
+            lat.extend(mine)
+    ths = [threading.Thread(target=client) for _ in range(args.clients)]
+    q0, b0 = pred.stats['queries'], pred.stats['batches']
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    time.sleep(args.seconds)
+    stop.set()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    nq = pred.stats['queries'] - q0
+    pred.stop()
+    lat_ms = np.array(lat) * 1e3
+    res['batcher'] = {'clients': args.clients, 'qps': round(nq / el, 1), 'p50_ms': round(float(np.percentile(lat_ms, 50)), 2),
+                      'p99_ms': round(float(np.percentile(lat_ms, 99)), 2),
+                      'mean_batch': round(nq / max(1, pred.stats['batches'] - b0), 1)}
+    line = json.dumps(res)
+    print(line)
+    if args.out:
+        with open(args.out, 'w') as f:
+            f.write(line + '\n')
+
+
+if __name__ == '__main__':
+    main()
