@@ -65,27 +65,45 @@ __global__ __launch_bounds__(256) void channel_stats_kernel(const bf16* __restri
   }
 }
 
+// Sum rows rl, rl+16, ... of a [R][2][C] partial table for channel c (both stats), loads issued
+// 8 rows at a time so a lane keeps 16 independent loads in flight (one latency per 8 rows).
+RK_DEV void rows_sum2(const float* __restrict__ part, int R, int C, int c, int rl, double& s, double& q) {
+  int r0 = rl;
+  for (; r0 + 16 * 7 < R; r0 += 16 * 8) {  // full groups: no per-load predicate (guide §5 trap (c))
+    float a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a[k] = part[(long long)(r0 + 16 * k) * 2 * C + c];
+      b[k] = part[(long long)(r0 + 16 * k) * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s += a[k]; q += b[k]; }
+  }
+  for (; r0 < R; r0 += 16) {
+    s += part[(long long)r0 * 2 * C + c];
+    q += part[(long long)r0 * 2 * C + C + c];
+  }
+}
+
 // ---- finalize forward stats: partial rows [R][2][C] -> mean, rstd, scale, shift (+running) ---
 __global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(const float* __restrict__ part, int R, int C,
                                                               double count, const float* gamma,
                                                               const float* beta, float eps, float* run_mean,
                                                               float* run_var, float momentum, float* mean,
                                                               float* rstd, float* scale, float* shift) {
-  __shared__ double rs[4][64], rss[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int q = threadIdx.x >> 6;
-  double s = 0.0, ss = 0.0;
-  if (c < C)
-    for (int r = q; r < R; r += 4) {
-      s += part[(long long)r * 2 * C + c];
-      ss += part[(long long)r * 2 * C + C + c];
-    }
-  rs[q][threadIdx.x & 63] = s;
-  rss[q][threadIdx.x & 63] = ss;
+  // 16 channels x 16 row lanes per block, two independent fp64 chains per lane, fixed order
+  __shared__ double rs[16][16], rss[16][16];
+  const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s0 = 0.0, q0 = 0.0;
+  if (c < C) rows_sum2(part, R, C, c, rl, s0, q0);
+  rs[rl][cl] = s0;
+  rss[rl][cl] = q0;
   __syncthreads();
-  if (q == 0 && c < C) {
-    s = rs[0][threadIdx.x] + rs[1][threadIdx.x] + rs[2][threadIdx.x] + rs[3][threadIdx.x];
-    ss = rss[0][threadIdx.x] + rss[1][threadIdx.x] + rss[2][threadIdx.x] + rss[3][threadIdx.x];
+  if (rl == 0 && c < C) {
+    double s = 0.0, ss = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { s += rs[q][cl]; ss += rss[q][cl]; }
     const double mu = s / count;
     double var = ss / count - mu * mu;
     if (var < 0.0) var = 0.0;
@@ -114,11 +132,12 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* be
 }
 
 // ---- apply: out = act(y*scale + shift) [maxpool 2x2] ----------------------------------------
+template <int POOL, int ACT>
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift, bf16* __restrict__ out,
-                                                         int N, int H, int W, int C, int pool, int act, float slope) {
+                                                         int N, int H, int W, int C, float slope) {
   const int CC = C >> 3;
-  const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
+  const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
   const long long total = (long long)N * Ho * Wo * CC;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
@@ -130,11 +149,11 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict_
     *(f32x4*)&sh[0] = *(const f32x4*)(shift + cc * 8);
     *(f32x4*)&sh[4] = *(const f32x4*)(shift + cc * 8 + 4);
     float o[8];
-    if (!pool) {
+    if constexpr (!POOL) {
       float f[8];
       unpack8(*(const uint4*)(y + pix * C + cc * 8), f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = act_f(f[e] * sc[e] + sh[e], act, slope);
+      for (int e = 0; e < 8; ++e) o[e] = act_f(f[e] * sc[e] + sh[e], ACT, slope);
     } else {
       const int wo = (int)(pix % Wo);
       const long long t = pix / Wo;
@@ -148,83 +167,111 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict_
         float f[8];
         unpack8(*(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C), f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], act_f(f[e] * sc[e] + sh[e], act, slope));
+        for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], act_f(f[e] * sc[e] + sh[e], ACT, slope));
       }
     }
     *(uint4*)(out + pix * C + cc * 8) = pack8(o);
   }
 }
 
-// dz for the 8 channels of one (pre-pool) pixel position q of an output pixel, given upstream g.
-// Pool routing: gradient goes to the first maximal element of the window (torch max_pool2d rule).
-struct BwdCtx {
-  float sc[8], sh[8];
-};
-
+// ---- backward pass 1: per-block partial (sum dz, sum dz*y) ------------------------------------
+// dz = d(act)/dz * (pool-routed upstream gradient), z = y*scale + shift recomputed from y.
+// sum dz*xhat = rstd*(sum dz*y - mean*sum dz) is formed in the finalize kernel, so this streaming
+// pass needs only scale/shift per channel (16 VGPRs) — the old form also held mean/rstd.
+// Every thread owns 8 channels (one 16-B vector) of PL pixels/windows per sweep; U independent
+// items are loaded before any is consumed so each wave keeps U*(1|4+1) 16-B loads in flight.
+template <int POOL, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
-                                                            const float* __restrict__ mean,
-                                                            const float* __restrict__ rstd, float* __restrict__ part,
-                                                            int N, int H, int W, int C, int pool, int act,
+                                                            float* __restrict__ part, int N, int H, int W, int C,
                                                             float slope) {
   extern __shared__ float red[];  // [PL][2][C]
+  constexpr int U = POOL ? 2 : 4;
   const int CC = C >> 3;
   const int CCt = CC < 256 ? CC : 256;
   const int PL = 256 / CCt;
   const int tid = threadIdx.x;
   const int pl = tid / CCt, c0 = tid % CCt;
-  const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
-  const long long Pout = (long long)N * Ho * Wo;
+  const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
+  const long long items = (long long)N * Ho * Wo;
+  const long long stride = (long long)gridDim.x * PL;
   if (pl < PL) {
     for (int cc = c0; cc < CC; cc += CCt) {
-      float sc[8], sh[8], mu[8], rs[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sc[e] = scale[cc * 8 + e]; sh[e] = shift[cc * 8 + e];
-        mu[e] = mean[cc * 8 + e]; rs[e] = rstd[cc * 8 + e];
-      }
+      float sc[8], sh[8];
+      *(f32x4*)&sc[0] = *(const f32x4*)(scale + cc * 8);
+      *(f32x4*)&sc[4] = *(const f32x4*)(scale + cc * 8 + 4);
+      *(f32x4*)&sh[0] = *(const f32x4*)(shift + cc * 8);
+      *(f32x4*)&sh[4] = *(const f32x4*)(shift + cc * 8 + 4);
       float s1[8] = {0}, s2[8] = {0};
-      for (long long pix = (long long)blockIdx.x * PL + pl; pix < Pout; pix += (long long)gridDim.x * PL) {
+      long long i = (long long)blockIdx.x * PL + pl;
+      auto base_of = [&](long long it) -> long long {
+        if (!POOL) return it * C + cc * 8;
+        const int wo = (int)(it % Wo);
+        const long long t = it / Wo;
+        const int ho = (int)(t % Ho);
+        const int n = (int)(t / Ho);
+        return (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
+      };
+      auto consume = [&](const uint4 gv, const uint4 (&yv)[POOL ? 4 : 1]) {
         float g[8];
-        unpack8(*(const uint4*)(dout + pix * C + cc * 8), g);
-        if (!pool) {
+        unpack8(gv, g);
+        if constexpr (!POOL) {
           float f[8];
-          unpack8(*(const uint4*)(y + pix * C + cc * 8), f);
+          unpack8(yv[0], f);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float dz = g[e] * act_d(f[e] * sc[e] + sh[e], act, slope);
+            const float dz = g[e] * act_d(f[e] * sc[e] + sh[e], ACT, slope);
             s1[e] += dz;
-            s2[e] += dz * (f[e] - mu[e]) * rs[e];
+            s2[e] += dz * f[e];
           }
         } else {
-          const int wo = (int)(pix % Wo);
-          const long long t = pix / Wo;
-          const int ho = (int)(t % Ho);
-          const int n = (int)(t / Ho);
-          const long long base = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
-          float f[4][8], best[8];
-          int arg[8];
+          float f[4][8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) unpack8(*(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C), f[q]);
+          for (int q = 0; q < 4; ++q) unpack8(yv[q], f[q]);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+          for (int e = 0; e < 8; ++e) {
+            float best = -INFINITY, zb = 0.f, yb = 0.f;
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float a = act_f(f[q][e] * sc[e] + sh[e], act, slope);
-              if (a > best[e]) { best[e] = a; arg[e] = q; }
+            for (int q = 0; q < 4; ++q) {  // first maximal element of the window (torch rule)
+              const float z = f[q][e] * sc[e] + sh[e];
+              const float a = act_f(z, ACT, slope);
+              if (a > best) { best = a; zb = z; yb = f[q][e]; }
             }
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float dz = (arg[e] == q) ? g[e] * act_d(f[q][e] * sc[e] + sh[e], act, slope) : 0.f;
-              s1[e] += dz;
-              s2[e] += dz * (f[q][e] - mu[e]) * rs[e];
-            }
+            const float dz = g[e] * act_d(zb, ACT, slope);
+            s1[e] += dz;
+            s2[e] += dz * yb;
+          }
         }
+      };
+      for (; i + (U - 1) * stride < items; i += U * stride) {
+        uint4 gv[U], yv[U][POOL ? 4 : 1];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long it = i + u * stride;
+          gv[u] = *(const uint4*)(dout + it * C + cc * 8);
+          const long long b = base_of(it);
+          if constexpr (!POOL) {
+            yv[u][0] = *(const uint4*)(y + b);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) yv[u][q] = *(const uint4*)(y + b + ((q >> 1) * W + (q & 1)) * (long long)C);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) consume(gv[u], yv[u]);
+      }
+      for (; i < items; i += stride) {
+        uint4 yv[POOL ? 4 : 1];
+        const uint4 gv = *(const uint4*)(dout + i * C + cc * 8);
+        const long long b = base_of(i);
+        if constexpr (!POOL) {
+          yv[0] = *(const uint4*)(y + b);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) yv[q] = *(const uint4*)(y + b + ((q >> 1) * W + (q & 1)) * (long long)C);
+        }
+        consume(gv, yv);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -241,30 +288,30 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
   }
 }
 
-// partial rows [R][2][C] of (sum dz, sum dz*xhat) -> dgamma, dbeta, coef[3][C]
+// ---- backward pass 2: partial rows [R][2][C] -> dgamma, dbeta, coef[3][C] ----------------------
+// 16 channels x 16 row lanes per block, fp64 accumulation, fixed order (deterministic).
 __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float* __restrict__ part, int R, int C,
                                                               double count, const float* gamma,
                                                               const float* mean, const float* rstd,
                                                               float* dgamma, float* dbeta, float* coef,
                                                               int accumulate) {
-  __shared__ double rs[4][64], rss[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int q = threadIdx.x >> 6;
-  double s = 0.0, ss = 0.0;
-  if (c < C)
-    for (int r = q; r < R; r += 4) {
-      s += part[(long long)r * 2 * C + c];
-      ss += part[(long long)r * 2 * C + C + c];
-    }
-  rs[q][threadIdx.x & 63] = s;
-  rss[q][threadIdx.x & 63] = ss;
+  __shared__ double r1[16][16], r2[16][16];
+  const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double a0 = 0.0, b0 = 0.0;
+  if (c < C) rows_sum2(part, R, C, c, rl, a0, b0);
+  r1[rl][cl] = a0;
+  r2[rl][cl] = b0;
   __syncthreads();
-  if (q == 0 && c < C) {
-    const double db = rs[0][threadIdx.x] + rs[1][threadIdx.x] + rs[2][threadIdx.x] + rs[3][threadIdx.x];
-    const double dg = rss[0][threadIdx.x] + rss[1][threadIdx.x] + rss[2][threadIdx.x] + rss[3][threadIdx.x];
+  if (rl == 0 && c < C) {
+    double sdz = 0.0, sdzy = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { sdz += r1[q][cl]; sdzy += r2[q][cl]; }
+    const double g = gamma ? gamma[c] : 1.0, r = rstd[c], mu = mean[c];
+    const double db = sdz;
+    const double dg = r * (sdzy - mu * sdz);  // sum dz * xhat
     if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)dg;
     if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)db;
-    const double g = gamma ? gamma[c] : 1.0, r = rstd[c], mu = mean[c];
     const double k1 = g * r;
     const double k2 = -g * r * r * dg / count;
     const double k3 = -g * r * db / count - k2 * mu;
@@ -274,61 +321,78 @@ __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float* __res
   }
 }
 
+// ---- backward pass 3: dy = k1*dz + k2*y + k3 ---------------------------------------------------
+template <int POOL, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            const float* __restrict__ coef, bf16* __restrict__ dy,
-                                                           int N, int H, int W, int C, int pool, int act, float slope) {
+                                                           int N, int H, int W, int C, float slope) {
   const int CC = C >> 3;
-  const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
+  const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
   const long long total = (long long)N * Ho * Wo * CC;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
     const int cc = (int)(idx % CC);
     const long long pix = idx / CC;
-    float sc[8], sh[8], k1[8], k2[8], k3[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = cc * 8 + e;
-      sc[e] = scale[c]; sh[e] = shift[c];
-      k1[e] = coef[c]; k2[e] = coef[C + c]; k3[e] = coef[2 * C + c];
-    }
-    float g[8];
-    unpack8(*(const uint4*)(dout + pix * C + cc * 8), g);
-    if (!pool) {
-      float f[8], o[8];
-      unpack8(*(const uint4*)(y + pix * C + cc * 8), f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float dz = g[e] * act_d(f[e] * sc[e] + sh[e], act, slope);
-        o[e] = k1[e] * dz + k2[e] * f[e] + k3[e];
-      }
-      *(uint4*)(dy + pix * C + cc * 8) = pack8(o);
+    const uint4 gv = *(const uint4*)(dout + pix * C + cc * 8);
+    long long base;
+    uint4 yv[POOL ? 4 : 1];
+    if constexpr (!POOL) {
+      base = pix * C + cc * 8;
+      yv[0] = *(const uint4*)(y + base);
     } else {
       const int wo = (int)(pix % Wo);
       const long long t = pix / Wo;
       const int ho = (int)(t % Ho);
       const int n = (int)(t / Ho);
-      const long long base = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
-      float f[4][8], best[8];
+      base = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) yv[q] = *(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C);
+    }
+    float sc[8], sh[8], k1[8], k2[8], k3[8];
+    *(f32x4*)&sc[0] = *(const f32x4*)(scale + cc * 8);
+    *(f32x4*)&sc[4] = *(const f32x4*)(scale + cc * 8 + 4);
+    *(f32x4*)&sh[0] = *(const f32x4*)(shift + cc * 8);
+    *(f32x4*)&sh[4] = *(const f32x4*)(shift + cc * 8 + 4);
+    *(f32x4*)&k1[0] = *(const f32x4*)(coef + cc * 8);
+    *(f32x4*)&k1[4] = *(const f32x4*)(coef + cc * 8 + 4);
+    *(f32x4*)&k2[0] = *(const f32x4*)(coef + C + cc * 8);
+    *(f32x4*)&k2[4] = *(const f32x4*)(coef + C + cc * 8 + 4);
+    *(f32x4*)&k3[0] = *(const f32x4*)(coef + 2 * C + cc * 8);
+    *(f32x4*)&k3[4] = *(const f32x4*)(coef + 2 * C + cc * 8 + 4);
+    float g[8];
+    unpack8(gv, g);
+    if constexpr (!POOL) {
+      float f[8], o[8];
+      unpack8(yv[0], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dz = g[e] * act_d(f[e] * sc[e] + sh[e], ACT, slope);
+        o[e] = k1[e] * dz + k2[e] * f[e] + k3[e];
+      }
+      *(uint4*)(dy + base) = pack8(o);
+    } else {
+      float f[4][8];
       int arg[8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) unpack8(*(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C), f[q]);
+      for (int q = 0; q < 4; ++q) unpack8(yv[q], f[q]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+      for (int e = 0; e < 8; ++e) {
+        float best = -INFINITY;
+        arg[e] = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float a = act_f(f[q][e] * sc[e] + sh[e], act, slope);
-          if (a > best[e]) { best[e] = a; arg[e] = q; }
+        for (int q = 0; q < 4; ++q) {
+          const float a = act_f(f[q][e] * sc[e] + sh[e], ACT, slope);
+          if (a > best) { best = a; arg[e] = q; }
         }
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float o[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float dz = (arg[e] == q) ? g[e] * act_d(f[q][e] * sc[e] + sh[e], act, slope) : 0.f;
+          const float dz = (arg[e] == q) ? g[e] * act_d(f[q][e] * sc[e] + sh[e], ACT, slope) : 0.f;
           o[e] = k1[e] * dz + k2[e] * f[q][e] + k3[e];
         }
         *(uint4*)(dy + base + ((q >> 1) * W + (q & 1)) * (long long)C) = pack8(o);
@@ -394,7 +458,7 @@ extern "C" int rk_channel_stats(const void* x, float* part, long long P, int C, 
 extern "C" int rk_bn_finalize_fwd(const float* part, int R, int C, double count, const float* gamma,
                                   const float* beta, float eps, float* run_mean, float* run_var, float momentum,
                                   float* mean, float* rstd, float* scale, float* shift, void* stream) {
-  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(rk_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, R, C,
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(rk_cdiv(C, 16)), dim3(256), 0, (hipStream_t)stream, part, R, C,
                      count, gamma, beta, eps, run_mean, run_var, momentum, mean, rstd, scale, shift);
   RK_LAUNCH_CHECK();
   return RK_OK;
@@ -408,22 +472,48 @@ extern "C" int rk_bn_eval_coeffs(int C, const float* gamma, const float* beta, c
   return RK_OK;
 }
 
+#define RK_DISPATCH_POOL_ACT(POOLV, ACTV, ...)                                          \
+  do {                                                                                 \
+    if (POOLV) {                                                                       \
+      if ((ACTV) == ACT_RELU) { constexpr int P_ = 1, A_ = ACT_RELU; __VA_ARGS__; }    \
+      else if ((ACTV) == ACT_LRELU) { constexpr int P_ = 1, A_ = ACT_LRELU; __VA_ARGS__; } \
+      else { constexpr int P_ = 1, A_ = ACT_NONE; __VA_ARGS__; }                       \
+    } else {                                                                           \
+      if ((ACTV) == ACT_RELU) { constexpr int P_ = 0, A_ = ACT_RELU; __VA_ARGS__; }    \
+      else if ((ACTV) == ACT_LRELU) { constexpr int P_ = 0, A_ = ACT_LRELU; __VA_ARGS__; } \
+      else { constexpr int P_ = 0, A_ = ACT_NONE; __VA_ARGS__; }                       \
+    }                                                                                  \
+  } while (0)
+
 extern "C" int rk_bn_act_fwd(const void* y, const float* scale, const float* shift, void* out, int N, int H, int W,
                              int C, int pool, int act, float slope, void* stream) {
   if (C % 8) return RK_EUNSUPPORTED;
   const long long work = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 8);
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)y, scale, shift, (bf16*)out, N, H, W, C, pool, act, slope);
+  const dim3 grid(grid_for(work, 256, 8192));
+  RK_DISPATCH_POOL_ACT(pool, act,
+                       hipLaunchKernelGGL((bn_act_fwd_kernel<P_, A_>), grid, dim3(256), 0, (hipStream_t)stream,
+                                          (const bf16*)y, scale, shift, (bf16*)out, N, H, W, C, slope));
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
+// Partial-row count for rk_bn_bwd_reduce: enough blocks to stream at full bandwidth (~4 per CU),
+// few enough rows that the finalize reads them in one pass.
+extern "C" int rk_bn_bwd_rows(long long items, int C) {
+  const int CC = C >> 3;
+  const int CCt = CC < 256 ? CC : 256;
+  const int PL = 256 / CCt;
+  return grid_for(items, PL * 8, 512);
+}
+
 extern "C" int rk_bn_bwd_reduce(const void* dout, const void* y, const float* scale, const float* shift,
-                                const float* mean, const float* rstd, float* part, int rows, int N, int H, int W,
-                                int C, int pool, int act, float slope, void* stream) {
+                                float* part, int rows, int N, int H, int W, int C, int pool, int act, float slope,
+                                void* stream) {
   if (C % 8 || C > 8192) return RK_EUNSUPPORTED;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(rows), dim3(256), red_lds_bytes(C), (hipStream_t)stream,
-                     (const bf16*)dout, (const bf16*)y, scale, shift, mean, rstd, part, N, H, W, C, pool, act, slope);
+  RK_DISPATCH_POOL_ACT(pool, act,
+                       hipLaunchKernelGGL((bn_bwd_reduce_kernel<P_, A_>), dim3(rows), dim3(256), red_lds_bytes(C),
+                                          (hipStream_t)stream, (const bf16*)dout, (const bf16*)y, scale, shift, part,
+                                          N, H, W, C, slope));
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -431,7 +521,7 @@ extern "C" int rk_bn_bwd_reduce(const void* dout, const void* y, const float* sc
 extern "C" int rk_bn_finalize_bwd(const float* part, int R, int C, double count, const float* gamma,
                                   const float* mean, const float* rstd, float* dgamma, float* dbeta, float* coef,
                                   int accumulate, void* stream) {
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(rk_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, R, C,
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(rk_cdiv(C, 16)), dim3(256), 0, (hipStream_t)stream, part, R, C,
                      count, gamma, mean, rstd, dgamma, dbeta, coef, accumulate);
   RK_LAUNCH_CHECK();
   return RK_OK;
@@ -442,8 +532,11 @@ extern "C" int rk_bn_bwd_apply(const void* dout, const void* y, const float* sca
                                float slope, void* stream) {
   if (C % 8) return RK_EUNSUPPORTED;
   const long long work = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 8);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)dout, (const bf16*)y, scale, shift, coef, (bf16*)dy, N, H, W, C, pool, act, slope);
+  const dim3 grid(grid_for(work, 256, 8192));
+  RK_DISPATCH_POOL_ACT(pool, act,
+                       hipLaunchKernelGGL((bn_bwd_apply_kernel<P_, A_>), grid, dim3(256), 0, (hipStream_t)stream,
+                                          (const bf16*)dout, (const bf16*)y, scale, shift, coef, (bf16*)dy, N, H, W,
+                                          C, slope));
   RK_LAUNCH_CHECK();
   if (pool && ((H & 1) || (W & 1))) {
     hipLaunchKernelGGL(bn_bwd_edge_kernel, dim3(grid_for((long long)N * H * W * (C / 8), 256, 8192)), dim3(256), 0,

@@ -143,10 +143,58 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restri
   const long long n4 = n >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     f32x4 a = ((const f32x4*)slab)[i];
-    for (int s = 1; s < S; ++s) a += ((const f32x4*)(slab + s * n))[i];
+    int s0 = 1;
+    for (; s0 + 3 < S; s0 += 4) {  // 4 independent slab loads in flight, fixed summation order
+      f32x4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = ((const f32x4*)(slab + (s0 + k) * n))[i];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a += v[k];
+    }
+    for (; s0 < S; ++s0) a += ((const f32x4*)(slab + s0 * n))[i];
     a *= scale;
     if (accumulate) a += ((const f32x4*)out)[i];
     ((f32x4*)out)[i] = a;
+  }
+}
+
+// split-K combine with the dense epilogue: out[M][N] (bf16 or fp32, row stride ldc) =
+// act(alpha * sum_s slab[s] + bias).  Lets a small-M dense layer (fc at batch 256: 32 output tiles)
+// spread K over the chip and still write the bf16 activation the next layer reads.
+__global__ __launch_bounds__(256) void reduce_slabs_epi_kernel(const float* __restrict__ slab, int S, int M, int N,
+                                                               const float* __restrict__ bias, int act, float slope,
+                                                               float alpha, bf16* __restrict__ outb,
+                                                               float* __restrict__ outf, int ldc) {
+  const long long n4 = (long long)M * N / 4;
+  const long long sn = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 a = ((const f32x4*)slab)[i];
+    int s0 = 1;
+    for (; s0 + 3 < S; s0 += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = ((const f32x4*)(slab + (s0 + k) * sn))[i];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a += v[k];
+    }
+    for (; s0 < S; ++s0) a += ((const f32x4*)(slab + s0 * sn))[i];
+    const long long e0 = i * 4;
+    const int m = (int)(e0 / N), n = (int)(e0 - (long long)m * N);
+    a *= alpha;
+    if (bias) a += *(const f32x4*)(bias + n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (act == 1) a[e] = fmaxf(a[e], 0.f);
+      else if (act == 2) a[e] = a[e] > 0.f ? a[e] : a[e] * slope;
+    }
+    if (outb) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)a[e];
+      *(bf16x4*)(outb + (long long)m * ldc + n) = o;
+    } else {
+      *(f32x4*)(outf + (long long)m * ldc + n) = a;
+    }
   }
 }
 
@@ -180,7 +228,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16* __restrict__ x,
   __shared__ float red[4][64];
   float s = 0.f;
   if (c < C)
-    for (int r = q; r < R; r += 4) s += (float)x[(long long)r * ld + c];
+  {
+    int r0 = q;
+    for (; r0 + 4 * 7 < R; r0 += 4 * 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = (float)x[(long long)(r0 + 4 * k) * ld + c];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    for (; r0 < R; r0 += 4) s += (float)x[(long long)r0 * ld + c];
+  }
   red[q][threadIdx.x & 63] = s;
   __syncthreads();
   if (q == 0 && c < C) {
@@ -290,6 +348,15 @@ extern "C" int rk_reduce_slabs(const float* slab, int S, long long n, float* out
   if (n % 4) return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(n / 4, 4096)), dim3(256), 0, (hipStream_t)stream, slab, S, n,
                      out, accumulate, scale);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_reduce_slabs_epi(const float* slab, int S, int M, int N, const float* bias, int act, float slope,
+                                   float alpha, void* outb, float* outf, int ldc, void* stream) {
+  if (N % 4 || ldc % 4) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(reduce_slabs_epi_kernel, dim3(grid_for((long long)M * N / 4, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, slab, S, M, N, bias, act, slope, alpha, (bf16*)outb, outf, ldc);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

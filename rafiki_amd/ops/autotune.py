@@ -69,6 +69,38 @@ def can_tune():
         return False
 
 
+def _time_graph(cfg, run, reps):
+    """GPU time of ``reps`` back-to-back launches, captured into a hipGraph so host launch overhead
+    (10-20 us per op from Python) does not swamp kernels that take a few microseconds."""
+    run(cfg)  # warm: first-touch allocations happen outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            run(cfg)
+    g.replay()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    g.replay()
+    g.replay()
+    e.record()
+    e.synchronize()
+    t = s.elapsed_time(e) / (2 * reps)
+    del g
+    return t
+
+
+def _time_eager(cfg, run, reps):
+    run(cfg)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        run(cfg)
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
 def tune(key, candidates, run):
     """candidates: list of config tuples; run(cfg) launches the op once.  Returns the best cfg."""
     hit = lookup(key)
@@ -77,17 +109,15 @@ def tune(key, candidates, run):
     if not can_tune():
         return candidates[0]
     best, best_t = candidates[0], float('inf')
+    use_graph = os.environ.get('RAFIKI_AUTOTUNE_GRAPH', '1') != '0'
     for cfg in candidates:
         try:
-            run(cfg)  # warm (also compiles nothing: all variants are prebuilt)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(REPS):
-                run(cfg)
-            e.record()
-            e.synchronize()
-            t = s.elapsed_time(e)
+            t = _time_graph(cfg, run, max(REPS, 5)) if use_graph else _time_eager(cfg, run, REPS)
         except Exception:
+            try:
+                torch.cuda.synchronize()
+            except Exception:
+                pass
             continue
         if t < best_t:
             best, best_t = cfg, t

@@ -94,8 +94,8 @@ def _split_candidates(M, N, K):
     kt = cdiv(K, 64)
     for t in range(4):
         for v in (0, 64):
-            for s in (1, 2, 4, 8, 16, 32, 64):
-                if s > kt or (s == 1 and kt > 64):
+            for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+                if s > kt or (s == 1 and kt > 64) or s * M * N * 4 > (256 << 20):
                     continue
                 per = cdiv(kt, s)
                 s_eff = cdiv(kt, per)
@@ -223,6 +223,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
 # ----------------------------------------------------------------------------------------- dense
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0.2, out_dtype=torch.bfloat16,
            out=None, alpha=1.0):
+    """out = act(alpha * x @ w.T + bias).  Small-M layers (few output tiles) are autotuned between the
+    direct bf16 epilogue and split-K into fp32 slabs + one fused combine/epilogue kernel."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
@@ -232,8 +234,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0
     epi = 0 if out.dtype == torch.bfloat16 else 1
     if epi == 1 and act != ACT_NONE:
         raise ValueError("fp32 dense output supports no fused activation")
-    igemm(KIND_DENSE, epi, x, w, out, M, N, K, x.stride(0), w.stride(0), out.stride(0), bias=bias, flags=flags,
-          slope=slope, alpha=alpha)
+
+    def run(cfg):
+        tile, s = cfg
+        if s == 1:
+            igemm(KIND_DENSE, epi, x, w, out, M, N, K, x.stride(0), w.stride(0), out.stride(0), bias=bias,
+                  flags=flags, slope=slope, alpha=alpha, tile=tile)
+            return
+        slab = torch.empty((s, M, N), device=x.device, dtype=torch.float32)
+        igemm(KIND_DENSE, 1, x, w, slab, M, N, K, x.stride(0), w.stride(0), N, splits=s, slab_stride=M * N,
+              tile=tile)
+        _lib.call("rk_reduce_slabs_epi", _p(slab), s, M, N, _p(bias), act, float(slope), float(alpha),
+                  _p(out) if epi == 0 else None, _p(out) if epi == 1 else None, out.stride(0), _s())
+    t0 = pick_tile(M, N)
+    cands = [(t0, 1)]
+    if N % 4 == 0 and out.stride(0) % 4 == 0 and cdiv(M, 64) * cdiv(N, 64) < NUM_CU and K >= 512:
+        cands += [c for c in _split_candidates(M, N, K) if c[1] > 1 and c[1] <= 16]
+    run(_tuned(('dn', M, N, K, epi, act, bias is not None), cands, run) if len(cands) > 1 else cands[0])
     return out
 
 
@@ -289,8 +306,9 @@ def rows_reduce(x2d: torch.Tensor, groups: int) -> torch.Tensor:
     return out
 
 
-def _shrink_rows(part: torch.Tensor, max_rows: int = 64) -> torch.Tensor:
-    """Cut a [R][2][C] partial-stat table to <= max_rows rows with a parallel pass (~32 rows/block)."""
+def _shrink_rows(part: torch.Tensor, max_rows: int = 512) -> torch.Tensor:
+    """Cut a [R][2][C] partial-stat table to <= max_rows rows with a parallel pass (~32 rows/block);
+    the finalize kernels read up to ~512 rows in one pass (16 row lanes x 2 chains)."""
     R = part.shape[0]
     if R <= max_rows:
         return part
@@ -331,15 +349,13 @@ def bn_bwd(dout, y, coeffs, gamma, *, pool=False, act=ACT_RELU, slope=0.2, dgamm
     """Backward of out = pool(act(bn(y))).  coeffs = [mean, rstd, scale, shift] rows from forward."""
     Nb, H, W, C = y.shape
     P_out = dout.numel() // C
-    rows = bn_partial_rows(P_out, C)
+    rows = _lib.lib().rk_bn_bwd_rows(P_out, C)
     part = torch.empty((rows, 2, C), device=y.device, dtype=torch.float32)
     mean, rstd, scale, shift = coeffs[0], coeffs[1], coeffs[2], coeffs[3]
     s = _s()
-    _lib.call("rk_bn_bwd_reduce", _p(dout), _p(y), _p(scale), _p(shift), _p(mean), _p(rstd), _p(part), rows, Nb, H,
-              W, C, int(pool), act, float(slope), s)
+    _lib.call("rk_bn_bwd_reduce", _p(dout), _p(y), _p(scale), _p(shift), _p(part), rows, Nb, H, W, C, int(pool), act,
+              float(slope), s)
     coef = torch.empty((3, C), device=y.device, dtype=torch.float32)
-    part = _shrink_rows(part)
-    rows = part.shape[0]
     _lib.call("rk_bn_finalize_bwd", _p(part), rows, C, float(Nb * H * W), _p(gamma), _p(mean), _p(rstd), _p(dgamma),
               _p(dbeta), _p(coef), int(accumulate), s)
     if dy is None:
