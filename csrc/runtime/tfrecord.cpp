@@ -16,6 +16,8 @@
 
 namespace {
 
+constexpr uint64_t kMaxRecord = 1ull << 30;  // a record never exceeds 1 GiB: reject hostile lengths
+
 uint32_t g_table[256];
 bool g_table_init = false;
 
@@ -172,6 +174,9 @@ uint32_t rt_masked_crc32c(const uint8_t* p, long long n) { return masked(crc32c(
 long long rt_tfrecord_info(const char* path, int verify, long long* shape) {
   FILE* f = fopen(path, "rb");
   if (!f) return -1;
+  fseek(f, 0, SEEK_END);
+  const long long fsize = ftell(f);
+  fseek(f, 0, SEEK_SET);
   long long n = 0;
   std::vector<uint8_t> buf;
   uint8_t head[12];
@@ -185,6 +190,7 @@ long long rt_tfrecord_info(const char* path, int verify, long long* shape) {
     uint32_t lcrc;
     memcpy(&lcrc, head + 8, 4);
     if (verify && lcrc != masked(crc32c(head, 8))) { rc = -3; break; }
+    if (len > kMaxRecord) { rc = -2; break; }
     const bool need = verify || (n == 0 && shape);
     if (need) {
       buf.resize(len + 4);
@@ -202,7 +208,7 @@ long long rt_tfrecord_info(const char* path, int verify, long long* shape) {
         if (!parse_image(buf.data(), buf.data() + len, s, nd, d, dl)) { rc = -4; break; }
         shape[0] = s[0]; shape[1] = s[1]; shape[2] = s[2];
       }
-    } else if (fseek(f, (long)(len + 4), SEEK_CUR) != 0) {
+    } else if ((long long)len + 4 > fsize - ftell(f) || fseek(f, (long)(len + 4), SEEK_CUR) != 0) {
       rc = -2;
       break;
     }
@@ -227,6 +233,7 @@ long long rt_tfrecord_decode_images(const char* path, uint8_t* out, long long ma
     if (got < 12) { rc = -2; break; }
     uint64_t len;
     memcpy(&len, head, 8);
+    if (len > kMaxRecord) { rc = -2; break; }
     buf.resize(len + 4);
     if (fread(buf.data(), 1, len + 4, f) != len + 4) { rc = -2; break; }
     if (verify) {

@@ -157,6 +157,7 @@ class LocalProcessManager(ContainerManager):
                     svc['restarts'] += 1
                     logger.warning('service %s exited %s; restart %d', sid, codes, svc['restarts'])
                     svc['master_port'] = free_port()
+                    svc['started_at'] = time.time()
                     svc['procs'] = [self._spawn(svc, r) for r in range(svc['world'])]
                     continue
                 for cb in self._exit_callbacks:
@@ -171,7 +172,32 @@ class LocalProcessManager(ContainerManager):
                 for p in svc['procs']:
                     if p.poll() is None:
                         self._kill(p)
+            elif self._stale(svc):
+                # a live process whose heartbeat stopped (hung collective, wedged kernel): kill the
+                # group; the non-zero exit then goes through the restart policy above
+                logger.warning('service %s heartbeat stale for > %.0fs; killing it', sid, self.heartbeat_timeout)
+                for p in svc['procs']:
+                    if p.poll() is None:
+                        self._kill(p)
             time.sleep(0.5)
+
+    heartbeat_timeout = float(os.environ.get('RAFIKI_HEARTBEAT_TIMEOUT_S', '600'))
+
+    def _stale(self, svc):
+        """True when any rank of a heartbeating service has been silent for heartbeat_timeout."""
+        from ..utils.service import last_heartbeat
+        workdir = svc['env'].get('WORKDIR_PATH') or os.environ.get('WORKDIR_PATH')
+        sid = svc['env'].get('RAFIKI_SERVICE_ID')
+        if not workdir or not sid or self.heartbeat_timeout <= 0:
+            return False
+        now = time.time()
+        started = svc.setdefault('started_at', now)
+        for r in range(svc['world']):
+            hb = last_heartbeat(workdir, sid, r)
+            ref = hb if hb is not None and hb >= started else started
+            if now - ref > self.heartbeat_timeout:
+                return True
+        return False
 
     @staticmethod
     def _kill(p, grace=10.0):

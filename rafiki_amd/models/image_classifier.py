@@ -12,6 +12,7 @@ import base64
 import io
 import math
 import pickle
+import time
 
 import numpy as np
 import torch
@@ -19,6 +20,7 @@ import torch
 from ..engine.convnet import ConvNetEngine
 from ..model import BaseModel, dataset_utils, logger
 from ..parallel.context import current as trial_context
+from ..utils import faults
 
 
 class NativeImageClassifier(BaseModel):
@@ -77,15 +79,27 @@ class NativeImageClassifier(BaseModel):
         gen.manual_seed(int(self._knobs.get('seed', 0)))
         logger.define_loss_plot()
         logger.define_plot('Train accuracy', ['train_acc'], x_axis='epoch')
+        logger.define_plot('Throughput', ['images_per_sec'], x_axis='epoch')
         sched = self._knobs.get('lr_schedule', 'cosine')
+        ctx = trial_context()
+        ck = ctx.checkpoint
         step = 0
         epoch = 0
+        if ck is not None:
+            saved = ck.load()
+            if saved is not None:
+                self._restore_ckpt(saved['state'], gen)
+                step, epoch = int(saved['state']['step']), int(saved['epoch']) + 1
+                logger.log('resumed from checkpoint after epoch {} (step {})'.format(saved['epoch'], step))
         while step < total:
             perm = torch.randperm(n, device=eng.device, generator=gen)
             eng.reset_metrics()
+            t0 = time.perf_counter()
+            done = 0
             for b in range(steps_per_epoch):
                 if step >= total:
                     break
+                faults.maybe_fail('train_step', step=step, rank=ctx.rank)
                 if hasattr(eng.opt, 'set_lr_scale') and sched == 'cosine':
                     eng.opt.set_lr_scale(0.5 * (1.0 + math.cos(math.pi * step / total)))
                 idx = perm[b * bs:(b + 1) * bs]
@@ -96,11 +110,36 @@ class NativeImageClassifier(BaseModel):
                 else:
                     eng.train_step(xb, yb)
                 step += 1
-            seen = max(1, int(eng.seen.item()))
+                done += 1
+            seen = max(1, int(eng.seen.item()))  # host sync once per epoch
+            dt = max(1e-9, time.perf_counter() - t0)
             logger.log_loss(loss=float(eng.loss_sum.item()) / seen, epoch=epoch)
             logger.log(train_acc=float(eng.correct.item()) / seen, epoch=epoch)
+            logger.log(images_per_sec=done * bs / dt, epoch=epoch)
+            if ck is not None and ck.due(epoch) and step < total:
+                ck.save(self._ckpt_state(step, gen), epoch)
+            faults.maybe_fail('crash', epoch=epoch, rank=ctx.rank)
             epoch += 1
+        if eng.device.type == 'cuda':
+            logger.log(hbm_peak_bytes=int(torch.cuda.max_memory_allocated(eng.device)))
         eng.prepare_eval()
+
+    # ----------------------------------------------------------------- checkpoint / resume
+    def _ckpt_state(self, step, gen):
+        eng = self._engine
+        opt = [t.detach().cpu().numpy().copy() for t in eng._opt_tensors()]
+        return {'step': int(step), 'master': eng.flat.master.detach().cpu().numpy().copy(),
+                'running': eng.running.detach().cpu().numpy().copy(), 'opt': opt,
+                'gen': gen.get_state().numpy().copy(), 'meta': dict(self._meta)}
+
+    def _restore_ckpt(self, st, gen):
+        eng = self._engine
+        eng.flat.master.copy_(torch.as_tensor(st['master']))
+        eng.flat.sync_bf16()
+        eng.running.copy_(torch.as_tensor(st['running']))
+        for t, v in zip(eng._opt_tensors(), st['opt']):
+            t.copy_(torch.as_tensor(v))
+        gen.set_state(torch.as_tensor(st['gen']))
 
     def _probs(self, images_uint8):
         eng = self._engine

@@ -22,6 +22,7 @@ class TrialContext:
     dist: DistInfo = field(default_factory=DistInfo)
     data_parallel: bool = False  # True: this trial is trained jointly by every rank of the group
     trial_id: Optional[str] = None
+    checkpoint: Optional[object] = None  # utils.checkpoint.TrialCheckpoint when the worker supports resume
 
     @property
     def is_gpu(self):

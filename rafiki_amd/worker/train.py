@@ -33,6 +33,7 @@ from ..model.log import logger as model_logger
 from ..model.model import load_model_class
 from ..parallel import dist as D
 from ..parallel.context import TrialContext, default_device, use_context
+from ..utils.checkpoint import TrialCheckpoint
 
 logger = logging.getLogger(__name__)
 
@@ -51,7 +52,7 @@ class _TrialLogHandler(logging.Handler):
 
 class TrainWorker:
     def __init__(self, service_id, worker_id, db=None, dist_info: D.DistInfo = None, params_dir=None,
-                 max_trial_errors=3, advisor_type=None, seed=None):
+                 max_trial_errors=3, advisor_type=None, seed=None, checkpoint_every_epochs=1):
         from ..config import get_config
         from ..db.database import Database
         self._service_id = service_id
@@ -62,6 +63,7 @@ class TrainWorker:
         self._params_dir = params_dir or os.path.join(cfg.workdir, cfg.params_dir)
         os.makedirs(self._params_dir, exist_ok=True)
         self._max_trial_errors = max_trial_errors
+        self._ckpt_every = checkpoint_every_epochs
         self._advisor_type = advisor_type
         self._seed = seed
         self._trial_id = None
@@ -88,6 +90,9 @@ class TrainWorker:
         advisor = make_advisor(knob_config, self._advisor_type, self._seed) if info.is_main else None
         device = default_device()
         errors = 0
+        # trials this worker was running when its previous incarnation died, with a checkpoint to
+        # resume from; re-run first, under their original ids and knobs
+        resume = self._orphaned_trials(sub.id) if (info.is_main and not data_parallel) else []
         while not self._stop:
             # ---- rank 0 decides this round (budget is enforced by exactly one process)
             if info.is_main:
@@ -98,14 +103,20 @@ class TrainWorker:
                 if errors >= self._max_trial_errors:
                     remaining = 0
                 n_active = min(remaining, 1 if data_parallel else info.world_size)
-                props = advisor.propose_batch(n_active) if n_active > 0 else []
+                resumed = resume[:n_active]
+                resume = resume[n_active:]
+                props = [k for _, k in resumed]
+                if n_active > len(props):
+                    props += advisor.propose_batch(n_active - len(props))
+                resume_ids = [t for t, _ in resumed] + [None] * (info.world_size - len(resumed))
                 padded = props + [props[0] if props else advisor._random_knobs()] * (info.world_size - len(props))
             else:
-                n_active, padded = 0, None
+                n_active, padded, resume_ids = 0, None, None
             n_active = self._broadcast_int(n_active)
             if n_active == 0:
                 break
             proposals = D.broadcast_proposals(info, knob_config, padded) if info.world_size > 1 else padded
+            resume_ids = self._broadcast_obj(resume_ids)
             my = 0 if data_parallel else info.rank
             active = my < n_active
             ctx = TrialContext(device=device, dist=info, data_parallel=data_parallel)
@@ -114,7 +125,8 @@ class TrainWorker:
                 record = (not data_parallel) or info.is_main
                 knobs = proposals[my]
                 t0 = time.time()
-                score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, record)
+                score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, record,
+                                            resume_id=None if data_parallel else resume_ids[my])
                 secs = time.time() - t0
             table = D.gather_floats(info, [score if ok else float('nan'), ok, secs, float(active)])
             if info.is_main:
@@ -127,6 +139,23 @@ class TrainWorker:
             logger.info('sub-train-job %s budget reached', sub.id)
             self._db.mark_sub_train_job_as_stopped(self._db.get_sub_train_job(sub.id))
 
+    def _orphaned_trials(self, sub_id):
+        out = []
+        for t in self._db.get_trials_of_sub_train_job(sub_id):
+            if t.status in (TrialStatus.STARTED, TrialStatus.RUNNING, TrialStatus.TERMINATED) and t.knobs and \
+                    t.worker_id == self._worker_id and TrialCheckpoint(self._params_dir, t.id).exists():
+                out.append((t.id, dict(t.knobs)))
+        if out:
+            logger.info('resuming %d checkpointed trial(s): %s', len(out), [t for t, _ in out])
+        return out
+
+    def _broadcast_obj(self, obj):
+        if self._dist.world_size == 1:
+            return obj
+        lst = [obj]
+        torch.distributed.broadcast_object_list(lst, src=0)
+        return lst[0]
+
     def _broadcast_int(self, v):
         info = self._dist
         if info.world_size == 1:
@@ -136,12 +165,15 @@ class TrainWorker:
         return int(t.item())
 
     # -------------------------------------------------------------------------------- trial
-    def _run_trial(self, clazz, model, sub, knobs, train_job, ctx, record):
+    def _run_trial(self, clazz, model, sub, knobs, train_job, ctx, record, resume_id=None):
         trial = None
         if record:
-            trial = self._db.create_trial(sub.id, model.id, self._worker_id)
+            trial = self._db.get_trial(resume_id) if resume_id else None
+            if trial is None:
+                trial = self._db.create_trial(sub.id, model.id, self._worker_id)
             self._trial_id = trial.id
             ctx.trial_id = trial.id
+            ctx.checkpoint = TrialCheckpoint(self._params_dir, trial.id, self._ckpt_every)
             self._db.mark_trial_as_running(trial, knobs)
         handler = _TrialLogHandler(self._db, trial.id) if record else None
         prev_logger = model_logger.get_logger()
@@ -173,12 +205,14 @@ class TrainWorker:
             if record:
                 self._db.mark_trial_as_complete(trial, score, params_path)
                 self.completed_trials.append((trial.id, score))
+                ctx.checkpoint.remove()
             return score, 1.0
         except Exception:
             logger.error('trial failed:\n%s', traceback.format_exc())
             if record and trial is not None:
                 self._db.add_trial_log(trial.id, traceback.format_exc(), 'ERROR')
                 self._db.mark_trial_as_errored(trial)
+                ctx.checkpoint.remove()
             return float('nan'), 0.0
         finally:
             if inst is not None:

@@ -1,0 +1,24 @@
+"""Host C++ runtime under AddressSanitizer + UBSan: build csrc/tests/test_runtime.cpp
+(which includes the runtime sources) with -fsanitize=address,undefined and run its round-trip and
+fuzz checks.  CPU only; sanitizers are applied to host code only."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason='g++ not available')
+def test_runtime_asan_ubsan(tmp_path):
+    exe = str(tmp_path / 'rt_test')
+    src = os.path.join(ROOT, 'csrc', 'tests', 'test_runtime.cpp')
+    subprocess.run(['g++', '-std=c++17', '-O1', '-g', '-fsanitize=address,undefined', '-fno-omit-frame-pointer',
+                    '-fno-sanitize-recover=all', src, '-o', exe], check=True, capture_output=True, timeout=300)
+    # verify_asan_link_order=0: tolerate libraries the environment preloads ahead of the ASan runtime
+    env = dict(os.environ, ASAN_OPTIONS='detect_leaks=1:abort_on_error=1:verify_asan_link_order=0',
+               UBSAN_OPTIONS='print_stacktrace=1')
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert 'runtime tests ok' in r.stdout
