@@ -61,6 +61,9 @@ def create_app(admin: Admin = None) -> Flask:
     def index():
         return 'Rafiki Admin is up.'
 
+    from ..utils.metrics import admin_gauges, instrument
+    instrument(app, 'admin', admin_gauges(lambda: get_admin().db))
+
     # ------------------------------------------------------------------------------ users
     @app.route('/users', methods=['POST'])
     @auth([UserType.ADMIN])

@@ -39,6 +39,9 @@ def create_app(predictor):
         body = request.get_json(silent=True) or {}
         return jsonify({'predictions': predictor.predict(body['queries'])})
 
+    from ..utils.metrics import instrument, predictor_gauges
+    instrument(app, 'predictor', predictor_gauges(predictor))
+
     @app.route('/stats', methods=['GET'])
     def stats():
         return jsonify({**predictor.stats, 'models': [n for n, _ in predictor.models],

@@ -159,3 +159,12 @@ def test_web_ui_served(stack):
     assert r.status_code == 200 and r.headers['Content-Type'].startswith('text/html')
     for frag in ('/tokens', '/train_jobs', '/trials/', 'plotSvg', 'x_axis'):
         assert frag in r.text
+
+
+def test_metrics_endpoint(stack):
+    import requests
+    client(stack).get_users()
+    r = requests.get('http://127.0.0.1:{}/metrics'.format(stack['port']), timeout=10)
+    assert r.status_code == 200
+    assert 'rafiki_http_requests_total{method="GET",route="/users",service="admin",status="200"}' in r.text
+    assert 'rafiki_train_jobs' in r.text and 'rafiki_http_request_seconds_bucket' in r.text

@@ -147,3 +147,16 @@ def test_ensemble_predictions():
     assert np.allclose(out, [[0.4, 0.6], [0.5, 0.5]])
     assert ensemble_predictions([[[1, 2]], [[3, 4]]], TaskType.POS_TAGGING) == [[1, 2]]
     assert ensemble_predictions([], TaskType.IMAGE_CLASSIFICATION) == []
+
+
+def test_graph_utils():
+    from types import SimpleNamespace as NS
+    from rafiki_amd.utils import graph as G
+    subs = [NS(id='a', model_id='m1'), NS(id='b', model_id='m2'), NS(id='e', model_id='ens')]
+    adj = G.build_dag(subs, NS(id='ens'))
+    assert adj == {'a': ['e'], 'b': ['e'], 'e': []}
+    assert G.topological_order(adj) == ['a', 'b', 'e'] and G.validate_dag(adj)
+    assert G.get_parents('e', adj) == ['a', 'b'] and G.get_children('a', adj) == ['e']
+    assert G.get_nodes_with_zero_incoming_degrees(adj) == ['a', 'b']
+    assert not G.validate_dag({'x': ['y'], 'y': ['x']})
+    assert G.build_dag(subs, None) == {'a': [], 'b': [], 'e': []}
