@@ -2,7 +2,7 @@
 
 * ``csrc/kernels/*.hip``  -> ``rafiki_amd/_native/librafiki_kernels.so``  (hipcc, gfx950 only)
 * ``csrc/runtime/*.cpp``  -> ``rafiki_amd/_native/librafiki_runtime.so``  (g++, host-only C++
-  runtime: dynamic batcher queue, GPU ledger, param arena bookkeeping)
+  runtime: TFRecord reader/CRC32C, shared-memory message queues for inference workers)
 
 Kernels are plain ``extern "C"`` launchers taking raw device pointers and the HIP stream, bound
 from Python with ``ctypes`` (``rafiki_amd/ops/_lib.py``).  That keeps each kernel TU a few seconds
@@ -82,7 +82,7 @@ def build_runtime(verbose: bool = False) -> Path | None:
     headers = sorted(RUNTIME_SRC.glob("*.h"))
     if _stale(RUNTIME_LIB, [*srcs, *headers]):
         tmp = RUNTIME_LIB.with_suffix(".so.tmp")
-        _run([CXX, *CXX_FLAGS, "-shared", *srcs, "-o", tmp], verbose)
+        _run([CXX, *CXX_FLAGS, "-shared", *srcs, "-o", tmp, "-lrt", "-lpthread"], verbose)
         os.replace(tmp, RUNTIME_LIB)
     return RUNTIME_LIB
 

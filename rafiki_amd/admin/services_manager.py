@@ -49,6 +49,8 @@ class ServicesManager:
         if not best_trials:
             self._db.mark_inference_job_as_errored(inference_job)
             raise ServiceDeploymentError('no completed trials to serve')
+        if os.environ.get('RAFIKI_INFERENCE_MODE', 'local') == 'workers':
+            return self._create_inference_worker_services(inference_job, best_trials)
         try:
             workers = []
             for trial in best_trials:  # rows the predictor reads at start-up exist before it launches
@@ -73,13 +75,43 @@ class ServicesManager:
             self._db.mark_inference_job_as_errored(inference_job)
             raise
 
+    def _create_inference_worker_services(self, inference_job, best_trials):
+        """``workers`` mode: one InferenceWorker process per trial (its own GPU when free), then a
+        predictor that fans out through the shared-memory Cache (reference services_manager.py:53-87)."""
+        try:
+            workers = []
+            for trial in best_trials:
+                gpus = 1 if self._gpus_available() else 0
+                svc = self._create_service(
+                    ServiceType.INFERENCE, WORKER_IMAGE, args=['-m', 'rafiki_amd.worker'],
+                    environment_vars={'RAFIKI_SERVICE_TYPE': ServiceType.INFERENCE}, gpus=gpus,
+                    before_launch=lambda s, t=trial: self._db.create_inference_job_worker(s.id, inference_job.id,
+                                                                                         t.id))
+                workers.append(svc)
+            self._wait_until_services_running(workers)
+            predictor = self._create_service(
+                ServiceType.PREDICT, PREDICTOR_IMAGE, args=['-m', 'rafiki_amd.predictor.server'],
+                environment_vars={'RAFIKI_INFERENCE_JOB_ID': inference_job.id, 'RAFIKI_INFERENCE_MODE': 'workers'},
+                container_port=self._cfg.predictor_port, gpus=0,
+                before_launch=lambda s: self._db.update_inference_job(inference_job, predictor_service_id=s.id))
+            self._wait_until_services_running([predictor])
+            self._db.mark_inference_job_as_running(inference_job)
+            return inference_job, self._db.get_service(predictor.id)
+        except Exception:
+            self._db.mark_inference_job_as_errored(inference_job)
+            raise
+
     def stop_inference_services(self, inference_job_id):
         inference_job = self._db.get_inference_job(inference_job_id)
         if inference_job.predictor_service_id:
             self._stop_service(self._db.get_service(inference_job.predictor_service_id))
         for w in self._db.get_workers_of_inference_job(inference_job_id):
             svc = self._db.get_service(w.service_id)
-            if svc is not None and svc.status != ServiceStatus.STOPPED:
+            if svc is not None and svc.container_service_id and svc.container_service_id != \
+                    (self._db.get_service(inference_job.predictor_service_id).container_service_id
+                     if inference_job.predictor_service_id else None):
+                self._stop_service(svc)  # a real worker process (``workers`` mode)
+            elif svc is not None and svc.status != ServiceStatus.STOPPED:
                 self._db.mark_service_as_stopped(svc)
         return self._db.mark_inference_job_as_stopped(inference_job)
 

@@ -183,6 +183,10 @@ class ModelDatasetUtils:
             size = int(q.get('size', image_size or 32))
             imgs, labels = synthetic_images(int(q.get('n', 1024)), size=size, channels=int(q.get('channels', 1)),
                                             classes=int(q.get('classes', 10)), seed=int(q.get('seed', 0)))
+            if image_size is not None:  # same contract as a zip: decoded images come back at image_size
+                want = (image_size, image_size) if isinstance(image_size, int) else tuple(image_size)
+                if imgs.shape[1:3] != tuple(want):
+                    imgs = self.resize_as_images(imgs, want)
             return ImageFilesDataset(dataset_uri, image_size, images=imgs, labels=labels)
         return ImageFilesDataset(self.download_dataset_from_uri(dataset_uri), image_size)
 

@@ -72,6 +72,31 @@ class ParamCache:
         return list(self._order)
 
 
+class RemoteWorkerModel:
+    """Proxy for a model served by an ``InferenceWorker`` process (``workers`` serving mode)."""
+
+    def __init__(self, worker_id, cache):
+        self.worker_id = worker_id
+        self.cache = cache
+
+    def submit(self, ids, queries):
+        self.cache.add_queries_of_worker(self.worker_id, list(zip(ids, queries)))
+
+    def collect(self, ids, deadline):
+        from ..cache.cache import MISSING
+        out = []
+        for i in ids:
+            while True:
+                left_ms = int((deadline - time.perf_counter()) * 1000)
+                p = self.cache.pop_prediction_of_worker(self.worker_id, i, timeout_ms=max(0, min(left_ms, 200)))
+                if p is not MISSING or left_ms <= 0:
+                    break
+            if p is MISSING:
+                raise TimeoutError('worker {} did not answer in time'.format(self.worker_id))
+            out.append(p)
+        return out
+
+
 class Predictor:
     def __init__(self, models: Optional[List[Tuple[str, object]]] = None, task=TaskType.IMAGE_CLASSIFICATION,
                  max_batch: int = 256, max_wait_ms: float = 2.0, timeout_s: float = None,
@@ -94,6 +119,8 @@ class Predictor:
     # ------------------------------------------------------------------ loading from the DB
     @classmethod
     def from_inference_job(cls, inference_job_id, db=None, **kw):
+        if os.environ.get('RAFIKI_INFERENCE_MODE', 'local') == 'workers':
+            return cls.from_inference_workers(inference_job_id, db=db, **kw)
         from ..db.database import Database
         from ..model.model import load_model_class
         db = db or Database()
@@ -111,6 +138,18 @@ class Predictor:
             models.append((trial.id, inst))
         return cls(models, task=tj.task, **kw)
 
+    @classmethod
+    def from_inference_workers(cls, inference_job_id, db=None, cache=None, **kw):
+        from ..cache import Cache
+        from ..db.database import Database
+        db = db or Database()
+        ij = db.get_inference_job(inference_job_id)
+        tj = db.get_train_job(ij.train_job_id)
+        cache = cache or Cache()
+        models = [(w.trial_id, RemoteWorkerModel(w.service_id, cache))
+                  for w in db.get_workers_of_inference_job(inference_job_id)]
+        return cls(models, task=tj.task, **kw)
+
     # ------------------------------------------------------------------------- inference
     def _fast_path(self):
         return self.task == TaskType.IMAGE_CLASSIFICATION and self.models and all(
@@ -120,6 +159,8 @@ class Predictor:
         """Synchronous batched prediction over the whole ensemble."""
         if not queries:
             return []
+        if self.models and all(isinstance(m, RemoteWorkerModel) for _, m in self.models):
+            return self._predict_remote(queries)
         if self._fast_path():
             try:
                 return self._predict_fast(queries)
@@ -133,6 +174,29 @@ class Predictor:
             except Exception:
                 self.stats['errors'] += 1
                 logger.error('model %s failed:\n%s', name, traceback.format_exc())
+        if not preds:
+            raise RuntimeError('every model of the ensemble failed')
+        return ensemble_predictions(preds, self.task)
+
+    def _predict_remote(self, queries):
+        """Fan the batch out to every worker first, then gather (workers run concurrently); a worker
+        that misses the deadline is dropped from this batch's ensemble (partial-ensemble fallback)."""
+        import uuid
+        base = uuid.uuid4().hex[:12]
+        ids = ['{}-{}'.format(base, i) for i in range(len(queries))]
+        for _, m in self.models:
+            m.submit(ids, queries)
+        deadline = time.perf_counter() + self.timeout_s
+        preds = []
+        for name, m in self.models:
+            try:
+                p = m.collect(ids, deadline)
+                if any(x is None for x in p):
+                    raise RuntimeError('worker {} failed to predict'.format(name))
+                preds.append(p)
+            except Exception:
+                self.stats['errors'] += 1
+                logger.error('remote model %s dropped from ensemble:\n%s', name, traceback.format_exc())
         if not preds:
             raise RuntimeError('every model of the ensemble failed')
         return ensemble_predictions(preds, self.task)

@@ -21,6 +21,12 @@ _SIGS = {
     "rt_tfrecord_decode_images": (ctypes.c_longlong,
                                   [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
                                    ctypes.c_int]),
+    "rt_mq_open": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_int]),
+    "rt_mq_close": (None, [ctypes.c_void_p]),
+    "rt_mq_unlink": (ctypes.c_int, [ctypes.c_char_p]),
+    "rt_mq_push": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_longlong, ctypes.c_int]),
+    "rt_mq_pop": (ctypes.c_longlong, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int]),
+    "rt_mq_size": (ctypes.c_longlong, [ctypes.c_void_p]),
 }
 
 

@@ -34,6 +34,10 @@ def main():
                        workdir=cfg.workdir)
         finally:
             D.destroy(info)
+    elif service_type == ServiceType.INFERENCE:
+        from .inference import InferenceWorker
+        worker = InferenceWorker(service_id, db=db)
+        run_worker(db, lambda sid, cid: worker.start(), worker.stop, service_id=service_id, workdir=cfg.workdir)
     else:
         raise SystemExit('unknown service type {}'.format(service_type))
 
