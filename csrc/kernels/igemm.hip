@@ -23,6 +23,7 @@
 // (pg_gans.py:998-1029).  Numerics: fp32 accumulate of bf16 products (tests compare against a
 // PyTorch fp32 reference of the same op).
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -38,7 +39,7 @@ enum OpMode {
   OP_CONVUP_KIN = 6,  // NHWC gather from a 2x nearest-upscaled input (fused upscale2d + conv3x3)
 };
 enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
-enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16,
+enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16, FLAG_NOFAST = 64,
              FLAG_LRELU = 32 };
 
 struct IgemmParams {
@@ -320,6 +321,12 @@ struct DmaOperand {
   unsigned vmask[NI];  // K-inner conv: tap mask; dense: row-valid; K-outer: column-valid
   int sub[NI];         // K-inner: logical chunk c; K-outer: k-row within the tile
   int dh[NI], dw[NI];  // K-outer conv: tap shift of this lane's column
+  // Fast path (uniform flag): when a 64-wide K-tile never straddles a tap / image-row boundary the
+  // tile-dependent part of every address is wave-uniform (scalar ALU), so each DMA costs ~3 VALU
+  // instead of ~15 (integer multiplies, branches).  fbase[q] folds the lane-constant part in.
+  bool fast;
+  unsigned fbase[NI];
+  int fh[NI];          // CONV_KOUT: (k-row's image-row offset + tap dh) of this lane
 
   RK_DEV void init(const IgemmParams& p, const bf16* ptr, unsigned long long bytes, int ld, int tile0, int extent,
                    int wid, int lane) {
@@ -374,6 +381,34 @@ struct DmaOperand {
         vmask[q] = ok ? 1u : 0u;
       }
     }
+    // ---- fast-path preconditions (uniform) and lane constants
+    const bool k64 = (p.K & (BK - 1)) == 0 && !(p.flags & FLAG_NOFAST);
+    if constexpr (MODE == OP_DENSE_KIN) {
+      fast = k64;
+#pragma unroll
+      for (int q = 0; q < NI; ++q) fbase[q] = vmask[q] ? base[q] : OOB;
+    } else if constexpr (MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN) {
+      fast = p.log2C >= 6 && !(p.flags & FLAG_NOFAST);  // C % 64 == 0: one tap per K-tile
+#pragma unroll
+      for (int q = 0; q < NI; ++q) fbase[q] = base[q] + (unsigned)sub[q] * 16u;
+    } else if constexpr (MODE == OP_DENSE_KOUT) {
+      fast = k64;
+#pragma unroll
+      for (int q = 0; q < NI; ++q) fbase[q] = vmask[q] ? base[q] + (unsigned)sub[q] * (unsigned)ld * 2u : OOB;
+    } else if constexpr (MODE == OP_WTAP_KOUT) {
+      fast = k64 && p.log2Cb >= 6;
+#pragma unroll
+      for (int q = 0; q < NI; ++q) fbase[q] = vmask[q] ? base[q] + (unsigned)sub[q] * (unsigned)ld * 2u : OOB;
+    } else {  // OP_CONV_KOUT: pixel rows; a 64-pixel tile = 64/W whole image rows of one image
+      fast = k64 && p.log2W >= 0 && p.log2H >= 0 && p.W <= BK && p.log2C >= 0 && (p.H * p.W) % BK == 0;
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const int wl = sub[q] & (p.W - 1);
+        const bool wok = (unsigned)(wl + dw[q]) < (unsigned)p.W;
+        fh[q] = (sub[q] >> (p.log2W > 0 ? p.log2W : 0)) + dh[q];
+        fbase[q] = (vmask[q] && wok) ? base[q] + ((unsigned)(sub[q] + dh[q] * p.W + dw[q]) << p.log2C) * 2u : OOB;
+      }
+    }
   }
 
   // byte offset (or OOB) of this lane's chunk for instruction q of K-tile kt
@@ -410,6 +445,46 @@ struct DmaOperand {
   }
 
   RK_DEV void issue(const IgemmParams& p, char* lds_tile, int kt, int K, int ld, int wid) const {
+    if (fast) {
+      unsigned off[NI];
+      const int k0 = kt * BK;  // wave-uniform below: scalar ALU
+      if constexpr (MODE == OP_DENSE_KIN) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) off[q] = fbase[q] == OOB ? OOB : fbase[q] + (unsigned)k0 * 2u;
+      } else if constexpr (MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN) {
+        const int tap = k0 >> p.log2C, ci0 = k0 & (p.C - 1);
+        int dy = 0, dx = 0;
+        if (p.taps == 9) {
+          dy = tap_dy(tap);
+          dx = tap_dx(tap);
+          if constexpr (MODE == OP_CONVT_KIN) { dy = -dy; dx = -dx; }
+        }
+        const int delta = ((((dy * p.W + dx) << p.log2C) + ci0) * 2);
+#pragma unroll
+        for (int q = 0; q < NI; ++q) off[q] = ((vmask[q] >> tap) & 1u) ? (unsigned)((int)fbase[q] + delta) : OOB;
+      } else if constexpr (MODE == OP_DENSE_KOUT) {
+        const unsigned delta = (unsigned)k0 * (unsigned)ld * 2u;
+#pragma unroll
+        for (int q = 0; q < NI; ++q) off[q] = fbase[q] == OOB ? OOB : fbase[q] + delta;
+      } else if constexpr (MODE == OP_WTAP_KOUT) {
+        const int tap = k0 >> p.log2Cb, co0 = k0 & ((1 << p.log2Cb) - 1);
+        const unsigned delta = ((unsigned)co0 * (unsigned)ld + (unsigned)tap * (unsigned)p.N) * 2u;
+#pragma unroll
+        for (int q = 0; q < NI; ++q) off[q] = fbase[q] == OOB ? OOB : fbase[q] + delta;
+      } else {  // OP_CONV_KOUT
+        const int h0 = (k0 >> p.log2W) & (p.H - 1);
+        const unsigned delta = ((unsigned)k0 << p.log2C) * 2u;
+#pragma unroll
+        for (int q = 0; q < NI; ++q)
+          off[q] = (fbase[q] != OOB && (unsigned)(h0 + fh[q]) < (unsigned)p.H) ? fbase[q] + delta : OOB;
+      }
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        char* dst = lds_tile + (wid * NI + q) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)dst, 16, (int)off[q], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       char* dst = lds_tile + (wid * NI + q) * 1024;
@@ -855,6 +930,8 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
   p.ktPer = rk_cdiv(kTiles, splits);
   p.slabStride = slabStride;
   p.flags = flags; p.alpha = alpha; p.slope = slope;
+  static const bool nofast = getenv("RAFIKI_IGEMM_NOFAST") != nullptr;  // A/B switch for the DMA fast path
+  if (nofast) p.flags |= FLAG_NOFAST;
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   hipStream_t st = (hipStream_t)stream;
   const bool conv = kind <= 2 || kind == 6;

@@ -27,16 +27,9 @@ B = args.batch
 
 
 def timeit(fn):
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(args.reps):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / args.reps * 1e3  # us
+    """GPU time per launch, measured on a captured hipGraph (no host launch overhead)."""
+    from rafiki_amd.ops import autotune
+    return autotune._time_graph(None, lambda _: fn(), args.reps) * 1e3  # us
 
 
 best_total = 0.0
