@@ -88,15 +88,17 @@ def main():
 
     use_graph = not args.no_graph
     if use_graph:
-        eng.capture(B)
+        # one hipGraph per step: minibatch gather (device-side step counter) + fwd + bwd + optimizer
+        eng.capture_scheduled(data, y_all, total_steps, B)
+        eng.set_schedule(idx)
 
     def step(i):
+        if use_graph:
+            eng.replay()
+            return
         torch.index_select(data, 0, idx[i], out=xb)
         torch.index_select(y_all, 0, idx[i], out=yb)
-        if use_graph:
-            eng.step_graph(xb, yb)
-        else:
-            eng.train_step(xb, yb)
+        eng.train_step(xb, yb)
 
     for i in range(args.warmup):
         step(i)

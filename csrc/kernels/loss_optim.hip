@@ -198,6 +198,26 @@ __global__ __launch_bounds__(256) void reduce_slabs_epi_kernel(const float* __re
   }
 }
 
+// Minibatch gather inside the captured training graph: out_x[b] = data[idx[step][b]] (rows of
+// row_vec 16-B vectors), out_y[b] = labels[idx[step][b]], where step = *counter is read on the
+// device — the replayed graph walks a precomputed index schedule with no per-step host copies.
+__global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restrict__ data, long long row_vec,
+                                                           const int* __restrict__ labels,
+                                                           const long long* __restrict__ sched,
+                                                           const int* __restrict__ counter, int B,
+                                                           uint4* __restrict__ out, int* __restrict__ out_y) {
+  const long long step = *counter;
+  const long long total = (long long)B * row_vec;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / row_vec);
+    const long long c = i - (long long)b * row_vec;
+    const long long src = sched[step * B + b];
+    out[i] = data[src * row_vec + c];
+    if (c == 0 && out_y) out_y[b] = labels[src];
+  }
+}
+
 // Stage-1 parallel row reduction: in [R][W] fp32 -> out [G][W], block (x, g) sums its slice of rows
 // for 256 consecutive columns (coalesced).  Turns the serial "sum thousands of partial rows" tails
 // of BN finalize / split-K combine into a chip-wide pass; stage 2 then reads only G rows.
@@ -357,6 +377,16 @@ extern "C" int rk_reduce_slabs_epi(const float* slab, int S, int M, int N, const
   if (N % 4 || ldc % 4) return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(reduce_slabs_epi_kernel, dim3(grid_for((long long)M * N / 4, 4096)), dim3(256), 0,
                      (hipStream_t)stream, slab, S, M, N, bias, act, slope, alpha, (bf16*)outb, outf, ldc);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_gather_batch(const void* data, long long row_bytes, const int* labels, const long long* sched,
+                               const int* counter, int B, void* out, int* out_y, void* stream) {
+  if (row_bytes % 16) return RK_EUNSUPPORTED;
+  const long long rv = row_bytes / 16;
+  hipLaunchKernelGGL(gather_batch_kernel, dim3(grid_for((long long)B * rv, 2048)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)data, rv, labels, sched, counter, B, (uint4*)out, out_y);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

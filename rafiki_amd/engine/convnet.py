@@ -391,6 +391,53 @@ class ConvNetEngine:
         self._graph, self._graph_batch = g, batch_size
         return g
 
+    def capture_scheduled(self, data, labels, max_steps: int, batch_size: int, warmup: int = 2):
+        """Capture gather + train step + counter increment into ONE hipGraph: every replay trains on
+        rows ``sched[ctr]`` of the device-resident dataset and advances ``ctr`` on the device, so a
+        training loop is just ``set_schedule(idx); for _: replay()`` — no per-step copies."""
+        if self.device.type != 'cuda':
+            raise RuntimeError('capture_scheduled needs a GPU')
+        self._data, self._labels = data, labels
+        self._sched = torch.zeros((max_steps, batch_size), dtype=torch.int64, device=self.device)
+        self._ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._static_x = torch.zeros(self.input_shape(batch_size), dtype=torch.bfloat16, device=self.device)
+        self._static_y = torch.zeros((batch_size,), dtype=torch.int32, device=self.device)
+
+        def body():
+            F.gather_batch(self._data, self._labels, self._sched, self._ctr, self._static_x, self._static_y)
+            self._train_step_gpu(self._static_x, self._static_y)
+            F.add_int_(self._ctr, 1)
+
+        snap = [self.flat.master.clone(), self.running.clone()]
+        opt_state = [t.clone() for t in self._opt_tensors()]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                body()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        torch.cuda.synchronize()
+        self.flat.master.copy_(snap[0])
+        self.flat.sync_bf16()
+        self.running.copy_(snap[1])
+        for t, v in zip(self._opt_tensors(), opt_state):
+            t.copy_(v)
+        self._ctr.zero_()
+        self.reset_metrics()
+        self._sched_graph = g
+        return g
+
+    def set_schedule(self, idx, start: int = 0):
+        """idx: [steps, B] row indices (device) -> schedule buffer; the next replay uses row ``start``."""
+        self._sched[:idx.shape[0]].copy_(idx)
+        self._ctr.fill_(start)
+
+    def replay(self):
+        self._sched_graph.replay()
+
     def _opt_tensors(self):
         o = self.opt
         if isinstance(o, FlatAdam):

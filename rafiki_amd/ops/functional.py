@@ -430,6 +430,15 @@ def ensemble_mean(probs, weights=None, out=None):
     return out
 
 
+def gather_batch(data, labels, sched, counter, out_x, out_y):
+    """out_x[b] = data[sched[*counter][b]], out_y likewise — device-side step counter (graph-safe)."""
+    B = out_x.shape[0]
+    row_bytes = data[0].numel() * data.element_size()
+    _lib.call("rk_gather_batch", _p(data), row_bytes, _p(labels), _p(sched), _p(counter), B, _p(out_x), _p(out_y),
+              _s())
+    return out_x
+
+
 def cast_bf16(src, dst):
     _lib.call("rk_cast_f32_bf16", _p(src), _p(dst), src.numel(), _s())
     return dst
