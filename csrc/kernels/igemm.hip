@@ -555,22 +555,36 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
     }
   };
 
-  if (kt0 < kt1) issue(kt0, 0);
-  if (kt0 + 1 < kt1) issue(kt0 + 1, 1);
-  int stage = 0;
-  for (int kt = kt0; kt < kt1; ++kt) {
-    if (kt + 1 < kt1) wait_vmcnt<L>();   // this wave's DMAs of tile kt landed (kt+1 may fly)
-    else wait_vmcnt<0>();
-    raw_barrier();                       // ... and every other wave's
-    if constexpr (NST == 3) {
-      if (kt + 2 < kt1) issue(kt + 2, stage == 0 ? 2 : stage - 1);  // stage of tile kt-1: free
+  if constexpr (NST == 2) {
+    if (kt0 < kt1) issue(kt0, 0);
+    if (kt0 + 1 < kt1) issue(kt0 + 1, 1);
+    int stage = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      if (kt + 1 < kt1) wait_vmcnt<L>();   // this wave's DMAs of tile kt landed (kt+1 may fly)
+      else wait_vmcnt<0>();
+      raw_barrier();                       // ... and every other wave's
       compute(smem + stage * SB);
-      stage = stage == 2 ? 0 : stage + 1;
-    } else {
-      compute(smem + stage * SB);
-      raw_barrier();                     // everyone is done reading this stage
+      raw_barrier();                       // everyone is done reading this stage
       if (kt + 2 < kt1) issue(kt + 2, stage);
       stage ^= 1;
+    }
+  } else {
+    // NST-stage ring, NST-1 tiles in flight: at tile kt, wait for it, one barrier, then refill the
+    // stage tile kt-1 used (every wave is past computing it) with tile kt+NST-1, then compute kt
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+      if (kt0 + t < kt1) issue(kt0 + t, t);
+    int stage = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int ahead = kt1 - 1 - kt;      // tiles after kt already issued (capped below)
+      if (ahead >= NST - 2) wait_vmcnt<L * (NST - 2)>();
+      else if (NST >= 4 && ahead == 2) wait_vmcnt<L * 2>();
+      else if (ahead == 1) wait_vmcnt<L>();
+      else wait_vmcnt<0>();
+      raw_barrier();
+      if (kt + NST - 1 < kt1) issue(kt + NST - 1, stage == 0 ? NST - 1 : stage - 1);
+      compute(smem + stage * SB);
+      stage = stage == NST - 1 ? 0 : stage + 1;
     }
   }
   wait_vmcnt<0>();
@@ -877,7 +891,9 @@ template <int BM, int BN, int AM, int BMODE, int EPI>
 int launch_tile(const IgemmParams& p, int splits, int pf, hipStream_t st) {
   const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
   dim3 grid(tiles, 1, splits);
-  if (pf == 3)
+  if (pf == 5)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, AM, BMODE, EPI, 4>), grid, dim3(256), 0, st, p);
+  else if (pf == 3)
     hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, AM, BMODE, EPI, 3>), grid, dim3(256), 0, st, p);
   else if (pf == 4)
     hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, AM, BMODE, EPI, 2>), grid, dim3(256), 0, st, p);
@@ -892,8 +908,8 @@ int launch_tile(const IgemmParams& p, int splits, int pf, hipStream_t st) {
 template <int AM, int BMODE, int EPI>
 int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
   // tile code: bits 0-3 tile shape; 16 = register ring (2 tiles in flight); 32 = LDS-DMA 3-stage
-  // ring; 64 = LDS-DMA 2-stage
-  const int pf = (tile & 32) ? 3 : (tile & 64) ? 4 : (tile & 16) ? 2 : 1;
+  // ring; 64 = LDS-DMA 2-stage; 128 = LDS-DMA 4-stage
+  const int pf = (tile & 128) ? 5 : (tile & 32) ? 3 : (tile & 64) ? 4 : (tile & 16) ? 2 : 1;
   switch (tile & 15) {
     case 0: return launch_tile<128, 128, AM, BMODE, EPI>(p, splits, pf, st);
     case 1: return launch_tile<128, 64, AM, BMODE, EPI>(p, splits, pf, st);

@@ -25,7 +25,7 @@ ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
 NUM_CU = 256
 # Kernel variant bits OR'ed into the tile code (see rk_igemm): 0 register-staged, 16 register ring,
-# 32 LDS-DMA 3-stage ring, 64 LDS-DMA 2-stage.
+# 32 LDS-DMA 3-stage ring, 64 LDS-DMA 2-stage, 128 LDS-DMA 4-stage.
 VARIANT = int(os.environ.get('RAFIKI_IGEMM_VARIANT', '0'))
 
 
@@ -80,7 +80,7 @@ def _tile_candidates(M, N, fixed_bm=None):
         shapes = list(range(4))
     out = [(first,)]
     for t in shapes:
-        for v in (0, 64, 32):
+        for v in (0, 64, 32, 128):
             c = (t | v,)
             if c not in out:
                 out.append(c)
@@ -93,7 +93,7 @@ def _split_candidates(M, N, K):
     out = [first]
     kt = cdiv(K, 64)
     for t in range(4):
-        for v in (0, 64):
+        for v in (0, 64, 128):
             for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
                 if s > kt or (s == 1 and kt > 64) or s * M * N * 4 > (256 << 20):
                     continue
