@@ -49,6 +49,7 @@ def main():
     from rafiki_amd.engine.convnet import ConvNetEngine
     from rafiki_amd.model.dataset import synthetic_images
     from rafiki_amd.model.knob import FixedKnob, FloatKnob
+    from rafiki_amd.ops import autotune
     from rafiki_amd.ops import functional as F
     from rafiki_amd.parallel import dist as D
 
@@ -152,6 +153,7 @@ def main():
             'trials_per_hour': round(trials_per_hour, 2),
             'trial_definition': '{} epochs x {} images per trial'.format(args.trial_epochs, args.dataset_size),
             'model_tflops': round(tflops, 2),
+            'autotune': dict(autotune.stats),
             'train_loss': round(loss, 4),
             'train_acc': round(acc, 4),
             'knobs_rank0': proposals[0],

@@ -18,6 +18,7 @@ import torch
 _lock = threading.Lock()
 _cache = {}
 _loaded = False
+stats = {'tuned': 0, 'seconds': 0.0, 'candidates': 0}
 ENABLED = os.environ.get('RAFIKI_AUTOTUNE', '1') != '0'
 REPS = int(os.environ.get('RAFIKI_AUTOTUNE_REPS', '3'))
 
@@ -108,6 +109,8 @@ def tune(key, candidates, run):
         return hit
     if not can_tune():
         return candidates[0]
+    import time as _time
+    t_start = _time.perf_counter()
     best, best_t = candidates[0], float('inf')
     use_graph = os.environ.get('RAFIKI_AUTOTUNE_GRAPH', '1') != '0'
     for cfg in candidates:
@@ -124,6 +127,9 @@ def tune(key, candidates, run):
     with _lock:
         _cache[key] = tuple(best)
         _save()
+        stats['tuned'] += 1
+        stats['candidates'] += len(candidates)
+        stats['seconds'] += _time.perf_counter() - t_start
     return best
 
 

@@ -89,13 +89,19 @@ def _tile_candidates(M, N, fixed_bm=None):
 
 def _split_candidates(M, N, K):
     t0 = pick_tile(M, N)
-    first = (t0, pick_splits(M, N, K, t0))
+    s_h = pick_splits(M, N, K, t0)
+    first = (t0, s_h)
     out = [first]
     kt = cdiv(K, 64)
     for t in range(4):
+        blocks = cdiv(M, TILES[t][0]) * cdiv(N, TILES[t][1])
         for v in (0, 64, 128):
             for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
                 if s > kt or (s == 1 and kt > 64) or s * M * N * 4 > (256 << 20):
+                    continue
+                # keep the grid between ~1/2 and ~8 waves of the chip: fewer blocks idle CUs, more only
+                # add slab traffic (prunes ~2/3 of the space; tuning time matters for short trials)
+                if not (NUM_CU // 2 <= blocks * s <= 8 * NUM_CU) and s != s_h and not (s == 1 and blocks >= NUM_CU // 2):
                     continue
                 per = cdiv(kt, s)
                 s_eff = cdiv(kt, per)
