@@ -544,8 +544,9 @@ class ConvNetEngine:
             self.prepare_eval()
         B = x.shape[0]
         bucket = next((b for b in self.EVAL_BUCKETS if b >= B), None)
-        if bucket is None:  # larger than the biggest bucket: chunk it
-            outs = [self.forward_eval_graphed(x[i:i + self.EVAL_BUCKETS[-1]]) for i in
+        if bucket is None:  # larger than the biggest bucket: chunk it (each chunk's result is a view
+            # of the bucket's static output buffer, so copy it out before the next replay reuses it)
+            outs = [self.forward_eval_graphed(x[i:i + self.EVAL_BUCKETS[-1]]).clone() for i in
                     range(0, B, self.EVAL_BUCKETS[-1])]
             return torch.cat(outs)
         ent = self._eval_graphs.get(bucket)
