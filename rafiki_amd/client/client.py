@@ -155,6 +155,19 @@ class Client:
                                timeout=self._timeout)
         return self._parse_response(r)['predictions']
 
+    def predict_array(self, predictor_host, array):
+        """Binary batch prediction: a numpy batch in, a float32 numpy [Q, classes] out
+        (``POST /predict_batch_npy``; no JSON for the pixels)."""
+        import io
+        import numpy as np
+        buf = io.BytesIO()
+        np.save(buf, np.asarray(array), allow_pickle=False)
+        r = self._session.post('http://{}/predict_batch_npy'.format(predictor_host), data=buf.getvalue(),
+                               headers={'Content-Type': 'application/octet-stream'}, timeout=self._timeout)
+        if r.status_code != 200:
+            raise RafikiConnectionError(r.text)
+        return np.load(io.BytesIO(r.content), allow_pickle=False)
+
     # ----------------------------------------------------------------------------- advisors
     def _create_advisor(self, knob_config_str, advisor_id=None):
         return self._post('/advisors', target='advisor',

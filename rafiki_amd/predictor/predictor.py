@@ -178,6 +178,29 @@ class Predictor:
             raise RuntimeError('every model of the ensemble failed')
         return ensemble_predictions(preds, self.task)
 
+    def predict_array(self, arr):
+        """Ensemble probabilities for a numpy batch (images already decoded): skips the per-query
+        list handling of ``predict``; native models take the uint8 batch straight to the device."""
+        if self._fast_path():
+            import numpy as np
+            import torch
+            dev = None
+            for _, m in self.models:
+                d = getattr(m, 'device', None)
+                if d is not None and torch.device(d).type == 'cuda':
+                    dev = torch.device(d)
+                    break
+            if dev is not None and all(callable(getattr(m, 'input_signature', None)) for _, m in self.models):
+                inputs = {}
+                for _, m in self.models:
+                    sig = m.input_signature()
+                    if sig not in inputs:
+                        imgs = np.ascontiguousarray(m.queries_to_images(arr))
+                        inputs[sig] = torch.from_numpy(imgs).pin_memory().to(dev, non_blocking=True)
+                self.stats['queries'] += len(arr)
+                return self.predict_proba_device(inputs).cpu().numpy()
+        return self.predict(arr.tolist())
+
     def _predict_remote(self, queries):
         """Fan the batch out to every worker first, then gather (workers run concurrently); a worker
         that misses the deadline is dropped from this batch's ensemble (partial-ensemble fallback)."""

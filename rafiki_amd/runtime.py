@@ -21,6 +21,8 @@ _SIGS = {
     "rt_tfrecord_decode_images": (ctypes.c_longlong,
                                   [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
                                    ctypes.c_int]),
+    "rt_json_u8_array": (ctypes.c_longlong, [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_char_p, ctypes.c_void_p,
+                                            ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p]),
     "rt_mq_open": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_int]),
     "rt_mq_close": (None, [ctypes.c_void_p]),
     "rt_mq_unlink": (ctypes.c_int, [ctypes.c_char_p]),
@@ -55,3 +57,20 @@ def reset():
     global _lib, _tried
     with _lock:
         _lib, _tried = None, False
+
+
+def json_u8_array(body: bytes, key: str, max_elems: int = 1 << 26):
+    """Parse ``body[key]`` as a rectangular uint8 integer array with the native parser.
+    Returns a numpy array, or None when the runtime is missing or the value is not such an array."""
+    h = lib()
+    if h is None:
+        return None
+    import numpy as np
+    cap = min(max_elems, len(body))  # every element takes >= 1 byte of JSON
+    out = np.empty(cap, dtype=np.uint8)
+    shape = (ctypes.c_longlong * 8)()
+    nd = ctypes.c_int(0)
+    n = h.rt_json_u8_array(body, len(body), key.encode(), out.ctypes.data, cap, shape, ctypes.byref(nd))
+    if n < 0:
+        return None
+    return out[:n].reshape([int(shape[i]) for i in range(nd.value)])

@@ -49,6 +49,69 @@ def timed(fn, iters):
     return time.perf_counter() - t
 
 
+def _client_proc(url, kind, threads, seconds, q, payload):
+    import requests
+    stop = threading.Event()
+    counts = [0] * threads
+
+    def worker(i):
+        s = requests.Session()
+        while not stop.is_set():
+            if kind == 'json1':
+                s.post(url + '/predict', json={'query': payload}, timeout=30).raise_for_status()
+                counts[i] += 1
+            else:
+                s.post(url + '/predict_batch_npy', data=payload, timeout=30).raise_for_status()
+                counts[i] += 128
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    for t in ths:
+        t.start()
+    time.sleep(seconds)
+    stop.set()
+    for t in ths:
+        t.join()
+    q.put(sum(counts))
+
+
+def http_bench(pred, rng, args):
+    import io
+    import requests
+    from werkzeug.serving import make_server
+    from rafiki_amd.container.container_manager import free_port
+    from rafiki_amd.predictor.server import create_app
+    port = free_port()
+    srv = make_server('127.0.0.1', port, create_app(pred), threaded=True)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    url = 'http://127.0.0.1:{}'.format(port)
+    out = {}
+    one = rng.integers(0, 256, (32, 32, 3)).tolist()
+    batch = rng.integers(0, 256, (128, 32, 32, 3), dtype=np.uint8)
+    buf = io.BytesIO()
+    np.save(buf, batch, allow_pickle=False)
+    body = buf.getvalue()
+
+    def run(kind, procs, threads, seconds=4.0):
+        """Load from separate client processes (a load generator sharing the server's GIL would
+        measure itself)."""
+        import multiprocessing as mproc
+        ctx = mproc.get_context('spawn')
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_client_proc, args=(url, kind, threads, seconds, q, one if kind == 'json1' else body))
+              for _ in range(procs)]
+        for p in ps:
+            p.start()
+        total = sum(q.get(timeout=120) for _ in ps)
+        for p in ps:
+            p.join(30)
+        return round(total / seconds, 1)
+    pred.start()
+    out['json_single_query_qps_8x8clients'] = run('json1', 8, 8)
+    out['npy_batch128_qps_4x2clients'] = run('npy', 4, 2)
+    srv.shutdown()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--models', type=int, default=4)
@@ -80,6 +143,16 @@ def main():
         it = max(3, args.iters // 5)
         dt = timed(lambda: pred.predict(q), it)
         res['api'][b] = {'qps': round(b * it / dt, 1), 'ms_per_batch': round(1e3 * dt / it, 3)}
+    # numpy batches straight into the device path (what POST /predict_batch_npy does)
+    res['array'] = {}
+    for b in (128, 512):
+        arr = rng.integers(0, 256, (b, 32, 32, 3), dtype=np.uint8)
+        pred.predict_array(arr)
+        it = max(3, args.iters // 5)
+        dt = timed(lambda: pred.predict_array(arr), it)
+        res['array'][b] = {'qps': round(b * it / dt, 1), 'ms_per_batch': round(1e3 * dt / it, 3)}
+    # real HTTP: the predictor's Flask app on a local port, concurrent clients
+    res['http'] = http_bench(pred, rng, args)
     # dynamic batcher under concurrent single-query clients
     pred.start()
     one = rng.integers(0, 256, (32, 32, 3)).tolist()

@@ -134,6 +134,10 @@ def test_train_infer_predict(stack):
     assert len(pred) >= 4 and abs(sum(pred) - 1.0) < 1e-3
     preds = dev_c.predict_batch(ij['predictor_host'], [stack_query, stack_query])
     assert len(preds) == 2
+    import numpy as np
+    arr = np.asarray([stack_query, stack_query], dtype=np.uint8)
+    npy = dev_c.predict_array(ij['predictor_host'], arr)
+    assert npy.shape == (2, len(preds[0])) and np.allclose(npy, np.asarray(preds), atol=1e-5)
     with pytest.raises(RafikiConnectionError):  # one running inference job per train job
         dev_c.create_inference_job(app)
     dev_c.stop_inference_job(app)
