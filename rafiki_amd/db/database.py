@@ -428,6 +428,33 @@ class Database:
                             status=TrialStatus.STARTED, datetime_started=_now(), knobs=None, score=0.0,
                             params_file_path=None, datetime_stopped=None)
 
+    def claim_trial(self, sub_train_job_id, model_id, worker_id, max_trials):
+        """Atomically create a trial if the sub-train-job still has budget: counts COMPLETED, ERRORED
+        and in-flight (STARTED/RUNNING) trials inside one ``BEGIN IMMEDIATE`` transaction, so concurrent
+        workers (threads or processes) can never overshoot MODEL_TRIAL_COUNT (the reference's budget
+        race, worker/train.py:50).  Returns the new trial or None."""
+        with self._wlock:
+            c = self._conn()
+            c.execute('BEGIN IMMEDIATE')
+            try:
+                n = c.execute('SELECT COUNT(*) FROM trial WHERE sub_train_job_id = ? AND status IN (?,?,?,?)',
+                              (sub_train_job_id, TrialStatus.COMPLETED, TrialStatus.ERRORED, TrialStatus.STARTED,
+                               TrialStatus.RUNNING)).fetchone()[0]
+                if n >= max_trials:
+                    c.execute('ROLLBACK')
+                    return None
+                tid = _uuid()
+                c.execute('INSERT INTO trial (id, sub_train_job_id, model_id, worker_id, status, datetime_started, '
+                          'knobs, score, params_file_path, datetime_stopped) VALUES (?,?,?,?,?,?,?,?,?,?)',
+                          (tid, sub_train_job_id, model_id, worker_id, TrialStatus.STARTED, _enc('datetime_started',
+                                                                                                _now()),
+                           None, 0.0, None, None))
+                c.execute('COMMIT')
+            except Exception:
+                c.execute('ROLLBACK')
+                raise
+        return self.get_trial(tid)
+
     def get_trial(self, id):
         return self._one('trial', 'SELECT * FROM trial WHERE id = ?', (id,))
 

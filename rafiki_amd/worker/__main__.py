@@ -28,7 +28,9 @@ def main():
         from .train import TrainWorker
         backend = 'gloo' if os.environ.get('RAFIKI_CPU_ONLY') == '1' else None
         info = D.init_distributed(backend=backend)
-        worker = TrainWorker(service_id, os.environ.get('HOSTNAME', 'localhost'), db=db, dist_info=info)
+        host = os.environ.get('HOSTNAME', 'localhost')
+        worker_id = host if info.world_size == 1 else '{}-r{}'.format(host, info.rank)  # per-rank (resume)
+        worker = TrainWorker(service_id, worker_id, db=db, dist_info=info)
         try:
             run_worker(db, lambda sid, cid: worker.start(), worker.stop, service_id=service_id, rank=info.rank,
                        workdir=cfg.workdir)

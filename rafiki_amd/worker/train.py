@@ -52,7 +52,7 @@ class _TrialLogHandler(logging.Handler):
 
 class TrainWorker:
     def __init__(self, service_id, worker_id, db=None, dist_info: D.DistInfo = None, params_dir=None,
-                 max_trial_errors=3, advisor_type=None, seed=None, checkpoint_every_epochs=1):
+                 max_trial_errors=3, advisor_type=None, seed=None, checkpoint_every_epochs=1, scheduling=None):
         from ..config import get_config
         from ..db.database import Database
         self._service_id = service_id
@@ -64,6 +64,9 @@ class TrainWorker:
         os.makedirs(self._params_dir, exist_ok=True)
         self._max_trial_errors = max_trial_errors
         self._ckpt_every = checkpoint_every_epochs
+        # 'rounds': rank 0 proposes one knob set per rank per round over RCCL (lock-step);
+        # 'async' : ranks pull trials independently (heterogeneous trial lengths)
+        self._scheduling = scheduling or os.environ.get('RAFIKI_TRIAL_SCHEDULING', 'rounds')
         self._advisor_type = advisor_type
         self._seed = seed
         self._trial_id = None
@@ -89,6 +92,8 @@ class TrainWorker:
         data_parallel = bool(getattr(clazz, 'DATA_PARALLEL', False)) and info.world_size > 1
         advisor = make_advisor(knob_config, self._advisor_type, self._seed) if info.is_main else None
         device = default_device()
+        if self._scheduling == 'async' and not data_parallel:
+            return self._start_async(clazz, model, sub, train_job, knob_config, max_trials, deadline, device)
         errors = 0
         # trials this worker was running when its previous incarnation died, with a checkpoint to
         # resume from; re-run first, under their original ids and knobs
@@ -137,6 +142,48 @@ class TrainWorker:
                         errors = errors + 1 if table[r, 1] == 0 else 0
         if info.is_main:
             logger.info('sub-train-job %s budget reached', sub.id)
+            self._db.mark_sub_train_job_as_stopped(self._db.get_sub_train_job(sub.id))
+
+    # ------------------------------------------------------------------ asynchronous scheduling
+    def _start_async(self, clazz, model, sub, train_job, knob_config, max_trials, deadline, device):
+        """Asynchronous trial scheduling: every rank pulls its next trial as
+        soon as its GPU is free — no round barrier, so one slow trial never idles the other GPUs.
+
+        * budget: an atomic claim in the store (``Database.claim_trial``);
+        * knobs: each rank fits the GP-EI advisor on the SHARED history (completed trials of the
+          sub-train-job) with every in-flight trial's knobs as constant-liar pending points, so
+          concurrent proposals spread out exactly as in a batched proposal;
+        * end: when the budget is exhausted, a last barrier and rank 0 closes the sub-train-job."""
+        info = self._dist
+        errors = 0
+        n_local = 0
+        while not self._stop and errors < self._max_trial_errors:
+            if deadline is not None and time.time() > deadline:
+                break
+            trial = self._db.claim_trial(sub.id, model.id, self._worker_id, max_trials)
+            if trial is None:
+                break
+            history, pending = [], []
+            for t in self._db.get_trials_of_sub_train_job(sub.id):
+                if t.id == trial.id or not t.knobs:
+                    continue
+                if t.status == TrialStatus.COMPLETED:
+                    history.append((dict(t.knobs), float(t.score)))
+                elif t.status in (TrialStatus.STARTED, TrialStatus.RUNNING):
+                    pending.append(dict(t.knobs))
+            seed = None if self._seed is None else int(self._seed) * 1000003 + info.rank * 7919 + n_local
+            adv = make_advisor(knob_config, self._advisor_type, seed)
+            adv.history.extend(history)
+            adv._pending.extend(pending)
+            knobs = adv.propose()
+            ctx = TrialContext(device=device, dist=info, data_parallel=False)
+            score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, True, resume_id=trial.id)
+            errors = errors + 1 if not ok else 0
+            n_local += 1
+        if info.world_size > 1:
+            D.barrier(info)
+        if info.is_main:
+            logger.info('sub-train-job %s budget reached (async)', sub.id)
             self._db.mark_sub_train_job_as_stopped(self._db.get_sub_train_job(sub.id))
 
     def _orphaned_trials(self, sub_id):

@@ -64,14 +64,15 @@ def _setup_db(path, model_name, model_class, task, budget, train_uri, test_uri):
     return db, svc.id, sub.id
 
 
-def _worker_group(rank, world, port, db_path, service_id, workdir):
+def _worker_group(rank, world, port, db_path, service_id, workdir, scheduling='rounds'):
     _env(rank, world, port)
     os.environ['WORKDIR_PATH'] = workdir
     from rafiki_amd.db.database import Database
     from rafiki_amd.parallel import dist as D
     from rafiki_amd.worker.train import TrainWorker
     info = D.init_distributed(backend='gloo')
-    w = TrainWorker(service_id, 'w{}'.format(rank), db=Database(db_path), dist_info=info, seed=0)
+    w = TrainWorker(service_id, 'w{}'.format(rank), db=Database(db_path), dist_info=info, seed=0,
+                    scheduling=scheduling)
     w.start()
     D.destroy(info)
 
@@ -93,3 +94,41 @@ def test_trial_parallel_worker_group_skdt():
             logs = db.get_trial_logs(t.id)
             assert any('phase' in l.line for l in logs)
         assert db.get_sub_train_job(sub_id).datetime_stopped is not None
+
+
+def test_async_trial_scheduling_skdt():
+    """Asynchronous scheduling: ranks pull trials independently; the atomic claim keeps the budget
+    exact and constant-liar pending points keep concurrent proposals apart."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        db_path = os.path.join(d, 'db.sqlite3')
+        db, sid, sub_id = _setup_db(db_path, 'SkDt', 'SkDt', 'IMAGE_CLASSIFICATION', {'MODEL_TRIAL_COUNT': 7},
+                                    'synthetic://image?n=300&size=28&channels=1&classes=5&seed=0',
+                                    'synthetic://image?n=100&size=28&channels=1&classes=5&seed=1')
+        mp.spawn(_worker_group, args=(2, port, db_path, sid, d, 'async'), nprocs=2, join=True)
+        trials = db.get_trials_of_sub_train_job(sub_id)
+        assert len(trials) == 7 and all(t.status == 'COMPLETED' for t in trials)
+        assert len({t.worker_id for t in trials}) == 2
+        assert db.get_sub_train_job(sub_id).datetime_stopped is not None
+
+
+def test_claim_trial_is_atomic(tmp_path):
+    import threading
+    from rafiki_amd.db.database import Database
+    db, sid, sub_id = _setup_db(str(tmp_path / 'db.sqlite3'), 'SkDt', 'SkDt', 'IMAGE_CLASSIFICATION', {}, 'a', 'b')
+    sub = db.get_sub_train_job(sub_id)
+    got = []
+
+    def grab():
+        d2 = Database(str(tmp_path / 'db.sqlite3'))
+        while True:
+            t = d2.claim_trial(sub_id, sub.model_id, 'w', 25)
+            if t is None:
+                return
+            got.append(t.id)
+    ths = [threading.Thread(target=grab) for _ in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert len(got) == 25 and len(set(got)) == 25
