@@ -6,11 +6,14 @@ error (``NativeLibraryError``) — GPU code paths never silently fall back to Py
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 from pathlib import Path
 
 _NATIVE = Path(__file__).resolve().parent.parent / "_native"
-KERNEL_LIB = _NATIVE / "librafiki_kernels.so"
+# RAFIKI_KERNEL_LIB overrides the library path (A/B runs of two kernel builds on one box)
+KERNEL_LIB = Path(os.environ["RAFIKI_KERNEL_LIB"]) if os.environ.get("RAFIKI_KERNEL_LIB") else \
+    _NATIVE / "librafiki_kernels.so"
 
 _lock = threading.Lock()
 _lib = None

@@ -21,6 +21,7 @@ _loaded = False
 stats = {'tuned': 0, 'seconds': 0.0, 'candidates': 0}
 ENABLED = os.environ.get('RAFIKI_AUTOTUNE', '1') != '0'
 REPS = int(os.environ.get('RAFIKI_AUTOTUNE_REPS', '3'))
+PASSES = int(os.environ.get('RAFIKI_AUTOTUNE_PASSES', '2'))
 
 
 def _path():
@@ -111,19 +112,33 @@ def tune(key, candidates, run):
         return candidates[0]
     import time as _time
     t_start = _time.perf_counter()
-    best, best_t = candidates[0], float('inf')
     use_graph = os.environ.get('RAFIKI_AUTOTUNE_GRAPH', '1') != '0'
-    for cfg in candidates:
-        try:
-            t = _time_graph(cfg, run, max(REPS, 5)) if use_graph else _time_eager(cfg, run, REPS)
-        except Exception:
+    # PASSES sweeps over the candidates, min per candidate: the first sweep also absorbs clock
+    # ramp-up after idle, which otherwise penalises whichever candidates happen to run first
+    times = {}
+    for _ in range(PASSES):
+        for cfg in candidates:
+            if times.get(cfg, 0.0) == float('inf'):
+                continue
             try:
-                torch.cuda.synchronize()
+                t = _time_graph(cfg, run, max(REPS, 5)) if use_graph else _time_eager(cfg, run, REPS)
             except Exception:
-                pass
-            continue
-        if t < best_t:
-            best, best_t = cfg, t
+                try:
+                    torch.cuda.synchronize()
+                except Exception:
+                    pass
+                t = float('inf')
+            times[cfg] = min(times.get(cfg, float('inf')), t)
+    best = min(candidates, key=lambda c: times.get(c, float('inf')))
+    best_t = times.get(best, float('inf'))
+    log = os.environ.get('RAFIKI_AUTOTUNE_LOG', '')
+    if log:
+        try:
+            with open(log, 'a') as f:
+                f.write(json.dumps({'key': [str(k) for k in key], 'best': list(best), 'us': round(best_t * 1e3, 2),
+                                    'first_us': round(times.get(candidates[0], float('inf')) * 1e3, 2)}) + '\n')
+        except OSError:
+            pass
     with _lock:
         _cache[key] = tuple(best)
         _save()

@@ -71,6 +71,12 @@ def pick_splits(M: int, N: int, K: int, tile: int, target_blocks: int = 2 * NUM_
     return cdiv(ktiles, per)
 
 
+# Staging variants the tuner tries.  The 3/4-stage LDS-DMA rings (32/128) win some isolated timings
+# but lose inside the training step (less occupancy when neighbouring kernels share L2), so they are
+# opt-in: RAFIKI_IGEMM_DEEP=1.
+_VARIANTS = (0, 64, 32, 128) if os.environ.get('RAFIKI_IGEMM_DEEP', '0') == '1' else (0, 64)
+
+
 def _tile_candidates(M, N, fixed_bm=None):
     """Heuristic pick first (used when tuning is impossible), then every shape x staging variant."""
     first = pick_tile(M, N)
@@ -80,7 +86,7 @@ def _tile_candidates(M, N, fixed_bm=None):
         shapes = list(range(4))
     out = [(first,)]
     for t in shapes:
-        for v in (0, 64, 32, 128):
+        for v in _VARIANTS:
             c = (t | v,)
             if c not in out:
                 out.append(c)
@@ -144,11 +150,10 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
     assert w.numel() == Cout * K, (w.shape, taps, Cin)
     if out is None:
         out = torch.empty((Nb, H, W, Cout), device=x.device, dtype=torch.bfloat16)
-    tile = pick_tile(M, Cout)
     stats = None
     flags = 0
     if want_stats:
-        stats = torch.empty((stats_rows(M, Cout, tile), 2, Cout), device=x.device, dtype=torch.float32)
+        stats = _bn_rows_buffer(M, Cout, x.device)
         flags |= FLAG_STATS
     if bias is not None:
         flags |= FLAG_BIAS
@@ -159,10 +164,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
     def run(cfg):
         igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
               taps=taps, flags=flags, slope=slope, tile=cfg[0])
-    cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, bool(want_stats)),
-                 _tile_candidates(M, Cout, fixed_bm=TILES[tile][0] if want_stats else None), run)
+    cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, bool(want_stats)), _tile_candidates(M, Cout), run)
     run(cfg)
-    return (out, stats) if want_stats else out
+    return (out, stats[:stats_rows(M, Cout, cfg[0])]) if want_stats else out
 
 
 def conv_up(x: torch.Tensor, w: torch.Tensor, *, bias=None, act=ACT_NONE, slope=0.2, out=None):
@@ -183,6 +187,11 @@ def conv_up(x: torch.Tensor, w: torch.Tensor, *, bias=None, act=ACT_NONE, slope=
               flags=flags, slope=slope, tile=cfg[0])
     run(_tuned(('cu', M, Cout, K, H, W, Cin), [c for c in _tile_candidates(M, Cout) if c[0] < 32], run))
     return out
+
+
+def _bn_rows_buffer(M, C, device):
+    # sized for the smallest BM (64); the tuned tile's BM decides how many rows are written
+    return torch.empty((cdiv(M, 64) * 2, 2, C), device=device, dtype=torch.float32)
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, gate=None):
@@ -351,16 +360,25 @@ def bn_act_fwd(y, scale, shift, *, pool=False, act=ACT_RELU, slope=0.2, out=None
 
 
 def bn_bwd(dout, y, coeffs, gamma, *, pool=False, act=ACT_RELU, slope=0.2, dgamma=None, dbeta=None, dy=None,
-           accumulate=False):
-    """Backward of out = pool(act(bn(y))).  coeffs = [mean, rstd, scale, shift] rows from forward."""
+           accumulate=False, part=None):
+    """Backward of out = pool(act(bn(y))).  coeffs = [mean, rstd, scale, shift] rows from forward.
+    ``part``: precomputed (sum dz, sum dz*y) partial rows [R][2][C] — skips the reduce pass.
+
+    Measured alternative (MI355X, VGG-small): folding this reduction into the data-gradient GEMM
+    epilogue (reading y there) made the step 5% slower — +22 VGPRs in every igemm variant plus the
+    y-load latency exposed at each block's tail cost more than the separate streaming pass."""
     Nb, H, W, C = y.shape
-    P_out = dout.numel() // C
-    rows = _lib.lib().rk_bn_bwd_rows(P_out, C)
-    part = torch.empty((rows, 2, C), device=y.device, dtype=torch.float32)
     mean, rstd, scale, shift = coeffs[0], coeffs[1], coeffs[2], coeffs[3]
     s = _s()
-    _lib.call("rk_bn_bwd_reduce", _p(dout), _p(y), _p(scale), _p(shift), _p(part), rows, Nb, H, W, C, int(pool), act,
-              float(slope), s)
+    if part is not None:
+        part = _shrink_rows(part)
+        rows = part.shape[0]
+    else:
+        P_out = dout.numel() // C
+        rows = _lib.lib().rk_bn_bwd_rows(P_out, C)
+        part = torch.empty((rows, 2, C), device=y.device, dtype=torch.float32)
+        _lib.call("rk_bn_bwd_reduce", _p(dout), _p(y), _p(scale), _p(shift), _p(part), rows, Nb, H, W, C, int(pool),
+                  act, float(slope), s)
     coef = torch.empty((3, C), device=y.device, dtype=torch.float32)
     _lib.call("rk_bn_finalize_bwd", _p(part), rows, C, float(Nb * H * W), _p(gamma), _p(mean), _p(rstd), _p(dgamma),
               _p(dbeta), _p(coef), int(accumulate), s)
