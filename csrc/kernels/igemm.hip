@@ -919,6 +919,307 @@ int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
   return RK_EBADARG;
 }
 
+// ================================================================================================
+// Halo-tiled 3x3 convolution (forward and data-gradient), persistent over work items.
+//
+// The implicit GEMM above gathers the activation once per tap: every input pixel crosses the
+// L2->LDS path 9 times, which is what bounds the 32x32 / 16x16 VGG layers (~450 TB/s-class L2
+// traffic for ~20 % MFMA utilisation).  Here a work item is BM output pixels = TH whole rows of one
+// image (BM = TH*W) x BN output channels; per 64-channel input chunk the block DMAs ONE
+// (TH+2) x (W+2) halo patch into LDS and runs all 9 taps out of it — the tap is just a constant
+// shift of the patch pixel each lane reads (shift = dy*(W+2)+dx, negated for the data-gradient).
+// B (weights) streams per (tap, chunk) K-tile through a 3-stage LDS-DMA ring exactly as in
+// igemm_dma_kernel (same K-inner / K-outer LDS images and fragment readers).  Patches are double
+// buffered: the patch of the next phase (next chunk or next item) is in flight during the 9 taps
+// of the current one, so the pipeline never drains between items.  One raw barrier per tap.
+// Patch image: pixel pp = 128-byte row (64 channels), 16-B chunk c stored at c ^ (pp&7) — the one
+// XOR that keeps ds_read_b128 conflict-free (4 LDS cycles) for ANY start pixel, which the tap shift
+// makes arbitrary (the GEMM image's (i>>1)&7 averages 7 cycles here); the
+// DMA writes lane-linear, so each lane's SOURCE is the chunk that belongs in its slot, and slots
+// outside the image (halo at the border, padding) read zeros through the buffer range check.
+// ================================================================================================
+// (a device function, not a builtin call inside the kernel's lambdas: hipcc then silently drops the
+// host-side launch stub of the kernel template — undefined __device_stub__ at load time)
+RK_DEV void dma16(__amdgpu_buffer_rsrc_t r, char* dst, int off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, off, 0, 0, 0);
+}
+
+RK_DEV bf16x8 patch_frag(const char* patch, int pp, int kb, int lane) {
+  const int c = (kb >> 3) + (lane >> 4);
+  return *(const bf16x8*)(patch + pp * 128 + ((c ^ (pp & 7)) << 4));
+}
+
+// Sum over each 16-lane row of the wave with DPP lane permutes folded into the adds (no LDS
+// round trip, unlike __shfl_xor's ds_bpermute): quad xor 1, quad xor 2, half-row mirror, row mirror.
+RK_DEV float dpp_sum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+// Epilogue flag set FL is a template argument: with runtime flags hipcc if-converts every optional
+// step (activation, gate, statistics) into always-executed VALU + selects (~190 extra VALU per
+// tile).  hconv_epilogue dispatches the common sets to specialised copies.
+template <int MI, int NI, int FL>
+RK_DEV void hconv_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm, int lane) {
+  constexpr bool ST = FL & FLAG_STATS, BI = FL & FLAG_BIAS, RE = FL & FLAG_RELU, LR = FL & FLAG_LRELU,
+                 GA = FL & FLAG_GATE;
+  bf16* C = (bf16*)p.out;
+  float s[NI][4], ss[NI][4];
+#pragma unroll
+  for (int j = 0; j < NI; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[j][e] = ss[j][e] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = ncol + j * 16;
+    f32x4 b = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (BI) b = *(const f32x4*)(p.bias + n);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = mrow + i * 16;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = BI ? acc[i][j][e] * p.alpha + b[e] : acc[i][j][e] * p.alpha;
+        if constexpr (ST) {
+          s[j][e] += v[e];
+          ss[j][e] += v[e] * v[e];
+        }
+        if constexpr (RE) v[e] = fmaxf(v[e], 0.f);
+        if constexpr (LR) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope;
+      }
+      if constexpr (GA) {
+        const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+      *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
+      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if constexpr (ST) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[j][e] = dpp_sum16(s[j][e]);
+        ss[j][e] = dpp_sum16(ss[j][e]);
+      }
+    if ((lane & 15) == 0) {
+      float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int n = ncol + j * 16;
+        *(f32x4*)(row + n) = f32x4{s[j][0], s[j][1], s[j][2], s[j][3]};
+        *(f32x4*)(row + p.N + n) = f32x4{ss[j][0], ss[j][1], ss[j][2], ss[j][3]};
+      }
+    }
+  }
+}
+
+template <int MI, int NI>
+RK_DEV void hconv_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm,
+                           int lane) {
+  constexpr int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE;
+  switch (p.flags & (S_ | B_ | R_ | L_ | G_)) {
+    case 0: return hconv_epi<MI, NI, 0>(p, acc, mrow, ncol, mt, wm, lane);
+    case S_: return hconv_epi<MI, NI, S_>(p, acc, mrow, ncol, mt, wm, lane);
+    case G_: return hconv_epi<MI, NI, G_>(p, acc, mrow, ncol, mt, wm, lane);
+    case B_: return hconv_epi<MI, NI, B_>(p, acc, mrow, ncol, mt, wm, lane);
+    case B_ | R_: return hconv_epi<MI, NI, B_ | R_>(p, acc, mrow, ncol, mt, wm, lane);
+    case B_ | L_: return hconv_epi<MI, NI, B_ | L_>(p, acc, mrow, ncol, mt, wm, lane);
+    case R_: return hconv_epi<MI, NI, R_>(p, acc, mrow, ncol, mt, wm, lane);
+    case L_: return hconv_epi<MI, NI, L_>(p, acc, mrow, ncol, mt, wm, lane);
+    case S_ | B_: return hconv_epi<MI, NI, S_ | B_>(p, acc, mrow, ncol, mt, wm, lane);
+    default: __builtin_trap();  // rejected on the host (rk_hconv)
+  }
+}
+
+template <int BM, int BN, int W, int BMODE, int FLIP>
+__global__ __launch_bounds__(256, 2) void hconv_kernel(const IgemmParams p, const int per_block) {
+  constexpr int TH = BM / W;                   // output rows per item
+  constexpr int PC = W + 2, NPP = (TH + 2) * PC;
+  constexpr int LP = (NPP * 8 + 255) / 256;    // patch DMA instructions per wave
+  constexpr int P_BYTES = LP * 4 * 1024;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int LB = BN / 32;                  // B DMA instructions per wave per K-tile
+  constexpr int R = BN / 8;                    // K-outer B: 16-B slots per k-row
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
+  constexpr int LOG2W = W == 8 ? 3 : W == 16 ? 4 : 5;
+  static_assert(BM % W == 0 && LP + LB <= 63, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[2 * P_BYTES + 3 * B_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int log2C = p.log2C;
+  const int NCC = p.C >> 6;
+  const int tilesN = p.N / BN;
+  const int nItems = (p.M / BM) * tilesN;
+  const int tilesPerImg = (p.H * W) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int item0 = bid * per_block;
+  const int item1 = min(nItems, item0 + per_block);
+  if (item0 >= item1) return;
+  const int nPhases = (item1 - item0) * NCC;
+  const int S = nPhases * 9;
+
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(p.A, p.bytesA);
+  const __amdgpu_buffer_rsrc_t rB = make_rsrc(p.B, p.bytesB);
+
+  // ---- patch DMA lane constants
+  int prel[LP], prow[LP];
+#pragma unroll
+  for (int q = 0; q < LP; ++q) {
+    const int slot = (wid * LP + q) * 64 + lane;
+    const int pp = slot >> 3;
+    const int c = (slot & 7) ^ (pp & 7);
+    const int pr = pp / PC, pcol = pp - pr * PC;
+    const bool ok = pp < NPP && pcol >= 1 && pcol <= W;
+    prel[q] = ((((pr - 1) * W + (pcol - 1)) << log2C) << 1) + c * 16;
+    prow[q] = ok ? pr : -1000;
+  }
+  // ---- B DMA lane constants (tile-independent part of the source offset)
+  unsigned boff[LB];
+#pragma unroll
+  for (int q = 0; q < LB; ++q) {
+    const int slot = (wid * LB + q) * 64 + lane;
+    if constexpr (BMODE == OP_DENSE_KIN) {  // forward: B[n][k], k contiguous, row length ldb
+      const int i = slot >> 3;
+      const int c = (slot & 7) ^ ((i >> 1) & 7);
+      boff[q] = ((unsigned)i * (unsigned)p.ldb + (unsigned)c * 8u) * 2u;
+    } else {  // data-gradient: row k = tap*C + co of W[co][tap][n]
+      const int krow = slot / R;
+      int f;
+      if constexpr (R == 16) f = ((krow & 3) << 2) | ((krow >> 2) & 3);
+      else f = ((krow & 3) << 1) | ((krow >> 2) & 1);
+      const int ch = (slot % R) ^ f;
+      boff[q] = ((unsigned)krow * (unsigned)p.ldb + (unsigned)ch * 8u) * 2u;
+    }
+  }
+  // ---- A fragment rows: patch pixel of each lane's output pixel (before the tap shift)
+  int ppb[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int ml = wm * WM + i * 16 + (lane & 15);
+    ppb[i] = ((ml >> LOG2W) + 1) * PC + (ml & (W - 1)) + 1;
+  }
+
+  // phase = (item, 64-channel chunk): state of the current and the next phase, advanced once per
+  // phase on the scalar unit (no per-tap integer division)
+  struct Phase { int cc, mt, nt; };
+  auto advance = [&](Phase q) {
+    if (++q.cc == NCC) {
+      q.cc = 0;
+      if (++q.nt == tilesN) { q.nt = 0; ++q.mt; }
+    }
+    return q;
+  };
+  // B K-tile (phase q, tap t) source = bbase(q) + t * bstep
+  const unsigned bstep = BMODE == OP_DENSE_KIN ? (unsigned)p.C * 2u : (unsigned)p.N * 2u;
+  auto bbase = [&](const Phase& q) -> unsigned {
+    if constexpr (BMODE == OP_DENSE_KIN)
+      return ((unsigned)(q.nt * BN) * (unsigned)p.ldb + (unsigned)(q.cc * 64)) * 2u;
+    else
+      return ((unsigned)(q.cc * 64) * (unsigned)p.ldb + (unsigned)(q.nt * BN)) * 2u;
+  };
+  auto issue_patch = [&](const Phase& q, int buf) {
+    const int r0 = (q.mt & (tilesPerImg - 1)) * TH;  // tilesPerImg = H*W/BM is a power of two
+    const int base = (((q.mt * BM) << log2C) << 1) + q.cc * 128;
+    char* dst = smem + buf * P_BYTES + wid * LP * 1024;
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+      const bool in = (unsigned)(r0 - 1 + prow[j]) < (unsigned)p.H;
+      dma16(rA, dst + j * 1024, in ? base + prel[j] : (int)OOB);
+    }
+  };
+  auto issue_b = [&](unsigned src, int stage) {
+    char* dst = smem + 2 * P_BYTES + stage * B_BYTES + wid * LB * 1024;
+#pragma unroll
+    for (int j = 0; j < LB; ++j) dma16(rB, dst + j * 1024, (int)(boff[j] + src));
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Phase cur{0, item0 / tilesN, item0 % tilesN};
+  Phase nxt = advance(cur);
+  unsigned bcur = bbase(cur), bnxt = bbase(nxt);
+  issue_patch(cur, 0);
+  issue_b(bcur, 0);
+  if (S > 1) issue_b(bcur + bstep, 1);
+  for (int ph = 0; ph < nPhases; ++ph) {
+    const bool last = ph == nPhases - 1;
+    const char* pt = smem + (ph & 1) * P_BYTES;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      // loads issued after B(s): B(s+1), plus the next patch when it went out at tap 0 of this phase
+      if (last && tap == 8) wait_vmcnt<0>();
+      else if ((tap == 1 || tap == 2) && !last) wait_vmcnt<LB + LP>();
+      else wait_vmcnt<LB>();
+      raw_barrier();
+      if (tap + 2 < 9) issue_b(bcur + (unsigned)(tap + 2) * bstep, (tap + 2) % 3);
+      else if (!last) issue_b(bnxt + (unsigned)(tap - 7) * bstep, (tap + 2) % 3);
+      if (tap == 0 && !last) issue_patch(nxt, (ph + 1) & 1);
+      const char* lb = smem + 2 * P_BYTES + (tap % 3) * B_BYTES;
+      const int shift = FLIP ? -(tap_dy(tap) * PC + tap_dx(tap)) : (tap_dy(tap) * PC + tap_dx(tap));
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[MI], bfr[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = patch_frag(pt, ppb[i] + shift, ks * 32, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) bfr[j] = Operand<BMODE, BN>::frag(lb, wn * WN + j * 16, ks * 32, lane);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (cur.cc == NCC - 1)  // last chunk of this item: write it out
+      hconv_epilogue<MI, NI>(p, acc, cur.mt * BM + wm * WM + (lane & 15), cur.nt * BN + wn * WN + 4 * (lane >> 4),
+                             cur.mt, wm, lane);
+    cur = nxt;
+    nxt = advance(nxt);
+    bcur = bnxt;
+    bnxt = bbase(nxt);
+  }
+}
+
+template <int BM, int BN, int W>
+int launch_hconv_w(bool dgrad, const IgemmParams& p, int grid, hipStream_t st) {
+  const int items = (p.M / BM) * (p.N / BN);
+  if (grid <= 0 || grid > items) grid = items;
+  const int per = rk_cdiv(items, grid);
+  grid = rk_cdiv(items, per);
+  if (dgrad)
+    hipLaunchKernelGGL((hconv_kernel<BM, BN, W, OP_WTAP_KOUT, 1>), dim3(grid), dim3(256), 0, st, p, per);
+  else
+    hipLaunchKernelGGL((hconv_kernel<BM, BN, W, OP_DENSE_KIN, 0>), dim3(grid), dim3(256), 0, st, p, per);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+template <int BN>
+int launch_hconv_bn(bool dgrad, const IgemmParams& p, int grid, hipStream_t st) {
+  switch (p.W) {
+    case 8: return launch_hconv_w<64, BN, 8>(dgrad, p, grid, st);
+    case 16: return launch_hconv_w<128, BN, 16>(dgrad, p, grid, st);
+    case 32: return launch_hconv_w<128, BN, 32>(dgrad, p, grid, st);
+  }
+  return RK_EUNSUPPORTED;
+}
+
 }  // namespace
 
 // kind: 0 conv-fwd, 1 conv-dgrad, 2 conv-wgrad, 3 dense (A·Bᵀ), 4 dense dX (A·B), 5 dense dW (Aᵀ·B),
@@ -975,4 +1276,38 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
       return launch_modes<OP_CONVUP_KIN, OP_DENSE_KIN, EPI_BF16>(tile & (15 | 16), p, splits, st);
   }
   return RK_EBADARG;
+}
+
+// Halo-tiled 3x3 conv (see hconv_kernel).  dgrad = 0: y = conv(x, w) with w [N][9][C] (ldb = 9C);
+// dgrad = 1: dx = conv^T(dy, w) with w [C][9][N] (ldb = 9N), C = channels of the input (dy).
+// tile bit 0: BN = 128 (else 64).  grid <= 0: one item per block; otherwise the persistent grid
+// size (items are dealt in contiguous runs).  Returns RK_EUNSUPPORTED outside the covered shapes
+// (W in {8,16,32}, H a power of two with H*W a multiple of BM, C a power of two >= 64, N % BN == 0).
+extern "C" int rk_hconv(int dgrad, int tile, const void* A, const void* B, void* C, const float* bias, float* stats,
+                        const void* gate, int M, int N, int K, int ldb, int H, int W, int Cch, int flags, float alpha,
+                        float slope, long long bytesA, long long bytesB, int grid, void* stream) {
+  if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const int BN = (tile & 1) ? 128 : 64;
+  const int BM = W == 8 ? 64 : 128;
+  if (W != 8 && W != 16 && W != 32) return RK_EUNSUPPORTED;
+  if (rk_log2(H) < 0 || (H * W) % BM != 0 || M <= 0 || M % (H * W) != 0) return RK_EUNSUPPORTED;
+  if (rk_log2(Cch) < 6 || N <= 0 || N % BN != 0 || K != 9 * Cch) return RK_EUNSUPPORTED;
+  if (ldb != (dgrad ? 9 * N : K)) return RK_EBADARG;
+  {
+    const int f = flags & (FLAG_STATS | FLAG_BIAS | FLAG_RELU | FLAG_LRELU | FLAG_GATE);
+    const int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE;
+    if (!(f == 0 || f == S_ || f == G_ || f == B_ || f == (B_ | R_) || f == (B_ | L_) || f == R_ || f == L_ ||
+          f == (S_ | B_)))
+      return RK_EUNSUPPORTED;  // epilogue flag set without a specialised copy (see hconv_epilogue)
+  }
+  IgemmParams p{};
+  p.A = (const bf16*)A; p.B = (const bf16*)B; p.out = C; p.bias = bias; p.stats = stats;
+  p.gate = (const bf16*)gate;
+  p.M = M; p.N = N; p.K = K; p.lda = Cch; p.ldb = ldb; p.ldc = N;
+  p.H = H; p.W = W; p.C = Cch; p.taps = 9;
+  p.log2H = rk_log2(H); p.log2W = rk_log2(W); p.log2C = rk_log2(Cch); p.log2Cb = p.log2C;
+  p.flags = flags; p.alpha = alpha; p.slope = slope;
+  p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
+  hipStream_t st = (hipStream_t)stream;
+  return BN == 128 ? launch_hconv_bn<128>(dgrad != 0, p, grid, st) : launch_hconv_bn<64>(dgrad != 0, p, grid, st);
 }

@@ -24,6 +24,8 @@ vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_doubl
 _SIGS = {
     "rk_igemm": [i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                  i32, i32, i64, i32, f32, f32, i64, i64, vp],
+    "rk_hconv": [i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, f32, f32, i64, i64, i32,
+                 vp],
     "rk_bn_partial_rows": [i64, i32],
     "rk_channel_stats": [vp, vp, i64, i32, i32, vp],
     "rk_bn_finalize_fwd": [vp, i32, i32, f64, vp, vp, f32, vp, vp, f32, vp, vp, vp, vp, vp],

@@ -141,6 +141,42 @@ def stats_rows(M: int, N: int, tile: Optional[int] = None) -> int:
     return cdiv(M, TILES[t & 15][0]) * 2
 
 
+# Halo-tiled 3x3 conv (rk_hconv): one LDS patch per (item, 64-channel chunk) serves all 9 taps.
+# Candidates are ('h', bn_bit, grid): grid 0 = one item per block, else a persistent grid.
+HCONV = os.environ.get('RAFIKI_HCONV', '1') != '0'
+
+
+def _hconv_bm(W: int) -> int:
+    return 64 if W == 8 else 128
+
+
+def _hconv_candidates(M, N, H, W, C, taps):
+    if not HCONV or taps != 9 or W not in (8, 16, 32) or H & (H - 1) or (H * W) % _hconv_bm(W):
+        return []
+    if C < 64 or C & (C - 1) or N % 64:
+        return []
+    out = []
+    for bn_bit in ((0, 1) if N % 128 == 0 else (0,)):
+        items = (M // _hconv_bm(W)) * (N // (128 if bn_bit else 64))
+        per_cu = 1 if bn_bit else 2  # LDS-resident blocks per CU
+        for g in (0, NUM_CU * per_cu):
+            if g and g >= items:
+                continue
+            out.append(('h', bn_bit, g))
+    return out
+
+
+def _cfg_bm(cfg, W: int) -> int:
+    return _hconv_bm(W) if cfg[0] == 'h' else TILES[cfg[0] & 15][0]
+
+
+def hconv(dgrad, A, B, out, M, N, K, ldb, H, W, C, *, bias=None, stats=None, gate=None, flags=0, alpha=1.0,
+          slope=0.2, bn_bit=0, grid=0):
+    _lib.call("rk_hconv", int(dgrad), int(bn_bit), _p(A), _p(B), _p(out), _p(bias), _p(stats), _p(gate), M, N, K,
+              ldb, H, W, C, flags, float(alpha), float(slope), _nbytes(A), _nbytes(B), int(grid), _s())
+    return out
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want_stats=False, act=ACT_NONE,
              slope=0.2, out=None):
     """y = conv3x3(x, w) (stride 1, pad 1) [+bias][act]; optional per-channel partial stats."""
@@ -162,11 +198,16 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
     elif act == ACT_LRELU:
         flags |= FLAG_LRELU
     def run(cfg):
-        igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
-              taps=taps, flags=flags, slope=slope, tile=cfg[0])
-    cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, bool(want_stats)), _tile_candidates(M, Cout), run)
+        if cfg[0] == 'h':
+            hconv(0, x, w, out, M, Cout, K, K, H, W, Cin, bias=bias, stats=stats, flags=flags, slope=slope,
+                  bn_bit=cfg[1], grid=cfg[2])
+        else:
+            igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
+                  taps=taps, flags=flags, slope=slope, tile=cfg[0])
+    cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, bool(want_stats)),
+                 _tile_candidates(M, Cout) + _hconv_candidates(M, Cout, H, W, Cin, taps), run)
     run(cfg)
-    return (out, stats[:stats_rows(M, Cout, cfg[0])]) if want_stats else out
+    return (out, stats[:cdiv(M, _cfg_bm(cfg, W)) * 2]) if want_stats else out
 
 
 def conv_up(x: torch.Tensor, w: torch.Tensor, *, bias=None, act=ACT_NONE, slope=0.2, out=None):
@@ -203,9 +244,14 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, ga
     flags = FLAG_GATE if gate is not None else 0
 
     def run(cfg):
-        igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, H=H, W=W, C=Cout,
-              taps=taps, Cb=Cout, flags=flags, tile=cfg[0])
-    run(_tuned(('cd', M, Cin, K, H, W, Cout, taps), _tile_candidates(M, Cin), run))
+        if cfg[0] == 'h':
+            hconv(1, dy, w, out, M, Cin, K, taps * Cin, H, W, Cout, gate=gate, flags=flags, bn_bit=cfg[1],
+                  grid=cfg[2])
+        else:
+            igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, H=H, W=W, C=Cout,
+                  taps=taps, Cb=Cout, flags=flags, tile=cfg[0])
+    run(_tuned(('cd', M, Cin, K, H, W, Cout, taps),
+               _tile_candidates(M, Cin) + _hconv_candidates(M, Cin, H, W, Cout, taps), run))
     return out
 
 

@@ -191,3 +191,30 @@ def test_misc(fn):
     packed = fn.pack_nhwc(img, 8, 1 / 255.0, 0.0)
     assert torch.allclose(packed[..., :3].float(), (img.float() / 255).permute(0, 2, 3, 1), atol=4e-3)
     assert packed[..., 3:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,bn_bit,grid", [(2, 32, 32, 64, 64, 0, 0), (2, 16, 16, 128, 128, 1, 0),
+                                                        (3, 8, 8, 256, 64, 0, 7), (2, 32, 32, 128, 256, 1, 5),
+                                                        (4, 8, 8, 512, 128, 0, 0), (2, 16, 16, 64, 128, 0, 3)])
+def test_hconv_fwd_dgrad(fn, N, H, W, Cin, Cout, bn_bit, grid):
+    """Halo-tiled conv (forward with BN-stats epilogue, and data-gradient) vs PyTorch fp32."""
+    torch.manual_seed(11)
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    w = (torch.randn(Cout, 3, 3, Cin, device=DEV) / (3 * Cin ** 0.5)).bfloat16()
+    M, K = N * H * W, 9 * Cin
+    y = torch.empty(N, H, W, Cout, device=DEV, dtype=torch.bfloat16)
+    bm = 64 if W == 8 else 128
+    stats = torch.zeros(M // bm * 2, 2, Cout, device=DEV)
+    fn.hconv(0, x, w, y, M, Cout, K, K, H, W, Cin, stats=stats, flags=fn.FLAG_STATS, bn_bit=bn_bit, grid=grid)
+    ref = F.conv2d(_nhwc_to_nchw(x.float()), _w_to_oihw(w.float()), padding=1).permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-2
+    s = stats.sum(0)
+    assert torch.allclose(s[0], ref.reshape(-1, Cout).sum(0), rtol=2e-2, atol=0.5)
+    # data-gradient: dx = conv_transpose(dy, w)
+    dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    dx = torch.empty(N, H, W, Cin, device=DEV, dtype=torch.bfloat16)
+    fn.hconv(1, dy, w.reshape(Cout, -1), dx, M, Cin, 9 * Cout, 9 * Cin, H, W, Cout, bn_bit=bn_bit if Cin % 128 == 0
+             else 0, grid=grid)
+    xr = _nhwc_to_nchw(x.float()).requires_grad_(True)
+    F.conv2d(xr, _w_to_oihw(w.float()), padding=1).backward(_nhwc_to_nchw(dy.float()))
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
