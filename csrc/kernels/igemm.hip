@@ -504,6 +504,101 @@ RK_DEV void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Sum over each 16-lane row of the wave with DPP lane permutes folded into the adds (no LDS
+// round trip, unlike __shfl_xor's ds_bpermute): quad xor 1, quad xor 2, half-row mirror, row mirror.
+RK_DEV float dpp_sum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+// BF16 tile epilogue shared by every kernel: lane owns out[m][n..n+3] of each (i, j) fragment.
+// The flag set FL is a template argument: with runtime flags hipcc if-converts every optional step
+// (activation, gate, statistics) into always-executed VALU + selects (~190 extra VALU per tile).
+// tile_epilogue dispatches the common sets to specialised copies; FL = -1 is the runtime-flag
+// fallback for any other combination.  GUARD: partial tiles (m >= M or n >= N lanes skip).
+template <int MI, int NI, int FL, bool GUARD>
+RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm, int lane) {
+  const int fl = FL < 0 ? p.flags : FL;
+  const bool ST = fl & FLAG_STATS, BI = fl & FLAG_BIAS, RE = fl & FLAG_RELU, LR = fl & FLAG_LRELU,
+             GA = fl & FLAG_GATE;
+  bf16* C = (bf16*)p.out;
+  float s[NI][4], ss[NI][4];
+#pragma unroll
+  for (int j = 0; j < NI; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[j][e] = ss[j][e] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = ncol + j * 16;
+    const bool nok = !GUARD || n < p.N;
+    f32x4 b = {0.f, 0.f, 0.f, 0.f};
+    if (BI && nok) b = *(const f32x4*)(p.bias + n);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = mrow + i * 16;
+      if (GUARD && !(nok && m < p.M)) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = BI ? acc[i][j][e] * p.alpha + b[e] : acc[i][j][e] * p.alpha;
+        if (ST) {
+          s[j][e] += v[e];
+          ss[j][e] += v[e] * v[e];
+        }
+        if (RE) v[e] = fmaxf(v[e], 0.f);
+        else if (LR) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope;
+      }
+      if (GA) {
+        const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+      *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
+      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (ST) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[j][e] = dpp_sum16(s[j][e]);
+        ss[j][e] = dpp_sum16(ss[j][e]);
+      }
+    if ((lane & 15) == 0) {
+      float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int n = ncol + j * 16;
+        if (GUARD && n >= p.N) continue;
+        *(f32x4*)(row + n) = f32x4{s[j][0], s[j][1], s[j][2], s[j][3]};
+        *(f32x4*)(row + p.N + n) = f32x4{ss[j][0], ss[j][1], ss[j][2], ss[j][3]};
+      }
+    }
+  }
+}
+
+template <int MI, int NI, bool GUARD>
+RK_DEV void tile_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm,
+                          int lane) {
+  constexpr int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE;
+  switch (p.flags & (S_ | B_ | R_ | L_ | G_)) {
+    case 0: return tile_epi<MI, NI, 0, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case S_: return tile_epi<MI, NI, S_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case G_: return tile_epi<MI, NI, G_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case B_: return tile_epi<MI, NI, B_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case B_ | R_: return tile_epi<MI, NI, B_ | R_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case B_ | L_: return tile_epi<MI, NI, B_ | L_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    default: return tile_epi<MI, NI, -1, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+  }
+}
+
 template <int BM, int BN, int AM, int BMODE, int EPI, int NST>
 __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, SB = A_BYTES + B_BYTES;
@@ -593,76 +688,7 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
   const int mrow = m0 + wm * WM + (lane & 15);
   const int ncol = n0 + wn * WN + 4 * (lane >> 4);
   if constexpr (EPI == EPI_BF16) {
-    bf16* C = (bf16*)p.out;
-    float s[NI][4], ss[NI][4];
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[j][e] = ss[j][e] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = ncol + j * 16;
-      const bool nok = n < p.N;
-      float b[4] = {0.f, 0.f, 0.f, 0.f};
-      if ((p.flags & FLAG_BIAS) && nok) {
-        const f32x4 bv = *(const f32x4*)(p.bias + n);
-        b[0] = bv[0]; b[1] = bv[1]; b[2] = bv[2]; b[3] = bv[3];
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int m = mrow + i * 16;
-        if (!(nok && m < p.M)) continue;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = acc[i][j][e] * p.alpha + b[e];
-          s[j][e] += v[e];
-          ss[j][e] += v[e] * v[e];
-        }
-        if (p.flags & FLAG_RELU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        } else if (p.flags & FLAG_LRELU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope;
-        }
-        if (p.flags & FLAG_GATE) {
-          const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-        *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
-      }
-    }
-    if (p.flags & FLAG_STATS) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float a = s[j][e], b = ss[j][e];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            a += __shfl_xor(a, o, 64);
-            b += __shfl_xor(b, o, 64);
-          }
-          s[j][e] = a;
-          ss[j][e] = b;
-        }
-      if ((lane & 15) == 0) {
-        float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int n = ncol + j * 16;
-          if (n < p.N) {
-            *(f32x4*)(row + n) = f32x4{s[j][0], s[j][1], s[j][2], s[j][3]};
-            *(f32x4*)(row + p.N + n) = f32x4{ss[j][0], ss[j][1], ss[j][2], ss[j][3]};
-          }
-        }
-      }
-    }
+    tile_epilogue<MI, NI, true>(p, acc, mrow, ncol, mt, wm, lane);
   } else {
     float* C = (float*)p.out + (long long)blockIdx.z * p.slabStride;
 #pragma unroll
@@ -797,76 +823,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
   const int mrow = m0 + wm * WM + (lane & 15);
   const int ncol = n0 + wn * WN + 4 * (lane >> 4);
   if constexpr (EPI == EPI_BF16) {
-    bf16* C = (bf16*)p.out;
-    float s[NI][4], ss[NI][4];
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[j][e] = ss[j][e] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = ncol + j * 16;
-      const bool nok = n < p.N;
-      float b[4] = {0.f, 0.f, 0.f, 0.f};
-      if ((p.flags & FLAG_BIAS) && nok) {
-        const f32x4 bv = *(const f32x4*)(p.bias + n);
-        b[0] = bv[0]; b[1] = bv[1]; b[2] = bv[2]; b[3] = bv[3];
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int m = mrow + i * 16;
-        if (!(nok && m < p.M)) continue;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = acc[i][j][e] * p.alpha + b[e];
-          s[j][e] += v[e];
-          ss[j][e] += v[e] * v[e];
-        }
-        if (p.flags & FLAG_RELU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        } else if (p.flags & FLAG_LRELU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope;
-        }
-        if (p.flags & FLAG_GATE) {
-          const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-        *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
-      }
-    }
-    if (p.flags & FLAG_STATS) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float a = s[j][e], b = ss[j][e];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            a += __shfl_xor(a, o, 64);
-            b += __shfl_xor(b, o, 64);
-          }
-          s[j][e] = a;
-          ss[j][e] = b;
-        }
-      if ((lane & 15) == 0) {
-        float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int n = ncol + j * 16;
-          if (n < p.N) {
-            *(f32x4*)(row + n) = f32x4{s[j][0], s[j][1], s[j][2], s[j][3]};
-            *(f32x4*)(row + p.N + n) = f32x4{ss[j][0], ss[j][1], ss[j][2], ss[j][3]};
-          }
-        }
-      }
-    }
+    tile_epilogue<MI, NI, true>(p, acc, mrow, ncol, mt, wm, lane);
   } else {
     float* C = (float*)p.out + (long long)blockIdx.z * p.slabStride;
 #pragma unroll
@@ -949,100 +906,8 @@ RK_DEV bf16x8 patch_frag(const char* patch, int pp, int kb, int lane) {
   return *(const bf16x8*)(patch + pp * 128 + ((c ^ (pp & 7)) << 4));
 }
 
-// Sum over each 16-lane row of the wave with DPP lane permutes folded into the adds (no LDS
-// round trip, unlike __shfl_xor's ds_bpermute): quad xor 1, quad xor 2, half-row mirror, row mirror.
-RK_DEV float dpp_sum16(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
-  return v;
-}
-
-// Epilogue flag set FL is a template argument: with runtime flags hipcc if-converts every optional
-// step (activation, gate, statistics) into always-executed VALU + selects (~190 extra VALU per
-// tile).  hconv_epilogue dispatches the common sets to specialised copies.
-template <int MI, int NI, int FL>
-RK_DEV void hconv_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm, int lane) {
-  constexpr bool ST = FL & FLAG_STATS, BI = FL & FLAG_BIAS, RE = FL & FLAG_RELU, LR = FL & FLAG_LRELU,
-                 GA = FL & FLAG_GATE;
-  bf16* C = (bf16*)p.out;
-  float s[NI][4], ss[NI][4];
-#pragma unroll
-  for (int j = 0; j < NI; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s[j][e] = ss[j][e] = 0.f;
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int n = ncol + j * 16;
-    f32x4 b = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (BI) b = *(const f32x4*)(p.bias + n);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int m = mrow + i * 16;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = BI ? acc[i][j][e] * p.alpha + b[e] : acc[i][j][e] * p.alpha;
-        if constexpr (ST) {
-          s[j][e] += v[e];
-          ss[j][e] += v[e] * v[e];
-        }
-        if constexpr (RE) v[e] = fmaxf(v[e], 0.f);
-        if constexpr (LR) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope;
-      }
-      if constexpr (GA) {
-        const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-      *(bf16x4*)(C + (long long)m * p.ldc + n) = o;
-      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  if constexpr (ST) {
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s[j][e] = dpp_sum16(s[j][e]);
-        ss[j][e] = dpp_sum16(ss[j][e]);
-      }
-    if ((lane & 15) == 0) {
-      float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int n = ncol + j * 16;
-        *(f32x4*)(row + n) = f32x4{s[j][0], s[j][1], s[j][2], s[j][3]};
-        *(f32x4*)(row + p.N + n) = f32x4{ss[j][0], ss[j][1], ss[j][2], ss[j][3]};
-      }
-    }
-  }
-}
-
-template <int MI, int NI>
-RK_DEV void hconv_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm,
-                           int lane) {
-  constexpr int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE;
-  switch (p.flags & (S_ | B_ | R_ | L_ | G_)) {
-    case 0: return hconv_epi<MI, NI, 0>(p, acc, mrow, ncol, mt, wm, lane);
-    case S_: return hconv_epi<MI, NI, S_>(p, acc, mrow, ncol, mt, wm, lane);
-    case G_: return hconv_epi<MI, NI, G_>(p, acc, mrow, ncol, mt, wm, lane);
-    case B_: return hconv_epi<MI, NI, B_>(p, acc, mrow, ncol, mt, wm, lane);
-    case B_ | R_: return hconv_epi<MI, NI, B_ | R_>(p, acc, mrow, ncol, mt, wm, lane);
-    case B_ | L_: return hconv_epi<MI, NI, B_ | L_>(p, acc, mrow, ncol, mt, wm, lane);
-    case R_: return hconv_epi<MI, NI, R_>(p, acc, mrow, ncol, mt, wm, lane);
-    case L_: return hconv_epi<MI, NI, L_>(p, acc, mrow, ncol, mt, wm, lane);
-    case S_ | B_: return hconv_epi<MI, NI, S_ | B_>(p, acc, mrow, ncol, mt, wm, lane);
-    default: __builtin_trap();  // rejected on the host (rk_hconv)
-  }
-}
-
 template <int BM, int BN, int W, int BMODE, int FLIP>
-__global__ __launch_bounds__(256, 2) void hconv_kernel(const IgemmParams p, const int per_block) {
+__global__ __launch_bounds__(256, BN == 64 ? 2 : 1) void hconv_kernel(const IgemmParams p, const int per_block) {
   constexpr int TH = BM / W;                   // output rows per item
   constexpr int PC = W + 2, NPP = (TH + 2) * PC;
   constexpr int LP = (NPP * 8 + 255) / 256;    // patch DMA instructions per wave
@@ -1187,7 +1052,7 @@ __global__ __launch_bounds__(256, 2) void hconv_kernel(const IgemmParams p, cons
       }
     }
     if (cur.cc == NCC - 1)  // last chunk of this item: write it out
-      hconv_epilogue<MI, NI>(p, acc, cur.mt * BM + wm * WM + (lane & 15), cur.nt * BN + wn * WN + 4 * (lane >> 4),
+      tile_epilogue<MI, NI, false>(p, acc, cur.mt * BM + wm * WM + (lane & 15), cur.nt * BN + wn * WN + 4 * (lane >> 4),
                              cur.mt, wm, lane);
     cur = nxt;
     nxt = advance(nxt);
@@ -1218,6 +1083,149 @@ int launch_hconv_bn(bool dgrad, const IgemmParams& p, int grid, hipStream_t st) 
     case 32: return launch_hconv_w<128, BN, 32>(dgrad, p, grid, st);
   }
   return RK_EUNSUPPORTED;
+}
+
+// ================================================================================================
+// Halo-tiled 3x3 weight gradient, dW[co][tap][ci] = sum_p dy[p][co] * x[p + tap][ci].
+//
+// A block owns a (64 co x 64 ci x 9 taps) output tile and a contiguous run of pixel items (TH whole
+// image rows = 128 pixels; 64 at W = 8).  Per item it DMAs the dy tile [pixels][64 co] and ONE
+// halo patch of x [(TH+2)(W+2) pixels][64 ci] into LDS and runs all 9 taps out of that patch.  Wave
+// w owns ci 16w..16w+15 for all 64 co and 9 taps: 36 accumulators (144 AGPRs); per 32-pixel
+// K-block a wave reads 4 dy fragments (shared by the 9 taps) + 9 x fragments for 36 MFMAs.  Both
+// operands are K-outer (pixels are the reduction index), read with ds_read_b64_tr_b16; the tap
+// shift makes the first patch row of a read arbitrary, so the image uses the XOR
+// chunk ^ 2*(((row>>1)&1) | ((row>>3)&1)<<1), conflict-free for every start row (the two 4-row
+// blocks of a 32-lane half are 8 rows apart).  Items are double buffered.  Each block writes its
+// fp32 partial tile into slab blockIdx % S of [S][Cout][9*Cin]; rk_reduce_slabs sums the slabs.
+// ================================================================================================
+RK_DEV int wtr_off(int k, int ch) {
+  return k * 128 + ((ch ^ ((((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1)) << 4);
+}
+
+// 16 (M or N) x 32 (K) MFMA operand from a K-outer [rows = K][64 cols] image (wtr_off): K rows
+// kb0..kb0+7 of lane group g start at image row rowbase (consecutive), columns c0..c0+15.
+RK_DEV bf16x8 wtr_frag(const char* lds, int rowbase, int c0, int lane) {
+  const int ii = lane & 15, q = ii >> 2, pp = ii & 3;
+  const int ch = (c0 >> 3) + (pp >> 1);
+  const int a0 = wtr_off(rowbase + q, ch) + 8 * (pp & 1);
+  const int a1 = wtr_off(rowbase + q + 4, ch) + 8 * (pp & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + a1));
+  const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+  bf16x8 f;
+  f[0] = l4[0]; f[1] = l4[1]; f[2] = l4[2]; f[3] = l4[3];
+  f[4] = h4[0]; f[5] = h4[1]; f[6] = h4[2]; f[7] = h4[3];
+  return f;
+}
+
+template <int W>
+__global__ __launch_bounds__(256, 1) void hconv_wgrad_kernel(const IgemmParams p, const int S, const int per_block) {
+  constexpr int P = W == 8 ? 64 : 128;         // pixels per item
+  constexpr int TH = P / W, PC = W + 2, NPP = (TH + 2) * PC;
+  constexpr int LP = (NPP * 8 + 255) / 256;    // patch DMA instructions per wave
+  constexpr int LY = P / 32;                   // dy-tile DMA instructions per wave
+  constexpr int P_BYTES = LP * 4 * 1024, Y_BYTES = P * 128, SB = P_BYTES + Y_BYTES;
+  constexpr int LOG2W = W == 8 ? 3 : W == 16 ? 4 : 5;
+  constexpr int KB = P / 32;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int log2C = p.log2C;                   // Cin (x channels)
+  const int Cout = p.M;
+  const int tilesCi = p.C >> 6;
+  const int tile = blockIdx.x / S, sl = blockIdx.x - tile * S;
+  const int cot = tile / tilesCi, cit = tile - cot * tilesCi;
+  const int co0 = cot * 64, ci0 = cit * 64;
+  const int nItems = p.K / P;                  // K = pixels
+  const int item0 = sl * per_block;
+  const int item1 = min(nItems, item0 + per_block);
+  const int tilesPerImg = (p.H * W) / P;
+
+  const __amdgpu_buffer_rsrc_t rX = make_rsrc(p.B, p.bytesB);   // x  [pixels][Cin]
+  const __amdgpu_buffer_rsrc_t rY = make_rsrc(p.A, p.bytesA);   // dy [pixels][Cout]
+
+  int prel[LP], prow[LP];
+#pragma unroll
+  for (int q = 0; q < LP; ++q) {
+    const int slot = (wid * LP + q) * 64 + lane;
+    const int pp = slot >> 3;
+    const int c = (slot & 7) ^ ((((pp >> 1) & 1) | (((pp >> 3) & 1) << 1)) << 1);
+    const int pr = pp / PC, pcol = pp - pr * PC;
+    const bool ok = pp < NPP && pcol >= 1 && pcol <= W;
+    prel[q] = ((((pr - 1) * W + (pcol - 1)) << log2C) << 1) + c * 16;
+    prow[q] = ok ? pr : -1000;
+  }
+  unsigned yoff[LY];
+#pragma unroll
+  for (int q = 0; q < LY; ++q) {
+    const int slot = (wid * LY + q) * 64 + lane;
+    const int krow = slot >> 3;
+    const int c = (slot & 7) ^ ((((krow >> 1) & 1) | (((krow >> 3) & 1) << 1)) << 1);
+    yoff[q] = ((unsigned)krow * (unsigned)Cout + (unsigned)c * 8u) * 2u;
+  }
+  // first patch row of each lane group's 8 pixels in K-block kb (before the tap shift)
+  int prb[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int k = kb * 32 + 8 * (lane >> 4);
+    prb[kb] = ((k >> LOG2W) + 1) * PC + (k & (W - 1)) + 1;
+  }
+
+  auto issue = [&](int it, int buf) {
+    const int r0 = (it & (tilesPerImg - 1)) * TH;  // tilesPerImg is a power of two
+    const int pbase = (((it * P) << log2C) << 1) + ci0 * 2;
+    char* dst = smem + buf * SB;
+#pragma unroll
+    for (int q = 0; q < LP; ++q) {
+      const bool in = (unsigned)(r0 - 1 + prow[q]) < (unsigned)p.H;
+      dma16(rX, dst + (wid * LP + q) * 1024, in ? pbase + prel[q] : (int)OOB);
+    }
+    const unsigned ybase = ((unsigned)(it * P) * (unsigned)Cout + (unsigned)co0) * 2u;
+#pragma unroll
+    for (int q = 0; q < LY; ++q) dma16(rY, dst + P_BYTES + (wid * LY + q) * 1024, (int)(ybase + yoff[q]));
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (item0 < item1) issue(item0, 0);
+  for (int it = item0; it < item1; ++it) {
+    const int buf = (it - item0) & 1;
+    wait_vmcnt<0>();
+    raw_barrier();
+    if (it + 1 < item1) issue(it + 1, buf ^ 1);
+    const char* pt = smem + buf * SB;
+    const char* yt = pt + P_BYTES;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = wtr_frag(yt, kb * 32 + 8 * (lane >> 4), 16 * i, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const bf16x8 bt = wtr_frag(pt, prb[kb] + tap_dy(t) * PC + tap_dx(t), 16 * wid, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bt, af[i], acc[i][t], 0, 0, 0);
+      }
+    }
+  }
+  // partial tile -> slab sl: lane owns dW[co0 + 16i + (lane&15)][t][ci0 + 16 wid + 4(lane>>4) .. +3]
+  float* out = (float*)p.out + (long long)sl * p.slabStride;
+  const int N = p.N;  // 9 * Cin
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = co0 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int n = (t << log2C) + ci0 + 16 * wid + 4 * (lane >> 4);
+      *(f32x4*)(out + (long long)co * N + n) = acc[i][t];
+    }
+  }
 }
 
 }  // namespace
@@ -1293,13 +1301,6 @@ extern "C" int rk_hconv(int dgrad, int tile, const void* A, const void* B, void*
   if (rk_log2(H) < 0 || (H * W) % BM != 0 || M <= 0 || M % (H * W) != 0) return RK_EUNSUPPORTED;
   if (rk_log2(Cch) < 6 || N <= 0 || N % BN != 0 || K != 9 * Cch) return RK_EUNSUPPORTED;
   if (ldb != (dgrad ? 9 * N : K)) return RK_EBADARG;
-  {
-    const int f = flags & (FLAG_STATS | FLAG_BIAS | FLAG_RELU | FLAG_LRELU | FLAG_GATE);
-    const int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE;
-    if (!(f == 0 || f == S_ || f == G_ || f == B_ || f == (B_ | R_) || f == (B_ | L_) || f == R_ || f == L_ ||
-          f == (S_ | B_)))
-      return RK_EUNSUPPORTED;  // epilogue flag set without a specialised copy (see hconv_epilogue)
-  }
   IgemmParams p{};
   p.A = (const bf16*)A; p.B = (const bf16*)B; p.out = C; p.bias = bias; p.stats = stats;
   p.gate = (const bf16*)gate;
@@ -1310,4 +1311,36 @@ extern "C" int rk_hconv(int dgrad, int tile, const void* A, const void* B, void*
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   hipStream_t st = (hipStream_t)stream;
   return BN == 128 ? launch_hconv_bn<128>(dgrad != 0, p, grid, st) : launch_hconv_bn<64>(dgrad != 0, p, grid, st);
+}
+
+// Halo-tiled 3x3 weight gradient (see hconv_wgrad_kernel) into fp32 slabs [S][Cout][9*Cin]:
+// dy [pixels][Cout], x [pixels][Cin] (NHWC, pixels = Nb*H*W).  Every slab element is written
+// (blocks of slab s cover all tiles); sum the slabs with rk_reduce_slabs.  S = blocks per tile.
+extern "C" int rk_hconv_wgrad(const void* dy, const void* x, float* slab, int Nb, int H, int W, int Cin, int Cout,
+                              int S, long long bytesY, long long bytesX, void* stream) {
+  if (bytesY <= 0 || bytesX <= 0 || bytesY >= (1ll << 31) || bytesX >= (1ll << 31)) return RK_EUNSUPPORTED;
+  if (W != 8 && W != 16 && W != 32) return RK_EUNSUPPORTED;
+  const int P = W == 8 ? 64 : 128;
+  if (rk_log2(H) < 0 || (H * W) % P != 0 || Nb <= 0) return RK_EUNSUPPORTED;
+  if (rk_log2(Cin) < 6 || Cout % 64 != 0 || S <= 0) return RK_EUNSUPPORTED;
+  IgemmParams p{};
+  p.A = (const bf16*)dy; p.B = (const bf16*)x; p.out = slab;
+  p.M = Cout; p.N = 9 * Cin; p.K = Nb * H * W;
+  p.H = H; p.W = W; p.C = Cin; p.taps = 9;
+  p.log2H = rk_log2(H); p.log2W = rk_log2(W); p.log2C = rk_log2(Cin);
+  p.slabStride = (long long)Cout * 9 * Cin;
+  p.bytesA = (unsigned long long)bytesY; p.bytesB = (unsigned long long)bytesX;
+  const int items = p.K / P;
+  const int per = rk_cdiv(items, S);
+  const int tiles = (Cout / 64) * (Cin / 64);
+  // S is fixed (the caller sized the slab array); blocks past the last item write zero tiles
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(tiles * S);
+  switch (W) {
+    case 8: hipLaunchKernelGGL((hconv_wgrad_kernel<8>), grid, dim3(256), 0, st, p, S, per); break;
+    case 16: hipLaunchKernelGGL((hconv_wgrad_kernel<16>), grid, dim3(256), 0, st, p, S, per); break;
+    default: hipLaunchKernelGGL((hconv_wgrad_kernel<32>), grid, dim3(256), 0, st, p, S, per); break;
+  }
+  RK_LAUNCH_CHECK();
+  return RK_OK;
 }

@@ -263,6 +263,12 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
     if out is None:
         out = torch.empty((Cout, N), device=dy.device, dtype=torch.float32)
     def run(cfg):
+        if cfg[0] == 'hw':
+            s = cfg[1]
+            slab = torch.empty((s, M, N), device=dy.device, dtype=torch.float32)
+            hconv_wgrad(dy, x, slab, s)
+            reduce_slabs(slab, out, accumulate=accumulate)
+            return
         tile, s = cfg
         if s == 1:
             igemm(KIND_CONV_WGRAD, 1, dy, x, out, M, N, K, Cout, 0, N, H=H, W=W, C=Cin, taps=taps, splits=1,
@@ -276,9 +282,34 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
         t0 = pick_tile(M, N)
         run((t0, splits))
         return out
-    cands = _split_candidates(M, N, K)
+    cands = _split_candidates(M, N, K) + _hconv_wgrad_candidates(Nb, H, W, Cin, Cout, taps)
     run(_tuned(('cw', M, N, K, H, W, Cin, taps, bool(accumulate)), cands, run) if not accumulate else cands[0])
     return out
+
+
+def _hconv_wgrad_candidates(Nb, H, W, Cin, Cout, taps):
+    if not HCONV or taps != 9 or W not in (8, 16, 32) or H & (H - 1) or Cin < 64 or Cin & (Cin - 1) or Cout % 64:
+        return []
+    P = 64 if W == 8 else 128
+    if (H * W) % P:
+        return []
+    items = Nb * H * W // P
+    tiles = (Cout // 64) * (Cin // 64)
+    out = []
+    for blocks in (NUM_CU // 2, NUM_CU, 2 * NUM_CU):
+        s = max(1, min(items, blocks // tiles))
+        c = ('hw', s)
+        if c not in out and s * Cout * 9 * Cin * 4 <= (256 << 20):
+            out.append(c)
+    return out
+
+
+def hconv_wgrad(dy, x, slab, S):
+    """Halo-tiled weight gradient into fp32 slabs [S][Cout][9*Cin] (sum them with reduce_slabs)."""
+    Nb, H, W, Cout = dy.shape
+    Cin = x.shape[-1]
+    _lib.call("rk_hconv_wgrad", _p(dy), _p(x), _p(slab), Nb, H, W, Cin, Cout, int(S), _nbytes(dy), _nbytes(x), _s())
+    return slab
 
 
 # ----------------------------------------------------------------------------------------- dense

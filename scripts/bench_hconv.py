@@ -30,8 +30,26 @@ def main():
         stats = torch.empty(M // 64 * 2, 2, cout, device=dev)
         dy = torch.randn(B, hw, hw, cout, device=dev).bfloat16()
         dx = torch.empty(B, hw, hw, cin, device=dev, dtype=torch.bfloat16)
-        for kind in ('fwd', 'dgrad'):
-            if kind == 'fwd':
+        for kind in ('fwd', 'dgrad', 'wgrad'):
+            if kind == 'wgrad':
+                gw = torch.empty(cout, K, device=dev)
+                cands = F._split_candidates(cout, K, M) + F._hconv_wgrad_candidates(B, hw, hw, cin, cout, 9)
+
+                def run(cfg):
+                    if cfg[0] == 'hw':
+                        slab = torch.empty((cfg[1], cout, K), device=dev)
+                        F.hconv_wgrad(dy, x, slab, cfg[1])
+                        F.reduce_slabs(slab, gw)
+                        return
+                    t, s = cfg
+                    slab = torch.empty((s, cout, K), device=dev)
+                    F.igemm(F.KIND_CONV_WGRAD, 1, dy, x, slab, cout, K, M, cout, 0, K, H=hw, W=hw, C=cin, taps=9,
+                            splits=s, slab_stride=cout * K, tile=t)
+                    F.reduce_slabs(slab, gw)
+                N, C = cout, cin
+            elif False:
+                pass
+            elif kind == 'fwd':
                 N, C = cout, cin
                 cands = F._tile_candidates(M, N) + F._hconv_candidates(M, N, hw, hw, C, 9)
 
@@ -57,10 +75,10 @@ def main():
                 for c in cands:
                     t = autotune._time_graph(c, run, 5) * 1e3
                     times[c] = min(times.get(c, 1e9), t)
-            ig = min((t, c) for c, t in times.items() if c[0] != 'h')
-            hc = [(t, c) for c, t in times.items() if c[0] == 'h']
+            ig = min((t, c) for c, t in times.items() if c[0] not in ('h', 'hw'))
+            hc = [(t, c) for c, t in times.items() if c[0] in ('h', 'hw')]
             hb = min(hc) if hc else (float('nan'), None)
-            flops = 2.0 * M * N * 9 * C
+            flops = 2.0 * M * cin * cout * 9
             r = {'layer': f'{hw}x{hw} {cin}->{cout}', 'kind': kind, 'igemm_us': round(ig[0], 2), 'igemm_cfg': ig[1],
                  'hconv_us': round(hb[0], 2), 'hconv_cfg': hb[1],
                  'igemm_tflops': round(flops / ig[0] / 1e6, 1),

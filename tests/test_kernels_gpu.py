@@ -218,3 +218,20 @@ def test_hconv_fwd_dgrad(fn, N, H, W, Cin, Cout, bn_bit, grid):
     xr = _nhwc_to_nchw(x.float()).requires_grad_(True)
     F.conv2d(xr, _w_to_oihw(w.float()), padding=1).backward(_nhwc_to_nchw(dy.float()))
     assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,S", [(2, 32, 32, 64, 64, 3), (2, 16, 16, 128, 128, 4), (4, 8, 8, 256, 64, 5),
+                                              (1, 16, 16, 64, 128, 1), (3, 32, 32, 64, 128, 64)])
+def test_hconv_wgrad(fn, N, H, W, Cin, Cout, S):
+    """Halo-tiled weight gradient (slabs + reduce) vs PyTorch fp32 (incl. more slabs than items)."""
+    torch.manual_seed(12)
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    slab = torch.full((S, Cout, 9 * Cin), float('nan'), device=DEV)
+    fn.hconv_wgrad(dy, x, slab, S)
+    out = torch.empty(Cout, 9 * Cin, device=DEV)
+    fn.reduce_slabs(slab, out)
+    w = torch.zeros(Cout, Cin, 3, 3, device=DEV, requires_grad=True)
+    F.conv2d(_nhwc_to_nchw(x.float()), w, padding=1).backward(_nhwc_to_nchw(dy.float()))
+    ref = w.grad.permute(0, 2, 3, 1).reshape(Cout, -1)
+    assert rel_err(out, ref) < 2e-3
