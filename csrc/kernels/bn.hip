@@ -132,10 +132,30 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* be
 }
 
 // ---- apply: out = act(y*scale + shift) [maxpool 2x2] ----------------------------------------
-template <int POOL, int ACT>
-__global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
-                                                         const float* __restrict__ shift, bf16* __restrict__ out,
-                                                         int N, int H, int W, int C, float slope) {
+// Per-channel coefficients come from global memory (after rk_bn_finalize_fwd) or from LDS (the
+// fused-finalize variant below computes them in its prologue): the body is shared.
+struct CoefLds {
+  const float* sc;  // __shared__ arrays (inlined: the compiler sees the LDS address space)
+  const float* sh;
+  RK_DEV void load(int cc, float (&a)[8], float (&b)[8]) const {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a[e] = sc[cc * 8 + e]; b[e] = sh[cc * 8 + e]; }
+  }
+};
+struct CoefPtr {
+  const float* sc;
+  const float* sh;
+  RK_DEV void load(int cc, float (&a)[8], float (&b)[8]) const {
+    *(f32x4*)&a[0] = *(const f32x4*)(sc + cc * 8);
+    *(f32x4*)&a[4] = *(const f32x4*)(sc + cc * 8 + 4);
+    *(f32x4*)&b[0] = *(const f32x4*)(sh + cc * 8);
+    *(f32x4*)&b[4] = *(const f32x4*)(sh + cc * 8 + 4);
+  }
+};
+
+template <int POOL, int ACT, class CS>
+RK_DEV void bn_act_fwd_body(const CS& cs, const bf16* __restrict__ y, bf16* __restrict__ out, int N, int H, int W,
+                            int C, float slope) {
   const int CC = C >> 3;
   const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
   const long long total = (long long)N * Ho * Wo * CC;
@@ -144,10 +164,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict_
     const int cc = (int)(idx % CC);
     const long long pix = idx / CC;
     float sc[8], sh[8];
-    *(f32x4*)&sc[0] = *(const f32x4*)(scale + cc * 8);
-    *(f32x4*)&sc[4] = *(const f32x4*)(scale + cc * 8 + 4);
-    *(f32x4*)&sh[0] = *(const f32x4*)(shift + cc * 8);
-    *(f32x4*)&sh[4] = *(const f32x4*)(shift + cc * 8 + 4);
+    cs.load(cc, sc, sh);
     float o[8];
     if constexpr (!POOL) {
       float f[8];
@@ -174,6 +191,64 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict_
   }
 }
 
+template <int POOL, int ACT>
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, bf16* __restrict__ out,
+                                                         int N, int H, int W, int C, float slope) {
+  bn_act_fwd_body<POOL, ACT>(CoefPtr{scale, shift}, y, out, N, H, W, C, slope);
+}
+
+// ---- fused finalize + apply ---------------------------------------------------------------------
+// Statistics arrive as fp64 sums in SL slots [SL][2][C] (atomically accumulated by the conv
+// epilogue, igemm FLAG_SATOM): every block folds them into scale/shift in LDS (8 KiB of reads per
+// block, the grid is capped at 1024 blocks), block 0 also publishes mean/rstd/scale/shift and
+// updates the running statistics.  Replaces rows_reduce + bn_finalize_fwd (two launches).
+constexpr int FUSED_MAX_C = 1024;
+
+RK_DEV void acc_sums(const double* __restrict__ acc, int SL, int C, int c, double& a, double& b) {
+  a = 0.0;
+  b = 0.0;
+  for (int s = 0; s < SL; ++s) {
+    a += acc[(long long)(2 * s) * C + c];
+    b += acc[(long long)(2 * s + 1) * C + c];
+  }
+}
+
+template <int POOL, int ACT>
+__global__ __launch_bounds__(256) void bn_act_fwd_acc_kernel(const bf16* __restrict__ y, const double* __restrict__ acc,
+                                                             int SL, double count, const float* gamma,
+                                                             const float* beta, float eps, float* run_mean,
+                                                             float* run_var, float momentum, float* coeffs,
+                                                             bf16* __restrict__ out, int N, int H, int W, int C,
+                                                             float slope) {
+  __shared__ __attribute__((aligned(16))) float s_sc[FUSED_MAX_C], s_sh[FUSED_MAX_C];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double s, q;
+    acc_sums(acc, SL, C, c, s, q);
+    const double mu = s / count;
+    double var = q / count - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const float r = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    const float sc = g * r, sh = b - (float)mu * g * r;
+    s_sc[c] = sc;
+    s_sh[c] = sh;
+    if (blockIdx.x == 0) {
+      coeffs[c] = (float)mu;
+      coeffs[C + c] = r;
+      coeffs[2 * C + c] = sc;
+      coeffs[3 * C + c] = sh;
+      if (run_mean) {
+        const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mu;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
+      }
+    }
+  }
+  __syncthreads();
+  bn_act_fwd_body<POOL, ACT>(CoefLds{s_sc, s_sh}, y, out, N, H, W, C, slope);
+}
+
 // ---- backward pass 1: per-block partial (sum dz, sum dz*y) ------------------------------------
 // dz = d(act)/dz * (pool-routed upstream gradient), z = y*scale + shift recomputed from y.
 // sum dz*xhat = rstd*(sum dz*y - mean*sum dz) is formed in the finalize kernel, so this streaming
@@ -185,7 +260,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             float* __restrict__ part, int N, int H, int W, int C,
-                                                            float slope) {
+                                                            float slope, double* __restrict__ acc, int slmask) {
   extern __shared__ float red[];  // [PL][2][C]
   constexpr int U = POOL ? 2 : 4;
   const int CC = C >> 3;
@@ -281,10 +356,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
     }
   }
   __syncthreads();
+  // acc != null: add the block's row into fp64 slot (block & slmask) of [SL][2][C] (consumed by the
+  // fused finalize of bn_bwd_apply_acc_kernel); else write partial row blockIdx of [R][2][C]
+  double* dst = acc ? acc + (long long)(blockIdx.x & slmask) * 2 * C : nullptr;
   for (int i = tid; i < 2 * C; i += 256) {
     float a = 0.f;
     for (int q = 0; q < PL; ++q) a += red[q * 2 * C + i];
-    part[(long long)blockIdx.x * 2 * C + i] = a;
+    if (dst) unsafeAtomicAdd(dst + i, (double)a);
+    else part[(long long)blockIdx.x * 2 * C + i] = a;
   }
 }
 
@@ -322,12 +401,43 @@ __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float* __res
 }
 
 // ---- backward pass 3: dy = k1*dz + k2*y + k3 ---------------------------------------------------
-template <int POOL, int ACT>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y,
-                                                           const float* __restrict__ scale,
-                                                           const float* __restrict__ shift,
-                                                           const float* __restrict__ coef, bf16* __restrict__ dy,
-                                                           int N, int H, int W, int C, float slope) {
+struct BwdCoefPtr {
+  const float* sc;
+  const float* sh;
+  const float* coef;  // [3][C]
+  int C;
+  RK_DEV void load(int cc, float (&a)[8], float (&b)[8], float (&k1)[8], float (&k2)[8], float (&k3)[8]) const {
+    *(f32x4*)&a[0] = *(const f32x4*)(sc + cc * 8);
+    *(f32x4*)&a[4] = *(const f32x4*)(sc + cc * 8 + 4);
+    *(f32x4*)&b[0] = *(const f32x4*)(sh + cc * 8);
+    *(f32x4*)&b[4] = *(const f32x4*)(sh + cc * 8 + 4);
+    *(f32x4*)&k1[0] = *(const f32x4*)(coef + cc * 8);
+    *(f32x4*)&k1[4] = *(const f32x4*)(coef + cc * 8 + 4);
+    *(f32x4*)&k2[0] = *(const f32x4*)(coef + C + cc * 8);
+    *(f32x4*)&k2[4] = *(const f32x4*)(coef + C + cc * 8 + 4);
+    *(f32x4*)&k3[0] = *(const f32x4*)(coef + 2 * C + cc * 8);
+    *(f32x4*)&k3[4] = *(const f32x4*)(coef + 2 * C + cc * 8 + 4);
+  }
+};
+struct BwdCoefLds {
+  const float* sc;  // __shared__
+  const float* sh;
+  const float* k;   // __shared__ [3][FUSED_MAX_C]
+  RK_DEV void load(int cc, float (&a)[8], float (&b)[8], float (&k1)[8], float (&k2)[8], float (&k3)[8]) const {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] = sc[cc * 8 + e];
+      b[e] = sh[cc * 8 + e];
+      k1[e] = k[cc * 8 + e];
+      k2[e] = k[FUSED_MAX_C + cc * 8 + e];
+      k3[e] = k[2 * FUSED_MAX_C + cc * 8 + e];
+    }
+  }
+};
+
+template <int POOL, int ACT, class CS>
+RK_DEV void bn_bwd_apply_body(const CS& cs, const bf16* __restrict__ dout, const bf16* __restrict__ y,
+                              bf16* __restrict__ dy, int N, int H, int W, int C, float slope) {
   const int CC = C >> 3;
   const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
   const long long total = (long long)N * Ho * Wo * CC;
@@ -351,16 +461,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
       for (int q = 0; q < 4; ++q) yv[q] = *(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C);
     }
     float sc[8], sh[8], k1[8], k2[8], k3[8];
-    *(f32x4*)&sc[0] = *(const f32x4*)(scale + cc * 8);
-    *(f32x4*)&sc[4] = *(const f32x4*)(scale + cc * 8 + 4);
-    *(f32x4*)&sh[0] = *(const f32x4*)(shift + cc * 8);
-    *(f32x4*)&sh[4] = *(const f32x4*)(shift + cc * 8 + 4);
-    *(f32x4*)&k1[0] = *(const f32x4*)(coef + cc * 8);
-    *(f32x4*)&k1[4] = *(const f32x4*)(coef + cc * 8 + 4);
-    *(f32x4*)&k2[0] = *(const f32x4*)(coef + C + cc * 8);
-    *(f32x4*)&k2[4] = *(const f32x4*)(coef + C + cc * 8 + 4);
-    *(f32x4*)&k3[0] = *(const f32x4*)(coef + 2 * C + cc * 8);
-    *(f32x4*)&k3[4] = *(const f32x4*)(coef + 2 * C + cc * 8 + 4);
+    cs.load(cc, sc, sh, k1, k2, k3);
     float g[8];
     unpack8(gv, g);
     if constexpr (!POOL) {
@@ -399,6 +500,54 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
       }
     }
   }
+}
+
+template <int POOL, int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ coef, bf16* __restrict__ dy,
+                                                           int N, int H, int W, int C, float slope) {
+  bn_bwd_apply_body<POOL, ACT>(BwdCoefPtr{scale, shift, coef, C}, dout, y, dy, N, H, W, C, slope);
+}
+
+// Fused backward finalize + apply: (sum dz, sum dz*y) arrive as fp64 sums in SL slots
+// (rk_bn_bwd_reduce with an accumulator); each block forms k1/k2/k3 in LDS, block 0 also writes
+// dgamma/dbeta and coef (the odd-pool edge kernel reads it).  Replaces rk_bn_finalize_bwd.
+template <int POOL, int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const bf16* __restrict__ dout,
+                                                               const bf16* __restrict__ y,
+                                                               const float* __restrict__ coeffs,
+                                                               const double* __restrict__ acc, int SL, double count,
+                                                               const float* gamma, float* dgamma, float* dbeta,
+                                                               float* coef, int accumulate, bf16* __restrict__ dy,
+                                                               int N, int H, int W, int C, float slope) {
+  __shared__ __attribute__((aligned(16))) float s_sc[FUSED_MAX_C], s_sh[FUSED_MAX_C], s_k[3 * FUSED_MAX_C];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double sdz, sdzy;
+    acc_sums(acc, SL, C, c, sdz, sdzy);
+    const double mu = coeffs[c], r = coeffs[C + c];
+    const double g = gamma ? gamma[c] : 1.0;
+    const double db = sdz;
+    const double dg = r * (sdzy - mu * sdz);  // sum dz * xhat
+    const double k1 = g * r;
+    const double k2 = -g * r * r * dg / count;
+    const double k3 = -g * r * db / count - k2 * mu;
+    s_sc[c] = coeffs[2 * C + c];
+    s_sh[c] = coeffs[3 * C + c];
+    s_k[c] = (float)k1;
+    s_k[FUSED_MAX_C + c] = (float)k2;
+    s_k[2 * FUSED_MAX_C + c] = (float)k3;
+    if (blockIdx.x == 0) {
+      if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)dg;
+      if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)db;
+      coef[c] = (float)k1;
+      coef[C + c] = (float)k2;
+      coef[2 * C + c] = (float)k3;
+    }
+  }
+  __syncthreads();
+  bn_bwd_apply_body<POOL, ACT>(BwdCoefLds{s_sc, s_sh, s_k}, dout, y, dy, N, H, W, C, slope);
 }
 
 // odd H or W with 2x2 pooling (VGG16 at 48x48 pools 3x3 -> 1x1): the last row / column belongs to
@@ -513,7 +662,56 @@ extern "C" int rk_bn_bwd_reduce(const void* dout, const void* y, const float* sc
   RK_DISPATCH_POOL_ACT(pool, act,
                        hipLaunchKernelGGL((bn_bwd_reduce_kernel<P_, A_>), dim3(rows), dim3(256), red_lds_bytes(C),
                                           (hipStream_t)stream, (const bf16*)dout, (const bf16*)y, scale, shift, part,
-                                          N, H, W, C, slope));
+                                          N, H, W, C, slope, (double*)nullptr, 0));
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// Same reduction, accumulated atomically (fp64) into the SL-slot table acc [SL][2][C] (SL a power of
+// two; the caller zeroes it) for rk_bn_bwd_apply_acc.
+extern "C" int rk_bn_bwd_reduce_acc(const void* dout, const void* y, const float* scale, const float* shift,
+                                    double* acc, int SL, int rows, int N, int H, int W, int C, int pool, int act,
+                                    float slope, void* stream) {
+  if (C % 8 || C > FUSED_MAX_C || SL <= 0 || (SL & (SL - 1))) return RK_EUNSUPPORTED;
+  RK_DISPATCH_POOL_ACT(pool, act,
+                       hipLaunchKernelGGL((bn_bwd_reduce_kernel<P_, A_>), dim3(rows), dim3(256), red_lds_bytes(C),
+                                          (hipStream_t)stream, (const bf16*)dout, (const bf16*)y, scale, shift,
+                                          (float*)nullptr, N, H, W, C, slope, acc, SL - 1));
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_bn_bwd_apply_acc(const void* dout, const void* y, const float* coeffs, const double* acc, int SL,
+                                   double count, const float* gamma, float* dgamma, float* dbeta, float* coef,
+                                   int accumulate, void* dy, int N, int H, int W, int C, int pool, int act,
+                                   float slope, void* stream) {
+  if (C % 8 || C > FUSED_MAX_C) return RK_EUNSUPPORTED;
+  const long long work = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 8);
+  const dim3 grid(grid_for(work, 256, 1024));
+  RK_DISPATCH_POOL_ACT(pool, act,
+                       hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<P_, A_>), grid, dim3(256), 0, (hipStream_t)stream,
+                                          (const bf16*)dout, (const bf16*)y, coeffs, acc, SL, count, gamma, dgamma,
+                                          dbeta, coef, accumulate, (bf16*)dy, N, H, W, C, slope));
+  RK_LAUNCH_CHECK();
+  if (pool && ((H & 1) || (W & 1))) {
+    hipLaunchKernelGGL(bn_bwd_edge_kernel, dim3(grid_for((long long)N * H * W * (C / 8), 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16*)y, (const float*)coef, (bf16*)dy, N, H, W, C);
+    RK_LAUNCH_CHECK();
+  }
+  return RK_OK;
+}
+
+extern "C" int rk_bn_act_fwd_acc(const void* y, const double* acc, int SL, double count, const float* gamma,
+                                 const float* beta, float eps, float* run_mean, float* run_var, float momentum,
+                                 float* coeffs, void* out, int N, int H, int W, int C, int pool, int act, float slope,
+                                 void* stream) {
+  if (C % 8 || C > FUSED_MAX_C) return RK_EUNSUPPORTED;
+  const long long work = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 8);
+  const dim3 grid(grid_for(work, 256, 1024));
+  RK_DISPATCH_POOL_ACT(pool, act,
+                       hipLaunchKernelGGL((bn_act_fwd_acc_kernel<P_, A_>), grid, dim3(256), 0, (hipStream_t)stream,
+                                          (const bf16*)y, acc, SL, count, gamma, beta, eps, run_mean, run_var,
+                                          momentum, coeffs, (bf16*)out, N, H, W, C, slope));
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

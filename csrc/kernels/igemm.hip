@@ -39,8 +39,10 @@ enum OpMode {
   OP_CONVUP_KIN = 6,  // NHWC gather from a 2x nearest-upscaled input (fused upscale2d + conv3x3)
 };
 enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
+// FLAG_SATOM (with FLAG_STATS): add the per-wave (sum, sumsq) into fp64 slots [SL][2][N] at p.stats
+// with device-scope atomics instead of writing partial rows; slot = blockIdx & ((flags >> 12) & 15).
 enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16, FLAG_NOFAST = 64,
-             FLAG_LRELU = 32 };
+             FLAG_LRELU = 32, FLAG_SATOM = 256 };
 
 struct IgemmParams {
   const bf16* A;
@@ -571,7 +573,24 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
         s[j][e] = dpp_sum16(s[j][e]);
         ss[j][e] = dpp_sum16(ss[j][e]);
       }
-    if ((lane & 15) == 0) {
+    if (fl & FLAG_SATOM) {
+      // every lane of a 16-lane row holds the row's 8*NI sums: lane l adds value l (+16k)
+      double* accd = (double*)p.stats + (long long)(blockIdx.x & ((p.flags >> 12) & 15)) * 2 * p.N;
+      const int l16 = lane & 15;
+#pragma unroll
+      for (int k = 0; k < NI / 2; ++k) {
+        const int v = l16 + 16 * k;
+        const int kind = v / (4 * NI), r = v - kind * 4 * NI, jsel = r >> 2, esel = r & 3;
+        float val = 0.f;
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (j == jsel && e == esel) val = kind ? ss[j][e] : s[j][e];
+        const int n = ncol + jsel * 16 + esel;
+        if (!GUARD || n < p.N) unsafeAtomicAdd(accd + kind * p.N + n, (double)val);
+      }
+    } else if ((lane & 15) == 0) {
       float* row = p.stats + (long long)(mt * 2 + wm) * 2 * p.N;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -587,10 +606,11 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
 template <int MI, int NI, bool GUARD>
 RK_DEV void tile_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm,
                           int lane) {
-  constexpr int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE;
-  switch (p.flags & (S_ | B_ | R_ | L_ | G_)) {
+  constexpr int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE, A_ = FLAG_SATOM;
+  switch (p.flags & (S_ | B_ | R_ | L_ | G_ | A_)) {
     case 0: return tile_epi<MI, NI, 0, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case S_: return tile_epi<MI, NI, S_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case S_ | A_: return tile_epi<MI, NI, S_ | A_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case G_: return tile_epi<MI, NI, G_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case B_: return tile_epi<MI, NI, B_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case B_ | R_: return tile_epi<MI, NI, B_ | R_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);

@@ -212,12 +212,20 @@ class ConvNetEngine:
         acts = [x]
         saved = []
         h = x
+        accs = self._bn_accumulators() if self._use_bn_acc() else None
+        if accs is not None:
+            self._bn_acc_flat.zero_()  # one memset node for every layer's fp64 statistic slots
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
-            y, stats = F.conv_fwd(h, fl.wb(name + '.w'), want_stats=True)
             rm, rv = self.running_stats(bi)
-            coeffs = F.bn_finalize_fwd(stats, B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'), self.bn_eps,
-                                       rm, rv, self.bn_momentum)
-            h = F.bn_act_fwd(y, coeffs[2], coeffs[3], pool=pool, act=F.ACT_RELU)
+            if accs is not None:
+                y, _ = F.conv_fwd(h, fl.wb(name + '.w'), stats_acc=accs[bi][0])
+                h, coeffs = F.bn_act_fwd_acc(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
+                                             self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
+            else:
+                y, stats = F.conv_fwd(h, fl.wb(name + '.w'), want_stats=True)
+                coeffs = F.bn_finalize_fwd(stats, B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
+                                           self.bn_eps, rm, rv, self.bn_momentum)
+                h = F.bn_act_fwd(y, coeffs[2], coeffs[3], pool=pool, act=F.ACT_RELU)
             saved.append((y, coeffs))
             acts.append(h)
         in_saved = None
@@ -269,8 +277,12 @@ class ConvNetEngine:
         for bi in range(len(self.blocks) - 1, -1, -1):
             name, cin, cout, pool, hw = self.blocks[bi]
             y, coeffs = saved[bi]
-            dy = F.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), pool=pool, act=F.ACT_RELU,
-                          dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'))
+            if accs is not None:
+                dy = F.bn_bwd_acc(d, y, coeffs, fl.w(name + '.gamma'), accs[bi][1], pool=pool, act=F.ACT_RELU,
+                                  dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'))
+            else:
+                dy = F.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), pool=pool, act=F.ACT_RELU,
+                              dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'))
             if self.overlap_wgrad:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
@@ -283,6 +295,24 @@ class ConvNetEngine:
                 d = F.conv_dgrad(dy, fl.wb(name + '.w'))
         if self.overlap_wgrad:
             main.wait_stream(side)
+
+    def _use_bn_acc(self) -> bool:
+        return F.BN_ATOMIC and all(b[2] <= 1024 and b[2] % 8 == 0 for b in self.blocks)
+
+    def _bn_accumulators(self):
+        """Per conv block: (forward, backward) fp64 slot tables [SL][2][C], views of one flat
+        buffer so a single memset per step zeroes them all."""
+        accs = getattr(self, '_bn_accs', None)
+        if accs is None:
+            sizes = [F.bn_slots(b[2]) * 2 * b[2] for b in self.blocks]
+            flat = torch.zeros(2 * sum(sizes), dtype=torch.float64, device=self.device)
+            accs, off = [], 0
+            for b, n in zip(self.blocks, sizes):
+                shape = (F.bn_slots(b[2]), 2, b[2])
+                accs.append((flat[off:off + n].view(shape), flat[off + n:off + 2 * n].view(shape)))
+                off += 2 * n
+            self._bn_acc_flat, self._bn_accs = flat, accs
+        return accs
 
     # ------------------------------------------------------------------------ reference path
     def reference_loss(self, x_nhwc: torch.Tensor, labels: torch.Tensor, params: Optional[dict] = None,

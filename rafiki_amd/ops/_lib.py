@@ -27,6 +27,9 @@ _SIGS = {
     "rk_hconv": [i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, f32, f32, i64, i64, i32,
                  vp],
     "rk_hconv_wgrad": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i64, i64, vp],
+    "rk_bn_bwd_reduce_acc": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_bn_bwd_apply_acc": [vp, vp, vp, vp, i32, f64, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_bn_act_fwd_acc": [vp, vp, i32, f64, vp, vp, f32, vp, vp, f32, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "rk_bn_partial_rows": [i64, i32],
     "rk_channel_stats": [vp, vp, i64, i32, i32, vp],
     "rk_bn_finalize_fwd": [vp, i32, i32, f64, vp, vp, f32, vp, vp, f32, vp, vp, vp, vp, vp],

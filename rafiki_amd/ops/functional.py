@@ -17,10 +17,16 @@ from typing import Optional
 
 import torch
 
-from . import _lib
+from . import _lib, autotune
 
 KIND_CONV_FWD, KIND_CONV_DGRAD, KIND_CONV_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW, KIND_CONV_UP = range(7)
 FLAG_RELU, FLAG_BIAS, FLAG_STATS, FLAG_GATE, FLAG_ACCUM, FLAG_LRELU = 1, 2, 4, 8, 16, 32
+FLAG_SATOM = 256
+# BatchNorm statistics as fp64 atomic sums in a few slots (conv epilogue / bwd reduce) consumed by
+# fused finalize+apply kernels: 2 launches per BN layer and direction instead of 4 / 3.  Summation
+# order then varies run to run in the last bits; RAFIKI_BN_ATOMIC=0 keeps the deterministic
+# partial-row path.
+BN_ATOMIC = os.environ.get('RAFIKI_BN_ATOMIC', '1') != '0'
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
 NUM_CU = 256
@@ -177,8 +183,18 @@ def hconv(dgrad, A, B, out, M, N, K, ldb, H, W, C, *, bias=None, stats=None, gat
     return out
 
 
+def bn_slots(C: int) -> int:
+    """Atomic-accumulator slots for C channels (fewer adders per address; the consumers read
+    slots*2*C doubles per block, kept at 8 KiB)."""
+    return max(1, min(8, 512 // C))
+
+
+def bn_acc_buffer(C: int, device) -> torch.Tensor:
+    return torch.zeros((bn_slots(C), 2, C), device=device, dtype=torch.float64)
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want_stats=False, act=ACT_NONE,
-             slope=0.2, out=None):
+             slope=0.2, out=None, stats_acc=None):
     """y = conv3x3(x, w) (stride 1, pad 1) [+bias][act]; optional per-channel partial stats."""
     Nb, H, W, Cin = x.shape
     Cout = w.shape[0]
@@ -188,7 +204,11 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
         out = torch.empty((Nb, H, W, Cout), device=x.device, dtype=torch.bfloat16)
     stats = None
     flags = 0
-    if want_stats:
+    if stats_acc is not None:  # fp64 atomic sums into a zeroed [SL][2][Cout] table
+        assert stats_acc.dtype == torch.float64 and stats_acc.shape[-1] == Cout
+        stats = stats_acc
+        flags |= FLAG_STATS | FLAG_SATOM | ((stats_acc.shape[0] - 1) << 12)
+    elif want_stats:
         stats = _bn_rows_buffer(M, Cout, x.device)
         flags |= FLAG_STATS
     if bias is not None:
@@ -204,9 +224,14 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
         else:
             igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
                   taps=taps, flags=flags, slope=slope, tile=cfg[0])
-    cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, bool(want_stats)),
+    mode = 'acc' if stats_acc is not None else bool(want_stats)
+    cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, mode),
                  _tile_candidates(M, Cout) + _hconv_candidates(M, Cout, H, W, Cin, taps), run)
+    if stats_acc is not None and autotune.can_tune():
+        stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
+    if stats_acc is not None:
+        return out, stats_acc
     return (out, stats[:cdiv(M, _cfg_bm(cfg, W)) * 2]) if want_stats else out
 
 
@@ -416,6 +441,41 @@ def bn_finalize_fwd(part, count, gamma, beta, eps, running_mean=None, running_va
     _lib.call("rk_bn_finalize_fwd", _p(part), R, C, float(count), _p(gamma), _p(beta), float(eps), _p(running_mean),
               _p(running_var), float(momentum), _p(mean), _p(rstd), _p(scale), _p(shift), _s())
     return outs
+
+
+def bn_act_fwd_acc(y, acc, count, gamma, beta, eps, running_mean=None, running_var=None, momentum=0.1, *,
+                   coeffs=None, pool=False, act=ACT_RELU, slope=0.2, out=None):
+    """Fused BN finalize + apply from fp64 slot sums ``acc`` [SL][2][C] (conv_fwd(stats_acc=...)).
+    Writes ``coeffs`` [4][C] = mean, rstd, scale, shift (for backward) and returns out."""
+    Nb, H, W, C = y.shape
+    if coeffs is None:
+        coeffs = torch.empty((4, C), device=y.device, dtype=torch.float32)
+    if out is None:
+        shape = (Nb, H // 2, W // 2, C) if pool else (Nb, H, W, C)
+        out = torch.empty(shape, device=y.device, dtype=torch.bfloat16)
+    _lib.call("rk_bn_act_fwd_acc", _p(y), _p(acc), acc.shape[0], float(count), _p(gamma), _p(beta), float(eps),
+              _p(running_mean), _p(running_var), float(momentum), _p(coeffs), _p(out), Nb, H, W, C, int(pool), act,
+              float(slope), _s())
+    return out, coeffs
+
+
+def bn_bwd_acc(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, dgamma=None, dbeta=None,
+               dy=None, accumulate=False):
+    """bn_bwd with the reduction accumulated atomically into the zeroed fp64 table ``acc`` [SL][2][C]
+    and the finalize fused into the apply kernel (2 launches instead of 3)."""
+    Nb, H, W, C = y.shape
+    P_out = dout.numel() // C
+    rows = _lib.lib().rk_bn_bwd_rows(P_out, C)
+    s = _s()
+    _lib.call("rk_bn_bwd_reduce_acc", _p(dout), _p(y), _p(coeffs[2]), _p(coeffs[3]), _p(acc), acc.shape[0], rows,
+              Nb, H, W, C, int(pool), act, float(slope), s)
+    coef = torch.empty((3, C), device=y.device, dtype=torch.float32)
+    if dy is None:
+        dy = torch.empty_like(y)
+    _lib.call("rk_bn_bwd_apply_acc", _p(dout), _p(y), _p(coeffs), _p(acc), acc.shape[0], float(Nb * H * W),
+              _p(gamma), _p(dgamma), _p(dbeta), _p(coef), int(accumulate), _p(dy), Nb, H, W, C, int(pool), act,
+              float(slope), s)
+    return dy
 
 
 def bn_eval_coeffs(gamma, beta, running_mean, running_var, eps, outs=None):

@@ -235,3 +235,35 @@ def test_hconv_wgrad(fn, N, H, W, Cin, Cout, S):
     F.conv2d(_nhwc_to_nchw(x.float()), w, padding=1).backward(_nhwc_to_nchw(dy.float()))
     ref = w.grad.permute(0, 2, 3, 1).reshape(Cout, -1)
     assert rel_err(out, ref) < 2e-3
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,pool", [(4, 16, 64, 64, True), (2, 8, 128, 256, False), (3, 7, 64, 128, True),
+                                               (2, 4, 256, 512, True)])
+def test_bn_atomic_accumulator_path(fn, N, H, Cin, Cout, pool):
+    """conv_fwd(stats_acc) + fused finalize/apply (fwd) and atomic reduce + fused apply (bwd) agree with
+    the deterministic partial-row path."""
+    torch.manual_seed(13)
+    x = torch.randn(N, H, H, Cin, device=DEV).bfloat16()
+    w = (torch.randn(Cout, 9 * Cin, device=DEV) / (3 * Cin ** 0.5)).bfloat16()
+    gamma = torch.rand(Cout, device=DEV) + 0.5
+    beta = torch.randn(Cout, device=DEV) * 0.1
+    y1, st = fn.conv_fwd(x, w, want_stats=True)
+    rm1, rv1 = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    c1 = fn.bn_finalize_fwd(st, N * H * H, gamma, beta, 1e-5, rm1, rv1, 0.1)
+    o1 = fn.bn_act_fwd(y1, c1[2], c1[3], pool=pool)
+    acc = fn.bn_acc_buffer(Cout, DEV)
+    y2, _ = fn.conv_fwd(x, w, stats_acc=acc)
+    assert torch.equal(y1, y2)
+    rm2, rv2 = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    o2, c2 = fn.bn_act_fwd_acc(y2, acc, N * H * H, gamma, beta, 1e-5, rm2, rv2, 0.1, pool=pool)
+    assert torch.allclose(c1, c2, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(rm1, rm2, rtol=1e-4, atol=1e-6) and torch.allclose(rv1, rv2, rtol=1e-4, atol=1e-6)
+    assert rel_err(o2, o1) < 1e-2
+    dout = torch.randn_like(o1)
+    g1, b1 = torch.zeros(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    g2, b2 = torch.zeros(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    d1 = fn.bn_bwd(dout, y1, c1, gamma, pool=pool, dgamma=g1, dbeta=b1)
+    bacc = fn.bn_acc_buffer(Cout, DEV)
+    d2 = fn.bn_bwd_acc(dout, y2, c2, gamma, bacc, pool=pool, dgamma=g2, dbeta=b2)
+    assert rel_err(g2, g1) < 1e-4 and rel_err(b2, b1) < 1e-4
+    assert rel_err(d2, d1) < 1e-2
