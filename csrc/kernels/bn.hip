@@ -138,8 +138,10 @@ struct CoefLds {
   const float* sc;  // __shared__ arrays (inlined: the compiler sees the LDS address space)
   const float* sh;
   RK_DEV void load(int cc, float (&a)[8], float (&b)[8]) const {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { a[e] = sc[cc * 8 + e]; b[e] = sh[cc * 8 + e]; }
+    *(f32x4*)&a[0] = *(const f32x4*)(sc + cc * 8);
+    *(f32x4*)&a[4] = *(const f32x4*)(sc + cc * 8 + 4);
+    *(f32x4*)&b[0] = *(const f32x4*)(sh + cc * 8);
+    *(f32x4*)&b[4] = *(const f32x4*)(sh + cc * 8 + 4);
   }
 };
 struct CoefPtr {
@@ -159,12 +161,16 @@ RK_DEV void bn_act_fwd_body(const CS& cs, const bf16* __restrict__ y, bf16* __re
   const int CC = C >> 3;
   const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
   const long long total = (long long)N * Ho * Wo * CC;
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
+  // when the grid stride is a multiple of CC (every power-of-two C <= 2048) a thread's channel group
+  // never changes: load its coefficients once
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const bool hoist = stride % CC == 0;
+  float sc[8], sh[8];
+  if (hoist) cs.load((int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) % CC), sc, sh);
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
     const int cc = (int)(idx % CC);
     const long long pix = idx / CC;
-    float sc[8], sh[8];
-    cs.load(cc, sc, sh);
+    if (!hoist) cs.load(cc, sc, sh);
     float o[8];
     if constexpr (!POOL) {
       float f[8];
@@ -206,12 +212,14 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict_
 constexpr int FUSED_MAX_C = 1024;
 
 RK_DEV void acc_sums(const double* __restrict__ acc, int SL, int C, int c, double& a, double& b) {
-  a = 0.0;
-  b = 0.0;
-  for (int s = 0; s < SL; ++s) {
-    a += acc[(long long)(2 * s) * C + c];
-    b += acc[(long long)(2 * s + 1) * C + c];
+  double va[8], vb[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {  // SL <= 8: all loads in flight at once
+    va[s] = s < SL ? acc[(long long)(2 * s) * C + c] : 0.0;
+    vb[s] = s < SL ? acc[(long long)(2 * s + 1) * C + c] : 0.0;
   }
+  a = ((va[0] + va[1]) + (va[2] + va[3])) + ((va[4] + va[5]) + (va[6] + va[7]));
+  b = ((vb[0] + vb[1]) + (vb[2] + vb[3])) + ((vb[4] + vb[5]) + (vb[6] + vb[7]));
 }
 
 template <int POOL, int ACT>
@@ -424,13 +432,12 @@ struct BwdCoefLds {
   const float* sh;
   const float* k;   // __shared__ [3][FUSED_MAX_C]
   RK_DEV void load(int cc, float (&a)[8], float (&b)[8], float (&k1)[8], float (&k2)[8], float (&k3)[8]) const {
+    const float* src[5] = {sc, sh, k, k + FUSED_MAX_C, k + 2 * FUSED_MAX_C};
+    float* dst[5] = {a, b, k1, k2, k3};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      a[e] = sc[cc * 8 + e];
-      b[e] = sh[cc * 8 + e];
-      k1[e] = k[cc * 8 + e];
-      k2[e] = k[FUSED_MAX_C + cc * 8 + e];
-      k3[e] = k[2 * FUSED_MAX_C + cc * 8 + e];
+    for (int t = 0; t < 5; ++t) {
+      *(f32x4*)&dst[t][0] = *(const f32x4*)(src[t] + cc * 8);
+      *(f32x4*)&dst[t][4] = *(const f32x4*)(src[t] + cc * 8 + 4);
     }
   }
 };
@@ -441,8 +448,11 @@ RK_DEV void bn_bwd_apply_body(const CS& cs, const bf16* __restrict__ dout, const
   const int CC = C >> 3;
   const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
   const long long total = (long long)N * Ho * Wo * CC;
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const bool hoist = stride % CC == 0;  // see bn_act_fwd_body
+  float sc[8], sh[8], k1[8], k2[8], k3[8];
+  if (hoist) cs.load((int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) % CC), sc, sh, k1, k2, k3);
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
     const int cc = (int)(idx % CC);
     const long long pix = idx / CC;
     const uint4 gv = *(const uint4*)(dout + pix * C + cc * 8);
@@ -460,8 +470,7 @@ RK_DEV void bn_bwd_apply_body(const CS& cs, const bf16* __restrict__ dout, const
 #pragma unroll
       for (int q = 0; q < 4; ++q) yv[q] = *(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C);
     }
-    float sc[8], sh[8], k1[8], k2[8], k3[8];
-    cs.load(cc, sc, sh, k1, k2, k3);
+    if (!hoist) cs.load(cc, sc, sh, k1, k2, k3);
     float g[8];
     unpack8(gv, g);
     if constexpr (!POOL) {
@@ -672,7 +681,7 @@ extern "C" int rk_bn_bwd_reduce(const void* dout, const void* y, const float* sc
 extern "C" int rk_bn_bwd_reduce_acc(const void* dout, const void* y, const float* scale, const float* shift,
                                     double* acc, int SL, int rows, int N, int H, int W, int C, int pool, int act,
                                     float slope, void* stream) {
-  if (C % 8 || C > FUSED_MAX_C || SL <= 0 || (SL & (SL - 1))) return RK_EUNSUPPORTED;
+  if (C % 8 || C > FUSED_MAX_C || SL <= 0 || SL > 8 || (SL & (SL - 1))) return RK_EUNSUPPORTED;
   RK_DISPATCH_POOL_ACT(pool, act,
                        hipLaunchKernelGGL((bn_bwd_reduce_kernel<P_, A_>), dim3(rows), dim3(256), red_lds_bytes(C),
                                           (hipStream_t)stream, (const bf16*)dout, (const bf16*)y, scale, shift,
@@ -685,7 +694,7 @@ extern "C" int rk_bn_bwd_apply_acc(const void* dout, const void* y, const float*
                                    double count, const float* gamma, float* dgamma, float* dbeta, float* coef,
                                    int accumulate, void* dy, int N, int H, int W, int C, int pool, int act,
                                    float slope, void* stream) {
-  if (C % 8 || C > FUSED_MAX_C) return RK_EUNSUPPORTED;
+  if (C % 8 || C > FUSED_MAX_C || SL <= 0 || SL > 8) return RK_EUNSUPPORTED;
   const long long work = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 8);
   const dim3 grid(grid_for(work, 256, 1024));
   RK_DISPATCH_POOL_ACT(pool, act,
@@ -705,7 +714,7 @@ extern "C" int rk_bn_act_fwd_acc(const void* y, const double* acc, int SL, doubl
                                  const float* beta, float eps, float* run_mean, float* run_var, float momentum,
                                  float* coeffs, void* out, int N, int H, int W, int C, int pool, int act, float slope,
                                  void* stream) {
-  if (C % 8 || C > FUSED_MAX_C) return RK_EUNSUPPORTED;
+  if (C % 8 || C > FUSED_MAX_C || SL <= 0 || SL > 8) return RK_EUNSUPPORTED;
   const long long work = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 8);
   const dim3 grid(grid_for(work, 256, 1024));
   RK_DISPATCH_POOL_ACT(pool, act,

@@ -183,6 +183,9 @@ def hconv(dgrad, A, B, out, M, N, K, ldb, H, W, C, *, bias=None, stats=None, gat
     return out
 
 
+_BWD_RED_CAP = int(os.environ.get('RAFIKI_BN_RED_CAP', '2048'))
+
+
 def bn_slots(C: int) -> int:
     """Atomic-accumulator slots for C channels (fewer adders per address; the consumers read
     slots*2*C doubles per block, kept at 8 KiB)."""
@@ -465,7 +468,9 @@ def bn_bwd_acc(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0
     and the finalize fused into the apply kernel (2 launches instead of 3)."""
     Nb, H, W, C = y.shape
     P_out = dout.numel() // C
-    rows = _lib.lib().rk_bn_bwd_rows(P_out, C)
+    # no finalize reads these rows any more: size the grid for streaming only (4 pixels per lane)
+    pl = 256 // min(C // 8, 256)
+    rows = max(1, min(_BWD_RED_CAP, cdiv(P_out, pl * 4)))
     s = _s()
     _lib.call("rk_bn_bwd_reduce_acc", _p(dout), _p(y), _p(coeffs[2]), _p(coeffs[3]), _p(acc), acc.shape[0], rows,
               Nb, H, W, C, int(pool), act, float(slope), s)
