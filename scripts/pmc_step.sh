@@ -1,0 +1,17 @@
+# Hardware counters of the steady-state VGG-small training step (bench.py), three rocprofv3
+# passes (SQ+GRBM, FETCH_SIZE, WRITE_SIZE+L2 hit/miss), each under its own time limit, then a
+# per-kernel summary of the last 2 steps -> gpurun_out/pmc_step/summary.{txt,csv}.
+set -e -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/pmc_step
+mkdir -p $OUT
+ARGS="bench.py --steps 2 --warmup 1"
+timeout -k 10 180 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA \
+  SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY GRBM_GUI_ACTIVE \
+  --output-format csv -d $OUT/p0 -o run -- python3 $ARGS > $OUT/p0.log 2>&1
+timeout -k 10 180 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE \
+  --output-format csv -d $OUT/p1 -o run -- python3 $ARGS > $OUT/p1.log 2>&1
+timeout -k 10 180 rocprofv3 --kernel-trace --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE \
+  --output-format csv -d $OUT/p2 -o run -- python3 $ARGS > $OUT/p2.log 2>&1
+python3 scripts/pmc_summary.py $OUT/p0 $OUT/p1 $OUT/p2 --steps 2 --csv $OUT/summary.csv > $OUT/summary.txt
+cat $OUT/summary.txt
