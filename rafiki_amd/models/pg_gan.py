@@ -175,23 +175,23 @@ class PgNetworks:
         """latents [N, latent] fp32, labels [N, label_size] -> images NHWC [N, r, r, cpad] (bf16 on GPU)
         at r = 2 ** (L - floor(lod)), in [-1, 1] drange (pg_gans.py:803-880, 'recursive' structure)."""
         dt = torch.bfloat16 if self.device.type == 'cuda' else torch.float32
-        lrelu, PN = A.leaky_relu, A.pixel_norm
+        PN, LPN = A.pixel_norm, A.lrelu_pixel_norm
         N = latents.shape[0]
         combo = torch.cat([latents, labels], 1) if self.label_size else latents
         combo = PN(combo.float())
         if self.combo_p > self.combo:
             combo = torch.cat([combo, combo.new_zeros(N, self.combo_p - self.combo)], 1)
         x = self._dense(P, '4x4/Dense', combo.to(dt), bias=False).reshape(N, 4, 4, self.nf(1))
-        x = PN(lrelu(x + P.w('4x4/Dense/bias').to(dt)))
-        x = PN(lrelu(self._conv(P, '4x4/Conv', x)))
+        x = LPN(x, P.w('4x4/Dense/bias'))
+        x = LPN(self._conv(P, '4x4/Conv', x))
         cur = self.L - int(math.floor(lod))
         frac = lod - math.floor(lod)
         prev = None
         for res in range(3, cur + 1):
             prev = x
             tag = '%dx%d' % (2 ** res, 2 ** res)
-            x = PN(lrelu(self._upconv(P, tag + '/Conv0_up', x)))
-            x = PN(lrelu(self._conv(P, tag + '/Conv1', x)))
+            x = LPN(self._upconv(P, tag + '/Conv0_up', x))
+            x = LPN(self._conv(P, tag + '/Conv1', x))
         img = self._conv(P, 'ToRGB_lod%d' % (self.L - cur), x, taps=1)
         if frac > 0 and cur > 2:
             lo = A.upscale2d(self._conv(P, 'ToRGB_lod%d' % (self.L - cur + 1), prev, taps=1))
@@ -355,6 +355,92 @@ class _ArrayPyramid:
 
 
 # ============================================================================== model
+class TrialRng:
+    """Per-trial random source.  GPU: the Philox HIP kernel keyed by (seed, call-site stream id,
+    device step counter) — a captured training round bumps the counter itself, so graph replays
+    draw fresh latents / indices / mixing factors with no host work.  CPU: a torch.Generator."""
+
+    # call-site stream ids
+    D_IDX, D_LAT, D_ALPHA, G_LAB, G_LAT = 1, 2, 3, 4, 5
+
+    def __init__(self, device, seed):
+        self.device, self.seed = device, int(seed)
+        if device.type == 'cuda':
+            self.step = torch.zeros(1, dtype=torch.int32, device=device)
+        else:
+            self.gen = torch.Generator()
+            self.gen.manual_seed(self.seed)
+
+    def _draw(self, shape, dist, sid, hi=0):
+        from rafiki_amd.ops import functional as F
+        out = torch.empty(shape, dtype=torch.int32 if dist == F.RNG_RANDINT else torch.float32, device=self.device)
+        return F.philox_(out, dist, seed=self.seed, stream_id=sid, step=self.step, hi=hi)
+
+    def randint(self, hi, n, sid):
+        if self.device.type == 'cuda':
+            from rafiki_amd.ops import functional as F
+            return self._draw((n,), F.RNG_RANDINT, sid, hi=hi)
+        return torch.randint(0, hi, (n,), generator=self.gen)
+
+    def randn(self, shape, sid):
+        if self.device.type == 'cuda':
+            from rafiki_amd.ops import functional as F
+            return self._draw(shape, F.RNG_NORMAL, sid)
+        return torch.randn(shape, generator=self.gen)
+
+    def rand(self, shape, sid):
+        if self.device.type == 'cuda':
+            from rafiki_amd.ops import functional as F
+            return self._draw(shape, F.RNG_UNIFORM, sid)
+        return torch.rand(shape, generator=self.gen)
+
+    def advance(self):
+        if self.device.type == 'cuda':
+            from rafiki_amd.ops import functional as F
+            F.add_int_(self.step, 1)
+
+
+class GraphedRounds:
+    """hipGraph cache of training rounds (D_repeats D steps + Gs EMA + one G step).
+
+    A round's shapes, learning rates and LOD are static inside a stable LOD phase, so the first
+    round with a new key runs eagerly (it also autotunes every GEMM shape), the second one is
+    captured, and every later round is one graph replay — the PG-GAN step at 4x4 is otherwise
+    bound by host-side launch overhead of ~600 small kernels.  Randomness comes from TrialRng's
+    device counter, the Adam step count lives on the device, and the loss accumulators are
+    persistent buffers, so replays need no host input."""
+
+    def __init__(self, enabled):
+        self.enabled = enabled
+        self.graphs = {}
+        self.seen = set()
+        self.captures = 0
+
+    def clear(self):
+        self.graphs.clear()
+        self.seen.clear()
+
+    def run(self, key, fn):
+        if not self.enabled:
+            fn()
+            return
+        g = self.graphs.get(key)
+        if g is not None:
+            g.replay()
+            return
+        if key not in self.seen:
+            self.seen.add(key)
+            fn()
+            return
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            fn()
+        self.graphs[key] = g
+        self.captures += 1
+        g.replay()
+
+
 class PgGan(BaseModel):
     DATA_PARALLEL = True
 
@@ -450,8 +536,10 @@ class PgGan(BaseModel):
         if self.world > 1:
             g_ar = FlatGradAllReduce(nets.G.grad, nets.G.param_ranges(), list(nets.g_params.values()), self.world)
             d_ar = FlatGradAllReduce(nets.D.grad, nets.D.param_ranges(), list(nets.d_params.values()), self.world)
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(self.seed * 7919 + self.rank)
+        rng = TrialRng(dev, self.seed * 7919 + self.rank)
+        graphs = GraphedRounds(dev.type == 'cuda' and self.world == 1 and bool(knobs.get('cuda_graph', True))
+                               and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0')
+        acc = torch.zeros(6, dtype=torch.float32, device=dev)
         level_cache = {}
         labels_all = torch.as_tensor(ds.labels, device=dev)
         cur_nimg, prev_lod, tick = 0, -1.0, 0
@@ -462,6 +550,7 @@ class PgGan(BaseModel):
             lod_int = int(math.floor(sched.lod))
             if lod_int not in level_cache:
                 level_cache.clear()
+                graphs.clear()
                 level_cache[lod_int] = torch.as_tensor(ds.images[lod_int]).to(dev)
             level = level_cache[lod_int]
             if np.floor(sched.lod) != np.floor(prev_lod) or np.ceil(sched.lod) != np.ceil(prev_lod):
@@ -472,15 +561,21 @@ class PgGan(BaseModel):
             mb = sched.minibatch // self.world
             if mb % min(nets.mbstd_group_size, mb) != 0:
                 mb -= mb % nets.mbstd_group_size
-            acc = torch.zeros(6, dtype=torch.float32, device=dev)
+            acc.zero_()
             nD = nG = 0
+            frac = sched.lod - math.floor(sched.lod)
+            key = (sched.lod, mb, G_opt.lr, D_opt.lr, D_repeats, G_smoothing)
+
+            def round_fn():
+                self.train_round(sched.lod, mb, level, labels_all, rng, G_opt, D_opt, acc, D_repeats=D_repeats,
+                                 G_smoothing=G_smoothing, d_ar=d_ar, g_ar=g_ar)
             for _ in range(minibatch_repeats):
-                for _ in range(D_repeats):
-                    acc[:4] += self._d_step(sched.lod, mb, level, labels_all, gen, D_opt, d_ar)
-                    nets.update_Gs(G_smoothing)
-                    cur_nimg += sched.minibatch
-                    nD += 1
-                acc[4] += self._g_step(sched.lod, mb, labels_all, gen, G_opt, g_ar)
+                if frac == 0:
+                    graphs.run(key, round_fn)
+                else:   # LOD transition: the fade factor changes every tick, run eagerly
+                    round_fn()
+                cur_nimg += sched.minibatch * D_repeats
+                nD += D_repeats
                 nG += 1
             tick += 1
             a = acc.cpu().numpy()
@@ -494,14 +589,24 @@ class PgGan(BaseModel):
             g_ar.remove()
             d_ar.remove()
 
-    def _latents(self, n, gen):
-        return torch.randn((n, self.nets.latent_size), generator=gen, device=self.device)
+    def _latents(self, n, rng, sid):
+        return rng.randn((n, self.nets.latent_size), sid)
 
-    def _rand_labels(self, labels_all, n, gen):
+    def _rand_labels(self, labels_all, n, rng):
         if self.nets.label_size == 0:
             return torch.zeros((n, 0), device=self.device)
-        idx = torch.randint(0, labels_all.shape[0], (n,), generator=gen, device=self.device)
-        return labels_all.index_select(0, idx)
+        idx = rng.randint(labels_all.shape[0], n, TrialRng.G_LAB)
+        return labels_all.index_select(0, idx.to(labels_all.device))
+
+    def train_round(self, lod, mb, level, labels_all, rng, G_opt, D_opt, acc, *, D_repeats=1, G_smoothing=0.99,
+                    d_ar=None, g_ar=None):
+        """D_repeats D steps (each followed by the Gs EMA) then one G step (pg_gans.py:338-342);
+        losses accumulate on the device into acc[:4] (D) and acc[4] (G).  Host-sync free, so a
+        round is captured whole by GraphedRounds."""
+        for _ in range(D_repeats):
+            acc[:4] += self._d_step(lod, mb, level, labels_all, rng, D_opt, d_ar)
+            self.nets.update_Gs(G_smoothing)
+        acc[4] += self._g_step(lod, mb, labels_all, rng, G_opt, g_ar)
 
     def _finite_guard(self, flat, opt):
         opt.skip_flag.zero_()
@@ -511,7 +616,7 @@ class PgGan(BaseModel):
         else:
             opt.skip_flag.fill_(0 if bool(torch.isfinite(flat.grad).all()) else 1)
 
-    def _d_step(self, lod, mb, level, labels_all, gen, opt, ar, wgan_lambda=10.0, wgan_epsilon=0.001,
+    def _d_step(self, lod, mb, level, labels_all, rng, opt, ar, wgan_lambda=10.0, wgan_epsilon=0.001,
                 wgan_target=1.0):
         """_D_wgangp_acgan (pg_gans.py:1291-1328) + D optimizer step."""
         nets = self.nets
@@ -519,15 +624,15 @@ class PgGan(BaseModel):
         nets.set_requires_grad(nets.g_params, False)
         nets.set_requires_grad(nets.d_params, True)
         nets.D.grad.zero_()
-        idx = torch.randint(0, level.shape[0], (mb,), generator=gen, device=self.device)
+        idx = rng.randint(level.shape[0], mb, TrialRng.D_IDX).to(level.device)
         reals = self._reals(level, idx, lod - math.floor(lod))
         labels = labels_all.index_select(0, idx) if nets.label_size else torch.zeros((mb, 0), device=self.device)
         with torch.no_grad():
-            fakes = nets.generator(PG, self._latents(mb, gen), labels, lod)
+            fakes = nets.generator(PG, self._latents(mb, rng, TrialRng.D_LAT), labels, lod)
         real_s, real_l = nets.discriminator(PD, reals, lod)
         fake_s, fake_l = nets.discriminator(PD, fakes, lod)
         loss = fake_s - real_s
-        alpha = torch.rand((mb, 1, 1, 1), generator=gen, device=self.device)
+        alpha = rng.rand((mb, 1, 1, 1), TrialRng.D_ALPHA)
         mixed = (reals.float() + (fakes.float() - reals.float()) * alpha).to(reals.dtype).detach().requires_grad_(True)
         mixed_s, _ = nets.discriminator(PD, mixed, lod)
         if ar is not None:
@@ -543,18 +648,19 @@ class PgGan(BaseModel):
             ar.finish()
         self._finite_guard(nets.D, opt)
         opt.step()
+        rng.advance()
         return torch.stack([loss.mean().detach(), real_s.mean().detach(), fake_s.mean().detach(),
                             norms.mean().detach()])
 
-    def _g_step(self, lod, mb, labels_all, gen, opt, ar):
+    def _g_step(self, lod, mb, labels_all, rng, opt, ar):
         """_G_wgan_acgan (pg_gans.py:1276-1289) + G optimizer step."""
         nets = self.nets
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.d_params, False)
         nets.set_requires_grad(nets.g_params, True)
         nets.G.grad.zero_()
-        labels = self._rand_labels(labels_all, mb, gen)
-        fakes = nets.generator(PG, self._latents(mb, gen), labels, lod)
+        labels = self._rand_labels(labels_all, mb, rng)
+        fakes = nets.generator(PG, self._latents(mb, rng, TrialRng.G_LAT), labels, lod)
         fake_s, fake_l = nets.discriminator(PD, fakes, lod)
         loss = -fake_s
         if nets.label_size:
@@ -566,6 +672,7 @@ class PgGan(BaseModel):
             ar.finish()
         self._finite_guard(nets.G, opt)
         opt.step()
+        rng.advance()
         nets.set_requires_grad(nets.d_params, True)
         return loss.mean().detach()
 

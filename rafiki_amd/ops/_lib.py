@@ -53,6 +53,8 @@ _SIGS = {
     "rk_ensemble_mean": [vp, i32, i64, vp, vp, vp],
     "rk_cast_f32_bf16": [vp, vp, i64, vp],
     "rk_pack_nhwc": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
+    "rk_philox": [vp, i64, i32, i32, f32, f32, C.c_ulonglong, C.c_uint, vp, vp],
+    "rk_lrelu_pixelnorm": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
 }
 
 _OPTIONAL: set[str] = set()

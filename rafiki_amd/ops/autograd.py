@@ -289,6 +289,39 @@ def pixel_norm(x, eps=1e-8):
     return (xf * torch.rsqrt(xf.square().mean(-1, keepdim=True) + eps)).to(x.dtype)
 
 
+class LReluPixelNormFn(torch.autograd.Function):
+    """z = pixel_norm(leaky_relu(x + b)) in one fused HIP pass (the generator's per-layer epilogue,
+    pg_gans.py:853-869).  Generator-side only, so once-differentiable: WGAN-GP differentiates the
+    discriminator twice, never the generator."""
+
+    @staticmethod
+    def forward(ctx, x, b, slope, eps):
+        x = x.contiguous()
+        bd = None if b is None else b.detach().float().contiguous()
+        z = F.lrelu_pixelnorm(x, bd, slope=slope, eps=eps)
+        ctx.save_for_backward(x)
+        ctx.bd, ctx.slope, ctx.eps, ctx.has_b = bd, slope, eps, b is not None
+        return z
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gz):
+        (x,) = ctx.saved_tensors
+        gx = F.lrelu_pixelnorm(x, ctx.bd, slope=ctx.slope, eps=ctx.eps, dz=gz)
+        gb = None
+        if ctx.has_b and ctx.needs_input_grad[1]:
+            Cc = x.shape[-1]
+            gb = F.colsum(gx.reshape(-1, Cc), torch.empty(Cc, device=x.device, dtype=torch.float32))
+        return (gx if ctx.needs_input_grad[0] else None), gb, None, None
+
+
+def lrelu_pixel_norm(x, b=None, slope=0.2, eps=1e-8):
+    """pixel_norm(leaky_relu(x + b)); fused HIP kernel on GPU, torch composite on CPU."""
+    if x.device.type != 'cuda':
+        return pixel_norm(leaky_relu(x if b is None else x + b.to(x.dtype), slope), eps)
+    return LReluPixelNormFn.apply(x, b, float(slope), float(eps))
+
+
 def minibatch_stddev(x, group_size=4, pad_to=8):
     """Append the group-stddev feature map (pg_gans.py:1070-1082) and zero-pad the channel count
     to a multiple of ``pad_to`` so the following conv can run on the MFMA path (512+1 -> 520)."""

@@ -28,6 +28,11 @@ def _path():
     return os.environ.get('RAFIKI_TUNE_CACHE', '')
 
 
+def _tup(v):
+    """JSON lists back to the (nested) tuples used as cache keys / configs."""
+    return tuple(_tup(x) for x in v) if isinstance(v, list) else v
+
+
 def _load():
     global _loaded
     if _loaded:
@@ -38,7 +43,7 @@ def _load():
         try:
             with open(p) as f:
                 for k, v in json.load(f).items():
-                    _cache[k] = tuple(v)
+                    _cache[_tup(json.loads(k))] = _tup(v)
         except (OSError, ValueError):
             pass
 
@@ -50,7 +55,7 @@ def _save():
     try:
         tmp = p + '.tmp'
         with open(tmp, 'w') as f:
-            json.dump({k: list(v) for k, v in _cache.items()}, f)
+            json.dump({json.dumps(k): v for k, v in _cache.items()}, f)
         os.replace(tmp, p)
     except OSError:
         pass

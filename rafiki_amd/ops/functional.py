@@ -622,5 +622,38 @@ def pack_nhwc(images, cpad=8, scale=1.0, shift=0.0, out=None):
     return out
 
 
+RNG_UNIFORM, RNG_NORMAL, RNG_RANDINT = 0, 1, 2
+
+
+def philox_(out, dist, *, seed, stream_id, step=None, hi=0, a=0.0, b=1.0):
+    """Fill ``out`` (fp32, or int32 for RNG_RANDINT) from the Philox4x32-10 stream
+    (seed, stream_id, *step): uniform a + b*U[0,1), normal a + b*N(0,1), or randint [0, hi).
+    ``step`` is a device int32 counter (graph-safe: bumping it draws new numbers per replay)."""
+    want = torch.int32 if dist == RNG_RANDINT else torch.float32
+    if out.dtype != want or not out.is_contiguous():
+        raise ValueError('philox_: out must be contiguous %s' % want)
+    _lib.call("rk_philox", _p(out), out.numel(), int(dist), int(hi), float(a), float(b),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, int(stream_id) & 0xFFFFFFFF, _p(step), _s())
+    return out
+
+
+def lrelu_pixelnorm(x, bias=None, *, slope=0.2, eps=1e-8, dz=None, out=None):
+    """z = PN(lrelu(x + bias)) over the last (channel) dim of bf16 NHWC rows; with ``dz`` the
+    backward dL/dx instead (recomputes the activation from x)."""
+    Cc = x.shape[-1]
+    P = x.numel() // Cc
+    if x.dtype != torch.bfloat16 or Cc % 8 or Cc > 1024:
+        raise ValueError('lrelu_pixelnorm: bf16 rows with C % 8 == 0 and C <= 1024 required')
+    x = x.contiguous()
+    if dz is not None:
+        dz = dz.to(torch.bfloat16).contiguous()
+    if bias is not None:
+        bias = bias.float().contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("rk_lrelu_pixelnorm", _p(x), _p(bias), _p(dz), P, Cc, float(slope), float(eps), _p(out), _s())
+    return out
+
+
 def pad8(n: int) -> int:
     return int(math.ceil(n / 8.0) * 8)

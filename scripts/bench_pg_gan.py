@@ -23,6 +23,7 @@ def main():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--minibatch', type=int, default=0, help='0: reference schedule minibatch for the LOD')
+    ap.add_argument('--no-graph', action='store_true', help='eager rounds (no hipGraph replay)')
     a = ap.parse_args()
     from rafiki_amd.engine.flat import FlatAdam
     from rafiki_amd.models.pg_gan import PgGan, TrainingSchedule
@@ -37,8 +38,9 @@ def main():
     D_opt = FlatAdam(nets.D, 1e-3, betas=(0.0, 0.99))
     for o in (G_opt, D_opt):
         o.skip_flag = torch.zeros(1, dtype=torch.int32, device=dev)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(0)
+    from rafiki_amd.models.pg_gan import GraphedRounds, TrialRng
+    rng = TrialRng(dev, 0)
+    acc = torch.zeros(6, device=dev)
     res = {'metric': 'PG-GAN train throughput (images/s through D+G steps), 1 GPU', 'params_G': nets.G.num_params(),
            'params_D': nets.D.num_params(), 'dtype': 'bf16', 'data': 'synthetic uint8 32x32x1, random-init weights',
            'lods': {}}
@@ -49,11 +51,11 @@ def main():
         level = torch.randint(0, 256, (4096, 1, r, r), dtype=torch.uint8, device=dev)
         labels = torch.zeros((4096, 0), device=dev)
 
+        graphs = GraphedRounds(not a.no_graph)
+
         def step():
-            m._d_step(lod, mb, level, labels, gen, D_opt, None)
-            nets.update_Gs(0.99)
-            m._g_step(lod, mb, labels, gen, G_opt, None)
-        for _ in range(a.warmup):
+            graphs.run(lod, lambda: m.train_round(lod, mb, level, labels, rng, G_opt, D_opt, acc))
+        for _ in range(max(2, a.warmup)):
             step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -62,7 +64,7 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
         res['lods'][str(lod)] = {'resolution': r, 'minibatch': mb, 'ms_per_DG_step': round(dt * 1e3, 3),
-                                 'images_per_sec': round(mb / dt, 1)}
+                                 'images_per_sec': round(mb / dt, 1), 'hipgraph': not a.no_graph}
     print(json.dumps(res))
 
 

@@ -4,8 +4,11 @@ Reads the ``counter_collection.csv`` files of several rocprofv3 ``--pmc`` passes
 program (``scripts/pmc_step.sh``), keeps the dispatches of the last K steps (the trace is cut at
 the optimizer kernel that ends every step, as in ``trace_steps.py``) and aggregates per kernel:
 
-* ``mfma_util_pct``  = sum SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024 SIMDs) * 100
-  (the rocprofiler-sdk ``MfmaUtil`` expression; GRBM_GUI_ACTIVE is taken per dispatch)
+* ``mfma_util_pct``  = sum SQ_VALU_MFMA_BUSY_CYCLES / (kernel cycles * 1024 SIMDs) * 100 (the
+  rocprofiler-sdk ``MfmaUtil`` expression).  Counter collection serialises dispatches and stretches
+  GRBM_GUI_ACTIVE far past the kernel, so the kernel cycles come from an unperturbed kernel trace
+  of the same run (``--durations``, a ``trace_steps.py --csv`` file) at the 2.4 GHz peak clock;
+  without it GRBM_GUI_ACTIVE is used (a lower bound)
 * ``lds_conflict_pct`` = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE * 100 (extra cycles / LDS cycles)
 * ``fetch_MB`` / ``write_MB`` = FETCH_SIZE / WRITE_SIZE (KB) per step; NOTE gfx950 FETCH_SIZE
   counts wide coalesced reads at half their bytes (MI355X_MICROARCH.md, HBM section), so the
@@ -25,7 +28,7 @@ import re
 def short(name):
     name = re.sub(r'\(anonymous namespace\)::', '', name)
     m = re.match(r'(?:void )?([\w:<>, ]+?)\(', name)
-    return (m.group(1) if m else name)[:80]
+    return (m.group(1) if m else name)[:90]
 
 
 def load_pass(d, steps, marker):
@@ -40,7 +43,10 @@ def load_pass(d, steps, marker):
                 ent = disp.setdefault(did, [r['Kernel_Name'], collections.defaultdict(float)])
                 ent[1][r['Counter_Name']] += float(r['Counter_Value'])
     order = sorted(disp)
-    marks = [i for i, did in enumerate(order) if marker in disp[order[i]][0]]
+    ends = [i for i, did in enumerate(order) if marker in disp[did][0]]
+    # the marker may launch several times per step (one per parameter range): a step ends at the
+    # last launch of each consecutive group (same rule as trace_steps.py)
+    marks = [e for j, e in enumerate(ends) if j + 1 == len(ends) or ends[j + 1] != e + 1]
     if len(marks) < steps + 1:
         raise SystemExit('%s: only %d step markers' % (d, len(marks)))
     lo, hi = marks[-steps - 1] + 1, marks[-1] + 1
@@ -53,7 +59,13 @@ def main():
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--marker', default='sgd_kernel')
     ap.add_argument('--csv', default='')
+    ap.add_argument('--durations', default='', help='trace_steps.py --csv output of an unprofiled run')
+    ap.add_argument('--ghz', type=float, default=2.4)
     a = ap.parse_args()
+    dur = {}
+    if a.durations:
+        with open(a.durations) as f:
+            dur = {r['kernel']: float(r['us_per_step']) for r in csv.DictReader(f)}
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     launches = collections.Counter()
     for pi, d in enumerate(a.passes):
@@ -70,9 +82,12 @@ def main():
     tot = collections.defaultdict(float)
     for k, c in agg.items():
         gui = c.get('GRBM_GUI_ACTIVE@0', 0.0)
-        r = {'kernel': k, 'launches_per_step': launches[k] / a.steps}
-        if 'SQ_VALU_MFMA_BUSY_CYCLES' in c and gui:
-            r['mfma_util_pct'] = round(100.0 * c['SQ_VALU_MFMA_BUSY_CYCLES'] / (gui * 1024), 2)
+        r = {'kernel': k, 'launches_per_step': launches[k] / a.steps, 'us_per_step': dur.get(k, '')}
+        cyc = dur[k] * 1e3 * a.ghz * a.steps if k in dur else gui
+        if 'SQ_VALU_MFMA_BUSY_CYCLES' in c and cyc:
+            r['mfma_util_pct'] = round(100.0 * c['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * 1024), 2)
+        if k in dur and dur[k] > 0 and ('FETCH_SIZE' in c or 'WRITE_SIZE' in c):
+            r['GBps'] = round((c.get('FETCH_SIZE', 0) + c.get('WRITE_SIZE', 0)) * 1024 / a.steps / (dur[k] * 1e3), 1)
         if c.get('SQ_LDS_IDX_ACTIVE'):
             r['lds_conflict_pct'] = round(100.0 * c.get('SQ_LDS_BANK_CONFLICT', 0) / c['SQ_LDS_IDX_ACTIVE'], 2)
         if 'FETCH_SIZE' in c:
@@ -86,16 +101,17 @@ def main():
         for key in ('SQ_VALU_MFMA_BUSY_CYCLES', 'FETCH_SIZE', 'WRITE_SIZE'):
             tot[key] += c.get(key, 0)
         tot['gui'] += gui
+        tot['cyc'] += cyc
         rows.append(r)
-    rows.sort(key=lambda r: -r['gui_kcycles_per_step'])
-    cols = ['kernel', 'launches_per_step', 'gui_kcycles_per_step', 'mfma_util_pct', 'lds_conflict_pct',
-            'fetch_MB', 'write_MB', 'l2_hit_pct']
+    rows.sort(key=lambda r: -(r['us_per_step'] or 0) * 1e6 - r['gui_kcycles_per_step'])
+    cols = ['kernel', 'launches_per_step', 'us_per_step', 'mfma_util_pct', 'lds_conflict_pct',
+            'fetch_MB', 'write_MB', 'GBps', 'l2_hit_pct']
     print(('%-60s' + '%11s' * (len(cols) - 1)) % tuple(c[:10] for c in cols))
     for r in rows:
         print(('%-60s' + '%11s' * (len(cols) - 1)) % tuple([r['kernel'][:60]] + [r.get(c, '') for c in cols[1:]]))
     if tot['gui']:
         print('step total: MfmaUtil %.2f%%  fetch %.1f MB  write %.1f MB  busy %.1f kcycles' % (
-            100.0 * tot['SQ_VALU_MFMA_BUSY_CYCLES'] / (tot['gui'] * 1024), tot['FETCH_SIZE'] / 1024 / a.steps,
+            100.0 * tot['SQ_VALU_MFMA_BUSY_CYCLES'] / (tot['cyc'] * 1024), tot['FETCH_SIZE'] / 1024 / a.steps,
             tot['WRITE_SIZE'] / 1024 / a.steps, tot['gui'] / 1e3 / a.steps))
     if a.csv:
         with open(a.csv, 'w', newline='') as f:

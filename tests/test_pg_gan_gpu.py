@@ -138,3 +138,83 @@ def test_pg_gan_trains_on_gpu(tmp_path, monkeypatch):
     assert 1.0 <= s <= 4.0 + 1e-6
     paths = m.predict([2, 2, 1])
     assert len(paths) == 1
+
+
+# ------------------------------------------------------------------ Philox RNG + fused G epilogue
+def test_philox_distributions_and_counter(fn):
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    n = 1 << 20
+    u = fn.philox_(torch.empty(n, device=DEV), fn.RNG_UNIFORM, seed=123, stream_id=1, step=step)
+    assert 0.0 <= u.min().item() and u.max().item() < 1.0
+    assert abs(u.mean().item() - 0.5) < 3e-3 and abs(u.var().item() - 1 / 12) < 2e-3
+    z = fn.philox_(torch.empty(n, device=DEV), fn.RNG_NORMAL, seed=123, stream_id=2, step=step, a=1.0, b=2.0)
+    assert abs(z.mean().item() - 1.0) < 1e-2 and abs(z.std().item() - 2.0) < 1e-2
+    k = fn.philox_(torch.empty(n, dtype=torch.int32, device=DEV), fn.RNG_RANDINT, seed=123, stream_id=3, step=step,
+                   hi=10)
+    counts = torch.bincount(k.long(), minlength=10).float()
+    assert k.min().item() == 0 and k.max().item() == 9 and (counts / n - 0.1).abs().max().item() < 3e-3
+    # reproducible for the same (seed, stream, step); different for a new step or stream
+    u2 = fn.philox_(torch.empty(n, device=DEV), fn.RNG_UNIFORM, seed=123, stream_id=1, step=step)
+    assert torch.equal(u, u2)
+    fn.add_int_(step, 1)
+    u3 = fn.philox_(torch.empty(n, device=DEV), fn.RNG_UNIFORM, seed=123, stream_id=1, step=step)
+    assert (u3 != u).float().mean().item() > 0.99
+    # odd length tail
+    t = fn.philox_(torch.empty(7, device=DEV), fn.RNG_NORMAL, seed=5, stream_id=9, step=None)
+    assert torch.isfinite(t).all()
+
+
+@pytest.mark.parametrize("P,C,with_bias", [(64 * 16, 512, True), (300, 512, False), (77, 256, True), (50, 1024, False),
+                                          (33, 24, True)])
+def test_lrelu_pixelnorm_fwd_bwd(P, C, with_bias):
+    from rafiki_amd.ops import autograd as A
+    torch.manual_seed(0)
+    x = torch.randn(P, C, device=DEV).bfloat16()
+    b = (torch.randn(C, device=DEV) * 0.3) if with_bias else None
+    dz = torch.randn(P, C, device=DEV).bfloat16()
+    xg = x.clone().requires_grad_(True)
+    bg = b.clone().requires_grad_(True) if with_bias else None
+    z = A.lrelu_pixel_norm(xg, bg)
+    z.backward(dz)
+    # fp32 oracle
+    xr = x.float().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if with_bias else None
+    y = F.leaky_relu(xr + br if with_bias else xr, 0.2)
+    zr = y * torch.rsqrt(y.square().mean(-1, keepdim=True) + 1e-8)
+    zr.backward(dz.float())
+    assert rel_err(z, zr) < 1e-2
+    assert cos(xg.grad, xr.grad) > 0.999 and rel_err(xg.grad, xr.grad) < 3e-2
+    if with_bias:
+        assert cos(bg.grad, br.grad) > 0.999 and rel_err(bg.grad, br.grad) < 3e-2
+
+
+def test_graphed_rounds_match_eager():
+    """Two identical PG-GAN trials, one replaying captured rounds, one eager: same RNG stream,
+    same kernels -> same weights up to atomics / reduction-order noise."""
+    from rafiki_amd.engine.flat import FlatAdam
+    from rafiki_amd.models.pg_gan import GraphedRounds, PgGan, TrialRng
+    outs = []
+    for graphed in (False, True):
+        m = PgGan(D_repeats=1, minibatch_base=16, fmap_base=1024, fmap_max=128, seed=3)
+        m.device = torch.device(DEV)
+        m._build([1, 16, 16], 0)
+        nets = m.nets
+        G_opt = FlatAdam(nets.G, 1e-3, betas=(0.0, 0.99))
+        D_opt = FlatAdam(nets.D, 1e-3, betas=(0.0, 0.99))
+        for o in (G_opt, D_opt):
+            o.skip_flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+        rng = TrialRng(m.device, 11)
+        acc = torch.zeros(6, device=DEV)
+        level = torch.randint(0, 256, (256, 1, 4, 4), dtype=torch.uint8, device=DEV)
+        labels = torch.zeros((256, 0), device=DEV)
+        graphs = GraphedRounds(graphed)
+        for _ in range(5):
+            graphs.run('k', lambda: m.train_round(2.0, 64, level, labels, rng, G_opt, D_opt, acc))
+        torch.cuda.synchronize()
+        assert graphs.captures == (1 if graphed else 0)
+        assert int(rng.step.item()) == 10
+        outs.append((nets.G.master.clone(), nets.D.master.clone(), acc.clone()))
+    (g0, d0, a0), (g1, d1, a1) = outs
+    assert torch.isfinite(a1).all()
+    assert cos(g0, g1) > 0.9999 and cos(d0, d1) > 0.9999
+    assert rel_err(a1, a0) < 5e-2
