@@ -310,6 +310,32 @@ __global__ __launch_bounds__(256) void pack_nhwc_kernel(const void* __restrict__
   }
 }
 
+// Column sums of a tall bf16 matrix in two deterministic stages: block (x, y) sums 512 columns
+// (8 per lane, 16-byte loads) over row chunk y into part[y][C]; rk_reduce_slabs folds the chunks.
+__global__ __launch_bounds__(256) void colsum_part_kernel(const bf16* __restrict__ x, int R, int C, int ld,
+                                                          int rows_per, float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + lane * 8;
+  const int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < C) {
+    for (int r = r0 + q; r < r1; r += 4) {
+      float f[8];
+      unpack8(*(const uint4*)(x + (long long)r * ld + c0), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[q][lane * 8 + j] = s[j];
+  __syncthreads();
+  for (int t = threadIdx.x; t < 512; t += 256) {
+    const int c = blockIdx.x * 512 + t;
+    if (c < C) part[(long long)blockIdx.y * C + c] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+  }
+}
+
 __global__ void add_int_kernel(int* p, int v) { if (threadIdx.x == 0) p[0] += v; }
 
 int grid_for(long long work, int cap) {
@@ -394,6 +420,15 @@ extern "C" int rk_gather_batch(const void* data, long long row_bytes, const int*
 extern "C" int rk_colsum(const void* x, int R, int C, int ld, float* out, int accumulate, void* stream) {
   hipLaunchKernelGGL(colsum_kernel, dim3(rk_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, R, C, ld,
                      out, accumulate);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_colsum_part(const void* x, int R, int C, int ld, int chunks, float* part, void* stream) {
+  if (C % 8 || ld % 8 || chunks < 1 || chunks > 65535) return RK_EUNSUPPORTED;
+  const int rows_per = rk_cdiv(R, chunks);
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(rk_cdiv(C, 512), chunks), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x, R, C, ld, rows_per, part);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -11,6 +11,16 @@
 //    (C <= 1024: up to 2 x 8 bf16 per lane), so the reduction is a 64-lane shuffle tree and the
 //    tensor is read once and written once.  The backward recomputes y and the norm from x:
 //    dy = r*dz - (r^3/C) * y * sum(dz*y),  dx = dy * (y_pre >= 0 ? 1 : slope).
+//  * rk_mbstd (K12, pg_gans.py:1070-1082): minibatch-stddev feature, its backward and the backward
+//    of that backward (WGAN-GP differentiates the discriminator twice).  One block per stddev
+//    group: the group's g samples are read together, the statistics never leave registers/LDS.
+//    With n = N/g, sample i = k*n + j belongs to group j (tf.reshape(x, [g, -1, ...])); with
+//    `segs` > 1 the batch is `segs` independent minibatches (grouping stays inside each), so
+//    several D evaluations can share one batched forward.
+//      s_pc = sqrt(var_k x_kpc + 1e-8),  f_j = mean_pc s_pc,  out = [x, f_j, 0-pad]
+//      bwd:   gx_k = gout_k[:C] + G_j * (x_k - mu) / (g s P C),   G_j = sum_{k,p} gout_k[p, C]
+//      bwd2:  gg_out = [ggx, H_j, 0],  H_j = sum_{k,pc} ggx_k (x_k - mu) / (g s P C)
+//             g_x_k = G_j / (g P C s) * (ggx_k - mean(ggx) - u_k * mean(ggx * u)),  u = (x - mu) / s
 #include "common.h"
 
 namespace {
@@ -164,6 +174,162 @@ __global__ __launch_bounds__(256) void lrelu_pn_bwd_kernel(const bf16* __restric
   }
 }
 
+constexpr int MB_MAXG = 8;
+
+// sample index of member k of group J (segs independent minibatches of N/segs samples each)
+RK_DEV long long mb_sample(int J, int k, int N, int g, int segs) {
+  const int ns = N / segs, n = ns / g;
+  const int sg = J / n, j = J - sg * n;
+  return (long long)sg * ns + (long long)k * n + j;
+}
+
+RK_DEV float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;
+}
+
+// group statistics of one channel element: mean and 1/s over the g members
+template <int G>
+RK_DEV void mb_stats(const float (&xv)[G], int g, float& mu, float& rs) {
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < G; ++k) if (k < g) m += xv[k];
+  m /= (float)g;
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < G; ++k) if (k < g) { const float d = xv[k] - m; v += d * d; }
+  mu = m;
+  rs = rsqrtf(v / (float)g + 1e-8f);
+}
+
+// mode 0: forward   out[N,P,Cp] = [x, f, 0]
+// mode 1: backward  out[N,P,C]  = gx from gout [N,P,Cp]
+// mode 2: backward of backward: out = g_x [N,P,C], out2 = gg_out [N,P,Cp]; a = ggx [N,P,C], b = gout
+__global__ __launch_bounds__(256) void mbstd_kernel(int mode, const bf16* __restrict__ x, const bf16* __restrict__ a,
+                                                    const bf16* __restrict__ b, int N, int P, int C, int Cp, int g,
+                                                    int segs, bf16* __restrict__ out, bf16* __restrict__ out2) {
+  __shared__ float red[4];
+  const int J = blockIdx.x;
+  const int PC = P * C;
+  const float inv = 1.0f / ((float)g * (float)PC);
+  long long smp[MB_MAXG];
+#pragma unroll
+  for (int k = 0; k < MB_MAXG; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
+  float red0 = 0.f;
+  if (mode == 0) {
+    for (int e = threadIdx.x; e < PC; e += blockDim.x) {
+      float xv[MB_MAXG], mu, rs;
+#pragma unroll
+      for (int k = 0; k < MB_MAXG; ++k) xv[k] = k < g ? (float)x[smp[k] * PC + e] : 0.f;
+      mb_stats<MB_MAXG>(xv, g, mu, rs);
+      red0 += 1.0f / rs;   // s = sqrt(var + eps)
+    }
+    const float f = block_sum(red0, red) / (float)PC;
+    for (int e = threadIdx.x; e < P * Cp; e += blockDim.x) {
+      const int p = e / Cp, c = e - p * Cp;
+#pragma unroll
+      for (int k = 0; k < MB_MAXG; ++k) {
+        if (k >= g) break;
+        const float v = c < C ? (float)x[smp[k] * PC + (long long)p * C + c] : (c == C ? f : 0.f);
+        out[smp[k] * P * Cp + e] = (bf16)v;
+      }
+    }
+    return;
+  }
+  // G_j = sum over the group's extra-channel gradient (mode 1: gout = a; mode 2: gout = b)
+  const bf16* gout = mode == 1 ? a : b;
+  float gs = 0.f;
+  for (int t = threadIdx.x; t < g * P; t += blockDim.x) {
+    const int k = t / P, p = t - k * P;
+    long long sk = 0;
+#pragma unroll
+    for (int q = 0; q < MB_MAXG; ++q) if (q == k) sk = smp[q];
+    gs += (float)gout[(sk * P + p) * Cp + C];
+  }
+  const float Gj = block_sum(gs, red);
+  if (mode == 1) {
+    for (int e = threadIdx.x; e < PC; e += blockDim.x) {
+      const int p = e / C, c = e - p * C;
+      float xv[MB_MAXG], mu, rs;
+#pragma unroll
+      for (int k = 0; k < MB_MAXG; ++k) xv[k] = k < g ? (float)x[smp[k] * PC + e] : 0.f;
+      mb_stats<MB_MAXG>(xv, g, mu, rs);
+#pragma unroll
+      for (int k = 0; k < MB_MAXG; ++k) {
+        if (k >= g) break;
+        const float go = (float)gout[(smp[k] * P + p) * Cp + c];
+        out[smp[k] * PC + e] = (bf16)(go + Gj * (xv[k] - mu) * rs * inv);
+      }
+    }
+    return;
+  }
+  // mode 2: g_x (gg_out comes from mbstd_h_kernel)
+  for (int e = threadIdx.x; e < PC; e += blockDim.x) {
+    float xv[MB_MAXG], mu, rs;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) xv[k] = k < g ? (float)x[smp[k] * PC + e] : 0.f;
+    mb_stats<MB_MAXG>(xv, g, mu, rs);
+    float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) {
+      if (k >= g) break;
+      const float gg = (float)a[smp[k] * PC + e];
+      const float u = (xv[k] - mu) * rs;
+      m1 += gg;
+      m2 += gg * u;
+    }
+    const float kk = Gj * rs * inv;
+    m1 /= (float)g;
+    m2 /= (float)g;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) {
+      if (k >= g) break;
+      const float gg = (float)a[smp[k] * PC + e];
+      const float u = (xv[k] - mu) * rs;
+      out[smp[k] * PC + e] = (bf16)(kk * (gg - m1 - u * m2));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void mbstd_h_kernel(const bf16* __restrict__ x, const bf16* __restrict__ a, int N,
+                                                      int P, int C, int Cp, int g, int segs, bf16* __restrict__ out2) {
+  __shared__ float red[4];
+  const int J = blockIdx.x;
+  const int PC = P * C;
+  const float inv = 1.0f / ((float)g * (float)PC);
+  long long smp[MB_MAXG];
+#pragma unroll
+  for (int k = 0; k < MB_MAXG; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
+  float hs = 0.f;
+  for (int e = threadIdx.x; e < PC; e += blockDim.x) {
+    float xv[MB_MAXG], mu, rs;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) xv[k] = k < g ? (float)x[smp[k] * PC + e] : 0.f;
+    mb_stats<MB_MAXG>(xv, g, mu, rs);
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) {
+      if (k >= g) break;
+      hs += (float)a[smp[k] * PC + e] * (xv[k] - mu) * rs;
+    }
+  }
+  const float H = block_sum(hs, red) * inv;
+  for (int e = threadIdx.x; e < P * Cp; e += blockDim.x) {
+    const int p = e / Cp, c = e - p * Cp;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) {
+      if (k >= g) break;
+      const float v = c < C ? (float)a[smp[k] * PC + (long long)p * C + c] : (c == C ? H : 0.f);
+      out2[smp[k] * P * Cp + e] = (bf16)v;
+    }
+  }
+}
+
 int grid_for(long long work, int cap) {
   long long g = (work + 255) / 256;
   if (g > cap) g = cap;
@@ -179,6 +345,21 @@ extern "C" int rk_philox(void* out, long long n, int dist, int hi, float a, floa
   if (dist < 0 || dist > 2 || (dist == 2 && hi <= 0)) return RK_EBADARG;
   hipLaunchKernelGGL(philox_kernel, dim3(grid_for((n + 3) / 4, 2048)), dim3(256), 0, (hipStream_t)stream, out, n,
                      dist, hi, a, b, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)stream_id, step);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_mbstd(int mode, const void* x, const void* a, const void* b, int N, int P, int C, int Cp, int g,
+                        int segs, void* out, void* out2, void* stream) {
+  if (g < 1 || g > MB_MAXG || segs < 1 || N % segs || (N / segs) % g || Cp <= C || mode < 0 || mode > 2)
+    return RK_EBADARG;
+  const dim3 grid(N / g), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(mbstd_kernel, grid, block, 0, s, mode, (const bf16*)x, (const bf16*)a, (const bf16*)b, N, P, C,
+                     Cp, g, segs, (bf16*)out, (bf16*)out2);
+  if (mode == 2)
+    hipLaunchKernelGGL(mbstd_h_kernel, grid, block, 0, s, (const bf16*)x, (const bf16*)a, N, P, C, Cp, g, segs,
+                       (bf16*)out2);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

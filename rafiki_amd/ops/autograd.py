@@ -51,6 +51,16 @@ def _needed(ctx, i):
         return True
 
 
+def _bias_grad(gy):
+    """sum of gy over all but the channel axis, fp32.  Outside a create_graph backward the result
+    is never differentiated, so it comes from the fused bf16 column-sum kernel instead of a
+    bf16->fp32 copy plus a reduction."""
+    Cc = gy.shape[-1]
+    if not torch.is_grad_enabled() and gy.dtype == BF16 and gy.is_contiguous():
+        return F.colsum(gy.reshape(-1, Cc), torch.empty(Cc, device=gy.device, dtype=torch.float32))
+    return gy.float().reshape(-1, Cc).sum(0)
+
+
 def _k(taps):
     return 3 if taps == 9 else 1
 
@@ -88,21 +98,35 @@ def sumpool2(x):
 
 
 # ------------------------------------------------------------------------------------- conv
+def _lrelu_gate(gy, y, slope):
+    """gy * lrelu'(.) with the mask read from the activation OUTPUT y (same sign as its input);
+    linear in gy, so it differentiates again through torch (WGAN-GP double backward).  The mask is
+    piecewise constant, so y is detached: no (zero) gradient is routed back into y's producer."""
+    return torch.ops.aten.leaky_relu_backward(gy, y.detach(), slope, True)
+
+
 class ConvFn(torch.autograd.Function):
-    """y = conv_{taps}(x, w) + b   (x NHWC bf16, w fp32 [Cout, taps*Cin] tap-major)."""
+    """y = act(conv_{taps}(x, w) + b)   (x NHWC bf16, w fp32 [Cout, taps*Cin] tap-major); act is
+    leaky ReLU(slope) fused into the GEMM epilogue when ``slope`` is given, else the identity."""
 
     @staticmethod
-    def forward(ctx, x, w, b, wb, taps):
+    def forward(ctx, x, w, b, wb, taps, slope):
         x = x.contiguous()
         wbs = _wshadow(w, wb)
-        y = F.conv_fwd(x, wbs, taps=taps, bias=None if b is None else b.detach().float().contiguous())
-        ctx.save_for_backward(x, w)
-        ctx.wb, ctx.taps, ctx.has_b = wb, taps, b is not None
+        y = F.conv_fwd(x, wbs, taps=taps, bias=None if b is None else b.detach().float().contiguous(),
+                       act=F.ACT_NONE if slope is None else F.ACT_LRELU, slope=0.2 if slope is None else slope)
+        if slope is None:
+            ctx.save_for_backward(x, w)
+        else:
+            ctx.save_for_backward(x, w, y)
+        ctx.wb, ctx.taps, ctx.has_b, ctx.slope = wb, taps, b is not None, slope
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w = ctx.saved_tensors
+        x, w = ctx.saved_tensors[:2]
+        if ctx.slope is not None:
+            gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
         gy = gy.to(BF16).contiguous()
         gx = gw = gb = None
         if _needed(ctx, 0):
@@ -110,8 +134,8 @@ class ConvFn(torch.autograd.Function):
         if _needed(ctx, 1):
             gw = ConvWgradFn.apply(x, gy, ctx.taps)
         if ctx.has_b and _needed(ctx, 2):
-            gb = gy.float().sum((0, 1, 2))
-        return gx, gw, gb, None, None
+            gb = _bias_grad(gy)
+        return gx, gw, gb, None, None, None
 
 
 class ConvDgradFn(torch.autograd.Function):
@@ -131,7 +155,7 @@ class ConvDgradFn(torch.autograd.Function):
         ggx = ggx.to(BF16).contiguous()
         g_gy = g_w = None
         if _needed(ctx, 0):
-            g_gy = ConvFn.apply(ggx, w, None, ctx.wb, ctx.taps)
+            g_gy = ConvFn.apply(ggx, w, None, ctx.wb, ctx.taps, None)
         if _needed(ctx, 1):
             g_w = ConvWgradFn.apply(ggx, gy, ctx.taps)
         return g_gy, g_w, None, None
@@ -156,15 +180,17 @@ class ConvWgradFn(torch.autograd.Function):
         if _needed(ctx, 0):
             g_x = ConvDgradFn.apply(gy, ggw, None, ctx.taps)
         if _needed(ctx, 1):
-            g_gy = ConvFn.apply(x, ggw, None, None, ctx.taps)
+            g_gy = ConvFn.apply(x, ggw, None, None, ctx.taps, None)
         return g_x, g_gy, None
 
 
-def conv2d(x, w, b=None, *, taps=9, wb=None):
-    """NHWC conv, stride 1, SAME padding (3x3 when taps == 9, 1x1 when taps == 1)."""
+def conv2d(x, w, b=None, *, taps=9, wb=None, lrelu=None):
+    """NHWC conv, stride 1, SAME padding (3x3 when taps == 9, 1x1 when taps == 1); ``lrelu`` = slope
+    of a fused leaky-ReLU epilogue."""
     if x.device.type != 'cuda':
-        return _conv_ref(x, w, b, taps)
-    return ConvFn.apply(x, w, b, wb, taps)
+        y = _conv_ref(x, w, b, taps)
+        return y if lrelu is None else leaky_relu(y, lrelu)
+    return ConvFn.apply(x, w, b, wb, taps, None if lrelu is None else float(lrelu))
 
 
 class UpConvFn(torch.autograd.Function):
@@ -189,7 +215,7 @@ class UpConvFn(torch.autograd.Function):
         if _needed(ctx, 1):
             gw = ConvWgradFn.apply(upscale2d(x).contiguous(), gy, 9)
         if ctx.has_b and _needed(ctx, 2):
-            gb = gy.float().sum((0, 1, 2))
+            gb = _bias_grad(gy)
         return gx, gw, gb, None
 
 
@@ -206,19 +232,25 @@ def conv2d_downscale2d(x, w, b=None, *, wb=None):
 
 # ------------------------------------------------------------------------------------ dense
 class DenseFn(torch.autograd.Function):
-    """y = x @ w.T + b   (x [M, K] bf16, w fp32 [N, K])."""
+    """y = act(x @ w.T + b)   (x [M, K] bf16, w fp32 [N, K]; act as in ConvFn)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, wb):
+    def forward(ctx, x, w, b, wb, slope):
         x = x.contiguous()
-        y = F.linear(x, _wshadow(w, wb), None if b is None else b.detach().float().contiguous())
-        ctx.save_for_backward(x, w)
-        ctx.wb, ctx.has_b = wb, b is not None
+        y = F.linear(x, _wshadow(w, wb), None if b is None else b.detach().float().contiguous(),
+                     act=F.ACT_NONE if slope is None else F.ACT_LRELU, slope=0.2 if slope is None else slope)
+        if slope is None:
+            ctx.save_for_backward(x, w)
+        else:
+            ctx.save_for_backward(x, w, y)
+        ctx.wb, ctx.has_b, ctx.slope = wb, b is not None, slope
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w = ctx.saved_tensors
+        x, w = ctx.saved_tensors[:2]
+        if ctx.slope is not None:
+            gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
         gy = gy.to(BF16).contiguous()
         gx = gw = gb = None
         if _needed(ctx, 0):
@@ -226,8 +258,8 @@ class DenseFn(torch.autograd.Function):
         if _needed(ctx, 1):
             gw = DenseDwFn.apply(x, gy)
         if ctx.has_b and _needed(ctx, 2):
-            gb = gy.float().sum(0)
-        return gx, gw, gb, None
+            gb = _bias_grad(gy)
+        return gx, gw, gb, None, None
 
 
 class DenseDxFn(torch.autograd.Function):
@@ -245,7 +277,7 @@ class DenseDxFn(torch.autograd.Function):
         ggx = ggx.to(BF16).contiguous()
         g_gy = g_w = None
         if _needed(ctx, 0):
-            g_gy = DenseFn.apply(ggx, w, None, ctx.wb)
+            g_gy = DenseFn.apply(ggx, w, None, ctx.wb, None)
         if _needed(ctx, 1):
             g_w = DenseDwFn.apply(ggx, gy)
         return g_gy, g_w, None
@@ -267,14 +299,15 @@ class DenseDwFn(torch.autograd.Function):
         if _needed(ctx, 0):
             g_x = DenseDxFn.apply(gy, ggw, None)
         if _needed(ctx, 1):
-            g_gy = DenseFn.apply(x, ggw, None, None)
+            g_gy = DenseFn.apply(x, ggw, None, None, None)
         return g_x, g_gy
 
 
-def dense(x, w, b=None, *, wb=None):
+def dense(x, w, b=None, *, wb=None, lrelu=None):
     if x.device.type != 'cuda':
-        return TF.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
-    return DenseFn.apply(x, w, b, wb)
+        y = TF.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
+        return y if lrelu is None else leaky_relu(y, lrelu)
+    return DenseFn.apply(x, w, b, wb, None if lrelu is None else float(lrelu))
 
 
 # ---------------------------------------------------------------------------- elementwise glue
@@ -322,10 +355,48 @@ def lrelu_pixel_norm(x, b=None, slope=0.2, eps=1e-8):
     return LReluPixelNormFn.apply(x, b, float(slope), float(eps))
 
 
-def minibatch_stddev(x, group_size=4, pad_to=8):
+class MbstdFn(torch.autograd.Function):
+    """Minibatch-stddev feature (pg_gans.py:1070-1082) on the fused HIP kernels; its backward is
+    MbstdBwdFn so the WGAN-GP penalty can differentiate through it once more."""
+
+    @staticmethod
+    def forward(ctx, x, group, segs, cp):
+        ctx.save_for_backward(x)
+        ctx.group, ctx.segs = group, segs
+        return F.mbstd(0, x, group=group, segs=segs, cp=cp)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (x,) = ctx.saved_tensors
+        return MbstdBwdFn.apply(gout, x, ctx.group, ctx.segs), None, None, None
+
+
+class MbstdBwdFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gout, x, group, segs):
+        gout = gout.to(BF16).contiguous()
+        ctx.save_for_backward(gout, x)
+        ctx.group, ctx.segs = group, segs
+        return F.mbstd(1, x, gout, group=group, segs=segs)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, ggx):
+        gout, x = ctx.saved_tensors
+        g_x, gg_out = F.mbstd(2, x, ggx, gout, group=ctx.group, segs=ctx.segs)
+        return (gg_out if ctx.needs_input_grad[0] else None), (g_x if ctx.needs_input_grad[1] else None), None, None
+
+
+def minibatch_stddev(x, group_size=4, pad_to=8, segs=1):
     """Append the group-stddev feature map (pg_gans.py:1070-1082) and zero-pad the channel count
-    to a multiple of ``pad_to`` so the following conv can run on the MFMA path (512+1 -> 520)."""
+    to a multiple of ``pad_to`` so the following conv can run on the MFMA path (512+1 -> 520).
+    ``segs`` > 1: x is that many independent minibatches stacked (grouping stays inside each)."""
     N, H, W, C = x.shape
+    g = min(group_size, N // segs)
+    if x.device.type == 'cuda' and x.dtype == BF16 and g <= 8 and (N // segs) % g == 0:
+        return MbstdFn.apply(x, g, segs, C + 1 + (-(C + 1)) % pad_to)
+    if segs > 1:
+        return torch.cat([minibatch_stddev(t, group_size, pad_to) for t in x.chunk(segs)], 0)
     g = min(group_size, N)
     y = x.float().reshape(g, -1, H, W, C)
     y = y - y.mean(0, keepdim=True)

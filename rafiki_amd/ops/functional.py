@@ -581,9 +581,40 @@ def reduce_slabs(slab, out, *, accumulate=False, scale=1.0):
 
 
 def colsum(x2d, out, *, accumulate=False):
+    """out[c] (+)= sum_r x2d[r, c] (bf16 in, fp32 out).  Tall inputs (R > 2048, C % 8 == 0) take the
+    two-stage path: row chunks summed by ~2 blocks per CU, then folded by reduce_slabs."""
     R, Cc = x2d.shape
-    _lib.call("rk_colsum", _p(x2d), R, Cc, x2d.stride(0), _p(out), int(accumulate), _s())
+    ld = x2d.stride(0)
+    if R > 2048 and Cc % 8 == 0 and ld % 8 == 0 and Cc % 4 == 0 and x2d.stride(1) == 1:
+        chunks = max(1, min(cdiv(R, 64), cdiv(2 * NUM_CU, cdiv(Cc, 512))))
+        part = torch.empty((chunks, Cc), device=x2d.device, dtype=torch.float32)
+        _lib.call("rk_colsum_part", _p(x2d), R, Cc, ld, chunks, _p(part), _s())
+        return reduce_slabs(part, out, accumulate=accumulate)
+    _lib.call("rk_colsum", _p(x2d), R, Cc, ld, _p(out), int(accumulate), _s())
     return out
+
+
+def mbstd(mode, x, a=None, b=None, *, group, segs=1, cp=None):
+    """Minibatch-stddev kernels over NHWC bf16 x [N, H, W, C] (see pggan.hip):
+    mode 0 -> [N, H, W, cp] = [x, f, 0];  mode 1 -> gx from gout=a;  mode 2 -> (g_x, gg_out) from
+    ggx=a and gout=b."""
+    N, H, W, Cc = x.shape
+    cp = cp or (a.shape[-1] if mode == 1 else b.shape[-1] if mode == 2 else Cc + 1)
+    if x.dtype != torch.bfloat16 or N % segs or (N // segs) % group:
+        raise ValueError('mbstd: bf16 input with N divisible by segs * group required')
+    x = x.contiguous()
+    a = None if a is None else a.to(torch.bfloat16).contiguous()
+    b = None if b is None else b.to(torch.bfloat16).contiguous()
+    out2 = None
+    if mode == 0:
+        out = torch.empty((N, H, W, cp), device=x.device, dtype=torch.bfloat16)
+    else:
+        out = torch.empty_like(x)
+        if mode == 2:
+            out2 = torch.empty((N, H, W, cp), device=x.device, dtype=torch.bfloat16)
+    _lib.call("rk_mbstd", int(mode), _p(x), _p(a), _p(b), N, H * W, Cc, cp, int(group), int(segs), _p(out),
+              _p(out2), _s())
+    return (out, out2) if mode == 2 else out
 
 
 def ensemble_mean(probs, weights=None, out=None):

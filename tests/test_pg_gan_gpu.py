@@ -218,3 +218,33 @@ def test_graphed_rounds_match_eager():
     assert torch.isfinite(a1).all()
     assert cos(g0, g1) > 0.9999 and cos(d0, d1) > 0.9999
     assert rel_err(a1, a0) < 5e-2
+
+
+@pytest.mark.parametrize("N,H,C,segs", [(8, 4, 24, 1), (16, 4, 512, 2), (12, 2, 40, 3)])
+def test_minibatch_stddev_double_backward(N, H, C, segs):
+    """fused mbstd forward, backward and backward-of-backward vs the fp32 torch composite."""
+    from rafiki_amd.ops import autograd as A
+    torch.manual_seed(1)
+    x0 = torch.randn(N, H, H, C).bfloat16().float()
+    Wt = torch.randn(N, H, H, C + 1 + (-(C + 1)) % 8)
+    V = torch.randn(N, H, H, C)
+    res = []
+    for dev in ("cpu", DEV):
+        x = (x0.to(dev).bfloat16() if dev == DEV else x0.clone()).requires_grad_(True)
+        Wd = Wt.to(dev).clone().requires_grad_(True)
+        out = A.minibatch_stddev(x, 4, pad_to=8, segs=segs)
+        (gx,) = torch.autograd.grad((out.float() * Wd).sum(), x, create_graph=True)
+        (gx.float() * V.to(dev)).sum().backward()
+        res.append((out.float().cpu(), gx.float().cpu(), x.grad.float().cpu(), Wd.grad.float().cpu()))
+    (o0, g0, xx0, w0), (o1, g1, xx1, w1) = res
+    assert rel_err(o1, o0) < 1e-2
+    assert cos(g1, g0) > 0.999 and rel_err(g1, g0) < 3e-2
+    assert cos(xx1, xx0) > 0.99 and rel_err(xx1, xx0) < 6e-2
+    assert cos(w1, w0) > 0.999 and rel_err(w1, w0) < 3e-2
+
+
+def test_colsum_tall(fn):
+    x = torch.randn(8192 + 37, 520, device=DEV).bfloat16()
+    out = torch.zeros(520, device=DEV)
+    fn.colsum(x, out)
+    assert rel_err(out, x.float().sum(0)) < 1e-3
