@@ -23,6 +23,8 @@
 //             g_x_k = G_j / (g P C s) * (ggx_k - mean(ggx) - u_k * mean(ggx * u)),  u = (x - mu) / s
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 struct U4 { uint32_t v[4]; };
@@ -330,6 +332,162 @@ __global__ __launch_bounds__(256) void mbstd_h_kernel(const bf16* __restrict__ x
   }
 }
 
+// ---- vectorised minibatch-stddev (C % 8 == 0): stage A reduces per-group partial sums over
+// row chunks (grid groups x chunks, deterministic), stage B recomputes the per-channel group
+// statistics and writes every member's output, one thread per (group, 8-channel vector).
+// part[J][chunk][2]: mode 0 {sum s, -}; mode 1 {sum gout[.., C], -}; mode 2 {G sum, H sum}.
+template <int G>
+RK_DEV void mb_load(const bf16* __restrict__ base, const long long (&smp)[MB_MAXG], long long stride, long long off,
+                    int g, float (&v)[MB_MAXG][8]) {
+#pragma unroll
+  for (int k = 0; k < G; ++k)
+    if (k < g) unpack8(*(const uint4*)(base + smp[k] * stride + off), v[k]);
+}
+
+RK_DEV void mb_vstats(const float (&xv)[MB_MAXG][8], int g, float (&mu)[8], float (&rs)[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) if (k < g) m += xv[k][c];
+    m /= (float)g;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) if (k < g) { const float d = xv[k][c] - m; v += d * d; }
+    mu[c] = m;
+    rs[c] = rsqrtf(v / (float)g + 1e-8f);
+  }
+}
+
+__global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const bf16* __restrict__ x,
+                                                          const bf16* __restrict__ a, const bf16* __restrict__ gout,
+                                                          int N, int P, int C, int Cp, int g, int segs, int chunks,
+                                                          float* __restrict__ part) {
+  __shared__ float red[4];
+  const int J = blockIdx.x, ch = blockIdx.y;
+  const int C8 = C >> 3, V = P * C8;
+  long long smp[MB_MAXG];
+#pragma unroll
+  for (int k = 0; k < MB_MAXG; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
+  const int per = (V + chunks - 1) / chunks, v0 = ch * per, v1 = min(V, v0 + per);
+  float s0 = 0.f, s1 = 0.f;
+  if (mode != 1) {
+    for (int v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+      float xv[MB_MAXG][8], mu[8], rs[8];
+      mb_load<MB_MAXG>(x, smp, (long long)P * C, (long long)v * 8, g, xv);
+      mb_vstats(xv, g, mu, rs);
+      if (mode == 0) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) s0 += 1.0f / rs[c];
+      } else {
+        float av[MB_MAXG][8];
+        mb_load<MB_MAXG>(a, smp, (long long)P * C, (long long)v * 8, g, av);
+#pragma unroll
+        for (int k = 0; k < MB_MAXG; ++k)
+          if (k < g)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) s1 += av[k][c] * (xv[k][c] - mu[c]) * rs[c];
+      }
+    }
+  }
+  if (mode != 0) {   // G_j: the extra channel of gout over this chunk's pixels, all members
+    const int p0 = (int)(((long long)P * ch) / chunks), p1 = (int)(((long long)P * (ch + 1)) / chunks);
+    for (int t = threadIdx.x; t < g * (p1 - p0); t += blockDim.x) {
+      const int k = t / (p1 - p0), p = p0 + t - k * (p1 - p0);
+      long long sk = 0;
+#pragma unroll
+      for (int q = 0; q < MB_MAXG; ++q) if (q == k) sk = smp[q];
+      s0 += (float)gout[(sk * P + p) * Cp + C];
+    }
+  }
+  s0 = block_sum(s0, red);
+  s1 = block_sum(s1, red);
+  if (threadIdx.x == 0) {
+    part[((long long)J * chunks + ch) * 2] = s0;
+    part[((long long)J * chunks + ch) * 2 + 1] = s1;
+  }
+}
+
+__global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const bf16* __restrict__ x,
+                                                          const bf16* __restrict__ a, const bf16* __restrict__ gout,
+                                                          int N, int P, int C, int Cp, int g, int segs, int chunks,
+                                                          const float* __restrict__ part, bf16* __restrict__ out,
+                                                          bf16* __restrict__ out2) {
+  const int C8 = C >> 3, V = P * C8;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int J = (int)(t / V), v = (int)(t - (long long)J * V);
+  if (J >= N / g) return;
+  long long smp[MB_MAXG];
+#pragma unroll
+  for (int k = 0; k < MB_MAXG; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
+  float S0 = 0.f, S1 = 0.f;
+  for (int c = 0; c < chunks; ++c) {
+    S0 += part[((long long)J * chunks + c) * 2];
+    S1 += part[((long long)J * chunks + c) * 2 + 1];
+  }
+  const long long PC = (long long)P * C, PCp = (long long)P * Cp;
+  const int p = v / C8, c8 = v - p * C8;
+  const float inv = 1.0f / ((float)g * (float)PC);
+  float xv[MB_MAXG][8], mu[8], rs[8];
+  if (mode == 0) {
+    mb_load<MB_MAXG>(x, smp, PC, (long long)v * 8, g, xv);
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) {
+      if (k >= g) break;
+      *(uint4*)(out + smp[k] * PCp + (long long)p * Cp + c8 * 8) = pack8(xv[k]);
+      if (c8 == 0) {
+        float f[8] = {S0 / (float)PC, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        *(uint4*)(out + smp[k] * PCp + (long long)p * Cp + C) = pack8(f);
+      }
+    }
+    return;
+  }
+  mb_load<MB_MAXG>(x, smp, PC, (long long)v * 8, g, xv);
+  mb_vstats(xv, g, mu, rs);
+  if (mode == 1) {
+    float go[MB_MAXG][8];
+    mb_load<MB_MAXG>(gout, smp, PCp, (long long)p * Cp + c8 * 8, g, go);
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k) {
+      if (k >= g) break;
+      float o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[c] = go[k][c] + S0 * (xv[k][c] - mu[c]) * rs[c] * inv;
+      *(uint4*)(out + smp[k] * PC + (long long)v * 8) = pack8(o);
+    }
+    return;
+  }
+  // mode 2: g_x -> out, gg_out -> out2
+  float av[MB_MAXG][8];
+  mb_load<MB_MAXG>(a, smp, PC, (long long)v * 8, g, av);
+  float m1[8], m2[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MB_MAXG; ++k)
+      if (k < g) { s1 += av[k][c]; s2 += av[k][c] * (xv[k][c] - mu[c]) * rs[c]; }
+    m1[c] = s1 / (float)g;
+    m2[c] = s2 / (float)g;
+  }
+#pragma unroll
+  for (int k = 0; k < MB_MAXG; ++k) {
+    if (k >= g) break;
+    float o[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float u = (xv[k][c] - mu[c]) * rs[c];
+      o[c] = S0 * rs[c] * inv * (av[k][c] - m1[c] - u * m2[c]);
+    }
+    *(uint4*)(out + smp[k] * PC + (long long)v * 8) = pack8(o);
+    *(uint4*)(out2 + smp[k] * PCp + (long long)p * Cp + c8 * 8) = pack8(av[k]);
+    if (c8 == 0) {
+      float f[8] = {S1 * inv, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      *(uint4*)(out2 + smp[k] * PCp + (long long)p * Cp + C) = pack8(f);
+    }
+  }
+}
+
 int grid_for(long long work, int cap) {
   long long g = (work + 255) / 256;
   if (g > cap) g = cap;
@@ -349,12 +507,26 @@ extern "C" int rk_philox(void* out, long long n, int dist, int hi, float a, floa
   return RK_OK;
 }
 
+// part: fp32 scratch of >= (N/g) * 16 * 2 floats (vectorised path, C % 8 == 0 and Cp == C + 8)
 extern "C" int rk_mbstd(int mode, const void* x, const void* a, const void* b, int N, int P, int C, int Cp, int g,
-                        int segs, void* out, void* out2, void* stream) {
+                        int segs, void* out, void* out2, float* part, void* stream) {
   if (g < 1 || g > MB_MAXG || segs < 1 || N % segs || (N / segs) % g || Cp <= C || mode < 0 || mode > 2)
     return RK_EBADARG;
   const dim3 grid(N / g), block(256);
   hipStream_t s = (hipStream_t)stream;
+  if (part && C % 8 == 0 && Cp == C + 8) {
+    const int groups = N / g;
+    const int chunks = std::max(1, std::min(16, 1024 / groups));
+    const bf16* gout = (const bf16*)(mode == 1 ? a : b);
+    hipLaunchKernelGGL(mbstd_vec_a_kernel, dim3(groups, chunks), block, 0, s, mode, (const bf16*)x, (const bf16*)a,
+                       gout, N, P, C, Cp, g, segs, chunks, part);
+    const long long threads = (long long)groups * P * (C / 8);
+    hipLaunchKernelGGL(mbstd_vec_b_kernel, dim3((unsigned)((threads + 255) / 256)), block, 0, s, mode,
+                       (const bf16*)x, (const bf16*)a, gout, N, P, C, Cp, g, segs, chunks, part, (bf16*)out,
+                       (bf16*)out2);
+    RK_LAUNCH_CHECK();
+    return RK_OK;
+  }
   hipLaunchKernelGGL(mbstd_kernel, grid, block, 0, s, mode, (const bf16*)x, (const bf16*)a, (const bf16*)b, N, P, C,
                      Cp, g, segs, (bf16*)out, (bf16*)out2);
   if (mode == 2)

@@ -55,7 +55,7 @@ _SIGS = {
     "rk_pack_nhwc": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
     "rk_philox": [vp, i64, i32, i32, f32, f32, C.c_ulonglong, C.c_uint, vp, vp],
     "rk_lrelu_pixelnorm": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
-    "rk_mbstd": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+    "rk_mbstd": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_colsum_part": [vp, i32, i32, i32, i32, vp, vp],
 }
 

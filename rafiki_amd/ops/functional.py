@@ -612,8 +612,9 @@ def mbstd(mode, x, a=None, b=None, *, group, segs=1, cp=None):
         out = torch.empty_like(x)
         if mode == 2:
             out2 = torch.empty((N, H, W, cp), device=x.device, dtype=torch.bfloat16)
+    part = torch.empty((N // group) * 32, device=x.device, dtype=torch.float32)
     _lib.call("rk_mbstd", int(mode), _p(x), _p(a), _p(b), N, H * W, Cc, cp, int(group), int(segs), _p(out),
-              _p(out2), _s())
+              _p(out2), _p(part), _s())
     return (out, out2) if mode == 2 else out
 
 

@@ -220,7 +220,7 @@ def test_graphed_rounds_match_eager():
     assert rel_err(a1, a0) < 5e-2
 
 
-@pytest.mark.parametrize("N,H,C,segs", [(8, 4, 24, 1), (16, 4, 512, 2), (12, 2, 40, 3)])
+@pytest.mark.parametrize("N,H,C,segs", [(8, 4, 24, 1), (16, 4, 512, 2), (12, 2, 40, 3), (8, 4, 12, 2)])
 def test_minibatch_stddev_double_backward(N, H, C, segs):
     """fused mbstd forward, backward and backward-of-backward vs the fp32 torch composite."""
     from rafiki_amd.ops import autograd as A
