@@ -41,8 +41,12 @@ enum OpMode {
 enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
 // FLAG_SATOM (with FLAG_STATS): add the per-wave (sum, sumsq) into fp64 slots [SL][2][N] at p.stats
 // with device-scope atomics instead of writing partial rows; slot = blockIdx & ((flags >> 12) & 15).
+// FLAG_BNB (data-gradient into a BatchNorm+ReLU layer): out = v * [y*scale + shift > 0] with y read
+// through `gate` and scale/shift = bias[0:N] / bias[N:2N]; the per-channel sums (sum dz,
+// sum dz*y) that BN backward needs go to the fp64 slot table `stats` (with FLAG_SATOM), so that
+// layer's separate reduction pass disappears.
 enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16, FLAG_NOFAST = 64,
-             FLAG_LRELU = 32, FLAG_SATOM = 256 };
+             FLAG_LRELU = 32, FLAG_SATOM = 256, FLAG_BNB = 512 };
 
 struct IgemmParams {
   const bf16* A;
@@ -525,7 +529,7 @@ template <int MI, int NI, int FL, bool GUARD>
 RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm, int lane) {
   const int fl = FL < 0 ? p.flags : FL;
   const bool ST = fl & FLAG_STATS, BI = fl & FLAG_BIAS, RE = fl & FLAG_RELU, LR = fl & FLAG_LRELU,
-             GA = fl & FLAG_GATE;
+             GA = fl & FLAG_GATE, BB = fl & FLAG_BNB;
   bf16* C = (bf16*)p.out;
   float s[NI][4], ss[NI][4];
 #pragma unroll
@@ -536,8 +540,9 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
   for (int j = 0; j < NI; ++j) {
     const int n = ncol + j * 16;
     const bool nok = !GUARD || n < p.N;
-    f32x4 b = {0.f, 0.f, 0.f, 0.f};
-    if (BI && nok) b = *(const f32x4*)(p.bias + n);
+    f32x4 b = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    if ((BI || BB) && nok) b = *(const f32x4*)(p.bias + n);
+    if (BB && nok) sh = *(const f32x4*)(p.bias + p.N + n);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int m = mrow + i * 16;
@@ -558,6 +563,16 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = (float)g[e] > 0.f ? v[e] : 0.f;
       }
+      if (BB) {
+        const bf16x4 g = *(const bf16x4*)(p.gate + (long long)m * p.ldc + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float yv = (float)g[e];
+          v[e] = yv * b[e] + sh[e] > 0.f ? v[e] : 0.f;
+          s[j][e] += v[e];
+          ss[j][e] += v[e] * yv;
+        }
+      }
       bf16x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
@@ -565,7 +580,7 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
       acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  if (ST) {
+  if (ST || BB) {
 #pragma unroll
     for (int j = 0; j < NI; ++j)
 #pragma unroll
@@ -607,7 +622,7 @@ template <int MI, int NI, bool GUARD>
 RK_DEV void tile_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm,
                           int lane) {
   constexpr int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE, A_ = FLAG_SATOM;
-  switch (p.flags & (S_ | B_ | R_ | L_ | G_ | A_)) {
+  switch (p.flags & (S_ | B_ | R_ | L_ | G_ | A_ | FLAG_BNB)) {
     case 0: return tile_epi<MI, NI, 0, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case S_: return tile_epi<MI, NI, S_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case S_ | A_: return tile_epi<MI, NI, S_ | A_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
@@ -615,6 +630,7 @@ RK_DEV void tile_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, 
     case B_: return tile_epi<MI, NI, B_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case B_ | R_: return tile_epi<MI, NI, B_ | R_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case B_ | L_: return tile_epi<MI, NI, B_ | L_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case FLAG_BNB | A_: return tile_epi<MI, NI, FLAG_BNB | A_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     default: return tile_epi<MI, NI, -1, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
   }
 }

@@ -23,6 +23,7 @@ and the numerics oracle for GPU tests.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -188,6 +189,7 @@ class ConvNetEngine:
     # 11% SLOWER (1.161 -> 1.289 ms; the concurrent GEMMs and split-K slab traffic interfere), so it
     # is off by default and kept as an option for layer shapes where it pays.
     overlap_wgrad = False
+    fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
 
     def _side_stream(self):
         st = getattr(self, '_wgrad_stream', None)
@@ -274,12 +276,13 @@ class ConvNetEngine:
         # stream waits is captured into the hipGraph as graph edges.
         main = torch.cuda.current_stream(self.device)
         side = self._side_stream()
+        reduced = False
         for bi in range(len(self.blocks) - 1, -1, -1):
             name, cin, cout, pool, hw = self.blocks[bi]
             y, coeffs = saved[bi]
             if accs is not None:
                 dy = F.bn_bwd_acc(d, y, coeffs, fl.w(name + '.gamma'), accs[bi][1], pool=pool, act=F.ACT_RELU,
-                                  dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'))
+                                  dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'), reduced=reduced)
             else:
                 dy = F.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), pool=pool, act=F.ACT_RELU,
                               dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'))
@@ -292,7 +295,14 @@ class ConvNetEngine:
             else:
                 F.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
             if bi > 0:
-                d = F.conv_dgrad(dy, fl.wb(name + '.w'))
+                # into a pool-free BN+ReLU block: its ReLU mask and BN-backward sums ride in the
+                # dgrad epilogue (FLAG_BNB), so its bn_bwd_acc is a single apply pass
+                py, pco = saved[bi - 1]
+                reduced = accs is not None and self.fuse_bn_dgrad and not self.blocks[bi - 1][3]
+                if reduced:
+                    d = F.conv_dgrad(dy, fl.wb(name + '.w'), bn_y=py, bn_coeffs=pco, bn_acc=accs[bi - 1][1])
+                else:
+                    d = F.conv_dgrad(dy, fl.wb(name + '.w'))
         if self.overlap_wgrad:
             main.wait_stream(side)
 

@@ -22,6 +22,7 @@ from . import _lib, autotune
 KIND_CONV_FWD, KIND_CONV_DGRAD, KIND_CONV_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW, KIND_CONV_UP = range(7)
 FLAG_RELU, FLAG_BIAS, FLAG_STATS, FLAG_GATE, FLAG_ACCUM, FLAG_LRELU = 1, 2, 4, 8, 16, 32
 FLAG_SATOM = 256
+FLAG_BNB = 512
 # BatchNorm statistics as fp64 atomic sums in a few slots (conv epilogue / bwd reduce) consumed by
 # fused finalize+apply kernels: 2 launches per BN layer and direction instead of 4 / 3.  Summation
 # order then varies run to run in the last bits; RAFIKI_BN_ATOMIC=0 keeps the deterministic
@@ -263,23 +264,35 @@ def _bn_rows_buffer(M, C, device):
     return torch.empty((cdiv(M, 64) * 2, 2, C), device=device, dtype=torch.float32)
 
 
-def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, gate=None):
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, gate=None, bn_y=None,
+               bn_coeffs=None, bn_acc=None):
+    """dx = dgrad(dy, w).  With ``bn_y``/``bn_coeffs``/``bn_acc`` (the input layer's BN input,
+    its [4][C] coefficients and its zeroed fp64 backward slot table) the epilogue applies that
+    layer's ReLU mask and accumulates BN backward's (sum dz, sum dz*y), so bn_bwd_acc(...,
+    reduced=True) skips its reduction pass (FLAG_BNB)."""
     Nb, H, W, Cout = dy.shape
     Cin = w.numel() // (Cout * taps)
     M, K = Nb * H * W, taps * Cout
     if out is None:
         out = torch.empty((Nb, H, W, Cin), device=dy.device, dtype=torch.bfloat16)
-    flags = FLAG_GATE if gate is not None else 0
+    flags, bias, stats = (FLAG_GATE if gate is not None else 0), None, None
+    if bn_y is not None:
+        assert bn_y.shape == out.shape and bn_acc.dtype == torch.float64 and bn_acc.shape[-1] == Cin
+        gate, bias, stats = bn_y, bn_coeffs[2], bn_acc
+        flags = FLAG_BNB | FLAG_SATOM | ((bn_acc.shape[0] - 1) << 12)
 
     def run(cfg):
         if cfg[0] == 'h':
-            hconv(1, dy, w, out, M, Cin, K, taps * Cin, H, W, Cout, gate=gate, flags=flags, bn_bit=cfg[1],
-                  grid=cfg[2])
+            hconv(1, dy, w, out, M, Cin, K, taps * Cin, H, W, Cout, gate=gate, bias=bias, stats=stats, flags=flags,
+                  bn_bit=cfg[1], grid=cfg[2])
         else:
-            igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, H=H, W=W, C=Cout,
-                  taps=taps, Cb=Cout, flags=flags, tile=cfg[0])
-    run(_tuned(('cd', M, Cin, K, H, W, Cout, taps),
-               _tile_candidates(M, Cin) + _hconv_candidates(M, Cin, H, W, Cout, taps), run))
+            igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, bias=bias,
+                  stats=stats, H=H, W=W, C=Cout, taps=taps, Cb=Cout, flags=flags, tile=cfg[0])
+    cfg = _tuned(('cd', M, Cin, K, H, W, Cout, taps),
+                 _tile_candidates(M, Cin) + _hconv_candidates(M, Cin, H, W, Cout, taps), run)
+    if bn_acc is not None and autotune.can_tune():
+        bn_acc.zero_()  # tuning runs accumulated into it
+    run(cfg)
     return out
 
 
@@ -463,17 +476,19 @@ def bn_act_fwd_acc(y, acc, count, gamma, beta, eps, running_mean=None, running_v
 
 
 def bn_bwd_acc(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, dgamma=None, dbeta=None,
-               dy=None, accumulate=False):
+               dy=None, accumulate=False, reduced=False):
     """bn_bwd with the reduction accumulated atomically into the zeroed fp64 table ``acc`` [SL][2][C]
-    and the finalize fused into the apply kernel (2 launches instead of 3)."""
+    and the finalize fused into the apply kernel (2 launches instead of 3).  ``reduced``: the
+    producer of ``dout`` already accumulated the sums (conv_dgrad(bn_y=...)), apply only."""
     Nb, H, W, C = y.shape
     P_out = dout.numel() // C
     # no finalize reads these rows any more: size the grid for streaming only (4 pixels per lane)
     pl = 256 // min(C // 8, 256)
     rows = max(1, min(_BWD_RED_CAP, cdiv(P_out, pl * 4)))
     s = _s()
-    _lib.call("rk_bn_bwd_reduce_acc", _p(dout), _p(y), _p(coeffs[2]), _p(coeffs[3]), _p(acc), acc.shape[0], rows,
-              Nb, H, W, C, int(pool), act, float(slope), s)
+    if not reduced:
+        _lib.call("rk_bn_bwd_reduce_acc", _p(dout), _p(y), _p(coeffs[2]), _p(coeffs[3]), _p(acc), acc.shape[0],
+                  rows, Nb, H, W, C, int(pool), act, float(slope), s)
     coef = torch.empty((3, C), device=y.device, dtype=torch.float32)
     if dy is None:
         dy = torch.empty_like(y)
