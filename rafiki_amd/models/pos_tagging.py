@@ -122,8 +122,8 @@ class PyBiLstm(BaseModel):
         self.device = trial_context().device
 
     def _create(self):
-        import torch
         import torch.nn as nn
+        from rafiki_amd.ops.lstm import bilstm
         k = self._knobs
         V = len(self._word_dict) + 2  # 0 = pad, 1 = unknown
 
@@ -137,7 +137,8 @@ class PyBiLstm(BaseModel):
                 s.out = nn.Linear(2 * int(k.get('word_rnn_hidden_size', 64)), self._tag_count)
 
             def forward(s, x):
-                h, _ = s.lstm(s.drop(s.emb(x)))
+                # gfx950 persistent-recurrence BiLSTM kernels on GPU (rafiki_amd.ops.lstm)
+                h = bilstm(s.drop(s.emb(x)), s.lstm)
                 return s.out(h)
 
         return Net().to(self.device)

@@ -57,6 +57,8 @@ _SIGS = {
     "rk_lrelu_pixelnorm": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
     "rk_mbstd": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_colsum_part": [vp, i32, i32, i32, i32, vp, vp],
+    "rk_lstm_fwd": [vp, vp, i32, i32, i32, vp, vp, vp, vp],
+    "rk_lstm_bwd": [vp, i32, i32, i32, vp, vp, vp, vp, vp],
 }
 
 _OPTIONAL: set[str] = set()

@@ -1,0 +1,96 @@
+"""Bidirectional LSTM on the persistent gfx950 recurrence kernels (csrc/kernels/lstm.hip).
+
+Reference: examples/models/pos_tagging/PyBiLstm.py:249-268 (``nn.LSTM(Ew, h, batch_first=True,
+bidirectional=True)`` over a padded batch, zero initial state).  Split of the work:
+
+* the input projection ``x @ W_ih^T + b_ih + b_hh`` of every timestep and both directions is one
+  plain GEMM (hipBLASLt through torch), as are the three weight/input-gradient GEMMs of the
+  backward — they have no time dependence;
+* the sequential part (T steps of ``h @ W_hh^T`` + the cell) is ONE kernel launch per direction
+  pair, forward and backward (``rk_lstm_fwd`` / ``rk_lstm_bwd``).
+
+Hidden sizes are zero-padded per gate block to HP in {64, 128}; padded units stay exactly zero,
+so the result equals the unpadded LSTM.  On CPU (or hidden > 128) ``bilstm`` runs torch's LSTM.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .functional import _p, _s
+
+
+def _hp(H: int) -> int:
+    return 64 if H <= 64 else 128
+
+
+def _pad_gate_rows(w: torch.Tensor, H: int, HP: int) -> torch.Tensor:
+    """[2, 4H, ...] -> [2, 4HP, ...] with each gate block zero-padded from H to HP rows."""
+    rest = w.shape[2:]
+    out = w.new_zeros((2, 4, HP) + tuple(rest))
+    out[:, :, :H] = w.reshape((2, 4, H) + tuple(rest))
+    return out.reshape((2, 4 * HP) + tuple(rest))
+
+
+class BiLstmFn(torch.autograd.Function):
+    """x [T, B, E] fp32, w_ih [2, 4H, E], w_hh [2, 4H, H], b [2, 4H] (b_ih + b_hh) -> [T, B, 2H]."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b):
+        T, B, E = x.shape
+        H = w_hh.shape[-1]
+        HP = _hp(H)
+        w_ih_p = _pad_gate_rows(w_ih.detach().float(), H, HP)                          # [2, 4HP, E]
+        w_hh_p = torch.zeros((2, 4 * HP, HP), device=x.device, dtype=torch.float32)
+        w_hh_p[:, :, :H] = _pad_gate_rows(w_hh.detach().float(), H, HP)
+        w_hh_b = w_hh_p.to(torch.bfloat16).contiguous()
+        b_p = _pad_gate_rows(b.detach().float(), H, HP)                                  # [2, 4HP]
+        x2 = x.detach().float().reshape(T * B, E)
+        gin = torch.addmm(b_p.reshape(1, -1), x2, w_ih_p.reshape(2 * 4 * HP, E).t()).contiguous()
+        hout = torch.empty((T, B, 2, HP), device=x.device, dtype=torch.float32)
+        gsave = torch.empty((T, B, 2, 4 * HP), device=x.device, dtype=torch.float32)
+        csave = torch.empty((T, B, 2, HP), device=x.device, dtype=torch.float32)
+        _lib.call("rk_lstm_fwd", _p(gin), _p(w_hh_b), T, B, HP, _p(hout), _p(gsave), _p(csave), _s())
+        ctx.save_for_backward(x2, w_ih_p, w_hh_b, hout, gsave, csave)
+        ctx.dims = (T, B, E, H, HP)
+        return hout[..., :H].reshape(T, B, 2 * H)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gy):
+        x2, w_ih_p, w_hh_b, hout, gsave, csave = ctx.saved_tensors
+        T, B, E, H, HP = ctx.dims
+        dh = torch.zeros((T, B, 2, HP), device=gy.device, dtype=torch.float32)
+        dh[..., :H] = gy.reshape(T, B, 2, H)
+        dg = torch.empty((T, B, 2, 4 * HP), device=gy.device, dtype=torch.float32)
+        _lib.call("rk_lstm_bwd", _p(w_hh_b), T, B, HP, _p(dh), _p(gsave), _p(csave), _p(dg), _s())
+        dg2 = dg.reshape(T * B, 2 * 4 * HP)
+        gx = gw_ih = gw_hh = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (dg2 @ w_ih_p.reshape(2 * 4 * HP, E)).reshape(T, B, E)
+        if ctx.needs_input_grad[1]:
+            gw = torch.einsum('ndg,ne->dge', dg2.reshape(T * B, 2, 4 * HP), x2)          # [2, 4HP, E]
+            gw_ih = gw.reshape(2, 4, HP, E)[:, :, :H].reshape(2, 4 * H, E)
+        if ctx.needs_input_grad[2]:
+            # h_{t-1} of the forward direction / h_{t+1} of the reverse one (zero initial state)
+            hp = torch.zeros_like(hout)
+            hp[1:, :, 0] = hout[:-1, :, 0]
+            hp[:-1, :, 1] = hout[1:, :, 1]
+            gw = torch.einsum('tbdg,tbdh->dgh', dg, hp)                                     # [2, 4HP, HP]
+            gw_hh = gw.reshape(2, 4, HP, HP)[:, :, :H, :H].reshape(2, 4 * H, H)
+        if ctx.needs_input_grad[3]:
+            gb = dg.sum((0, 1)).reshape(2, 4, HP)[:, :, :H].reshape(2, 4 * H)
+        return gx, gw_ih, gw_hh, gb
+
+
+def bilstm(x, lstm: torch.nn.LSTM):
+    """Run a 1-layer bidirectional ``nn.LSTM`` (batch_first) on the gfx950 kernels; returns
+    [B, T, 2H] like ``lstm(x)[0]``.  CPU tensors and hidden > 128 use torch's own LSTM."""
+    H = lstm.hidden_size
+    if x.device.type != 'cuda' or H > 128 or lstm.num_layers != 1 or not lstm.bidirectional:
+        return lstm(x)[0]
+    w_ih = torch.stack([lstm.weight_ih_l0, lstm.weight_ih_l0_reverse])
+    w_hh = torch.stack([lstm.weight_hh_l0, lstm.weight_hh_l0_reverse])
+    b = torch.stack([lstm.bias_ih_l0 + lstm.bias_hh_l0, lstm.bias_ih_l0_reverse + lstm.bias_hh_l0_reverse])
+    y = BiLstmFn.apply(x.transpose(0, 1).contiguous(), w_ih, w_hh, b)
+    return y.transpose(0, 1)
