@@ -24,8 +24,10 @@ from __future__ import annotations
 
 import math
 import os
+import warnings
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.nn.functional as TF
 
@@ -500,7 +502,12 @@ class ConvNetEngine:
         """uint8 images [N, H, W] or [N, H, W, C] (host numpy / torch) -> device tensor in this engine's
         input layout (bf16 NHWC with channels padded to 8, or flat [N, D] padded to 8).  The
         normalisation (x*scale+shift) and packing run in one gfx950 kernel on the GPU."""
-        t = torch.as_tensor(images)
+        if isinstance(images, np.ndarray) and not images.flags.writeable:
+            with warnings.catch_warnings():   # shared read-only dataset cache arrays: only read here
+                warnings.simplefilter('ignore', UserWarning)
+                t = torch.as_tensor(images)
+        else:
+            t = torch.as_tensor(images)
         if t.dim() == 3:
             t = t.unsqueeze(-1)
         N = t.shape[0]

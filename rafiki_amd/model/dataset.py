@@ -14,10 +14,12 @@ Design changes for one MI355X node:
 """
 from __future__ import annotations
 
+import collections
 import csv
 import io
 import os
 import tempfile
+import threading
 import zipfile
 from concurrent.futures import ThreadPoolExecutor
 from urllib.parse import parse_qs, urlparse
@@ -176,8 +178,49 @@ class ModelDatasetUtils:
 
     def __init__(self):
         self._uri_to_path = {}
+        # decoded IMAGE_FILES datasets, reused by every trial of a worker process (a train job runs
+        # many trials on the same URIs; the reference memoised only the download).  Arrays are
+        # handed out read-only; byte budget RAFIKI_DATASET_CACHE_MB (0 disables).
+        self._decoded = collections.OrderedDict()
+        self._decoded_bytes = 0
+        self._lock = threading.Lock()
+
+    def _cache_key(self, dataset_uri, image_size):
+        uri = str(dataset_uri)
+        if not uri.startswith('synthetic://') and os.path.exists(uri):
+            st = os.stat(uri)
+            return (uri, image_size, st.st_mtime_ns, st.st_size)
+        return (uri, image_size)
 
     def load_dataset_of_image_files(self, dataset_uri, image_size=None):
+        budget = int(os.environ.get('RAFIKI_DATASET_CACHE_MB', '8192')) << 20
+        key = self._cache_key(dataset_uri, image_size if image_size is None or isinstance(image_size, int)
+                              else tuple(image_size))
+        with self._lock:
+            hit = self._decoded.get(key)
+            if hit is not None:
+                self._decoded.move_to_end(key)
+                return ImageFilesDataset(dataset_uri, image_size, images=hit[0], labels=hit[1])
+        ds = self._load_image_files(dataset_uri, image_size)
+        nbytes = ds.images.nbytes + ds.labels.nbytes
+        if budget > 0 and nbytes <= budget:
+            ds.images.setflags(write=False)
+            ds.labels.setflags(write=False)
+            with self._lock:
+                if key not in self._decoded:
+                    self._decoded[key] = (ds.images, ds.labels)
+                    self._decoded_bytes += nbytes
+                while self._decoded_bytes > budget and self._decoded:
+                    _, (im, lb) = self._decoded.popitem(last=False)
+                    self._decoded_bytes -= im.nbytes + lb.nbytes
+        return ds
+
+    def clear_cache(self):
+        with self._lock:
+            self._decoded.clear()
+            self._decoded_bytes = 0
+
+    def _load_image_files(self, dataset_uri, image_size=None):
         if str(dataset_uri).startswith('synthetic://'):
             kind, q = _parse_synthetic(dataset_uri)
             size = int(q.get('size', image_size or 32))

@@ -59,20 +59,27 @@ class NativeImageClassifier(BaseModel):
 
     # ------------------------------------------------------------------------ BaseModel API
     def train(self, dataset_uri):
+        tm = self.timings = {}
+        t_start = time.perf_counter()
         images, labels, classes = self._load(dataset_uri)
+        tm['load'] = time.perf_counter() - t_start
         channels = 1 if images.ndim == 3 else images.shape[-1]
         self._build(max(classes, 2), channels)
+        tm['build'] = time.perf_counter() - t_start - tm['load']
         eng = self._engine
         x_all = eng.prepare_inputs(images)
         y_all = torch.as_tensor(labels, dtype=torch.int32, device=eng.device)
+        tm['upload'] = time.perf_counter() - t_start - tm['load'] - tm['build']
         n = x_all.shape[0]
         bs = int(min(self._knobs.get('batch_size', 128), n))
         epochs = float(self._knobs.get('epochs', 1))
         steps_per_epoch = max(1, n // bs)
         total = max(1, int(math.ceil(epochs * steps_per_epoch)))
         use_graph = eng.device.type == 'cuda'
+        t_cap = time.perf_counter()
         if use_graph:
             eng.capture(bs)
+        tm['capture'] = time.perf_counter() - t_cap
         xb = torch.empty(eng.input_shape(bs), dtype=x_all.dtype, device=eng.device)
         yb = torch.empty((bs,), dtype=torch.int32, device=eng.device)
         gen = torch.Generator(device=eng.device) if eng.device.type == 'cuda' else torch.Generator()
@@ -122,7 +129,11 @@ class NativeImageClassifier(BaseModel):
             epoch += 1
         if eng.device.type == 'cuda':
             logger.log(hbm_peak_bytes=int(torch.cuda.max_memory_allocated(eng.device)))
+        t_pe = time.perf_counter()
         eng.prepare_eval()
+        tm['prepare_eval'] = time.perf_counter() - t_pe
+        tm['total'] = time.perf_counter() - t_start
+        self.timings = {k: round(v, 4) for k, v in tm.items()}
 
     # ----------------------------------------------------------------- checkpoint / resume
     def _ckpt_state(self, step, gen):
