@@ -68,7 +68,7 @@ class NativeImageClassifier(BaseModel):
         tm['build'] = time.perf_counter() - t_start - tm['load']
         eng = self._engine
         x_all = eng.prepare_inputs(images)
-        y_all = torch.as_tensor(labels, dtype=torch.int32, device=eng.device)
+        y_all = torch.from_numpy(np.asarray(labels, dtype=np.int32)).to(eng.device)  # (cached arrays are read-only)
         tm['upload'] = time.perf_counter() - t_start - tm['load'] - tm['build']
         n = x_all.shape[0]
         bs = int(min(self._knobs.get('batch_size', 128), n))
