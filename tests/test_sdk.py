@@ -160,3 +160,47 @@ def test_graph_utils():
     assert G.get_nodes_with_zero_incoming_degrees(adj) == ['a', 'b']
     assert not G.validate_dag({'x': ['y'], 'y': ['x']})
     assert G.build_dag(subs, None) == {'a': [], 'b': [], 'e': []}
+
+
+def test_decoded_dataset_cache(tmp_path, monkeypatch):
+    """A worker's trials decode an IMAGE_FILES dataset once; cached arrays are read-only, a
+    rewritten file is re-decoded, and the byte budget evicts least-recently-used entries."""
+    import os
+    import numpy as np
+    from rafiki_amd.model.dataset import ModelDatasetUtils, synthetic_images, write_image_files_zip
+    du = ModelDatasetUtils()
+    uri = 'synthetic://image?n=64&size=8&channels=3&classes=4&seed=0'
+    a = du.load_dataset_of_image_files(uri)
+    b = du.load_dataset_of_image_files(uri)
+    assert a.images is b.images and not a.images.flags.writeable
+    imgs, labels = synthetic_images(16, size=8, channels=1, classes=3, seed=2)
+    path = str(tmp_path / 'd.zip')
+    write_image_files_zip(path, imgs, labels)
+    c = du.load_dataset_of_image_files(path)
+    np.testing.assert_array_equal(c.images, imgs)
+    write_image_files_zip(path, imgs[:8], labels[:8])
+    os.utime(path, ns=(1, 10 ** 18))  # force a new mtime
+    assert du.load_dataset_of_image_files(path).size == 8
+    monkeypatch.setenv('RAFIKI_DATASET_CACHE_MB', '0')
+    du.clear_cache()
+    d = du.load_dataset_of_image_files(uri)
+    assert d.images.flags.writeable and du._decoded_bytes == 0
+
+
+def test_autotune_cache_file_roundtrip(tmp_path, monkeypatch):
+    """Tuned picks (tuple keys / nested tuple configs) survive a JSON cache file."""
+    from rafiki_amd.ops import autotune
+    monkeypatch.setenv('RAFIKI_TUNE_CACHE', str(tmp_path / 'tune.json'))
+    saved = autotune.snapshot()
+    try:
+        autotune.clear()
+        autotune._cache[('cf', 4096, 512, 4608, 4, 4, 512, 9, 'acc')] = ('h', 0, 512)
+        autotune._cache[('cw', 64, 576, 262144, False)] = (67, 256)
+        autotune._save()
+        autotune.clear()
+        autotune._loaded = False
+        assert autotune.lookup(('cf', 4096, 512, 4608, 4, 4, 512, 9, 'acc')) == ('h', 0, 512)
+        assert autotune.lookup(('cw', 64, 576, 262144, False)) == (67, 256)
+    finally:
+        autotune.clear()
+        autotune._cache.update(saved)
