@@ -32,6 +32,7 @@ import torch
 import torch.nn.functional as TF
 
 from ..ops import functional as F
+from ..ops.graphs import capture as _capture
 from .flat import FlatAdam, FlatParams, FlatSGD, init_const, init_kaiming
 
 VGG_SMALL_CFG = (64, 64, 'M', 128, 128, 'M', 256, 256, 'M', 512, 512, 'M')
@@ -421,7 +422,7 @@ class ConvNetEngine:
                 self._train_step_gpu(self._static_x, self._static_y)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _capture(g):
             self._train_step_gpu(self._static_x, self._static_y)
         torch.cuda.synchronize()
         self.flat.master.copy_(snap[0])
@@ -459,7 +460,7 @@ class ConvNetEngine:
                 body()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _capture(g):
             body()
         torch.cuda.synchronize()
         self.flat.master.copy_(snap[0])
@@ -606,7 +607,7 @@ class ConvNetEngine:
                 self._forward_eval_gpu(sx, so)
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _capture(g):
                 self._forward_eval_gpu(sx, so)
             ent = self._eval_graphs[bucket] = (g, sx, so)
         g, sx, so = ent

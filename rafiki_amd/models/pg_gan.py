@@ -42,6 +42,7 @@ from rafiki_amd.constants import TaskType  # noqa: F401
 from rafiki_amd.engine.flat import FlatAdam, FlatParams, init_const, init_normal
 from rafiki_amd.model import BaseModel, CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, logger
 from rafiki_amd.ops import autograd as A
+from rafiki_amd.ops.graphs import capture as _capture
 from rafiki_amd.parallel.context import current as trial_context
 
 
@@ -436,7 +437,7 @@ class GraphedRounds:
             return
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(g):
+        with _capture(g):
             fn()
         self.graphs[key] = g
         self.captures += 1

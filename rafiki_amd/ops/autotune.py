@@ -15,6 +15,8 @@ import threading
 
 import torch
 
+from .graphs import LOCK as _GRAPH_LOCK, capture as _capture
+
 _lock = threading.Lock()
 _cache = {}
 _loaded = False
@@ -82,7 +84,7 @@ def _time_graph(cfg, run, reps):
     run(cfg)  # warm: first-touch allocations happen outside the capture
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with _capture(g):
         for _ in range(reps):
             run(cfg)
     g.replay()
@@ -115,6 +117,14 @@ def tune(key, candidates, run):
         return hit
     if not can_tune():
         return candidates[0]
+    with _GRAPH_LOCK:   # sweeps time captured graphs: never interleave with another thread's capture
+        hit = lookup(key)
+        if hit is not None:
+            return hit
+        return _tune_locked(key, candidates, run)
+
+
+def _tune_locked(key, candidates, run):
     import time as _time
     t_start = _time.perf_counter()
     use_graph = os.environ.get('RAFIKI_AUTOTUNE_GRAPH', '1') != '0'

@@ -1,0 +1,131 @@
+"""Serving and the train->serve flow on the GPU: the top-k ensemble on one MI355X (per-model HIP
+streams, hipGraph-bucketed forwards, gfx950 ensemble-mean kernel, dynamic batcher) and the REST
+train job -> inference job -> POST /predict flow with GPU trials (reference quickstart flow,
+examples/scripts/quickstart.py:68-146)."""
+import os
+import threading
+import time
+import uuid
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TRAIN = 'synthetic://image?n=1024&size=32&channels=3&classes=10&seed=0'
+TEST = 'synthetic://image?n=256&size=32&channels=3&classes=10&seed=1'
+
+
+@pytest.fixture(scope="module")
+def ensemble():
+    from rafiki_amd.models.vgg_small import VggSmall
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    models = []
+    with use_context(TrialContext(device=torch.device(DEV))):
+        for i in range(4):
+            m = VggSmall(epochs=1, learning_rate=0.05, momentum=0.9, weight_decay=5e-4, batch_size=128,
+                         width_mult=0.5, image_size=32, seed=i)
+            m.train(TRAIN)
+            models.append(('t%d' % i, m))
+    return models
+
+
+def test_ensemble_matches_mean_of_members(ensemble):
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor.predictor import Predictor
+    imgs, _ = synthetic_images(37, size=32, channels=3, classes=10, seed=7)
+    queries = imgs.tolist()
+    p = Predictor(ensemble)
+    probs = p.predict_proba(queries).float().cpu()
+    members = torch.stack([m.predict_proba(queries).float().cpu() for _, m in ensemble])
+    assert probs.shape == (37, 10)
+    assert torch.allclose(probs, members.mean(0), atol=1e-5)
+    assert torch.allclose(probs.sum(1), torch.ones(37), atol=1e-3)
+    # binary fast path and list path agree
+    arr = p.predict_array(np.asarray(imgs))
+    assert np.allclose(np.asarray(arr), probs.numpy(), atol=1e-5)
+
+
+def test_dynamic_batcher_under_concurrency(ensemble):
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor.predictor import Predictor
+    imgs, _ = synthetic_images(64, size=32, channels=3, classes=10, seed=9)
+    p = Predictor(ensemble, max_batch=32, max_wait_ms=2.0).start()
+    try:
+        ref = p.predict_proba(imgs.tolist()).float().cpu().numpy()
+        out = [None] * len(imgs)
+
+        def worker(lo, hi):
+            for i in range(lo, hi):
+                out[i] = p.predict_one(imgs[i].tolist())
+        ts = [threading.Thread(target=worker, args=(k * 16, (k + 1) * 16)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+        assert all(o is not None for o in out)
+        assert np.allclose(np.asarray(out, dtype=np.float32), ref, atol=1e-4)
+        assert p.stats['queries'] >= 64 and p.stats['batches'] < 64   # queries were batched
+    finally:
+        p.stop()
+
+
+def test_rest_train_infer_predict_on_gpu(tmp_path):
+    """Admin REST + in-process services, GPU trials (VggSmall + FeedForward), inference, predict."""
+    from werkzeug.serving import make_server
+
+    from rafiki_amd.admin.admin import Admin
+    from rafiki_amd.admin.app import create_app
+    from rafiki_amd.client import Client
+    from rafiki_amd.constants import TaskType, UserType
+    from rafiki_amd.container.container_manager import InProcessManager, free_port
+    from rafiki_amd.container.inline import InlineServiceRunner
+    from rafiki_amd.db.database import Database
+    from rafiki_amd.model.dataset import synthetic_images, write_image_files_zip
+    from rafiki_amd.models import model_file
+    os.environ['WORKDIR_PATH'] = str(tmp_path)
+    os.environ.pop('RAFIKI_CPU_ONLY', None)
+    db_path = str(tmp_path / 'db.sqlite3')
+    runner = InlineServiceRunner(db_path)
+    admin = Admin(db=Database(db_path), container_manager=InProcessManager(runner))
+    admin.seed()
+    port = free_port()
+    srv = make_server('127.0.0.1', port, create_app(admin), threaded=True)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        imgs, labels = synthetic_images(400, size=32, channels=3, classes=10, seed=0)
+        train = write_image_files_zip(str(tmp_path / 'train.zip'), imgs[:320], labels[:320])
+        test = write_image_files_zip(str(tmp_path / 'test.zip'), imgs[320:], labels[320:])
+        c = Client(admin_host='127.0.0.1', admin_port=port)
+        c.login('superadmin@rafiki', 'rafiki')
+        email = '{}@test'.format(uuid.uuid4().hex[:8])
+        c.create_user(email, 'pw', UserType.MODEL_DEVELOPER)
+        dev_c = Client(admin_host='127.0.0.1', admin_port=port)
+        dev_c.login(email, 'pw')
+        m1 = dev_c.create_model('vgg_' + uuid.uuid4().hex[:6], TaskType.IMAGE_CLASSIFICATION,
+                                model_file('VggSmall'), 'VggSmall')
+        m2 = dev_c.create_model('ff_' + uuid.uuid4().hex[:6], TaskType.IMAGE_CLASSIFICATION,
+                                model_file('FeedForward'), 'FeedForward')
+        app = 'cifar_' + uuid.uuid4().hex[:6]
+        dev_c.create_train_job(app, TaskType.IMAGE_CLASSIFICATION, train, test,
+                               {'MODEL_TRIAL_COUNT': 1, 'GPU_COUNT': 1}, models=[m1['id'], m2['id']])
+        t0 = time.time()
+        while True:
+            tj = dev_c.get_train_job(app)
+            if tj['status'] in ('STOPPED', 'ERRORED'):
+                break
+            assert time.time() - t0 < 100, tj
+            time.sleep(0.5)
+        assert tj['status'] == 'STOPPED', tj
+        trials = dev_c.get_trials_of_train_job(app)
+        assert len(trials) == 2 and all(t['status'] == 'COMPLETED' for t in trials), trials
+        logs = dev_c.get_trial_logs(trials[0]['id'])
+        assert any('images_per_sec' in mm for mm in logs['metrics']) or logs['metrics']
+        ij = dev_c.create_inference_job(app)
+        pred = dev_c.predict(ij['predictor_host'], imgs[330].tolist())
+        assert len(pred) == 10 and abs(sum(pred) - 1.0) < 1e-3
+        dev_c.stop_inference_job(app)
+    finally:
+        srv.shutdown()
+        runner.shutdown()
