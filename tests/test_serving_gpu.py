@@ -129,3 +129,43 @@ def test_rest_train_infer_predict_on_gpu(tmp_path):
     finally:
         srv.shutdown()
         runner.shutdown()
+
+
+def test_worker_process_on_gpu_over_rccl(tmp_path):
+    """The deployment path: LocalProcessManager spawns `python -m rafiki_amd.worker` pinned to GPU 0
+    via HIP_VISIBLE_DEVICES; the worker joins an RCCL ("nccl") process group and runs VggSmall
+    trials to the budget, writing params files the inference side reads."""
+    from rafiki_amd.container.container_manager import LocalProcessManager
+    from rafiki_amd.db.database import Database
+    from rafiki_amd.models import model_file
+    from rafiki_amd.utils.auth import hash_password
+    db_path = str(tmp_path / 'db.sqlite3')
+    db = Database(db_path)
+    u = db.create_user('u@x', hash_password('p'), 'ADMIN')
+    with open(model_file('VggSmall'), 'rb') as f:
+        m = db.create_model(u.id, 'VggSmall', 'IMAGE_CLASSIFICATION', f.read(), 'VggSmall', 'img', {}, 'PRIVATE')
+    tj = db.create_train_job(u.id, 'app', 1, 'IMAGE_CLASSIFICATION', {'MODEL_TRIAL_COUNT': 2, 'GPU_COUNT': 1},
+                             'synthetic://image?n=512&size=32&channels=3&classes=10&seed=0',
+                             'synthetic://image?n=128&size=32&channels=3&classes=10&seed=1')
+    sub = db.create_sub_train_job(tj.id, m.id, u.id)
+    svc = db.create_service('TRAIN', 'test', 'img', 1, 1)
+    db.create_train_job_worker(svc.id, sub.id)
+    mgr = LocalProcessManager(logs_dir=str(tmp_path / 'logs'))
+    env = {'RAFIKI_SERVICE_ID': svc.id, 'RAFIKI_SERVICE_TYPE': 'TRAIN', 'RAFIKI_DB_PATH': db_path,
+           'WORKDIR_PATH': str(tmp_path)}
+    cs = mgr.create_service('train-test', 'img', ['-m', 'rafiki_amd.worker'], env, gpus=1)
+    assert cs.info['gpus'] == [0] and cs.info['world_size'] == 1
+    t0 = time.time()
+    while time.time() - t0 < 150:
+        trials = db.get_trials_of_sub_train_job(sub.id)
+        if len(trials) == 2 and all(t.status in ('COMPLETED', 'ERRORED') for t in trials):
+            break
+        time.sleep(1.0)
+    log = ''
+    for fn in os.listdir(tmp_path / 'logs'):
+        log += open(os.path.join(tmp_path / 'logs', fn), errors='replace').read()
+    mgr.destroy_service(cs)
+    trials = db.get_trials_of_sub_train_job(sub.id)
+    assert len(trials) == 2 and all(t.status == 'COMPLETED' for t in trials), log[-3000:]
+    for t in trials:
+        assert os.path.exists(t.params_file_path) and 0.0 <= t.score <= 1.0
