@@ -37,15 +37,12 @@ class InlineServiceRunner:
                     sub = db.get_sub_train_job(w.sub_train_job_id)
                     ServicesManager(db, None).refresh_train_job_status(sub.train_job_id)
             elif stype == ServiceType.PREDICT:
-                from werkzeug.serving import make_server
-
+                from ..predictor.fastserve import FastPredictorServer
                 from ..predictor.predictor import Predictor
-                from ..predictor.server import create_app
                 predictor = Predictor.from_inference_job(env['RAFIKI_INFERENCE_JOB_ID'], db=db)
-                srv = make_server('127.0.0.1', int(env['RAFIKI_SERVICE_PORT']), create_app(predictor), threaded=True)
+                srv = FastPredictorServer(predictor, '127.0.0.1', int(env['RAFIKI_SERVICE_PORT'])).start()
                 self.servers[sid] = srv
                 db.mark_service_as_running(db.get_service(sid))
-                srv.serve_forever()
         except Exception:
             logger.error('inline service %s failed:\n%s', sid, traceback.format_exc())
             db.mark_service_as_errored(db.get_service(sid))

@@ -3,7 +3,9 @@ rafiki/predictor/app.py:23-30) plus ``POST /predict_batch {"queries": [...]}`` (
 ``predict_batch`` TODO, predictor.py:85-87).  Unauthenticated, like the reference.
 
 Run as a service: ``python -m rafiki_amd.predictor.server`` with RAFIKI_INFERENCE_JOB_ID,
-RAFIKI_SERVICE_ID and RAFIKI_SERVICE_PORT in the environment.
+RAFIKI_SERVICE_ID and RAFIKI_SERVICE_PORT in the environment.  The service serves through the
+event-loop front end (``fastserve.FastPredictorServer``, same routes); RAFIKI_PREDICTOR_SERVER=flask
+selects this Flask app instead.
 """
 from __future__ import annotations
 
@@ -90,11 +92,18 @@ def main():
         if sid:
             db.mark_service_as_errored(db.get_service(sid))
         return 1
-    app = create_app(predictor)
+    port = int(os.environ.get('RAFIKI_SERVICE_PORT', '3003'))
+    if os.environ.get('RAFIKI_PREDICTOR_SERVER', 'fast') == 'flask':
+        app = create_app(predictor)
+        if sid:
+            db.mark_service_as_running(db.get_service(sid))
+        app.run(host='0.0.0.0', port=port, threaded=True)
+        return 0
+    from .fastserve import FastPredictorServer
+    srv = FastPredictorServer(predictor, '0.0.0.0', port)
     if sid:
         db.mark_service_as_running(db.get_service(sid))
-    port = int(os.environ.get('RAFIKI_SERVICE_PORT', '3003'))
-    app.run(host='0.0.0.0', port=port, threaded=True)
+    srv.serve_forever()
     return 0
 
 

@@ -73,16 +73,18 @@ def _client_proc(url, kind, threads, seconds, q, payload):
     q.put(sum(counts))
 
 
-def http_bench(pred, rng, args):
+def http_bench(pred, rng, args, server='fast'):
     import io
-    import requests
-    from werkzeug.serving import make_server
     from rafiki_amd.container.container_manager import free_port
-    from rafiki_amd.predictor.server import create_app
     port = free_port()
-    srv = make_server('127.0.0.1', port, create_app(pred), threaded=True)
-    th = threading.Thread(target=srv.serve_forever, daemon=True)
-    th.start()
+    if server == 'fast':
+        from rafiki_amd.predictor.fastserve import FastPredictorServer
+        srv = FastPredictorServer(pred, '127.0.0.1', port).start()
+    else:
+        from werkzeug.serving import make_server
+        from rafiki_amd.predictor.server import create_app
+        srv = make_server('127.0.0.1', port, create_app(pred), threaded=True)
+        threading.Thread(target=srv.serve_forever, daemon=True).start()
     url = 'http://127.0.0.1:{}'.format(port)
     out = {}
     one = rng.integers(0, 256, (32, 32, 3)).tolist()
@@ -108,6 +110,8 @@ def http_bench(pred, rng, args):
     pred.start()
     out['json_single_query_qps_8x8clients'] = run('json1', 8, 8)
     out['npy_batch128_qps_4x2clients'] = run('npy', 4, 2)
+    if server == 'fast':
+        out['json_single_query_qps_16x16clients'] = run('json1', 16, 16)
     srv.shutdown()
     return out
 
@@ -152,7 +156,8 @@ def main():
         dt = timed(lambda: pred.predict_array(arr), it)
         res['array'][b] = {'qps': round(b * it / dt, 1), 'ms_per_batch': round(1e3 * dt / it, 3)}
     # real HTTP: the predictor's Flask app on a local port, concurrent clients
-    res['http'] = http_bench(pred, rng, args)
+    res['http'] = http_bench(pred, rng, args, 'fast')
+    res['http_flask'] = http_bench(pred, rng, args, 'flask')
     # dynamic batcher under concurrent single-query clients
     pred.start()
     one = rng.integers(0, 256, (32, 32, 3)).tolist()

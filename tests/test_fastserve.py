@@ -1,0 +1,99 @@
+"""The event-loop predictor front end (rafiki_amd.predictor.fastserve) against a numpy stand-in
+predictor: wire contract of the reference predictor app (POST /predict {query} -> {prediction}),
+keep-alive and Connection: close, batching of concurrent single queries, errors as HTTP 500."""
+import io
+import threading
+
+import numpy as np
+import pytest
+import requests
+
+
+class FakeCache:
+    used = 0
+
+
+class FakePredictor:
+    def __init__(self):
+        self.models = [('a', None), ('b', None)]
+        self.stats = {'queries': 0}
+        self.cache = FakeCache()
+        self.batch_sizes = []
+        self.lock = threading.Lock()
+
+    def _fast_path(self):
+        return True
+
+    def _probs(self, arr):
+        s = arr.reshape(len(arr), -1).astype(np.float64).sum(1)
+        return np.stack([s % 7, s % 5, s % 3], 1).astype(np.float32)
+
+    def predict_array(self, arr):
+        arr = np.asarray(arr)
+        if arr.reshape(len(arr), -1).max(initial=0) == 255:
+            raise ValueError('poisoned query')
+        with self.lock:
+            self.batch_sizes.append(len(arr))
+        return self._probs(arr)
+
+    def predict(self, queries):
+        return [self._probs(np.asarray([q], dtype=np.uint8))[0].tolist() for q in queries]
+
+
+@pytest.fixture()
+def server():
+    from rafiki_amd.predictor.fastserve import FastPredictorServer
+    fake = FakePredictor()
+    srv = FastPredictorServer(fake, '127.0.0.1', 0).start()
+    yield srv, fake, 'http://127.0.0.1:{}'.format(srv.port)
+    srv.shutdown()
+
+
+def test_single_and_batch_contract(server):
+    srv, fake, url = server
+    assert requests.get(url + '/').text == 'Rafiki Predictor is up.'
+    q = np.arange(12, dtype=np.uint8).reshape(3, 4)
+    r = requests.post(url + '/predict', json={'query': q.tolist()})
+    assert r.status_code == 200 and r.json()['prediction'] == fake._probs(q[None])[0].tolist()
+    qs = np.arange(24, dtype=np.uint8).reshape(2, 3, 4)
+    r = requests.post(url + '/predict_batch', json={'queries': qs.tolist()})
+    assert np.allclose(r.json()['predictions'], fake._probs(qs))
+    buf = io.BytesIO()
+    np.save(buf, qs, allow_pickle=False)
+    r = requests.post(url + '/predict_batch_npy', data=buf.getvalue())
+    assert np.allclose(np.load(io.BytesIO(r.content)), fake._probs(qs))
+    # non-image query (e.g. POS tokens) goes through predict()
+    r = requests.post(url + '/predict', json={'query': [[1, 2], [3, 4]]})
+    assert r.status_code == 200
+    assert requests.get(url + '/nope').status_code == 404
+    assert requests.get(url + '/predict').status_code == 405
+    assert requests.get(url + '/stats').json()['server']['requests'] >= 5
+    assert 'rafiki_predictor_requests' in requests.get(url + '/metrics').text
+
+
+def test_errors_are_500_and_connection_close(server):
+    srv, fake, url = server
+    bad = np.full((2, 2), 255, dtype=np.uint8).tolist()
+    r = requests.post(url + '/predict', json={'query': bad})
+    assert r.status_code == 500 and 'poisoned query' in r.text
+    r = requests.post(url + '/predict', json={'query': [[1, 2]]}, headers={'Connection': 'close'})
+    assert r.status_code == 200 and r.headers.get('Connection', '').lower() == 'close'
+
+
+def test_concurrent_single_queries_are_batched(server):
+    srv, fake, url = server
+    rng = np.random.default_rng(0)
+    qs = rng.integers(0, 200, (96, 4, 4), dtype=np.uint8)
+    out = [None] * len(qs)
+
+    def client(lo, hi):
+        s = requests.Session()
+        for i in range(lo, hi):
+            out[i] = s.post(url + '/predict', json={'query': qs[i].tolist()}).json()['prediction']
+    ts = [threading.Thread(target=client, args=(k * 12, (k + 1) * 12)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert np.allclose(np.asarray(out), fake._probs(qs))
+    assert sum(fake.batch_sizes) == 96 and len(fake.batch_sizes) < 96   # stacked into batches
