@@ -169,3 +169,54 @@ def test_worker_process_on_gpu_over_rccl(tmp_path):
     assert len(trials) == 2 and all(t.status == 'COMPLETED' for t in trials), log[-3000:]
     for t in trials:
         assert os.path.exists(t.params_file_path) and 0.0 <= t.score <= 1.0
+
+
+def test_crash_resume_on_gpu_matches_uninterrupted(tmp_path, monkeypatch):
+    """Epoch checkpoint of a GPU trial (hipGraph-captured step, flat arena, device RNG) restored in
+    place after a crash: the resumed trial ends where an uninterrupted one does."""
+    import pickle
+    from rafiki_amd.constants import TrialStatus
+    from rafiki_amd.db.database import Database
+    from rafiki_amd.models import model_file
+    from rafiki_amd.utils import faults
+    from rafiki_amd.utils.auth import hash_password
+    from rafiki_amd.worker.train import TrainWorker
+    monkeypatch.delenv('RAFIKI_CPU_ONLY', raising=False)
+    data = 'synthetic://image?n=2048&size=28&channels=1&classes=10&seed=0'
+    test = 'synthetic://image?n=256&size=28&channels=1&classes=10&seed=1'
+
+    def setup(d):
+        os.makedirs(d, exist_ok=True)
+        monkeypatch.setenv('WORKDIR_PATH', d)
+        db = Database(os.path.join(d, 'db.sqlite3'))
+        u = db.create_user('u@x', hash_password('p'), 'ADMIN')
+        with open(model_file('FeedForward'), 'rb') as f:
+            m = db.create_model(u.id, 'ff', 'IMAGE_CLASSIFICATION', f.read(), 'FeedForward', 'img', {}, 'PRIVATE')
+        tj = db.create_train_job(u.id, 'app', 1, 'IMAGE_CLASSIFICATION', {'MODEL_TRIAL_COUNT': 1}, data, test)
+        sub = db.create_sub_train_job(tj.id, m.id, u.id)
+        svc = db.create_service('TRAIN', 'test', 'img', 1, 1)
+        db.create_train_job_worker(svc.id, sub.id)
+        return db, svc.id, sub.id
+
+    finals = []
+    for crash in (False, True):
+        d = str(tmp_path / ('crash' if crash else 'clean'))
+        db, sid, sub_id = setup(d)
+        params = os.path.join(d, 'params')
+        faults.reset()
+        if crash:
+            monkeypatch.setenv('RAFIKI_FAULT_INJECT', 'crash:epoch=1')
+            with pytest.raises(faults.WorkerCrash):
+                TrainWorker(sid, 'w0', db=db, seed=0, params_dir=params).start()
+            monkeypatch.setenv('RAFIKI_FAULT_INJECT', '')
+            faults.reset()
+        TrainWorker(sid, 'w0', db=db, seed=0, params_dir=params).start()
+        (t,) = db.get_trials_of_sub_train_job(sub_id)
+        assert t.status == TrialStatus.COMPLETED
+        with open(t.params_file_path, 'rb') as f:
+            st = pickle.load(f)['state']
+        finals.append(np.concatenate([np.asarray(v, dtype=np.float64).ravel() for k, v in sorted(st.items())
+                                      if isinstance(v, np.ndarray)]))
+    a, b = finals
+    cosv = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+    assert cosv > 0.999, cosv
