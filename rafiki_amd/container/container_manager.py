@@ -131,6 +131,12 @@ class LocalProcessManager(ContainerManager):
         env.update({'RANK': str(rank), 'LOCAL_RANK': str(rank), 'WORLD_SIZE': str(svc['world']),
                     'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(svc['master_port'])})
         env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        if env.get('RAFIKI_DEBUG_SYNC', '0') not in ('', '0'):
+            # race/fault triage: every kernel launch serialised and synchronous, so a
+            # faulting kernel is reported at its own launch instead of at a later sync point
+            env['AMD_SERIALIZE_KERNEL'] = '3'
+            env['AMD_SERIALIZE_COPY'] = '3'
+            env['HIP_LAUNCH_BLOCKING'] = '1'
         if svc['gpus']:
             env['HIP_VISIBLE_DEVICES'] = ','.join(str(g) for g in svc['gpus'])
         else:

@@ -61,11 +61,21 @@ class ModelLogger:
             self.lg, self.phase = lg, phase
 
         def __enter__(self):
+            self.cuda = _cuda_in_use()
+            if self.cuda is not None:
+                self.cuda.synchronize()
+                self.cuda.reset_peak_memory_stats()
             self.t0 = time.perf_counter()
             return self
 
         def __exit__(self, *exc):
-            self.lg.log_phase(self.phase, time.perf_counter() - self.t0)
+            extra = {}
+            if self.cuda is not None:
+                # GPU telemetry: queued work is part of the phase, HBM peak of it
+                self.cuda.synchronize()
+                extra = {'hbm_peak_bytes': int(self.cuda.max_memory_allocated()),
+                         'hbm_reserved_bytes': int(self.cuda.memory_reserved())}
+            self.lg.log_phase(self.phase, time.perf_counter() - self.t0, **extra)
             return False
 
     def phase(self, name):
@@ -136,3 +146,15 @@ class ModelLoggerDebugHandler(logging.Handler):
 
 
 logger = ModelLogger()
+
+
+def _cuda_in_use():
+    """torch.cuda if this process already initialised a GPU (never initialises one itself)."""
+    import sys
+    torch = sys.modules.get('torch')
+    if torch is None:
+        return None
+    try:
+        return torch.cuda if torch.cuda.is_initialized() else None
+    except Exception:
+        return None

@@ -122,6 +122,8 @@ def test_rest_train_infer_predict_on_gpu(tmp_path):
         assert len(trials) == 2 and all(t['status'] == 'COMPLETED' for t in trials), trials
         logs = dev_c.get_trial_logs(trials[0]['id'])
         assert any('images_per_sec' in mm for mm in logs['metrics']) or logs['metrics']
+        train_phase = [mm for mm in logs['metrics'] if mm.get('phase') == 'train']
+        assert train_phase and train_phase[0]['hbm_peak_bytes'] > 0, logs['metrics']
         ij = dev_c.create_inference_job(app)
         pred = dev_c.predict(ij['predictor_host'], imgs[330].tolist())
         assert len(pred) == 10 and abs(sum(pred) - 1.0) < 1e-3
