@@ -745,6 +745,132 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
   }
 }
 
+// ================================================================================================
+// Wave-K-split 64x64 tile (tile shape 4).  The 2x2 wave grid above gives each wave a 32x32 quarter:
+// 8 fragment reads (ds_read) per 8 MFMAs, and with the DMA writes that is ~1.5x the LDS bandwidth
+// a CU has at full MFMA rate — the wall the small-M layers hit (VGG 4x4 / 8x8 convs: M = 4096 /
+// 16384, where 64x64 is the only tile that fills 256 CUs without split-K slabs).  Here every wave
+// owns the WHOLE 64x64 output tile for one 32-wide k-slice of each PAIR of K-tiles (4 slices per
+// ring stage, one per wave): 8 fragment reads per 16 MFMAs.  The four partial tiles meet in LDS at
+// the end and wave w runs the epilogue for rows 16w..16w+15 (fp64-atomic statistics only: the
+// per-wave partial-row layout of FLAG_STATS without FLAG_SATOM is refused on the host).
+// Ring: NST stages of two K-tiles, NST-1 pairs in flight, one raw barrier per pair.  An odd K-tile
+// count leaves the last pair half-filled (waves 2-3 skip it); while that pair is in flight the
+// counted waits fall back to vmcnt(0), since it carries fewer DMAs than the count assumes.
+// ================================================================================================
+template <int AM, int BMODE, int EPI, int NST>
+__global__ __launch_bounds__(256) void igemm_ks_kernel(const IgemmParams p) {
+  constexpr int BM = 64, BN = 64, MI = 4, NI = 4;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, TB = A_BYTES + B_BYTES, SB = 2 * TB;
+  constexpr int L2 = 2 * (DmaOperand<AM, BM>::NI + DmaOperand<BMODE, BN>::NI);  // DMA instr / wave / pair
+  constexpr int SMEM = NST * SB > 4 * MI * NI * 64 * 16 ? NST * SB : 4 * MI * NI * 64 * 16;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wid >> 1, ks = wid & 1;  // K-tile of the pair, 32-wide slice of that tile
+  const int tilesN = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / tilesN, nt = bid - mt * tilesN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kTiles = (p.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * p.ktPer;
+  const int kt1 = min(kTiles, kt0 + p.ktPer);
+  const int nPairs = kt1 > kt0 ? (kt1 - kt0 + 1) >> 1 : 0;
+  const bool oddTail = ((kt1 - kt0) & 1) != 0;
+
+  DmaOperand<AM, BM> opA;
+  DmaOperand<BMODE, BN> opB;
+  opA.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane);
+  opB.init(p, p.B, p.bytesB, p.ldb, n0, p.N, wid, lane);
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int pr, int stage) {
+    char* st = smem + stage * SB;
+    const int kt = kt0 + 2 * pr;
+    opA.issue(p, st, kt, p.K, p.lda, wid);
+    opB.issue(p, st + A_BYTES, kt, p.K, p.ldb, wid);
+    if (kt + 1 < kt1) {
+      opA.issue(p, st + TB, kt + 1, p.K, p.lda, wid);
+      opB.issue(p, st + TB + A_BYTES, kt + 1, p.K, p.ldb, wid);
+    }
+  };
+  auto compute = [&](const char* sp) {
+    const char* la = sp + half * TB;
+    const char* lb = la + A_BYTES;
+    bf16x8 af[MI], bfr[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[i] = Operand<AM, BM>::frag(la, i * 16, ks * 32, lane);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) bfr[j] = Operand<BMODE, BN>::frag(lb, j * 16, ks * 32, lane);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  };
+
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nPairs) issue(t, t);
+  int stage = 0;
+  for (int pr = 0; pr < nPairs; ++pr) {
+    const int ahead = nPairs - 1 - pr;  // pairs after pr already issued (capped at NST-2 below)
+    if (oddTail && ahead >= 1 && ahead <= NST - 2) wait_vmcnt<0>();
+    else if (ahead >= NST - 2) wait_vmcnt<L2 * (NST - 2)>();
+    else if (NST >= 4 && ahead == 2) wait_vmcnt<L2 * 2>();
+    else if (ahead == 1) wait_vmcnt<L2>();
+    else wait_vmcnt<0>();
+    raw_barrier();
+    if (pr + NST - 1 < nPairs) issue(pr + NST - 1, stage == 0 ? NST - 1 : stage - 1);
+    if (half == 0 || kt0 + 2 * pr + 1 < kt1) compute(smem + stage * SB);
+    stage = stage == NST - 1 ? 0 : stage + 1;
+  }
+  wait_vmcnt<0>();
+  raw_barrier();  // every wave is done with the ring: reuse it for the cross-wave reduction
+
+  // partial tile of wave w, fragment (i, j) -> red[i][w][j][lane]; wave w then sums row-block i = w
+  f32x4* red = (f32x4*)smem;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) red[((i * 4 + wid) * NI + j) * 64 + lane] = acc[i][j];
+  __syncthreads();
+  f32x4 r[1][NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    f32x4 v = red[((wid * 4 + 0) * NI + j) * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += red[((wid * 4 + w) * NI + j) * 64 + lane];
+    r[0][j] = v;
+  }
+
+  const int mrow = m0 + wid * 16 + (lane & 15);
+  const int ncol = n0 + 4 * (lane >> 4);
+  if constexpr (EPI == EPI_BF16) {
+    tile_epilogue<1, NI, true>(p, r, mrow, ncol, mt, 0, lane);
+  } else {
+    float* C = (float*)p.out + (long long)blockIdx.z * p.slabStride;
+    if (mrow < p.M) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int n = ncol + j * 16;
+        if (n >= p.N) continue;
+        f32x4 v = r[0][j] * p.alpha;
+        if (p.flags & FLAG_BIAS) v += *(const f32x4*)(p.bias + n);
+        float* dst = C + (long long)mrow * p.ldc + n;
+        if (p.flags & FLAG_ACCUM) v += *(const f32x4*)dst;
+        *(f32x4*)dst = v;
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int AM, int BMODE, int EPI, int PF>
 __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -908,6 +1034,15 @@ int launch_modes(int tile, const IgemmParams& p, int splits, hipStream_t st) {
     case 1: return launch_tile<128, 64, AM, BMODE, EPI>(p, splits, pf, st);
     case 2: return launch_tile<64, 128, AM, BMODE, EPI>(p, splits, pf, st);
     case 3: return launch_tile<64, 64, AM, BMODE, EPI>(p, splits, pf, st);
+    case 4: {  // 64x64 wave-K-split (LDS-DMA only; fp64-atomic statistics only)
+      if (pf != 3 && pf != 4) return RK_EUNSUPPORTED;
+      if ((p.flags & FLAG_STATS) && !(p.flags & FLAG_SATOM)) return RK_EUNSUPPORTED;
+      dim3 grid(rk_cdiv(p.M, 64) * rk_cdiv(p.N, 64), 1, splits);
+      if (pf == 3) hipLaunchKernelGGL((igemm_ks_kernel<AM, BMODE, EPI, 3>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((igemm_ks_kernel<AM, BMODE, EPI, 2>), grid, dim3(256), 0, st, p);
+      RK_LAUNCH_CHECK();
+      return RK_OK;
+    }
   }
   return RK_EBADARG;
 }
@@ -942,18 +1077,22 @@ RK_DEV bf16x8 patch_frag(const char* patch, int pp, int kb, int lane) {
   return *(const bf16x8*)(patch + pp * 128 + ((c ^ (pp & 7)) << 4));
 }
 
-template <int BM, int BN, int W, int BMODE, int FLIP>
-__global__ __launch_bounds__(256, BN == 64 ? 2 : 1) void hconv_kernel(const IgemmParams p, const int per_block) {
-  constexpr int TH = BM / W;                   // output rows per item
-  constexpr int PC = W + 2, NPP = (TH + 2) * PC;
+// IH > 0: whole-image items for small images (VGG 4x4 layers): an item is BM / (IH*W) images, the
+// patch stacks one (IH+2) x (W+2) halo image per image, so the tap shift stays a constant offset.
+template <int BM, int BN, int W, int BMODE, int FLIP, int IH = 0>
+__global__ __launch_bounds__(256, BN == 64 && IH == 0 ? 2 : 1) void hconv_kernel(const IgemmParams p,
+                                                                                const int per_block) {
+  constexpr int TH = IH ? IH : BM / W;         // output rows per item (per image when IH > 0)
+  constexpr int IMG = IH ? BM / (IH * W) : 1;  // images per item
+  constexpr int PC = W + 2, PIMG = (TH + 2) * PC, NPP = IMG * PIMG;
   constexpr int LP = (NPP * 8 + 255) / 256;    // patch DMA instructions per wave
   constexpr int P_BYTES = LP * 4 * 1024;
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int LB = BN / 32;                  // B DMA instructions per wave per K-tile
   constexpr int R = BN / 8;                    // K-outer B: 16-B slots per k-row
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
-  constexpr int LOG2W = W == 8 ? 3 : W == 16 ? 4 : 5;
-  static_assert(BM % W == 0 && LP + LB <= 63, "tile");
+  constexpr int LOG2W = W == 4 ? 2 : W == 8 ? 3 : W == 16 ? 4 : 5;
+  static_assert(BM % W == 0 && LP + LB <= 63 && (IH == 0 || BM % (IH * W) == 0), "tile");
   __shared__ __attribute__((aligned(16))) char smem[2 * P_BYTES + 3 * B_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -981,9 +1120,10 @@ __global__ __launch_bounds__(256, BN == 64 ? 2 : 1) void hconv_kernel(const Igem
     const int slot = (wid * LP + q) * 64 + lane;
     const int pp = slot >> 3;
     const int c = (slot & 7) ^ (pp & 7);
-    const int pr = pp / PC, pcol = pp - pr * PC;
-    const bool ok = pp < NPP && pcol >= 1 && pcol <= W;
-    prel[q] = ((((pr - 1) * W + (pcol - 1)) << log2C) << 1) + c * 16;
+    const int img = pp / PIMG, rem = pp - img * PIMG;
+    const int pr = rem / PC, pcol = rem - pr * PC;
+    const bool ok = pp < NPP && pcol >= 1 && pcol <= W && (IH == 0 || (pr >= 1 && pr <= TH));
+    prel[q] = ((((img * TH + pr - 1) * W + (pcol - 1)) << log2C) << 1) + c * 16;
     prow[q] = ok ? pr : -1000;
   }
   // ---- B DMA lane constants (tile-independent part of the source offset)
@@ -1009,7 +1149,8 @@ __global__ __launch_bounds__(256, BN == 64 ? 2 : 1) void hconv_kernel(const Igem
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int ml = wm * WM + i * 16 + (lane & 15);
-    ppb[i] = ((ml >> LOG2W) + 1) * PC + (ml & (W - 1)) + 1;
+    const int img = ml / (TH * W), rem = ml - img * (TH * W);
+    ppb[i] = img * PIMG + ((rem >> LOG2W) + 1) * PC + (rem & (W - 1)) + 1;
   }
 
   // phase = (item, 64-channel chunk): state of the current and the next phase, advanced once per
@@ -1031,7 +1172,7 @@ __global__ __launch_bounds__(256, BN == 64 ? 2 : 1) void hconv_kernel(const Igem
       return ((unsigned)(q.cc * 64) * (unsigned)p.ldb + (unsigned)(q.nt * BN)) * 2u;
   };
   auto issue_patch = [&](const Phase& q, int buf) {
-    const int r0 = (q.mt & (tilesPerImg - 1)) * TH;  // tilesPerImg = H*W/BM is a power of two
+    const int r0 = IH ? 0 : (q.mt & (tilesPerImg - 1)) * TH;  // tilesPerImg = H*W/BM: a power of two
     const int base = (((q.mt * BM) << log2C) << 1) + q.cc * 128;
     char* dst = smem + buf * P_BYTES + wid * LP * 1024;
 #pragma unroll
@@ -1097,16 +1238,16 @@ __global__ __launch_bounds__(256, BN == 64 ? 2 : 1) void hconv_kernel(const Igem
   }
 }
 
-template <int BM, int BN, int W>
+template <int BM, int BN, int W, int IH = 0>
 int launch_hconv_w(bool dgrad, const IgemmParams& p, int grid, hipStream_t st) {
   const int items = (p.M / BM) * (p.N / BN);
   if (grid <= 0 || grid > items) grid = items;
   const int per = rk_cdiv(items, grid);
   grid = rk_cdiv(items, per);
   if (dgrad)
-    hipLaunchKernelGGL((hconv_kernel<BM, BN, W, OP_WTAP_KOUT, 1>), dim3(grid), dim3(256), 0, st, p, per);
+    hipLaunchKernelGGL((hconv_kernel<BM, BN, W, OP_WTAP_KOUT, 1, IH>), dim3(grid), dim3(256), 0, st, p, per);
   else
-    hipLaunchKernelGGL((hconv_kernel<BM, BN, W, OP_DENSE_KIN, 0>), dim3(grid), dim3(256), 0, st, p, per);
+    hipLaunchKernelGGL((hconv_kernel<BM, BN, W, OP_DENSE_KIN, 0, IH>), dim3(grid), dim3(256), 0, st, p, per);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -1114,6 +1255,7 @@ int launch_hconv_w(bool dgrad, const IgemmParams& p, int grid, hipStream_t st) {
 template <int BN>
 int launch_hconv_bn(bool dgrad, const IgemmParams& p, int grid, hipStream_t st) {
   switch (p.W) {
+    case 4: return launch_hconv_w<128, BN, 4, 4>(dgrad, p, grid, st);  // 8 whole 4x4 images per item
     case 8: return launch_hconv_w<64, BN, 8>(dgrad, p, grid, st);
     case 16: return launch_hconv_w<128, BN, 16>(dgrad, p, grid, st);
     case 32: return launch_hconv_w<128, BN, 32>(dgrad, p, grid, st);
@@ -1304,10 +1446,13 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
   if (conv && (p.log2C < 0 || p.log2H < 0 || p.log2W < 0)) tile &= 15 | 16;
   if (epi == 0 && splits != 1) return RK_EBADARG;
   switch (kind) {
-    case 0: if (epi != 0) return RK_EBADARG;
-      return launch_modes<OP_CONV_KIN, OP_DENSE_KIN, EPI_BF16>(tile, p, splits, st);
-    case 1: if (epi != 0 || p.log2Cb < 0) return RK_EUNSUPPORTED;
-      return launch_modes<OP_CONVT_KIN, OP_WTAP_KOUT, EPI_BF16>(tile, p, splits, st);
+    // conv forward / data-gradient with epi 1: split-K fp32 slabs for the small-M layers (4x4 / 8x8
+    // VGG convs), combined by rk_slab_epi (bf16 out + BN statistics / BN-backward gate)
+    case 0: return epi == 0 ? launch_modes<OP_CONV_KIN, OP_DENSE_KIN, EPI_BF16>(tile, p, splits, st)
+                            : launch_modes<OP_CONV_KIN, OP_DENSE_KIN, EPI_F32>(tile, p, splits, st);
+    case 1: if (p.log2Cb < 0) return RK_EUNSUPPORTED;
+      return epi == 0 ? launch_modes<OP_CONVT_KIN, OP_WTAP_KOUT, EPI_BF16>(tile, p, splits, st)
+                      : launch_modes<OP_CONVT_KIN, OP_WTAP_KOUT, EPI_F32>(tile, p, splits, st);
     case 2: if (epi != 1) return RK_EBADARG;
       return launch_modes<OP_DENSE_KOUT, OP_CONV_KOUT, EPI_F32>(tile, p, splits, st);
     case 3: return epi == 0 ? launch_modes<OP_DENSE_KIN, OP_DENSE_KIN, EPI_BF16>(tile, p, splits, st)
@@ -1333,8 +1478,12 @@ extern "C" int rk_hconv(int dgrad, int tile, const void* A, const void* B, void*
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
   const int BN = (tile & 1) ? 128 : 64;
   const int BM = W == 8 ? 64 : 128;
-  if (W != 8 && W != 16 && W != 32) return RK_EUNSUPPORTED;
-  if (rk_log2(H) < 0 || (H * W) % BM != 0 || M <= 0 || M % (H * W) != 0) return RK_EUNSUPPORTED;
+  if (W != 4 && W != 8 && W != 16 && W != 32) return RK_EUNSUPPORTED;
+  if (W == 4) {  // whole-image items: 8 images of 4x4
+    if (H != 4 || M <= 0 || M % BM != 0) return RK_EUNSUPPORTED;
+  } else if (rk_log2(H) < 0 || (H * W) % BM != 0 || M <= 0 || M % (H * W) != 0) {
+    return RK_EUNSUPPORTED;
+  }
   if (rk_log2(Cch) < 6 || N <= 0 || N % BN != 0 || K != 9 * Cch) return RK_EUNSUPPORTED;
   if (ldb != (dgrad ? 9 * N : K)) return RK_EBADARG;
   IgemmParams p{};

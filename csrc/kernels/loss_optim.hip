@@ -407,6 +407,97 @@ extern "C" int rk_reduce_slabs_epi(const float* slab, int S, int M, int N, const
   return RK_OK;
 }
 
+// ---- split-K combine for conv forward / data-gradient ----------------------------------------
+// out[m][n] (bf16) = sum_s slab[s][m][n] with the igemm tile epilogue's BatchNorm options, so the
+// small-M convs (VGG 4x4 / 8x8 layers: 64-128 output tiles of 128x128) can split K over the chip:
+//   mode 0 plain; mode 1 forward statistics (sum v, sum v^2) -> fp64 slot table acc [SL][2][N];
+//   mode 2 FLAG_BNB data-gradient: v *= [y*scale + shift > 0], (sum v, sum v*y) -> acc;
+//   mode 3 ReLU-backward gate: v *= [gate > 0].
+// A block sweeps whole rows: N/4 threads per row (4 fixed channels each), 256/(N/4) rows per sweep,
+// so a thread's channel sums stay in registers; one LDS fold per block, then one fp64 atomic per
+// (kind, channel) per block into slot blockIdx & slmask (the grid is capped to bound atomics).
+__global__ __launch_bounds__(256) void slab_epi_kernel(const float* __restrict__ slab, int S, int M, int N, int mode,
+                                                       const bf16* __restrict__ gate, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, double* __restrict__ acc,
+                                                       int slmask, bf16* __restrict__ out) {
+  __shared__ float red[2][1024];
+  const int tpr = N >> 2, rpb = 256 / tpr;
+  const int tid = threadIdx.x, c4 = tid % tpr, r0 = tid / tpr;
+  const long long sn = (long long)M * N;
+  float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
+  if (mode == 2) {
+    sc = *(const f32x4*)(scale + 4 * c4);
+    sh = *(const f32x4*)(shift + 4 * c4);
+  }
+  for (int m = blockIdx.x * rpb + r0; m < M; m += gridDim.x * rpb) {
+    const long long i = (long long)m * N + 4 * c4;
+    f32x4 a = *(const f32x4*)(slab + i);
+    int s0 = 1;
+    for (; s0 + 3 < S; s0 += 4) {  // 4 independent slab loads in flight, fixed summation order
+      f32x4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = *(const f32x4*)(slab + (s0 + k) * sn + i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a += v[k];
+    }
+    for (; s0 < S; ++s0) a += *(const f32x4*)(slab + s0 * sn + i);
+    if (mode >= 2) {
+      const bf16x4 g = *(const bf16x4*)(gate + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float yv = (float)g[e];
+        if (mode == 3) {
+          a[e] = yv > 0.f ? a[e] : 0.f;
+        } else {
+          a[e] = yv * sc[e] + sh[e] > 0.f ? a[e] : 0.f;
+          s[e] += a[e];
+          q[e] += a[e] * yv;
+        }
+      }
+    } else if (mode == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[e] += a[e];
+        q[e] += a[e] * a[e];
+      }
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (bf16)a[e];
+    *(bf16x4*)(out + i) = o;
+  }
+  if (mode == 1 || mode == 2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[0][r0 * N + 4 * c4 + e] = s[e];
+      red[1][r0 * N + 4 * c4 + e] = q[e];
+    }
+    __syncthreads();
+    double* dst = acc + (long long)(blockIdx.x & slmask) * 2 * N;
+    for (int c = tid; c < 2 * N; c += 256) {
+      const int k = c >= N ? 1 : 0, ch = c - k * N;
+      float v = 0.f;
+      for (int r = 0; r < rpb; ++r) v += red[k][r * N + ch];
+      unsafeAtomicAdd(dst + (long long)k * N + ch, (double)v);
+    }
+  }
+}
+
+extern "C" int rk_slab_epi(const float* slab, int S, int M, int N, int mode, const void* gate, const float* scale,
+                           const float* shift, double* acc, int slmask, void* out, void* stream) {
+  if (S <= 0 || M <= 0 || N % 4 || N > 1024 || 256 % (N / 4) || mode < 0 || mode > 3) return RK_EUNSUPPORTED;
+  if ((mode == 1 || mode == 2) && !acc) return RK_EBADARG;
+  if (mode >= 2 && !gate) return RK_EBADARG;
+  if (mode == 2 && (!scale || !shift)) return RK_EBADARG;
+  const int rpb = 256 / (N / 4);
+  const int blocks = min((M + rpb - 1) / rpb, 256);
+  hipLaunchKernelGGL(slab_epi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab, S, M, N, mode,
+                     (const bf16*)gate, scale, shift, acc, slmask, (bf16*)out);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
 extern "C" int rk_gather_batch(const void* data, long long row_bytes, const int* labels, const long long* sched,
                                const int* counter, int B, void* out, int* out_y, void* stream) {
   if (row_bytes % 16) return RK_EUNSUPPORTED;

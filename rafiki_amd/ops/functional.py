@@ -29,7 +29,11 @@ FLAG_BNB = 512
 # partial-row path.
 BN_ATOMIC = os.environ.get('RAFIKI_BN_ATOMIC', '1') != '0'
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
-TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
+# shape 4: 64x64 wave-K-split kernel (igemm_ks_kernel, LDS-DMA rings only): each wave owns the whole
+# tile for a quarter of every K-tile pair — half the LDS reads per MFMA of shape 3 (small-M layers)
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (64, 64)]
+KS_TILE = 4
+_KS_VARIANTS = (64, 32)  # 2-stage (64 KiB LDS, 2 blocks/CU) and 3-stage (96 KiB) rings
 NUM_CU = 256
 # Kernel variant bits OR'ed into the tile code (see rk_igemm): 0 register-staged, 16 register ring,
 # 32 LDS-DMA 3-stage ring, 64 LDS-DMA 2-stage, 128 LDS-DMA 4-stage.
@@ -56,7 +60,7 @@ def cdiv(a: int, b: int) -> int:
 def pick_tile(M: int, N: int) -> int:
     """Largest tile that still gives >= 2 blocks per CU without padding waste > 30%."""
     best, best_blocks = 3, -1
-    for t, (bm, bn) in enumerate(TILES):
+    for t, (bm, bn) in enumerate(TILES[:4]):
         blocks = cdiv(M, bm) * cdiv(N, bn)
         waste = (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N)
         if waste > 1.3 and t != 3:
@@ -84,8 +88,9 @@ def pick_splits(M: int, N: int, K: int, tile: int, target_blocks: int = 2 * NUM_
 _VARIANTS = (0, 64, 32, 128) if os.environ.get('RAFIKI_IGEMM_DEEP', '0') == '1' else (0, 64)
 
 
-def _tile_candidates(M, N, fixed_bm=None):
-    """Heuristic pick first (used when tuning is impossible), then every shape x staging variant."""
+def _tile_candidates(M, N, fixed_bm=None, ks=True):
+    """Heuristic pick first (used when tuning is impossible), then every shape x staging variant.
+    ks=False leaves out the wave-K-split shape (it cannot write per-wave partial statistics rows)."""
     first = pick_tile(M, N)
     if fixed_bm is not None:  # stats partial-row count depends on BM: keep BM fixed for stats outputs
         shapes = [t for t in range(4) if TILES[t][0] == fixed_bm]
@@ -97,6 +102,8 @@ def _tile_candidates(M, N, fixed_bm=None):
             c = (t | v,)
             if c not in out:
                 out.append(c)
+    if ks and KS and fixed_bm in (None, 64):
+        out += [(KS_TILE | v,) for v in _KS_VARIANTS]
     return out
 
 
@@ -106,9 +113,9 @@ def _split_candidates(M, N, K):
     first = (t0, s_h)
     out = [first]
     kt = cdiv(K, 64)
-    for t in range(4):
+    for t in range(5 if KS else 4):
         blocks = cdiv(M, TILES[t][0]) * cdiv(N, TILES[t][1])
-        for v in (0, 64, 128):
+        for v in ((0, 64, 128) if t != KS_TILE else _KS_VARIANTS):
             for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
                 if s > kt or (s == 1 and kt > 64) or s * M * N * 4 > (256 << 20):
                     continue
@@ -151,6 +158,7 @@ def stats_rows(M: int, N: int, tile: Optional[int] = None) -> int:
 # Halo-tiled 3x3 conv (rk_hconv): one LDS patch per (item, 64-channel chunk) serves all 9 taps.
 # Candidates are ('h', bn_bit, grid): grid 0 = one item per block, else a persistent grid.
 HCONV = os.environ.get('RAFIKI_HCONV', '1') != '0'
+KS = os.environ.get('RAFIKI_IGEMM_KS', '1') != '0'
 
 
 def _hconv_bm(W: int) -> int:
@@ -158,8 +166,10 @@ def _hconv_bm(W: int) -> int:
 
 
 def _hconv_candidates(M, N, H, W, C, taps):
-    if not HCONV or taps != 9 or W not in (8, 16, 32) or H & (H - 1) or (H * W) % _hconv_bm(W):
+    if not HCONV or taps != 9 or W not in (4, 8, 16, 32) or H & (H - 1):
         return []
+    if (W == 4 and (H != 4 or M % _hconv_bm(W))) or (W != 4 and (H * W) % _hconv_bm(W)):
+        return []  # W = 4: items of 8 whole 4x4 images
     if C < 64 or C & (C - 1) or N % 64:
         return []
     out = []
@@ -181,6 +191,40 @@ def hconv(dgrad, A, B, out, M, N, K, ldb, H, W, C, *, bias=None, stats=None, gat
           slope=0.2, bn_bit=0, grid=0):
     _lib.call("rk_hconv", int(dgrad), int(bn_bit), _p(A), _p(B), _p(out), _p(bias), _p(stats), _p(gate), M, N, K,
               ldb, H, W, C, flags, float(alpha), float(slope), _nbytes(A), _nbytes(B), int(grid), _s())
+    return out
+
+
+def slab_epi(slab, S, M, N, out, *, mode=0, gate=None, scale=None, shift=None, acc=None):
+    """bf16 out[M][N] = sum of S fp32 split-K slabs, plus BN statistics into ``acc`` (mode 1), the
+    BN-backward ReLU mask and sums (mode 2, as FLAG_BNB) or a ReLU-backward gate (mode 3)."""
+    slmask = acc.shape[0] - 1 if acc is not None else 0
+    _lib.call("rk_slab_epi", _p(slab), int(S), int(M), int(N), int(mode), _p(gate), _p(scale), _p(shift), _p(acc),
+              int(slmask), _p(out), _s())
+    return out
+
+
+# Split-K conv forward / data-gradient: ('k', tile, S) = S fp32 slabs from the igemm + one rk_slab_epi
+# combine.  Offered only where a big tile shape (fewer L2->LDS re-reads of both operands) has too few
+# output tiles to fill the chip on its own: the VGG 4x4 / 8x8 layers (M = 4096 / 16384 at batch 256).
+CONV_SPLIT = os.environ.get('RAFIKI_CONV_SPLIT', '1') != '0'
+
+
+def _conv_split_candidates(M, N, K, H, W, C):
+    if not CONV_SPLIT or N % 4 or N > 1024 or 256 % (N // 4) or C & (C - 1) or H & (H - 1) or W & (W - 1):
+        return []
+    kt = cdiv(K, 64)
+    out = []
+    for t in (0, 1, 2):
+        blocks = cdiv(M, TILES[t][0]) * cdiv(N, TILES[t][1])
+        if blocks >= 2 * NUM_CU:
+            continue
+        for s in (2, 3, 4):
+            if s > kt // 4 or blocks * s > 4 * NUM_CU:
+                continue
+            per = cdiv(kt, s)
+            c = ('k', t | 64, cdiv(kt, per))
+            if c not in out:
+                out.append(c)
     return out
 
 
@@ -225,12 +269,21 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, bias=None, want
         if cfg[0] == 'h':
             hconv(0, x, w, out, M, Cout, K, K, H, W, Cin, bias=bias, stats=stats, flags=flags, slope=slope,
                   bn_bit=cfg[1], grid=cfg[2])
+        elif cfg[0] == 'k':
+            slab = torch.empty((cfg[2], M, Cout), device=x.device, dtype=torch.float32)
+            igemm(KIND_CONV_FWD, 1, x, w, slab, M, Cout, K, Cin, K, Cout, H=H, W=W, C=Cin, taps=taps,
+                  splits=cfg[2], slab_stride=M * Cout, tile=cfg[1])
+            slab_epi(slab, cfg[2], M, Cout, out, mode=1 if stats_acc is not None else 0, acc=stats_acc)
         else:
             igemm(KIND_CONV_FWD, 0, x, w, out, M, Cout, K, Cin, K, Cout, bias=bias, stats=stats, H=H, W=W, C=Cin,
                   taps=taps, flags=flags, slope=slope, tile=cfg[0])
     mode = 'acc' if stats_acc is not None else bool(want_stats)
+    partial_rows = want_stats and stats_acc is None
+    split_ok = bias is None and act == ACT_NONE and not partial_rows
     cfg = _tuned(('cf', M, Cout, K, H, W, Cin, taps, mode),
-                 _tile_candidates(M, Cout) + _hconv_candidates(M, Cout, H, W, Cin, taps), run)
+                 _tile_candidates(M, Cout, ks=not partial_rows)
+                 + _hconv_candidates(M, Cout, H, W, Cin, taps)
+                 + (_conv_split_candidates(M, Cout, K, H, W, Cin) if split_ok else []), run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -285,11 +338,21 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, ga
         if cfg[0] == 'h':
             hconv(1, dy, w, out, M, Cin, K, taps * Cin, H, W, Cout, gate=gate, bias=bias, stats=stats, flags=flags,
                   bn_bit=cfg[1], grid=cfg[2])
+        elif cfg[0] == 'k':
+            slab = torch.empty((cfg[2], M, Cin), device=dy.device, dtype=torch.float32)
+            igemm(KIND_CONV_DGRAD, 1, dy, w, slab, M, Cin, K, Cout, taps * Cin, Cin, H=H, W=W, C=Cout, taps=taps,
+                  Cb=Cout, splits=cfg[2], slab_stride=M * Cin, tile=cfg[1])
+            if bn_y is not None:
+                slab_epi(slab, cfg[2], M, Cin, out, mode=2, gate=bn_y, scale=bn_coeffs[2], shift=bn_coeffs[3],
+                         acc=bn_acc)
+            else:
+                slab_epi(slab, cfg[2], M, Cin, out, mode=3 if gate is not None else 0, gate=gate)
         else:
             igemm(KIND_CONV_DGRAD, 0, dy, w, out, M, Cin, K, Cout, taps * Cin, Cin, gate=gate, bias=bias,
                   stats=stats, H=H, W=W, C=Cout, taps=taps, Cb=Cout, flags=flags, tile=cfg[0])
     cfg = _tuned(('cd', M, Cin, K, H, W, Cout, taps),
-                 _tile_candidates(M, Cin) + _hconv_candidates(M, Cin, H, W, Cout, taps), run)
+                 _tile_candidates(M, Cin) + _hconv_candidates(M, Cin, H, W, Cout, taps)
+                 + _conv_split_candidates(M, Cin, K, H, W, Cout), run)
     if bn_acc is not None and autotune.can_tune():
         bn_acc.zero_()  # tuning runs accumulated into it
     run(cfg)

@@ -17,6 +17,9 @@ ap.add_argument('--batch', type=int, default=256)
 ap.add_argument('--reps', type=int, default=20)
 ap.add_argument('--passes', default='fwd,dgrad,wgrad')
 ap.add_argument('--variants', default='0,1,2,3,32,33,34,35,64,65,66,67')
+ap.add_argument('--layers', default='0,1,2,3,4,5,6,7')
+ap.add_argument('--satom', action='store_true', help='forward statistics as fp64 atomic slots (training path; '
+                'required by the wave-K-split tiles 68/36)')
 args = ap.parse_args()
 VARIANTS = [int(v) for v in args.variants.split(',')]
 
@@ -34,6 +37,8 @@ def timeit(fn):
 
 best_total = 0.0
 for li, (cin, cout, hw) in enumerate(LAYERS):
+    if str(li) not in args.layers.split(','):
+        continue
     x = torch.randn(B, hw, hw, cin, device=dev).bfloat16()
     w = (torch.randn(cout, 3, 3, cin, device=dev) * 0.05).bfloat16()
     dy = torch.randn(B, hw, hw, cout, device=dev).bfloat16()
@@ -46,9 +51,14 @@ for li, (cin, cout, hw) in enumerate(LAYERS):
     if 'fwd' in args.passes:
         res = {}
         for t in VARIANTS:
-            stats = torch.empty((F.stats_rows(M, cout, t), 2, cout), device=dev)
+            if args.satom:
+                stats = F.bn_acc_buffer(cout, dev)
+                fl = F.FLAG_STATS | F.FLAG_SATOM | ((stats.shape[0] - 1) << 12)
+            else:
+                stats = torch.empty((F.stats_rows(M, cout, t), 2, cout), device=dev)
+                fl = F.FLAG_STATS
             res[t] = timeit(lambda: F.igemm(F.KIND_CONV_FWD, 0, x, w, y, M, cout, 9 * cin, cin, 9 * cin, cout,
-                                            stats=stats, H=hw, W=hw, C=cin, taps=9, flags=F.FLAG_STATS, tile=t))
+                                            stats=stats, H=hw, W=hw, C=cin, taps=9, flags=fl, tile=t))
         b = min(res, key=res.get)
         best_total += res[b]
         print('c{} fwd   M={:6d} N={:4d} K={:5d} '.format(li, M, cout, 9 * cin) +

@@ -195,7 +195,9 @@ def test_misc(fn):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,bn_bit,grid", [(2, 32, 32, 64, 64, 0, 0), (2, 16, 16, 128, 128, 1, 0),
                                                         (3, 8, 8, 256, 64, 0, 7), (2, 32, 32, 128, 256, 1, 5),
-                                                        (4, 8, 8, 512, 128, 0, 0), (2, 16, 16, 64, 128, 0, 3)])
+                                                        (4, 8, 8, 512, 128, 0, 0), (2, 16, 16, 64, 128, 0, 3),
+                                                        (8, 4, 4, 256, 512, 0, 0), (16, 4, 4, 512, 256, 1, 3),
+                                                        (24, 4, 4, 64, 128, 0, 2)])
 def test_hconv_fwd_dgrad(fn, N, H, W, Cin, Cout, bn_bit, grid):
     """Halo-tiled conv (forward with BN-stats epilogue, and data-gradient) vs PyTorch fp32."""
     torch.manual_seed(11)
@@ -267,3 +269,125 @@ def test_bn_atomic_accumulator_path(fn, N, H, Cin, Cout, pool):
     d2 = fn.bn_bwd_acc(dout, y2, c2, gamma, bacc, pool=pool, dgamma=g2, dbeta=b2)
     assert rel_err(g2, g1) < 1e-4 and rel_err(b2, b1) < 1e-4
     assert rel_err(d2, d1) < 1e-2
+
+
+@pytest.mark.parametrize("stages", [64, 32])
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(16, 4, 4, 512, 512), (4, 8, 8, 256, 128), (3, 4, 4, 64, 128),
+                                            (5, 2, 2, 64, 64)])
+def test_wave_ksplit_tile_all_kinds(fn, stages, N, H, W, Cin, Cout):
+    """64x64 wave-K-split kernel (tile shape 4): conv fwd with fp64-atomic stats, dgrad with the
+    ReLU-gate epilogue, split-K wgrad (odd K-tile counts per split), dense fwd/dX/dW vs fp32."""
+    torch.manual_seed(14)
+    tile = fn.KS_TILE | stages
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    w = (torch.randn(Cout, 9 * Cin, device=DEV) / (3 * Cin ** 0.5)).bfloat16()
+    M, K = N * H * W, 9 * Cin
+    # conv forward + SATOM statistics
+    y = torch.empty(N, H, W, Cout, device=DEV, dtype=torch.bfloat16)
+    acc = fn.bn_acc_buffer(Cout, DEV)
+    flags = fn.FLAG_STATS | fn.FLAG_SATOM | ((acc.shape[0] - 1) << 12)
+    fn.igemm(fn.KIND_CONV_FWD, 0, x, w, y, M, Cout, K, Cin, K, Cout, stats=acc, H=H, W=W, C=Cin, taps=9,
+             flags=flags, tile=tile)
+    ref = F.conv2d(_nhwc_to_nchw(x.float()), _w_to_oihw(w.float().reshape(Cout, 3, 3, Cin)),
+                   padding=1).permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-2
+    s = acc.sum(0).float()
+    assert torch.allclose(s[0], ref.reshape(-1, Cout).sum(0), rtol=1e-3, atol=1e-2 * M ** 0.5)
+    assert torch.allclose(s[1], (ref ** 2).reshape(-1, Cout).sum(0), rtol=2e-3, atol=1e-1)
+    # data gradient with a ReLU gate
+    dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    gate = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    dx = torch.empty(N, H, W, Cin, device=DEV, dtype=torch.bfloat16)
+    fn.igemm(fn.KIND_CONV_DGRAD, 0, dy, w, dx, M, Cin, 9 * Cout, Cout, 9 * Cin, Cin, gate=gate, H=H, W=W, C=Cout,
+             taps=9, Cb=Cout, flags=fn.FLAG_GATE, tile=tile)
+    xr = _nhwc_to_nchw(x.float()).requires_grad_(True)
+    F.conv2d(xr, _w_to_oihw(w.float().reshape(Cout, 3, 3, Cin)), padding=1).backward(_nhwc_to_nchw(dy.float()))
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1) * (gate.float() > 0)) < 1e-2
+    # weight gradient, split-K slabs (3 splits: uneven, odd K-tile counts)
+    splits = 3
+    slab = torch.full((splits, Cout, K), float('nan'), device=DEV)
+    kt = (M + 63) // 64
+    per = (kt + splits - 1) // splits
+    s_eff = (kt + per - 1) // per
+    fn.igemm(fn.KIND_CONV_WGRAD, 1, dy, x, slab, Cout, K, M, Cout, 0, K, H=H, W=W, C=Cin, taps=9, splits=s_eff,
+             slab_stride=Cout * K, tile=tile)
+    dw = slab[:s_eff].sum(0)
+    wr = torch.zeros(Cout, Cin, 3, 3, device=DEV, requires_grad=True)
+    F.conv2d(_nhwc_to_nchw(x.float()), wr, padding=1).backward(_nhwc_to_nchw(dy.float()))
+    assert rel_err(dw, wr.grad.permute(0, 2, 3, 1).reshape(Cout, -1)) < 5e-3
+    # dense forward (bias + ReLU), dX and dW on flattened operands
+    a = x.reshape(M, Cin)
+    wd = (torch.randn(Cout, Cin, device=DEV) / Cin ** 0.5).bfloat16()
+    b = torch.randn(Cout, device=DEV)
+    yd = torch.empty(M, Cout, device=DEV, dtype=torch.bfloat16)
+    fn.igemm(fn.KIND_DENSE, 0, a, wd, yd, M, Cout, Cin, Cin, Cin, Cout, bias=b, flags=fn.FLAG_BIAS | fn.FLAG_RELU,
+             tile=tile)
+    assert rel_err(yd, torch.relu(a.float() @ wd.float().t() + b)) < 1e-2
+    dyd = dy.reshape(M, Cout)
+    dxd = torch.empty(M, Cin, device=DEV, dtype=torch.bfloat16)
+    fn.igemm(fn.KIND_DENSE_DX, 0, dyd, wd, dxd, M, Cin, Cout, Cout, Cin, Cin, tile=tile)
+    assert rel_err(dxd, dyd.float() @ wd.float()) < 1e-2
+    dwd = torch.empty(Cout, Cin, device=DEV)
+    fn.igemm(fn.KIND_DENSE_DW, 1, dyd, a, dwd, Cout, Cin, M, Cout, Cin, Cin, splits=1, tile=tile)
+    assert rel_err(dwd, dyd.float().t() @ a.float()) < 5e-3
+
+
+def test_wave_ksplit_refuses_partial_row_stats(fn):
+    x = torch.randn(2, 4, 4, 64, device=DEV).bfloat16()
+    w = torch.randn(64, 9 * 64, device=DEV).bfloat16()
+    y = torch.empty(2, 4, 4, 64, device=DEV, dtype=torch.bfloat16)
+    stats = torch.zeros(4, 2, 64, device=DEV)
+    with pytest.raises(Exception):
+        fn.igemm(fn.KIND_CONV_FWD, 0, x, w, y, 32, 64, 576, 64, 576, 64, stats=stats, H=4, W=4, C=64, taps=9,
+                 flags=fn.FLAG_STATS, tile=fn.KS_TILE | 64)
+
+
+@pytest.mark.parametrize("tile,S", [(64, 2), (65, 3), (66, 4), (0, 2)])
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(16, 4, 4, 512, 512), (4, 8, 8, 256, 128), (3, 4, 4, 64, 64)])
+def test_conv_split_k_slab_epilogue(fn, tile, S, N, H, W, Cin, Cout):
+    """Split-K conv forward / data-gradient into fp32 slabs + rk_slab_epi: forward statistics (mode 1),
+    the BN-backward mask and sums (mode 2, FLAG_BNB semantics) and a ReLU gate (mode 3) vs fp32."""
+    torch.manual_seed(15)
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    w = (torch.randn(Cout, 9 * Cin, device=DEV) / (3 * Cin ** 0.5)).bfloat16()
+    M, K = N * H * W, 9 * Cin
+    kt = (K + 63) // 64
+    per = (kt + S - 1) // S
+    s_eff = (kt + per - 1) // per
+    slab = torch.full((s_eff, M, Cout), float('nan'), device=DEV)
+    fn.igemm(fn.KIND_CONV_FWD, 1, x, w, slab, M, Cout, K, Cin, K, Cout, H=H, W=W, C=Cin, taps=9, splits=s_eff,
+             slab_stride=M * Cout, tile=tile)
+    y = torch.empty(N, H, W, Cout, device=DEV, dtype=torch.bfloat16)
+    acc = fn.bn_acc_buffer(Cout, DEV)
+    fn.slab_epi(slab, s_eff, M, Cout, y, mode=1, acc=acc)
+    ref = F.conv2d(_nhwc_to_nchw(x.float()), _w_to_oihw(w.float().reshape(Cout, 3, 3, Cin)),
+                   padding=1).permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-2
+    st = acc.sum(0).float()
+    assert torch.allclose(st[0], ref.reshape(-1, Cout).sum(0), rtol=1e-3, atol=1e-2 * M ** 0.5)
+    assert torch.allclose(st[1], (ref ** 2).reshape(-1, Cout).sum(0), rtol=2e-3, atol=1e-1)
+    # data gradient: split-K slabs, then BNB (mode 2) and gate (mode 3) combines
+    dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    kt = (9 * Cout + 63) // 64
+    per = (kt + S - 1) // S
+    s_eff = (kt + per - 1) // per
+    slab = torch.full((s_eff, M, Cin), float('nan'), device=DEV)
+    fn.igemm(fn.KIND_CONV_DGRAD, 1, dy, w, slab, M, Cin, 9 * Cout, Cout, 9 * Cin, Cin, H=H, W=W, C=Cout, taps=9,
+             Cb=Cout, splits=s_eff, slab_stride=M * Cin, tile=tile)
+    xr = _nhwc_to_nchw(x.float()).requires_grad_(True)
+    F.conv2d(xr, _w_to_oihw(w.float().reshape(Cout, 3, 3, Cin)), padding=1).backward(_nhwc_to_nchw(dy.float()))
+    dref = xr.grad.permute(0, 2, 3, 1)
+    yb = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    scale = torch.rand(Cin, device=DEV) + 0.5
+    shift = torch.randn(Cin, device=DEV) * 0.1
+    dx = torch.empty(N, H, W, Cin, device=DEV, dtype=torch.bfloat16)
+    bacc = fn.bn_acc_buffer(Cin, DEV)
+    fn.slab_epi(slab, s_eff, M, Cin, dx, mode=2, gate=yb, scale=scale, shift=shift, acc=bacc)
+    mask = (yb.float() * scale + shift) > 0
+    dz = dref * mask
+    assert rel_err(dx, dz) < 1e-2
+    sb = bacc.sum(0).float()
+    assert torch.allclose(sb[0], dz.reshape(-1, Cin).sum(0), rtol=1e-2, atol=1e-1)
+    assert torch.allclose(sb[1], (dz * yb.float()).reshape(-1, Cin).sum(0), rtol=1e-2, atol=1e-1)
+    fn.slab_epi(slab, s_eff, M, Cin, dx, mode=3, gate=yb)
+    assert rel_err(dx, dref * (yb.float() > 0)) < 1e-2
