@@ -166,8 +166,57 @@ RK_DEV void bn_act_fwd_body(const CS& cs, const bf16* __restrict__ y, bf16* __re
   const long long stride = (long long)gridDim.x * blockDim.x;
   const bool hoist = stride % CC == 0;
   float sc[8], sh[8];
-  if (hoist) cs.load((int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) % CC), sc, sh);
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (hoist) {
+    cs.load((int)(idx % CC), sc, sh);
+    // U items per sweep with every load issued before any is consumed: a one-item grid-stride loop
+    // keeps one 16-B load per lane in flight and runs at ~half the HBM rate on these sizes
+    constexpr int U = POOL ? 2 : 4;
+    constexpr int NL = POOL ? 4 : 1;
+    const int cc = (int)(idx % CC);
+    for (; idx + (U - 1) * stride < total; idx += U * stride) {
+      uint4 v[U][NL];
+      long long pixs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long pix = (idx + u * stride) / CC;
+        pixs[u] = pix;
+        if constexpr (!POOL) {
+          v[u][0] = *(const uint4*)(y + pix * C + cc * 8);
+        } else {
+          const int wo = (int)(pix % Wo);
+          const long long t = pix / Wo;
+          const int ho = (int)(t % Ho);
+          const int n = (int)(t / Ho);
+          const long long base = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[u][q] = *(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float o[8];
+        if constexpr (!POOL) {
+          float f[8];
+          unpack8(v[u][0], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = act_f(f[e] * sc[e] + sh[e], ACT, slope);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = -INFINITY;
+#pragma unroll
+          for (int q = 0; q < NL; ++q) {
+            float f[8];
+            unpack8(v[u][q], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], act_f(f[e] * sc[e] + sh[e], ACT, slope));
+          }
+        }
+        *(uint4*)(out + pixs[u] * C + cc * 8) = pack8(o);
+      }
+    }
+  }
+  for (; idx < total; idx += stride) {
     const int cc = (int)(idx % CC);
     const long long pix = idx / CC;
     if (!hoist) cs.load(cc, sc, sh);
@@ -442,6 +491,11 @@ struct BwdCoefLds {
   }
 };
 
+template <int POOL, int ACT>
+RK_DEV void bn_bwd_apply_item(const uint4 gv, const uint4 (&yv)[POOL ? 4 : 1], long long base, const float (&sc)[8],
+                              const float (&sh)[8], const float (&k1)[8], const float (&k2)[8],
+                              const float (&k3)[8], bf16* __restrict__ dy, int W, int C, float slope);
+
 template <int POOL, int ACT, class CS>
 RK_DEV void bn_bwd_apply_body(const CS& cs, const bf16* __restrict__ dout, const bf16* __restrict__ y,
                               bf16* __restrict__ dy, int N, int H, int W, int C, float slope) {
@@ -451,13 +505,10 @@ RK_DEV void bn_bwd_apply_body(const CS& cs, const bf16* __restrict__ dout, const
   const long long stride = (long long)gridDim.x * blockDim.x;
   const bool hoist = stride % CC == 0;  // see bn_act_fwd_body
   float sc[8], sh[8], k1[8], k2[8], k3[8];
-  if (hoist) cs.load((int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) % CC), sc, sh, k1, k2, k3);
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
-    const int cc = (int)(idx % CC);
-    const long long pix = idx / CC;
-    const uint4 gv = *(const uint4*)(dout + pix * C + cc * 8);
+  constexpr int NL = POOL ? 4 : 1;
+  auto load_item = [&](long long pix, int cc, uint4& gv, uint4 (&yv)[NL]) -> long long {
+    gv = *(const uint4*)(dout + pix * C + cc * 8);
     long long base;
-    uint4 yv[POOL ? 4 : 1];
     if constexpr (!POOL) {
       base = pix * C + cc * 8;
       yv[0] = *(const uint4*)(y + base);
@@ -470,7 +521,38 @@ RK_DEV void bn_bwd_apply_body(const CS& cs, const bf16* __restrict__ dout, const
 #pragma unroll
       for (int q = 0; q < 4; ++q) yv[q] = *(const uint4*)(y + base + ((q >> 1) * W + (q & 1)) * (long long)C);
     }
+    return base;
+  };
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (hoist) {
+    cs.load((int)(idx % CC), sc, sh, k1, k2, k3);
+    // U items per sweep, all loads issued before any is consumed (see bn_act_fwd_body)
+    constexpr int U = POOL ? 2 : 4;
+    const int cc = (int)(idx % CC);
+    for (; idx + (U - 1) * stride < total; idx += U * stride) {
+      uint4 gv[U], yv[U][NL];
+      long long base[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) base[u] = load_item((idx + u * stride) / CC, cc, gv[u], yv[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) bn_bwd_apply_item<POOL, ACT>(gv[u], yv[u], base[u], sc, sh, k1, k2, k3, dy, W, C, slope);
+    }
+  }
+  for (; idx < total; idx += stride) {
+    const int cc = (int)(idx % CC);
+    const long long pix = idx / CC;
+    uint4 gv, yv[NL];
+    const long long base = load_item(pix, cc, gv, yv);
     if (!hoist) cs.load(cc, sc, sh, k1, k2, k3);
+    bn_bwd_apply_item<POOL, ACT>(gv, yv, base, sc, sh, k1, k2, k3, dy, W, C, slope);
+  }
+}
+
+template <int POOL, int ACT>
+RK_DEV void bn_bwd_apply_item(const uint4 gv, const uint4 (&yv)[POOL ? 4 : 1], long long base, const float (&sc)[8],
+                              const float (&sh)[8], const float (&k1)[8], const float (&k2)[8],
+                              const float (&k3)[8], bf16* __restrict__ dy, int W, int C, float slope) {
+  {
     float g[8];
     unpack8(gv, g);
     if constexpr (!POOL) {

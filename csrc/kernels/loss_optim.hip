@@ -201,20 +201,34 @@ __global__ __launch_bounds__(256) void reduce_slabs_epi_kernel(const float* __re
 // Minibatch gather inside the captured training graph: out_x[b] = data[idx[step][b]] (rows of
 // row_vec 16-B vectors), out_y[b] = labels[idx[step][b]], where step = *counter is read on the
 // device — the replayed graph walks a precomputed index schedule with no per-step host copies.
+// Step prologue of a scheduled training graph, one launch: gather minibatch rows sched[*counter],
+// zero the step's fp64 BatchNorm slot tables (`zero`, zero_n doubles) and, with `done`, advance the
+// device step counter once every block has read it (the last block to arrive bumps it) — replaces a
+// memset node and a separate counter-increment kernel (~4 us of dispatch each).
 __global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restrict__ data, long long row_vec,
                                                            const int* __restrict__ labels,
                                                            const long long* __restrict__ sched,
-                                                           const int* __restrict__ counter, int B,
-                                                           uint4* __restrict__ out, int* __restrict__ out_y) {
+                                                           int* __restrict__ counter, int B,
+                                                           uint4* __restrict__ out, int* __restrict__ out_y,
+                                                           double* __restrict__ zero, long long zero_n,
+                                                           int* __restrict__ done) {
   const long long step = *counter;
   const long long total = (long long)B * row_vec;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  const long long gstride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gstride) {
     const int b = (int)(i / row_vec);
     const long long c = i - (long long)b * row_vec;
     const long long src = sched[step * B + b];
     out[i] = data[src * row_vec + c];
     if (c == 0 && out_y) out_y[b] = labels[src];
+  }
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += gstride) zero[i] = 0.0;
+  if (done) {
+    __syncthreads();  // this block's reads of *counter are done (every thread used the value)
+    if (threadIdx.x == 0 && atomicAdd(done, 1) == (int)gridDim.x - 1) {
+      *done = 0;
+      atomicAdd(counter, 1);
+    }
   }
 }
 
@@ -430,42 +444,61 @@ __global__ __launch_bounds__(256) void slab_epi_kernel(const float* __restrict__
     sc = *(const f32x4*)(scale + 4 * c4);
     sh = *(const f32x4*)(shift + 4 * c4);
   }
-  for (int m = blockIdx.x * rpb + r0; m < M; m += gridDim.x * rpb) {
-    const long long i = (long long)m * N + 4 * c4;
-    f32x4 a = *(const f32x4*)(slab + i);
-    int s0 = 1;
-    for (; s0 + 3 < S; s0 += 4) {  // 4 independent slab loads in flight, fixed summation order
-      f32x4 v[4];
+  // rows of one sweep: U rows per thread with every slab (and gate) load issued before any add —
+  // the grid is capped (atomics), so each thread walks many rows and a one-row loop is latency-bound
+  constexpr int U = 4;
+  const int step = gridDim.x * rpb;
+  for (int m0 = blockIdx.x * rpb + r0; m0 < M; m0 += U * step) {
+    f32x4 av[U];
+    bf16x4 gv[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = *(const f32x4*)(slab + (s0 + k) * sn + i);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a += v[k];
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + u * step;
+      const long long i = (long long)(m < M ? m : m0) * N + 4 * c4;
+      av[u] = *(const f32x4*)(slab + i);
+      if (mode >= 2) gv[u] = *(const bf16x4*)(gate + i);
     }
-    for (; s0 < S; ++s0) a += *(const f32x4*)(slab + s0 * sn + i);
-    if (mode >= 2) {
-      const bf16x4 g = *(const bf16x4*)(gate + i);
+    for (int s1 = 1; s1 < S; ++s1) {  // fixed summation order per element
+      f32x4 v[U];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float yv = (float)g[e];
-        if (mode == 3) {
-          a[e] = yv > 0.f ? a[e] : 0.f;
-        } else {
-          a[e] = yv * sc[e] + sh[e] > 0.f ? a[e] : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int m = m0 + u * step;
+        v[u] = *(const f32x4*)(slab + s1 * sn + (long long)(m < M ? m : m0) * N + 4 * c4);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) av[u] += v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + u * step;
+      if (m >= M) break;
+      const long long i = (long long)m * N + 4 * c4;
+      f32x4 a = av[u];
+      if (mode >= 2) {
+        const bf16x4 g = gv[u];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float yv = (float)g[e];
+          if (mode == 3) {
+            a[e] = yv > 0.f ? a[e] : 0.f;
+          } else {
+            a[e] = yv * sc[e] + sh[e] > 0.f ? a[e] : 0.f;
+            s[e] += a[e];
+            q[e] += a[e] * yv;
+          }
+        }
+      } else if (mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
           s[e] += a[e];
-          q[e] += a[e] * yv;
+          q[e] += a[e] * a[e];
         }
       }
-    } else if (mode == 1) {
+      bf16x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s[e] += a[e];
-        q[e] += a[e] * a[e];
-      }
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)a[e];
+      *(bf16x4*)(out + i) = o;
     }
-    bf16x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (bf16)a[e];
-    *(bf16x4*)(out + i) = o;
   }
   if (mode == 1 || mode == 2) {
 #pragma unroll
@@ -499,11 +532,12 @@ extern "C" int rk_slab_epi(const float* slab, int S, int M, int N, int mode, con
 }
 
 extern "C" int rk_gather_batch(const void* data, long long row_bytes, const int* labels, const long long* sched,
-                               const int* counter, int B, void* out, int* out_y, void* stream) {
-  if (row_bytes % 16) return RK_EUNSUPPORTED;
+                               int* counter, int B, void* out, int* out_y, double* zero, long long zero_n, int* done,
+                               void* stream) {
+  if (row_bytes % 16 || zero_n < 0 || (zero_n && !zero)) return RK_EUNSUPPORTED;
   const long long rv = row_bytes / 16;
   hipLaunchKernelGGL(gather_batch_kernel, dim3(grid_for((long long)B * rv, 2048)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)data, rv, labels, sched, counter, B, (uint4*)out, out_y);
+                     (const uint4*)data, rv, labels, sched, counter, B, (uint4*)out, out_y, zero, zero_n, done);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

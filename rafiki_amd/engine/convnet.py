@@ -192,6 +192,7 @@ class ConvNetEngine:
     # 11% SLOWER (1.161 -> 1.289 ms; the concurrent GEMMs and split-K slab traffic interfere), so it
     # is off by default and kept as an option for layer shapes where it pays.
     overlap_wgrad = False
+    _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
 
     def _side_stream(self):
@@ -218,7 +219,7 @@ class ConvNetEngine:
         saved = []
         h = x
         accs = self._bn_accumulators() if self._use_bn_acc() else None
-        if accs is not None:
+        if accs is not None and not self._acc_zeroed_by_prologue:
             self._bn_acc_flat.zero_()  # one memset node for every layer's fp64 statistic slots
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             rm, rv = self.running_stats(bi)
@@ -446,10 +447,18 @@ class ConvNetEngine:
         self._static_x = torch.zeros(self.input_shape(batch_size), dtype=torch.bfloat16, device=self.device)
         self._static_y = torch.zeros((batch_size,), dtype=torch.int32, device=self.device)
 
+        self._done = torch.zeros(1, dtype=torch.int32, device=self.device)
+        accs = self._bn_accumulators() if self._use_bn_acc() else None
+
         def body():
-            F.gather_batch(self._data, self._labels, self._sched, self._ctr, self._static_x, self._static_y)
-            self._train_step_gpu(self._static_x, self._static_y)
-            F.add_int_(self._ctr, 1)
+            # one prologue launch: gather + zero the BN slot tables + advance the step counter
+            F.gather_batch(self._data, self._labels, self._sched, self._ctr, self._static_x, self._static_y,
+                           zero=self._bn_acc_flat if accs is not None else None, done=self._done)
+            self._acc_zeroed_by_prologue = accs is not None
+            try:
+                self._train_step_gpu(self._static_x, self._static_y)
+            finally:
+                self._acc_zeroed_by_prologue = False
 
         snap = [self.flat.master.clone(), self.running.clone()]
         opt_state = [t.clone() for t in self._opt_tensors()]

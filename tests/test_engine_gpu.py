@@ -58,6 +58,25 @@ def test_graph_replay_matches_eager():
     assert torch.allclose(e1.running, e2.running)
 
 
+def test_scheduled_graph_matches_eager_and_advances_counter():
+    """capture_scheduled: one prologue kernel gathers rows sched[ctr], zeroes the BN slot tables and
+    bumps the device counter; replays must track an eager loop over the same rows."""
+    e1, e2 = _engine(), _engine()
+    data, labels = _batch(96, seed=7)
+    steps, B = 4, 32
+    idx = torch.randint(0, 96, (steps, B), device='cuda', generator=torch.Generator('cuda').manual_seed(1))
+    e2.capture_scheduled(data, labels, steps, B)
+    e2.set_schedule(idx)
+    for i in range(steps):
+        e1.train_step(data[idx[i]].contiguous(), labels[idx[i]].contiguous())
+        e2.replay()
+    torch.cuda.synchronize()
+    assert int(e2._ctr.item()) == steps and int(e2._done.item()) == 0
+    assert torch.allclose(e1.flat.master, e2.flat.master, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(e1.running, e2.running, rtol=1e-4, atol=1e-6)
+    assert abs(e1.loss_sum.item() - e2.loss_sum.item()) < 1e-3 * max(1.0, abs(e1.loss_sum.item()))
+
+
 def test_training_reduces_loss_and_eval():
     eng = _engine(lr=0.05)
     x, y = _batch(128, seed=5)

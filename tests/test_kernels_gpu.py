@@ -255,7 +255,7 @@ def test_bn_atomic_accumulator_path(fn, N, H, Cin, Cout, pool):
     o1 = fn.bn_act_fwd(y1, c1[2], c1[3], pool=pool)
     acc = fn.bn_acc_buffer(Cout, DEV)
     y2, _ = fn.conv_fwd(x, w, stats_acc=acc)
-    assert torch.equal(y1, y2)
+    assert rel_err(y2, y1) < 1e-2  # the two stats modes may tune to different (split-K) configs
     rm2, rv2 = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
     o2, c2 = fn.bn_act_fwd_acc(y2, acc, N * H * H, gamma, beta, 1e-5, rm2, rv2, 0.1, pool=pool)
     assert torch.allclose(c1, c2, rtol=1e-4, atol=1e-5)
