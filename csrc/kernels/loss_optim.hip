@@ -61,15 +61,19 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   }
 }
 
+// One launch over the whole arena: weight decay applies to elements [0, decay_end) (the arena puts
+// decayed parameters first).  bump: a device step counter advanced once (the last kernel of a
+// scheduled training step owns it, so no separate increment launch is needed).
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, bf16* __restrict__ wb,
                                                   const float* __restrict__ g, float* __restrict__ mom, long long n,
                                                   float lr, float momentum, float wd, int nesterov, float gscale,
-                                                  const float* lr_ptr) {
+                                                  const float* lr_ptr, long long decay_end, int* bump) {
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(bump, 1);
   const float lrv = lr_ptr ? lr_ptr[0] * lr : lr;
   const long long n4 = n >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     f32x4 wv = ((const f32x4*)w)[i];
-    f32x4 gv = ((const f32x4*)g)[i] * gscale + wd * wv;
+    f32x4 gv = ((const f32x4*)g)[i] * gscale + (4 * i < decay_end ? wd : 0.f) * wv;
     f32x4 d = gv;
     if (mom) {
       f32x4 m = ((const f32x4*)mom)[i] * momentum + gv;
@@ -372,10 +376,11 @@ extern "C" int rk_softmax_xent(const float* logits, int ldl, const int* labels, 
 }
 
 extern "C" int rk_sgd_step(float* w, void* wb, const float* g, float* mom, long long n, float lr, float momentum,
-                           float wd, int nesterov, float gscale, const float* lr_ptr, void* stream) {
-  if (n % 4) return RK_EUNSUPPORTED;
+                           float wd, int nesterov, float gscale, const float* lr_ptr, long long decay_end, int* bump,
+                           void* stream) {
+  if (n % 4 || decay_end % 4) return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4, 4096)), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wb, g, mom,
-                     n, lr, momentum, wd, nesterov, gscale, lr_ptr);
+                     n, lr, momentum, wd, nesterov, gscale, lr_ptr, decay_end, bump);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -446,7 +451,7 @@ __global__ __launch_bounds__(256) void slab_epi_kernel(const float* __restrict__
   }
   // rows of one sweep: U rows per thread with every slab (and gate) load issued before any add —
   // the grid is capped (atomics), so each thread walks many rows and a one-row loop is latency-bound
-  constexpr int U = 4;
+  constexpr int U = 8;
   const int step = gridDim.x * rpb;
   for (int m0 = blockIdx.x * rpb + r0; m0 < M; m0 += U * step) {
     f32x4 av[U];
@@ -524,7 +529,11 @@ extern "C" int rk_slab_epi(const float* slab, int S, int M, int N, int mode, con
   if (mode >= 2 && !gate) return RK_EBADARG;
   if (mode == 2 && (!scale || !shift)) return RK_EBADARG;
   const int rpb = 256 / (N / 4);
-  const int blocks = min((M + rpb - 1) / rpb, 256);
+  // with statistics every block adds 2N fp64 values into at most 8 slots: same-address atomics from
+  // many blocks serialise at the memory side (measured 17 us at 256 blocks for a 4 MB output), so
+  // the statistics modes run fewer, wider blocks
+  const int cap = (mode == 1 || mode == 2) ? 64 : 256;
+  const int blocks = min((M + rpb - 1) / rpb, cap);
   hipLaunchKernelGGL(slab_epi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab, S, M, N, mode,
                      (const bf16*)gate, scale, shift, acc, slmask, (bf16*)out);
   RK_LAUNCH_CHECK();

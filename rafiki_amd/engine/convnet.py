@@ -450,15 +450,24 @@ class ConvNetEngine:
         self._done = torch.zeros(1, dtype=torch.int32, device=self.device)
         accs = self._bn_accumulators() if self._use_bn_acc() else None
 
+        # the step counter advances inside the step's last kernel (SGD) or, for other optimizers, in
+        # the prologue once every gather block has read it
+        opt_bumps = isinstance(self.opt, FlatSGD)
+
         def body():
-            # one prologue launch: gather + zero the BN slot tables + advance the step counter
+            # one prologue launch: gather + zero the BN slot tables (+ counter)
             F.gather_batch(self._data, self._labels, self._sched, self._ctr, self._static_x, self._static_y,
-                           zero=self._bn_acc_flat if accs is not None else None, done=self._done)
+                           zero=self._bn_acc_flat if accs is not None else None,
+                           done=None if opt_bumps else self._done)
             self._acc_zeroed_by_prologue = accs is not None
+            if opt_bumps:
+                self.opt.bump = self._ctr
             try:
                 self._train_step_gpu(self._static_x, self._static_y)
             finally:
                 self._acc_zeroed_by_prologue = False
+                if opt_bumps:
+                    self.opt.bump = None
 
         snap = [self.flat.master.clone(), self.running.clone()]
         opt_state = [t.clone() for t in self._opt_tensors()]

@@ -167,16 +167,15 @@ class FlatSGD:
         self.mom = torch.zeros_like(flat.master) if momentum > 0 else None
         # device-side LR multiplier: schedules change it without re-capturing the graph
         self.lr_scale = torch.ones(1, dtype=torch.float32, device=flat.device)
+        self.bump: Optional[torch.Tensor] = None  # int32 device counter the step kernel advances
 
     def step(self):
         f = self.flat
         if f.device.type == 'cuda':
-            ranges = [(0, f.decay_end, self.wd), (f.decay_end, f.total, 0.0)]
-            for a, b, wd in ranges:
-                if b > a:
-                    F.sgd_step(f.master[a:b], f.grad[a:b], None if self.mom is None else self.mom[a:b],
-                               wb=f.bf16[a:b], lr=self.lr, momentum=self.momentum, weight_decay=wd,
-                               nesterov=self.nesterov, lr_tensor=self.lr_scale)
+            # one launch: decayed parameters come first in the arena, wd applies below decay_end
+            F.sgd_step(f.master, f.grad, self.mom, wb=f.bf16, lr=self.lr, momentum=self.momentum,
+                       weight_decay=self.wd, nesterov=self.nesterov, lr_tensor=self.lr_scale,
+                       decay_end=f.decay_end, bump=self.bump)
             return
         # CPU reference path (same math as sgd_kernel)
         lr = self.lr * float(self.lr_scale.item())

@@ -621,9 +621,13 @@ def softmax_xent(logits, labels, ncls, *, dlogits=None, probs=None, loss_sum=Non
 
 
 def sgd_step(w, g, mom=None, *, wb=None, lr, momentum=0.0, weight_decay=0.0, nesterov=False, grad_scale=1.0,
-             lr_tensor=None):
-    _lib.call("rk_sgd_step", _p(w), _p(wb), _p(g), _p(mom), w.numel(), float(lr), float(momentum),
-              float(weight_decay), int(nesterov), float(grad_scale), _p(lr_tensor), _s())
+             lr_tensor=None, decay_end=None, bump=None):
+    """Fused SGD over a flat range; ``weight_decay`` applies to elements [0, decay_end) (default: all).
+    ``bump``: int32 device counter incremented once by the launch (graph-step counters)."""
+    n = w.numel()
+    _lib.call("rk_sgd_step", _p(w), _p(wb), _p(g), _p(mom), n, float(lr), float(momentum),
+              float(weight_decay), int(nesterov), float(grad_scale), _p(lr_tensor), n if decay_end is None else
+              int(decay_end), _p(bump), _s())
 
 
 def adam_step(w, g, m, v, *, wb=None, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, decoupled=False,
