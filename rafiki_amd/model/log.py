@@ -63,7 +63,8 @@ class ModelLogger:
         def __enter__(self):
             self.cuda = _cuda_in_use()
             if self.cuda is not None:
-                self.cuda.synchronize()
+                # allocator accounting is host-side: no synchronize (one would be refused while another
+                # thread of the process — in-process worker, predictor — captures a hipGraph)
                 self.cuda.reset_peak_memory_stats()
             self.t0 = time.perf_counter()
             return self
@@ -71,8 +72,7 @@ class ModelLogger:
         def __exit__(self, *exc):
             extra = {}
             if self.cuda is not None:
-                # GPU telemetry: queued work is part of the phase, HBM peak of it
-                self.cuda.synchronize()
+                # GPU telemetry: HBM peak of the phase
                 extra = {'hbm_peak_bytes': int(self.cuda.max_memory_allocated()),
                          'hbm_reserved_bytes': int(self.cuda.memory_reserved())}
             self.lg.log_phase(self.phase, time.perf_counter() - self.t0, **extra)
