@@ -1283,11 +1283,13 @@ RK_DEV int wtr_off(int k, int ch) {
 
 // 16 (M or N) x 32 (K) MFMA operand from a K-outer [rows = K][64 cols] image (wtr_off): K rows
 // kb0..kb0+7 of lane group g start at image row rowbase (consecutive), columns c0..c0+15.
-RK_DEV bf16x8 wtr_frag(const char* lds, int rowbase, int c0, int lane) {
+// hrow: patch-row distance of K rows 4..7 from rows 0..3 (4 = consecutive; W + 2 for 4-wide images,
+// whose 8 consecutive pixels span two patch rows).
+RK_DEV bf16x8 wtr_frag(const char* lds, int rowbase, int c0, int lane, int hrow = 4) {
   const int ii = lane & 15, q = ii >> 2, pp = ii & 3;
   const int ch = (c0 >> 3) + (pp >> 1);
   const int a0 = wtr_off(rowbase + q, ch) + 8 * (pp & 1);
-  const int a1 = wtr_off(rowbase + q + 4, ch) + 8 * (pp & 1);
+  const int a1 = wtr_off(rowbase + q + hrow, ch) + 8 * (pp & 1);
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + a0));
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + a1));
   const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
@@ -1297,14 +1299,17 @@ RK_DEV bf16x8 wtr_frag(const char* lds, int rowbase, int c0, int lane) {
   return f;
 }
 
+// W = 4: an item is 8 whole 4x4 images, their halo patches stacked (as hconv_kernel's IH > 0).
 template <int W>
 __global__ __launch_bounds__(256, 1) void hconv_wgrad_kernel(const IgemmParams p, const int S, const int per_block) {
   constexpr int P = W == 8 ? 64 : 128;         // pixels per item
-  constexpr int TH = P / W, PC = W + 2, NPP = (TH + 2) * PC;
+  constexpr int IH = W == 4 ? 4 : 0;           // whole-image items of IH rows
+  constexpr int TH = IH ? IH : P / W, PC = W + 2, PIMG = (TH + 2) * PC, NPP = (IH ? P / ((IH ? IH : 1) * W) : 1) * PIMG;
+  constexpr int HI = W == 4 ? PC : 4;          // patch-row distance of a lane group's pixels 4..7
   constexpr int LP = (NPP * 8 + 255) / 256;    // patch DMA instructions per wave
   constexpr int LY = P / 32;                   // dy-tile DMA instructions per wave
   constexpr int P_BYTES = LP * 4 * 1024, Y_BYTES = P * 128, SB = P_BYTES + Y_BYTES;
-  constexpr int LOG2W = W == 8 ? 3 : W == 16 ? 4 : 5;
+  constexpr int LOG2W = W == 4 ? 2 : W == 8 ? 3 : W == 16 ? 4 : 5;
   constexpr int KB = P / 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * SB];
 
@@ -1330,9 +1335,10 @@ __global__ __launch_bounds__(256, 1) void hconv_wgrad_kernel(const IgemmParams p
     const int slot = (wid * LP + q) * 64 + lane;
     const int pp = slot >> 3;
     const int c = (slot & 7) ^ ((((pp >> 1) & 1) | (((pp >> 3) & 1) << 1)) << 1);
-    const int pr = pp / PC, pcol = pp - pr * PC;
-    const bool ok = pp < NPP && pcol >= 1 && pcol <= W;
-    prel[q] = ((((pr - 1) * W + (pcol - 1)) << log2C) << 1) + c * 16;
+    const int img = pp / PIMG, rem = pp - img * PIMG;
+    const int pr = rem / PC, pcol = rem - pr * PC;
+    const bool ok = pp < NPP && pcol >= 1 && pcol <= W && (IH == 0 || (pr >= 1 && pr <= TH));
+    prel[q] = ((((img * TH + pr - 1) * W + (pcol - 1)) << log2C) << 1) + c * 16;
     prow[q] = ok ? pr : -1000;
   }
   unsigned yoff[LY];
@@ -1348,11 +1354,12 @@ __global__ __launch_bounds__(256, 1) void hconv_wgrad_kernel(const IgemmParams p
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     const int k = kb * 32 + 8 * (lane >> 4);
-    prb[kb] = ((k >> LOG2W) + 1) * PC + (k & (W - 1)) + 1;
+    const int img = k / (TH * W), rem = k - img * (TH * W);
+    prb[kb] = img * PIMG + ((rem >> LOG2W) + 1) * PC + (rem & (W - 1)) + 1;
   }
 
   auto issue = [&](int it, int buf) {
-    const int r0 = (it & (tilesPerImg - 1)) * TH;  // tilesPerImg is a power of two
+    const int r0 = IH ? 0 : (it & (tilesPerImg - 1)) * TH;  // tilesPerImg is a power of two
     const int pbase = (((it * P) << log2C) << 1) + ci0 * 2;
     char* dst = smem + buf * SB;
 #pragma unroll
@@ -1379,17 +1386,24 @@ __global__ __launch_bounds__(256, 1) void hconv_wgrad_kernel(const IgemmParams p
     if (it + 1 < item1) issue(it + 1, buf ^ 1);
     const char* pt = smem + buf * SB;
     const char* yt = pt + P_BYTES;
+    // one wave per SIMD: nothing else hides LDS latency, so the 13 fragments of K-block kb+1 are
+    // read while the 36 MFMAs of kb run (register double buffer) instead of one tap at a time
+    bf16x8 af[2][4], bt[2][9];
+    auto load_frags = [&](int kb, bf16x8 (&a)[4], bf16x8 (&b)[9]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = wtr_frag(yt, kb * 32 + 8 * (lane >> 4), 16 * i, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) b[t] = wtr_frag(pt, prb[kb] + tap_dy(t) * PC + tap_dx(t), 16 * wid, lane, HI);
+    };
+    load_frags(0, af[0], bt[0]);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-      bf16x8 af[4];
+      if (kb + 1 < KB) load_frags(kb + 1, af[(kb + 1) & 1], bt[(kb + 1) & 1]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = wtr_frag(yt, kb * 32 + 8 * (lane >> 4), 16 * i, lane);
+      for (int t = 0; t < 9; ++t)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const bf16x8 bt = wtr_frag(pt, prb[kb] + tap_dy(t) * PC + tap_dx(t), 16 * wid, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bt, af[i], acc[i][t], 0, 0, 0);
-      }
+        for (int i = 0; i < 4; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bt[kb & 1][t], af[kb & 1][i], acc[i][t], 0, 0, 0);
     }
   }
   // partial tile -> slab sl: lane owns dW[co0 + 16i + (lane&15)][t][ci0 + 16 wid + 4(lane>>4) .. +3]
@@ -1504,9 +1518,13 @@ extern "C" int rk_hconv(int dgrad, int tile, const void* A, const void* B, void*
 extern "C" int rk_hconv_wgrad(const void* dy, const void* x, float* slab, int Nb, int H, int W, int Cin, int Cout,
                               int S, long long bytesY, long long bytesX, void* stream) {
   if (bytesY <= 0 || bytesX <= 0 || bytesY >= (1ll << 31) || bytesX >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (W != 8 && W != 16 && W != 32) return RK_EUNSUPPORTED;
+  if (W != 4 && W != 8 && W != 16 && W != 32) return RK_EUNSUPPORTED;
   const int P = W == 8 ? 64 : 128;
-  if (rk_log2(H) < 0 || (H * W) % P != 0 || Nb <= 0) return RK_EUNSUPPORTED;
+  if (W == 4) {  // whole-image items: 8 images of 4x4
+    if (H != 4 || Nb <= 0 || (Nb * 16) % P != 0) return RK_EUNSUPPORTED;
+  } else if (rk_log2(H) < 0 || (H * W) % P != 0 || Nb <= 0) {
+    return RK_EUNSUPPORTED;
+  }
   if (rk_log2(Cin) < 6 || Cout % 64 != 0 || S <= 0) return RK_EUNSUPPORTED;
   IgemmParams p{};
   p.A = (const bf16*)dy; p.B = (const bf16*)x; p.out = slab;
@@ -1522,6 +1540,7 @@ extern "C" int rk_hconv_wgrad(const void* dy, const void* x, float* slab, int Nb
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(tiles * S);
   switch (W) {
+    case 4: hipLaunchKernelGGL((hconv_wgrad_kernel<4>), grid, dim3(256), 0, st, p, S, per); break;
     case 8: hipLaunchKernelGGL((hconv_wgrad_kernel<8>), grid, dim3(256), 0, st, p, S, per); break;
     case 16: hipLaunchKernelGGL((hconv_wgrad_kernel<16>), grid, dim3(256), 0, st, p, S, per); break;
     default: hipLaunchKernelGGL((hconv_wgrad_kernel<32>), grid, dim3(256), 0, st, p, S, per); break;

@@ -392,11 +392,11 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
 
 
 def _hconv_wgrad_candidates(Nb, H, W, Cin, Cout, taps):
-    if not HCONV or taps != 9 or W not in (8, 16, 32) or H & (H - 1) or Cin < 64 or Cin & (Cin - 1) or Cout % 64:
+    if not HCONV or taps != 9 or W not in (4, 8, 16, 32) or H & (H - 1) or Cin < 64 or Cin & (Cin - 1) or Cout % 64:
         return []
     P = 64 if W == 8 else 128
-    if (H * W) % P:
-        return []
+    if (W == 4 and (H != 4 or (Nb * 16) % P)) or (W != 4 and (H * W) % P):
+        return []  # W = 4: items of 8 whole 4x4 images
     items = Nb * H * W // P
     tiles = (Cout // 64) * (Cin // 64)
     out = []

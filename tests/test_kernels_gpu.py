@@ -223,7 +223,8 @@ def test_hconv_fwd_dgrad(fn, N, H, W, Cin, Cout, bn_bit, grid):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,S", [(2, 32, 32, 64, 64, 3), (2, 16, 16, 128, 128, 4), (4, 8, 8, 256, 64, 5),
-                                              (1, 16, 16, 64, 128, 1), (3, 32, 32, 64, 128, 64)])
+                                              (1, 16, 16, 64, 128, 1), (3, 32, 32, 64, 128, 64),
+                                              (16, 4, 4, 256, 128, 2), (8, 4, 4, 64, 64, 3)])
 def test_hconv_wgrad(fn, N, H, W, Cin, Cout, S):
     """Halo-tiled weight gradient (slabs + reduce) vs PyTorch fp32 (incl. more slabs than items)."""
     torch.manual_seed(12)
