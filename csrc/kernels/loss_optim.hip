@@ -540,6 +540,64 @@ extern "C" int rk_slab_epi(const float* slab, int S, int M, int N, int mode, con
   return RK_OK;
 }
 
+// ---- flipped, transposed conv weights for the data gradient ------------------------------------
+// wt[ci][8 - t][co] = w[co][t][ci] for every listed 3x3 layer in ONE launch: the data gradient is then
+// a FORWARD conv of dy with wt, so it runs on the forward kernels, whose weight operand is K-inner
+// (one ds_read_b128 per MFMA fragment; the K-outer dgrad operand needs two transposing reads) and
+// whose tuned tiles are the faster ones.  A block moves one 64 co x 64 ci tile of one tap through LDS
+// (coalesced 128-B rows both ways).  desc[b] = {layer, tap, co0, ci0}; meta[l] = {src, dst, Cout, Cin}
+// (element offsets into the two bf16 arenas).
+__global__ __launch_bounds__(256) void conv_wt_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                      const int* __restrict__ desc, const long long* __restrict__ meta) {
+  __shared__ bf16 tile[64][64 + 8];
+  const int4 d = ((const int4*)desc)[blockIdx.x];
+  const int layer = d.x, tap = d.y, co0 = d.z, ci0 = d.w;
+  const long long so = meta[4 * layer], dso = meta[4 * layer + 1];
+  const int Cout = (int)meta[4 * layer + 2], Cin = (int)meta[4 * layer + 3];
+  const int tid = threadIdx.x;
+  // load: row r = co (64 rows), 64 ci per row as 8 x 16-B vectors
+  for (int v = tid; v < 64 * 8; v += 256) {
+    const int r = v >> 3, c8 = (v & 7) * 8;
+    const int co = co0 + r, ci = ci0 + c8;
+    if (co < Cout && ci < Cin) {
+      const bf16* s = src + so + ((long long)co * 9 + tap) * Cin + ci;
+      if (ci + 8 <= Cin) {
+        const bf16x8 x = *(const bf16x8*)s;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tile[r][c8 + e] = x[e];
+      } else {
+        for (int e = 0; e < Cin - ci; ++e) tile[r][c8 + e] = s[e];
+      }
+    }
+  }
+  __syncthreads();
+  // store: row = ci, 64 co contiguous
+  for (int v = tid; v < 64 * 8; v += 256) {
+    const int r = v >> 3, c8 = (v & 7) * 8;
+    const int ci = ci0 + r, co = co0 + c8;
+    if (ci < Cin && co < Cout) {
+      bf16* t = dst + dso + ((long long)ci * 9 + (8 - tap)) * Cout + co;
+      if (co + 8 <= Cout) {
+        bf16x8 x;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = tile[c8 + e][r];
+        *(bf16x8*)t = x;
+      } else {
+        for (int e = 0; e < Cout - co; ++e) t[e] = tile[c8 + e][r];
+      }
+    }
+  }
+}
+
+extern "C" int rk_conv_wt(const void* src, void* dst, const int* desc, int nblocks, const long long* meta,
+                          void* stream) {
+  if (nblocks <= 0) return RK_EBADARG;
+  hipLaunchKernelGGL(conv_wt_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst,
+                     desc, meta);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
 extern "C" int rk_gather_batch(const void* data, long long row_bytes, const int* labels, const long long* sched,
                                int* counter, int B, void* out, int* out_y, double* zero, long long zero_n, int* done,
                                void* stream) {

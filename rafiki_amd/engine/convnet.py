@@ -194,6 +194,9 @@ class ConvNetEngine:
     overlap_wgrad = False
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
+    # data gradients as forward convs of dy with flipped/transposed weights (F.ConvWT, one transpose
+    # launch per step): the forward kernels' K-inner weight operand and tiles are the faster ones
+    dgrad_wt = os.environ.get('RAFIKI_DGRAD_WT', '1') != '0'
 
     def _side_stream(self):
         st = getattr(self, '_wgrad_stream', None)
@@ -281,6 +284,9 @@ class ConvNetEngine:
         main = torch.cuda.current_stream(self.device)
         side = self._side_stream()
         reduced = False
+        wt = self._conv_wt() if self.dgrad_wt else None
+        if wt is not None:
+            wt.refresh()  # one launch: flipped/transposed bf16 weights of every dgrad layer
         for bi in range(len(self.blocks) - 1, -1, -1):
             name, cin, cout, pool, hw = self.blocks[bi]
             y, coeffs = saved[bi]
@@ -303,12 +309,27 @@ class ConvNetEngine:
                 # dgrad epilogue (FLAG_BNB), so its bn_bwd_acc is a single apply pass
                 py, pco = saved[bi - 1]
                 reduced = accs is not None and self.fuse_bn_dgrad and not self.blocks[bi - 1][3]
-                if reduced:
+                if wt is not None:
+                    if reduced:
+                        d = F.conv_dgrad_t(dy, wt.view(bi - 1), bn_y=py, bn_coeffs=pco, bn_acc=accs[bi - 1][1])
+                    else:
+                        d = F.conv_dgrad_t(dy, wt.view(bi - 1))
+                elif reduced:
                     d = F.conv_dgrad(dy, fl.wb(name + '.w'), bn_y=py, bn_coeffs=pco, bn_acc=accs[bi - 1][1])
                 else:
                     d = F.conv_dgrad(dy, fl.wb(name + '.w'))
         if self.overlap_wgrad:
             main.wait_stream(side)
+
+    def _conv_wt(self):
+        """ConvWT over the weights of blocks 1.. (block 0 has no data gradient), built once."""
+        wt = getattr(self, '_wt', None)
+        if wt is None and len(self.blocks) > 1:
+            fl = self.flat
+            ws = [fl.wb(b[0] + '.w') for b in self.blocks[1:]]
+            if all(w.shape[0] % 8 == 0 and (w.numel() // (9 * w.shape[0])) % 8 == 0 for w in ws):
+                wt = self._wt = F.ConvWT(fl.bf16, ws)
+        return wt
 
     def _use_bn_acc(self) -> bool:
         return F.BN_ATOMIC and all(b[2] <= 1024 and b[2] % 8 == 0 for b in self.blocks)

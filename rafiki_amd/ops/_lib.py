@@ -40,6 +40,7 @@ _SIGS = {
     "rk_gather_batch": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i64, vp, vp],
     "rk_reduce_slabs_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, vp, i32, vp],
     "rk_slab_epi": [vp, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp],
+    "rk_conv_wt": [vp, vp, vp, i32, vp, vp],
     "rk_bn_finalize_bwd": [vp, i32, i32, f64, vp, vp, vp, vp, vp, vp, i32, vp],
     "rk_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "rk_softmax_xent": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],

@@ -359,6 +359,83 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, *, taps: int = 9, out=None, ga
     return out
 
 
+class ConvWT:
+    """Flipped, transposed bf16 copies wt[ci][8-t][co] = w[co][t][ci] of several 3x3 conv weights that
+    live in one bf16 arena, refreshed by ONE rk_conv_wt launch per training step.  With them the data
+    gradient is a forward conv of dy (``conv_dgrad_t``) on the forward kernels."""
+
+    def __init__(self, arena: torch.Tensor, weights):
+        """arena: contiguous bf16 tensor; weights: list of bf16 views into it, shaped [Cout, 9*Cin]
+        (or [Cout, 3, 3, Cin])."""
+        self.arena = arena
+        meta, desc, self._views, off = [], [], [], 0
+        for l, w in enumerate(weights):
+            Cout = w.shape[0]
+            Cin = w.numel() // (9 * Cout)
+            so = (w.data_ptr() - arena.data_ptr()) // 2
+            assert so % 8 == 0 and Cin % 8 == 0 and Cout % 8 == 0, (so, Cin, Cout)
+            meta.append([so, off, Cout, Cin])
+            for t in range(9):
+                for co0 in range(0, Cout, 64):
+                    for ci0 in range(0, Cin, 64):
+                        desc.append([l, t, co0, ci0])
+            self._views.append((off, Cin, Cout))
+            off += (Cin * 9 * Cout + 63) // 64 * 64
+        dev = arena.device
+        self.buf = torch.zeros(max(off, 64), dtype=torch.bfloat16, device=dev)
+        self.meta = torch.tensor(meta, dtype=torch.int64, device=dev)
+        self.desc = torch.tensor(desc, dtype=torch.int32, device=dev)
+
+    def refresh(self):
+        _lib.call("rk_conv_wt", _p(self.arena), _p(self.buf), _p(self.desc), self.desc.shape[0], _p(self.meta), _s())
+
+    def view(self, l: int) -> torch.Tensor:
+        off, Cin, Cout = self._views[l]
+        return self.buf[off:off + Cin * 9 * Cout].view(Cin, 9 * Cout)
+
+
+def conv_dgrad_t(dy: torch.Tensor, wt: torch.Tensor, *, out=None, gate=None, bn_y=None, bn_coeffs=None,
+                 bn_acc=None):
+    """dx = dgrad(dy, w) computed as conv3x3(dy, wt) with wt = ConvWT.view(...) [Cin][9*Cout]: the forward
+    kernels (halo-tiled / implicit GEMM / split-K) with the data-gradient epilogues of conv_dgrad
+    (ReLU gate, or FLAG_BNB: the input layer's BN+ReLU mask and BN-backward sums)."""
+    Nb, H, W, Cout = dy.shape
+    Cin = wt.shape[0]
+    M, K = Nb * H * W, 9 * Cout
+    assert wt.numel() == Cin * K
+    if out is None:
+        out = torch.empty((Nb, H, W, Cin), device=dy.device, dtype=torch.bfloat16)
+    flags, bias, stats = (FLAG_GATE if gate is not None else 0), None, None
+    if bn_y is not None:
+        assert bn_y.shape == out.shape and bn_acc.dtype == torch.float64 and bn_acc.shape[-1] == Cin
+        gate, bias, stats = bn_y, bn_coeffs[2], bn_acc
+        flags = FLAG_BNB | FLAG_SATOM | ((bn_acc.shape[0] - 1) << 12)
+
+    def run(cfg):
+        if cfg[0] == 'h':
+            hconv(0, dy, wt, out, M, Cin, K, K, H, W, Cout, gate=gate, bias=bias, stats=stats, flags=flags,
+                  bn_bit=cfg[1], grid=cfg[2])
+        elif cfg[0] == 'k':
+            slab = torch.empty((cfg[2], M, Cin), device=dy.device, dtype=torch.float32)
+            igemm(KIND_CONV_FWD, 1, dy, wt, slab, M, Cin, K, Cout, K, Cin, H=H, W=W, C=Cout, taps=9,
+                  splits=cfg[2], slab_stride=M * Cin, tile=cfg[1])
+            if bn_y is not None:
+                slab_epi(slab, cfg[2], M, Cin, out, mode=2, gate=bn_y, scale=bn_coeffs[2], shift=bn_coeffs[3],
+                         acc=bn_acc)
+            else:
+                slab_epi(slab, cfg[2], M, Cin, out, mode=3 if gate is not None else 0, gate=gate)
+        else:
+            igemm(KIND_CONV_FWD, 0, dy, wt, out, M, Cin, K, Cout, K, Cin, gate=gate, bias=bias, stats=stats, H=H,
+                  W=W, C=Cout, taps=9, flags=flags, tile=cfg[0])
+    cfg = _tuned(('cdT', M, Cin, K, H, W, Cout, bn_y is not None),
+                 _tile_candidates(M, Cin) + _hconv_candidates(M, Cin, H, W, Cout, 9)
+                 + _conv_split_candidates(M, Cin, K, H, W, Cout), run)
+    if bn_acc is not None and autotune.can_tune():
+        bn_acc.zero_()  # tuning runs accumulated into it
+    run(cfg)
+    return out
+
+
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, accumulate=False, splits=None):
     """dW[co][tap][ci] (fp32) = sum over pixels of dy[p][co] * x[shift_tap(p)][ci]."""
     Nb, H, W, Cout = dy.shape

@@ -392,3 +392,40 @@ def test_conv_split_k_slab_epilogue(fn, tile, S, N, H, W, Cin, Cout):
     assert torch.allclose(sb[1], (dz * yb.float()).reshape(-1, Cin).sum(0), rtol=1e-2, atol=1e-1)
     fn.slab_epi(slab, s_eff, M, Cin, dx, mode=3, gate=yb)
     assert rel_err(dx, dref * (yb.float() > 0)) < 1e-2
+
+
+def test_conv_wt_transposed_dgrad(fn):
+    """ConvWT (one launch for several layers) + conv_dgrad_t (forward kernels on the flipped/transposed
+    weights) vs the PyTorch fp32 data gradient, plain, with a ReLU gate and with the BNB epilogue."""
+    torch.manual_seed(16)
+    shapes = [(16, 4, 4, 512, 512), (8, 8, 8, 128, 256), (2, 32, 32, 64, 64), (3, 16, 16, 64, 128), (2, 6, 6, 64, 64)]
+    ws = [(torch.randn(co, 9 * ci, device=DEV) / (3 * ci ** 0.5)).bfloat16() for (_, _, _, ci, co) in shapes]
+    arena = torch.zeros(sum((w.numel() + 63) // 64 * 64 for w in ws) + 64, device=DEV, dtype=torch.bfloat16)
+    views, off = [], 0
+    for w in ws:
+        v = arena[off:off + w.numel()].view_as(w)
+        v.copy_(w)
+        views.append(v)
+        off += (w.numel() + 63) // 64 * 64
+    wt = fn.ConvWT(arena, views)
+    wt.refresh()
+    for l, (N, H, W, Cin, Cout) in enumerate(shapes):
+        w4 = ws[l].float().reshape(Cout, 3, 3, Cin)
+        ref_t = w4.flip(1).flip(2).permute(3, 1, 2, 0).reshape(Cin, 9 * Cout)
+        assert torch.equal(wt.view(l).float(), ref_t)
+        dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+        xr = torch.zeros(N, Cin, H, W, device=DEV, requires_grad=True)
+        F.conv2d(xr, _w_to_oihw(w4), padding=1).backward(_nhwc_to_nchw(dy.float()))
+        dref = xr.grad.permute(0, 2, 3, 1)
+        assert rel_err(fn.conv_dgrad_t(dy, wt.view(l)), dref) < 1e-2
+        gate = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+        assert rel_err(fn.conv_dgrad_t(dy, wt.view(l), gate=gate), dref * (gate.float() > 0)) < 1e-2
+        scale = torch.rand(Cin, device=DEV) + 0.5
+        coeffs = torch.stack([torch.zeros(Cin, device=DEV), torch.ones(Cin, device=DEV), scale,
+                              torch.randn(Cin, device=DEV) * 0.1])
+        bacc = fn.bn_acc_buffer(Cin, DEV)
+        dz = fn.conv_dgrad_t(dy, wt.view(l), bn_y=gate, bn_coeffs=coeffs, bn_acc=bacc)
+        dz_ref = dref * ((gate.float() * coeffs[2] + coeffs[3]) > 0)
+        assert rel_err(dz, dz_ref) < 1e-2
+        sb = bacc.sum(0).float()
+        assert torch.allclose(sb[0], dz_ref.reshape(-1, Cin).sum(0), rtol=1e-2, atol=2e-1)
