@@ -58,8 +58,10 @@ def main():
 
     info = D.init_distributed()
     world = info.world_size
-    torch.cuda.set_device(info.local_rank)
-    dev = torch.device('cuda', info.local_rank)
+    # one GPU per rank; with the gloo rehearsal backend on a smaller box ranks wrap onto the GPUs present
+    gpu = info.local_rank if info.backend == 'nccl' else info.local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device('cuda', gpu)
 
     knob_config = {
         'lr': FloatKnob(1e-3, 2e-1, is_exp=True),
