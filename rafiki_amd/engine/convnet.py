@@ -189,9 +189,10 @@ class ConvNetEngine:
         return fl
 
     # Measured on MI355X (VGG-small, batch 256): overlapping wgrad on a side stream made the step
-    # 11% SLOWER (1.161 -> 1.289 ms; the concurrent GEMMs and split-K slab traffic interfere), so it
-    # is off by default and kept as an option for layer shapes where it pays.
-    overlap_wgrad = False
+    # 11% SLOWER (1.161 -> 1.289 ms; the concurrent GEMMs and split-K slab traffic interfere) and,
+    # re-measured with the current kernels, still 5-6% slower (258k -> 243-245k img/s), so it is off
+    # by default (RAFIKI_OVERLAP_WGRAD=1) and kept as an option for layer shapes where it pays.
+    overlap_wgrad = os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') == '1'
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
     # data gradients as forward convs of dy with flipped/transposed weights (F.ConvWT, one transpose
