@@ -58,10 +58,13 @@ def test_graph_replay_matches_eager():
     assert torch.allclose(e1.running, e2.running)
 
 
-def test_scheduled_graph_matches_eager_and_advances_counter():
-    """capture_scheduled: one prologue kernel gathers rows sched[ctr], zeroes the BN slot tables and
-    bumps the device counter; replays must track an eager loop over the same rows."""
-    e1, e2 = _engine(), _engine()
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_scheduled_graph_matches_eager_and_advances_counter(opt):
+    """capture_scheduled: one prologue kernel gathers rows sched[ctr] and zeroes the BN slot tables; the
+    step counter advances in the SGD kernel (sgd) or in the prologue once every block has read it
+    (adam); replays must track an eager loop over the same rows."""
+    e1, e2 = _engine(optimizer=opt, lr=0.01 if opt == 'adam' else 0.05), _engine(optimizer=opt,
+                                                                               lr=0.01 if opt == 'adam' else 0.05)
     data, labels = _batch(96, seed=7)
     steps, B = 4, 32
     idx = torch.randint(0, 96, (steps, B), device='cuda', generator=torch.Generator('cuda').manual_seed(1))
