@@ -46,7 +46,11 @@ enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
 // sum dz*y) that BN backward needs go to the fp64 slot table `stats` (with FLAG_SATOM), so that
 // layer's separate reduction pass disappears.
 enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16, FLAG_NOFAST = 64,
-             FLAG_LRELU = 32, FLAG_SATOM = 256, FLAG_BNB = 512 };
+             FLAG_LRELU = 32, FLAG_SATOM = 256, FLAG_BNB = 512, FLAG_BNP = 1024 };
+// FLAG_BNP (data-gradient into a BatchNorm+ReLU+2x2-max-pool layer): the output is that layer's
+// pooled gradient (stored unchanged); its BN-backward sums are formed here: per output element the
+// window's first maximal act(y*scale+shift) (y read through `gate` at the 2Hx2W input resolution,
+// power-of-two geometry) routes the gradient, (sum dz, sum dz*y) -> fp64 slots (with FLAG_SATOM).
 
 struct IgemmParams {
   const bf16* A;
@@ -529,7 +533,7 @@ template <int MI, int NI, int FL, bool GUARD>
 RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm, int lane) {
   const int fl = FL < 0 ? p.flags : FL;
   const bool ST = fl & FLAG_STATS, BI = fl & FLAG_BIAS, RE = fl & FLAG_RELU, LR = fl & FLAG_LRELU,
-             GA = fl & FLAG_GATE, BB = fl & FLAG_BNB;
+             GA = fl & FLAG_GATE, BB = fl & FLAG_BNB, BP = fl & FLAG_BNP;
   bf16* C = (bf16*)p.out;
   float s[NI][4], ss[NI][4];
 #pragma unroll
@@ -541,8 +545,8 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
     const int n = ncol + j * 16;
     const bool nok = !GUARD || n < p.N;
     f32x4 b = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
-    if ((BI || BB) && nok) b = *(const f32x4*)(p.bias + n);
-    if (BB && nok) sh = *(const f32x4*)(p.bias + p.N + n);
+    if ((BI || BB || BP) && nok) b = *(const f32x4*)(p.bias + n);
+    if ((BB || BP) && nok) sh = *(const f32x4*)(p.bias + p.N + n);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int m = mrow + i * 16;
@@ -573,6 +577,30 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
           ss[j][e] += v[e] * yv;
         }
       }
+      if (BP) {
+        const int wo = m & (p.W - 1), t = m >> p.log2W, ho = t & (p.H - 1), nimg = t >> p.log2H;
+        const long long row = 2LL * p.W * p.ldc;
+        const long long b0 = (((long long)nimg * 2 * p.H + 2 * ho) * (2LL * p.W) + 2 * wo) * p.ldc + n;
+        bf16x4 g4[4];
+        g4[0] = *(const bf16x4*)(p.gate + b0);
+        g4[1] = *(const bf16x4*)(p.gate + b0 + p.ldc);
+        g4[2] = *(const bf16x4*)(p.gate + b0 + row);
+        g4[3] = *(const bf16x4*)(p.gate + b0 + row + p.ldc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float best = -INFINITY, zb = 0.f, yb = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // first maximal element of the window (torch rule)
+            const float yv = (float)g4[q][e];
+            const float z = yv * b[e] + sh[e];
+            const float a = fmaxf(z, 0.f);
+            if (a > best) { best = a; zb = z; yb = yv; }
+          }
+          const float dz = zb > 0.f ? v[e] : 0.f;
+          s[j][e] += dz;
+          ss[j][e] += dz * yb;
+        }
+      }
       bf16x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
@@ -580,7 +608,7 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
       acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  if (ST || BB) {
+  if (ST || BB || BP) {
 #pragma unroll
     for (int j = 0; j < NI; ++j)
 #pragma unroll
@@ -622,7 +650,7 @@ template <int MI, int NI, bool GUARD>
 RK_DEV void tile_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int ncol, int mt, int wm,
                           int lane) {
   constexpr int S_ = FLAG_STATS, B_ = FLAG_BIAS, R_ = FLAG_RELU, L_ = FLAG_LRELU, G_ = FLAG_GATE, A_ = FLAG_SATOM;
-  switch (p.flags & (S_ | B_ | R_ | L_ | G_ | A_ | FLAG_BNB)) {
+  switch (p.flags & (S_ | B_ | R_ | L_ | G_ | A_ | FLAG_BNB | FLAG_BNP)) {
     case 0: return tile_epi<MI, NI, 0, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case S_: return tile_epi<MI, NI, S_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case S_ | A_: return tile_epi<MI, NI, S_ | A_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
@@ -631,6 +659,7 @@ RK_DEV void tile_epilogue(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, 
     case B_ | R_: return tile_epi<MI, NI, B_ | R_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case B_ | L_: return tile_epi<MI, NI, B_ | L_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     case FLAG_BNB | A_: return tile_epi<MI, NI, FLAG_BNB | A_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
+    case FLAG_BNP | A_: return tile_epi<MI, NI, FLAG_BNP | A_, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
     default: return tile_epi<MI, NI, -1, GUARD>(p, acc, mrow, ncol, mt, wm, lane);
   }
 }
@@ -1459,6 +1488,8 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
   // the LDS-DMA operands use shift-only index arithmetic: other extents run register-staged
   if (conv && (p.log2C < 0 || p.log2H < 0 || p.log2W < 0)) tile &= 15 | 16;
   if (epi == 0 && splits != 1) return RK_EBADARG;
+  if ((flags & FLAG_BNP) && (epi != 0 || p.log2H < 0 || p.log2W < 0 || !gate || !bias || !(flags & FLAG_SATOM)))
+    return RK_EUNSUPPORTED;
   switch (kind) {
     // conv forward / data-gradient with epi 1: split-K fp32 slabs for the small-M layers (4x4 / 8x8
     // VGG convs), combined by rk_slab_epi (bf16 out + BN statistics / BN-backward gate)
@@ -1500,6 +1531,7 @@ extern "C" int rk_hconv(int dgrad, int tile, const void* A, const void* B, void*
   }
   if (rk_log2(Cch) < 6 || N <= 0 || N % BN != 0 || K != 9 * Cch) return RK_EUNSUPPORTED;
   if (ldb != (dgrad ? 9 * N : K)) return RK_EBADARG;
+  if ((flags & FLAG_BNP) && (!gate || !bias || !(flags & FLAG_SATOM))) return RK_EUNSUPPORTED;
   IgemmParams p{};
   p.A = (const bf16*)A; p.B = (const bf16*)B; p.out = C; p.bias = bias; p.stats = stats;
   p.gate = (const bf16*)gate;

@@ -195,6 +195,8 @@ class ConvNetEngine:
     overlap_wgrad = os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') == '1'
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
+    # ... and into BN+ReLU+max-pool blocks (FLAG_BNP: argmax routing in the dgrad epilogue)
+    fuse_bn_pool = os.environ.get('RAFIKI_BN_POOL_FUSE', '1') != '0'
     # data gradients as forward convs of dy with flipped/transposed weights (F.ConvWT, one transpose
     # launch per step): the forward kernels' K-inner weight operand and tiles are the faster ones
     dgrad_wt = os.environ.get('RAFIKI_DGRAD_WT', '1') != '0'
@@ -310,9 +312,17 @@ class ConvNetEngine:
                 # dgrad epilogue (FLAG_BNB), so its bn_bwd_acc is a single apply pass
                 py, pco = saved[bi - 1]
                 reduced = accs is not None and self.fuse_bn_dgrad and not self.blocks[bi - 1][3]
+                # into a BN+ReLU+max-pool block (power-of-two geometry): its BN-backward sums ride in
+                # the dgrad epilogue too (FLAG_BNP, argmax routing from the pre-BN output)
+                pool_fused = (accs is not None and self.fuse_bn_dgrad and wt is not None and self.blocks[bi - 1][3]
+                              and self.fuse_bn_pool and not (hw & (hw - 1)))
                 if wt is not None:
                     if reduced:
                         d = F.conv_dgrad_t(dy, wt.view(bi - 1), bn_y=py, bn_coeffs=pco, bn_acc=accs[bi - 1][1])
+                    elif pool_fused:
+                        d = F.conv_dgrad_t(dy, wt.view(bi - 1), bn_pool_y=py, bn_coeffs=pco,
+                                           bn_acc=accs[bi - 1][1])
+                        reduced = True
                     else:
                         d = F.conv_dgrad_t(dy, wt.view(bi - 1))
                 elif reduced:

@@ -23,6 +23,7 @@ KIND_CONV_FWD, KIND_CONV_DGRAD, KIND_CONV_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND
 FLAG_RELU, FLAG_BIAS, FLAG_STATS, FLAG_GATE, FLAG_ACCUM, FLAG_LRELU = 1, 2, 4, 8, 16, 32
 FLAG_SATOM = 256
 FLAG_BNB = 512
+FLAG_BNP = 1024  # dgrad into a BN+ReLU+maxpool layer: its BN-backward sums in the epilogue
 # BatchNorm statistics as fp64 atomic sums in a few slots (conv epilogue / bwd reduce) consumed by
 # fused finalize+apply kernels: 2 launches per BN layer and direction instead of 4 / 3.  Summation
 # order then varies run to run in the last bits; RAFIKI_BN_ATOMIC=0 keeps the deterministic
@@ -395,7 +396,7 @@ class ConvWT:
 
 
 def conv_dgrad_t(dy: torch.Tensor, wt: torch.Tensor, *, out=None, gate=None, bn_y=None, bn_coeffs=None,
-                 bn_acc=None):
+                 bn_acc=None, bn_pool_y=None):
     """dx = dgrad(dy, w) computed as conv3x3(dy, wt) with wt = ConvWT.view(...) [Cin][9*Cout]: the forward
     kernels (halo-tiled / implicit GEMM / split-K) with the data-gradient epilogues of conv_dgrad
     (ReLU gate, or FLAG_BNB: the input layer's BN+ReLU mask and BN-backward sums)."""
@@ -410,6 +411,11 @@ def conv_dgrad_t(dy: torch.Tensor, wt: torch.Tensor, *, out=None, gate=None, bn_
         assert bn_y.shape == out.shape and bn_acc.dtype == torch.float64 and bn_acc.shape[-1] == Cin
         gate, bias, stats = bn_y, bn_coeffs[2], bn_acc
         flags = FLAG_BNB | FLAG_SATOM | ((bn_acc.shape[0] - 1) << 12)
+    elif bn_pool_y is not None:
+        assert bn_pool_y.shape == (Nb, 2 * H, 2 * W, Cin) and bn_acc.dtype == torch.float64
+        assert not (H & (H - 1)) and not (W & (W - 1)), 'FLAG_BNP needs power-of-two geometry'
+        gate, bias, stats = bn_pool_y, bn_coeffs[2], bn_acc
+        flags = FLAG_BNP | FLAG_SATOM | ((bn_acc.shape[0] - 1) << 12)
 
     def run(cfg):
         if cfg[0] == 'h':
@@ -427,9 +433,10 @@ def conv_dgrad_t(dy: torch.Tensor, wt: torch.Tensor, *, out=None, gate=None, bn_
         else:
             igemm(KIND_CONV_FWD, 0, dy, wt, out, M, Cin, K, Cout, K, Cin, gate=gate, bias=bias, stats=stats, H=H,
                   W=W, C=Cout, taps=9, flags=flags, tile=cfg[0])
-    cfg = _tuned(('cdT', M, Cin, K, H, W, Cout, bn_y is not None),
+    mode = 'bnb' if bn_y is not None else 'bnp' if bn_pool_y is not None else bool(gate is not None)
+    cfg = _tuned(('cdT', M, Cin, K, H, W, Cout, mode),
                  _tile_candidates(M, Cin) + _hconv_candidates(M, Cin, H, W, Cout, 9)
-                 + _conv_split_candidates(M, Cin, K, H, W, Cout), run)
+                 + (_conv_split_candidates(M, Cin, K, H, W, Cout) if bn_pool_y is None else []), run)
     if bn_acc is not None and autotune.can_tune():
         bn_acc.zero_()  # tuning runs accumulated into it
     run(cfg)

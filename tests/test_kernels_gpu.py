@@ -429,3 +429,43 @@ def test_conv_wt_transposed_dgrad(fn):
         assert rel_err(dz, dz_ref) < 1e-2
         sb = bacc.sum(0).float()
         assert torch.allclose(sb[0], dz_ref.reshape(-1, Cin).sum(0), rtol=1e-2, atol=2e-1)
+
+
+def test_conv_wt_dgrad_bn_pool_sums(fn):
+    """conv_dgrad_t(bn_pool_y=...) (FLAG_BNP): the output is the unchanged pooled data gradient and the
+    fp64 slots hold the BN-backward sums (sum dz, sum dz*y) of the BN+ReLU+2x2-max-pool layer below,
+    dz routed to the window's first maximum — vs torch max_pool2d indices in fp32."""
+    torch.manual_seed(17)
+    shapes = [(16, 4, 4, 512, 512), (8, 8, 8, 128, 256), (2, 16, 16, 64, 128)]
+    ws = [(torch.randn(co, 9 * ci, device=DEV) / (3 * ci ** 0.5)).bfloat16() for (_, _, _, ci, co) in shapes]
+    arena = torch.zeros(sum((w.numel() + 63) // 64 * 64 for w in ws) + 64, device=DEV, dtype=torch.bfloat16)
+    views, off = [], 0
+    for w in ws:
+        v = arena[off:off + w.numel()].view_as(w)
+        v.copy_(w)
+        views.append(v)
+        off += (w.numel() + 63) // 64 * 64
+    wt = fn.ConvWT(arena, views)
+    wt.refresh()
+    for l, (N, H, W, Cin, Cout) in enumerate(shapes):
+        w4 = ws[l].float().reshape(Cout, 3, 3, Cin)
+        dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+        xr = torch.zeros(N, Cin, H, W, device=DEV, requires_grad=True)
+        F.conv2d(xr, _w_to_oihw(w4), padding=1).backward(_nhwc_to_nchw(dy.float()))
+        dref = xr.grad.permute(0, 2, 3, 1)
+        y = torch.randn(N, 2 * H, 2 * W, Cin, device=DEV).bfloat16()
+        scale = torch.rand(Cin, device=DEV) + 0.5
+        coeffs = torch.stack([torch.zeros(Cin, device=DEV), torch.ones(Cin, device=DEV), scale,
+                              torch.randn(Cin, device=DEV) * 0.1])
+        bacc = fn.bn_acc_buffer(Cin, DEV)
+        d = fn.conv_dgrad_t(dy, wt.view(l), bn_pool_y=y, bn_coeffs=coeffs, bn_acc=bacc)
+        assert rel_err(d, dref) < 1e-2
+        z = y.float() * coeffs[2] + coeffs[3]
+        _, idx = F.max_pool2d(_nhwc_to_nchw(z.relu()), 2, return_indices=True)
+        # route the kernel's own (bf16) pooled gradient so only the sums are compared
+        routed = F.max_unpool2d(_nhwc_to_nchw(d.float()), idx, 2).permute(0, 2, 3, 1)
+        dz = routed * (z > 0)
+        sb = bacc.sum(0).float()
+        s0, s1 = dz.reshape(-1, Cin).sum(0), (dz * y.float()).reshape(-1, Cin).sum(0)
+        assert torch.allclose(sb[0], s0, rtol=1e-2, atol=2e-1)
+        assert torch.allclose(sb[1], s1, rtol=1e-2, atol=2e-1)
