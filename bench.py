@@ -43,6 +43,8 @@ def parse():
     ap.add_argument('--trial-epochs', type=float, default=10.0)
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--dtype', default=os.environ.get('RAFIKI_DTYPE', 'fp32'), choices=('fp32', 'bf16'),
+                    help='compute dtype (fp32 = the reference precision; bf16 is opt-in)')
     return ap.parse_args()
 
 
@@ -53,6 +55,7 @@ def main():
     from rafiki_amd.model.dataset import synthetic_images
     from rafiki_amd.model.knob import FixedKnob, FloatKnob
     from rafiki_amd.ops import autotune
+    from rafiki_amd.ops import f32 as S
     from rafiki_amd.ops import functional as F
     from rafiki_amd.parallel import dist as D
 
@@ -74,22 +77,23 @@ def main():
     proposals = D.broadcast_proposals(info, knob_config, proposals)
     knobs = proposals[info.rank]
 
-    # synthetic CIFAR-shaped data, resident in HBM as packed NHWC bf16 (8 channels)
+    eng = ConvNetEngine(num_classes=10, in_channels=3, image_size=32, device=dev, seed=args.seed + info.rank,
+                        lr=knobs['lr'], momentum=knobs['momentum'], weight_decay=knobs['weight_decay'],
+                        dtype=args.dtype)
+    # synthetic CIFAR-shaped data, resident in HBM as packed NHWC in the engine's dtype
     imgs, labels = synthetic_images(args.dataset_size, size=32, channels=3, classes=10,
                                     seed=args.seed + info.rank)
     x_u8 = torch.from_numpy(imgs).permute(0, 3, 1, 2).contiguous().to(dev)
-    data = F.pack_nhwc(x_u8, 8, 1.0 / 127.5, -1.0)
+    pack = S.pack_nhwc if eng.f32 else F.pack_nhwc
+    data = pack(x_u8, eng.cin_p, 1.0 / 127.5, -1.0)
     del x_u8
     y_all = torch.from_numpy(labels).to(dev, torch.int32)
-
-    eng = ConvNetEngine(num_classes=10, in_channels=3, image_size=32, device=dev, seed=args.seed + info.rank,
-                        lr=knobs['lr'], momentum=knobs['momentum'], weight_decay=knobs['weight_decay'])
     B = args.batch
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 17 * info.rank)
     total_steps = args.warmup + args.steps
     idx = torch.randint(0, args.dataset_size, (total_steps, B), device=dev, generator=gen)
-    xb = torch.empty((B, 32, 32, 8), dtype=torch.bfloat16, device=dev)
+    xb = torch.empty((B, 32, 32, eng.cin_p), dtype=eng.act_dtype, device=dev)
     yb = torch.empty((B,), dtype=torch.int32, device=dev)
 
     use_graph = not args.no_graph
@@ -147,7 +151,7 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
-            'dtype': 'bf16',
+            'dtype': eng.dtype,
             'data': 'synthetic (class-conditional 32x32x3 images, random-init weights)',
             'config': {'model': 'VGG-small 32x32x3 (8 conv3x3+BN+ReLU, 4 maxpool, FC512, FC10)',
                        'global_batch': B * world, 'per_trial_batch': B, 'seq_len': None,

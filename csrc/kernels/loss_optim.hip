@@ -13,10 +13,11 @@
 
 namespace {
 
+template <typename DT>  // d(logits) storage: bf16 (bf16 engine) or float (fp32 engine)
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits, int ldl,
                                                            const int* __restrict__ labels, int B, int ncls,
                                                            int ignore_index, float grad_scale,
-                                                           bf16* __restrict__ dlogits, int ldd,
+                                                           DT* __restrict__ dlogits, int ldd,
                                                            float* __restrict__ probs, float* loss_sum,
                                                            int* correct, int* counted) {
   const int lane = threadIdx.x & 63;
@@ -43,11 +44,11 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   const int y = labels ? labels[row] : -1;
   const bool valid = labels && y != ignore_index && y >= 0 && y < ncls;
   if (dlogits) {
-    bf16* dr = dlogits + (long long)row * ldd;
+    DT* dr = dlogits + (long long)row * ldd;
     for (int c = lane; c < ldd; c += 64) {
       float g = 0.f;
       if (valid && c < ncls) g = (__expf(lr[c] - lse) - (c == y ? 1.f : 0.f)) * grad_scale;
-      dr[c] = (bf16)g;
+      dr[c] = (DT)g;
     }
   }
   if (probs) {
@@ -369,8 +370,19 @@ extern "C" int rk_softmax_xent(const float* logits, int ldl, const int* labels, 
                                float grad_scale, void* dlogits, int ldd, float* probs, float* loss_sum, int* correct,
                                int* counted, void* stream) {
   if (B <= 0) return RK_OK;
-  hipLaunchKernelGGL(softmax_xent_kernel, dim3(rk_cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, logits, ldl, labels,
-                     B, ncls, ignore_index, grad_scale, (bf16*)dlogits, ldd, probs, loss_sum, correct, counted);
+  hipLaunchKernelGGL(softmax_xent_kernel<bf16>, dim3(rk_cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, logits, ldl,
+                     labels, B, ncls, ignore_index, grad_scale, (bf16*)dlogits, ldd, probs, loss_sum, correct, counted);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// same with fp32 d(logits) (fp32 training path)
+extern "C" int rk_softmax_xent_f32(const float* logits, int ldl, const int* labels, int B, int ncls, int ignore_index,
+                                   float grad_scale, float* dlogits, int ldd, float* probs, float* loss_sum,
+                                   int* correct, int* counted, void* stream) {
+  if (B <= 0) return RK_OK;
+  hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(rk_cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, logits, ldl,
+                     labels, B, ncls, ignore_index, grad_scale, dlogits, ldd, probs, loss_sum, correct, counted);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -1,0 +1,430 @@
+// fp32 implicit-GEMM engine for gfx950: 3x3/1x1 convolutions (forward, data-grad as a forward conv
+// of dy with flipped/transposed weights, weight-grad) and dense GEMMs on v_mfma_f32_32x32x2_f32 —
+// exact fp32 products with fp32 accumulation (bit-equal to an fmaf chain), i.e. the reference's own
+// precision (pg_gans.py:830,914 dtype='float32'; Keras fp32 in TfFeedForward.py:141-164 and
+// TfVgg16.py:115-130).  No bf16 anywhere on this path.
+//
+// Design for the f32 MFMA rate (64 FLOP/clk/SIMD, 1/16 of bf16): the arithmetic, not the memory
+// system, is the bound, so a block owns a large tile and keeps every SIMD issuing MFMAs:
+//   * 256 threads = 4 waves as 2x2; wave tile (32*MI) x (32*NI), MI, NI in {1,2} -> block tile up to
+//     128x128 (64 fp32 accumulator registers per lane), BK = 32 fp32 (128-B LDS rows);
+//   * operands go global -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging, no ds_write):
+//     "K-inner" operands (reduction index contiguous: NHWC activations gathered per 3x3 tap, [N][K]
+//     weights) land as XOR-swizzled [T][32] rows read with ds_read_b128; "K-outer" operands
+//     (reduction over rows: dY / X in the weight gradients, W in dense dX) land as [32][T] rows read
+//     with ds_read_b32 (32 consecutive dwords per half-wave: conflict-free);
+//   * the K order inside a 8-deep group is permuted so one ds_read_b128 feeds 4 MFMAs: lane half h
+//     supplies k = 8g + 4h + e at MFMA step e, for both operands;
+//   * an NST-stage LDS ring (2: 64 KiB at 128x128, 2 blocks/CU; 3: one block/CU, two tiles in
+//     flight) with ONE raw s_barrier per K-tile and a counted vmcnt;
+//   * out-of-range lanes (conv halo, tile edges, K tail) DMA zeros through the buffer range check;
+//   * the accumulator layout puts one output channel per lane and 16 pixels in registers, so BN
+//     statistics are 16 in-register adds + one lane swap, and stores are 2 x 128-B rows per
+//     instruction.
+// Epilogues (runtime flags: the epilogue runs once per tile after K/32 x 4096 MFMA cycles, so its
+// VALU is noise): bias, ReLU / leaky-ReLU, ReLU gate (dense dX), BN statistics (fp64 atomic slots),
+// FLAG_BNB / FLAG_BNP (data-gradient into a BN+ReLU [+2x2 max-pool] layer: mask + BN-backward sums),
+// split-K fp32 slabs, accumulate.
+#include "common.h"
+
+namespace {
+
+constexpr int SBK = 32;  // fp32 elements per K-tile: 128-B LDS rows
+constexpr unsigned SOOB = 0x80000000u;
+
+enum SMode { SM_KIN_DENSE = 0, SM_KIN_CONV = 1, SM_KOUT_DENSE = 2, SM_KOUT_CONV = 3 };
+enum SFlags { SF_RELU = 1, SF_BIAS = 2, SF_STATS = 4, SF_GATE = 8, SF_ACCUM = 16, SF_LRELU = 32,
+              SF_BNB = 512, SF_BNP = 1024 };
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct SgParams {
+  const float* A;
+  const float* B;
+  float* out;
+  const float* bias;    // [N] bias; FLAG_BNB/BNP: BN scale [N] then shift [N] of the gated layer
+  double* stats;        // fp64 slot table [slotMask+1][2][N]
+  const float* gate;    // ReLU gate [M][ldc] (SF_GATE) or the gated layer's BN input y (BNB / BNP)
+  int M, N, K;
+  int lda, ldb, ldc;
+  int H, W, C, taps;    // geometry of the gathered (conv) operand; BNP: H, W = pooled resolution
+  int log2H, log2W, log2C;
+  float invC, invH, invW;
+  int ktPer;            // K-tiles per split (gridDim.z splits)
+  long long slabStride; // floats between split-K slabs
+  int flags, slotMask;
+  float alpha, slope;
+  unsigned long long bytesA, bytesB;
+};
+
+RK_DEV __amdgpu_buffer_rsrc_t s_rsrc(const void* base, unsigned long long bytes) {
+  const unsigned nrec = bytes >= 0x80000000ull ? 0x80000000u : (unsigned)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec, 0x00020000);
+}
+
+RK_DEV int s_tap_dy(int t) { return ((t * 11) >> 5) - 1; }
+RK_DEV int s_tap_dx(int t) { return t - 3 * ((t * 11) >> 5) - 1; }
+
+// channel -> tap (power-of-two C by shift, else an fp32 reciprocal, exact below 2^22)
+RK_DEV int s_cdiv(int k, const SgParams& p) {
+  return p.log2C >= 0 ? (k >> p.log2C) : (int)(((float)k + 0.5f) * p.invC);
+}
+// pixel -> (h, w) of an H x W map
+RK_DEV void s_hw(int k, int H, int W, int log2H, int log2W, float invH, float invW, int& h, int& w) {
+  if (log2H >= 0 && log2W >= 0) {
+    w = k & (W - 1);
+    h = (k >> log2W) & (H - 1);
+  } else {
+    const int q = (int)(((float)k + 0.5f) * invW);
+    w = k - q * W;
+    const int n = (int)(((float)q + 0.5f) * invH);
+    h = q - n * H;
+  }
+}
+
+// One operand tile of T rows (K-inner) or T columns (K-outer) per K-tile; T*128 bytes = T/8 DMA
+// wave-instructions, T/32 per wave.
+template <int MODE, int T>
+struct SOperand {
+  static constexpr bool KIN = MODE == SM_KIN_DENSE || MODE == SM_KIN_CONV;
+  static constexpr int NQ = T / 32;
+  static constexpr int RS = T / 4;  // 16-B slots per K-outer row
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned base[NQ];
+  unsigned mask[NQ];
+  int sub[NQ];
+  int dyx[NQ];  // K-outer conv: (dy, dx) packed as dy*W + dx
+  int dy[NQ], dx[NQ];
+
+  RK_DEV void init(const SgParams& p, const float* ptr, unsigned long long bytes, int ld, int tile0, int extent,
+                   int wid, int lane) {
+    rsrc = s_rsrc(ptr, bytes);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int slot = (wid * NQ + q) * 64 + lane;
+      dy[q] = dx[q] = dyx[q] = 0;
+      if constexpr (KIN) {
+        const int i = slot >> 3;
+        const int c = (slot & 7) ^ ((i >> 1) & 7);  // logical 16-B chunk stored at this slot
+        sub[q] = c;
+        const int gi = tile0 + i;
+        const bool ok = gi < extent;
+        if constexpr (MODE == SM_KIN_DENSE) {
+          base[q] = (unsigned)gi * (unsigned)ld * 4u;
+          mask[q] = ok ? 1u : 0u;
+        } else {
+          int h, w;
+          s_hw(gi, p.H, p.W, p.log2H, p.log2W, p.invH, p.invW, h, w);
+          base[q] = (unsigned)gi * (unsigned)p.C * 4u;
+          unsigned m = 1u;
+          if (p.taps == 9) {
+            m = 0u;
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+              m |= (((unsigned)(h + s_tap_dy(t)) < (unsigned)p.H && (unsigned)(w + s_tap_dx(t)) < (unsigned)p.W) ? 1u : 0u)
+                   << t;
+          }
+          mask[q] = ok ? m : 0u;
+        }
+      } else {
+        const int krow = slot / RS;
+        const int col = tile0 + 4 * (slot % RS);
+        sub[q] = krow;
+        bool ok = col < extent;
+        if constexpr (MODE == SM_KOUT_DENSE) {
+          base[q] = (unsigned)col * 4u;
+        } else {  // SM_KOUT_CONV: column = (tap, channel) of the gathered activation
+          const int tap = s_cdiv(col, p);
+          const int ci = col - tap * p.C;
+          ok = ok && tap < p.taps;
+          if (p.taps == 9) {
+            dy[q] = s_tap_dy(tap);
+            dx[q] = s_tap_dx(tap);
+          }
+          dyx[q] = dy[q] * p.W + dx[q];
+          base[q] = (unsigned)ci * 4u;
+        }
+        mask[q] = ok ? 1u : 0u;
+      }
+    }
+  }
+
+  // byte offset (or SOOB) of this lane's 16-B chunk for instruction q of K-tile kt
+  RK_DEV unsigned offset(const SgParams& p, int q, int kt, int K, int ld) const {
+    if constexpr (MODE == SM_KIN_DENSE) {
+      const int k = kt * SBK + 4 * sub[q];
+      return (mask[q] && k < K) ? base[q] + (unsigned)k * 4u : SOOB;
+    } else if constexpr (MODE == SM_KIN_CONV) {
+      const int k = kt * SBK + 4 * sub[q];
+      if (k >= K) return SOOB;
+      const int tap = s_cdiv(k, p);
+      const int ci = k - tap * p.C;
+      if (!((mask[q] >> tap) & 1u)) return SOOB;
+      const int d = p.taps == 9 ? s_tap_dy(tap) * p.W + s_tap_dx(tap) : 0;
+      return (unsigned)((int)base[q] + (d * p.C + ci) * 4);
+    } else if constexpr (MODE == SM_KOUT_DENSE) {
+      const int k = kt * SBK + sub[q];
+      return (mask[q] && k < K) ? base[q] + (unsigned)k * (unsigned)ld * 4u : SOOB;
+    } else {  // SM_KOUT_CONV: row k = pixel, column chunk = 4 channels of one tap
+      const int k = kt * SBK + sub[q];
+      if (!mask[q] || k >= K) return SOOB;
+      int h, w;
+      s_hw(k, p.H, p.W, p.log2H, p.log2W, p.invH, p.invW, h, w);
+      if ((unsigned)(h + dy[q]) >= (unsigned)p.H || (unsigned)(w + dx[q]) >= (unsigned)p.W) return SOOB;
+      return (unsigned)(k + dyx[q]) * (unsigned)p.C * 4u + base[q];
+    }
+  }
+
+  RK_DEV void issue(const SgParams& p, char* tile, int kt, int K, int ld, int wid) const {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      char* dst = tile + (wid * NQ + q) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)dst, 16, (int)offset(p, q, kt, K, ld), 0, 0, 0);
+    }
+  }
+
+  // fragment of 32 rows starting at r0 for k-group g: element e is k = 8g + 4h + e (h = lane >> 5)
+  RK_DEV f32x4 frag(const char* tile, int r0, int g, int lane) const {
+    const int h = lane >> 5;
+    if constexpr (KIN) {
+      const int r = r0 + (lane & 31);
+      return *(const f32x4*)(tile + r * 128 + ((((2 * g + h) ^ ((r >> 1) & 7))) << 4));
+    } else {
+      const float* t = (const float*)tile + (8 * g + 4 * h) * T + r0 + (lane & 31);
+      return f32x4{t[0], t[T], t[2 * T], t[3 * T]};
+    }
+  }
+};
+
+template <int N>
+RK_DEV void s_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+RK_DEV void s_barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// accumulator register r of a 32x32 block: row (r&3) + 8(r>>2) + 4h, column lane&31
+RK_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+template <int MI, int NI>
+RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int nbase, int lane) {
+  const int fl = p.flags;
+  const int h = lane >> 5;
+  float* C = p.out + (long long)blockIdx.z * p.slabStride;
+  const bool want_sums = fl & (SF_STATS | SF_BNB | SF_BNP);
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int n = nbase + ni * 32 + (lane & 31);
+    const bool nok = n < p.N;
+    float b = 0.f, sh = 0.f;
+    if ((fl & (SF_BIAS | SF_BNB | SF_BNP)) && nok) b = p.bias[n];
+    if ((fl & (SF_BNB | SF_BNP)) && nok) sh = p.bias[p.N + n];
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mbase + mi * 32 + acc_row(r, h);
+        if (!(nok && m < p.M)) continue;
+        float v = acc[mi][ni][r] * p.alpha;
+        const long long idx = (long long)m * p.ldc + n;
+        if (fl & SF_BIAS) v += b;
+        if (fl & SF_STATS) {
+          s += v;
+          ss += v * v;
+        }
+        if (fl & SF_RELU) v = fmaxf(v, 0.f);
+        else if (fl & SF_LRELU) v = v > 0.f ? v : v * p.slope;
+        if (fl & SF_GATE) v = p.gate[idx] > 0.f ? v : 0.f;
+        if (fl & SF_BNB) {
+          const float yv = p.gate[idx];
+          v = yv * b + sh > 0.f ? v : 0.f;
+          s += v;
+          ss += v * yv;
+        }
+        if (fl & SF_BNP) {
+          // m = pooled pixel (img, ho, wo) of an H x W map; its window sits at 2H x 2W
+          int ho, wo;
+          s_hw(m, p.H, p.W, p.log2H, p.log2W, p.invH, p.invW, ho, wo);
+          const long long img = (long long)(m - (ho * p.W + wo)) / ((long long)p.H * p.W);
+          const long long W2 = 2LL * p.W;
+          const long long b0 = ((img * 2 * p.H + 2 * ho) * W2 + 2 * wo) * p.ldc + n;
+          const float y4[4] = {p.gate[b0], p.gate[b0 + p.ldc], p.gate[b0 + W2 * p.ldc], p.gate[b0 + W2 * p.ldc + p.ldc]};
+          float best = -INFINITY, zb = 0.f, yb = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // first maximal relu(z) of the window (torch max_pool2d rule)
+            const float z = y4[q] * b + sh;
+            const float a = fmaxf(z, 0.f);
+            if (a > best) { best = a; zb = z; yb = y4[q]; }
+          }
+          const float dz = zb > 0.f ? v : 0.f;
+          s += dz;
+          ss += dz * yb;
+        }
+        if (fl & SF_ACCUM) v += C[idx];
+        C[idx] = v;
+      }
+    }
+    if (want_sums) {
+      s += __shfl_xor(s, 32, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (nok) {
+        double* slot = p.stats + (long long)(blockIdx.x & p.slotMask) * 2 * p.N;
+        unsafeAtomicAdd(slot + (h ? p.N : 0) + n, (double)(h ? ss : s));
+      }
+    }
+  }
+}
+
+template <int MI, int NI, int AM, int BMD, int NST>
+__global__ __launch_bounds__(256) void sgemm_kernel(const SgParams p) {
+  constexpr int BM = 64 * MI, BN = 64 * NI;
+  constexpr int ABYTES = BM * 128, SB = (BM + BN) * 128;
+  constexpr int L = BM / 32 + BN / 32;  // DMA wave-instructions per wave per K-tile
+  __shared__ __attribute__((aligned(16))) char smem[NST * SB];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tilesN = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / tilesN, nt = bid - mt * tilesN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nk = (p.K + SBK - 1) / SBK;
+  const int kt0 = blockIdx.z * p.ktPer;
+  const int kt1 = min(nk, kt0 + p.ktPer);
+
+  SOperand<AM, BM> A;
+  SOperand<BMD, BN> B;
+  A.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane);
+  B.init(p, p.B, p.bytesB, p.ldb, n0, p.N, wid, lane);
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto issue = [&](int kt, int st) {
+    char* t = smem + st * SB;
+    A.issue(p, t, kt, p.K, p.lda, wid);
+    B.issue(p, t + ABYTES, kt, p.K, p.ldb, wid);
+  };
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (kt0 + s < kt1) issue(kt0 + s, s);
+
+  int st = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    // tile kt has landed once only the younger tiles' DMAs are outstanding
+    if constexpr (NST == 3) {
+      if (kt + 1 < kt1) s_wait_vmcnt<L>();
+      else s_wait_vmcnt<0>();
+    } else {
+      s_wait_vmcnt<0>();
+    }
+    s_barrier_lds();  // every wave's DMA for tile kt is in LDS; every wave is done with tile kt-1
+    if (kt + NST - 1 < kt1) issue(kt + NST - 1, st == 0 ? NST - 1 : st - 1);
+    const char* As = smem + st * SB;
+    const char* Bs = As + ABYTES;
+#pragma unroll
+    for (int g = 0; g < SBK / 8; ++g) {
+      f32x4 a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = A.frag(As, wm * (BM / 2) + i * 32, g, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = B.frag(Bs, wn * (BN / 2) + j * 32, g, lane);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+    }
+    st = st + 1 == NST ? 0 : st + 1;
+  }
+  s_epilogue<MI, NI>(p, acc, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
+}
+
+template <int MI, int NI, int AM, int BMD>
+int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
+  const int tiles = rk_cdiv(p.M, 64 * MI) * rk_cdiv(p.N, 64 * NI);
+  dim3 grid(tiles, 1, splits);
+  if (nst == 3) hipLaunchKernelGGL((sgemm_kernel<MI, NI, AM, BMD, 3>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((sgemm_kernel<MI, NI, AM, BMD, 2>), grid, dim3(256), 0, st, p);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+template <int AM, int BMD>
+int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t st) {
+  switch (tile) {
+    case 0: return s_launch<2, 2, AM, BMD>(p, nst, splits, st);
+    case 1: return s_launch<2, 1, AM, BMD>(p, nst, splits, st);
+    case 2: return s_launch<1, 2, AM, BMD>(p, nst, splits, st);
+    case 3: return s_launch<1, 1, AM, BMD>(p, nst, splits, st);
+  }
+  return RK_EBADARG;
+}
+
+}  // namespace
+
+// fp32 implicit GEMM.  kind: 0 conv forward (A = NHWC activation gathered per tap [M = pixels][K = taps*C],
+// B = weights [N][K]; the data gradient is kind 0 on dy with rk_swt-transposed weights), 2 conv weight
+// gradient (A = dy [K = pixels][M = Cout] K-outer, B = x gathered [K = pixels][N = taps*C]),
+// 3 dense A·Bᵀ (A [M][K], B [N][K]), 4 dense dX A·B (A [M][K], B [K][N]), 5 dense dW Aᵀ·B
+// (A [K][M], B [K][N]).  tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64.  nst: LDS ring stages (2, 3).
+// splits > 1: fp32 slabs out + z * slabStride (combine with rk_reduce_slabs / rk_sreduce_epi).
+// flags: SF_* above; stats = fp64 slots [slotMask+1][2][N] (zeroed by the caller).
+extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float* B, float* C, const float* bias,
+                        double* stats, int slotMask, const float* gate, int M, int N, int K, int lda, int ldb,
+                        int ldc, int H, int W, int Cch, int taps, int splits, long long slabStride, int flags,
+                        float alpha, float slope, long long bytesA, long long bytesB, void* stream) {
+  if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 3) return RK_EBADARG;
+  if (taps != 1 && taps != 9) return RK_EBADARG;
+  const bool conv = kind == 0 || kind == 2;
+  // 16-B chunks: K-inner operands need K % 4 == 0 (and 16-B aligned rows); K-outer ones need the
+  // non-reduction extent % 4 == 0
+  if (kind == 0 || kind == 3 || kind == 4) {
+    if (K % 4 || lda % 4) return RK_EUNSUPPORTED;
+  }
+  if ((kind == 0 || kind == 3) && ldb % 4) return RK_EUNSUPPORTED;
+  if ((kind == 4 || kind == 5 || kind == 2) && (N % 4 || ldb % 4)) return RK_EUNSUPPORTED;
+  if ((kind == 5 || kind == 2) && (M % 4 || lda % 4)) return RK_EUNSUPPORTED;
+  if (conv && (Cch % 4 || Cch <= 0 || H <= 0 || W <= 0)) return RK_EUNSUPPORTED;
+  if (splits > 1 && (flags & (SF_BIAS | SF_RELU | SF_LRELU | SF_GATE | SF_STATS | SF_BNB | SF_BNP)))
+    return RK_EBADARG;  // split-K writes raw partial slabs
+  SgParams p{};
+  p.A = A; p.B = B; p.out = C; p.bias = bias; p.stats = stats; p.gate = gate;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.H = H; p.W = W; p.C = Cch; p.taps = taps;
+  p.log2H = rk_log2(H); p.log2W = rk_log2(W); p.log2C = rk_log2(Cch);
+  p.invC = 1.0f / (float)Cch; p.invH = 1.0f / (float)H; p.invW = 1.0f / (float)W;
+  // reciprocal decodes are exact below 2^22 (pixel indices, tap*C column indices)
+  if (conv && (p.log2H < 0 || p.log2W < 0) && (long long)(kind == 2 ? K : M) + (long long)W * (H + 2) >= (1ll << 22))
+    return RK_EUNSUPPORTED;
+  if ((flags & SF_BNP) && (p.log2H < 0 || p.log2W < 0 || !gate || !bias || !stats)) return RK_EUNSUPPORTED;
+  if ((flags & (SF_STATS | SF_BNB)) && !stats) return RK_EBADARG;
+  p.ktPer = rk_cdiv(rk_cdiv(K, SBK), splits);
+  p.slabStride = splits > 1 ? slabStride : 0;
+  p.flags = flags; p.slotMask = slotMask; p.alpha = alpha; p.slope = slope;
+  p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
+  hipStream_t st = (hipStream_t)stream;
+  switch (kind) {
+    case 0: return s_launch_tile<SM_KIN_CONV, SM_KIN_DENSE>(tile, p, nst, splits, st);
+    case 2: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_CONV>(tile, p, nst, splits, st);
+    case 3: return s_launch_tile<SM_KIN_DENSE, SM_KIN_DENSE>(tile, p, nst, splits, st);
+    case 4: return s_launch_tile<SM_KIN_DENSE, SM_KOUT_DENSE>(tile, p, nst, splits, st);
+    case 5: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_DENSE>(tile, p, nst, splits, st);
+  }
+  return RK_EBADARG;
+}

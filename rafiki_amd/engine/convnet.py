@@ -4,11 +4,18 @@ The whole training step — forward, backward, loss, optimizer — is a fixed se
 kernel launches over pre-planned buffers, captured once into a hipGraph (``torch.cuda.CUDAGraph``
 is hipGraph on ROCm) and replayed per step.  There is no autograd tape and no per-step host work.
 
+Precision: fp32 by default — the reference's precision (pg_gans.py:830,914; Keras fp32 in
+TfVgg16.py:115-130 / TfFeedForward.py:141-164): every GEMM on v_mfma_f32_32x32x2_f32 with fp32
+activations, gradients and BatchNorm (``rafiki_amd.ops.f32``: sgemm.hip + bnf.hip).  ``dtype='bf16'``
+(or RAFIKI_DTYPE=bf16) opts into the bf16 MFMA engine (igemm.hip + bn.hip; fp32 master weights).
+
 Per conv block (conv3x3 -> BatchNorm -> ReLU [-> maxpool2x2]) the step runs
-  fwd : igemm conv (BN partial stats from the accumulators) -> bn finalize -> bn+relu(+pool) apply
-  bwd : bn backward reduce -> finalize (dgamma/dbeta) -> bn backward apply -> conv wgrad (split-K)
-        -> conv dgrad
-then one fused SGD/Adam pass over the flat parameter arena (which also refreshes the bf16 weights).
+  fwd : conv (BN (sum, sum^2) from the accumulators, fp64 slots) -> fused BN finalize + apply + ReLU
+        (+pool)
+  bwd : BN backward (reduce, or its sums already formed in the next layer's dgrad epilogue) + apply
+        -> conv wgrad (split-K) -> conv dgrad as a forward conv of dy with flipped/transposed weights
+        (epilogue: the input layer's ReLU mask / max-pool routing + BN-backward sums)
+then one fused SGD/Adam pass over the flat parameter arena.
 
 VGG-small (the BASELINE benchmark architecture; the reference's TfVgg16.py:115-130 is 48x48x3
 VGG16 without BN — SURVEY §7.4 item 8 asks for an explicit definition):
@@ -31,15 +38,30 @@ import numpy as np
 import torch
 import torch.nn.functional as TF
 
+from ..ops import f32 as S
 from ..ops import functional as F
 from ..ops.graphs import capture as _capture
 from .flat import FlatAdam, FlatParams, FlatSGD, init_const, init_kaiming
 
 VGG_SMALL_CFG = (64, 64, 'M', 128, 128, 'M', 256, 256, 'M', 512, 512, 'M')
+DTYPES = ('fp32', 'bf16')
+
+
+def default_dtype() -> str:
+    """Compute dtype of the native engines: fp32 (the reference's precision) unless RAFIKI_DTYPE=bf16."""
+    d = os.environ.get('RAFIKI_DTYPE', 'fp32').lower()
+    d = {'float32': 'fp32', 'f32': 'fp32', 'bfloat16': 'bf16'}.get(d, d)
+    if d not in DTYPES:
+        raise ValueError('RAFIKI_DTYPE must be one of {}'.format(DTYPES))
+    return d
 
 
 def _pad8(n):
     return (n + 7) // 8 * 8
+
+
+def _pad4(n):
+    return (n + 3) // 4 * 4
 
 
 def _is_pow2(n):
@@ -93,10 +115,16 @@ class ConvNetEngine:
                  cfg: Sequence = VGG_SMALL_CFG, fc_dims: Sequence[int] = (512,), device='cuda', seed: int = 0,
                  bn_eps: float = 1e-5, bn_momentum: float = 0.1, optimizer: str = 'sgd', lr: float = 0.05,
                  momentum: float = 0.9, weight_decay: float = 5e-4, nesterov: bool = True,
-                 betas=(0.9, 0.999), input_bn: bool = False):
+                 betas=(0.9, 0.999), input_bn: bool = False, dtype: Optional[str] = None):
         self.device = torch.device(device)
+        self.dtype = dtype or default_dtype()
+        if self.dtype not in DTYPES:
+            raise ValueError('dtype must be one of {}'.format(DTYPES))
+        self.f32 = self.dtype == 'fp32'
+        self.act_dtype = torch.float32 if self.f32 else torch.bfloat16
         self.num_classes, self.in_channels, self.image_size = num_classes, in_channels, image_size
-        self.cin_p = _pad8(in_channels)
+        # fp32 K-inner operands move 16-B = 4-channel chunks, bf16 ones 8-channel chunks
+        self.cin_p = _pad4(in_channels) if self.f32 else _pad8(in_channels)
         self.ncls_p = _pad8(num_classes)
         self.bn_eps, self.bn_momentum = bn_eps, bn_momentum
         self.flat_input = not any(v != 'M' for v in cfg)
@@ -105,7 +133,7 @@ class ConvNetEngine:
             raise ValueError('input_bn is for fully-connected nets (no conv blocks)')
         # any image size: power-of-two maps use the shift-decoded (and LDS-DMA) gather, others the
         # reciprocal-decoded register-staged gather (VGG16 at 48x48: 48/24/12/6/3)
-        flat = FlatParams(self.device, seed)
+        flat = FlatParams(self.device, seed, compute_bf16=not self.f32)
         self.blocks = []  # (name, cin, cout, pool, H_in)
         cin, hw, i = self.cin_p, image_size, 0
         real_cin = in_channels
@@ -127,7 +155,7 @@ class ConvNetEngine:
         self.feat_hw = hw
         if self.flat_input:
             self.in_dim = image_size * image_size * in_channels
-            self.feat_dim = _pad8(self.in_dim)
+            self.feat_dim = _pad4(self.in_dim) if self.f32 else _pad8(self.in_dim)
             real_in = self.in_dim
         else:
             self.feat_dim = hw * hw * cin
@@ -218,7 +246,9 @@ class ConvNetEngine:
         self.opt.step()
 
     def _fwd_bwd_gpu(self, x, labels):
-        """x: [B, H, W, cin_p] bf16 NHWC, labels: [B] int32. Everything stays on-device."""
+        """x: [B, H, W, cin_p] NHWC (engine dtype), labels: [B] int32. Everything stays on-device."""
+        if self.f32:
+            return self._fwd_bwd_gpu_f32(x, labels)
         fl = self.flat
         B = x.shape[0]
         acts = [x]
@@ -315,7 +345,7 @@ class ConvNetEngine:
                 # into a BN+ReLU+max-pool block (power-of-two geometry): its BN-backward sums ride in
                 # the dgrad epilogue too (FLAG_BNP, argmax routing from the pre-BN output)
                 pool_fused = (accs is not None and self.fuse_bn_dgrad and wt is not None and self.blocks[bi - 1][3]
-                              and self.fuse_bn_pool and not (hw & (hw - 1)))
+                              and self.fuse_bn_pool and not (hw & (hw - 1)) and self.blocks[bi - 1][4] == 2 * hw)
                 if wt is not None:
                     if reduced:
                         d = F.conv_dgrad_t(dy, wt.view(bi - 1), bn_y=py, bn_coeffs=pco, bn_acc=accs[bi - 1][1])
@@ -332,9 +362,92 @@ class ConvNetEngine:
         if self.overlap_wgrad:
             main.wait_stream(side)
 
+    # ------------------------------------------------------------------------- fp32 train
+    def _fwd_bwd_gpu_f32(self, x, labels):
+        """The fp32 step: x [B, H, W, cin_p] fp32 NHWC, labels [B] int32; every GEMM on the f32 MFMA."""
+        fl = self.flat
+        B = x.shape[0]
+        accs = self._bn_accumulators()
+        if not self._acc_zeroed_by_prologue:
+            self._bn_acc_flat.zero_()  # one memset node for every layer's fp64 statistic slots
+        acts, saved, h = [x], [], x
+        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            rm, rv = self.running_stats(bi)
+            y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0])
+            h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
+                                 self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
+            saved.append((y, coeffs))
+            acts.append(h)
+        in_saved = None
+        if self.input_bn:
+            raw = h.reshape(B, 1, 1, self.feat_dim)
+            acc_f, acc_b = accs[-1]
+            S.col_stats(raw.view(B, self.feat_dim), acc_f)
+            rm, rv = self.running_stats('in')
+            h, coeffs = S.bn_fwd(raw, acc_f, B, fl.w('in_bn.gamma'), fl.w('in_bn.beta'), self.bn_eps, rm, rv,
+                                 self.bn_momentum, pool=False, act=F.ACT_NONE)
+            in_saved = (raw, coeffs)
+        feat = h.reshape(B, self.feat_dim)
+        fc_in = [feat]
+        z = feat
+        for (name, di, do, _) in self.fcs:
+            z = S.linear(z, fl.w(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
+            fc_in.append(z)
+        logits = S.linear(z, fl.w('out.w'), fl.w('out.b'))
+        dlogits = torch.empty((B, self.ncls_p), dtype=torch.float32, device=self.device)
+        S.softmax_xent(logits, labels, self.num_classes, dlogits=dlogits, loss_sum=self.loss_sum,
+                       correct=self.correct, counted=self.seen)
+        # ---- backward
+        S.linear_dw(dlogits, fc_in[-1], out=fl.g('out.w'))
+        S.colsum(dlogits, fl.g('out.b'))
+        d, wname = dlogits, 'out'
+        for k in range(len(self.fcs) - 1, -1, -1):
+            name = self.fcs[k][0]
+            d = S.linear_dx(d, fl.w(wname + '.w'), gate=fc_in[k + 1])
+            S.linear_dw(d, fc_in[k], out=fl.g(name + '.w'))
+            S.colsum(d, fl.g(name + '.b'))
+            wname = name
+        if not self.blocks and not self.input_bn:
+            return
+        d = S.linear_dx(d, fl.w(wname + '.w'))
+        if self.input_bn:
+            raw, coeffs = in_saved
+            S.bn_bwd(d.view(B, 1, 1, self.feat_dim), raw, coeffs, fl.w('in_bn.gamma'), accs[-1][1], pool=False,
+                     act=F.ACT_NONE, dgamma=fl.g('in_bn.gamma'), dbeta=fl.g('in_bn.beta'))
+            return
+        d = d.view(B, self.feat_hw, self.feat_hw, -1)
+        wt = self._conv_wt()
+        if wt is not None:
+            wt.refresh()  # one launch: flipped/transposed fp32 weights of every dgrad layer
+        reduced = False
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            name, cin, cout, pool, hw = self.blocks[bi]
+            y, coeffs = saved[bi]
+            dy = S.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), accs[bi][1], pool=pool, act=F.ACT_RELU,
+                          dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'), reduced=reduced)
+            S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
+            if bi == 0:
+                break
+            py, pco = saved[bi - 1]
+            pname, pcin, pcout, ppool, phw = self.blocks[bi - 1]
+            if not ppool:
+                # the input block is BN+ReLU: its mask and BN-backward sums ride in this dgrad's epilogue
+                d = S.conv_dgrad(dy, wt.view(bi - 1), bnb=(py, pco, accs[bi - 1][1]))
+                reduced = True
+            elif phw == 2 * hw and not (hw & (hw - 1)):
+                # BN+ReLU+max-pool input (even power-of-two geometry): pool routing + sums in the epilogue
+                d = S.conv_dgrad(dy, wt.view(bi - 1), bnp=(py, pco, accs[bi - 1][1]))
+                reduced = True
+            else:
+                d = S.conv_dgrad(dy, wt.view(bi - 1))
+                reduced = False
+
     def _conv_wt(self):
         """ConvWT over the weights of blocks 1.. (block 0 has no data gradient), built once."""
         wt = getattr(self, '_wt', None)
+        if wt is None and len(self.blocks) > 1 and self.f32:
+            fl = self.flat
+            wt = self._wt = S.SConvWT(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]])
         if wt is None and len(self.blocks) > 1:
             fl = self.flat
             ws = [fl.wb(b[0] + '.w') for b in self.blocks[1:]]
@@ -343,18 +456,21 @@ class ConvNetEngine:
         return wt
 
     def _use_bn_acc(self) -> bool:
+        if self.f32:
+            return True
         return F.BN_ATOMIC and all(b[2] <= 1024 and b[2] % 8 == 0 for b in self.blocks)
 
     def _bn_accumulators(self):
-        """Per conv block: (forward, backward) fp64 slot tables [SL][2][C], views of one flat
-        buffer so a single memset per step zeroes them all."""
+        """Per conv block (and, fp32 path, the input BN): (forward, backward) fp64 slot tables
+        [SL][2][C], views of one flat buffer so a single memset per step zeroes them all."""
         accs = getattr(self, '_bn_accs', None)
         if accs is None:
-            sizes = [F.bn_slots(b[2]) * 2 * b[2] for b in self.blocks]
+            chans = [b[2] for b in self.blocks] + ([self.feat_dim] if self.input_bn and self.f32 else [])
+            sizes = [F.bn_slots(c) * 2 * c for c in chans]
             flat = torch.zeros(2 * sum(sizes), dtype=torch.float64, device=self.device)
             accs, off = [], 0
-            for b, n in zip(self.blocks, sizes):
-                shape = (F.bn_slots(b[2]), 2, b[2])
+            for c, n in zip(chans, sizes):
+                shape = (F.bn_slots(c), 2, c)
                 accs.append((flat[off:off + n].view(shape), flat[off + n:off + 2 * n].view(shape)))
                 off += 2 * n
             self._bn_acc_flat, self._bn_accs = flat, accs
@@ -372,11 +488,15 @@ class ConvNetEngine:
         P = params if params is not None else {n: fl.w(n) for n in fl.names()}
         rnd = _bf16_storage if emulate_bf16 else (lambda t: t)
         rndw = (lambda t: t + (t.bfloat16().float() - t).detach()) if emulate_bf16 else (lambda t: t)
-        h = x_nhwc.float().permute(0, 3, 1, 2) if x_nhwc.dim() == 4 else x_nhwc.float()
+        # fp64 inputs keep fp64 (the fp32 kernels' numerics oracle); everything else runs in fp32
+        up = (lambda t: t) if x_nhwc.dtype == torch.float64 else (lambda t: t.float())
+        h = up(x_nhwc).permute(0, 3, 1, 2) if x_nhwc.dim() == 4 else up(x_nhwc)
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             w = rndw(P[name + '.w']).permute(0, 3, 1, 2)
             h = rnd(TF.conv2d(h, w, padding=1))
             rm, rv = self.running_stats(bi)
+            if not update_running:
+                rm, rv = rm.to(h), rv.to(h)
             if training:
                 h = TF.batch_norm(h, rm if update_running else None, rv if update_running else None,
                                   P[name + '.gamma'], P[name + '.beta'], training=True,
@@ -389,9 +509,11 @@ class ConvNetEngine:
                 h = TF.max_pool2d(h, 2)
             h = rnd(h)
         if self.flat_input:
-            h = x_nhwc.float().reshape(x_nhwc.shape[0], -1)
+            h = up(x_nhwc).reshape(x_nhwc.shape[0], -1)
             if self.input_bn:
                 rm, rv = self.running_stats('in')
+                if not update_running:
+                    rm, rv = rm.to(h), rv.to(h)
                 if training:
                     h = TF.batch_norm(h, rm if update_running else None, rv if update_running else None,
                                       P['in_bn.gamma'], P['in_bn.beta'], training=True, momentum=self.bn_momentum,
@@ -442,7 +564,7 @@ class ConvNetEngine:
         """Capture one training step on static input buffers into a hipGraph."""
         if self.device.type != 'cuda':
             return None
-        self._static_x = torch.zeros(self.input_shape(batch_size), dtype=torch.bfloat16, device=self.device)
+        self._static_x = torch.zeros(self.input_shape(batch_size), dtype=self.act_dtype, device=self.device)
         self._static_y = torch.zeros((batch_size,), dtype=torch.int32, device=self.device)
         # warm the allocator / library outside capture; these steps use zero inputs and are
         # undone by restoring the parameter state afterwards.
@@ -476,7 +598,7 @@ class ConvNetEngine:
         self._data, self._labels = data, labels
         self._sched = torch.zeros((max_steps, batch_size), dtype=torch.int64, device=self.device)
         self._ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self._static_x = torch.zeros(self.input_shape(batch_size), dtype=torch.bfloat16, device=self.device)
+        self._static_x = torch.zeros(self.input_shape(batch_size), dtype=self.act_dtype, device=self.device)
         self._static_y = torch.zeros((batch_size,), dtype=torch.int32, device=self.device)
 
         self._done = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -572,11 +694,12 @@ class ConvNetEngine:
             out[..., :x.shape[-1]] = x
             return out
         t = t.to(self.device, non_blocking=True)
+        pack = S.pack_nhwc if self.f32 else F.pack_nhwc
         if self.flat_input:
             nchw = t.reshape(N, -1, 1, 1)
-            return F.pack_nhwc(nchw.contiguous(), self.feat_dim, scale, shift).view(N, self.feat_dim)
+            return pack(nchw.contiguous(), self.feat_dim, scale, shift).view(N, self.feat_dim)
         nchw = t.permute(0, 3, 1, 2).contiguous()
-        return F.pack_nhwc(nchw, self.cin_p, scale, shift)
+        return pack(nchw, self.cin_p, scale, shift)
 
     # ------------------------------------------------------------------------------ inference
     def prepare_eval(self):
@@ -600,7 +723,28 @@ class ConvNetEngine:
         return coeffs
 
     @torch.no_grad()
+    def _forward_eval_gpu_f32(self, x, out_probs):
+        fl = self.flat
+        h = x
+        B = x.shape[0]
+        for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            y = S.conv_fwd(h, fl.w(name + '.w'))
+            c = self._eval_coeffs[bi]
+            h = S.bn_eval(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
+        if self.input_bn:
+            c = self._eval_coeffs[-1]
+            h = S.bn_eval(h.reshape(B, 1, 1, self.feat_dim), c[2], c[3], pool=False, act=F.ACT_NONE)
+        z = h.reshape(B, self.feat_dim)
+        for (name, di, do, _) in self.fcs:
+            z = S.linear(z, fl.w(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
+        logits = S.linear(z, fl.w('out.w'), fl.w('out.b'))
+        S.softmax_xent(logits, None, self.num_classes, probs=out_probs)
+        return out_probs
+
+    @torch.no_grad()
     def _forward_eval_gpu(self, x, out_probs):
+        if self.f32:
+            return self._forward_eval_gpu_f32(x, out_probs)
         fl = self.flat
         h = x
         B = x.shape[0]
@@ -649,7 +793,7 @@ class ConvNetEngine:
             return torch.cat(outs)
         ent = self._eval_graphs.get(bucket)
         if ent is None:
-            sx = torch.zeros(self.input_shape(bucket), dtype=torch.bfloat16, device=self.device)
+            sx = torch.zeros(self.input_shape(bucket), dtype=self.act_dtype, device=self.device)
             so = torch.empty((bucket, self.num_classes), dtype=torch.float32, device=self.device)
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -668,7 +812,7 @@ class ConvNetEngine:
         return so[:B]
 
     def resident_bytes(self):
-        return self.flat.total * (4 + 2 + 4) + self.running.numel() * 4
+        return self.flat.total * (4 + (0 if self.f32 else 2) + 4) + self.running.numel() * 4
 
     # ---------------------------------------------------------------------------- state I/O
     def state_dict(self):

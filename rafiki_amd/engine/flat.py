@@ -1,7 +1,7 @@
 """Flat parameter arena + fused optimizers.
 
-All trainable parameters of a model live in ONE fp32 master buffer (plus a bf16 compute copy and
-an fp32 gradient buffer of the same layout).  Consequences, all deliberate for MI355X:
+All trainable parameters of a model live in ONE fp32 master buffer (plus, for the opt-in bf16
+compute path, a bf16 compute copy) and an fp32 gradient buffer of the same layout.  Consequences, all deliberate for MI355X:
   * the optimizer is one streaming kernel over the whole model (multi-tensor for free, §2.4 K9),
     and it writes the bf16 copy the next forward reads — no separate cast pass;
   * data-parallel gradient all-reduce is a handful of large contiguous RCCL buckets over the flat
@@ -69,9 +69,10 @@ def init_kaiming(fan_in, gain=math.sqrt(2.0), zero_in_slice=None):
 
 
 class FlatParams:
-    def __init__(self, device, seed: int = 0):
+    def __init__(self, device, seed: int = 0, compute_bf16: bool = True):
         self.device = torch.device(device)
         self.seed = seed
+        self.compute_bf16 = bool(compute_bf16)  # fp32 engines read the master weights directly
         self.specs: List[ParamSpec] = []
         self._by_name: Dict[str, ParamSpec] = {}
         self.master = self.bf16 = self.grad = None
@@ -104,7 +105,7 @@ class FlatParams:
             s.init(t, g)
             host[s.offset:s.offset + s.numel] = t.reshape(-1)
         self.master.copy_(host)
-        self.bf16 = self.master.to(torch.bfloat16)
+        self.bf16 = self.master.to(torch.bfloat16) if self.compute_bf16 else None
         return self
 
     # views
@@ -116,6 +117,8 @@ class FlatParams:
         return self._view(self.master, name)
 
     def wb(self, name):
+        if self.bf16 is None:
+            raise RuntimeError('fp32 arena has no bf16 compute copy')
         return self._view(self.bf16, name)
 
     def g(self, name):
@@ -145,7 +148,8 @@ class FlatParams:
         return sum(s.numel for s in self.specs)
 
     def sync_bf16(self):
-        self.bf16.copy_(self.master)
+        if self.bf16 is not None:
+            self.bf16.copy_(self.master)
 
     def state_dict(self):
         """{name: float32 numpy array} — picklable, device-independent."""
@@ -219,7 +223,8 @@ class FlatAdam:
             F.add_int_(self.t, 1)
             for a, b, wd, mult in segs:
                 if b > a:
-                    F.adam_step(f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b], wb=f.bf16[a:b],
+                    F.adam_step(f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b],
+                                wb=None if f.bf16 is None else f.bf16[a:b],
                                 lr=self.lr * mult, beta1=self.b1, beta2=self.b2, eps=self.eps * mult,
                                 weight_decay=wd, decoupled=self.decoupled, step_tensor=self.t,
                                 skip_flag=self.skip_flag)

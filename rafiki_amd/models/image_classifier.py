@@ -17,7 +17,7 @@ import time
 import numpy as np
 import torch
 
-from ..engine.convnet import ConvNetEngine
+from ..engine.convnet import ConvNetEngine, default_dtype
 from ..model import BaseModel, dataset_utils, logger
 from ..parallel.context import current as trial_context
 from ..utils import faults
@@ -51,11 +51,14 @@ class NativeImageClassifier(BaseModel):
             images = dataset_utils.resize_as_images(images, self.image_size)
         return images, labels, ds.classes
 
-    def _build(self, num_classes, channels):
+    def _build(self, num_classes, channels, dtype=None):
         kw = self._engine_kwargs(num_classes, channels, self.image_size)
+        # compute dtype: fp32 (reference precision) unless the trial / RAFIKI_DTYPE opts into bf16
+        kw.setdefault('dtype', dtype or self._knobs.get('dtype') or default_dtype())
         self._engine = ConvNetEngine(num_classes=num_classes, in_channels=channels, image_size=self.image_size,
                                      device=self.device, seed=int(self._knobs.get('seed', 0)), **kw)
-        self._meta = {'num_classes': num_classes, 'channels': channels, 'image_size': self.image_size}
+        self._meta = {'num_classes': num_classes, 'channels': channels, 'image_size': self.image_size,
+                      'dtype': self._engine.dtype}
 
     # ------------------------------------------------------------------------ BaseModel API
     def train(self, dataset_uri):
@@ -208,7 +211,7 @@ class NativeImageClassifier(BaseModel):
 
     def load_parameters(self, params):
         meta = params['meta']
-        self._build(meta['num_classes'], meta['channels'])
+        self._build(meta['num_classes'], meta['channels'], dtype=meta.get('dtype', 'bf16'))
         self._engine.load_state_dict(params['state'])
         self._engine.prepare_eval()
 

@@ -61,6 +61,18 @@ _SIGS = {
     "rk_colsum_part": [vp, i32, i32, i32, i32, vp, vp],
     "rk_lstm_fwd": [vp, vp, i32, i32, i32, vp, vp, vp, vp],
     "rk_lstm_bwd": [vp, i32, i32, i32, vp, vp, vp, vp, vp],
+    # fp32 path (sgemm.hip, bnf.hip)
+    "rk_sgemm": [i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                 i64, i32, f32, f32, i64, i64, vp],
+    "rk_bnf_fwd": [vp, vp, i32, f64, vp, vp, f32, vp, vp, f32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_bnf_bwd_reduce": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_bnf_bwd_apply": [vp, vp, vp, vp, i32, f64, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp],
+    "rk_bnf_colstats": [vp, vp, i32, i32, vp, vp],
+    "rk_swt": [vp, vp, vp, i32, vp, vp],
+    "rk_colsum_f32": [vp, i32, i32, i32, vp, i32, vp],
+    "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, vp],
+    "rk_pack_nhwc_f32": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
+    "rk_softmax_xent_f32": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],
 }
 
 _OPTIONAL: set[str] = set()

@@ -1,0 +1,410 @@
+"""fp32 tensor ops over the gfx950 kernels (``csrc/kernels/sgemm.hip`` + ``bnf.hip``) — the
+reference-precision training path.  Every GEMM runs on v_mfma_f32_32x32x2_f32 (exact fp32 products,
+fp32 accumulation); activations, gradients and BatchNorm are fp32.  The reference trains in fp32
+everywhere (pg_gans.py:830,914; Keras defaults in TfFeedForward.py / TfVgg16.py).
+
+Layouts (all device tensors contiguous):
+  * activations  : NHWC fp32 ``[N, H, W, C]`` with C % 4 == 0 (the stem pads RGB to 4 channels)
+  * conv weights : fp32 ``[Cout, kh, kw, Cin]`` (GEMM B operand ``[N][K]``, K = taps*Cin)
+  * dense weights: fp32 ``[out, in]``
+
+Every function launches on the current HIP stream and allocates only through the torch caching
+allocator, so whole steps capture into one hipGraph.  Tile shape / LDS-ring depth / split-K are
+picked per layer shape by the autotuner (``rafiki_amd.ops.autotune``) outside capture.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from . import _lib, autotune
+from .functional import ACT_LRELU, ACT_NONE, ACT_RELU, bn_slots, cdiv  # noqa: F401
+
+KIND_CONV, KIND_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW = 0, 2, 3, 4, 5
+F_RELU, F_BIAS, F_STATS, F_GATE, F_ACCUM, F_LRELU, F_BNB, F_BNP = 1, 2, 4, 8, 16, 32, 512, 1024
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
+NUM_CU = 256
+# RAFIKI_SGEMM_CFG="tile,nst" pins every sgemm launch (A/B runs without the tuner)
+_PIN = tuple(int(v) for v in os.environ['RAFIKI_SGEMM_CFG'].split(',')) if os.environ.get('RAFIKI_SGEMM_CFG') else None
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _nbytes(t):
+    return t.untyped_storage().nbytes() - t.storage_offset() * t.element_size()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(t, name):
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise ValueError('{}: contiguous fp32 tensor required (got {} contiguous={})'.format(
+            name, t.dtype, t.is_contiguous()))
+
+
+def sgemm(kind, A, B, out, M, N, K, lda, ldb, ldc, *, tile=0, nst=2, splits=1, slab_stride=0, bias=None,
+          stats=None, gate=None, H=1, W=1, C=4, taps=1, flags=0, alpha=1.0, slope=0.2):
+    slot_mask = 0
+    if stats is not None:
+        assert stats.dtype == torch.float64 and stats.is_contiguous()
+        slot_mask = stats.shape[0] - 1
+    _lib.call("rk_sgemm", int(kind), int(tile), int(nst), _p(A), _p(B), _p(out), _p(bias), _p(stats), int(slot_mask),
+              _p(gate), int(M), int(N), int(K), int(lda), int(ldb), int(ldc), int(H), int(W), int(C), int(taps),
+              int(splits), int(slab_stride), int(flags), float(alpha), float(slope), _nbytes(A), _nbytes(B), _s())
+    return out
+
+
+# ------------------------------------------------------------------------------ config selection
+def pick_tile(M: int, N: int) -> int:
+    """Largest tile that still puts >= one block on every CU (else the tile with most blocks)."""
+    best, best_blocks = 3, -1
+    for t, (bm, bn) in enumerate(TILES):
+        blocks = cdiv(M, bm) * cdiv(N, bn)
+        waste = (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N)
+        if waste > 1.3 and t != 3:
+            continue
+        if blocks >= NUM_CU:
+            return t
+        if blocks > best_blocks:
+            best, best_blocks = t, blocks
+    return best
+
+
+def _cands(M, N, splittable=False, K=0):
+    """(tile, nst, splits) configs: the heuristic first, then every tile x ring depth, plus split-K
+    variants for grids that leave the chip idle."""
+    t0 = pick_tile(M, N)
+    out = [(t0, 2, 1)]
+    for t in range(4):
+        for nst in (2, 3):
+            c = (t, nst, 1)
+            if c not in out:
+                out.append(c)
+    if splittable:
+        kt = cdiv(K, 32)
+        for t in range(4):
+            blocks = cdiv(M, TILES[t][0]) * cdiv(N, TILES[t][1])
+            for s in (2, 4, 8, 16, 32, 64, 128, 256):
+                if s > kt // 2 or blocks * s > 8 * NUM_CU or s * M * N * 4 > (512 << 20):
+                    continue
+                if blocks * s < NUM_CU // 2:
+                    continue
+                s_eff = cdiv(kt, cdiv(kt, s))
+                for nst in (2, 3):
+                    c = (t, nst, s_eff)
+                    if c not in out:
+                        out.append(c)
+    return out
+
+
+def _pick(key, cands, run):
+    if _PIN is not None:
+        return (_PIN[0], _PIN[1], cands[0][2])
+    if not autotune.ENABLED:
+        return cands[0]
+    return autotune.tune(key, cands, run)
+
+
+def _slots_flags(acc):
+    return 0 if acc is None else acc.shape[0] - 1
+
+
+# ------------------------------------------------------------------------------------------ conv
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None, bias=None, act=ACT_NONE,
+             slope=0.2, out=None):
+    """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
+    [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue."""
+    _check(x, 'conv_fwd x')
+    Nb, H, W, Cin = x.shape
+    Cout = w.shape[0]
+    M, K = Nb * H * W, taps * Cin
+    assert w.numel() == Cout * K, (w.shape, taps, Cin)
+    if out is None:
+        out = torch.empty((Nb, H, W, Cout), device=x.device, dtype=torch.float32)
+    flags = (F_STATS if stats_acc is not None else 0) | (F_BIAS if bias is not None else 0)
+    flags |= F_RELU if act == ACT_RELU else F_LRELU if act == ACT_LRELU else 0
+
+    def run(cfg):
+        sgemm(KIND_CONV, x, w, out, M, Cout, K, Cin, K, Cout, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats_acc,
+              H=H, W=W, C=Cin, taps=taps, flags=flags, slope=slope)
+    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags), _cands(M, Cout), run)
+    if stats_acc is not None and autotune.can_tune():
+        stats_acc.zero_()  # tuning runs accumulated into it
+    run(cfg)
+    return out
+
+
+def conv_dgrad(dy: torch.Tensor, wt: torch.Tensor, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None):
+    """dx = data gradient of a 3x3 conv as conv3x3(dy, wt) with wt = SConvWT.view() [Cin][taps*Cout].
+    Epilogue options: ``gate`` (ReLU mask of the input activation), ``bnb = (y, coeffs, acc)`` (the input
+    is BN+ReLU(y): mask + BN-backward sums into acc), ``bnp = (y, coeffs, acc)`` (the input is
+    maxpool(BN+ReLU(y)), y at 2x resolution: routing + sums; dx stays the pooled gradient)."""
+    _check(dy, 'conv_dgrad dy')
+    Nb, H, W, Cout = dy.shape
+    Cin = wt.shape[0]
+    M, K = Nb * H * W, taps * Cout
+    assert wt.numel() == Cin * K
+    if out is None:
+        out = torch.empty((Nb, H, W, Cin), device=dy.device, dtype=torch.float32)
+    flags, bias, stats = 0, None, None
+    if bnb is not None:
+        y, coeffs, stats = bnb
+        assert y.shape == out.shape and stats.dtype == torch.float64 and stats.shape[-1] == Cin
+        gate, bias, flags = y, coeffs[2:4].reshape(-1), F_BNB
+    elif bnp is not None:
+        y, coeffs, stats = bnp
+        assert y.shape == (Nb, 2 * H, 2 * W, Cin) and stats.dtype == torch.float64
+        assert not (H & (H - 1)) and not (W & (W - 1)), 'pooled BN fusion needs power-of-two maps'
+        gate, bias, flags = y, coeffs[2:4].reshape(-1), F_BNP
+    elif gate is not None:
+        flags = F_GATE
+
+    def run(cfg):
+        sgemm(KIND_CONV, dy, wt, out, M, Cin, K, Cout, K, Cin, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats,
+              gate=gate, H=H, W=W, C=Cout, taps=taps, flags=flags)
+    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags), _cands(M, Cin), run)
+    if stats is not None and autotune.can_tune():
+        stats.zero_()
+    run(cfg)
+    return out
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, accumulate=False):
+    """dW[co][tap][ci] (fp32 [Cout][taps*Cin]) = sum over pixels of dy[p][co] * x[shift_tap(p)][ci]."""
+    _check(dy, 'conv_wgrad dy')
+    _check(x, 'conv_wgrad x')
+    Nb, H, W, Cout = dy.shape
+    Cin = x.shape[-1]
+    M, N, K = Cout, taps * Cin, Nb * H * W
+    if out is None:
+        out = torch.empty((Cout, N), device=dy.device, dtype=torch.float32)
+
+    def run(cfg):
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm(KIND_WGRAD, dy, x, out, M, N, K, Cout, Cin, N, tile=tile, nst=nst, H=H, W=W, C=Cin, taps=taps,
+                  flags=F_ACCUM if accumulate else 0)
+            return
+        slab = torch.empty((s, M, N), device=dy.device, dtype=torch.float32)
+        sgemm(KIND_WGRAD, dy, x, slab, M, N, K, Cout, Cin, N, tile=tile, nst=nst, splits=s, slab_stride=M * N,
+              H=H, W=W, C=Cin, taps=taps)
+        reduce_slabs(slab, out, accumulate=accumulate)
+    cands = _cands(M, N, splittable=True, K=K)
+    # the split-K configs fill the chip: lead with the best-filling heuristic one
+    split = [c for c in cands if c[2] > 1]
+    if split:
+        cands = [max(split, key=lambda c: min(cdiv(M, TILES[c[0]][0]) * cdiv(N, TILES[c[0]][1]) * c[2],
+                                              2 * NUM_CU))] + cands
+    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate)), cands, run)
+    run(cfg)
+    return out
+
+
+class SConvWT:
+    """Flipped, transposed fp32 copies wt[ci][taps-1-t][co] = w[co][t][ci] of several conv weights living
+    in one fp32 arena, refreshed by ONE rk_swt launch per step; with them the data gradient is a forward
+    conv of dy on the forward kernels (``conv_dgrad``)."""
+
+    def __init__(self, arena: torch.Tensor, weights, taps: int = 9):
+        self.arena = arena
+        meta, desc, self._views, off = [], [], [], 0
+        for l, w in enumerate(weights):
+            Cout = w.shape[0]
+            Cin = w.numel() // (taps * Cout)
+            so = (w.data_ptr() - arena.data_ptr()) // 4
+            meta.append([so, off, Cout, Cin, taps])
+            for t in range(taps):
+                for co0 in range(0, Cout, 32):
+                    for ci0 in range(0, Cin, 32):
+                        desc.append([l, t, co0, ci0])
+            self._views.append((off, Cin, Cout))
+            off += (Cin * taps * Cout + 63) // 64 * 64
+        dev = arena.device
+        self.taps = taps
+        self.buf = torch.zeros(max(off, 64), dtype=torch.float32, device=dev)
+        self.meta = torch.tensor(meta, dtype=torch.int64, device=dev)
+        self.desc = torch.tensor(desc, dtype=torch.int32, device=dev)
+
+    def refresh(self):
+        _lib.call("rk_swt", _p(self.arena), _p(self.buf), _p(self.desc), self.desc.shape[0], _p(self.meta), _s())
+
+    def view(self, l: int) -> torch.Tensor:
+        off, Cin, Cout = self._views[l]
+        return self.buf[off:off + Cin * self.taps * Cout].view(Cin, self.taps * Cout)
+
+
+# ----------------------------------------------------------------------------------------- dense
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0.2, out=None, alpha=1.0):
+    """out = act(alpha * x @ w.T + bias), fp32; small-M layers autotune split-K + a fused combine."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), device=x.device, dtype=torch.float32)
+    flags = (F_BIAS if bias is not None else 0) | (F_RELU if act == ACT_RELU else F_LRELU if act == ACT_LRELU else 0)
+
+    def run(cfg):
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm(KIND_DENSE, x, w, out, M, N, K, x.stride(0), w.stride(0), out.stride(0), tile=tile, nst=nst,
+                  bias=bias, flags=flags, slope=slope, alpha=alpha)
+            return
+        slab = torch.empty((s, M, N), device=x.device, dtype=torch.float32)
+        sgemm(KIND_DENSE, x, w, slab, M, N, K, x.stride(0), w.stride(0), N, tile=tile, nst=nst, splits=s,
+              slab_stride=M * N)
+        sreduce_epi(slab, M, N, out, bias=bias, act=act, slope=slope, alpha=alpha)
+    cands = _cands(M, N, splittable=N % 4 == 0 and out.stride(0) % 4 == 0, K=K)
+    run(_pick(('sl', M, N, K, act, bias is not None, float(alpha)), cands, run))
+    return out
+
+
+def linear_dx(dy: torch.Tensor, w: torch.Tensor, *, gate=None, out=None):
+    """dx[M][in] = dy[M][out] @ w[out][in], optionally gated (dx = 0 where gate <= 0)."""
+    M, Nout = dy.shape
+    Nin = w.shape[1]
+    if out is None:
+        out = torch.empty((M, Nin), device=dy.device, dtype=torch.float32)
+
+    def run(cfg):
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm(KIND_DENSE_DX, dy, w, out, M, Nin, Nout, dy.stride(0), w.stride(0), out.stride(0), tile=tile,
+                  nst=nst, gate=gate, flags=F_GATE if gate is not None else 0)
+            return
+        slab = torch.empty((s, M, Nin), device=dy.device, dtype=torch.float32)
+        sgemm(KIND_DENSE_DX, dy, w, slab, M, Nin, Nout, dy.stride(0), w.stride(0), Nin, tile=tile, nst=nst,
+              splits=s, slab_stride=M * Nin)
+        sreduce_epi(slab, M, Nin, out, gate=gate)
+    cands = _cands(M, Nin, splittable=Nin % 4 == 0, K=Nout)
+    run(_pick(('sx', M, Nin, Nout, gate is not None), cands, run))
+    return out
+
+
+def linear_dw(dy: torch.Tensor, x: torch.Tensor, *, out=None, accumulate=False):
+    """dw[out][in] = dy[M][out]^T @ x[M][in] (fp32)."""
+    M, Nout = dy.shape
+    Nin = x.shape[1]
+    if out is None:
+        out = torch.empty((Nout, Nin), device=dy.device, dtype=torch.float32)
+
+    def run(cfg):
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm(KIND_DENSE_DW, dy, x, out, Nout, Nin, M, dy.stride(0), x.stride(0), Nin, tile=tile, nst=nst,
+                  flags=F_ACCUM if accumulate else 0)
+            return
+        slab = torch.empty((s, Nout, Nin), device=dy.device, dtype=torch.float32)
+        sgemm(KIND_DENSE_DW, dy, x, slab, Nout, Nin, M, dy.stride(0), x.stride(0), Nin, tile=tile, nst=nst,
+              splits=s, slab_stride=Nout * Nin)
+        reduce_slabs(slab, out, accumulate=accumulate)
+    cands = _cands(Nout, Nin, splittable=True, K=M)
+    run(_pick(('sdw', M, Nout, Nin, bool(accumulate)), cands, run))
+    return out
+
+
+def sreduce_epi(slab, M, N, out, *, bias=None, act=ACT_NONE, slope=0.2, alpha=1.0, gate=None):
+    _lib.call("rk_sreduce_epi", _p(slab), slab.shape[0], int(M), int(N), _p(bias), int(act), float(slope),
+              float(alpha), _p(gate), 0 if gate is None else gate.stride(0), _p(out), out.stride(0), _s())
+    return out
+
+
+def reduce_slabs(slab, out, *, accumulate=False, scale=1.0):
+    from .functional import reduce_slabs as _rs
+    return _rs(slab, out, accumulate=accumulate, scale=scale)
+
+
+def colsum(x2d, out, *, accumulate=False):
+    R, Cc = x2d.shape
+    _lib.call("rk_colsum_f32", _p(x2d), R, Cc, x2d.stride(0), _p(out), int(accumulate), _s())
+    return out
+
+
+# -------------------------------------------------------------------------------------- batchnorm
+def bn_fwd(y, acc, count, gamma, beta, eps, running_mean=None, running_var=None, momentum=0.1, *, pool=False,
+           act=ACT_RELU, slope=0.2, coeffs=None, out=None):
+    """Train-mode BN (+act, +2x2 max-pool) from the fp64 slot sums ``acc`` [SL][2][C]; writes coeffs
+    [4][C] = mean, rstd, scale, shift (for backward).  Returns (out, coeffs)."""
+    Nb, H, W, C = y.shape
+    if coeffs is None:
+        coeffs = torch.empty((4, C), device=y.device, dtype=torch.float32)
+    if out is None:
+        shape = (Nb, H // 2, W // 2, C) if pool else (Nb, H, W, C)
+        out = torch.empty(shape, device=y.device, dtype=torch.float32)
+    _lib.call("rk_bnf_fwd", _p(y), _p(acc), acc.shape[0], float(count), _p(gamma), _p(beta), float(eps),
+              _p(running_mean), _p(running_var), float(momentum), None, None, _p(coeffs), _p(out), Nb, H, W, C,
+              int(pool), int(act), float(slope), _s())
+    return out, coeffs
+
+
+def bn_eval(y, scale, shift, *, pool=False, act=ACT_RELU, slope=0.2, out=None):
+    Nb, H, W, C = y.shape
+    if out is None:
+        shape = (Nb, H // 2, W // 2, C) if pool else (Nb, H, W, C)
+        out = torch.empty(shape, device=y.device, dtype=torch.float32)
+    _lib.call("rk_bnf_fwd", _p(y), None, 0, 1.0, None, None, 0.0, None, None, 0.0, _p(scale), _p(shift), None, _p(out),
+              Nb, H, W, C, int(pool), int(act), float(slope), _s())
+    return out
+
+
+def col_stats(a2d, acc, b2d=None):
+    """fp64 slot 0 of ``acc`` += per-column (sum a, sum a*b) (b = a when None)."""
+    R, C = a2d.shape
+    _lib.call("rk_bnf_colstats", _p(a2d), _p(b2d), R, C, _p(acc), _s())
+    return acc
+
+
+_BWD_BLOCKS = int(os.environ.get('RAFIKI_BNF_BWD_BLOCKS', '1024'))
+
+
+def bn_bwd(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, dgamma=None, dbeta=None, dy=None,
+           accumulate=False, reduced=False):
+    """Backward of out = pool?(act(BN(y))).  ``acc``: zeroed fp64 [SL][2][C] for (sum dz, sum dz*y);
+    ``reduced``: the producer of dout already accumulated them (conv_dgrad(bnb=/bnp=...))."""
+    Nb, H, W, C = y.shape
+    s = _s()
+    if not reduced:
+        if C <= 1024 and not (C & (C - 1)):
+            npix = dout.numel() // C
+            blocks = max(1, min(_BWD_BLOCKS, cdiv(npix, max(1, 256 // (C // 4)) * 8)))
+            _lib.call("rk_bnf_bwd_reduce", _p(dout), _p(y), _p(coeffs), _p(acc), acc.shape[0], blocks, Nb, H, W, C,
+                      int(pool), int(act), float(slope), s)
+        elif not pool and act == ACT_NONE:
+            col_stats(dout.reshape(-1, C), acc, y.reshape(-1, C))
+        else:
+            raise ValueError('bn_bwd: unsupported channel count {} for pool/act'.format(C))
+    if dy is None:
+        dy = torch.empty_like(y)
+    _lib.call("rk_bnf_bwd_apply", _p(dout), _p(y), _p(coeffs), _p(acc), acc.shape[0], float(Nb * H * W), _p(gamma),
+              _p(dgamma), _p(dbeta), int(accumulate), _p(dy), Nb, H, W, C, int(pool), int(act), float(slope), s)
+    return dy
+
+
+# ----------------------------------------------------------------------------------- loss / misc
+def softmax_xent(logits, labels, ncls, *, dlogits=None, probs=None, loss_sum=None, correct=None, counted=None,
+                 ignore_index=-100, grad_scale=None):
+    B = logits.shape[0]
+    if grad_scale is None:
+        grad_scale = 1.0 / max(1, B)
+    if dlogits is not None:
+        _check(dlogits, 'softmax_xent dlogits')
+    _lib.call("rk_softmax_xent_f32", _p(logits), logits.stride(0), _p(labels), B, ncls, ignore_index,
+              float(grad_scale), _p(dlogits), 0 if dlogits is None else dlogits.stride(0), _p(probs), _p(loss_sum),
+              _p(correct), _p(counted), _s())
+
+
+def pack_nhwc(images, cpad=4, scale=1.0, shift=0.0, out=None):
+    """uint8/float32 NCHW -> fp32 NHWC with channels padded to ``cpad``."""
+    Nb, Cc, H, W = images.shape
+    if out is None:
+        out = torch.empty((Nb, H, W, cpad), device=images.device, dtype=torch.float32)
+    is_u8 = 1 if images.dtype == torch.uint8 else 0
+    if not is_u8 and images.dtype != torch.float32:
+        images = images.float()
+    _lib.call("rk_pack_nhwc_f32", _p(images.contiguous()), is_u8, Nb, Cc, H, W, cpad, float(scale), float(shift),
+              _p(out), _s())
+    return out

@@ -1,4 +1,5 @@
-"""VGG-style static-graph engine on the GPU vs the PyTorch fp32 reference of the same network."""
+"""VGG-style static-graph engine on the GPU, opt-in bf16 compute path (dtype='bf16'), vs the PyTorch
+fp32 reference of the same network.  The default fp32 path is covered by tests/test_f32_gpu.py."""
 import pytest
 import torch
 
@@ -8,7 +9,7 @@ pytestmark = pytest.mark.gpu
 def _engine(**kw):
     from rafiki_amd.engine.convnet import ConvNetEngine
     args = dict(num_classes=10, in_channels=3, image_size=16, cfg=(16, 'M', 32, 32, 'M'), fc_dims=(32,),
-                device='cuda', seed=3, lr=0.05)
+                device='cuda', seed=3, lr=0.05, dtype='bf16')
     args.update(kw)
     return ConvNetEngine(**args)
 
@@ -120,7 +121,7 @@ def test_grads_match_reference_non_pow2_vgg16_layout():
 def test_vgg16_model_trains():
     import numpy as np
     from rafiki_amd.models.vgg16 import Vgg16
-    m = Vgg16(epochs=1, learning_rate=1e-3, batch_size=32)
+    m = Vgg16(epochs=1, learning_rate=1e-3, batch_size=32, dtype='bf16')
     m._knobs['epochs'] = 6
     m.train('synthetic://image?n=512&size=28&channels=1&classes=4&seed=0')
     acc = m.evaluate('synthetic://image?n=256&size=28&channels=1&classes=4&seed=1')
@@ -145,6 +146,6 @@ def test_mlp_model_learns_on_gpu():
     from rafiki_amd.models import model_file
     clazz = load_model_class(open(model_file('FeedForward'), 'rb').read(), 'FeedForward')
     m = clazz(epochs=3, hidden_layer_count=2, hidden_layer_units=64, learning_rate=0.001, batch_size=128,
-              image_size=28)
+              image_size=28, dtype='bf16')
     m.train('synthetic://image?n=3000&size=28&channels=1&classes=10&seed=0')
     assert m.evaluate('synthetic://image?n=1500&size=28&channels=1&classes=10&seed=1') > 0.9
