@@ -32,7 +32,9 @@ namespace {
 constexpr int SBK = 32;  // fp32 elements per K-tile: 128-B LDS rows
 constexpr unsigned SOOB = 0x80000000u;
 
-enum SMode { SM_KIN_DENSE = 0, SM_KIN_CONV = 1, SM_KOUT_DENSE = 2, SM_KOUT_CONV = 3 };
+// SM_KIN_CONVF: SM_KIN_CONV with C % 32 == 0, so a 32-deep K-tile never straddles a tap and the
+// tap / channel offset of every DMA is wave-uniform (~4 VALU per DMA instead of ~20)
+enum SMode { SM_KIN_DENSE = 0, SM_KIN_CONV = 1, SM_KOUT_DENSE = 2, SM_KOUT_CONV = 3, SM_KIN_CONVF = 4 };
 enum SFlags { SF_RELU = 1, SF_BIAS = 2, SF_STATS = 4, SF_GATE = 8, SF_ACCUM = 16, SF_LRELU = 32,
               SF_BNB = 512, SF_BNP = 1024 };
 
@@ -87,7 +89,7 @@ RK_DEV void s_hw(int k, int H, int W, int log2H, int log2W, float invH, float in
 // wave-instructions, T/32 per wave.
 template <int MODE, int T>
 struct SOperand {
-  static constexpr bool KIN = MODE == SM_KIN_DENSE || MODE == SM_KIN_CONV;
+  static constexpr bool KIN = MODE == SM_KIN_DENSE || MODE == SM_KIN_CONV || MODE == SM_KIN_CONVF;
   static constexpr int NQ = T / 32;
   static constexpr int RS = T / 4;  // 16-B slots per K-outer row
   __amdgpu_buffer_rsrc_t rsrc;
@@ -117,6 +119,7 @@ struct SOperand {
           int h, w;
           s_hw(gi, p.H, p.W, p.log2H, p.log2W, p.invH, p.invW, h, w);
           base[q] = (unsigned)gi * (unsigned)p.C * 4u;
+          if constexpr (MODE == SM_KIN_CONVF) base[q] += (unsigned)c * 16u;
           unsigned m = 1u;
           if (p.taps == 9) {
             m = 0u;
@@ -150,37 +153,51 @@ struct SOperand {
     }
   }
 
-  // byte offset (or SOOB) of this lane's 16-B chunk for instruction q of K-tile kt
+  // byte offset (or SOOB) of this lane's 16-B chunk for instruction q of K-tile kt.  Branch-free
+  // (selects; reciprocal decodes, exact below 2^22), so the DMA issue code is straight-line and the
+  // scheduler can interleave it with the MFMA stream.
+  // (invalid lanes get bit 31 OR'ed in: >= 2 GiB, past every descriptor's range -> zeros)
   RK_DEV unsigned offset(const SgParams& p, int q, int kt, int K, int ld) const {
     if constexpr (MODE == SM_KIN_DENSE) {
       const int k = kt * SBK + 4 * sub[q];
-      return (mask[q] && k < K) ? base[q] + (unsigned)k * 4u : SOOB;
+      const bool ok = mask[q] && k < K;
+      return (base[q] + (unsigned)k * 4u) | ((unsigned)!ok << 31);
+    } else if constexpr (MODE == SM_KIN_CONVF) {
+      const int k0 = kt * SBK;  // wave-uniform: one tap per K-tile
+      const int tap = (int)(((float)k0 + 0.5f) * p.invC);
+      const int ci0 = k0 - tap * p.C;
+      const int d = p.taps == 9 ? s_tap_dy(tap) * p.W + s_tap_dx(tap) : 0;
+      const bool ok = k0 < K && ((mask[q] >> tap) & 1u);
+      return (unsigned)((int)base[q] + (d * p.C + ci0) * 4) | ((unsigned)!ok << 31);
     } else if constexpr (MODE == SM_KIN_CONV) {
       const int k = kt * SBK + 4 * sub[q];
-      if (k >= K) return SOOB;
-      const int tap = s_cdiv(k, p);
+      const int tap = (int)(((float)k + 0.5f) * p.invC);
       const int ci = k - tap * p.C;
-      if (!((mask[q] >> tap) & 1u)) return SOOB;
       const int d = p.taps == 9 ? s_tap_dy(tap) * p.W + s_tap_dx(tap) : 0;
-      return (unsigned)((int)base[q] + (d * p.C + ci) * 4);
+      const bool ok = k < K && ((mask[q] >> tap) & 1u);
+      return (unsigned)((int)base[q] + (d * p.C + ci) * 4) | ((unsigned)!ok << 31);
     } else if constexpr (MODE == SM_KOUT_DENSE) {
       const int k = kt * SBK + sub[q];
-      return (mask[q] && k < K) ? base[q] + (unsigned)k * (unsigned)ld * 4u : SOOB;
+      const bool ok = mask[q] && k < K;
+      return (base[q] + (unsigned)k * (unsigned)ld * 4u) | ((unsigned)!ok << 31);
     } else {  // SM_KOUT_CONV: row k = pixel, column chunk = 4 channels of one tap
       const int k = kt * SBK + sub[q];
-      if (!mask[q] || k >= K) return SOOB;
-      int h, w;
-      s_hw(k, p.H, p.W, p.log2H, p.log2W, p.invH, p.invW, h, w);
-      if ((unsigned)(h + dy[q]) >= (unsigned)p.H || (unsigned)(w + dx[q]) >= (unsigned)p.W) return SOOB;
-      return (unsigned)(k + dyx[q]) * (unsigned)p.C * 4u + base[q];
+      const int qq = (int)(((float)k + 0.5f) * p.invW);
+      const int w = k - qq * p.W;
+      const int n = (int)(((float)qq + 0.5f) * p.invH);
+      const int h = qq - n * p.H;
+      const bool ok = mask[q] && k < K && (unsigned)(h + dy[q]) < (unsigned)p.H && (unsigned)(w + dx[q]) < (unsigned)p.W;
+      return ((unsigned)(k + dyx[q]) * (unsigned)p.C * 4u + base[q]) | ((unsigned)!ok << 31);
     }
   }
 
-  RK_DEV void issue(const SgParams& p, char* tile, int kt, int K, int ld, int wid) const {
+  // live = false: every lane DMAs zeros (keeps the issue code branch-free at the end of the K loop)
+  RK_DEV void issue(const SgParams& p, char* tile, int kt, int K, int ld, int wid, bool live = true) const {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       char* dst = tile + (wid * NQ + q) * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)dst, 16, (int)offset(p, q, kt, K, ld), 0, 0, 0);
+      const unsigned off = offset(p, q, kt, K, ld) | ((unsigned)!live << 31);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)dst, 16, (int)off, 0, 0, 0);
     }
   }
 
@@ -206,6 +223,23 @@ RK_DEV void s_barrier_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// Scheduling pattern of one 8-deep k-group (NMF MFMAs): one MFMA, the NR LDS reads of the next
+// group's fragments, then ND (MFMA, DMA) pairs, then the remaining MFMAs.
+template <int NMF, int NR, int ND>
+RK_DEV void s_group_sched() {
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  if constexpr (NR > 0) __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+  if constexpr (ND > 0) {
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+  }
+  if constexpr (NMF - 1 - ND > 0) __builtin_amdgcn_sched_group_barrier(0x008, NMF - 1 - ND, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 256, 0);  // leftover VALU after the MFMAs
 }
 
 // accumulator register r of a 32x32 block: row (r&3) + 8(r>>2) + 4h, column lane&31
@@ -331,26 +365,53 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const SgParams p) {
       s_wait_vmcnt<0>();
     }
     s_barrier_lds();  // every wave's DMA for tile kt is in LDS; every wave is done with tile kt-1
-    if (kt + NST - 1 < kt1) issue(kt + NST - 1, st == 0 ? NST - 1 : st - 1);
     const char* As = smem + st * SB;
     const char* Bs = As + ABYTES;
+    const bool more = kt + NST - 1 < kt1;
+    char* nxt = smem + (st == 0 ? NST - 1 : st - 1) * SB;  // stage of tile kt + NST - 1
+    // Fragments are double-buffered in registers (group g+1 is read from LDS while group g's MFMAs
+    // run) and the next tile's DMAs are spread over the first two groups' MFMAs; the schedule is
+    // pinned with sched_group_barrier (left alone, hipcc sinks the reads behind the MFMAs they should
+    // overlap and clusters the DMA issue in front of them).
+    constexpr int NMF = 4 * MI * NI;
+    constexpr int RA = A.KIN ? MI : 4 * MI, RB = B.KIN ? NI : 4 * NI;  // LDS read instructions per group
+    constexpr int DA = BM / 32, DB = BN / 32;                          // DMA instructions per wave
+    f32x4 a[2][MI], b[2][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) a[0][i] = A.frag(As, wm * (BM / 2) + i * 32, 0, lane);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) b[0][j] = B.frag(Bs, wn * (BN / 2) + j * 32, 0, lane);
 #pragma unroll
     for (int g = 0; g < SBK / 8; ++g) {
-      f32x4 a[MI], b[NI];
+      const int cur = g & 1;
+      if (g + 1 < SBK / 8) {
 #pragma unroll
-      for (int i = 0; i < MI; ++i) a[i] = A.frag(As, wm * (BM / 2) + i * 32, g, lane);
+        for (int i = 0; i < MI; ++i) a[cur ^ 1][i] = A.frag(As, wm * (BM / 2) + i * 32, g + 1, lane);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) b[j] = B.frag(Bs, wn * (BN / 2) + j * 32, g, lane);
+        for (int j = 0; j < NI; ++j) b[cur ^ 1][j] = B.frag(Bs, wn * (BN / 2) + j * 32, g + 1, lane);
+      }
+      // the reads above may not sink below this group's MFMAs (that would collapse the two fragment
+      // register sets into one and expose the LDS latency at every group boundary)
+      __builtin_amdgcn_sched_barrier(0);
+      // unconditional (zeros past the end: that stage is never read again) — no branch splits the
+      // scheduling region
+      if (g == 0) A.issue(p, nxt, kt + NST - 1, p.K, p.lda, wid, more);
+      if (g == 1) B.issue(p, nxt + ABYTES, kt + NST - 1, p.K, p.ldb, wid, more);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i][e], b[cur][j][e], acc[i][j], 0, 0, 0);
+      // group schedule: MFMAs with one DMA (and its address VALU) after each of the first few
+      if (g == 0) s_group_sched<NMF, 0, DA>();
+      else if (g == 1) s_group_sched<NMF, 0, DB>();
+      __builtin_amdgcn_sched_barrier(0);
     }
     st = st + 1 == NST ? 0 : st + 1;
   }
+  s_wait_vmcnt<0>();  // the trailing zero-DMAs land before the workgroup's LDS is released
   s_epilogue<MI, NI>(p, acc, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
 }
 
@@ -420,7 +481,9 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   hipStream_t st = (hipStream_t)stream;
   switch (kind) {
-    case 0: return s_launch_tile<SM_KIN_CONV, SM_KIN_DENSE>(tile, p, nst, splits, st);
+    case 0:
+      if (Cch % SBK == 0) return s_launch_tile<SM_KIN_CONVF, SM_KIN_DENSE>(tile, p, nst, splits, st);
+      return s_launch_tile<SM_KIN_CONV, SM_KIN_DENSE>(tile, p, nst, splits, st);
     case 2: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_CONV>(tile, p, nst, splits, st);
     case 3: return s_launch_tile<SM_KIN_DENSE, SM_KIN_DENSE>(tile, p, nst, splits, st);
     case 4: return s_launch_tile<SM_KIN_DENSE, SM_KOUT_DENSE>(tile, p, nst, splits, st);

@@ -53,38 +53,52 @@ void deadline(timespec& ts, int timeout_ms) {
   if (ts.tv_nsec >= 1000000000L) { ts.tv_sec += 1; ts.tv_nsec -= 1000000000L; }
 }
 
-int lock(Header* h) {
-  int rc = pthread_mutex_lock(&h->mu);
-  if (rc == EOWNERDEAD) {  // previous owner died mid-operation: the ring is only ever modified
-    pthread_mutex_consistent(&h->mu);  // after a full copy, so the header is still consistent
+// Copies work on local offsets; the header (tail/used/count on push, head/used/count on pop) is
+// published only after the whole frame (4-byte length + payload) is copied.  A process that dies
+// mid-copy therefore leaves the previous, consistent header; one that dies between the publishing
+// stores is caught by validate() below.
+uint64_t ring_copy_in(Queue* q, uint64_t off, const uint8_t* src, uint64_t n) {
+  const uint64_t cap = q->h->capacity;
+  const uint64_t first = n < cap - off ? n : cap - off;
+  memcpy(q->data + off, src, first);
+  if (n > first) memcpy(q->data, src + first, n - first);
+  return (off + n) % cap;
+}
+
+uint64_t ring_copy_out(Queue* q, uint64_t off, uint8_t* dst, uint64_t n) {
+  const uint64_t cap = q->h->capacity;
+  const uint64_t first = n < cap - off ? n : cap - off;
+  memcpy(dst, q->data + off, first);
+  if (n > first) memcpy(dst + first, q->data, n - first);
+  return (off + n) % cap;
+}
+
+// After EOWNERDEAD: the frames from head must account for exactly `count` messages and `used`
+// bytes, ending at tail; otherwise the header was torn by the dead owner -> drop the queue's
+// contents (lost messages time out at the caller; a corrupt ring would misframe forever).
+void validate(Queue* q) {
+  Header* h = q->h;
+  bool ok = h->head < h->capacity && h->tail < h->capacity && h->used <= h->capacity;
+  uint64_t off = h->head, bytes = 0;
+  for (uint64_t i = 0; ok && i < h->count; ++i) {
+    uint32_t n32;
+    off = ring_copy_out(q, off, (uint8_t*)&n32, 4);
+    bytes += 4 + (uint64_t)n32;
+    if (bytes > h->used) { ok = false; break; }
+    off = (off + n32) % h->capacity;
+  }
+  ok = ok && bytes == h->used && off == (h->used == h->capacity ? h->head : h->tail);
+  if (!ok) h->head = h->tail = h->used = h->count = 0;
+}
+
+int lock(Queue* q) {
+  int rc = pthread_mutex_lock(&q->h->mu);
+  if (rc == EOWNERDEAD) {
+    validate(q);
+    pthread_mutex_consistent(&q->h->mu);
     rc = 0;
   }
   return rc;
-}
-
-void ring_write(Queue* q, const uint8_t* src, uint64_t n) {
-  Header* h = q->h;
-  const uint64_t first = n < h->capacity - h->tail ? n : h->capacity - h->tail;
-  memcpy(q->data + h->tail, src, first);
-  if (n > first) memcpy(q->data, src + first, n - first);
-  h->tail = (h->tail + n) % h->capacity;
-  h->used += n;
-}
-
-void ring_read(Queue* q, uint8_t* dst, uint64_t n) {
-  Header* h = q->h;
-  const uint64_t first = n < h->capacity - h->head ? n : h->capacity - h->head;
-  memcpy(dst, q->data + h->head, first);
-  if (n > first) memcpy(dst + first, q->data, n - first);
-  h->head = (h->head + n) % h->capacity;
-  h->used -= n;
-}
-
-void ring_peek(Queue* q, uint8_t* dst, uint64_t n) {
-  Header* h = q->h;
-  const uint64_t first = n < h->capacity - h->head ? n : h->capacity - h->head;
-  memcpy(dst, q->data + h->head, first);
-  if (n > first) memcpy(dst + first, q->data, n - first);
 }
 
 }  // namespace
@@ -155,16 +169,19 @@ int rt_mq_push(void* handle, const uint8_t* data, long long len, int timeout_ms)
   if (len < 0 || len > 0xFFFFFFFFll || need > h->capacity) return -2;
   timespec ts;
   deadline(ts, timeout_ms < 0 ? 0 : timeout_ms);
-  if (lock(h) != 0) return -3;
+  if (lock(q) != 0) return -3;
   while (h->capacity - h->used < need) {
     if (timeout_ms == 0) { pthread_mutex_unlock(&h->mu); return -1; }
     const int rc = pthread_cond_timedwait(&h->not_full, &h->mu, &ts);
-    if (rc == EOWNERDEAD) pthread_mutex_consistent(&h->mu);
+    if (rc == EOWNERDEAD) { validate(q); pthread_mutex_consistent(&h->mu); }
     if (rc == ETIMEDOUT && h->capacity - h->used < need) { pthread_mutex_unlock(&h->mu); return -1; }
   }
   const uint32_t n32 = (uint32_t)len;
-  ring_write(q, (const uint8_t*)&n32, 4);
-  ring_write(q, data, (uint64_t)len);
+  uint64_t off = ring_copy_in(q, h->tail, (const uint8_t*)&n32, 4);
+  off = ring_copy_in(q, off, data, (uint64_t)len);
+  // publish the complete frame
+  h->tail = off;
+  h->used += need;
   h->count += 1;
   pthread_cond_signal(&h->not_empty);
   pthread_mutex_unlock(&h->mu);
@@ -176,21 +193,23 @@ long long rt_mq_pop(void* handle, uint8_t* buf, long long cap, int timeout_ms) {
   Header* h = q->h;
   timespec ts;
   deadline(ts, timeout_ms < 0 ? 0 : timeout_ms);
-  if (lock(h) != 0) return -3;
+  if (lock(q) != 0) return -3;
   while (h->count == 0) {
     if (timeout_ms == 0) { pthread_mutex_unlock(&h->mu); return -1; }
     const int rc = pthread_cond_timedwait(&h->not_empty, &h->mu, &ts);
-    if (rc == EOWNERDEAD) pthread_mutex_consistent(&h->mu);
+    if (rc == EOWNERDEAD) { validate(q); pthread_mutex_consistent(&h->mu); }
     if (rc == ETIMEDOUT && h->count == 0) { pthread_mutex_unlock(&h->mu); return -1; }
   }
   uint32_t n32;
-  ring_peek(q, (uint8_t*)&n32, 4);
+  uint64_t off = ring_copy_out(q, h->head, (uint8_t*)&n32, 4);
   if ((long long)n32 > cap) {  // leave the message queued; tell the caller the size it needs
     pthread_mutex_unlock(&h->mu);
     return -(long long)n32 - 16;
   }
-  ring_read(q, (uint8_t*)&n32, 4);
-  ring_read(q, buf, n32);
+  off = ring_copy_out(q, off, buf, n32);
+  // publish the consumed frame
+  h->head = off;
+  h->used -= 4 + (uint64_t)n32;
   h->count -= 1;
   pthread_cond_signal(&h->not_full);
   pthread_mutex_unlock(&h->mu);
@@ -199,7 +218,7 @@ long long rt_mq_pop(void* handle, uint8_t* buf, long long cap, int timeout_ms) {
 
 long long rt_mq_size(void* handle) {
   Queue* q = (Queue*)handle;
-  if (lock(q->h) != 0) return -3;
+  if (lock(q) != 0) return -3;
   const long long n = (long long)q->h->count;
   pthread_mutex_unlock(&q->h->mu);
   return n;

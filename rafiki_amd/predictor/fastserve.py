@@ -26,7 +26,8 @@ import numpy as np
 logger = logging.getLogger(__name__)
 
 _REASON = {200: b'OK', 400: b'Bad Request', 404: b'Not Found', 405: b'Method Not Allowed',
-           500: b'Internal Server Error'}
+           413: b'Payload Too Large', 500: b'Internal Server Error'}
+MAX_BODY = 256 << 20  # request bodies above this are refused (413) before any byte is buffered
 
 
 class FastPredictorServer:
@@ -140,22 +141,36 @@ class FastPredictorServer:
                     break
                 method, target, version = parts[0], parts[1], parts[2]
                 path = target.split(b'?', 1)[0].decode('latin-1')
-                clen, keep = 0, version == b'HTTP/1.1'
+                clen, keep, bad = 0, version == b'HTTP/1.1', None
                 for ln in lines[1:]:
                     k, _, v = ln.partition(b':')
                     k = k.strip().lower()
                     if k == b'content-length':
-                        clen = int(v.strip() or 0)
+                        v = v.strip()
+                        if not v.isdigit():
+                            bad = (400, b'bad Content-Length')
+                        else:
+                            clen = int(v)
+                            if clen > MAX_BODY:
+                                bad = (413, b'request body too large')
                     elif k == b'connection':
                         v = v.strip().lower()
                         keep = v == b'keep-alive' or (keep and v != b'close')
+                if bad is not None:  # answer and drop the connection: the body is never read
+                    self.counters['errors'] += 1
+                    writer.write(b'HTTP/1.1 %d %s\r\nContent-Type: text/plain\r\nContent-Length: %d\r\n'
+                                 b'Connection: close\r\n\r\n' % (bad[0], _REASON[bad[0]], len(bad[1])) + bad[1])
+                    await writer.drain()
+                    break
                 body = await reader.readexactly(clen) if clen else b''
                 self.counters['requests'] += 1
                 try:
                     status, ctype, payload = await self._route(method, path, body)
-                except Exception:
+                except Exception as e:
+                    # the traceback stays in the server log; the client gets the error type + message
                     self.counters['errors'] += 1
-                    status, ctype, payload = 500, b'text/plain', traceback.format_exc().encode()
+                    logger.error('predictor request failed:\n%s', traceback.format_exc())
+                    status, ctype, payload = 500, b'text/plain', '{}: {}'.format(type(e).__name__, e).encode()
                 writer.write(b'HTTP/1.1 %d %s\r\nContent-Type: %s\r\nContent-Length: %d\r\n%s\r\n' % (
                     status, _REASON.get(status, b'OK'), ctype, len(payload),
                     b'' if keep else b'Connection: close\r\n') + payload)
@@ -200,9 +215,11 @@ class FastPredictorServer:
 
     def shutdown(self):
         if self._loop is not None and self._server is not None:
-            self._loop.call_soon_threadsafe(self._server.close)
-            fut = asyncio.run_coroutine_threadsafe(self._cancel_all(), self._loop)
             try:
+                # closing the server ends serve_forever, and asyncio.run may close the loop before
+                # the cancel coroutine below is scheduled: either order is a clean shutdown
+                self._loop.call_soon_threadsafe(self._server.close)
+                fut = asyncio.run_coroutine_threadsafe(self._cancel_all(), self._loop)
                 fut.result(5)
             except Exception:
                 pass

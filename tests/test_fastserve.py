@@ -97,3 +97,17 @@ def test_concurrent_single_queries_are_batched(server):
         t.join(60)
     assert np.allclose(np.asarray(out), fake._probs(qs))
     assert sum(fake.batch_sizes) == 96 and len(fake.batch_sizes) < 96   # stacked into batches
+
+
+def test_bad_and_oversized_content_length(server):
+    """Content-Length is validated before any body byte is buffered (400 / 413)."""
+    import socket
+    srv, fake, url = server
+    for hdr, code in ((b'Content-Length: -5', b'400'), (b'Content-Length: abc', b'400'),
+                      (b'Content-Length: 99999999999', b'413')):
+        s = socket.create_connection(('127.0.0.1', srv.port), timeout=10)
+        s.sendall(b'POST /predict HTTP/1.1\r\nHost: x\r\n' + hdr + b'\r\n\r\n')
+        resp = s.recv(4096)
+        s.close()
+        assert resp.split(b' ')[1] == code, resp
+    assert requests.get(url + '/').status_code == 200   # server still serving
