@@ -774,7 +774,7 @@ class ConvNetEngine:
             out_probs = torch.empty((x.shape[0], self.num_classes), dtype=torch.float32, device=self.device)
         return self._forward_eval_gpu(x, out_probs)
 
-    EVAL_BUCKETS = (1, 8, 32, 128, 512)
+    EVAL_BUCKETS = (1, 8, 32, 64, 128, 256, 512)
 
     @torch.no_grad()
     def forward_eval_graphed(self, x):

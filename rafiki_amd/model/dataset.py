@@ -143,15 +143,22 @@ class CorpusDataset(ModelDataset):
 
 
 # ------------------------------------------------------------------------------- synthetic data
-def synthetic_images(n, size=32, channels=3, classes=10, seed=0, separable=True):
-    """Deterministic class-conditional images: a per-class template plus noise (learnable)."""
+def synthetic_images(n, size=32, channels=3, classes=10, seed=0, separable=True, noise=None, flip=0.0):
+    """Deterministic class-conditional images: a per-class template plus Gaussian noise (std ``noise``,
+    default 48 / 96 for separable / not).  ``flip`` relabels that fraction of the images uniformly at
+    random, so no classifier exceeds ~1 - flip*(1 - 1/classes) accuracy (a non-separable task)."""
     rng = np.random.default_rng(seed)
     shape = (size, size) if channels == 1 else (size, size, channels)
     tmpl_rng = np.random.default_rng(1234)
     templates = tmpl_rng.uniform(0, 255, size=(classes, *shape)).astype(np.float32)
     labels = rng.integers(0, classes, size=n)
-    noise = rng.normal(0, 48 if separable else 96, size=(n, *shape)).astype(np.float32)
-    imgs = np.clip(templates[labels] * 0.6 + 50 + noise, 0, 255).astype(np.uint8)
+    std = float(noise) if noise is not None else (48.0 if separable else 96.0)
+    nz = rng.normal(0, std, size=(n, *shape)).astype(np.float32)
+    imgs = np.clip(templates[labels] * 0.6 + 50 + nz, 0, 255).astype(np.uint8)
+    if flip > 0:
+        sel = rng.random(n) < float(flip)
+        labels = labels.copy()
+        labels[sel] = rng.integers(0, classes, size=int(sel.sum()))
     return imgs, labels.astype(np.int64)
 
 
@@ -225,7 +232,9 @@ class ModelDatasetUtils:
             kind, q = _parse_synthetic(dataset_uri)
             size = int(q.get('size', image_size or 32))
             imgs, labels = synthetic_images(int(q.get('n', 1024)), size=size, channels=int(q.get('channels', 1)),
-                                            classes=int(q.get('classes', 10)), seed=int(q.get('seed', 0)))
+                                            classes=int(q.get('classes', 10)), seed=int(q.get('seed', 0)),
+                                            noise=float(q['noise']) if 'noise' in q else None,
+                                            flip=float(q.get('flip', 0.0)))
             if image_size is not None:  # same contract as a zip: decoded images come back at image_size
                 want = (image_size, image_size) if isinstance(image_size, int) else tuple(image_size)
                 if imgs.shape[1:3] != tuple(want):

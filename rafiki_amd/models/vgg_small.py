@@ -35,6 +35,23 @@ class VggSmall(NativeImageClassifier):
                     weight_decay=float(k.get('weight_decay', 5e-4)), nesterov=True)
 
 
+class VggSmallTrial(VggSmall):
+    """The benchmark's trial definition (bench.py phase 2): VggSmall at full width, batch 256, two
+    epochs per trial; the advisor searches the SGD knobs only, so every trial does the same work."""
+
+    @staticmethod
+    def get_knob_config():
+        return {
+            'epochs': FixedKnob(2),
+            'learning_rate': FloatKnob(1e-2, 2e-1, is_exp=True),
+            'momentum': FloatKnob(0.8, 0.95),
+            'weight_decay': FloatKnob(1e-5, 1e-3, is_exp=True),
+            'batch_size': FixedKnob(256),
+            'width_mult': FixedKnob(1.0),
+            'image_size': FixedKnob(32),
+        }
+
+
 if __name__ == '__main__':
     from rafiki_amd.model import test_model_class
     test_model_class(__file__, 'VggSmall', TaskType.IMAGE_CLASSIFICATION, {},

@@ -133,6 +133,15 @@ def all_reduce_max(info: DistInfo, v: float) -> float:
     return float(t.item())
 
 
+def broadcast_object(info: DistInfo, obj):
+    """Rank 0's picklable ``obj`` on every rank (control-plane metadata: ids, small configs)."""
+    if info.world_size == 1:
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=0, device=comm_device(info))
+    return lst[0]
+
+
 def destroy(info: DistInfo):
     if info.world_size > 1 and dist.is_initialized():
         dist.destroy_process_group()
