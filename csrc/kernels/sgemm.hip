@@ -6,8 +6,10 @@
 //
 // Design for the f32 MFMA rate (64 FLOP/clk/SIMD, 1/16 of bf16): the arithmetic, not the memory
 // system, is the bound, so a block owns a large tile and keeps every SIMD issuing MFMAs:
-//   * 256 threads = 4 waves as 2x2; wave tile (32*MI) x (32*NI), MI, NI in {1,2} -> block tile up to
-//     128x128 (64 fp32 accumulator registers per lane), BK = 32 fp32 (128-B LDS rows);
+//   * 4 or 8 waves (2x2, 4x1, 1x4, 4x2, 2x4); wave tile (32*MI) x (32*NI), MI, NI in {1,2} -> block
+//     tiles 64x64 .. 256x128 (up to 64 fp32 accumulator registers per lane), BK = 32 fp32 (128-B
+//     LDS rows); the big tiles cut the L2 / Infinity-Cache bytes per FLOP (a 64x64 tile needs
+//     16 B/clk/CU of operands at the f32 MFMA rate — the measured bound of the small tiles);
 //   * operands go global -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging, no ds_write):
 //     "K-inner" operands (reduction index contiguous: NHWC activations gathered per 3x3 tap, [N][K]
 //     weights) land as XOR-swizzled [T][32] rows read with ds_read_b128; "K-outer" operands
@@ -26,6 +28,7 @@
 // FLAG_BNB / FLAG_BNP (data-gradient into a BN+ReLU [+2x2 max-pool] layer: mask + BN-backward sums),
 // split-K fp32 slabs, accumulate.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -58,6 +61,7 @@ struct SgParams {
   int flags, slotMask;
   float alpha, slope;
   unsigned long long bytesA, bytesB;
+  int dbg;  // diagnostics (RAFIKI_SGEMM_DBG): 1 no DMA in the K loop (stale LDS), 2 no K-loop barrier
 };
 
 RK_DEV __amdgpu_buffer_rsrc_t s_rsrc(const void* base, unsigned long long bytes) {
@@ -86,11 +90,12 @@ RK_DEV void s_hw(int k, int H, int W, int log2H, int log2W, float invH, float in
 }
 
 // One operand tile of T rows (K-inner) or T columns (K-outer) per K-tile; T*128 bytes = T/8 DMA
-// wave-instructions, T/32 per wave.
-template <int MODE, int T>
+// wave-instructions, T/(8*NW) per wave of an NW-wave workgroup.
+template <int MODE, int T, int NW>
 struct SOperand {
   static constexpr bool KIN = MODE == SM_KIN_DENSE || MODE == SM_KIN_CONV || MODE == SM_KIN_CONVF;
-  static constexpr int NQ = T / 32;
+  static constexpr int NQ = T / (8 * NW);
+  static_assert(NQ >= 1 && NQ * 8 * NW == T, "operand tile must split evenly over the waves");
   static constexpr int RS = T / 4;  // 16-B slots per K-outer row
   __amdgpu_buffer_rsrc_t rsrc;
   unsigned base[NQ];
@@ -234,7 +239,7 @@ RK_DEV void s_group_sched() {
   if constexpr (ND > 0) {
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (d + 1 < NMF) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
     }
   }
@@ -315,15 +320,18 @@ RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int 
   }
 }
 
-template <int MI, int NI, int AM, int BMD, int NST>
-__global__ __launch_bounds__(256) void sgemm_kernel(const SgParams p) {
-  constexpr int BM = 64 * MI, BN = 64 * NI;
+// Workgroup = WGM x WGN waves, each owning (32*MI) x (32*NI) outputs: block tile BM x BN.
+template <int WGM, int WGN, int MI, int NI, int AM, int BMD, int NST>
+__global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p) {
+  constexpr int NW = WGM * WGN;
+  constexpr int WMT = 32 * MI, WNT = 32 * NI;  // wave tile
+  constexpr int BM = WGM * WMT, BN = WGN * WNT;
   constexpr int ABYTES = BM * 128, SB = (BM + BN) * 128;
-  constexpr int L = BM / 32 + BN / 32;  // DMA wave-instructions per wave per K-tile
+  constexpr int L = (BM + BN) / (8 * NW);  // DMA wave-instructions per wave per K-tile
   __shared__ __attribute__((aligned(16))) char smem[NST * SB];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid - (wid / WGN) * WGN;
   const int tilesN = (p.N + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = bid / tilesN, nt = bid - mt * tilesN;
@@ -332,8 +340,8 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const SgParams p) {
   const int kt0 = blockIdx.z * p.ktPer;
   const int kt1 = min(nk, kt0 + p.ktPer);
 
-  SOperand<AM, BM> A;
-  SOperand<BMD, BN> B;
+  SOperand<AM, BM, NW> A;
+  SOperand<BMD, BN, NW> B;
   A.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane);
   B.init(p, p.B, p.bytesB, p.ldb, n0, p.N, wid, lane);
 
@@ -364,7 +372,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const SgParams p) {
     } else {
       s_wait_vmcnt<0>();
     }
-    s_barrier_lds();  // every wave's DMA for tile kt is in LDS; every wave is done with tile kt-1
+    if (!(p.dbg & 2)) s_barrier_lds();  // every wave's DMA for tile kt is in LDS; done with tile kt-1
     const char* As = smem + st * SB;
     const char* Bs = As + ABYTES;
     const bool more = kt + NST - 1 < kt1;
@@ -375,28 +383,32 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const SgParams p) {
     // overlap and clusters the DMA issue in front of them).
     constexpr int NMF = 4 * MI * NI;
     constexpr int RA = A.KIN ? MI : 4 * MI, RB = B.KIN ? NI : 4 * NI;  // LDS read instructions per group
-    constexpr int DA = BM / 32, DB = BN / 32;                          // DMA instructions per wave
+    constexpr int DA = BM / (8 * NW), DB = BN / (8 * NW);              // DMA instructions per wave
     f32x4 a[2][MI], b[2][NI];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) a[0][i] = A.frag(As, wm * (BM / 2) + i * 32, 0, lane);
+    for (int i = 0; i < MI; ++i) a[0][i] = A.frag(As, wm * WMT + i * 32, 0, lane);
 #pragma unroll
-    for (int j = 0; j < NI; ++j) b[0][j] = B.frag(Bs, wn * (BN / 2) + j * 32, 0, lane);
+    for (int j = 0; j < NI; ++j) b[0][j] = B.frag(Bs, wn * WNT + j * 32, 0, lane);
 #pragma unroll
     for (int g = 0; g < SBK / 8; ++g) {
       const int cur = g & 1;
       if (g + 1 < SBK / 8) {
 #pragma unroll
-        for (int i = 0; i < MI; ++i) a[cur ^ 1][i] = A.frag(As, wm * (BM / 2) + i * 32, g + 1, lane);
+        for (int i = 0; i < MI; ++i) a[cur ^ 1][i] = A.frag(As, wm * WMT + i * 32, g + 1, lane);
 #pragma unroll
-        for (int j = 0; j < NI; ++j) b[cur ^ 1][j] = B.frag(Bs, wn * (BN / 2) + j * 32, g + 1, lane);
+        for (int j = 0; j < NI; ++j) b[cur ^ 1][j] = B.frag(Bs, wn * WNT + j * 32, g + 1, lane);
       }
       // the reads above may not sink below this group's MFMAs (that would collapse the two fragment
       // register sets into one and expose the LDS latency at every group boundary)
       __builtin_amdgcn_sched_barrier(0);
       // unconditional (zeros past the end: that stage is never read again) — no branch splits the
       // scheduling region
-      if (g == 0) A.issue(p, nxt, kt + NST - 1, p.K, p.lda, wid, more);
-      if (g == 1) B.issue(p, nxt + ABYTES, kt + NST - 1, p.K, p.ldb, wid, more);
+      // the next tile's DMAs go out in the first group, so they have (NST-1) whole K-tiles of MFMAs
+      // to land (a 64x64 tile's K-tile is only 16 MFMAs = ~1k cycles per wave)
+      if (g == 0 && !(p.dbg & 1)) {
+        A.issue(p, nxt, kt + NST - 1, p.K, p.lda, wid, more);
+        B.issue(p, nxt + ABYTES, kt + NST - 1, p.K, p.ldb, wid, more);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -405,35 +417,52 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const SgParams p) {
           for (int j = 0; j < NI; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i][e], b[cur][j][e], acc[i][j], 0, 0, 0);
       // group schedule: MFMAs with one DMA (and its address VALU) after each of the first few
-      if (g == 0) s_group_sched<NMF, 0, DA>();
-      else if (g == 1) s_group_sched<NMF, 0, DB>();
+      if (g == 0) s_group_sched<NMF, 0, DA + DB>();
       __builtin_amdgcn_sched_barrier(0);
     }
     st = st + 1 == NST ? 0 : st + 1;
   }
   s_wait_vmcnt<0>();  // the trailing zero-DMAs land before the workgroup's LDS is released
-  s_epilogue<MI, NI>(p, acc, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
+  s_epilogue<MI, NI>(p, acc, m0 + wm * WMT, n0 + wn * WNT, lane);
 }
 
-template <int MI, int NI, int AM, int BMD>
+template <int WGM, int WGN, int MI, int NI, int AM, int BMD>
 int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
-  const int tiles = rk_cdiv(p.M, 64 * MI) * rk_cdiv(p.N, 64 * NI);
+  constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
+  const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
   dim3 grid(tiles, 1, splits);
-  if (nst == 3) hipLaunchKernelGGL((sgemm_kernel<MI, NI, AM, BMD, 3>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((sgemm_kernel<MI, NI, AM, BMD, 2>), grid, dim3(256), 0, st, p);
+  if (nst == 3) {
+    if constexpr (WGM * WGN == 4)  // 3-stage rings only for the 4-wave tiles (8-wave ones fill LDS at 2)
+      hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3>), grid, dim3(64 * WGM * WGN), 0, st, p);
+    else
+      return RK_EUNSUPPORTED;
+  } else {
+    hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 2>), grid, dim3(64 * WGM * WGN), 0, st, p);
+  }
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
-template <int AM, int BMD>
+// tile codes (block tile, waves): 0 128x128 (2x2), 1 128x64 (2x2), 2 64x128 (2x2), 3 64x64 (2x2),
+// 4 256x64 (4x1), 5 256x128 (4x2, 512 threads), 6 128x256 (2x4, 512 threads), 7 64x256 (1x4).
+// BIG = false instantiates only tiles 0-3 (dense layers, the general conv gather).
+template <int AM, int BMD, bool BIG>
 int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t st) {
   switch (tile) {
-    case 0: return s_launch<2, 2, AM, BMD>(p, nst, splits, st);
-    case 1: return s_launch<2, 1, AM, BMD>(p, nst, splits, st);
-    case 2: return s_launch<1, 2, AM, BMD>(p, nst, splits, st);
-    case 3: return s_launch<1, 1, AM, BMD>(p, nst, splits, st);
+    case 0: return s_launch<2, 2, 2, 2, AM, BMD>(p, nst, splits, st);
+    case 1: return s_launch<2, 2, 2, 1, AM, BMD>(p, nst, splits, st);
+    case 2: return s_launch<2, 2, 1, 2, AM, BMD>(p, nst, splits, st);
+    case 3: return s_launch<2, 2, 1, 1, AM, BMD>(p, nst, splits, st);
   }
-  return RK_EBADARG;
+  if constexpr (BIG) {
+    switch (tile) {
+      case 4: return s_launch<4, 1, 2, 2, AM, BMD>(p, nst, splits, st);
+      case 5: return s_launch<4, 2, 2, 2, AM, BMD>(p, nst, splits, st);
+      case 6: return s_launch<2, 4, 2, 2, AM, BMD>(p, nst, splits, st);
+      case 7: return s_launch<1, 4, 2, 2, AM, BMD>(p, nst, splits, st);
+    }
+  }
+  return RK_EUNSUPPORTED;
 }
 
 }  // namespace
@@ -450,7 +479,7 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
                         int ldc, int H, int W, int Cch, int taps, int splits, long long slabStride, int flags,
                         float alpha, float slope, long long bytesA, long long bytesB, void* stream) {
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 3) return RK_EBADARG;
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 7) return RK_EBADARG;
   if (taps != 1 && taps != 9) return RK_EBADARG;
   const bool conv = kind == 0 || kind == 2;
   // 16-B chunks: K-inner operands need K % 4 == 0 (and 16-B aligned rows); K-outer ones need the
@@ -479,15 +508,17 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
   p.slabStride = splits > 1 ? slabStride : 0;
   p.flags = flags; p.slotMask = slotMask; p.alpha = alpha; p.slope = slope;
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
+  static const int dbg = getenv("RAFIKI_SGEMM_DBG") ? atoi(getenv("RAFIKI_SGEMM_DBG")) : 0;
+  p.dbg = dbg;
   hipStream_t st = (hipStream_t)stream;
   switch (kind) {
     case 0:
-      if (Cch % SBK == 0) return s_launch_tile<SM_KIN_CONVF, SM_KIN_DENSE>(tile, p, nst, splits, st);
-      return s_launch_tile<SM_KIN_CONV, SM_KIN_DENSE>(tile, p, nst, splits, st);
-    case 2: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_CONV>(tile, p, nst, splits, st);
-    case 3: return s_launch_tile<SM_KIN_DENSE, SM_KIN_DENSE>(tile, p, nst, splits, st);
-    case 4: return s_launch_tile<SM_KIN_DENSE, SM_KOUT_DENSE>(tile, p, nst, splits, st);
-    case 5: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_DENSE>(tile, p, nst, splits, st);
+      if (Cch % SBK == 0) return s_launch_tile<SM_KIN_CONVF, SM_KIN_DENSE, true>(tile, p, nst, splits, st);
+      return s_launch_tile<SM_KIN_CONV, SM_KIN_DENSE, false>(tile, p, nst, splits, st);
+    case 2: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_CONV, true>(tile, p, nst, splits, st);
+    case 3: return s_launch_tile<SM_KIN_DENSE, SM_KIN_DENSE, false>(tile, p, nst, splits, st);
+    case 4: return s_launch_tile<SM_KIN_DENSE, SM_KOUT_DENSE, false>(tile, p, nst, splits, st);
+    case 5: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_DENSE, false>(tile, p, nst, splits, st);
   }
   return RK_EBADARG;
 }

@@ -24,7 +24,10 @@ from .functional import ACT_LRELU, ACT_NONE, ACT_RELU, bn_slots, cdiv  # noqa: F
 
 KIND_CONV, KIND_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW = 0, 2, 3, 4, 5
 F_RELU, F_BIAS, F_STATS, F_GATE, F_ACCUM, F_LRELU, F_BNB, F_BNP = 1, 2, 4, 8, 16, 32, 512, 1024
-TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
+# block tiles (see rk_sgemm): 0-3 four-wave 2x2, 4 256x64 (4x1 waves), 5 256x128 / 6 128x256 (8 waves),
+# 7 64x256 (1x4).  Tiles 4-7 exist for the conv kinds with C % 32 == 0 and the weight gradient.
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 64), (256, 128), (128, 256), (64, 256)]
+_NST3 = (0, 1, 2, 3, 4, 7)
 NUM_CU = 256
 # RAFIKI_SGEMM_CFG="tile,nst" pins every sgemm launch (A/B runs without the tuner)
 _PIN = tuple(int(v) for v in os.environ['RAFIKI_SGEMM_CFG'].split(',')) if os.environ.get('RAFIKI_SGEMM_CFG') else None
@@ -64,7 +67,7 @@ def sgemm(kind, A, B, out, M, N, K, lda, ldb, ldc, *, tile=0, nst=2, splits=1, s
 def pick_tile(M: int, N: int) -> int:
     """Largest tile that still puts >= one block on every CU (else the tile with most blocks)."""
     best, best_blocks = 3, -1
-    for t, (bm, bn) in enumerate(TILES):
+    for t, (bm, bn) in enumerate(TILES[:4]):
         blocks = cdiv(M, bm) * cdiv(N, bn)
         waste = (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N)
         if waste > 1.3 and t != 3:
@@ -76,27 +79,34 @@ def pick_tile(M: int, N: int) -> int:
     return best
 
 
-def _cands(M, N, splittable=False, K=0):
-    """(tile, nst, splits) configs: the heuristic first, then every tile x ring depth, plus split-K
-    variants for grids that leave the chip idle."""
+def _cands(M, N, splittable=False, K=0, big=False):
+    """(tile, nst, splits) configs: the heuristic first, then every tile x ring depth (``big``: also the
+    256-wide tiles), plus split-K variants for grids that leave the chip idle."""
     t0 = pick_tile(M, N)
     out = [(t0, 2, 1)]
-    for t in range(4):
-        for nst in (2, 3):
+    tiles = range(8 if big else 4)
+    for t in tiles:
+        bm, bn = TILES[t]
+        if t >= 4 and (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N) > 1.3:
+            continue  # the big tiles only where they do not mostly compute padding
+        for nst in ((2, 3) if t in _NST3 else (2,)):
             c = (t, nst, 1)
             if c not in out:
                 out.append(c)
     if splittable:
         kt = cdiv(K, 32)
-        for t in range(4):
-            blocks = cdiv(M, TILES[t][0]) * cdiv(N, TILES[t][1])
+        for t in tiles:
+            bm, bn = TILES[t]
+            if t >= 4 and (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N) > 1.3:
+                continue
+            blocks = cdiv(M, bm) * cdiv(N, bn)
             for s in (2, 4, 8, 16, 32, 64, 128, 256):
                 if s > kt // 2 or blocks * s > 8 * NUM_CU or s * M * N * 4 > (512 << 20):
                     continue
                 if blocks * s < NUM_CU // 2:
                     continue
                 s_eff = cdiv(kt, cdiv(kt, s))
-                for nst in (2, 3):
+                for nst in ((2, 3) if t in _NST3 else (2,)):
                     c = (t, nst, s_eff)
                     if c not in out:
                         out.append(c)
@@ -133,7 +143,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     def run(cfg):
         sgemm(KIND_CONV, x, w, out, M, Cout, K, Cin, K, Cout, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats_acc,
               H=H, W=W, C=Cin, taps=taps, flags=flags, slope=slope)
-    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags), _cands(M, Cout), run)
+    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags), _cands(M, Cout, big=Cin % 32 == 0), run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -168,7 +178,7 @@ def conv_dgrad(dy: torch.Tensor, wt: torch.Tensor, *, taps: int = 9, out=None, g
     def run(cfg):
         sgemm(KIND_CONV, dy, wt, out, M, Cin, K, Cout, K, Cin, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats,
               gate=gate, H=H, W=W, C=Cout, taps=taps, flags=flags)
-    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags), _cands(M, Cin), run)
+    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags), _cands(M, Cin, big=Cout % 32 == 0), run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -195,7 +205,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
         sgemm(KIND_WGRAD, dy, x, slab, M, N, K, Cout, Cin, N, tile=tile, nst=nst, splits=s, slab_stride=M * N,
               H=H, W=W, C=Cin, taps=taps)
         reduce_slabs(slab, out, accumulate=accumulate)
-    cands = _cands(M, N, splittable=True, K=K)
+    cands = _cands(M, N, splittable=True, K=K, big=True)
     # the split-K configs fill the chip: lead with the best-filling heuristic one
     split = [c for c in cands if c[2] > 1]
     if split:

@@ -57,20 +57,20 @@ def main():
             res = []
             if pas == 'fwd':
                 y = torch.empty(B, hw, hw, cout, device=dev)
-                for cfg in S._cands(M, cout):
+                for cfg in S._cands(M, cout, big=cin % 32 == 0):
                     fn = lambda cfg=cfg: S.sgemm(S.KIND_CONV, x, w, y, M, cout, 9 * cin, cin, 9 * cin, cout,
                                                  tile=cfg[0], nst=cfg[1], H=hw, W=hw, C=cin, taps=9)
                     res.append((cfg, time_fn(fn, a.reps)))
             elif pas == 'dgrad':
                 dx = torch.empty(B, hw, hw, cin, device=dev)
-                for cfg in S._cands(M, cin):
+                for cfg in S._cands(M, cin, big=True):
                     fn = lambda cfg=cfg: S.sgemm(S.KIND_CONV, dy, wt, dx, M, cin, 9 * cout, cout, 9 * cout, cin,
                                                  tile=cfg[0], nst=cfg[1], H=hw, W=hw, C=cout, taps=9)
                     res.append((cfg, time_fn(fn, a.reps)))
             else:
                 N = 9 * cin
                 out = torch.empty(cout, N, device=dev)
-                for cfg in S._cands(cout, N, splittable=True, K=M):
+                for cfg in S._cands(cout, N, splittable=True, K=M, big=True):
                     tile, nst, s = cfg
                     slab = torch.empty(max(1, s), cout, N, device=dev)
 

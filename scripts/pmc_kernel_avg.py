@@ -29,6 +29,13 @@ def main():
     by = collections.defaultdict(list)
     for did in sorted(disp):
         by[disp[did][0]].append(disp[did][1])
+    # kernel durations of the same run (kernel_trace.csv), if collected: effective clock
+    dur = collections.defaultdict(list)
+    for fn in glob.glob(os.path.join(a.d, '**', '*kernel_trace.csv'), recursive=True):
+        with open(fn) as f:
+            for r in csv.DictReader(f):
+                if a.match in r['Kernel_Name']:
+                    dur[r['Kernel_Name']].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
     for name, lst in by.items():
         lst = lst[a.skip:] or lst
         keys = sorted({k for d in lst for k in d})
@@ -40,6 +47,10 @@ def main():
         if 'SQ_VALU_MFMA_BUSY_CYCLES' in mean and 'GRBM_GUI_ACTIVE' in mean:
             cyc = mean['GRBM_GUI_ACTIVE'] / 8.0
             print('  mfma_util_pct (vs GRBM span) {:.1f}'.format(100.0 * mean['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * 1024)))
+        if dur.get(name) and 'GRBM_GUI_ACTIVE' in mean:
+            d = sorted(dur[name])[len(dur[name]) // 2] * 1e-9
+            print('  median_dispatch_us {:.1f}  effective_clock_GHz {:.3f}'.format(
+                d * 1e6, mean['GRBM_GUI_ACTIVE'] / 8.0 / d / 1e9))
         if 'SQ_BUSY_CYCLES' in mean and 'GRBM_GUI_ACTIVE' in mean:
             print('  sq_busy / grbm_per_xcd {:.3f}'.format(mean['SQ_BUSY_CYCLES'] / (mean['GRBM_GUI_ACTIVE'] / 8.0)))
 
