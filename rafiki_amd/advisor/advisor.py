@@ -19,10 +19,24 @@ import math
 import threading
 
 import numpy as np
+from scipy.linalg import solve_triangular
+from scipy.special import ndtr
 
 from ..constants import AdvisorType
 from ..model.knob import (CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, decode_knobs, encode_knobs,
                           knob_space_dims)
+
+
+def _one_blas_thread():
+    """The GP's matrices are tiny (tens of observations): multi-threaded BLAS only adds spin-waiting,
+    and with one trial worker per GPU on a node those spinning pools steal each other's cores (a
+    4-worker node measured 40-50 ms per proposal instead of 6)."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:  # pragma: no cover
+        import contextlib
+        return contextlib.nullcontext()
+    return threadpool_limits(limits=1, user_api='blas')
 
 
 def _simplify(v):
@@ -44,13 +58,13 @@ class BaseAdvisor:
         self._pending = []
 
     def propose(self):
-        with self._lock:
+        with self._lock, _one_blas_thread():
             knobs = self._propose_locked(1)[0]
             self._pending.append(knobs)
             return knobs
 
     def propose_batch(self, q):
-        with self._lock:
+        with self._lock, _one_blas_thread():
             out = self._propose_locked(q)
             self._pending.extend(out)
             return out
@@ -92,52 +106,64 @@ class RandomAdvisor(BaseAdvisor):
     """Uniform random search on the (log-)scaled knob space."""
 
 
+def _tri(L, b, lower):
+    return solve_triangular(L, b, lower=lower, check_finite=False)
+
+
 class _GP:
     """Minimal GP regressor with a Matern-5/2 kernel (numpy, float64)."""
 
     def __init__(self, ls=0.3, sf2=1.0, sn2=1e-4):
         self.ls, self.sf2, self.sn2 = ls, sf2, sn2
 
-    def _k(self, A, B):
-        d = np.sqrt(np.maximum(((A[:, None, :] - B[None, :, :]) ** 2).sum(-1), 0.0)) / self.ls
+    @staticmethod
+    def _dist(A, B):
+        return np.sqrt(np.maximum(((A[:, None, :] - B[None, :, :]) ** 2).sum(-1), 0.0))
+
+    def _kd(self, D):
+        d = D / self.ls
         s5 = math.sqrt(5.0)
         return self.sf2 * (1.0 + s5 * d + 5.0 / 3.0 * d * d) * np.exp(-s5 * d)
+
+    def _k(self, A, B):
+        return self._kd(self._dist(A, B))
 
     def fit(self, X, y):
         self.X = X
         self.ym, self.ys = float(y.mean()), float(y.std() + 1e-9)
         yn = (y - self.ym) / self.ys
+        D = self._dist(X, X)  # shared by every hyper-parameter candidate
+        eye = np.eye(len(X))
         best = None
         for ls in (0.08, 0.15, 0.3, 0.6, 1.2):
+            self.ls = ls
+            Kls = self._kd(D)
             for sn2 in (1e-6, 1e-3, 1e-2, 1e-1):
-                self.ls, self.sn2 = ls, sn2
-                K = self._k(X, X) + sn2 * np.eye(len(X))
                 try:
-                    L = np.linalg.cholesky(K)
+                    L = np.linalg.cholesky(Kls + sn2 * eye)
                 except np.linalg.LinAlgError:
                     continue
-                alpha = np.linalg.solve(L.T, np.linalg.solve(L, yn))
+                alpha = _tri(L.T, _tri(L, yn, True), False)
                 lml = -0.5 * yn @ alpha - np.log(np.diag(L)).sum()
                 if best is None or lml > best[0]:
                     best = (lml, ls, sn2, L, alpha)
         if best is None:  # pathological: fall back to heavy noise
             self.ls, self.sn2 = 0.3, 1.0
-            K = self._k(X, X) + np.eye(len(X))
-            L = np.linalg.cholesky(K)
-            best = (0, 0.3, 1.0, L, np.linalg.solve(L.T, np.linalg.solve(L, yn)))
+            L = np.linalg.cholesky(self._k(X, X) + eye)
+            best = (0, 0.3, 1.0, L, _tri(L.T, _tri(L, yn, True), False))
         _, self.ls, self.sn2, self.L, self.alpha = best
         return self
 
     def predict(self, Xs):
         Ks = self._k(Xs, self.X)
         mu = Ks @ self.alpha
-        v = np.linalg.solve(self.L, Ks.T)
+        v = _tri(self.L, Ks.T, True)
         var = np.maximum(self.sf2 - (v * v).sum(0), 1e-12)
         return mu * self.ys + self.ym, np.sqrt(var) * self.ys
 
 
 def _norm_cdf(z):
-    return 0.5 * (1.0 + np.vectorize(math.erf)(z / math.sqrt(2.0)))
+    return ndtr(z)
 
 
 def _norm_pdf(z):
@@ -155,22 +181,54 @@ class GpAdvisor(BaseAdvisor):
     def _encode(self, knobs):
         return np.asarray(encode_knobs(self.knob_config, knobs), dtype=np.float64)
 
+    def _snap(self, U):
+        """Raw unit-cube samples [n, dims] -> encodings of valid knob values (the vectorised
+        ``encode(decode(u))``: integers rounded on their own (log) scale, categoricals one-hot)."""
+        out = np.empty_like(U)
+        j = 0
+        for name in sorted(self.knob_config):
+            k = self.knob_config[name]
+            d = k.dims
+            if d == 0:
+                continue
+            u = U[:, j:j + d]
+            if isinstance(k, CategoricalKnob):
+                oh = np.zeros_like(u)
+                oh[np.arange(len(u)), np.argmax(u, 1)] = 1.0
+                out[:, j:j + d] = oh
+            elif isinstance(k, IntegerKnob):
+                lo, hi = k._fwd(k.value_min), k._fwd(k.value_max)
+                if hi == lo:
+                    out[:, j] = 0.5
+                else:
+                    x = lo + np.clip(u[:, 0], 0.0, 1.0) * (hi - lo)
+                    v = np.clip(np.round(np.exp(x) if k.is_exp else x), k.value_min, k.value_max)
+                    out[:, j] = np.clip(((np.log(v) if k.is_exp else v) - lo) / (hi - lo), 0.0, 1.0)
+            else:
+                out[:, j] = np.clip(u[:, 0], 0.0, 1.0)
+            j += d
+        return out
+
     def _candidates(self, top):
-        cands = [self._random_knobs() for _ in range(self.n_candidates)]
-        for knobs in top:  # local perturbations around the incumbents
-            for _ in range(max(1, self.n_candidates // (4 * max(1, len(top))))):
-                u = self._encode(knobs)
-                j = 0
-                new = dict(knobs)
-                for name in sorted(self.knob_config):
-                    k = self.knob_config[name]
-                    if isinstance(k, (IntegerKnob, FloatKnob)):
-                        new[name] = k.decode([float(np.clip(u[j] + self.rng.normal(0, 0.08), 0, 1))])
-                    elif isinstance(k, CategoricalKnob) and self.rng.random() < 0.2:
-                        new[name] = _simplify(k.values[self.rng.integers(len(k.values))])
-                    j += k.dims
-                cands.append(new)
-        return cands
+        """Encoded candidates [n, dims]: uniform samples plus local perturbations of the incumbents."""
+        parts = [self.rng.random((self.n_candidates, self.dims))]
+        cat_cols = []
+        j = 0
+        for name in sorted(self.knob_config):
+            k = self.knob_config[name]
+            if isinstance(k, CategoricalKnob):
+                cat_cols.append((j, k.dims))
+            j += k.dims
+        per = max(1, self.n_candidates // (4 * max(1, len(top))))
+        for knobs in top:
+            u = np.tile(self._encode(knobs), (per, 1)) + self.rng.normal(0, 0.08, (per, self.dims))
+            for (c, d) in cat_cols:  # a categorical is re-drawn with probability 0.2
+                flip = self.rng.random(per) < 0.2
+                u[flip, c:c + d] = self.rng.random((int(flip.sum()), d))
+                keep = ~flip
+                u[keep, c:c + d] = self._encode(knobs)[c:c + d]
+            parts.append(u)
+        return self._snap(np.concatenate(parts))
 
     def _propose_locked(self, q):
         if self.dims == 0:
@@ -188,27 +246,24 @@ class GpAdvisor(BaseAdvisor):
         lie = float(scores.mean())
         pending = [p for p in self._pending] + list(out)
         top = [k for k, _ in sorted(obs, key=lambda t: -t[1])[:3]]
+        X = np.stack([self._encode(k) for k, _ in obs] + [self._encode(p) for p in pending])
+        y = np.concatenate([scores, np.full(len(pending), lie)])
+        best = float(scores.max())
         while len(out) < q:
-            X = np.stack([self._encode(k) for k, _ in obs] + [self._encode(p) for p in pending])
-            y = np.concatenate([scores, np.full(len(pending), lie)])
             gp = _GP().fit(X, y)
-            cands = self._candidates(top)
-            C = np.stack([self._encode(c) for c in cands])
+            C = self._candidates(top)
             mu, sd = gp.predict(C)
-            best = float(scores.max())
             z = (mu - best - self.xi) / sd
             ei = (mu - best - self.xi) * _norm_cdf(z) + sd * _norm_pdf(z)
-            seen = {tuple(np.round(x, 6)) for x in X}
-            order = np.argsort(-ei)
-            pick = None
-            for i in order:
-                if tuple(np.round(C[i], 6)) not in seen:
-                    pick = cands[i]
-                    break
-            if pick is None:
-                pick = self._random_knobs()
+            # never re-propose an observed or pending point
+            d2 = ((C[:, None, :] - X[None, :, :]) ** 2).sum(-1).min(1)
+            ei[d2 < 1e-12] = -np.inf
+            i = int(np.argmax(ei))
+            pick = decode_knobs(self.knob_config, C[i]) if np.isfinite(ei[i]) else self._random_knobs()
+            pick = {k: _simplify(v) for k, v in pick.items()}
             out.append(pick)
-            pending.append(pick)
+            X = np.vstack([X, self._encode(pick)[None]])
+            y = np.append(y, lie)  # constant liar for the next proposal of this batch
         return out
 
 

@@ -64,14 +64,22 @@ class TrainWorker:
         os.makedirs(self._params_dir, exist_ok=True)
         self._max_trial_errors = max_trial_errors
         self._ckpt_every = checkpoint_every_epochs
-        # 'rounds': rank 0 proposes one knob set per rank per round over RCCL (lock-step);
-        # 'async' : ranks pull trials independently (heterogeneous trial lengths)
-        self._scheduling = scheduling or os.environ.get('RAFIKI_TRIAL_SCHEDULING', 'rounds')
+        # 'async' : ranks pull trials independently — an atomic budget claim in the store + a GP-EI
+        #           proposal over the shared history with in-flight trials as constant-liar points;
+        #           no round barrier, so heterogeneous trial lengths (epochs / batch size / width
+        #           knobs) never idle a GPU.  The default ('auto') for every non-data-parallel model.
+        # 'rounds': rank 0 proposes one knob set per rank per round, broadcast over RCCL (lock-step;
+        #           every round waits for its slowest trial).  Data-parallel models always use it.
+        self._scheduling = scheduling or os.environ.get('RAFIKI_TRIAL_SCHEDULING', 'auto')
         self._advisor_type = advisor_type
         self._seed = seed
         self._trial_id = None
         self._stop = False
         self.completed_trials = []
+        self.busy_s = 0.0  # wall seconds spent inside trials (train + evaluate + dump), for idle accounting
+        self.first_trial_t = None   # perf_counter at the first / after the last trial (idle accounting)
+        self.last_trial_end_t = None
+        self.gap_parts = {'claim': 0.0, 'propose': 0.0}  # async-loop seconds outside trials
 
     # ------------------------------------------------------------------------------ main loop
     def start(self):
@@ -92,7 +100,7 @@ class TrainWorker:
         data_parallel = bool(getattr(clazz, 'DATA_PARALLEL', False)) and info.world_size > 1
         advisor = make_advisor(knob_config, self._advisor_type, self._seed) if info.is_main else None
         device = default_device()
-        if self._scheduling == 'async' and not data_parallel:
+        if self._scheduling in ('async', 'auto') and not data_parallel:
             return self._start_async(clazz, model, sub, train_job, knob_config, max_trials, deadline, device)
         errors = 0
         # trials this worker was running when its previous incarnation died, with a checkpoint to
@@ -133,6 +141,7 @@ class TrainWorker:
                 score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, record,
                                             resume_id=None if data_parallel else resume_ids[my])
                 secs = time.time() - t0
+                self.busy_s += secs
             table = D.gather_floats(info, [score if ok else float('nan'), ok, secs, float(active)])
             if info.is_main:
                 for r in range(info.world_size):
@@ -154,32 +163,55 @@ class TrainWorker:
           sub-train-job) with every in-flight trial's knobs as constant-liar pending points, so
           concurrent proposals spread out exactly as in a batched proposal;
         * end: when the budget is exhausted, a last barrier and rank 0 closes the sub-train-job."""
+        import concurrent.futures as cf
         info = self._dist
         errors = 0
         n_local = 0
-        while not self._stop and errors < self._max_trial_errors:
-            if deadline is not None and time.time() > deadline:
-                break
-            trial = self._db.claim_trial(sub.id, model.id, self._worker_id, max_trials)
-            if trial is None:
-                break
-            history, pending = [], []
+        # propose-ahead: the knobs of this rank's NEXT trial are computed on a helper thread while the
+        # current trial runs (the current trial is one of the constant-liar pending points, exactly as
+        # in a batched proposal), so the GP fit never sits between two trials on the GPU
+        pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix='rafiki-advisor')
+
+        def propose(trial_id, extra_pending, salt):
+            history, pending = [], list(extra_pending)
             for t in self._db.get_trials_of_sub_train_job(sub.id):
-                if t.id == trial.id or not t.knobs:
+                if t.id == trial_id or not t.knobs:
                     continue
                 if t.status == TrialStatus.COMPLETED:
                     history.append((dict(t.knobs), float(t.score)))
                 elif t.status in (TrialStatus.STARTED, TrialStatus.RUNNING):
                     pending.append(dict(t.knobs))
-            seed = None if self._seed is None else int(self._seed) * 1000003 + info.rank * 7919 + n_local
+            seed = None if self._seed is None else int(self._seed) * 1000003 + info.rank * 7919 + salt
             adv = make_advisor(knob_config, self._advisor_type, seed)
             adv.history.extend(history)
             adv._pending.extend(pending)
-            knobs = adv.propose()
-            ctx = TrialContext(device=device, dist=info, data_parallel=False)
-            score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, True, resume_id=trial.id)
-            errors = errors + 1 if not ok else 0
-            n_local += 1
+            return adv.propose()
+
+        ahead = None
+        try:
+            while not self._stop and errors < self._max_trial_errors:
+                if deadline is not None and time.time() > deadline:
+                    break
+                tc = time.perf_counter()
+                trial = self._db.claim_trial(sub.id, model.id, self._worker_id, max_trials)
+                self.gap_parts['claim'] += time.perf_counter() - tc
+                if trial is None:
+                    break
+                th = time.perf_counter()
+                knobs = ahead.result() if ahead is not None else propose(trial.id, [], n_local)
+                self.gap_parts['propose'] += time.perf_counter() - th
+                ahead = pool.submit(propose, None, [dict(knobs)], n_local + 1)
+                ctx = TrialContext(device=device, dist=info, data_parallel=False)
+                t0 = time.perf_counter()
+                if self.first_trial_t is None:
+                    self.first_trial_t = t0
+                score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, True, resume_id=trial.id)
+                self.last_trial_end_t = time.perf_counter()
+                self.busy_s += self.last_trial_end_t - t0
+                errors = errors + 1 if not ok else 0
+                n_local += 1
+        finally:
+            pool.shutdown(wait=True)
         if info.world_size > 1:
             D.barrier(info)
         if info.is_main:
