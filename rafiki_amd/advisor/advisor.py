@@ -27,18 +27,6 @@ from ..model.knob import (CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, de
                           knob_space_dims)
 
 
-def _one_blas_thread():
-    """The GP's matrices are tiny (tens of observations): multi-threaded BLAS only adds spin-waiting,
-    and with one trial worker per GPU on a node those spinning pools steal each other's cores (a
-    4-worker node measured 40-50 ms per proposal instead of 6)."""
-    try:
-        from threadpoolctl import threadpool_limits
-    except ImportError:  # pragma: no cover
-        import contextlib
-        return contextlib.nullcontext()
-    return threadpool_limits(limits=1, user_api='blas')
-
-
 def _simplify(v):
     if isinstance(v, (np.integer,)):
         return int(v)
@@ -58,13 +46,13 @@ class BaseAdvisor:
         self._pending = []
 
     def propose(self):
-        with self._lock, _one_blas_thread():
+        with self._lock:
             knobs = self._propose_locked(1)[0]
             self._pending.append(knobs)
             return knobs
 
     def propose_batch(self, q):
-        with self._lock, _one_blas_thread():
+        with self._lock:
             out = self._propose_locked(q)
             self._pending.extend(out)
             return out
