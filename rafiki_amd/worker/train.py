@@ -188,6 +188,16 @@ class TrainWorker:
             return adv.propose()
 
         ahead = None
+        # trials this worker was running when its previous incarnation died, with a checkpoint to
+        # resume from: they keep their ids, knobs and budget slot, and run first
+        for tid, knobs in self._orphaned_trials(sub.id):
+            if self._stop:
+                break
+            ctx = TrialContext(device=device, dist=info, data_parallel=False)
+            t0 = time.perf_counter()
+            score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, True, resume_id=tid)
+            self.busy_s += time.perf_counter() - t0
+            errors = errors + 1 if not ok else 0
         try:
             while not self._stop and errors < self._max_trial_errors:
                 if deadline is not None and time.time() > deadline:
