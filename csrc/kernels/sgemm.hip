@@ -251,10 +251,10 @@ RK_DEV void s_group_sched() {
 RK_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 template <int MI, int NI>
-RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int nbase, int lane) {
+RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int nbase, int lane, int split) {
   const int fl = p.flags;
   const int h = lane >> 5;
-  float* C = p.out + (long long)blockIdx.z * p.slabStride;
+  float* C = p.out + (long long)split * p.slabStride;
   const bool want_sums = fl & (SF_STATS | SF_BNB | SF_BNP);
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
@@ -333,11 +333,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid - (wid / WGN) * WGN;
   const int tilesN = (p.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = ((p.M + BM - 1) / BM) * tilesN;
+  // 1-D grid of tiles x splits; the XCD-aware remap deals each XCD a contiguous range of logical ids
+  // ordered (split, tile), so the tiles that share a split's K range (the same dY / X pixel rows of a
+  // weight gradient) run on one XCD and hit one L2
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / tiles;
+  const int bid = lin - split * tiles;
   const int mt = bid / tilesN, nt = bid - mt * tilesN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int nk = (p.K + SBK - 1) / SBK;
-  const int kt0 = blockIdx.z * p.ktPer;
+  const int kt0 = split * p.ktPer;
   const int kt1 = min(nk, kt0 + p.ktPer);
 
   SOperand<AM, BM, NW> A;
@@ -423,14 +429,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
     st = st + 1 == NST ? 0 : st + 1;
   }
   s_wait_vmcnt<0>();  // the trailing zero-DMAs land before the workgroup's LDS is released
-  s_epilogue<MI, NI>(p, acc, m0 + wm * WMT, n0 + wn * WNT, lane);
+  s_epilogue<MI, NI>(p, acc, m0 + wm * WMT, n0 + wn * WNT, lane, split);
 }
 
 template <int WGM, int WGN, int MI, int NI, int AM, int BMD>
 int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
   const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
-  dim3 grid(tiles, 1, splits);
+  dim3 grid(tiles * splits);
   if (nst == 3) {
     if constexpr (WGM * WGN == 4)  // 3-stage rings only for the 4-wave tiles (8-wave ones fill LDS at 2)
       hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3>), grid, dim3(64 * WGM * WGN), 0, st, p);
@@ -472,7 +478,7 @@ int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t 
 // gradient (A = dy [K = pixels][M = Cout] K-outer, B = x gathered [K = pixels][N = taps*C]),
 // 3 dense A·Bᵀ (A [M][K], B [N][K]), 4 dense dX A·B (A [M][K], B [K][N]), 5 dense dW Aᵀ·B
 // (A [K][M], B [K][N]).  tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64.  nst: LDS ring stages (2, 3).
-// splits > 1: fp32 slabs out + z * slabStride (combine with rk_reduce_slabs / rk_sreduce_epi).
+// splits > 1: fp32 slabs out + split * slabStride (combine with rk_reduce_slabs / rk_sreduce_epi).
 // flags: SF_* above; stats = fp64 slots [slotMask+1][2][N] (zeroed by the caller).
 extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float* B, float* C, const float* bias,
                         double* stats, int slotMask, const float* gate, int M, int N, int K, int lda, int ldb,
