@@ -217,7 +217,32 @@ struct SOperand {
       return f32x4{t[0], t[T], t[2 * T], t[3 * T]};
     }
   }
+
+  // K-outer, two 32-row blocks at once with INTERLEAVED rows (block b, lane row r <-> tile row
+  // r0 + 2r + b): one ds_read_b64 per k feeds both blocks, halving the LDS read instructions of the
+  // weight-gradient operands.  The epilogue maps the rows back (s_epilogue PA / PB).
+  RK_DEV void frag_pair(const char* tile, int r0, int g, int lane, f32x4& f0, f32x4& f1) const {
+    const int h = lane >> 5;
+    const float* t = (const float*)tile + (8 * g + 4 * h) * T + r0 + 2 * (lane & 31);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float2 v = *(const float2*)(t + e * T);
+      f0[e] = v.x;
+      f1[e] = v.y;
+    }
+  }
 };
+
+// fragment loads of one operand for one k-group: MI (or NI) 32-row blocks of the wave's slab
+template <class OP, int NB>
+RK_DEV void load_frags(const OP& op, const char* tile, int r0, int g, int lane, f32x4 (&f)[NB]) {
+  if constexpr (!OP::KIN && NB == 2) {
+    op.frag_pair(tile, r0, g, lane, f[0], f[1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) f[i] = op.frag(tile, r0 + i * 32, g, lane);
+  }
+}
 
 template <int N>
 RK_DEV void s_wait_vmcnt() {
@@ -250,7 +275,8 @@ RK_DEV void s_group_sched() {
 // accumulator register r of a 32x32 block: row (r&3) + 8(r>>2) + 4h, column lane&31
 RK_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-template <int MI, int NI>
+// PA / PB: the A (rows) / B (columns) fragments were read interleaved (frag_pair)
+template <int MI, int NI, bool PA, bool PB>
 RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int nbase, int lane, int split) {
   const int fl = p.flags;
   const int h = lane >> 5;
@@ -258,7 +284,7 @@ RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int 
   const bool want_sums = fl & (SF_STATS | SF_BNB | SF_BNP);
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
-    const int n = nbase + ni * 32 + (lane & 31);
+    const int n = PB ? nbase + 2 * (lane & 31) + ni : nbase + ni * 32 + (lane & 31);
     const bool nok = n < p.N;
     float b = 0.f, sh = 0.f;
     if ((fl & (SF_BIAS | SF_BNB | SF_BNP)) && nok) b = p.bias[n];
@@ -268,7 +294,7 @@ RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int 
     for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = mbase + mi * 32 + acc_row(r, h);
+        const int m = PA ? mbase + 2 * acc_row(r, h) + mi : mbase + mi * 32 + acc_row(r, h);
         if (!(nok && m < p.M)) continue;
         float v = acc[mi][ni][r] * p.alpha;
         const long long idx = (long long)m * p.ldc + n;
@@ -384,25 +410,22 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
     const bool more = kt + NST - 1 < kt1;
     char* nxt = smem + (st == 0 ? NST - 1 : st - 1) * SB;  // stage of tile kt + NST - 1
     // Fragments are double-buffered in registers (group g+1 is read from LDS while group g's MFMAs
-    // run) and the next tile's DMAs are spread over the first two groups' MFMAs; the schedule is
+    // run) and the next tile's DMAs go out among the first group's MFMAs; the schedule is
     // pinned with sched_group_barrier (left alone, hipcc sinks the reads behind the MFMAs they should
     // overlap and clusters the DMA issue in front of them).
     constexpr int NMF = 4 * MI * NI;
-    constexpr int RA = A.KIN ? MI : 4 * MI, RB = B.KIN ? NI : 4 * NI;  // LDS read instructions per group
+    // LDS read instructions per group
+    constexpr int RA = A.KIN ? MI : (MI == 2 ? 4 : 4 * MI), RB = B.KIN ? NI : (NI == 2 ? 4 : 4 * NI);
     constexpr int DA = BM / (8 * NW), DB = BN / (8 * NW);              // DMA instructions per wave
     f32x4 a[2][MI], b[2][NI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i) a[0][i] = A.frag(As, wm * WMT + i * 32, 0, lane);
-#pragma unroll
-    for (int j = 0; j < NI; ++j) b[0][j] = B.frag(Bs, wn * WNT + j * 32, 0, lane);
+    load_frags(A, As, wm * WMT, 0, lane, a[0]);
+    load_frags(B, Bs, wn * WNT, 0, lane, b[0]);
 #pragma unroll
     for (int g = 0; g < SBK / 8; ++g) {
       const int cur = g & 1;
       if (g + 1 < SBK / 8) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i) a[cur ^ 1][i] = A.frag(As, wm * WMT + i * 32, g + 1, lane);
-#pragma unroll
-        for (int j = 0; j < NI; ++j) b[cur ^ 1][j] = B.frag(Bs, wn * WNT + j * 32, g + 1, lane);
+        load_frags(A, As, wm * WMT, g + 1, lane, a[cur ^ 1]);
+        load_frags(B, Bs, wn * WNT, g + 1, lane, b[cur ^ 1]);
       }
       // the reads above may not sink below this group's MFMAs (that would collapse the two fragment
       // register sets into one and expose the LDS latency at every group boundary)
@@ -429,7 +452,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
     st = st + 1 == NST ? 0 : st + 1;
   }
   s_wait_vmcnt<0>();  // the trailing zero-DMAs land before the workgroup's LDS is released
-  s_epilogue<MI, NI>(p, acc, m0 + wm * WMT, n0 + wn * WNT, lane, split);
+  s_epilogue<MI, NI, !SOperand<AM, BM, NW>::KIN && MI == 2, !SOperand<BMD, BN, NW>::KIN && NI == 2>(
+      p, acc, m0 + wm * WMT, n0 + wn * WNT, lane, split);
 }
 
 template <int WGM, int WGN, int MI, int NI, int AM, int BMD>
