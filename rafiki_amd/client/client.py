@@ -6,9 +6,11 @@ against a running predictor, and ``create_inference_job(..., max_models=k)`` for
 """
 from __future__ import annotations
 
+import functools
 import json
 import os
 import pickle
+import warnings
 
 import requests
 
@@ -17,6 +19,17 @@ from ..constants import ModelAccessRight
 
 class RafikiConnectionError(ConnectionError):
     pass
+
+
+def _removed(msg):
+    """Method kept for API compatibility that only warns (reference client.py:14-27, 123-125, 278-284)."""
+    def deco(func):
+        @functools.wraps(func)
+        def shim(*args, **kwargs):
+            warnings.warn('{} (see docs/api.md)'.format(msg), DeprecationWarning, stacklevel=2)
+            return None
+        return shim
+    return deco
 
 
 class Client:
@@ -54,6 +67,10 @@ class Client:
     def ban_user(self, email):
         return self._delete('/users', json={'email': email})
 
+    @_removed('`create_users` has been removed; call `create_user` per user')
+    def create_users(self, *args, **kwargs):
+        pass
+
     # ------------------------------------------------------------------------------ models
     def create_model(self, name, task, model_file_path, model_class, dependencies=None,
                      access_right=ModelAccessRight.PRIVATE, docker_image=None):
@@ -76,6 +93,14 @@ class Client:
 
     def get_available_models(self, task=None):
         return self._get('/models/available', params={'task': task} if task else {})
+
+    @_removed('`get_models` & `get_models_of_task` have been combined into `get_available_models`')
+    def get_models(self, *args, **kwargs):
+        pass
+
+    @_removed('`get_models` & `get_models_of_task` have been combined into `get_available_models`')
+    def get_models_of_task(self, *args, **kwargs):
+        pass
 
     def delete_model(self, model_id):
         return self._delete('/models/{}'.format(model_id))

@@ -70,6 +70,13 @@ def test_users_rbac(stack):
         admin_c.ban_user(admin_email)
 
 
+def test_deprecated_client_methods_warn():
+    c = Client(admin_host='127.0.0.1', admin_port=1)
+    for name in ('create_users', 'get_models', 'get_models_of_task'):
+        with pytest.warns(DeprecationWarning):
+            assert getattr(c, name)('anything', task='X') is None
+
+
 def test_models_crud_and_isolation(stack, tmp_path):
     dev_c, _ = make_user(stack, UserType.MODEL_DEVELOPER)
     other_c, _ = make_user(stack, UserType.MODEL_DEVELOPER)
