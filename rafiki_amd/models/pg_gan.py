@@ -16,6 +16,14 @@ predict contract ([grid_w, grid_h, n_images] -> JPEG file paths).  Re-designed f
   is split across them (pg_gans.py:290-293) and gradients are averaged by bucketed RCCL
   all-reduces over the flat gradient arena, overlapped with backward
   (``parallel.grad_bucket``; replaces the per-variable NCCL all-sum at pg_gans.py:1164-1171);
+* every rank draws the GLOBAL minibatch's indices / latents / mixing factors from one shared Philox
+  stream and keeps its strided shard (the columns of the [group, N/group] minibatch-stddev layout),
+  so N ranks x N/N-th of the minibatch compute exactly the 1-rank step (tests/test_pg_gan.py);
+* DP rounds on RCCL are captured in hipGraphs like single-GPU rounds, the bucketed all-reduces
+  included (``GraphedRounds``);
+* mid-trial checkpoint / resume (the reference only pickles at trial end,
+  pg_gans.py:219-232): G / D / Gs, both Adam states, the RNG counter and the schedule position,
+  saved by rank 0 every ``checkpoint_secs`` and broadcast to every rank on resume;
 * the non-finite-gradient guard (pg_gans.py:1180-1191) is a device flag read by the Adam kernel,
   so no host sync per step;
 * all work at the native resolution of the current level of detail: the reference upsamples G's
@@ -33,6 +41,7 @@ import math
 import os
 import pickle
 import tempfile
+import time
 import uuid
 
 import numpy as np
@@ -515,8 +524,51 @@ class PgGan(BaseModel):
         return img[..., :self.nets.num_channels]
 
     # ------------------------------------------------------------------ train
+    def _shard(self, t):
+        """Rank's part of a global-minibatch draw: the global batch is laid out [g, world, mb/g] in
+        minibatch-stddev group order (sample n -> group n % (N/g)), and a rank keeps its column block,
+        so every mbstd group lives on one rank and the local grouping reproduces the global one."""
+        if self.world == 1:
+            return t
+        mb = t.shape[0] // self.world
+        g = min(self.nets.mbstd_group_size, mb)
+        return t.reshape(g, self.world, mb // g, *t.shape[1:])[:, self.rank].reshape(mb, *t.shape[1:])
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def _ckpt_state(self, G_opt, D_opt, rng, cur_nimg, prev_lod, tick):
+        nets = self.nets
+
+        def host(t):
+            return t.detach().cpu().numpy().copy()
+        st = {'G': host(nets.G.master), 'D': host(nets.D.master), 'Gs': host(nets.Gs_master),
+              'opt': {k: [host(o.m), host(o.v), host(o.t)] for k, o in (('G', G_opt), ('D', D_opt))},
+              'cur_nimg': int(cur_nimg), 'prev_lod': float(prev_lod), 'tick': int(tick), 'stats': dict(self.stats),
+              'meta': dict(self._meta)}
+        st['rng'] = host(rng.step) if rng.device.type == 'cuda' else rng.gen.get_state().numpy().copy()
+        return st
+
+    def _restore_ckpt(self, st, G_opt, D_opt, rng):
+        nets = self.nets
+        nets.G.master.copy_(torch.as_tensor(st['G']))
+        nets.D.master.copy_(torch.as_tensor(st['D']))
+        nets.Gs_master.copy_(torch.as_tensor(st['Gs']))
+        nets.G.sync_bf16()
+        nets.D.sync_bf16()
+        nets.Gs_bf16.copy_(nets.Gs_master)
+        for k, o in (('G', G_opt), ('D', D_opt)):
+            for t, v in zip((o.m, o.v, o.t), st['opt'][k]):
+                t.copy_(torch.as_tensor(v))
+        if rng.device.type == 'cuda':
+            rng.step.copy_(torch.as_tensor(st['rng']))
+        else:
+            rng.gen.set_state(torch.as_tensor(st['rng']))
+        self.stats = dict(st['stats'])
+        return int(st['cur_nimg']), float(st['prev_lod']), int(st['tick'])
+
     def train(self, dataset_uri, **overrides):
+        from rafiki_amd.parallel import dist as D
         from rafiki_amd.parallel.grad_bucket import FlatGradAllReduce
+        from rafiki_amd.utils import faults
         knobs = dict(self._knobs, **overrides)
         ds = load_gan_dataset(dataset_uri)
         if self.nets is None:
@@ -536,16 +588,34 @@ class PgGan(BaseModel):
         for opt in (G_opt, D_opt):
             opt.skip_flag = torch.zeros(1, dtype=torch.int32, device=dev)
         g_ar = d_ar = None
-        if self.world > 1:
-            g_ar = FlatGradAllReduce(nets.G.grad, nets.G.param_ranges(), list(nets.g_params.values()), self.world)
-            d_ar = FlatGradAllReduce(nets.D.grad, nets.D.param_ranges(), list(nets.d_params.values()), self.world)
-        rng = TrialRng(dev, self.seed * 7919 + self.rank)
-        graphs = GraphedRounds(dev.type == 'cuda' and self.world == 1 and bool(knobs.get('cuda_graph', True))
+        # force_grad_allreduce: run the bucketed all-reduce path even on one rank (a 1-rank RCCL
+        # group rehearses capture of the DP round on a single GPU)
+        if self.world > 1 or bool(knobs.get('force_grad_allreduce', False)):
+            force = self.world == 1
+            g_ar = FlatGradAllReduce(nets.G.grad, nets.G.param_ranges(), list(nets.g_params.values()), self.world,
+                                     force=force)
+            d_ar = FlatGradAllReduce(nets.D.grad, nets.D.param_ranges(), list(nets.d_params.values()), self.world,
+                                     force=force)
+        rng = TrialRng(dev, self.seed * 7919)   # one stream for all ranks; each keeps its shard
+        # RCCL collectives are graph-capturable, gloo ones are not (a gloo group on GPUs is the
+        # one-box multi-rank rehearsal: eager)
+        capturable = g_ar is None or self.ctx.dist.backend == 'nccl'
+        graphs = GraphedRounds(dev.type == 'cuda' and capturable and bool(knobs.get('cuda_graph', True))
                                and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0')
+        self.graphs = graphs
         acc = torch.zeros(6, dtype=torch.float32, device=dev)
         level_cache = {}
         labels_all = torch.as_tensor(ds.labels, device=dev)
         cur_nimg, prev_lod, tick = 0, -1.0, 0
+        ck = self.ctx.checkpoint if self.rank == 0 else None
+        saved = ck.load() if ck is not None else None
+        if self.world > 1:
+            saved = D.broadcast_object(self.ctx.dist, saved)
+        if saved is not None:
+            cur_nimg, prev_lod, tick = self._restore_ckpt(saved['state'], G_opt, D_opt, rng)
+            logger.log('resumed from checkpoint at tick {} ({:.3f} kimg)'.format(tick, cur_nimg / 1000.0))
+        ckpt_secs = float(knobs.get('checkpoint_secs', 60.0))
+        last_ckpt = time.monotonic()
         logger.define_plot('Losses', ['D_loss', 'G_loss'], x_axis='kimg')
         logger.define_plot('Scores', ['real_score', 'fake_score', 'grad_norm'], x_axis='kimg')
         while cur_nimg < total_kimg * 1000:
@@ -587,18 +657,22 @@ class PgGan(BaseModel):
                               D_loss=float(a[0] / nD), real_score=float(a[1] / nD), fake_score=float(a[2] / nD),
                               grad_norm=float(a[3] / nD), G_loss=float(a[4] / nG))
             logger.log('tick {}'.format(tick), **self.stats)
+            if ck is not None and cur_nimg < total_kimg * 1000 and time.monotonic() - last_ckpt >= ckpt_secs:
+                ck.save(self._ckpt_state(G_opt, D_opt, rng, cur_nimg, prev_lod, tick), tick)
+                last_ckpt = time.monotonic()
+            faults.maybe_fail('crash', tick=tick, rank=self.rank)
         self.lod = prev_lod if prev_lod >= 0 else 0.0
         if g_ar is not None:
             g_ar.remove()
             d_ar.remove()
 
     def _latents(self, n, rng, sid):
-        return rng.randn((n, self.nets.latent_size), sid)
+        return self._shard(rng.randn((n * self.world, self.nets.latent_size), sid))
 
     def _rand_labels(self, labels_all, n, rng):
         if self.nets.label_size == 0:
             return torch.zeros((n, 0), device=self.device)
-        idx = rng.randint(labels_all.shape[0], n, TrialRng.G_LAB)
+        idx = self._shard(rng.randint(labels_all.shape[0], n * self.world, TrialRng.G_LAB))
         return labels_all.index_select(0, idx.to(labels_all.device))
 
     def train_round(self, lod, mb, level, labels_all, rng, G_opt, D_opt, acc, *, D_repeats=1, G_smoothing=0.99,
@@ -627,7 +701,7 @@ class PgGan(BaseModel):
         nets.set_requires_grad(nets.g_params, False)
         nets.set_requires_grad(nets.d_params, True)
         nets.D.grad.zero_()
-        idx = rng.randint(level.shape[0], mb, TrialRng.D_IDX).to(level.device)
+        idx = self._shard(rng.randint(level.shape[0], mb * self.world, TrialRng.D_IDX)).to(level.device)
         reals = self._reals(level, idx, lod - math.floor(lod))
         labels = labels_all.index_select(0, idx) if nets.label_size else torch.zeros((mb, 0), device=self.device)
         with torch.no_grad():
@@ -638,7 +712,7 @@ class PgGan(BaseModel):
         real_s, fake_s = rf_s[:mb], rf_s[mb:]
         real_l, fake_l = rf_l[:mb], rf_l[mb:]
         loss = fake_s - real_s
-        alpha = rng.rand((mb, 1, 1, 1), TrialRng.D_ALPHA)
+        alpha = self._shard(rng.rand((mb * self.world, 1, 1, 1), TrialRng.D_ALPHA))
         mixed = (reals.float() + (fakes.float() - reals.float()) * alpha).to(reals.dtype).detach().requires_grad_(True)
         mixed_s, _ = nets.discriminator(PD, mixed, lod)
         if ar is not None:

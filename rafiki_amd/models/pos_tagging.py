@@ -16,6 +16,19 @@ from rafiki_amd.constants import TaskType  # noqa: F401
 from rafiki_amd.model import (BaseModel, CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, dataset_utils,
                               logger)
 from rafiki_amd.parallel.context import current as trial_context
+from rafiki_amd.utils import faults
+
+
+def _to_cpu(obj):
+    """Nested state dicts with every tensor on the host (picklable, device-independent)."""
+    import torch
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
 
 
 def _accuracy(sents, preds):
@@ -178,18 +191,50 @@ class PyBiLstm(BaseModel):
         tags = [[t[1] for t in s] for s in sents]
         rng = np.random.default_rng(0)
         logger.define_loss_plot()
-        for ep in range(int(self._knobs.get('epochs', 10))):
+        epochs = int(self._knobs.get('epochs', 10))
+        ck = trial_context().checkpoint
+        start = 0
+        saved = ck.load() if ck is not None else None
+        if saved is not None:
+            self._restore_ckpt(saved['state'], opt, rng)
+            start = int(saved['epoch']) + 1
+            logger.log('resumed from checkpoint after epoch {}'.format(saved['epoch']))
+        for ep in range(start, epochs):
             self._net.train()
-            tot, n = 0.0, 0
+            tot = torch.zeros((), device=self.device)
+            n = 0
             for _, x, y in self._batches(ids, tags, int(self._knobs.get('batch_size', 32)), True, rng):
                 logits = self._net(x)
                 loss = F.cross_entropy(logits.reshape(-1, self._tag_count), y.reshape(-1), ignore_index=-100)
                 opt.zero_grad()
                 loss.backward()
                 opt.step()
-                tot += float(loss.item())
+                tot += loss.detach()   # summed on the device: one host sync per epoch
                 n += 1
-            logger.log_loss(loss=tot / max(1, n), epoch=ep)
+            logger.log_loss(loss=float(tot.item()) / max(1, n), epoch=ep)
+            if ck is not None and ck.due(ep) and ep + 1 < epochs:
+                ck.save(self._ckpt_state(opt, rng), ep)
+            faults.maybe_fail('crash', epoch=ep, rank=0)
+
+    # ----------------------------------------------------------------- checkpoint / resume
+    def _ckpt_state(self, opt, rng):
+        """Weights, Adam moments, and every RNG the epoch loop draws from (batch shuffling, dropout):
+        the reference saves model + optimizer state (PyBiLstm.py:66-84)."""
+        import torch
+        st = {'net': _to_cpu(self._net.state_dict()), 'opt': _to_cpu(opt.state_dict()),
+              'np_rng': rng.bit_generator.state, 'torch_rng': torch.get_rng_state()}
+        if self.device.type == 'cuda':
+            st['cuda_rng'] = torch.cuda.get_rng_state(self.device)
+        return st
+
+    def _restore_ckpt(self, st, opt, rng):
+        import torch
+        self._net.load_state_dict(st['net'])
+        opt.load_state_dict(st['opt'])
+        rng.bit_generator.state = st['np_rng']
+        torch.set_rng_state(st['torch_rng'])
+        if self.device.type == 'cuda' and 'cuda_rng' in st:
+            torch.cuda.set_rng_state(st['cuda_rng'], self.device)
 
     def _predict(self, sents_tokens):
         import torch

@@ -38,9 +38,13 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> Dis
     if ws <= 1:
         return DistInfo(0, 1, local, 'none')
     if backend is None:
-        # RAFIKI_DIST_BACKEND=gloo rehearses multi-rank control paths on a one-GPU box (ranks share
-        # the device; RCCL needs one GPU per rank)
-        backend = os.environ.get('RAFIKI_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
+        # NodeConfig.dist_backend (RAFIKI_DIST_BACKEND; gloo rehearses multi-rank control paths on a
+        # one-GPU box, ranks sharing the device); RCCL needs one GPU per rank, so a host without GPUs
+        # falls back to gloo
+        from ..config import NodeConfig
+        backend = NodeConfig().dist_backend
+        if backend == 'nccl' and not torch.cuda.is_available():
+            backend = 'gloo'
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     os.environ.setdefault('MASTER_PORT', '29500')
     if backend == 'nccl':

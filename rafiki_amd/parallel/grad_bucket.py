@@ -28,12 +28,20 @@ import torch.distributed as dist
 
 class FlatGradAllReduce:
     def __init__(self, grad: torch.Tensor, param_ranges: Sequence[Tuple[int, int]], params: Sequence[torch.Tensor],
-                 world_size: int, group=None, bucket_mb: float = 24.0, overlap: bool = True):
-        """grad: flat fp32 buffer; param_ranges[i] = (offset, numel) of params[i] inside it."""
+                 world_size: int, group=None, bucket_mb: Optional[float] = None, overlap: bool = True,
+                 force: bool = False):
+        """grad: flat fp32 buffer; param_ranges[i] = (offset, numel) of params[i] inside it.
+        bucket_mb: default NodeConfig.grad_bucket_mb (RAFIKI_GRAD_BUCKET_MB).  force: issue the
+        collectives even for a 1-rank group (single-GPU rehearsal of the DP path)."""
+        if bucket_mb is None:
+            from ..config import NodeConfig
+            bucket_mb = NodeConfig().grad_bucket_mb
+        self.bucket_mb = float(bucket_mb)
         self.grad = grad
         self.world = int(world_size)
         self.group = group
-        self.overlap = overlap and self.world > 1
+        self.force = bool(force)
+        self.overlap = overlap and (self.world > 1 or self.force)
         cap = max(1, int(bucket_mb * (1 << 20)) // 4)
         order = sorted(range(len(param_ranges)), key=lambda i: -param_ranges[i][0])  # reverse arena order
         self.buckets: List[Tuple[int, int]] = []
@@ -104,7 +112,7 @@ class FlatGradAllReduce:
 
     def finish(self, average: bool = True):
         self.active = False
-        if self.world <= 1:
+        if self.world <= 1 and not self.force:
             return
         for b in range(len(self.buckets)):
             if not self._launched[b]:

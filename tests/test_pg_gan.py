@@ -223,3 +223,83 @@ def test_pg_gan_data_parallel_gloo():
     for k in ('G', 'D', 'Gs'):
         assert torch.equal(r0[k], r1[k]), k
     assert not torch.equal(r0['stats'], r1['stats'])  # each rank saw its own minibatch shard
+
+
+def _dp_equiv_worker(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rafiki_amd.models.pg_gan import PgGan
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    info = D.init_distributed(backend='gloo')
+    with use_context(TrialContext(device=torch.device('cpu'), dist=info, data_parallel=True)):
+        m = PgGan(**EQUIV)
+        m.train(DATA)
+        torch.save({'G': m.nets.G.master.clone(), 'D': m.nets.D.master.clone(), 'Gs': m.nets.Gs_master.clone()},
+                   os.path.join(out_dir, 'r{}.pt'.format(rank)))
+    D.destroy(info)
+
+
+# 8 rounds of 128 (2 ranks x 64: 16 minibatch-stddev groups each) through a 4x4 -> 8x8 LOD fade
+EQUIV = dict(TINY, minibatch_base=8, total_kimg=1.0, lod_training_kimg=0.3, lod_transition_kimg=0.3)
+
+
+def test_pg_gan_dp_two_half_batches_equal_one_full_batch():
+    """2 ranks x half minibatch == 1 rank x full minibatch (same shared RNG stream, strided shards,
+    averaged bucketed all-reduce), up to fp32 summation order — a wrong averaging scale, a shard
+    that double-counts samples or per-rank data streams all fail this."""
+    from rafiki_amd.models.pg_gan import PgGan
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    with use_context(TrialContext(device=torch.device('cpu'))):
+        m = PgGan(**EQUIV)
+        m.train(DATA)
+        ref = {'G': m.nets.G.master.clone(), 'D': m.nets.D.master.clone(), 'Gs': m.nets.Gs_master.clone()}
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dp_equiv_worker, args=(2, port, d), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, 'r0.pt'), weights_only=True)
+        r1 = torch.load(os.path.join(d, 'r1.pt'), weights_only=True)
+    for k in ('G', 'D', 'Gs'):
+        assert torch.equal(r0[k], r1[k]), k
+        err = ((r0[k] - ref[k]).norm() / ref[k].norm()).item()
+        moved = ((ref[k] - PgGan_init(k)).norm() / ref[k].norm()).item()
+        print('dp-equivalence', k, 'rel err', err, 'moved', moved)
+        assert moved > 1e-5 and err < 1e-5 + 1e-3 * moved, (k, err, moved)
+
+
+def PgGan_init(k):
+    from rafiki_amd.models.pg_gan import PgGan
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    with use_context(TrialContext(device=torch.device('cpu'))):
+        m = PgGan(**EQUIV)
+        from rafiki_amd.models.pg_gan import load_gan_dataset
+        m._build(load_gan_dataset(DATA).shape, 0)
+        return {'G': m.nets.G.master, 'D': m.nets.D.master, 'Gs': m.nets.Gs_master}[k].clone()
+
+
+def test_pg_gan_crash_resume_matches_uninterrupted(tmp_path, monkeypatch):
+    """Checkpoint every tick, crash after tick 2, resume in a fresh model: the final G / D / Gs equal
+    the uninterrupted run's exactly (weights, both Adam states, RNG position and schedule restored)."""
+    from rafiki_amd.models.pg_gan import PgGan
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    from rafiki_amd.utils import faults
+    from rafiki_amd.utils.checkpoint import TrialCheckpoint
+    knobs = dict(TINY, total_kimg=0.5, checkpoint_secs=0)   # 4 ticks of 128 images
+    with use_context(TrialContext(device=torch.device('cpu'))):
+        a = PgGan(**knobs)
+        a.train(DATA)
+    ck = TrialCheckpoint(str(tmp_path), 'trial1')
+    monkeypatch.setenv('RAFIKI_FAULT_INJECT', 'crash:tick=2')
+    faults.reset()
+    with use_context(TrialContext(device=torch.device('cpu'), checkpoint=ck)):
+        with pytest.raises(faults.WorkerCrash):
+            PgGan(**knobs).train(DATA)
+        assert ck.exists()
+        monkeypatch.setenv('RAFIKI_FAULT_INJECT', '')
+        faults.reset()
+        b = PgGan(**knobs)
+        b.train(DATA)
+    assert ck.resumed_from == 2
+    for x, y in ((a.nets.G.master, b.nets.G.master), (a.nets.D.master, b.nets.D.master),
+                 (a.nets.Gs_master, b.nets.Gs_master)):
+        assert torch.equal(x, y)
+    assert a.stats == b.stats and a.lod == b.lod
