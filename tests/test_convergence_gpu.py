@@ -4,15 +4,16 @@ The fp32 engine is itself pinned to fp64 autograd at <= 1e-4 per-parameter gradi
 (tests/test_f32_gpu.py), so it stands in for the reference's fp32 training.  Both engines train the
 full-width VGG-small (the bench model) from the same initial weights on the same batch sequence of
 class-conditional 32x32 images with heavy noise and 20% uniformly relabelled targets (Bayes accuracy
-<= 82%), with nesterov SGD + weight decay.  Every step sees fresh images (38,400 = 300 x 128), so the
-training loss estimates the population loss.  Measured on MI355X (profiles/bf16_vs_fp32_convergence_r2.json,
-written via RAFIKI_CONVERGENCE_OUT): mean window gap 0.04 nats, largest 0.21 (the loss cliff around
-step 175-200 arrives ~10 steps later in bf16), final window 0.005, test accuracy 0.818 vs 0.816.
+<= 82%), with nesterov SGD (lr 0.01, momentum 0.9) + weight decay.  Every step sees fresh images
+(38,400 = 300 x 128), so the training loss estimates the population loss.  Measured on MI355X
+(profiles/bf16_vs_fp32_convergence_r2.json; scripts/convergence_sweep.py): mean window gap 0.019 nats,
+largest 0.089, final window 0.0025, test accuracy 0.815 (fp32) vs 0.818 (bf16).
 Gates:
-  * 25-step window-mean training loss: mean |bf16 - fp32| <= 0.08, max <= 0.35, last window <= 0.05 nats;
+  * 25-step window-mean training loss: mean |bf16 - fp32| <= 0.05, max <= 0.2, last window <= 0.03 nats;
   * held-out accuracy: |bf16 - fp32| <= 2 points, both > 0.7 (chance 0.1).
-The same profile records the multi-epoch (memorising) regime, where bf16 does NOT track fp32 —
-why bf16 stays opt-in.
+The same profile records where bf16 does NOT track fp32 — at lr 0.02 one of four bf16 processes
+collapsed to uniform predictions (fp32 runs are bitwise reproducible and never did), and in the
+multi-epoch memorising regime bf16 generalises far worse — which is why bf16 stays opt-in.
 """
 import json
 import os
@@ -37,13 +38,13 @@ def _copy_params(dst, src):
     dst.flat.sync_bf16()
 
 
-def run(steps=STEPS, seed=5):
+def run(steps=STEPS, seed=5, lr=0.01):
     from rafiki_amd.engine.convnet import ConvNetEngine, VGG_SMALL_CFG
     from rafiki_amd.model.dataset import synthetic_images
     imgs, labels = synthetic_images(N_TRAIN + N_TEST, size=32, channels=3, classes=10, seed=11, noise=96,
                                     flip=0.2)
     engines = {dt: ConvNetEngine(num_classes=10, in_channels=3, image_size=32, cfg=VGG_SMALL_CFG,
-                                 fc_dims=(512,), device='cuda', seed=seed, lr=0.02, momentum=0.9,
+                                 fc_dims=(512,), device='cuda', seed=seed, lr=lr, momentum=0.9,
                                  weight_decay=5e-4, dtype=dt) for dt in ('fp32', 'bf16')}
     _copy_params(engines['bf16'], engines['fp32'])
     order = np.random.default_rng(seed).permutation(np.tile(np.arange(N_TRAIN), steps * BATCH // N_TRAIN + 1))
@@ -94,7 +95,7 @@ def test_bf16_tracks_fp32_over_300_steps_non_separable():
         with open(os.environ['RAFIKI_CONVERGENCE_OUT'], 'w') as f:
             json.dump(s, f, indent=1)
     assert s['window_loss_fp32'][-1] < s['window_loss_fp32'][0] - 0.3, s   # it actually learns
-    assert s['mean_window_gap'] <= 0.08 and s['max_window_gap'] <= 0.35, s
-    assert s['last_window_gap'] <= 0.05, s
+    assert s['mean_window_gap'] <= 0.05 and s['max_window_gap'] <= 0.2, s
+    assert s['last_window_gap'] <= 0.03, s
     assert abs(s['acc_fp32'] - s['acc_bf16']) <= 0.02, s
     assert min(s['acc_fp32'], s['acc_bf16']) > 0.7, s   # chance is 0.1, Bayes ceiling ~0.82
