@@ -7,8 +7,9 @@ Placement model (MI355X-first):
     sub-train-job's advisor and broadcasts one knob set per rank per round, so every GPU runs its
     own trial while sharing one GP posterior (fixes reference bug (d): one advisor per worker);
     a sub-train-job with 0 GPUs gets one CPU worker (reference :123-126);
-  * an inference job is ONE predictor service on one GPU holding all top-k models in HBM
-    (288 GB/GPU), with one logical ``INFERENCE`` service row per model for API parity.
+  * an inference job is ONE predictor service holding all top-k models in HBM (288 GB/GPU) on
+    RAFIKI_PREDICTOR_GPUS GPUs (default 1), as INFERENCE_WORKER_REPLICAS_PER_TRIAL replicas of the
+    whole ensemble, with one logical ``INFERENCE`` service row per model for API parity.
 """
 from __future__ import annotations
 
@@ -61,7 +62,7 @@ class ServicesManager:
             predictor = self._create_service(
                 ServiceType.PREDICT, PREDICTOR_IMAGE, args=['-m', 'rafiki_amd.predictor.server'],
                 environment_vars={'RAFIKI_INFERENCE_JOB_ID': inference_job.id},
-                container_port=self._cfg.predictor_port, gpus=1 if self._gpus_available() else 0,
+                container_port=self._cfg.predictor_port, gpus=self._predictor_gpus(),
                 before_launch=lambda s: self._db.update_inference_job(inference_job, predictor_service_id=s.id))
             for w in workers:
                 self._db.update_service_container_info(w, predictor.container_service_id, None, None, None, None,
@@ -74,6 +75,13 @@ class ServicesManager:
         except Exception:
             self._db.mark_inference_job_as_errored(inference_job)
             raise
+
+    def _predictor_gpus(self):
+        """GPUs for the predictor service: RAFIKI_PREDICTOR_GPUS (default 1); its replicas
+        (INFERENCE_WORKER_REPLICAS_PER_TRIAL) are spread round-robin over them."""
+        if not self._gpus_available():
+            return 0
+        return max(1, int(os.environ.get('RAFIKI_PREDICTOR_GPUS', '1')))
 
     def _create_inference_worker_services(self, inference_job, best_trials):
         """``workers`` mode: one InferenceWorker process per trial (its own GPU when free), then a

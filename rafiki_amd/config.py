@@ -23,7 +23,7 @@ APP_SECRET = _env('APP_SECRET', 'rafiki')
 SUPERADMIN_EMAIL = 'superadmin@rafiki'
 SUPERADMIN_PASSWORD = _env('SUPERADMIN_PASSWORD', 'rafiki')
 SERVICE_STATUS_WAIT = 1
-INFERENCE_WORKER_REPLICAS_PER_TRIAL = 2
+INFERENCE_WORKER_REPLICAS_PER_TRIAL = _env('INFERENCE_WORKER_REPLICAS_PER_TRIAL', 2, int)
 INFERENCE_MAX_BEST_TRIALS = _env('INFERENCE_MAX_BEST_TRIALS', 2, int)
 PREDICTOR_PREDICT_SLEEP = 0.25
 INFERENCE_WORKER_SLEEP = 0.25

@@ -814,6 +814,15 @@ class ConvNetEngine:
     def resident_bytes(self):
         return self.flat.total * (4 + (0 if self.f32 else 2) + 4) + self.running.numel() * 4
 
+    def release_training(self):
+        """Drop what only training needs — the captured step graphs (and with them their private
+        activation pools), static batch buffers, the step schedule and the optimizer state — so a
+        finished trial can stay resident in HBM for serving at its inference footprint."""
+        for a in ('_graph', '_sched_graph', '_static_x', '_static_y', '_sched', '_ctr'):
+            if hasattr(self, a):
+                setattr(self, a, None)
+        self.opt = None
+
     # ---------------------------------------------------------------------------- state I/O
     def state_dict(self):
         d = self.flat.state_dict()

@@ -197,6 +197,27 @@ class NativeImageClassifier(BaseModel):
         """uint8 [Q, H, W(, C)] (host or device) at this model's size -> device probabilities [Q, C]."""
         return self._probs(images)
 
+    @property
+    def num_classes(self):
+        return int(self._meta['num_classes'])
+
+    def release_training(self):
+        """Keep only the inference state (trainer -> predictor HBM handoff, predictor.resident)."""
+        if self._engine is not None:
+            self._engine.release_training()
+
+    def prepare_serving(self):
+        """Fold BN into inference coefficients ahead of a graph capture (forward_into is capture-safe)."""
+        if self._engine._eval_coeffs is None:
+            self._engine.prepare_eval()
+
+    def forward_into(self, images_dev, out):
+        """uint8 device batch [Q, H, W(, C)] -> probabilities written into ``out`` [Q, C] fp32: the
+        pack kernel + the un-graphed eval forward, so a caller can capture it inside a larger graph
+        (the predictor's one-graph-per-bucket ensemble)."""
+        eng = self._engine
+        return eng._forward_eval_gpu(eng.prepare_inputs(images_dev), out)
+
     def predict_proba(self, queries) -> torch.Tensor:
         """Device tensor [Q, num_classes] (used by the predictor's on-device ensemble)."""
         return self._probs(self._queries_to_images(queries))

@@ -1,0 +1,168 @@
+"""One hipGraph per batch bucket for a whole top-k ensemble.
+
+The reference answers a query by pushing it through Redis to one inference-worker container per
+model and polling for the k answers (rafiki/predictor/predictor.py:31-74, worker/inference.py:
+31-93).  Here the k resident models of one replica are captured together: per bucket B the graph
+holds
+
+    pinned host uint8 [B, ...]  --H2D-->  device input (one per input signature)
+      -> for every model, on its own captured stream branch: pack/normalise kernel + eval forward
+         (conv + folded-BN + ReLU/pool ... + softmax) into slot i of a [k, B, C] buffer
+      -> gfx950 weighted ensemble-mean kernel -> [B, C]  --D2H-->  pinned host output
+
+so a request costs one host memcpy into the pinned buffer, ONE graph launch and one stream sync —
+independent of k and of the model depth (at batch 1 the per-model graphs + stack + ensemble of the
+previous design were launch-bound at ~0.9 ms for 4 fp32 models).  The k branches run concurrently
+on the GPU.  Buckets are captured lazily on first use; a replica's graphs are serialised by a lock
+(each replica owns its models, buffers and stream, so replicas run concurrently).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..ops.graphs import capture as _capture
+
+BUCKETS = (1, 8, 32, 64, 128, 256, 512)
+
+
+def supports(models: Sequence[object]) -> bool:
+    """True when every model can be captured in the shared graph: native device models with an
+    input signature, a capture-safe ``forward_into`` and one common class count, all on one GPU."""
+    if not models:
+        return False
+    devs, ncls = set(), set()
+    for m in models:
+        if not all(callable(getattr(m, a, None)) for a in ('forward_into', 'input_signature', 'prepare_serving')):
+            return False
+        d = getattr(m, 'device', None)
+        if d is None or torch.device(d).type != 'cuda':
+            return False
+        devs.add(torch.device(d))
+        ncls.add(int(getattr(m, 'num_classes', -1)))
+    return len(devs) == 1 and len(ncls) == 1 and -1 not in ncls
+
+
+class _Entry:
+    __slots__ = ('graph', 'h_in', 'd_in', 'slots', 'out', 'h_out', 'bucket', 'host')
+
+
+class EnsembleGraphs:
+    def __init__(self, models: Sequence[object], weights: Optional[Sequence[float]] = None):
+        self.models = list(models)
+        self.device = torch.device(getattr(self.models[0], 'device'))
+        self.num_classes = int(self.models[0].num_classes)
+        self.sigs: List[Tuple] = []
+        for m in self.models:
+            s = m.input_signature()
+            if s not in self.sigs:
+                self.sigs.append(s)
+        self.weights = None if weights is None else torch.tensor(list(weights), dtype=torch.float32,
+                                                                   device=self.device)
+        self.lock = threading.Lock()
+        self.stream = torch.cuda.Stream(device=self.device)
+        self._branches = [torch.cuda.Stream(device=self.device) for _ in self.models]
+        self._graphs: Dict[Tuple[int, bool], _Entry] = {}
+        self._shapes: Dict[Tuple, Tuple] = {}
+        self.replays = 0
+        for m in self.models:
+            m.prepare_serving()
+
+    # ------------------------------------------------------------------ capture
+    def _body(self, e: _Entry):
+        from ..ops import functional as F
+        main = torch.cuda.current_stream(self.device)
+        if e.host:
+            for s in self.sigs:
+                e.d_in[s].copy_(e.h_in[s], non_blocking=True)
+        for i, (m, br) in enumerate(zip(self.models, self._branches)):
+            br.wait_stream(main)
+            with torch.cuda.stream(br):
+                m.forward_into(e.d_in[m.input_signature()], e.slots[i])
+        for br in self._branches:
+            main.wait_stream(br)
+        F.ensemble_mean(e.slots, self.weights, out=e.out)
+        if e.host:
+            e.h_out.copy_(e.out, non_blocking=True)
+
+    def _entry(self, bucket: int, host: bool) -> _Entry:
+        e = self._graphs.get((bucket, host))
+        if e is not None:
+            return e
+        e = _Entry()
+        e.bucket, e.host = bucket, host
+        e.h_in = {s: torch.zeros((bucket,) + self._shapes[s], dtype=torch.uint8).pin_memory()
+                  for s in self.sigs} if host else None
+        e.d_in = {s: torch.zeros((bucket,) + self._shapes[s], dtype=torch.uint8, device=self.device)
+                  for s in self.sigs}
+        e.slots = torch.zeros((len(self.models), bucket, self.num_classes), dtype=torch.float32, device=self.device)
+        e.out = torch.zeros((bucket, self.num_classes), dtype=torch.float32, device=self.device)
+        e.h_out = torch.zeros((bucket, self.num_classes), dtype=torch.float32).pin_memory() if host else None
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            self._body(e)          # eager warm-up: autotunes every GEMM shape, sizes the allocator
+        self.stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with _capture(g, stream=self.stream):
+            self._body(e)
+        e.graph = g
+        self._graphs[(bucket, host)] = e
+        return e
+
+    def _check(self, arrays):
+        for s, a in arrays.items():
+            if s not in self.sigs:
+                raise KeyError('no model of this ensemble takes input {}'.format(s))
+            shp = tuple(a.shape[1:])
+            if self._shapes.setdefault(s, shp) != shp:
+                raise ValueError('input shape {} does not match {} for {}'.format(shp, self._shapes[s], s))
+
+    # ------------------------------------------------------------------ run
+    def run_host(self, images: Dict[Tuple, np.ndarray]) -> np.ndarray:
+        """{signature: uint8 numpy [B, ...]} -> ensemble probabilities numpy [B, C] (float32):
+        pinned staging copy, ONE graph launch (H2D, k forwards, ensemble, D2H), one stream sync."""
+        B = len(next(iter(images.values())))
+        if B == 0:
+            return np.zeros((0, self.num_classes), np.float32)
+        if B > BUCKETS[-1]:
+            step = BUCKETS[-1]
+            return np.concatenate([self.run_host({s: a[i:i + step] for s, a in images.items()})
+                                   for i in range(0, B, step)])
+        bucket = next(b for b in BUCKETS if b >= B)
+        with self.lock:
+            self._check(images)
+            e = self._entry(bucket, True)
+            for s, a in images.items():
+                e.h_in[s][:B].copy_(torch.from_numpy(np.ascontiguousarray(a)))
+            with torch.cuda.stream(self.stream):
+                e.graph.replay()
+            self.stream.synchronize()
+            self.replays += 1
+            return e.h_out[:B].numpy().copy()
+
+    def run_device(self, inputs: Dict[Tuple, torch.Tensor]) -> torch.Tensor:
+        """{signature: device uint8 [B, ...]} -> device probabilities [B, C] (a fresh tensor, ordered
+        after the caller's current stream; no host sync)."""
+        B = next(iter(inputs.values())).shape[0]
+        if B > BUCKETS[-1]:
+            step = BUCKETS[-1]
+            return torch.cat([self.run_device({s: t[i:i + step] for s, t in inputs.items()})
+                              for i in range(0, B, step)])
+        bucket = next(b for b in BUCKETS if b >= B)
+        cur = torch.cuda.current_stream(self.device)
+        with self.lock:
+            self._check(inputs)
+            e = self._entry(bucket, False)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                for s, t in inputs.items():
+                    e.d_in[s][:B].copy_(t, non_blocking=True)
+                e.graph.replay()
+                res = e.out[:B].clone()
+            cur.wait_stream(self.stream)
+            res.record_stream(cur)
+            self.replays += 1
+            return res

@@ -12,7 +12,15 @@ query out through Redis lists to one container per model and polls for answers e
     bucketed forwards) run on their own HIP streams and are ensembled by the gfx950
     ensemble-mean kernel; any other BaseModel falls back to ``predict()`` + host ensembling;
   * every request has a timeout (reference bug (g)); a model that fails is dropped from that
-    batch's ensemble (partial-ensemble fallback) instead of hanging the request.
+    batch's ensemble (partial-ensemble fallback) instead of hanging the request;
+  * native ensembles run as ONE hipGraph per batch bucket (``ensemble_graph``: H2D, the k
+    forwards on concurrent captured branches, the ensemble kernel, D2H);
+  * replicas (reference INFERENCE_WORKER_REPLICAS_PER_TRIAL, config.py:10 / services_manager.py:
+    53-87): R copies of the ensemble, spread over the predictor's GPUs, each with its own graphs,
+    buffers and stream; every request runs on the least-busy replica, so concurrent requests (HTTP
+    executor threads, the batcher) overlap instead of queueing behind one graph;
+  * trials trained in this process are taken from HBM (``resident.STORE``) instead of re-read
+    from their params files.
 """
 from __future__ import annotations
 
@@ -24,6 +32,7 @@ import threading
 import time
 import traceback
 from concurrent.futures import Future
+from contextlib import contextmanager
 from typing import List, Optional, Tuple
 
 from .. import config
@@ -97,46 +106,125 @@ class RemoteWorkerModel:
         return out
 
 
+class _Replica:
+    """One copy of the ensemble: its models, HIP streams and (lazily) its ensemble graphs."""
+
+    def __init__(self, idx, models):
+        self.idx = idx
+        self.models = list(models)
+        self.inflight = 0
+        self.served = 0
+        self.streams = None
+        self.graphs = None
+        self.graphs_failed = False
+
+
 class Predictor:
     def __init__(self, models: Optional[List[Tuple[str, object]]] = None, task=TaskType.IMAGE_CLASSIFICATION,
                  max_batch: int = 256, max_wait_ms: float = 2.0, timeout_s: float = None,
-                 weights: Optional[List[float]] = None):
+                 weights: Optional[List[float]] = None, replicas: Optional[List[List[Tuple[str, object]]]] = None):
+        """models: replica 0's [(trial id, model)]; replicas: further copies of the same ensemble
+        (same trial order), e.g. on other GPUs."""
         self.task = task
         self.models = list(models or [])
         self.max_batch = max_batch
         self.max_wait_s = max_wait_ms / 1000.0
         self.timeout_s = timeout_s or config.PREDICTOR_TIMEOUT_S
         self.weights = weights
+        self.replicas = [_Replica(0, self.models)] + [_Replica(i + 1, r) for i, r in enumerate(replicas or [])]
+        for r in self.replicas[1:]:
+            if [n for n, _ in r.models] != [n for n, _ in self.models]:
+                raise ValueError('every replica must hold the same trials in the same order')
+        self._rlock = threading.Lock()
         self.cache = ParamCache(config.get_config().node.param_cache_gb * 1e9)
-        for name, m in self.models:
-            self.cache.put(name, m)
+        for r in self.replicas:
+            for name, m in r.models:
+                self.cache.put((name, r.idx), m)
         self._q: "queue.Queue" = queue.Queue()
-        self._thread = None
+        self._threads = []
         self._stop = threading.Event()
-        self._streams = None
         self.stats = {'batches': 0, 'queries': 0, 'errors': 0}
+
+    @contextmanager
+    def _replica(self):
+        """The least-busy replica for the duration of one request."""
+        with self._rlock:
+            r = min(self.replicas, key=lambda x: (x.inflight, x.served))
+            r.inflight += 1
+        try:
+            yield r
+        finally:
+            with self._rlock:
+                r.inflight -= 1
+                r.served += 1
+
+    def _ensemble_graphs(self, r):
+        """The replica's one-graph-per-bucket ensemble, when its models support it."""
+        if r.graphs is not None or r.graphs_failed or os.environ.get('RAFIKI_ENSEMBLE_GRAPH', '1') == '0':
+            return r.graphs
+        from . import ensemble_graph as EG
+        if not EG.supports([m for _, m in r.models]):
+            r.graphs_failed = True
+            return None
+        r.graphs = EG.EnsembleGraphs([m for _, m in r.models], self.weights)
+        return r.graphs
+
+    def _graph_call(self, r, fn):
+        """Run fn(graphs) on the replica's ensemble graph; None when unavailable or it failed (the
+        replica then stays on the per-model path)."""
+        g = self._ensemble_graphs(r)
+        if g is None:
+            return None
+        try:
+            return fn(g)
+        except Exception:
+            logger.error('ensemble graph failed on replica %d, using per-model path:\n%s', r.idx,
+                         traceback.format_exc())
+            r.graphs, r.graphs_failed = None, True
+            return None
 
     # ------------------------------------------------------------------ loading from the DB
     @classmethod
-    def from_inference_job(cls, inference_job_id, db=None, **kw):
+    def from_inference_job(cls, inference_job_id, db=None, replicas=None, devices=None, **kw):
+        """Load the job's top-k trials.  ``replicas`` (default INFERENCE_WORKER_REPLICAS_PER_TRIAL)
+        copies go round-robin over ``devices`` (default: every GPU visible to this process).  A
+        trial trained in this process is taken from HBM (resident.STORE) for replica 0 on its own
+        GPU; everything else is read from the params file once and instantiated per replica."""
         if os.environ.get('RAFIKI_INFERENCE_MODE', 'local') == 'workers':
             return cls.from_inference_workers(inference_job_id, db=db, **kw)
         from ..db.database import Database
         from ..model.model import load_model_class
+        from ..parallel.context import TrialContext, current, use_context
+        from .resident import STORE
         db = db or Database()
         ij = db.get_inference_job(inference_job_id)
         tj = db.get_train_job(ij.train_job_id)
-        models = []
+        n_rep = max(1, int(replicas if replicas is not None else config.INFERENCE_WORKER_REPLICAS_PER_TRIAL))
+        if devices is None:
+            devices = _serving_devices()
+        sets = [[] for _ in range(n_rep)]
         for w in db.get_workers_of_inference_job(inference_job_id):
             trial = db.get_trial(w.trial_id)
             sub = db.get_sub_train_job(trial.sub_train_job_id)
             mrec = db.get_model(sub.model_id)
             clazz = load_model_class(mrec.model_file_bytes, mrec.model_class)
-            inst = clazz(**(trial.knobs or {}))
-            with open(trial.params_file_path, 'rb') as f:
-                inst.load_parameters(pickle.loads(f.read()))
-            models.append((trial.id, inst))
-        return cls(models, task=tj.task, **kw)
+            params = None
+            for r in range(n_rep):
+                dev = devices[r % len(devices)]
+                inst = STORE.take(trial.id) if r == 0 else None
+                if inst is not None and str(getattr(inst, 'device', '')) != str(dev):
+                    STORE.offer(trial.id, inst, float(trial.score or 0.0))   # trained on another GPU
+                    inst = None
+                if inst is None:
+                    if params is None:
+                        with open(trial.params_file_path, 'rb') as f:
+                            params = pickle.loads(f.read())
+                    ctx = TrialContext(device=dev) if dev is not None else current()
+                    with use_context(ctx):
+                        inst = clazz(**(trial.knobs or {}))
+                        inst.load_parameters(params)
+                sets[r].append((trial.id, inst))
+        return cls(sets[0], task=tj.task, replicas=sets[1:], **kw)
 
     @classmethod
     def from_inference_workers(cls, inference_job_id, db=None, cache=None, **kw):
@@ -166,8 +254,12 @@ class Predictor:
                 return self._predict_fast(queries)
             except Exception:
                 logger.error('fast path failed, falling back:\n%s', traceback.format_exc())
+        with self._replica() as r:
+            return self._predict_models(r, queries)
+
+    def _predict_models(self, r, queries):
         preds, ok = [], []
-        for name, m in self.models:
+        for name, m in r.models:
             try:
                 preds.append(m.predict(queries))
                 ok.append(name)
@@ -184,21 +276,16 @@ class Predictor:
         if self._fast_path():
             import numpy as np
             import torch
-            dev = None
-            for _, m in self.models:
-                d = getattr(m, 'device', None)
-                if d is not None and torch.device(d).type == 'cuda':
-                    dev = torch.device(d)
-                    break
-            if dev is not None and all(callable(getattr(m, 'input_signature', None)) for _, m in self.models):
-                inputs = {}
-                for _, m in self.models:
-                    sig = m.input_signature()
-                    if sig not in inputs:
-                        imgs = np.ascontiguousarray(m.queries_to_images(arr))
-                        inputs[sig] = torch.from_numpy(imgs).pin_memory().to(dev, non_blocking=True)
-                self.stats['queries'] += len(arr)
-                return self.predict_proba_device(inputs).cpu().numpy()
+            with self._replica() as r:
+                dev = _cuda_device_of(r.models)
+                if dev is not None and all(callable(getattr(m, 'input_signature', None)) for _, m in r.models):
+                    host = _decode_once(r.models, arr)
+                    self.stats['queries'] += len(arr)
+                    out = self._graph_call(r, lambda g: g.run_host(host))
+                    if out is not None:
+                        return out
+                    inputs = {s: torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) for s, a in host.items()}
+                    return self._proba_device_on(r, inputs).cpu().numpy()
         return self.predict(arr.tolist())
 
     def _predict_remote(self, queries):
@@ -233,36 +320,39 @@ class Predictor:
         Queries are decoded to uint8 once per distinct model input signature and uploaded once
         (pinned, non-blocking); every model then runs its hipGraph-captured bucketed forward on its
         own HIP stream, and the gfx950 ensemble-mean kernel reduces the [models, Q, C] stack."""
-        import numpy as np
         import torch
-        dev = None
-        for name, m in self.models:
-            d = getattr(m, 'device', None)
-            if d is not None and torch.device(d).type == 'cuda':
-                dev = torch.device(d)
-                break
-        if dev is None:
-            probs = [m.predict_proba(queries) for _, m in self.models]
-            return ensemble_probabilities(torch.stack([p.float().cpu() for p in probs]))
-        inputs = {}
-        for _, m in self.models:
-            sig_fn = getattr(m, 'input_signature', None)
-            sig = sig_fn() if callable(sig_fn) else None
-            if sig is not None and sig not in inputs:
-                arr = np.ascontiguousarray(m.queries_to_images(queries))
-                host = torch.from_numpy(arr).pin_memory()
-                inputs[sig] = host.to(dev, non_blocking=True)
-        return self.predict_proba_device(inputs, queries)
+        with self._replica() as r:
+            dev = _cuda_device_of(r.models)
+            if dev is None:
+                probs = [m.predict_proba(queries) for _, m in r.models]
+                return ensemble_probabilities(torch.stack([p.float().cpu() for p in probs]))
+            host = _decode_once(r.models, queries)
+            if len(host) and all(callable(getattr(m, 'input_signature', None)) for _, m in r.models):
+                out = self._graph_call(r, lambda g: g.run_host(host))
+                if out is not None:
+                    return torch.from_numpy(out)
+            inputs = {s: torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) for s, a in host.items()}
+            return self._proba_device_on(r, inputs, queries)
 
     def predict_proba_device(self, inputs, queries=None):
-        """inputs: {input_signature: device uint8 batch}.  Models without a signature get ``queries``."""
+        """inputs: {input_signature: device uint8 batch} -> device probabilities.  Models without
+        a signature get ``queries``."""
+        with self._replica() as r:
+            if queries is None and inputs and all(callable(getattr(m, 'input_signature', None)) for _, m in r.models):
+                out = self._graph_call(r, lambda g: g.run_device(inputs))
+                if out is not None:
+                    return out
+            return self._proba_device_on(r, inputs, queries)
+
+    def _proba_device_on(self, r, inputs, queries=None):
+        """Per-model path: each model's bucketed graph on its own HIP stream, then the ensemble kernel."""
         import torch
         dev = next(iter(inputs.values())).device if inputs else torch.device('cuda')
-        if self._streams is None or len(self._streams) != len(self.models):
-            self._streams = [torch.cuda.Stream(device=dev) for _ in self.models]
+        if r.streams is None or len(r.streams) != len(r.models):
+            r.streams = [torch.cuda.Stream(device=dev) for _ in r.models]
         main = torch.cuda.current_stream(dev)
         outs = []
-        for (name, m), s in zip(self.models, self._streams):
+        for (name, m), s in zip(r.models, r.streams):
             s.wait_stream(main)
             with torch.cuda.stream(s):
                 sig_fn = getattr(m, 'input_signature', None)
@@ -272,7 +362,7 @@ class Predictor:
                 else:
                     p = m.predict_proba(queries)
                 outs.append(p)
-        for s in self._streams:
+        for s in r.streams:
             main.wait_stream(s)
         for p in outs:
             p.record_stream(main)
@@ -284,22 +374,26 @@ class Predictor:
 
     # ------------------------------------------------------------------- dynamic batching
     def start(self):
-        if self._thread is None:
+        """One batching consumer per replica over the shared request queue (the reference's
+        replicas each pop from the same Redis queue)."""
+        if not self._threads:
             self._stop.clear()
-            self._thread = threading.Thread(target=self._batch_loop, name='rafiki-batcher', daemon=True)
-            self._thread.start()
+            for i in range(len(self.replicas)):
+                t = threading.Thread(target=self._batch_loop, name='rafiki-batcher-{}'.format(i), daemon=True)
+                t.start()
+                self._threads.append(t)
         return self
 
     def stop(self):
         self._stop.set()
-        if self._thread is not None:
-            self._thread.join(timeout=5)
-            self._thread = None
+        for t in self._threads:
+            t.join(timeout=5)
+        self._threads = []
 
     def submit(self, query) -> Future:
         fut = Future()
         self._q.put((query, fut))
-        if self._thread is None:
+        if not self._threads:
             self.start()
         return fut
 
@@ -330,3 +424,39 @@ class Predictor:
                     fut.set_exception(e)
             self.stats['batches'] += 1
             self.stats['queries'] += len(batch)
+
+
+def _cuda_device_of(models):
+    import torch
+    for _, m in models:
+        d = getattr(m, 'device', None)
+        if d is not None and torch.device(d).type == 'cuda':
+            return torch.device(d)
+    return None
+
+
+def _decode_once(models, queries):
+    """{input signature: contiguous uint8 numpy batch}: queries decoded once per distinct model
+    input signature, not once per model."""
+    import numpy as np
+    out = {}
+    for _, m in models:
+        sig_fn = getattr(m, 'input_signature', None)
+        sig = sig_fn() if callable(sig_fn) else None
+        if sig is not None and sig not in out:
+            out[sig] = np.ascontiguousarray(m.queries_to_images(queries))
+    return out
+
+
+def _serving_devices():
+    """GPUs this predictor serves from: RAFIKI_PREDICTOR_DEVICES ("0,1") or every visible GPU;
+    [None] (the current context's device) on a host without GPUs."""
+    import torch
+    env = os.environ.get('RAFIKI_PREDICTOR_DEVICES', '')
+    if env:
+        return [torch.device('cuda', int(v)) for v in env.split(',') if v.strip()]
+    try:
+        n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    except Exception:
+        n = 0
+    return [torch.device('cuda', i) for i in range(n)] or [None]

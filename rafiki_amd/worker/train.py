@@ -295,6 +295,11 @@ class TrainWorker:
                 self._db.mark_trial_as_complete(trial, score, params_path)
                 self.completed_trials.append((trial.id, score))
                 ctx.checkpoint.remove()
+                # in-process trainer -> predictor handoff: a kept model stays resident in HBM (the
+                # params file above remains the durable copy)
+                from ..predictor.resident import STORE
+                if not ctx.data_parallel and STORE.offer(trial.id, inst, score):
+                    inst = None
             return score, 1.0
         except Exception:
             logger.error('trial failed:\n%s', traceback.format_exc())

@@ -123,6 +123,8 @@ def main():
     ap.add_argument('--iters', type=int, default=50)
     ap.add_argument('--clients', type=int, default=64)
     ap.add_argument('--seconds', type=float, default=5.0)
+    ap.add_argument('--replicas', type=int, default=1)
+    ap.add_argument('--skip-http', action='store_true')
     ap.add_argument('--out', default='')
     args = ap.parse_args()
     from rafiki_amd.ops import _lib
@@ -130,10 +132,13 @@ def main():
     _lib.lib()
     dev = torch.device('cuda', 0)
     models = build_models(args.models, dev)
-    pred = Predictor(models, max_batch=512, max_wait_ms=2.0)
+    pred = Predictor(models, max_batch=512, max_wait_ms=2.0,
+                     replicas=[build_models(args.models, dev) for _ in range(args.replicas - 1)])
     rng = np.random.default_rng(0)
     res = {'metric': 'predictor ensemble QPS (top-{} VGG-small 32x32x3, 1 GPU)'.format(args.models),
-           'n_models': args.models, 'device': {}, 'api': {}, 'dtype': 'bf16', 'data': 'synthetic, random-init'}
+           'n_models': args.models, 'replicas': args.replicas, 'device': {}, 'api': {},
+           'dtype': models[0][1]._meta.get('dtype'), 'data': 'synthetic, random-init',
+           'ensemble_graph': os.environ.get('RAFIKI_ENSEMBLE_GRAPH', '1') != '0'}
     sig = models[0][1].input_signature()
     for b in [int(x) for x in args.batches.split(',')]:
         imgs = torch.from_numpy(rng.integers(0, 256, (b, 32, 32, 3), dtype=np.uint8)).to(dev)
@@ -156,8 +161,9 @@ def main():
         dt = timed(lambda: pred.predict_array(arr), it)
         res['array'][b] = {'qps': round(b * it / dt, 1), 'ms_per_batch': round(1e3 * dt / it, 3)}
     # real HTTP: the predictor's Flask app on a local port, concurrent clients
-    res['http'] = http_bench(pred, rng, args, 'fast')
-    res['http_flask'] = http_bench(pred, rng, args, 'flask')
+    if not args.skip_http:
+        res['http'] = http_bench(pred, rng, args, 'fast')
+        res['http_flask'] = http_bench(pred, rng, args, 'flask')
     # dynamic batcher under concurrent single-query clients
     pred.start()
     one = rng.integers(0, 256, (32, 32, 3)).tolist()

@@ -222,3 +222,79 @@ def test_crash_resume_on_gpu_matches_uninterrupted(tmp_path, monkeypatch):
     a, b = finals
     cosv = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
     assert cosv > 0.999, cosv
+
+
+def _copy_ensemble(ensemble):
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    out = []
+    with use_context(TrialContext(device=torch.device(DEV))):
+        for name, m in ensemble:
+            c = type(m)(**m._knobs)
+            c.load_parameters(m.dump_parameters())
+            out.append((name, c))
+    return out
+
+
+def test_one_graph_ensemble_matches_per_model_path(ensemble, monkeypatch):
+    """The whole top-4 ensemble captured as ONE hipGraph per bucket (H2D, 4 concurrent forward
+    branches, ensemble kernel, D2H) agrees with the per-model-stream path, for every bucket size
+    including a chunked > 512 batch, on the host-array and the device-tensor entry points."""
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor.predictor import Predictor
+    models = _copy_ensemble(ensemble)
+    p = Predictor(models)
+    monkeypatch.setenv('RAFIKI_ENSEMBLE_GRAPH', '0')
+    ref_p = Predictor(ensemble)
+    for n in (1, 5, 37, 600):
+        imgs, _ = synthetic_images(n, size=32, channels=3, classes=10, seed=n)
+        monkeypatch.setenv('RAFIKI_ENSEMBLE_GRAPH', '0')
+        ref = ref_p.predict_array(imgs)
+        monkeypatch.setenv('RAFIKI_ENSEMBLE_GRAPH', '1')
+        got = p.predict_array(imgs)
+        assert got.shape == (n, 10) and np.allclose(got, ref, atol=1e-5), n
+        sig = models[0][1].input_signature()
+        dev = p.predict_proba_device({sig: torch.from_numpy(imgs).to(DEV)})
+        assert np.allclose(dev.cpu().numpy(), ref, atol=1e-5), n
+    g = p.replicas[0].graphs
+    assert g is not None and g.replays >= 8 and ref_p.replicas[0].graphs is None
+    assert {b for b, _ in g._graphs} >= {1, 8, 64, 512}
+
+
+def test_replicas_serve_concurrent_requests(ensemble):
+    """Two replicas of the ensemble on one GPU (own models, graphs and streams): concurrent
+    requests spread over both and every answer matches the single-replica result."""
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor.predictor import Predictor
+    p = Predictor(_copy_ensemble(ensemble), replicas=[_copy_ensemble(ensemble)])
+    imgs, _ = synthetic_images(48, size=32, channels=3, classes=10, seed=3)
+    ref = Predictor(ensemble).predict_array(imgs)
+    out = [None] * 12
+
+    def worker(k):
+        for j in range(3):
+            i = (k * 3 + j) % 12
+            out[i] = p.predict_array(imgs[i * 4:(i + 1) * 4])
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert np.allclose(np.concatenate(out), ref, atol=1e-5)
+    assert all(r.served > 0 for r in p.replicas), [r.served for r in p.replicas]
+    assert all(r.graphs is not None for r in p.replicas)
+
+
+def test_resident_handoff_keeps_trained_model_in_hbm(ensemble):
+    """A finished trial offered to the resident store drops its training state (step graphs,
+    optimizer) but predicts exactly as before, and take() hands back the same object."""
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor.resident import ResidentStore
+    name, m = _copy_ensemble(ensemble[:1])[0]
+    imgs, _ = synthetic_images(16, size=32, channels=3, classes=10, seed=4)
+    before = m.predict_proba(imgs.tolist()).cpu()
+    store = ResidentStore(budget_bytes=10e9)
+    assert store.offer('trial-x', m, 0.9)
+    assert m._engine.opt is None and m._engine._graph is None
+    got = store.take('trial-x')
+    assert got is m and store.take('trial-x') is None
+    assert torch.equal(got.predict_proba(imgs.tolist()).cpu(), before)
