@@ -365,9 +365,11 @@ __global__ __launch_bounds__(256) void sreduce_epi_kernel(const float* __restric
 }
 
 // uint8/float NCHW images -> fp32 NHWC with channels zero-padded to Cp: out = in * scale + shift
-__global__ __launch_bounds__(256) void pack_nhwc_f32_kernel(const void* __restrict__ src, int is_u8, int N, int C,
+// flags bit 0: uint8 source (else fp32), bit 1: source already NHWC (else NCHW)
+__global__ __launch_bounds__(256) void pack_nhwc_f32_kernel(const void* __restrict__ src, int flags, int N, int C,
                                                             int H, int W, int Cp, float scale, float shift,
                                                             float* __restrict__ dst) {
+  const bool is_u8 = flags & 1, nhwc = flags & 2;
   const long long total = (long long)N * H * W * Cp;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int c = (int)(i % Cp);
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(256) void pack_nhwc_f32_kernel(const void* __restri
     const long long n = t / H;
     float v = 0.f;
     if (c < C) {
-      const long long si = ((n * C + c) * H + h) * W + w;
+      const long long si = nhwc ? pix * C + c : ((n * C + c) * H + h) * W + w;
       v = (is_u8 ? (float)((const unsigned char*)src)[si] : ((const float*)src)[si]) * scale + shift;
     }
     dst[i] = v;
@@ -483,10 +485,10 @@ extern "C" int rk_sreduce_epi(const float* slab, int S, int M, int N, const floa
   return RK_OK;
 }
 
-extern "C" int rk_pack_nhwc_f32(const void* src, int is_u8, int N, int C, int H, int W, int Cp, float scale,
+extern "C" int rk_pack_nhwc_f32(const void* src, int flags, int N, int C, int H, int W, int Cp, float scale,
                                 float shift, float* out, void* stream) {
   hipLaunchKernelGGL(pack_nhwc_f32_kernel, dim3(grid_cap((long long)N * H * W * Cp, 4096)), dim3(256), 0,
-                     (hipStream_t)stream, src, is_u8, N, C, H, W, Cp, scale, shift, out);
+                     (hipStream_t)stream, src, flags, N, C, H, W, Cp, scale, shift, out);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

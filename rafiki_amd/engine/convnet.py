@@ -698,6 +698,8 @@ class ConvNetEngine:
         if self.flat_input:
             nchw = t.reshape(N, -1, 1, 1)
             return pack(nchw.contiguous(), self.feat_dim, scale, shift).view(N, self.feat_dim)
+        if self.f32:   # the fp32 pack kernel reads NHWC directly (no transposing copy)
+            return S.pack_nhwc(t.contiguous(), self.cin_p, scale, shift, nhwc=True)
         nchw = t.permute(0, 3, 1, 2).contiguous()
         return pack(nchw, self.cin_p, scale, shift)
 

@@ -34,7 +34,12 @@ _PIN = tuple(int(v) for v in os.environ['RAFIKI_SGEMM_CFG'].split(',')) if os.en
 
 
 def _p(t: Optional[torch.Tensor]):
-    return None if t is None else t.data_ptr()
+    """Device pointer of a kernel operand; a host tensor here would be an illegal GPU access."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError('host tensor {} {} passed to a gfx950 kernel'.format(tuple(t.shape), t.dtype))
+    return t.data_ptr()
 
 
 def _nbytes(t):
@@ -141,9 +146,19 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     flags |= F_RELU if act == ACT_RELU else F_LRELU if act == ACT_LRELU else 0
 
     def run(cfg):
-        sgemm(KIND_CONV, x, w, out, M, Cout, K, Cin, K, Cout, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats_acc,
-              H=H, W=W, C=Cin, taps=taps, flags=flags, slope=slope)
-    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags), _cands(M, Cout, big=Cin % 32 == 0), run)
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm(KIND_CONV, x, w, out, M, Cout, K, Cin, K, Cout, tile=tile, nst=nst, bias=bias, stats=stats_acc,
+                  H=H, W=W, C=Cin, taps=taps, flags=flags, slope=slope)
+            return
+        # small-M deep layers (inference at small batch: 4x4 maps, K = 9 x 512): split-K slabs + one
+        # combine that applies bias / activation
+        slab = torch.empty((s, M, Cout), device=x.device, dtype=torch.float32)
+        sgemm(KIND_CONV, x, w, slab, M, Cout, K, Cin, K, Cout, tile=tile, nst=nst, splits=s, slab_stride=M * Cout,
+              H=H, W=W, C=Cin, taps=taps)
+        sreduce_epi(slab, M, Cout, out.view(M, Cout), bias=bias, act=act, slope=slope)
+    cands = _cands(M, Cout, splittable=stats_acc is None and Cout % 4 == 0, K=K, big=Cin % 32 == 0)
+    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags), cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -407,14 +422,17 @@ def softmax_xent(logits, labels, ncls, *, dlogits=None, probs=None, loss_sum=Non
               _p(correct), _p(counted), _s())
 
 
-def pack_nhwc(images, cpad=4, scale=1.0, shift=0.0, out=None):
-    """uint8/float32 NCHW -> fp32 NHWC with channels padded to ``cpad``."""
-    Nb, Cc, H, W = images.shape
+def pack_nhwc(images, cpad=4, scale=1.0, shift=0.0, out=None, nhwc=False):
+    """uint8/float32 NCHW (``nhwc``: NHWC) -> fp32 NHWC with channels padded to ``cpad``, x*scale+shift."""
+    if nhwc:
+        Nb, H, W, Cc = images.shape
+    else:
+        Nb, Cc, H, W = images.shape
     if out is None:
         out = torch.empty((Nb, H, W, cpad), device=images.device, dtype=torch.float32)
     is_u8 = 1 if images.dtype == torch.uint8 else 0
     if not is_u8 and images.dtype != torch.float32:
         images = images.float()
-    _lib.call("rk_pack_nhwc_f32", _p(images.contiguous()), is_u8, Nb, Cc, H, W, cpad, float(scale), float(shift),
-              _p(out), _s())
+    _lib.call("rk_pack_nhwc_f32", _p(images.contiguous()), is_u8 | (2 if nhwc else 0), Nb, Cc, H, W, cpad,
+              float(scale), float(shift), _p(out), _s())
     return out

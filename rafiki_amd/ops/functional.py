@@ -42,7 +42,12 @@ VARIANT = int(os.environ.get('RAFIKI_IGEMM_VARIANT', '0'))
 
 
 def _p(t: Optional[torch.Tensor]):
-    return None if t is None else t.data_ptr()
+    """Device pointer of a kernel operand; a host tensor here would be an illegal GPU access."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError('host tensor {} {} passed to a gfx950 kernel'.format(tuple(t.shape), t.dtype))
+    return t.data_ptr()
 
 
 def _nbytes(t):

@@ -7,8 +7,9 @@ WSGI server spends ~1 ms of GIL-bound Python per request before the model is eve
 capped single-query serving at ~1.1 k QPS.  Here one asyncio loop parses HTTP/1.1 keep-alive
 requests (request line + Content-Length only), decodes image queries with the native JSON parser,
 and batches by construction: every query that arrives while the GPU runs batch k becomes batch
-k+1 (no timer), which is submitted as ONE uint8 array to ``Predictor.predict_array`` on a single
-executor thread (HIP streams + hipGraph forwards + on-device ensemble mean).
+k+1 (no timer), which is submitted as ONE uint8 array to ``Predictor.predict_array`` (one hipGraph
+for the whole ensemble).  With R predictor replicas, up to R batches are in flight at once on R
+executor threads (each request lands on the least-busy replica).
 """
 from __future__ import annotations
 
@@ -35,7 +36,9 @@ class FastPredictorServer:
         self.predictor = predictor
         self.host, self.port = host, int(port)
         self.max_batch = int(max_batch)
-        self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix='rafiki-gpu')
+        self.slots = max(1, len(getattr(predictor, 'replicas', [None])))
+        self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self.slots, thread_name_prefix='rafiki-gpu')
+        self._inflight = 0
         self._pending = []            # (array, future) of single queries waiting for the next batch
         self._wake = None
         self._loop = None
@@ -49,31 +52,38 @@ class FastPredictorServer:
         self._lat_sum = 0.0
 
     # ----------------------------------------------------------------------------- batching
-    async def _batch_loop(self):
+    async def _run_batch(self, take):
         loop = asyncio.get_running_loop()
+        try:
+            probs = await loop.run_in_executor(self._pool, self.predictor.predict_array,
+                                               np.stack([a for a, _ in take]))
+            probs = np.asarray(probs)
+            for i, (_, fut) in enumerate(take):
+                if not fut.done():
+                    fut.set_result(probs[i])
+        except Exception as e:  # every waiter of the batch gets the error
+            for _, fut in take:
+                if not fut.done():
+                    fut.set_exception(e)
+        finally:
+            self.counters['batches'] += 1
+            self.counters['batched_queries'] += len(take)
+            self._inflight -= 1
+            self._wake.set()
+
+    async def _batch_loop(self):
         while True:
             await self._wake.wait()
             self._wake.clear()
-            while self._pending:
+            while self._pending and self._inflight < self.slots:
                 # one shape per batch (queries of the same model input size stack)
                 shape = self._pending[0][0].shape
                 take, rest = [], []
                 for item in self._pending:
                     (take if item[0].shape == shape and len(take) < self.max_batch else rest).append(item)
                 self._pending = rest
-                try:
-                    probs = await loop.run_in_executor(self._pool, self.predictor.predict_array,
-                                                       np.stack([a for a, _ in take]))
-                    probs = np.asarray(probs)
-                    for i, (_, fut) in enumerate(take):
-                        if not fut.done():
-                            fut.set_result(probs[i])
-                except Exception as e:  # every waiter of the batch gets the error
-                    for _, fut in take:
-                        if not fut.done():
-                            fut.set_exception(e)
-                self.counters['batches'] += 1
-                self.counters['batched_queries'] += len(take)
+                self._inflight += 1
+                asyncio.ensure_future(self._run_batch(take))
 
     def _enqueue(self, arr):
         fut = self._loop.create_future()
@@ -219,8 +229,11 @@ class FastPredictorServer:
                 # closing the server ends serve_forever, and asyncio.run may close the loop before
                 # the cancel coroutine below is scheduled: either order is a clean shutdown
                 self._loop.call_soon_threadsafe(self._server.close)
-                fut = asyncio.run_coroutine_threadsafe(self._cancel_all(), self._loop)
-                fut.result(5)
+                coro = self._cancel_all()
+                try:
+                    asyncio.run_coroutine_threadsafe(coro, self._loop).result(5)
+                except Exception:
+                    coro.close()   # the loop ended first: nothing left to cancel
             except Exception:
                 pass
         if self._thread is not None:

@@ -278,3 +278,39 @@ def test_eval_forward_matches_reference():
                                        params={n: eng.flat.w(n).double().cpu() for n in eng.flat.names()})
     ref = torch.softmax(ref_logits, 1)
     assert (probs.double().cpu() - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,splits", [(1, 4, 512, 512, 16), (2, 2, 256, 512, 8), (1, 8, 128, 256, 4)])
+def test_conv_fwd_split_k_small_batch(N, H, Cin, Cout, splits):
+    """Inference-sized convs (tiny M, K = 9 x Cin): split-K slabs + the bias/ReLU combine == fp64 conv."""
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, H, Cin, seed=1).to(DEV)
+    w = _rand(Cout, 3, 3, Cin, seed=2, scale=0.05).to(DEV)
+    b = _rand(Cout, seed=3, scale=0.1).to(DEV)
+    ref = torch.relu(_conv_ref(x.cpu().double(), w.cpu().double(), 9) + b.cpu().double())
+    M, K = N * H * H, 9 * Cin
+    slab = torch.empty(splits, M, Cout, device=DEV)
+    S.sgemm(S.KIND_CONV, x, w, slab, M, Cout, K, Cin, K, Cout, tile=3, nst=2, splits=splits, slab_stride=M * Cout,
+            H=H, W=H, C=Cin, taps=9)
+    out = torch.empty(N, H, H, Cout, device=DEV)
+    S.sreduce_epi(slab, M, Cout, out.view(M, Cout), bias=b, act=S.ACT_RELU)
+    assert rel(out.double(), ref) < 1e-5
+    y = S.conv_fwd(x, w, bias=b, act=S.ACT_RELU)   # whatever config the autotuner keeps
+    assert rel(y.double(), ref) < 1e-5
+
+
+def test_host_tensor_is_refused_before_launch():
+    from rafiki_amd.ops import f32 as S
+    with pytest.raises(ValueError, match='host tensor'):
+        S.conv_fwd(torch.zeros(1, 4, 4, 32), torch.zeros(32, 3, 3, 32, device=DEV))
+
+
+def test_prepare_inputs_nhwc_pack():
+    eng = _engine(image_size=16)
+    imgs = torch.randint(0, 256, (5, 16, 16, 3), dtype=torch.uint8)
+    got = eng.prepare_inputs(imgs.to(DEV)).cpu()
+    ref = torch.zeros(5, 16, 16, eng.cin_p)
+    ref[..., :3] = imgs.float() / 127.5 - 1.0
+    assert torch.allclose(got, ref, atol=1e-6)
+    got_host = eng.prepare_inputs(imgs.numpy()).cpu()
+    assert torch.allclose(got_host, ref, atol=1e-6)
