@@ -29,6 +29,22 @@ namespace {
 
 struct U4 { uint32_t v[4]; };
 
+// 8 consecutive channels of a bf16 or fp32 NHWC row <-> 8 floats (the PG-GAN ops run in either
+// precision: bf16 for the opt-in fast path, fp32 — the reference's precision — by default)
+template <class T> RK_DEV void ld8(const T* p, float (&f)[8]);
+template <> RK_DEV void ld8<bf16>(const bf16* p, float (&f)[8]) { unpack8(*(const uint4*)p, f); }
+template <> RK_DEV void ld8<float>(const float* p, float (&f)[8]) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[i] = a[i]; f[4 + i] = b[i]; }
+}
+template <class T> RK_DEV void st8(T* p, const float (&f)[8]);
+template <> RK_DEV void st8<bf16>(bf16* p, const float (&f)[8]) { *(uint4*)p = pack8(f); }
+template <> RK_DEV void st8<float>(float* p, const float (&f)[8]) {
+  *(f32x4*)p = f32x4{f[0], f[1], f[2], f[3]};
+  *(f32x4*)(p + 4) = f32x4{f[4], f[5], f[6], f[7]};
+}
+
 RK_DEV U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
   constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
@@ -87,14 +103,14 @@ __global__ __launch_bounds__(256) void philox_kernel(void* __restrict__ out, lon
 }
 
 // One wave per row of C channels (C % 8 == 0, C <= 64 * 8 * NV).  bias: fp32 [C] or null.
-template <int NV>
-__global__ __launch_bounds__(256) void lrelu_pn_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ bias,
+template <int NV, class T>
+__global__ __launch_bounds__(256) void lrelu_pn_fwd_kernel(const T* __restrict__ x, const float* __restrict__ bias,
                                                            int P, int C, float slope, float eps,
-                                                           bf16* __restrict__ z) {
+                                                           T* __restrict__ z) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= P) return;
-  const uint4* xr = (const uint4*)(x + (long long)row * C);
+  const T* xr = x + (long long)row * C;
   const int nvec = C >> 3;
   float y[NV][8];
   float ss = 0.f;
@@ -102,7 +118,7 @@ __global__ __launch_bounds__(256) void lrelu_pn_fwd_kernel(const bf16* __restric
   for (int v = 0; v < NV; ++v) {
     const int c8 = lane + v * 64;
     if (c8 < nvec) {
-      unpack8(xr[c8], y[v]);
+      ld8(xr + c8 * 8, y[v]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = y[v][j] + (bias ? bias[c8 * 8 + j] : 0.f);
@@ -113,7 +129,7 @@ __global__ __launch_bounds__(256) void lrelu_pn_fwd_kernel(const bf16* __restric
     }
   }
   const float r = rsqrtf(wave_sum(ss) / (float)C + eps);
-  uint4* zr = (uint4*)(z + (long long)row * C);
+  T* zr = z + (long long)row * C;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c8 = lane + v * 64;
@@ -121,20 +137,20 @@ __global__ __launch_bounds__(256) void lrelu_pn_fwd_kernel(const bf16* __restric
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = y[v][j] * r;
-      zr[c8] = pack8(o);
+      st8(zr + c8 * 8, o);
     }
   }
 }
 
-template <int NV>
-__global__ __launch_bounds__(256) void lrelu_pn_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ bias,
-                                                           const bf16* __restrict__ dz, int P, int C, float slope,
-                                                           float eps, bf16* __restrict__ dx) {
+template <int NV, class T>
+__global__ __launch_bounds__(256) void lrelu_pn_bwd_kernel(const T* __restrict__ x, const float* __restrict__ bias,
+                                                           const T* __restrict__ dz, int P, int C, float slope,
+                                                           float eps, T* __restrict__ dx) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= P) return;
-  const uint4* xr = (const uint4*)(x + (long long)row * C);
-  const uint4* dr = (const uint4*)(dz + (long long)row * C);
+  const T* xr = x + (long long)row * C;
+  const T* dr = dz + (long long)row * C;
   const int nvec = C >> 3;
   float y[NV][8], g[NV][8];
   float ss = 0.f, sd = 0.f;
@@ -142,8 +158,8 @@ __global__ __launch_bounds__(256) void lrelu_pn_bwd_kernel(const bf16* __restric
   for (int v = 0; v < NV; ++v) {
     const int c8 = lane + v * 64;
     if (c8 < nvec) {
-      unpack8(xr[c8], y[v]);
-      unpack8(dr[c8], g[v]);
+      ld8(xr + c8 * 8, y[v]);
+      ld8(dr + c8 * 8, g[v]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float pre = y[v][j] + (bias ? bias[c8 * 8 + j] : 0.f);
@@ -158,7 +174,7 @@ __global__ __launch_bounds__(256) void lrelu_pn_bwd_kernel(const bf16* __restric
   sd = wave_sum(sd);
   const float r = rsqrtf(ss / (float)C + eps);
   const float k = r * r * r * sd / (float)C;
-  uint4* xo = (uint4*)(dx + (long long)row * C);
+  T* xo = dx + (long long)row * C;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c8 = lane + v * 64;
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(256) void lrelu_pn_bwd_kernel(const bf16* __restric
         const float dy = r * g[v][j] - k * t;
         o[j] = pre >= 0.f ? dy : dy * slope;
       }
-      xo[c8] = pack8(o);
+      st8(xo + c8 * 8, o);
     }
   }
 }
@@ -213,9 +229,10 @@ RK_DEV void mb_stats(const float (&xv)[G], int g, float& mu, float& rs) {
 // mode 0: forward   out[N,P,Cp] = [x, f, 0]
 // mode 1: backward  out[N,P,C]  = gx from gout [N,P,Cp]
 // mode 2: backward of backward: out = g_x [N,P,C], out2 = gg_out [N,P,Cp]; a = ggx [N,P,C], b = gout
-__global__ __launch_bounds__(256) void mbstd_kernel(int mode, const bf16* __restrict__ x, const bf16* __restrict__ a,
-                                                    const bf16* __restrict__ b, int N, int P, int C, int Cp, int g,
-                                                    int segs, bf16* __restrict__ out, bf16* __restrict__ out2) {
+template <class T>
+__global__ __launch_bounds__(256) void mbstd_kernel(int mode, const T* __restrict__ x, const T* __restrict__ a,
+                                                    const T* __restrict__ b, int N, int P, int C, int Cp, int g,
+                                                    int segs, T* __restrict__ out, T* __restrict__ out2) {
   __shared__ float red[4];
   const int J = blockIdx.x;
   const int PC = P * C;
@@ -239,13 +256,13 @@ __global__ __launch_bounds__(256) void mbstd_kernel(int mode, const bf16* __rest
       for (int k = 0; k < MB_MAXG; ++k) {
         if (k >= g) break;
         const float v = c < C ? (float)x[smp[k] * PC + (long long)p * C + c] : (c == C ? f : 0.f);
-        out[smp[k] * P * Cp + e] = (bf16)v;
+        out[smp[k] * P * Cp + e] = (T)v;
       }
     }
     return;
   }
   // G_j = sum over the group's extra-channel gradient (mode 1: gout = a; mode 2: gout = b)
-  const bf16* gout = mode == 1 ? a : b;
+  const T* gout = mode == 1 ? a : b;
   float gs = 0.f;
   for (int t = threadIdx.x; t < g * P; t += blockDim.x) {
     const int k = t / P, p = t - k * P;
@@ -266,7 +283,7 @@ __global__ __launch_bounds__(256) void mbstd_kernel(int mode, const bf16* __rest
       for (int k = 0; k < MB_MAXG; ++k) {
         if (k >= g) break;
         const float go = (float)gout[(smp[k] * P + p) * Cp + c];
-        out[smp[k] * PC + e] = (bf16)(go + Gj * (xv[k] - mu) * rs * inv);
+        out[smp[k] * PC + e] = (T)(go + Gj * (xv[k] - mu) * rs * inv);
       }
     }
     return;
@@ -294,13 +311,14 @@ __global__ __launch_bounds__(256) void mbstd_kernel(int mode, const bf16* __rest
       if (k >= g) break;
       const float gg = (float)a[smp[k] * PC + e];
       const float u = (xv[k] - mu) * rs;
-      out[smp[k] * PC + e] = (bf16)(kk * (gg - m1 - u * m2));
+      out[smp[k] * PC + e] = (T)(kk * (gg - m1 - u * m2));
     }
   }
 }
 
-__global__ __launch_bounds__(256) void mbstd_h_kernel(const bf16* __restrict__ x, const bf16* __restrict__ a, int N,
-                                                      int P, int C, int Cp, int g, int segs, bf16* __restrict__ out2) {
+template <class T>
+__global__ __launch_bounds__(256) void mbstd_h_kernel(const T* __restrict__ x, const T* __restrict__ a, int N,
+                                                      int P, int C, int Cp, int g, int segs, T* __restrict__ out2) {
   __shared__ float red[4];
   const int J = blockIdx.x;
   const int PC = P * C;
@@ -327,7 +345,7 @@ __global__ __launch_bounds__(256) void mbstd_h_kernel(const bf16* __restrict__ x
     for (int k = 0; k < MB_MAXG; ++k) {
       if (k >= g) break;
       const float v = c < C ? (float)a[smp[k] * PC + (long long)p * C + c] : (c == C ? H : 0.f);
-      out2[smp[k] * P * Cp + e] = (bf16)v;
+      out2[smp[k] * P * Cp + e] = (T)v;
     }
   }
 }
@@ -336,12 +354,12 @@ __global__ __launch_bounds__(256) void mbstd_h_kernel(const bf16* __restrict__ x
 // row chunks (grid groups x chunks, deterministic), stage B recomputes the per-channel group
 // statistics and writes every member's output, one thread per (group, 8-channel vector).
 // part[J][chunk][2]: mode 0 {sum s, -}; mode 1 {sum gout[.., C], -}; mode 2 {G sum, H sum}.
-template <int G>
-RK_DEV void mb_load(const bf16* __restrict__ base, const long long (&smp)[MB_MAXG], long long stride, long long off,
+template <int G, class T>
+RK_DEV void mb_load(const T* __restrict__ base, const long long (&smp)[MB_MAXG], long long stride, long long off,
                     int g, float (&v)[MB_MAXG][8]) {
 #pragma unroll
   for (int k = 0; k < G; ++k)
-    if (k < g) unpack8(*(const uint4*)(base + smp[k] * stride + off), v[k]);
+    if (k < g) ld8(base + smp[k] * stride + off, v[k]);
 }
 
 RK_DEV void mb_vstats(const float (&xv)[MB_MAXG][8], int g, float (&mu)[8], float (&rs)[8]) {
@@ -359,8 +377,9 @@ RK_DEV void mb_vstats(const float (&xv)[MB_MAXG][8], int g, float (&mu)[8], floa
   }
 }
 
-__global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const bf16* __restrict__ x,
-                                                          const bf16* __restrict__ a, const bf16* __restrict__ gout,
+template <class T>
+__global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const T* __restrict__ x,
+                                                          const T* __restrict__ a, const T* __restrict__ gout,
                                                           int N, int P, int C, int Cp, int g, int segs, int chunks,
                                                           float* __restrict__ part) {
   __shared__ float red[4];
@@ -408,11 +427,12 @@ __global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const bf16* 
   }
 }
 
-__global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const bf16* __restrict__ x,
-                                                          const bf16* __restrict__ a, const bf16* __restrict__ gout,
+template <class T>
+__global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __restrict__ x,
+                                                          const T* __restrict__ a, const T* __restrict__ gout,
                                                           int N, int P, int C, int Cp, int g, int segs, int chunks,
-                                                          const float* __restrict__ part, bf16* __restrict__ out,
-                                                          bf16* __restrict__ out2) {
+                                                          const float* __restrict__ part, T* __restrict__ out,
+                                                          T* __restrict__ out2) {
   const int C8 = C >> 3, V = P * C8;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int J = (int)(t / V), v = (int)(t - (long long)J * V);
@@ -434,10 +454,10 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const bf16* 
 #pragma unroll
     for (int k = 0; k < MB_MAXG; ++k) {
       if (k >= g) break;
-      *(uint4*)(out + smp[k] * PCp + (long long)p * Cp + c8 * 8) = pack8(xv[k]);
+      st8(out + smp[k] * PCp + (long long)p * Cp + c8 * 8, xv[k]);
       if (c8 == 0) {
         float f[8] = {S0 / (float)PC, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        *(uint4*)(out + smp[k] * PCp + (long long)p * Cp + C) = pack8(f);
+        st8(out + smp[k] * PCp + (long long)p * Cp + C, f);
       }
     }
     return;
@@ -453,7 +473,7 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const bf16* 
       float o[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) o[c] = go[k][c] + S0 * (xv[k][c] - mu[c]) * rs[c] * inv;
-      *(uint4*)(out + smp[k] * PC + (long long)v * 8) = pack8(o);
+      st8(out + smp[k] * PC + (long long)v * 8, o);
     }
     return;
   }
@@ -479,11 +499,11 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const bf16* 
       const float u = (xv[k][c] - mu[c]) * rs[c];
       o[c] = S0 * rs[c] * inv * (av[k][c] - m1[c] - u * m2[c]);
     }
-    *(uint4*)(out + smp[k] * PC + (long long)v * 8) = pack8(o);
-    *(uint4*)(out2 + smp[k] * PCp + (long long)p * Cp + c8 * 8) = pack8(av[k]);
+    st8(out + smp[k] * PC + (long long)v * 8, o);
+    st8(out2 + smp[k] * PCp + (long long)p * Cp + c8 * 8, av[k]);
     if (c8 == 0) {
       float f[8] = {S1 * inv, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      *(uint4*)(out2 + smp[k] * PCp + (long long)p * Cp + C) = pack8(f);
+      st8(out2 + smp[k] * PCp + (long long)p * Cp + C, f);
     }
   }
 }
@@ -507,54 +527,77 @@ extern "C" int rk_philox(void* out, long long n, int dist, int hi, float a, floa
   return RK_OK;
 }
 
-// part: fp32 scratch of >= (N/g) * 16 * 2 floats (vectorised path, C % 8 == 0 and Cp == C + 8)
-extern "C" int rk_mbstd(int mode, const void* x, const void* a, const void* b, int N, int P, int C, int Cp, int g,
-                        int segs, void* out, void* out2, float* part, void* stream) {
+namespace {
+
+template <class T>
+int mbstd_launch(int mode, const void* x, const void* a, const void* b, int N, int P, int C, int Cp, int g, int segs,
+                 void* out, void* out2, float* part, hipStream_t s) {
   if (g < 1 || g > MB_MAXG || segs < 1 || N % segs || (N / segs) % g || Cp <= C || mode < 0 || mode > 2)
     return RK_EBADARG;
   const dim3 grid(N / g), block(256);
-  hipStream_t s = (hipStream_t)stream;
   if (part && C % 8 == 0 && Cp == C + 8) {
     const int groups = N / g;
     const int chunks = std::max(1, std::min(16, 1024 / groups));
-    const bf16* gout = (const bf16*)(mode == 1 ? a : b);
-    hipLaunchKernelGGL(mbstd_vec_a_kernel, dim3(groups, chunks), block, 0, s, mode, (const bf16*)x, (const bf16*)a,
+    const T* gout = (const T*)(mode == 1 ? a : b);
+    hipLaunchKernelGGL(mbstd_vec_a_kernel<T>, dim3(groups, chunks), block, 0, s, mode, (const T*)x, (const T*)a,
                        gout, N, P, C, Cp, g, segs, chunks, part);
     const long long threads = (long long)groups * P * (C / 8);
-    hipLaunchKernelGGL(mbstd_vec_b_kernel, dim3((unsigned)((threads + 255) / 256)), block, 0, s, mode,
-                       (const bf16*)x, (const bf16*)a, gout, N, P, C, Cp, g, segs, chunks, part, (bf16*)out,
-                       (bf16*)out2);
+    hipLaunchKernelGGL(mbstd_vec_b_kernel<T>, dim3((unsigned)((threads + 255) / 256)), block, 0, s, mode,
+                       (const T*)x, (const T*)a, gout, N, P, C, Cp, g, segs, chunks, part, (T*)out, (T*)out2);
     RK_LAUNCH_CHECK();
     return RK_OK;
   }
-  hipLaunchKernelGGL(mbstd_kernel, grid, block, 0, s, mode, (const bf16*)x, (const bf16*)a, (const bf16*)b, N, P, C,
-                     Cp, g, segs, (bf16*)out, (bf16*)out2);
+  hipLaunchKernelGGL(mbstd_kernel<T>, grid, block, 0, s, mode, (const T*)x, (const T*)a, (const T*)b, N, P, C, Cp, g,
+                     segs, (T*)out, (T*)out2);
   if (mode == 2)
-    hipLaunchKernelGGL(mbstd_h_kernel, grid, block, 0, s, (const bf16*)x, (const bf16*)a, N, P, C, Cp, g, segs,
-                       (bf16*)out2);
+    hipLaunchKernelGGL(mbstd_h_kernel<T>, grid, block, 0, s, (const T*)x, (const T*)a, N, P, C, Cp, g, segs, (T*)out2);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
-extern "C" int rk_lrelu_pixelnorm(const void* x, const float* bias, const void* dz, int P, int C, float slope,
-                                  float eps, void* out, void* stream) {
+template <class T>
+int lrelu_pn_launch(const void* x, const float* bias, const void* dz, int P, int C, float slope, float eps, void* out,
+                    hipStream_t s) {
   if (P <= 0) return RK_OK;
   if (C % 8 || C > 1024) return RK_EUNSUPPORTED;
   const dim3 grid(rk_cdiv(P, 4)), block(256);
-  hipStream_t s = (hipStream_t)stream;
   if (dz == nullptr) {
     if (C <= 512)
-      hipLaunchKernelGGL(lrelu_pn_fwd_kernel<1>, grid, block, 0, s, (const bf16*)x, bias, P, C, slope, eps, (bf16*)out);
+      hipLaunchKernelGGL((lrelu_pn_fwd_kernel<1, T>), grid, block, 0, s, (const T*)x, bias, P, C, slope, eps, (T*)out);
     else
-      hipLaunchKernelGGL(lrelu_pn_fwd_kernel<2>, grid, block, 0, s, (const bf16*)x, bias, P, C, slope, eps, (bf16*)out);
+      hipLaunchKernelGGL((lrelu_pn_fwd_kernel<2, T>), grid, block, 0, s, (const T*)x, bias, P, C, slope, eps, (T*)out);
   } else {
     if (C <= 512)
-      hipLaunchKernelGGL(lrelu_pn_bwd_kernel<1>, grid, block, 0, s, (const bf16*)x, bias, (const bf16*)dz, P, C, slope,
-                         eps, (bf16*)out);
+      hipLaunchKernelGGL((lrelu_pn_bwd_kernel<1, T>), grid, block, 0, s, (const T*)x, bias, (const T*)dz, P, C, slope,
+                         eps, (T*)out);
     else
-      hipLaunchKernelGGL(lrelu_pn_bwd_kernel<2>, grid, block, 0, s, (const bf16*)x, bias, (const bf16*)dz, P, C, slope,
-                         eps, (bf16*)out);
+      hipLaunchKernelGGL((lrelu_pn_bwd_kernel<2, T>), grid, block, 0, s, (const T*)x, bias, (const T*)dz, P, C, slope,
+                         eps, (T*)out);
   }
   RK_LAUNCH_CHECK();
   return RK_OK;
+}
+
+}  // namespace
+
+// part: fp32 scratch of >= (N/g) * 16 * 2 floats (vectorised path, C % 8 == 0 and Cp == C + 8).
+// rk_mbstd / rk_lrelu_pixelnorm: bf16 tensors; the _f32 entry points: fp32 tensors.
+extern "C" int rk_mbstd(int mode, const void* x, const void* a, const void* b, int N, int P, int C, int Cp, int g,
+                        int segs, void* out, void* out2, float* part, void* stream) {
+  return mbstd_launch<bf16>(mode, x, a, b, N, P, C, Cp, g, segs, out, out2, part, (hipStream_t)stream);
+}
+
+extern "C" int rk_mbstd_f32(int mode, const void* x, const void* a, const void* b, int N, int P, int C, int Cp, int g,
+                            int segs, void* out, void* out2, float* part, void* stream) {
+  return mbstd_launch<float>(mode, x, a, b, N, P, C, Cp, g, segs, out, out2, part, (hipStream_t)stream);
+}
+
+extern "C" int rk_lrelu_pixelnorm(const void* x, const float* bias, const void* dz, int P, int C, float slope,
+                                  float eps, void* out, void* stream) {
+  return lrelu_pn_launch<bf16>(x, bias, dz, P, C, slope, eps, out, (hipStream_t)stream);
+}
+
+extern "C" int rk_lrelu_pixelnorm_f32(const void* x, const float* bias, const void* dz, int P, int C, float slope,
+                                      float eps, void* out, void* stream) {
+  return lrelu_pn_launch<float>(x, bias, dz, P, C, slope, eps, out, (hipStream_t)stream);
 }

@@ -37,7 +37,11 @@ constexpr unsigned SOOB = 0x80000000u;
 
 // SM_KIN_CONVF: SM_KIN_CONV with C % 32 == 0, so a 32-deep K-tile never straddles a tap and the
 // tap / channel offset of every DMA is wave-uniform (~4 VALU per DMA instead of ~20)
-enum SMode { SM_KIN_DENSE = 0, SM_KIN_CONV = 1, SM_KOUT_DENSE = 2, SM_KOUT_CONV = 3, SM_KIN_CONVF = 4 };
+// SM_KIN_CONVG / SM_KOUT_CONVG: table-driven gathers for the PG-GAN resampling convs — rows over an
+// Ho x Wo output grid, source pixel stride*(i, j) + (dy_t, dx_t) of an H x W input, up to 16 taps
+// per parity group (see rk_sgemm_g)
+enum SMode { SM_KIN_DENSE = 0, SM_KIN_CONV = 1, SM_KOUT_DENSE = 2, SM_KOUT_CONV = 3, SM_KIN_CONVF = 4,
+             SM_KIN_CONVG = 5, SM_KOUT_CONVG = 6 };
 enum SFlags { SF_RELU = 1, SF_BIAS = 2, SF_STATS = 4, SF_GATE = 8, SF_ACCUM = 16, SF_LRELU = 32,
               SF_BNB = 512, SF_BNP = 1024 };
 
@@ -62,6 +66,13 @@ struct SgParams {
   float alpha, slope;
   unsigned long long bytesA, bytesB;
   int dbg;  // diagnostics (RAFIKI_SGEMM_DBG): 1 no DMA in the K loop (stale LDS), 2 no K-loop barrier
+  // table-driven gathers (SM_KIN_CONVG / SM_KOUT_CONVG); H, W above = the INPUT map
+  int Ho, Wo, log2Ho, log2Wo;  // row grid (output pixels of the gather)
+  float invHo, invWo;
+  int stride, ntaps, groups, os;
+  unsigned tpy[4], tpx[4];     // per group, tap t: offset = ((word >> 2t) & 3) - 1  (in -1 .. 2)
+  unsigned oyx;                // per group g: output parity (bits 2g: oy, 2g+1: ox) when os == 2
+  long long gstrideB;          // floats between the groups' B operands
 };
 
 RK_DEV __amdgpu_buffer_rsrc_t s_rsrc(const void* base, unsigned long long bytes) {
@@ -76,6 +87,26 @@ RK_DEV int s_tap_dx(int t) { return t - 3 * ((t * 11) >> 5) - 1; }
 RK_DEV int s_cdiv(int k, const SgParams& p) {
   return p.log2C >= 0 ? (k >> p.log2C) : (int)(((float)k + 0.5f) * p.invC);
 }
+// pixel -> (n, i, j) of an N x Ho x Wo grid
+RK_DEV void s_nhw(int k, const SgParams& p, int& n, int& i, int& j) {
+  int q;
+  if (p.log2Wo >= 0) {
+    q = k >> p.log2Wo;
+    j = k & (p.Wo - 1);
+  } else {
+    q = (int)(((float)k + 0.5f) * p.invWo);
+    j = k - q * p.Wo;
+  }
+  if (p.log2Ho >= 0) {
+    n = q >> p.log2Ho;
+    i = q & (p.Ho - 1);
+  } else {
+    n = (int)(((float)q + 0.5f) * p.invHo);
+    i = q - n * p.Ho;
+  }
+}
+RK_DEV int s_tapoff(unsigned word, int t) { return (int)((word >> (2 * t)) & 3u) - 1; }
+
 // pixel -> (h, w) of an H x W map
 RK_DEV void s_hw(int k, int H, int W, int log2H, int log2W, float invH, float invW, int& h, int& w) {
   if (log2H >= 0 && log2W >= 0) {
@@ -93,7 +124,8 @@ RK_DEV void s_hw(int k, int H, int W, int log2H, int log2W, float invH, float in
 // wave-instructions, T/(8*NW) per wave of an NW-wave workgroup.
 template <int MODE, int T, int NW>
 struct SOperand {
-  static constexpr bool KIN = MODE == SM_KIN_DENSE || MODE == SM_KIN_CONV || MODE == SM_KIN_CONVF;
+  static constexpr bool KIN = MODE == SM_KIN_DENSE || MODE == SM_KIN_CONV || MODE == SM_KIN_CONVF ||
+                              MODE == SM_KIN_CONVG;
   static constexpr int NQ = T / (8 * NW);
   static_assert(NQ >= 1 && NQ * 8 * NW == T, "operand tile must split evenly over the waves");
   static constexpr int RS = T / 4;  // 16-B slots per K-outer row
@@ -103,10 +135,16 @@ struct SOperand {
   int sub[NQ];
   int dyx[NQ];  // K-outer conv: (dy, dx) packed as dy*W + dx
   int dy[NQ], dx[NQ];
+  unsigned tpy, tpx;  // table-driven gathers: this group's tap offsets
 
   RK_DEV void init(const SgParams& p, const float* ptr, unsigned long long bytes, int ld, int tile0, int extent,
-                   int wid, int lane) {
+                   int wid, int lane, int grp = 0) {
     rsrc = s_rsrc(ptr, bytes);
+    tpy = tpx = 0u;
+    if constexpr (MODE == SM_KIN_CONVG || MODE == SM_KOUT_CONVG) {
+      tpy = p.tpy[grp];
+      tpx = p.tpx[grp];
+    }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int slot = (wid * NQ + q) * 64 + lane;
@@ -120,6 +158,16 @@ struct SOperand {
         if constexpr (MODE == SM_KIN_DENSE) {
           base[q] = (unsigned)gi * (unsigned)ld * 4u;
           mask[q] = ok ? 1u : 0u;
+        } else if constexpr (MODE == SM_KIN_CONVG) {
+          int n, i, j;
+          s_nhw(gi, p, n, i, j);
+          const int si = p.stride * i, sj = p.stride * j;
+          base[q] = (unsigned)(((n * p.H + si) * p.W + sj) * p.C) * 4u;
+          unsigned m = 0u;
+          for (int t = 0; t < p.ntaps; ++t)
+            m |= (((unsigned)(si + s_tapoff(tpy, t)) < (unsigned)p.H && (unsigned)(sj + s_tapoff(tpx, t)) < (unsigned)p.W)
+                      ? 1u : 0u) << t;
+          mask[q] = ok ? m : 0u;
         } else {
           int h, w;
           s_hw(gi, p.H, p.W, p.log2H, p.log2W, p.invH, p.invW, h, w);
@@ -142,6 +190,14 @@ struct SOperand {
         bool ok = col < extent;
         if constexpr (MODE == SM_KOUT_DENSE) {
           base[q] = (unsigned)col * 4u;
+        } else if constexpr (MODE == SM_KOUT_CONVG) {  // column = (tap, channel), tap from the table
+          const int tap = s_cdiv(col, p);
+          const int ci = col - tap * p.C;
+          ok = ok && tap < p.ntaps;
+          const int tt = tap < p.ntaps ? tap : 0;
+          dy[q] = s_tapoff(tpy, tt);
+          dx[q] = s_tapoff(tpx, tt);
+          base[q] = (unsigned)ci * 4u;
         } else {  // SM_KOUT_CONV: column = (tap, channel) of the gathered activation
           const int tap = s_cdiv(col, p);
           const int ci = col - tap * p.C;
@@ -181,10 +237,25 @@ struct SOperand {
       const int d = p.taps == 9 ? s_tap_dy(tap) * p.W + s_tap_dx(tap) : 0;
       const bool ok = k < K && ((mask[q] >> tap) & 1u);
       return (unsigned)((int)base[q] + (d * p.C + ci) * 4) | ((unsigned)!ok << 31);
+    } else if constexpr (MODE == SM_KIN_CONVG) {
+      const int k = kt * SBK + 4 * sub[q];
+      const int tap = s_cdiv(k, p);
+      const int ci = k - tap * p.C;
+      const int tt = tap & 15;
+      const int d = s_tapoff(tpy, tt) * p.W + s_tapoff(tpx, tt);
+      const bool ok = k < K && ((mask[q] >> tt) & 1u);
+      return (unsigned)((int)base[q] + (d * p.C + ci) * 4) | ((unsigned)!ok << 31);
     } else if constexpr (MODE == SM_KOUT_DENSE) {
       const int k = kt * SBK + sub[q];
       const bool ok = mask[q] && k < K;
       return (base[q] + (unsigned)k * (unsigned)ld * 4u) | ((unsigned)!ok << 31);
+    } else if constexpr (MODE == SM_KOUT_CONVG) {  // row k = output pixel (n, i, j) of the Ho x Wo grid
+      const int k = kt * SBK + sub[q];
+      int n, i, j;
+      s_nhw(k, p, n, i, j);
+      const int si = p.stride * i + dy[q], sj = p.stride * j + dx[q];
+      const bool ok = mask[q] && k < K && (unsigned)si < (unsigned)p.H && (unsigned)sj < (unsigned)p.W;
+      return (unsigned)(((n * p.H + si) * p.W + sj) * p.C * 4 + (int)base[q]) | ((unsigned)!ok << 31);
     } else {  // SM_KOUT_CONV: row k = pixel, column chunk = 4 channels of one tap
       const int k = kt * SBK + sub[q];
       const int qq = (int)(((float)k + 0.5f) * p.invW);
@@ -276,8 +347,9 @@ RK_DEV void s_group_sched() {
 RK_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // PA / PB: the A (rows) / B (columns) fragments were read interleaved (frag_pair)
-template <int MI, int NI, bool PA, bool PB>
-RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int nbase, int lane, int split) {
+template <int MI, int NI, bool PA, bool PB, bool OMAP = false>
+RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int nbase, int lane, int split,
+                       int grp = 0) {
   const int fl = p.flags;
   const int h = lane >> 5;
   float* C = p.out + (long long)split * p.slabStride;
@@ -297,7 +369,16 @@ RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int 
         const int m = PA ? mbase + 2 * acc_row(r, h) + mi : mbase + mi * 32 + acc_row(r, h);
         if (!(nok && m < p.M)) continue;
         float v = acc[mi][ni][r] * p.alpha;
-        const long long idx = (long long)m * p.ldc + n;
+        long long row = m;
+        if constexpr (OMAP) {   // parity group: row (n, i, j) of the Ho x Wo grid -> pixel (2i+oy, 2j+ox)
+          if (p.os == 2) {
+            int b, i, j;
+            s_nhw(m, p, b, i, j);
+            const int oy = (p.oyx >> (2 * grp)) & 1, ox = (p.oyx >> (2 * grp + 1)) & 1;
+            row = ((long long)b * 2 * p.Ho + 2 * i + oy) * (2 * p.Wo) + 2 * j + ox;
+          }
+        }
+        const long long idx = row * p.ldc + n;
         if (fl & SF_BIAS) v += b;
         if (fl & SF_STATS) {
           s += v;
@@ -364,8 +445,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
   // ordered (split, tile), so the tiles that share a split's K range (the same dY / X pixel rows of a
   // weight gradient) run on one XCD and hit one L2
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = lin / tiles;
-  const int bid = lin - split * tiles;
+  int grp = 0, rem = lin;
+  if constexpr (AM == SM_KIN_CONVG) {   // parity groups: grid = groups x splits x tiles
+    const int per = (int)(gridDim.x / p.groups);
+    grp = lin / per;
+    rem = lin - grp * per;
+  }
+  const int split = rem / tiles;
+  const int bid = rem - split * tiles;
   const int mt = bid / tilesN, nt = bid - mt * tilesN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int nk = (p.K + SBK - 1) / SBK;
@@ -374,8 +461,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
 
   SOperand<AM, BM, NW> A;
   SOperand<BMD, BN, NW> B;
-  A.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane);
-  B.init(p, p.B, p.bytesB, p.ldb, n0, p.N, wid, lane);
+  A.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane, grp);
+  if constexpr (AM == SM_KIN_CONVG)
+    B.init(p, p.B + grp * p.gstrideB, p.bytesB - (unsigned long long)(grp * p.gstrideB) * 4ull, p.ldb, n0, p.N,
+           wid, lane);
+  else
+    B.init(p, p.B, p.bytesB, p.ldb, n0, p.N, wid, lane);
 
   f32x16 acc[MI][NI];
 #pragma unroll
@@ -452,15 +543,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
     st = st + 1 == NST ? 0 : st + 1;
   }
   s_wait_vmcnt<0>();  // the trailing zero-DMAs land before the workgroup's LDS is released
-  s_epilogue<MI, NI, !SOperand<AM, BM, NW>::KIN && MI == 2, !SOperand<BMD, BN, NW>::KIN && NI == 2>(
-      p, acc, m0 + wm * WMT, n0 + wn * WNT, lane, split);
+  s_epilogue<MI, NI, !SOperand<AM, BM, NW>::KIN && MI == 2, !SOperand<BMD, BN, NW>::KIN && NI == 2,
+             AM == SM_KIN_CONVG>(p, acc, m0 + wm * WMT, n0 + wn * WNT, lane, split, grp);
 }
 
 template <int WGM, int WGN, int MI, int NI, int AM, int BMD>
 int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
   const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
-  dim3 grid(tiles * splits);
+  dim3 grid(tiles * splits * (AM == SM_KIN_CONVG ? p.groups : 1));
   if (nst == 3) {
     if constexpr (WGM * WGN == 4)  // 3-stage rings only for the 4-wave tiles (8-wave ones fill LDS at 2)
       hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3>), grid, dim3(64 * WGM * WGN), 0, st, p);
@@ -540,6 +631,8 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   static const int dbg = getenv("RAFIKI_SGEMM_DBG") ? atoi(getenv("RAFIKI_SGEMM_DBG")) : 0;
   p.dbg = dbg;
+  p.groups = 1;
+  p.Ho = H; p.Wo = W; p.log2Ho = p.log2H; p.log2Wo = p.log2W; p.invHo = p.invH; p.invWo = p.invW;
   hipStream_t st = (hipStream_t)stream;
   switch (kind) {
     case 0:
@@ -551,4 +644,54 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
     case 5: return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_DENSE, false>(tile, p, nst, splits, st);
   }
   return RK_EBADARG;
+}
+
+// Table-driven gathers (the PG-GAN resampling convolutions).
+// kind 6 — forward: out[row][n] = sum_{t, c} B_g[n][t*C + c] * A[src_t(row)][c] over `groups` parity
+//   groups (grid groups x splits x tiles); rows = pixels (b, i, j) of the Ho x Wo grid, source pixel
+//   (stride*i + dy_t, stride*j + dx_t) of the H x W input (zero outside), B_g = B + g * gstrideB
+//   ([N][ntaps*C]).  os == 2: group g writes output pixel (2i + oy_g, 2j + ox_g) of a 2Ho x 2Wo map.
+// kind 7 — weight gradient: out[m][t*C + c] = sum_rows A[row][m] * X[src_t(row)][c] (A = dY [rows][M],
+//   X = the gathered input), one group.
+// tpy / tpx: per group, 2-bit tap offsets (value + 1); oyx: per group 2 bits (oy, ox).
+extern "C" int rk_sgemm_g(int kind, int tile, int nst, const float* A, const float* B, float* C, const float* bias,
+                          int M, int N, int K, int lda, int ldb, int ldc, int H, int W, int Cch, int Ho, int Wo,
+                          int stride, int ntaps, int groups, const unsigned* tpy, const unsigned* tpx, unsigned oyx,
+                          int os, long long gstrideB, int splits, long long slabStride, int flags, float alpha,
+                          float slope, long long bytesA, long long bytesB, void* stream) {
+  if (kind != 6 && kind != 7) return RK_EBADARG;
+  if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 3) return RK_EBADARG;
+  if (ntaps < 1 || ntaps > 16 || groups < 1 || groups > 4 || (stride != 1 && stride != 2) || (os != 1 && os != 2))
+    return RK_EBADARG;
+  if (kind == 7 && groups != 1) return RK_EBADARG;
+  if (Cch % 4 || Cch <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return RK_EUNSUPPORTED;
+  if ((kind == 6 ? K : N) != ntaps * Cch) return RK_EBADARG;
+  if (kind == 6 && (lda % 4 || ldb % 4)) return RK_EUNSUPPORTED;
+  if (kind == 7 && (N % 4 || M % 4 || lda % 4)) return RK_EUNSUPPORTED;
+  if (splits > 1 && (flags & (SF_BIAS | SF_RELU | SF_LRELU | SF_GATE | SF_STATS | SF_BNB | SF_BNP))) return RK_EBADARG;
+  if (flags & (SF_GATE | SF_STATS | SF_BNB | SF_BNP)) return RK_EUNSUPPORTED;
+  // reciprocal decodes are exact below 2^22
+  const long long rows = kind == 6 ? M : K;
+  if (rows + (long long)W * (H + 2) >= (1ll << 22) || (long long)ntaps * Cch >= (1ll << 22)) return RK_EUNSUPPORTED;
+  SgParams p{};
+  p.A = A; p.B = B; p.out = C; p.bias = bias;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.H = H; p.W = W; p.C = Cch; p.taps = ntaps;
+  p.log2H = rk_log2(H); p.log2W = rk_log2(W); p.log2C = rk_log2(Cch);
+  p.invC = 1.0f / (float)Cch; p.invH = 1.0f / (float)H; p.invW = 1.0f / (float)W;
+  p.Ho = Ho; p.Wo = Wo; p.log2Ho = rk_log2(Ho); p.log2Wo = rk_log2(Wo);
+  p.invHo = 1.0f / (float)Ho; p.invWo = 1.0f / (float)Wo;
+  p.stride = stride; p.ntaps = ntaps; p.groups = groups; p.os = os; p.oyx = oyx; p.gstrideB = gstrideB;
+  for (int g = 0; g < 4; ++g) {
+    p.tpy[g] = g < groups ? tpy[g] : 0u;
+    p.tpx[g] = g < groups ? tpx[g] : 0u;
+  }
+  p.ktPer = rk_cdiv(rk_cdiv(K, SBK), splits);
+  p.slabStride = splits > 1 ? slabStride : 0;
+  p.flags = flags; p.alpha = alpha; p.slope = slope;
+  p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
+  hipStream_t st = (hipStream_t)stream;
+  if (kind == 6) return s_launch_tile<SM_KIN_CONVG, SM_KIN_DENSE, false>(tile, p, nst, splits, st);
+  return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_CONVG, false>(tile, p, nst, splits, st);
 }

@@ -19,6 +19,7 @@ _lock = threading.Lock()
 _lib = None
 
 vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
+u32p = C.POINTER(C.c_uint)
 
 # name -> argtypes (all return int status: 0 ok, <0 error)
 _SIGS = {
@@ -73,6 +74,13 @@ _SIGS = {
     "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, vp],
     "rk_pack_nhwc_f32": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
     "rk_softmax_xent_f32": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],
+    # table-driven gathers (PG-GAN up / down convs), resampling, fp32 PG-GAN side kernels
+    "rk_sgemm_g": [i32, i32, i32, vp, vp, vp, vp] + [i32] * 14 + [u32p, u32p, C.c_uint, i32, i64, i32, i64, i32, f32,
+                                                                 f32, i64, i64, vp],
+    "rk_resample2x": [i32, i32, vp, vp, i32, i32, i32, i32, f32, vp],
+    "rk_s2t_weights": [vp, vp, i32, i32, vp],
+    "rk_mbstd_f32": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
+    "rk_lrelu_pixelnorm_f32": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
 }
 
 _OPTIONAL: set[str] = set()

@@ -436,3 +436,162 @@ def pack_nhwc(images, cpad=4, scale=1.0, shift=0.0, out=None, nhwc=False):
     _lib.call("rk_pack_nhwc_f32", _p(images.contiguous()), is_u8 | (2 if nhwc else 0), Nb, Cc, H, W, cpad,
               float(scale), float(shift), _p(out), _s())
     return out
+
+
+# ------------------------------------------------------------------- stride-2 gather convolutions
+# The PG-GAN resampling convs as one family closed under differentiation:
+#   S2(x, W)  : y[o]  = sum_t W[t] x[2o + d_t]       (4x4 taps d_t in {-1..2}^2, stride 2)
+#   S2T(z, W) : x'[p] = sum_{o,t: 2o + d_t = p} W[t]^T z[o]    (its adjoint: the 2x transposed conv)
+#   S2W(x, g) : dW[t] = sum_o g[o] x[2o + d_t]^T   (weight gradient)
+# with W [Co][16][Ci] (tap t = 4(dy+1) + dx+1).  conv3x3 + 2x2 box downscale (_conv2d_downscale2d,
+# pg_gans.py:1053-1059) is S2 with box-summed weights; upscale2d + conv3x3 (_upscale2d_conv2d,
+# pg_gans.py:1032-1039) is S2T with box-summed flipped weights — both at 1/2.25 of the MACs of the
+# full-resolution conv and without any materialised 2x tensor.
+def _tap_word(vals):
+    w = 0
+    for t, v in enumerate(vals):
+        w |= (int(v) + 1 & 3) << (2 * t)
+    return w
+
+
+def _par_d(r, u):
+    return (0 if u == 0 else 2) if r == 0 else (1 if u == 0 else -1)
+
+
+_S2_TPY = _tap_word([t // 4 - 1 for t in range(16)])
+_S2_TPX = _tap_word([t % 4 - 1 for t in range(16)])
+# S2T parity group g = 2 ry + rx, tap t4 = 2u + v: source offset (r - d) / 2 of the matching S2 tap
+_S2T_TPY = [_tap_word([(g >> 1) - _par_d(g >> 1, t4 >> 1) >> 1 for t4 in range(4)]) for g in range(4)]
+_S2T_TPX = [_tap_word([(g & 1) - _par_d(g & 1, t4 & 1) >> 1 for t4 in range(4)]) for g in range(4)]
+_S2T_OYX = sum(((g >> 1) | ((g & 1) << 1)) << (2 * g) for g in range(4))
+
+
+def _u32x4(vals):
+    import ctypes
+    v = list(vals) + [0] * (4 - len(vals))
+    return (ctypes.c_uint * 4)(*v)
+
+
+def sgemm_g(kind, A, B, out, M, N, K, lda, ldb, ldc, H, W, C, Ho, Wo, stride, ntaps, tpy, tpx, *, groups=1, oyx=0,
+            os_=1, gstride_b=0, tile=0, nst=2, splits=1, slab_stride=0, bias=None, flags=0, alpha=1.0, slope=0.2):
+    _lib.call("rk_sgemm_g", int(kind), int(tile), int(nst), _p(A), _p(B), _p(out), _p(bias), int(M), int(N), int(K),
+              int(lda), int(ldb), int(ldc), int(H), int(W), int(C), int(Ho), int(Wo), int(stride), int(ntaps),
+              int(groups), _u32x4(tpy), _u32x4(tpx), int(oyx), int(os_), int(gstride_b), int(splits),
+              int(slab_stride), int(flags), float(alpha), float(slope), _nbytes(A), _nbytes(B), _s())
+    return out
+
+
+def _act_flags(bias, act):
+    return (F_BIAS if bias is not None else 0) | (F_RELU if act == ACT_RELU else F_LRELU if act == ACT_LRELU else 0)
+
+
+def s2_conv(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None):
+    """S2: x [N, H, W, Ci] -> [N, H/2, W/2, Co] with W [Co, 16*Ci] (+bias, act)."""
+    _check(x, 's2_conv x')
+    Nb, H, Wd, Ci = x.shape
+    Co = W.shape[0]
+    assert W.numel() == Co * 16 * Ci and H % 2 == 0 and Wd % 2 == 0, (W.shape, x.shape)
+    Ho, Wo = H // 2, Wd // 2
+    M, K = Nb * Ho * Wo, 16 * Ci
+    if out is None:
+        out = torch.empty((Nb, Ho, Wo, Co), device=x.device, dtype=torch.float32)
+    flags = _act_flags(bias, act)
+
+    def run(cfg):
+        tile, nst, s = cfg
+        geo = (H, Wd, Ci, Ho, Wo, 2, 16, [_S2_TPY], [_S2_TPX])
+        if s == 1:
+            sgemm_g(6, x, W, out, M, Co, K, Ci, K, Co, *geo, tile=tile, nst=nst, bias=bias, flags=flags, slope=slope)
+            return
+        slab = torch.empty((s, M, Co), device=x.device, dtype=torch.float32)
+        sgemm_g(6, x, W, slab, M, Co, K, Ci, K, Co, *geo, tile=tile, nst=nst, splits=s, slab_stride=M * Co)
+        sreduce_epi(slab, M, Co, out.view(M, Co), bias=bias, act=act, slope=slope)
+    run(_pick(('s2f', M, Co, K, H, Wd, Ci, flags), _cands(M, Co, splittable=Co % 4 == 0, K=K), run))
+    return out
+
+
+def s2t_weights(W, Co, Ci):
+    """W [Co, 16*Ci] -> the 4 parity groups' [Ci][4 taps * Co] B operands of S2T."""
+    out = torch.empty((4, Ci, 4 * Co), device=W.device, dtype=torch.float32)
+    _lib.call("rk_s2t_weights", _p(W), _p(out), int(Co), int(Ci), _s())
+    return out
+
+
+def s2t_conv(z, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wr=None):
+    """S2T: z [N, h, w, Co] -> [N, 2h, 2w, Ci] (the adjoint of S2 with the same W [Co, 16*Ci]):
+    four output-parity GEMMs of 4 taps each in ONE launch (grid = 4 parity groups x tiles)."""
+    _check(z, 's2t_conv z')
+    Nb, h, w, Co = z.shape
+    Ci = W.numel() // (16 * Co)
+    assert W.numel() == Co * 16 * Ci
+    if wr is None:
+        wr = s2t_weights(W, Co, Ci)
+    M, K = Nb * h * w, 4 * Co
+    if out is None:
+        out = torch.empty((Nb, 2 * h, 2 * w, Ci), device=z.device, dtype=torch.float32)
+    flags = _act_flags(bias, act)
+    geo = (h, w, Co, h, w, 1, 4, _S2T_TPY, _S2T_TPX)
+    kw = dict(groups=4, oyx=_S2T_OYX, os_=2, gstride_b=Ci * K)
+
+    def run(cfg):
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm_g(6, z, wr, out, M, Ci, K, Co, K, Ci, *geo, tile=tile, nst=nst, bias=bias, flags=flags, slope=slope,
+                    **kw)
+            return
+        slab = torch.empty((s, 4 * M, Ci), device=z.device, dtype=torch.float32)
+        sgemm_g(6, z, wr, slab, M, Ci, K, Co, K, Ci, *geo, tile=tile, nst=nst, splits=s, slab_stride=4 * M * Ci, **kw)
+        sreduce_epi(slab, 4 * M, Ci, out.view(4 * M, Ci), bias=bias, act=act, slope=slope)
+    run(_pick(('s2t', M, Ci, K, h, w, Co, flags), _cands(M, Ci, splittable=Ci % 4 == 0, K=K), run))
+    return out
+
+
+def s2_wgrad(x, g, *, out=None):
+    """S2W: dW [Co, 16*Ci] = sum_o g[o] (x) x[2o + d_t]; x [N, H, W, Ci], g [N, H/2, W/2, Co]."""
+    _check(x, 's2_wgrad x')
+    _check(g, 's2_wgrad g')
+    Nb, H, Wd, Ci = x.shape
+    Co = g.shape[-1]
+    Ho, Wo = H // 2, Wd // 2
+    assert g.shape == (Nb, Ho, Wo, Co), (g.shape, x.shape)
+    M, N, K = Co, 16 * Ci, Nb * Ho * Wo
+    if out is None:
+        out = torch.empty((Co, N), device=x.device, dtype=torch.float32)
+    geo = (H, Wd, Ci, Ho, Wo, 2, 16, [_S2_TPY], [_S2_TPX])
+
+    def run(cfg):
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm_g(7, g, x, out, M, N, K, Co, Ci, N, *geo, tile=tile, nst=nst)
+            return
+        slab = torch.empty((s, M, N), device=x.device, dtype=torch.float32)
+        sgemm_g(7, g, x, slab, M, N, K, Co, Ci, N, *geo, tile=tile, nst=nst, splits=s, slab_stride=M * N)
+        reduce_slabs(slab, out)
+    cands = _cands(M, N, splittable=True, K=K)
+    split = [c for c in cands if c[2] > 1]
+    if split:
+        cands = [max(split, key=lambda c: min(cdiv(M, TILES[c[0]][0]) * cdiv(N, TILES[c[0]][1]) * c[2],
+                                              2 * NUM_CU))] + cands
+    run(_pick(('s2w', M, N, K, H, Wd, Ci), cands, run))
+    return out
+
+
+# ------------------------------------------------------------------------------------ resampling
+def upscale2x(x, scale=1.0, out=None):
+    """nearest 2x upscale of NHWC fp32 / bf16 (times ``scale``)."""
+    Nb, H, W, Cc = x.shape
+    if out is None:
+        out = torch.empty((Nb, 2 * H, 2 * W, Cc), device=x.device, dtype=x.dtype)
+    _lib.call("rk_resample2x", 0, int(x.dtype == torch.bfloat16), _p(x.contiguous()), _p(out), Nb, H, W, Cc,
+              float(scale), _s())
+    return out
+
+
+def downscale2x(x, scale=0.25, out=None):
+    """``scale`` x 2x2 sum of NHWC fp32 / bf16 (0.25: the box-filter downscale2d)."""
+    Nb, H, W, Cc = x.shape
+    if out is None:
+        out = torch.empty((Nb, H // 2, W // 2, Cc), device=x.device, dtype=x.dtype)
+    _lib.call("rk_resample2x", 1, int(x.dtype == torch.bfloat16), _p(x.contiguous()), _p(out), Nb, H, W, Cc,
+              float(scale), _s())
+    return out
