@@ -101,6 +101,24 @@ __global__ __launch_bounds__(256) void s2t_weights_kernel(const float* __restric
   }
 }
 
+// data-gradient weights of a taps-tap conv: out[ci][taps-1-t][co] = w[co][t][ci] (dgrad = forward conv
+// of dy with these).  grid (ceil(Ci/32), ceil(Co/32), taps), block 256
+__global__ __launch_bounds__(256) void wflip_t_kernel(const float* __restrict__ w, float* __restrict__ out, int Co,
+                                                      int Ci, int taps) {
+  __shared__ float tile[32][33];
+  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 32, t = blockIdx.z;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8) {
+    const int co = co0 + r, ci = ci0 + tx;
+    tile[r][tx] = (co < Co && ci < Ci) ? w[((long long)co * taps + t) * Ci + ci] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (ci < Ci && co < Co) out[((long long)ci * taps + (taps - 1 - t)) * Co + co] = tile[tx][r];
+  }
+}
+
 int grid_n(long long work, int cap) {
   long long g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : g > cap ? cap : g);
@@ -138,6 +156,15 @@ extern "C" int rk_s2t_weights(const float* W, float* out, int Co, int Ci, void* 
   if (Co <= 0 || Ci <= 0) return RK_EBADARG;
   hipLaunchKernelGGL(s2t_weights_kernel, dim3(rk_cdiv(Ci, 32), rk_cdiv(Co, 32), 16), dim3(256), 0, (hipStream_t)stream,
                      W, out, Co, Ci);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// w [Co][taps][Ci] fp32 -> out [Ci][taps][Co] with the taps reversed (conv data-gradient weights)
+extern "C" int rk_wflip_t(const float* w, float* out, int Co, int Ci, int taps, void* stream) {
+  if (Co <= 0 || Ci <= 0 || taps <= 0) return RK_EBADARG;
+  hipLaunchKernelGGL(wflip_t_kernel, dim3(rk_cdiv(Ci, 32), rk_cdiv(Co, 32), taps), dim3(256), 0, (hipStream_t)stream,
+                     w, out, Co, Ci, taps);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

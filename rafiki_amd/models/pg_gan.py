@@ -5,12 +5,16 @@ Optimizer :1093-1225, TrainingSchedule :1227-1274, losses :1276-1328).  Same kno
 losses, Gs moving average, optimizer-state reset per level of detail, TFRecord dataset format and
 predict contract ([grid_w, grid_h, n_images] -> JPEG file paths).  Re-designed for MI355X:
 
-* NHWC bf16 activations, fp32 master weights in a flat arena (``engine.flat``); every conv / dense
-  runs on the gfx950 implicit-GEMM MFMA kernels through twice-differentiable autograd Functions
-  (``ops.autograd``) — the gradient penalty's double backward goes through the same kernels;
-* the fused upscale2d+conv3x3 (``Conv0_up``) gathers from the half-resolution input inside the
-  conv kernel (no materialised 2x tensor); the 513-channel minibatch-stddev conv runs on the
-  non-power-of-two channel path (padded to 520);
+* fp32 by default (the reference's precision, pg_gans.py:830,914): NHWC fp32 activations on the
+  v_mfma_f32_32x32x2_f32 kernels (``ops.f32``); ``dtype='bf16'`` (knob or RAFIKI_DTYPE) opts into the
+  bf16 MFMA kernels.  Weights live as fp32 masters in a flat arena (``engine.flat``); every conv /
+  dense runs through twice-differentiable autograd Functions (``ops.autograd``) — the gradient
+  penalty's double backward goes through the same kernels;
+* the resampling convs are native: ``Conv0_up`` (upscale2d + conv3x3) is one parity-grouped
+  transposed-conv launch reading the half-resolution input, ``Conv1_down`` (conv3x3 + downscale2d)
+  one 4x4 stride-2 gather conv — 1/2.25 of the full-resolution MACs, no 2x tensor, and their
+  backward passes are the same family; the LOD blends' upscale2d / downscale2d are native kernels;
+  the 513-channel minibatch-stddev conv runs on the non-power-of-two channel path (padded to 520);
 * equalized learning rate by re-parameterisation (arena holds c*w, Adam steps with lr*c, eps*c);
 * data parallel (``DATA_PARALLEL = True``): when the worker group has N ranks the trial's minibatch
   is split across them (pg_gans.py:290-293) and gradients are averaged by bucketed RCCL
@@ -48,6 +52,7 @@ import numpy as np
 import torch
 
 from rafiki_amd.constants import TaskType  # noqa: F401
+from rafiki_amd.engine.convnet import default_dtype
 from rafiki_amd.engine.flat import FlatAdam, FlatParams, init_const, init_normal
 from rafiki_amd.model import BaseModel, CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, logger
 from rafiki_amd.ops import autograd as A
@@ -64,7 +69,7 @@ class PgNetworks:
     """G, D (trainable, flat arenas) and Gs (EMA of G) for one resolution/channel configuration."""
 
     def __init__(self, num_channels=1, resolution=32, label_size=0, fmap_base=8192, fmap_decay=1.0, fmap_max=512,
-                 latent_size=None, mbstd_group_size=4, device='cpu', seed=0):
+                 latent_size=None, mbstd_group_size=4, device='cpu', seed=0, dtype='fp32'):
         self.num_channels, self.resolution, self.label_size = int(num_channels), int(resolution), int(label_size)
         self.L = int(np.log2(resolution))
         assert resolution == 2 ** self.L and resolution >= 4, resolution
@@ -72,18 +77,22 @@ class PgNetworks:
         self.latent_size = int(latent_size or self.nf(0))
         self.mbstd_group_size = int(mbstd_group_size)
         self.device = torch.device(device)
+        self.dtype = dtype
+        bf = dtype == 'bf16'
+        # activation dtype of the GPU path (CPU: the fp32 PyTorch reference)
+        self.act_dtype = torch.bfloat16 if (bf and self.device.type == 'cuda') else torch.float32
         self.cpad = _pad8(self.num_channels)
         self.combo = self.latent_size + self.label_size
         self.combo_p = _pad8(self.combo)
         self.dout_p = _pad8(1 + self.label_size)
-        self.G = FlatParams(self.device, seed)
-        self.D = FlatParams(self.device, seed + 1)
+        self.G = FlatParams(self.device, seed, compute_bf16=bf)
+        self.D = FlatParams(self.device, seed + 1, compute_bf16=bf)
         self._define_G()
         self._define_D()
         self.G.build()
         self.D.build()
         self.Gs_master = self.G.master.clone()
-        self.Gs_bf16 = self.Gs_master.to(torch.bfloat16)
+        self.Gs_bf16 = self.Gs_master.to(torch.bfloat16) if bf else None
         self.g_params = self._leaves(self.G)
         self.d_params = self._leaves(self.D)
 
@@ -154,14 +163,14 @@ class PgNetworks:
 
     # -- parameter sources
     def src_G(self):
-        return _Src(self.g_params, lambda n: self.G.wb(n))
+        return _Src(self.g_params, lambda n: self.G.wb(n) if self.Gs_bf16 is not None else None)
 
     def src_Gs(self):
         return _Src({s.name: _view(self.Gs_master, s) for s in self.G.specs},
-                    lambda n: _view(self.Gs_bf16, self.G._by_name[n]))
+                    lambda n: _view(self.Gs_bf16, self.G._by_name[n]) if self.Gs_bf16 is not None else None)
 
     def src_D(self):
-        return _Src(self.d_params, lambda n: self.D.wb(n))
+        return _Src(self.d_params, lambda n: self.D.wb(n) if self.Gs_bf16 is not None else None)
 
     def set_requires_grad(self, params, flag):
         for p in params.values():
@@ -177,6 +186,11 @@ class PgNetworks:
         w = P.w(name + '/weight')
         return A.upscale_conv2d(x, w, P.w(name + '/bias'), wb=_maybe2d(P.wb(name + '/weight'), w))
 
+    def _conv_down(self, P, name, x, lrelu=None):
+        w = P.w(name + '/weight')
+        return A.conv2d_downscale2d(x, w.reshape(w.shape[0], -1), P.w(name + '/bias'),
+                                    wb=_maybe2d(P.wb(name + '/weight'), w), lrelu=lrelu)
+
     def _dense(self, P, name, x, bias=True, lrelu=None):
         w = P.w(name + '/weight')
         return A.dense(x, w, P.w(name + '/bias') if bias else None, wb=P.wb(name + '/weight'), lrelu=lrelu)
@@ -184,7 +198,7 @@ class PgNetworks:
     def generator(self, P, latents, labels, lod):
         """latents [N, latent] fp32, labels [N, label_size] -> images NHWC [N, r, r, cpad] (bf16 on GPU)
         at r = 2 ** (L - floor(lod)), in [-1, 1] drange (pg_gans.py:803-880, 'recursive' structure)."""
-        dt = torch.bfloat16 if self.device.type == 'cuda' else torch.float32
+        dt = self.act_dtype
         PN, LPN = A.pixel_norm, A.lrelu_pixel_norm
         N = latents.shape[0]
         combo = torch.cat([latents, labels], 1) if self.label_size else latents
@@ -212,14 +226,13 @@ class PgNetworks:
         """img NHWC [N, r, r, cpad] at the current LOD resolution -> (scores [N] fp32, label logits).
         ``segs`` > 1: img stacks that many independent minibatches (one batched evaluation;
         minibatch-stddev groups stay inside each)."""
-        lrelu = A.leaky_relu
         cur = self.L - int(math.floor(lod))
         frac = lod - math.floor(lod)
         x = self._conv(P, 'FromRGB_lod%d' % (self.L - cur), img, taps=1, lrelu=0.2)
         for res in range(cur, 2, -1):
             tag = '%dx%d' % (2 ** res, 2 ** res)
             x = self._conv(P, tag + '/Conv0', x, lrelu=0.2)
-            x = lrelu(A.downscale2d(self._conv(P, tag + '/Conv1_down', x)))
+            x = self._conv_down(P, tag + '/Conv1_down', x, lrelu=0.2)
             if res == cur and frac > 0:
                 y = self._conv(P, 'FromRGB_lod%d' % (self.L - res + 1), A.downscale2d(img), taps=1, lrelu=0.2)
                 x = x + (y - x) * frac
@@ -238,7 +251,8 @@ class PgNetworks:
             F.lerp_(self.Gs_master, self.G.master, beta, dst_bf16=self.Gs_bf16)
         else:
             self.Gs_master.copy_(self.G.master + (self.Gs_master - self.G.master) * beta)
-            self.Gs_bf16.copy_(self.Gs_master)
+            if self.Gs_bf16 is not None:
+                self.Gs_bf16.copy_(self.Gs_master)
 
     def state(self):
         return {'G': self.G.state_dict(),
@@ -251,7 +265,8 @@ class PgNetworks:
         for s in self.G.specs:
             if s.name in st['Gs']:
                 _view(self.Gs_master, s).copy_(torch.as_tensor(st['Gs'][s.name]).reshape(s.shape))
-        self.Gs_bf16.copy_(self.Gs_master)
+        if self.Gs_bf16 is not None:
+            self.Gs_bf16.copy_(self.Gs_master)
 
 
 def _zero_tail_init(std, real_c):
@@ -490,7 +505,8 @@ class PgGan(BaseModel):
     def _build(self, shape, label_size):
         self._meta = dict(num_channels=int(shape[0]), resolution=int(shape[1]), label_size=int(label_size),
                           fmap_base=int(self._k('fmap_base', 8192)), fmap_max=int(self._k('fmap_max', 512)),
-                          mbstd_group_size=int(self._k('mbstd_group_size', 4)))
+                          mbstd_group_size=int(self._k('mbstd_group_size', 4)),
+                          dtype=str(self._k('dtype', default_dtype())))
         self.nets = PgNetworks(device=self.device, seed=self.seed, **self._meta)
         if self.world > 1:
             import torch.distributed as dist
@@ -499,7 +515,8 @@ class PgGan(BaseModel):
             self.nets.G.sync_bf16()
             self.nets.D.sync_bf16()
             self.nets.Gs_master.copy_(self.nets.G.master)
-            self.nets.Gs_bf16.copy_(self.nets.Gs_master)
+            if self.nets.Gs_bf16 is not None:
+                self.nets.Gs_bf16.copy_(self.nets.Gs_master)
 
     def _reals(self, level_u8, idx, frac):
         """uint8 [N, C, r, r] (device) rows idx -> NHWC [n, r, r, cpad] in [-1, 1] with LOD fade
@@ -507,8 +524,10 @@ class PgGan(BaseModel):
         x = level_u8.index_select(0, idx)
         nets = self.nets
         if self.device.type == 'cuda' and frac <= 0:
+            from rafiki_amd.ops import f32 as S
             from rafiki_amd.ops import functional as F
-            return F.pack_nhwc(x.contiguous(), nets.cpad, 2.0 / 255.0, -1.0)
+            pack = S.pack_nhwc if nets.act_dtype == torch.float32 else F.pack_nhwc
+            return pack(x.contiguous(), nets.cpad, 2.0 / 255.0, -1.0)
         x = x.float() * (2.0 / 255.0) - 1.0
         if frac > 0:
             N, C, r, _ = x.shape
@@ -517,8 +536,7 @@ class PgGan(BaseModel):
         x = x.permute(0, 2, 3, 1)
         if nets.cpad > x.shape[-1]:
             x = torch.cat([x, x.new_zeros(*x.shape[:3], nets.cpad - x.shape[-1])], -1)
-        dt = torch.bfloat16 if self.device.type == 'cuda' else torch.float32
-        return x.to(dt).contiguous()
+        return x.to(nets.act_dtype).contiguous()
 
     def _slice_images(self, img):
         return img[..., :self.nets.num_channels]
@@ -554,7 +572,8 @@ class PgGan(BaseModel):
         nets.Gs_master.copy_(torch.as_tensor(st['Gs']))
         nets.G.sync_bf16()
         nets.D.sync_bf16()
-        nets.Gs_bf16.copy_(nets.Gs_master)
+        if nets.Gs_bf16 is not None:
+            nets.Gs_bf16.copy_(nets.Gs_master)
         for k, o in (('G', G_opt), ('D', D_opt)):
             for t, v in zip((o.m, o.v, o.t), st['opt'][k]):
                 t.copy_(torch.as_tensor(v))

@@ -79,6 +79,7 @@ _SIGS = {
                                                                  f32, i64, i64, vp],
     "rk_resample2x": [i32, i32, vp, vp, i32, i32, i32, i32, f32, vp],
     "rk_s2t_weights": [vp, vp, i32, i32, vp],
+    "rk_wflip_t": [vp, vp, i32, i32, i32, vp],
     "rk_mbstd_f32": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_lrelu_pixelnorm_f32": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
 }

@@ -8,10 +8,16 @@ the discriminator's weights, so every backward here is itself expressed through 
     d(dgrad)/d(dy) = conv(., w)     d(dgrad)/d(w) = wgrad(., dy)
     d(wgrad)/d(x)  = dgrad(dy, .)   d(wgrad)/d(dy) = conv(x, .)
 
-and the same for dense (x @ w.T, dy @ w, dy.T @ x).  Conventions (see ops.functional):
-activations are NHWC / [M, K] bf16, weights are fp32 masters ``w`` with a bf16 shadow ``wb`` that
-the fused optimizer keeps in sync (pass ``wb=None`` to cast on the fly), weight gradients come out
-of the kernels in fp32 directly (no bf16 round trip on dW).
+and the same for dense (x @ w.T, dy @ w, dy.T @ x).  Conventions: activations are NHWC / [M, K] in
+the tensor's own precision — fp32 (the reference's, ``ops.f32``: v_mfma_f32_32x32x2_f32) or bf16
+(opt-in, ``ops.functional``: bf16 MFMA with fp32 masters ``w`` and a bf16 shadow ``wb`` the fused
+optimizer keeps in sync; ``wb=None`` casts on the fly); weight gradients are fp32 either way.
+
+The PG-GAN resampling convolutions (pg_gans.py:1032-1067) in fp32 are the stride-2 gather family
+(``S2Fn`` / ``S2TFn`` / ``S2WFn``, itself closed under differentiation): conv3x3 + 2x2 box downscale
+is one 4x4 stride-2 gather conv with box-summed weights, upscale2d + conv3x3 is its adjoint with
+box-summed flipped weights — 1/2.25 of the full-resolution MACs and no 2x tensor.  The weight
+transforms are tiny differentiable torch ops, so the gradient reaches the 3x3 parameters.
 
 On CPU tensors every op falls back to plain fp32 PyTorch (F.conv2d / matmul), which torch already
 differentiates twice — that path is the numerics oracle for the GPU tests.  On a GPU tensor the
@@ -24,9 +30,11 @@ from typing import Optional
 import torch
 import torch.nn.functional as TF
 
+from . import f32 as S
 from . import functional as F
 
 BF16 = torch.bfloat16
+F32 = torch.float32
 
 
 def _bf(t: Optional[torch.Tensor]):
@@ -53,12 +61,23 @@ def _needed(ctx, i):
 
 def _bias_grad(gy):
     """sum of gy over all but the channel axis, fp32.  Outside a create_graph backward the result
-    is never differentiated, so it comes from the fused bf16 column-sum kernel instead of a
-    bf16->fp32 copy plus a reduction."""
+    is never differentiated, so it comes from the fused column-sum kernels instead of a reduction."""
     Cc = gy.shape[-1]
-    if not torch.is_grad_enabled() and gy.dtype == BF16 and gy.is_contiguous():
-        return F.colsum(gy.reshape(-1, Cc), torch.empty(Cc, device=gy.device, dtype=torch.float32))
+    if not torch.is_grad_enabled() and gy.is_cuda and gy.is_contiguous():
+        out = torch.empty(Cc, device=gy.device, dtype=torch.float32)
+        if gy.dtype == BF16:
+            return F.colsum(gy.reshape(-1, Cc), out)
+        if gy.dtype == F32:
+            return S.colsum(gy.reshape(-1, Cc), out)
     return gy.float().reshape(-1, Cc).sum(0)
+
+
+def _as(t, dt):
+    return t.to(dt).contiguous()
+
+
+def _act(slope):
+    return F.ACT_NONE if slope is None else F.ACT_LRELU
 
 
 def _k(taps):
@@ -76,18 +95,25 @@ def _conv_ref(x, w, b, taps):
 
 
 def upscale2d(x, factor=2):
-    """Nearest-neighbour upscale of NHWC (pg_gans.py:1042-1050)."""
+    """Nearest-neighbour upscale of NHWC (pg_gans.py:1042-1050); native kernel on GPU."""
     if factor == 1:
+        return x
+    if x.is_cuda and x.shape[-1] % 4 == 0 and factor & (factor - 1) == 0:
+        while factor > 1:
+            x = Up2Fn.apply(x, 1.0)
+            factor //= 2
         return x
     N, h, w, C = x.shape
     return x[:, :, None, :, None, :].expand(N, h, factor, w, factor, C).reshape(N, h * factor, w * factor, C)
 
 
 def downscale2d(x, factor=2):
-    """Box-filter downscale of NHWC (pg_gans.py:1062-1067), accumulated in fp32."""
+    """Box-filter downscale of NHWC (pg_gans.py:1062-1067), accumulated in fp32; native kernel on GPU."""
     if factor == 1:
         return x
     N, H, W, C = x.shape
+    if x.is_cuda and factor == 2 and C % 4 == 0 and H % 2 == 0 and W % 2 == 0:
+        return Down2Fn.apply(x, 0.25)
     y = x.reshape(N, H // factor, factor, W // factor, factor, C).float().mean((2, 4))
     return y.to(x.dtype)
 
@@ -112,9 +138,14 @@ class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, wb, taps, slope):
         x = x.contiguous()
-        wbs = _wshadow(w, wb)
-        y = F.conv_fwd(x, wbs, taps=taps, bias=None if b is None else b.detach().float().contiguous(),
-                       act=F.ACT_NONE if slope is None else F.ACT_LRELU, slope=0.2 if slope is None else slope)
+        bd = None if b is None else b.detach().float().contiguous()
+        if x.dtype == F32:
+            y = S.conv_fwd(x, w.detach().contiguous(), taps=taps, bias=bd, act=_act(slope),
+                           slope=0.2 if slope is None else slope)
+        else:
+            y = F.conv_fwd(x, _wshadow(w, wb), taps=taps, bias=bd, act=_act(slope),
+                           slope=0.2 if slope is None else slope)
+        ctx.dt = x.dtype
         if slope is None:
             ctx.save_for_backward(x, w)
         else:
@@ -127,7 +158,7 @@ class ConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors[:2]
         if ctx.slope is not None:
             gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
-        gy = gy.to(BF16).contiguous()
+        gy = _as(gy, ctx.dt)
         gx = gw = gb = None
         if _needed(ctx, 0):
             gx = ConvDgradFn.apply(gy, w, ctx.wb, ctx.taps)
@@ -144,15 +175,18 @@ class ConvDgradFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gy, w, wb, taps):
         gy = gy.contiguous()
-        dx = F.conv_dgrad(gy, _wshadow(w, wb), taps=taps)
+        if gy.dtype == F32:
+            dx = S.conv_dgrad(gy, S.conv_wt(w.detach(), taps), taps=taps)
+        else:
+            dx = F.conv_dgrad(gy, _wshadow(w, wb), taps=taps)
         ctx.save_for_backward(gy, w)
-        ctx.wb, ctx.taps = wb, taps
+        ctx.wb, ctx.taps, ctx.dt = wb, taps, gy.dtype
         return dx
 
     @staticmethod
     def backward(ctx, ggx):
         gy, w = ctx.saved_tensors
-        ggx = ggx.to(BF16).contiguous()
+        ggx = _as(ggx, ctx.dt)
         g_gy = g_w = None
         if _needed(ctx, 0):
             g_gy = ConvFn.apply(ggx, w, None, ctx.wb, ctx.taps, None)
@@ -167,7 +201,7 @@ class ConvWgradFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gy, taps):
         x, gy = x.contiguous(), gy.contiguous()
-        dw = F.conv_wgrad(gy, x, taps=taps)
+        dw = S.conv_wgrad(gy, x, taps=taps) if x.dtype == F32 else F.conv_wgrad(gy, x, taps=taps)
         ctx.save_for_backward(x, gy)
         ctx.taps = taps
         return dw
@@ -219,15 +253,145 @@ class UpConvFn(torch.autograd.Function):
         return gx, gw, gb, None
 
 
-def upscale_conv2d(x, w, b=None, *, wb=None):
+def _box4(w3):
+    """[Co, 3, 3, Ci] -> [Co, 4, 4, Ci]: sum of the four 1-pixel shifts of the zero-padded kernel
+    (the reference's fused-resample weights, pg_gans.py:1035-1036 / 1055-1056)."""
+    wp = TF.pad(w3, (0, 0, 1, 1, 1, 1))
+    return wp[:, 1:, 1:] + wp[:, :-1, 1:] + wp[:, 1:, :-1] + wp[:, :-1, :-1]
+
+
+def down_weights(w, cin):
+    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cout, 16*Cin] of conv3x3 + 2x2 box downscale."""
+    co = w.shape[0]
+    return (_box4(w.reshape(co, 3, 3, cin)) * 0.25).reshape(co, 16 * cin)
+
+
+def up_weights(w, cin):
+    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cin, 16*Cout] whose adjoint S2T is upscale2d + conv3x3."""
+    co = w.shape[0]
+    return _box4(w.reshape(co, 3, 3, cin).flip(1, 2)).permute(3, 1, 2, 0).reshape(cin, 16 * co)
+
+
+def upscale_conv2d(x, w, b=None, *, wb=None, lrelu=None):
+    """conv3x3(upscale2d(x), w) + b (pg_gans.py:1032-1039)."""
     if x.device.type != 'cuda':
-        return _conv_ref(upscale2d(x), w, b, 9)
-    return UpConvFn.apply(x, w, b, wb)
+        y = _conv_ref(upscale2d(x), w, b, 9)
+        return y if lrelu is None else leaky_relu(y, lrelu)
+    if x.dtype == F32:
+        return S2TFn.apply(x.contiguous(), up_weights(w, x.shape[-1]), b, None if lrelu is None else float(lrelu))
+    y = UpConvFn.apply(x, w, b, wb)
+    return y if lrelu is None else leaky_relu(y, lrelu)
 
 
-def conv2d_downscale2d(x, w, b=None, *, wb=None):
-    """conv3x3 then 2x2 box downscale == the reference's fused 4x4 stride-2 conv (pg_gans.py:1053-1059)."""
-    return downscale2d(conv2d(x, w, b, taps=9, wb=wb))
+def conv2d_downscale2d(x, w, b=None, *, wb=None, lrelu=None):
+    """conv3x3 then 2x2 box downscale (+b) == the reference's fused 4x4 stride-2 conv (pg_gans.py:1053-1059)."""
+    if x.device.type == 'cuda' and x.dtype == F32:
+        return S2Fn.apply(x.contiguous(), down_weights(w, x.shape[-1]), b, None if lrelu is None else float(lrelu))
+    y = downscale2d(conv2d(x, w, b, taps=9, wb=wb))
+    return y if lrelu is None else leaky_relu(y, lrelu)
+
+
+# ------------------------------------------------------------------ stride-2 gather family (fp32)
+class S2Fn(torch.autograd.Function):
+    """y = act(S2(x, W) + b): 4x4 taps at -1..2, stride 2 (ops.f32.s2_conv)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, slope):
+        y = S.s2_conv(x, W.detach().contiguous(), bias=None if b is None else b.detach().float().contiguous(),
+                      act=_act(slope), slope=0.2 if slope is None else slope)
+        ctx.save_for_backward(*((x, W) if slope is None else (x, W, y)))
+        ctx.has_b, ctx.slope = b is not None, slope
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W = ctx.saved_tensors[:2]
+        if ctx.slope is not None:
+            gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
+        gy = _as(gy, F32)
+        gx = gW = gb = None
+        if _needed(ctx, 0):
+            gx = S2TFn.apply(gy, W, None, None)
+        if _needed(ctx, 1):
+            gW = S2WFn.apply(x, gy)
+        if ctx.has_b and _needed(ctx, 2):
+            gb = _bias_grad(gy)
+        return gx, gW, gb, None
+
+
+class S2TFn(torch.autograd.Function):
+    """y = act(S2T(z, W) + b): the adjoint of S2 (the 2x transposed conv, ops.f32.s2t_conv)."""
+
+    @staticmethod
+    def forward(ctx, z, W, b, slope):
+        y = S.s2t_conv(z, W.detach().contiguous(), bias=None if b is None else b.detach().float().contiguous(),
+                       act=_act(slope), slope=0.2 if slope is None else slope)
+        ctx.save_for_backward(*((z, W) if slope is None else (z, W, y)))
+        ctx.has_b, ctx.slope = b is not None, slope
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        z, W = ctx.saved_tensors[:2]
+        if ctx.slope is not None:
+            gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
+        gy = _as(gy, F32)
+        gz = gW = gb = None
+        if _needed(ctx, 0):
+            gz = S2Fn.apply(gy, W, None, None)
+        if _needed(ctx, 1):
+            gW = S2WFn.apply(gy, z)
+        if ctx.has_b and _needed(ctx, 2):
+            gb = _bias_grad(gy)
+        return gz, gW, gb, None
+
+
+class S2WFn(torch.autograd.Function):
+    """dW = S2W(x, g) (ops.f32.s2_wgrad); its own gradients are S2T(g, .) and S2(x, .)."""
+
+    @staticmethod
+    def forward(ctx, x, g):
+        x, g = x.contiguous(), g.contiguous()
+        ctx.save_for_backward(x, g)
+        return S.s2_wgrad(x, g)
+
+    @staticmethod
+    def backward(ctx, ggW):
+        x, g = ctx.saved_tensors
+        ggW = _as(ggW, F32)
+        gx = gg = None
+        if _needed(ctx, 0):
+            gx = S2TFn.apply(g, ggW, None, None)
+        if _needed(ctx, 1):
+            gg = S2Fn.apply(x, ggW, None, None)
+        return gx, gg
+
+
+# --------------------------------------------------------------------------- 2x resampling
+class Up2Fn(torch.autograd.Function):
+    """y = s * upscale2d(x) on the native kernel; its adjoint is s * 2x2 sum-pool (Down2Fn)."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.s = s
+        return S.upscale2x(x.contiguous(), scale=s)
+
+    @staticmethod
+    def backward(ctx, g):
+        return Down2Fn.apply(g.contiguous(), ctx.s), None
+
+
+class Down2Fn(torch.autograd.Function):
+    """y = s * (2x2 sum of x) on the native kernel (s = 0.25: downscale2d); adjoint s * upscale2d."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.s = s
+        return S.downscale2x(x.contiguous(), scale=s)
+
+    @staticmethod
+    def backward(ctx, g):
+        return Up2Fn.apply(g.contiguous(), ctx.s), None
 
 
 # ------------------------------------------------------------------------------------ dense
@@ -237,8 +401,12 @@ class DenseFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, wb, slope):
         x = x.contiguous()
-        y = F.linear(x, _wshadow(w, wb), None if b is None else b.detach().float().contiguous(),
-                     act=F.ACT_NONE if slope is None else F.ACT_LRELU, slope=0.2 if slope is None else slope)
+        bd = None if b is None else b.detach().float().contiguous()
+        if x.dtype == F32:
+            y = S.linear(x, w.detach().contiguous(), bd, act=_act(slope), slope=0.2 if slope is None else slope)
+        else:
+            y = F.linear(x, _wshadow(w, wb), bd, act=_act(slope), slope=0.2 if slope is None else slope)
+        ctx.dt = x.dtype
         if slope is None:
             ctx.save_for_backward(x, w)
         else:
@@ -251,7 +419,7 @@ class DenseFn(torch.autograd.Function):
         x, w = ctx.saved_tensors[:2]
         if ctx.slope is not None:
             gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
-        gy = gy.to(BF16).contiguous()
+        gy = _as(gy, ctx.dt)
         gx = gw = gb = None
         if _needed(ctx, 0):
             gx = DenseDxFn.apply(gy, w, ctx.wb)
@@ -266,15 +434,18 @@ class DenseDxFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gy, w, wb):
         gy = gy.contiguous()
-        dx = F.linear_dx(gy, _wshadow(w, wb))
+        if gy.dtype == F32:
+            dx = S.linear_dx(gy, w.detach().contiguous())
+        else:
+            dx = F.linear_dx(gy, _wshadow(w, wb))
         ctx.save_for_backward(gy, w)
-        ctx.wb = wb
+        ctx.wb, ctx.dt = wb, gy.dtype
         return dx
 
     @staticmethod
     def backward(ctx, ggx):
         gy, w = ctx.saved_tensors
-        ggx = ggx.to(BF16).contiguous()
+        ggx = _as(ggx, ctx.dt)
         g_gy = g_w = None
         if _needed(ctx, 0):
             g_gy = DenseFn.apply(ggx, w, None, ctx.wb, None)
@@ -287,7 +458,7 @@ class DenseDwFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gy):
         x, gy = x.contiguous(), gy.contiguous()
-        dw = F.linear_dw(gy, x)
+        dw = S.linear_dw(gy, x) if x.dtype == F32 else F.linear_dw(gy, x)
         ctx.save_for_backward(x, gy)
         return dw
 
@@ -343,8 +514,7 @@ class LReluPixelNormFn(torch.autograd.Function):
         gx = F.lrelu_pixelnorm(x, ctx.bd, slope=ctx.slope, eps=ctx.eps, dz=gz)
         gb = None
         if ctx.has_b and ctx.needs_input_grad[1]:
-            Cc = x.shape[-1]
-            gb = F.colsum(gx.reshape(-1, Cc), torch.empty(Cc, device=x.device, dtype=torch.float32))
+            gb = _bias_grad(gx)
         return (gx if ctx.needs_input_grad[0] else None), gb, None, None
 
 
@@ -374,7 +544,7 @@ class MbstdFn(torch.autograd.Function):
 class MbstdBwdFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gout, x, group, segs):
-        gout = gout.to(BF16).contiguous()
+        gout = _as(gout, x.dtype)
         ctx.save_for_backward(gout, x)
         ctx.group, ctx.segs = group, segs
         return F.mbstd(1, x, gout, group=group, segs=segs)
@@ -393,7 +563,7 @@ def minibatch_stddev(x, group_size=4, pad_to=8, segs=1):
     ``segs`` > 1: x is that many independent minibatches stacked (grouping stays inside each)."""
     N, H, W, C = x.shape
     g = min(group_size, N // segs)
-    if x.device.type == 'cuda' and x.dtype == BF16 and g <= 8 and (N // segs) % g == 0:
+    if x.device.type == 'cuda' and x.dtype in (BF16, F32) and g <= 8 and (N // segs) % g == 0:
         return MbstdFn.apply(x, g, segs, C + 1 + (-(C + 1)) % pad_to)
     if segs > 1:
         return torch.cat([minibatch_stddev(t, group_size, pad_to) for t in x.chunk(segs)], 0)

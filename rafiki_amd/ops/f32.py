@@ -595,3 +595,14 @@ def downscale2x(x, scale=0.25, out=None):
     _lib.call("rk_resample2x", 1, int(x.dtype == torch.bfloat16), _p(x.contiguous()), _p(out), Nb, H, W, Cc,
               float(scale), _s())
     return out
+
+
+def conv_wt(w, taps=9):
+    """w [Cout, taps*Cin] -> [Cin, taps*Cout] flipped transposed weights: conv_dgrad(dy, conv_wt(w)) is the
+    data gradient of conv_fwd(x, w) (one LDS-tiled transpose launch; the autograd path's per-call
+    equivalent of SConvWT)."""
+    Cout = w.shape[0]
+    Cin = w.numel() // (taps * Cout)
+    out = torch.empty((Cin, taps * Cout), device=w.device, dtype=torch.float32)
+    _lib.call("rk_wflip_t", _p(w.contiguous()), _p(out), int(Cout), int(Cin), int(taps), _s())
+    return out

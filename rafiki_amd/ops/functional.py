@@ -766,26 +766,27 @@ def colsum(x2d, out, *, accumulate=False):
 
 
 def mbstd(mode, x, a=None, b=None, *, group, segs=1, cp=None):
-    """Minibatch-stddev kernels over NHWC bf16 x [N, H, W, C] (see pggan.hip):
+    """Minibatch-stddev kernels over NHWC bf16 or fp32 x [N, H, W, C] (see pggan.hip):
     mode 0 -> [N, H, W, cp] = [x, f, 0];  mode 1 -> gx from gout=a;  mode 2 -> (g_x, gg_out) from
     ggx=a and gout=b."""
     N, H, W, Cc = x.shape
     cp = cp or (a.shape[-1] if mode == 1 else b.shape[-1] if mode == 2 else Cc + 1)
-    if x.dtype != torch.bfloat16 or N % segs or (N // segs) % group:
-        raise ValueError('mbstd: bf16 input with N divisible by segs * group required')
+    dt = x.dtype
+    if dt not in (torch.bfloat16, torch.float32) or N % segs or (N // segs) % group:
+        raise ValueError('mbstd: bf16 / fp32 input with N divisible by segs * group required')
     x = x.contiguous()
-    a = None if a is None else a.to(torch.bfloat16).contiguous()
-    b = None if b is None else b.to(torch.bfloat16).contiguous()
+    a = None if a is None else a.to(dt).contiguous()
+    b = None if b is None else b.to(dt).contiguous()
     out2 = None
     if mode == 0:
-        out = torch.empty((N, H, W, cp), device=x.device, dtype=torch.bfloat16)
+        out = torch.empty((N, H, W, cp), device=x.device, dtype=dt)
     else:
         out = torch.empty_like(x)
         if mode == 2:
-            out2 = torch.empty((N, H, W, cp), device=x.device, dtype=torch.bfloat16)
+            out2 = torch.empty((N, H, W, cp), device=x.device, dtype=dt)
     part = torch.empty((N // group) * 32, device=x.device, dtype=torch.float32)
-    _lib.call("rk_mbstd", int(mode), _p(x), _p(a), _p(b), N, H * W, Cc, cp, int(group), int(segs), _p(out),
-              _p(out2), _p(part), _s())
+    _lib.call("rk_mbstd" if dt == torch.bfloat16 else "rk_mbstd_f32", int(mode), _p(x), _p(a), _p(b), N, H * W, Cc,
+              cp, int(group), int(segs), _p(out), _p(out2), _p(part), _s())
     return (out, out2) if mode == 2 else out
 
 
@@ -845,20 +846,22 @@ def philox_(out, dist, *, seed, stream_id, step=None, hi=0, a=0.0, b=1.0):
 
 
 def lrelu_pixelnorm(x, bias=None, *, slope=0.2, eps=1e-8, dz=None, out=None):
-    """z = PN(lrelu(x + bias)) over the last (channel) dim of bf16 NHWC rows; with ``dz`` the
+    """z = PN(lrelu(x + bias)) over the last (channel) dim of bf16 or fp32 NHWC rows; with ``dz`` the
     backward dL/dx instead (recomputes the activation from x)."""
     Cc = x.shape[-1]
     P = x.numel() // Cc
-    if x.dtype != torch.bfloat16 or Cc % 8 or Cc > 1024:
-        raise ValueError('lrelu_pixelnorm: bf16 rows with C % 8 == 0 and C <= 1024 required')
+    dt = x.dtype
+    if dt not in (torch.bfloat16, torch.float32) or Cc % 8 or Cc > 1024:
+        raise ValueError('lrelu_pixelnorm: bf16 / fp32 rows with C % 8 == 0 and C <= 1024 required')
     x = x.contiguous()
     if dz is not None:
-        dz = dz.to(torch.bfloat16).contiguous()
+        dz = dz.to(dt).contiguous()
     if bias is not None:
         bias = bias.float().contiguous()
     if out is None:
         out = torch.empty_like(x)
-    _lib.call("rk_lrelu_pixelnorm", _p(x), _p(bias), _p(dz), P, Cc, float(slope), float(eps), _p(out), _s())
+    _lib.call("rk_lrelu_pixelnorm" if dt == torch.bfloat16 else "rk_lrelu_pixelnorm_f32", _p(x), _p(bias), _p(dz), P,
+              Cc, float(slope), float(eps), _p(out), _s())
     return out
 
 
