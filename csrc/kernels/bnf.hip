@@ -315,14 +315,17 @@ __global__ __launch_bounds__(256) void swt_kernel(const float* __restrict__ aren
 }
 
 // out[c] (+)= sum_r x[r][c] for an fp32 [R][C] matrix (bias gradients); 64 columns per block.
+// gridDim.y > 1: block row-chunk y writes its partial sums to out + y * C (combined by the caller).
 __global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict__ x, int R, int C, int ld,
                                                          float* __restrict__ out, int accumulate) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int q = threadIdx.x >> 6;
+  const int per = (R + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(R, r0 + per);
+  out += (long long)blockIdx.y * C;
   float s = 0.f;
   if (c < C)
-    for (int r = q; r < R; r += 4) s += x[(long long)r * ld + c];
+    for (int r = r0 + q; r < r1; r += 4) s += x[(long long)r * ld + c];
   red[q][threadIdx.x & 63] = s;
   __syncthreads();
   if (q == 0 && c < C) {
@@ -469,9 +472,12 @@ extern "C" int rk_swt(const float* arena, float* dst, const int* desc, int nbloc
   return RK_OK;
 }
 
-extern "C" int rk_colsum_f32(const float* x, int R, int C, int ld, float* out, int accumulate, void* stream) {
-  hipLaunchKernelGGL(colsum_f32_kernel, dim3(rk_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, x, R, C, ld, out,
-                     accumulate);
+// chunks > 1: out is [chunks][C] partial sums (accumulate must be 0)
+extern "C" int rk_colsum_f32(const float* x, int R, int C, int ld, float* out, int accumulate, int chunks,
+                             void* stream) {
+  if (chunks < 1 || (chunks > 1 && accumulate)) return RK_EBADARG;
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3(rk_cdiv(C, 64), chunks), dim3(256), 0, (hipStream_t)stream, x, R, C, ld,
+                     out, accumulate);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -70,7 +70,7 @@ _SIGS = {
     "rk_bnf_bwd_apply": [vp, vp, vp, vp, i32, f64, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "rk_bnf_colstats": [vp, vp, i32, i32, vp, vp],
     "rk_swt": [vp, vp, vp, i32, vp, vp],
-    "rk_colsum_f32": [vp, i32, i32, i32, vp, i32, vp],
+    "rk_colsum_f32": [vp, i32, i32, i32, vp, i32, i32, vp],
     "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, vp],
     "rk_pack_nhwc_f32": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
     "rk_softmax_xent_f32": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],

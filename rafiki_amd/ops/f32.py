@@ -344,9 +344,16 @@ def reduce_slabs(slab, out, *, accumulate=False, scale=1.0):
 
 
 def colsum(x2d, out, *, accumulate=False):
+    """out[c] (+)= sum_r x2d[r, c] (fp32).  Tall inputs split the rows over ~2 blocks per CU, then fold
+    the partial rows with reduce_slabs."""
     R, Cc = x2d.shape
-    _lib.call("rk_colsum_f32", _p(x2d), R, Cc, x2d.stride(0), _p(out), int(accumulate), _s())
-    return out
+    chunks = max(1, min(cdiv(R, 256), cdiv(2 * NUM_CU, cdiv(Cc, 64))))
+    if chunks == 1:
+        _lib.call("rk_colsum_f32", _p(x2d), R, Cc, x2d.stride(0), _p(out), int(accumulate), 1, _s())
+        return out
+    part = torch.empty((chunks, Cc), device=x2d.device, dtype=torch.float32)
+    _lib.call("rk_colsum_f32", _p(x2d), R, Cc, x2d.stride(0), _p(part), 0, chunks, _s())
+    return reduce_slabs(part, out, accumulate=accumulate)
 
 
 # -------------------------------------------------------------------------------------- batchnorm

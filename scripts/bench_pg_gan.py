@@ -24,13 +24,14 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--minibatch', type=int, default=0, help='0: reference schedule minibatch for the LOD')
     ap.add_argument('--no-graph', action='store_true', help='eager rounds (no hipGraph replay)')
+    ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'))
     a = ap.parse_args()
     from rafiki_amd.engine.flat import FlatAdam
     from rafiki_amd.models.pg_gan import PgGan, TrainingSchedule
     from rafiki_amd.ops import _lib
     _lib.lib()
     dev = torch.device('cuda', 0)
-    m = PgGan(D_repeats=1, minibatch_base=16, G_lrate=1e-3, D_lrate=1e-3)
+    m = PgGan(D_repeats=1, minibatch_base=16, G_lrate=1e-3, D_lrate=1e-3, dtype=a.dtype)
     m.device = dev
     m._build([1, 32, 32], 0)
     nets = m.nets
@@ -42,7 +43,7 @@ def main():
     rng = TrialRng(dev, 0)
     acc = torch.zeros(6, device=dev)
     res = {'metric': 'PG-GAN train throughput (images/s through D+G steps), 1 GPU', 'params_G': nets.G.num_params(),
-           'params_D': nets.D.num_params(), 'dtype': 'bf16', 'data': 'synthetic uint8 32x32x1, random-init weights',
+           'params_D': nets.D.num_params(), 'dtype': nets.dtype, 'data': 'synthetic uint8 32x32x1, random-init weights',
            'lods': {}}
     for lod in [float(x) for x in a.lods.split(',')]:
         r = 2 ** (5 - int(lod))
