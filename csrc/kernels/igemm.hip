@@ -572,7 +572,8 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float yv = (float)g[e];
-          v[e] = yv * b[e] + sh[e] > 0.f ? v[e] : 0.f;
+          // the sums see the bf16 value that is stored and that the BN-backward apply reads
+          v[e] = yv * b[e] + sh[e] > 0.f ? (float)(bf16)v[e] : 0.f;
           s[j][e] += v[e];
           ss[j][e] += v[e] * yv;
         }
@@ -596,6 +597,7 @@ RK_DEV void tile_epi(const IgemmParams& p, f32x4 (&acc)[MI][NI], int mrow, int n
             const float a = fmaxf(z, 0.f);
             if (a > best) { best = a; zb = z; yb = yv; }
           }
+          v[e] = (float)(bf16)v[e];   // as stored (the pooled gradient the apply pass reads)
           const float dz = zb > 0.f ? v[e] : 0.f;
           s[j][e] += dz;
           ss[j][e] += dz * yb;

@@ -779,12 +779,18 @@ class PgGan(BaseModel):
     @torch.no_grad()
     def generate(self, n, seed=1000, batch=256, use_Gs=True):
         """n images uint8 NHWC [n, R, R, C] at full resolution (pg_gans.py:124-136 / Network.run:
-        out_mul=127.5, out_add=127.5, nearest upscale of lower-LOD output)."""
+        out_mul=127.5, out_add=127.5, nearest upscale of lower-LOD output).
+
+        In a data-parallel trial every rank draws the same latents and renders only its slice of each
+        batch; an all-gather assembles the batch on every rank (the reference splits Network.run over
+        num_gpus towers, pg_gans.py:691-711)."""
         nets = self.nets
         P = nets.src_Gs() if use_Gs else nets.src_G()
         lod = float(self.lod or 0.0)
         g = torch.Generator(device=self.device)
         g.manual_seed(int(seed))
+        world, rank = self.world, self.rank
+        shard = world > 1 and torch.distributed.is_available() and torch.distributed.is_initialized()
         outs = []
         for b in range(0, n, batch):
             m = min(batch, n - b)
@@ -792,12 +798,30 @@ class PgGan(BaseModel):
             lab = torch.zeros((m, nets.label_size), device=self.device)
             if nets.label_size:
                 lab[torch.arange(m), torch.randint(0, nets.label_size, (m,), generator=g, device=self.device)] = 1.0
-            img = self._slice_images(nets.generator(P, lat, lab, lod)).float()
+            lo, hi = 0, m
+            if shard:
+                per = -(-m // world)
+                lo, hi = min(m, rank * per), min(m, (rank + 1) * per)
+            with torch.no_grad():
+                img = self._slice_images(nets.generator(P, lat[lo:hi], lab[lo:hi], lod)).float()
             factor = nets.resolution // img.shape[1]
             if factor > 1:
                 img = A.upscale2d(img, factor)
-            outs.append((img * 127.5 + 127.5).round().clamp(0, 255).to(torch.uint8).cpu())
+            u8 = (img * 127.5 + 127.5).round().clamp(0, 255).to(torch.uint8)
+            if shard:
+                u8 = self._gather_rows(u8, per, m)
+            outs.append(u8.cpu())
         return torch.cat(outs).numpy()
+
+    def _gather_rows(self, part, per, m):
+        """Concatenate every rank's rows (``per`` each, the last ranks may hold fewer) -> [m, ...]."""
+        import torch.distributed as dist
+        comm = torch.device('cuda', self.ctx.dist.local_rank) if self.ctx.dist.backend == 'nccl' else torch.device('cpu')
+        buf = torch.zeros((per,) + tuple(part.shape[1:]), dtype=part.dtype, device=comm)
+        buf[:part.shape[0]] = part.to(comm)
+        bufs = [torch.empty_like(buf) for _ in range(self.world)]
+        dist.all_gather(bufs, buf)
+        return torch.cat(bufs)[:m]
 
     # ------------------------------------------------------------------ evaluate
     def evaluate(self, dataset_uri):
