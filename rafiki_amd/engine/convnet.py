@@ -486,8 +486,11 @@ class ConvNetEngine:
         the kernel path (max-pool argmax routing then agrees with the kernels' bf16 values)."""
         fl = self.flat
         P = params if params is not None else {n: fl.w(n) for n in fl.names()}
-        rnd = _bf16_storage if emulate_bf16 else (lambda t: t)
-        rndw = (lambda t: t + (t.bfloat16().float() - t).detach()) if emulate_bf16 else (lambda t: t)
+        ste = (lambda t: t + (t.bfloat16().float() - t).detach())
+        # emulate_bf16='fwd': round the stored forward values only (gradients stay fp32) — the second
+        # placement of the same bf16 storage, used to measure the oracle's own rounding noise floor
+        rnd = ste if emulate_bf16 == 'fwd' else _bf16_storage if emulate_bf16 else (lambda t: t)
+        rndw = ste if emulate_bf16 else (lambda t: t)
         # fp64 inputs keep fp64 (the fp32 kernels' numerics oracle); everything else runs in fp32
         up = (lambda t: t) if x_nhwc.dtype == torch.float64 else (lambda t: t.float())
         h = up(x_nhwc).permute(0, 3, 1, 2) if x_nhwc.dim() == 4 else up(x_nhwc)
@@ -526,7 +529,7 @@ class ConvNetEngine:
         for (name, di, do, _) in self.fcs:
             h = rnd(torch.relu(h @ rndw(P[name + '.w']).t() + P[name + '.b']))
         logits = (h @ rndw(P['out.w']).t() + P['out.b'])[:, :self.num_classes]
-        logits = _bf16_grad(logits) if emulate_bf16 else logits
+        logits = _bf16_grad(logits) if emulate_bf16 and emulate_bf16 != 'fwd' else logits
         loss = TF.cross_entropy(logits, labels.long()) if labels is not None else None
         return loss, logits
 

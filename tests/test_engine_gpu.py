@@ -38,6 +38,7 @@ def test_grads_match_reference():
         fro = ((got - g).norm() / g.norm().clamp_min(1e-12)).item()
         cos = torch.nn.functional.cosine_similarity(got.flatten(), g.flatten(), 0).item()
         # residual = independent bf16 rounding of dy feeding the (cancelling) sum_p dy*x reduction
+        print('bf16-grad-vs-emulated', n, round(fro, 4), round(cos, 5))
         assert fro < 0.12 and cos > 0.99, (n, fro, cos)
     # loose oracle: plain fp32 reference (bf16 storage shifts pool routing: direction must agree)
     loss32, _ = eng.reference_loss(x, y, params, training=True)
@@ -45,6 +46,45 @@ def test_grads_match_reference():
     for n, g in zip(fl.names(), g32):
         cos = torch.nn.functional.cosine_similarity(fl.g(n).flatten(), g.flatten(), 0).item()
         assert cos > 0.97, (n, cos)
+
+
+def test_bf16_bn_backward_is_exact_given_its_inputs(monkeypatch):
+    """Localises the ~5% residual of the bf16 engine vs the bf16-emulating oracle (test above).
+    Every BN(+ReLU, +2x2 max-pool) backward of the engine — including the sums fused into the dgrad
+    epilogues — reproduces an fp64 autograd BatchNorm backward of ITS OWN inputs (bf16 y and incoming
+    gradient) to < 1% (measured 0.2%).  The oracle's inputs differ from the engine's by ~1% (another
+    bf16 rounding realisation of the same network: measured 1.3% on the last block's incoming
+    gradient), and the BN backward's cancelling projection dz = k1*(g - mean g - xhat*mean(g*xhat))
+    amplifies that ~4x (measured 5.4% on its output, scripts/diag_bf16_layers.py) — so the end-to-end
+    gate above stays loose by construction while the kernels are pinned tightly here."""
+    import torch.nn.functional as TF
+    from rafiki_amd.ops import functional as F
+    eng = _engine()
+    x, y = _batch(64)
+    cap = []
+    orig = F.bn_bwd_acc
+
+    def bb(d, yy, coeffs, gamma, acc, **kw):
+        out = orig(d, yy, coeffs, gamma, acc, **kw)
+        cap.append((d.clone(), yy.clone(), out.clone(), kw.get('pool', False)))
+        return out
+    monkeypatch.setattr(F, 'bn_bwd_acc', bb)
+    eng.forward_backward(x, y)
+    torch.cuda.synchronize()
+    assert len(cap) == len(eng.blocks)
+    for k, bi in enumerate(range(len(eng.blocks) - 1, -1, -1)):
+        d, yb, dz, pool = cap[k]
+        name = eng.blocks[bi][0]
+        y64 = yb.double().cpu().permute(0, 3, 1, 2).requires_grad_(True)
+        h = torch.relu(TF.batch_norm(y64, None, None, eng.flat.w(name + '.gamma').double().cpu(),
+                                     eng.flat.w(name + '.beta').double().cpu(), training=True, eps=eng.bn_eps))
+        if pool:
+            h = TF.max_pool2d(h, 2)
+        (ref,) = torch.autograd.grad(h, y64, d.double().cpu().permute(0, 3, 1, 2))
+        got = dz.double().cpu().permute(0, 3, 1, 2)
+        err = ((got - ref).norm() / ref.norm()).item()
+        print('bn backward vs fp64 of its inputs', name, round(err, 5))
+        assert err < 1e-2, (name, err)
 
 
 def test_graph_replay_matches_eager():
@@ -115,6 +155,7 @@ def test_grads_match_reference_non_pow2_vgg16_layout():
         cos = torch.nn.functional.cosine_similarity(got.flatten(), g.flatten(), 0).item()
         # 5 BN stages down to 1x1 at batch 32 amplify the bf16 dy rounding; the same net at 32x32 (the
         # power-of-two path) measures fro 0.18 / cos 0.983 on conv0 (scripts/diag_grads48.py)
+        print('bf16-grad48-vs-emulated', n, round(fro, 4), round(cos, 5))
         assert fro < 0.2 and cos > 0.98, (n, fro, cos)
 
 
