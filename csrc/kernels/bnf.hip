@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void sreduce_epi_kernel(const float* __restrict__ slab, int S, int M, int N,
                                                           const float* __restrict__ bias, int act, float slope,
                                                           float alpha, const float* __restrict__ gate, int ldg,
-                                                          float* __restrict__ out, int ldc) {
+                                                          float* __restrict__ out, int ldc, int brows) {
   const long long n4 = (long long)M * N / 4;
   const long long sn = (long long)M * N;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) void sreduce_epi_kernel(const float* __restric
     const long long e0 = i * 4;
     const int m = (int)(e0 / N), n = (int)(e0 - (long long)m * N);
     a *= alpha;
-    if (bias) a += *(const f32x4*)(bias + n);
+    if (bias) a += *(const f32x4*)(bias + (brows ? (long long)(m / brows) * N : 0) + n);
 #pragma unroll
     for (int e = 0; e < 4; ++e) a[e] = act_f(a[e], act, slope);
     if (gate) {
@@ -393,6 +393,43 @@ __global__ __launch_bounds__(256) void pack_nhwc_f32_kernel(const void* __restri
 int grid_cap(long long work, int cap) {
   long long g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : g > cap ? cap : g);
+}
+
+// eval BN(+act, +2x2 max-pool) of G stacked batches: y [G*Nb, H, W, C], scale / shift [G][C]
+template <bool POOL>
+__global__ __launch_bounds__(256) void bnf_eval_grp_kernel(const float* __restrict__ y, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, float* __restrict__ out,
+                                                           int GN, int Nb, int H, int W, int C, int act, float slope) {
+  const int Cg = C >> 2;
+  const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
+  const long long total = (long long)GN * Ho * Wo * Cg;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int cg = (int)(i % Cg);
+    const long long pix = i / Cg;
+    const int c = cg * 4;
+    const long long n = pix / ((long long)Ho * Wo);
+    const long long co = (n / Nb) * C + c;
+    const f32x4 sc = *(const f32x4*)(scale + co), sh = *(const f32x4*)(shift + co);
+    f32x4 o;
+    if constexpr (!POOL) {
+      const f32x4 v = *(const f32x4*)(y + pix * C + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act_f(v[e] * sc[e] + sh[e], act, slope);
+    } else {
+      const long long r = pix - n * Ho * Wo;
+      const int ho = (int)(r / Wo), wo = (int)(r - (long long)ho * Wo);
+      const long long b0 = ((n * H + 2 * ho) * W + 2 * wo) * C + c;
+      const f32x4 v0 = *(const f32x4*)(y + b0), v1 = *(const f32x4*)(y + b0 + C);
+      const f32x4 v2 = *(const f32x4*)(y + b0 + (long long)W * C), v3 = *(const f32x4*)(y + b0 + (long long)W * C + C);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a0 = act_f(v0[e] * sc[e] + sh[e], act, slope), a1 = act_f(v1[e] * sc[e] + sh[e], act, slope);
+        const float a2 = act_f(v2[e] * sc[e] + sh[e], act, slope), a3 = act_f(v3[e] * sc[e] + sh[e], act, slope);
+        o[e] = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+      }
+    }
+    *(f32x4*)(out + pix * C + c) = o;
+  }
 }
 
 bool bn_shape_ok(int C) { return C >= 4 && C <= 1024 && (C & (C - 1)) == 0; }
@@ -482,11 +519,12 @@ extern "C" int rk_colsum_f32(const float* x, int R, int C, int ld, float* out, i
   return RK_OK;
 }
 
+// brows > 0: rows [g*brows, (g+1)*brows) take bias + g*N (grouped GEMM slabs)
 extern "C" int rk_sreduce_epi(const float* slab, int S, int M, int N, const float* bias, int act, float slope,
-                              float alpha, const float* gate, int ldg, float* out, int ldc, void* stream) {
-  if (N % 4 || ldc % 4 || (gate && ldg % 4)) return RK_EUNSUPPORTED;
+                              float alpha, const float* gate, int ldg, float* out, int ldc, int brows, void* stream) {
+  if (N % 4 || ldc % 4 || (gate && ldg % 4) || brows < 0) return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(sreduce_epi_kernel, dim3(grid_cap((long long)M * N / 4, 2048)), dim3(256), 0,
-                     (hipStream_t)stream, slab, S, M, N, bias, act, slope, alpha, gate, ldg, out, ldc);
+                     (hipStream_t)stream, slab, S, M, N, bias, act, slope, alpha, gate, ldg, out, ldc, brows);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -495,6 +533,20 @@ extern "C" int rk_pack_nhwc_f32(const void* src, int flags, int N, int C, int H,
                                 float shift, float* out, void* stream) {
   hipLaunchKernelGGL(pack_nhwc_f32_kernel, dim3(grid_cap((long long)N * H * W * Cp, 4096)), dim3(256), 0,
                      (hipStream_t)stream, src, flags, N, C, H, W, Cp, scale, shift, out);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_bnf_eval_grp(const float* y, const float* scale, const float* shift, float* out, int G, int Nb,
+                               int H, int W, int C, int pool, int act, float slope, void* stream) {
+  if (C % 4 || G < 1 || Nb < 1 || (pool && (H < 2 || W < 2))) return RK_EUNSUPPORTED;
+  const long long work = (long long)G * Nb * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
+  if (pool)
+    hipLaunchKernelGGL(bnf_eval_grp_kernel<true>, dim3(grid_cap(work, 2048)), dim3(256), 0, (hipStream_t)stream, y,
+                       scale, shift, out, G * Nb, Nb, H, W, C, act, slope);
+  else
+    hipLaunchKernelGGL(bnf_eval_grp_kernel<false>, dim3(grid_cap(work, 2048)), dim3(256), 0, (hipStream_t)stream, y,
+                       scale, shift, out, G * Nb, Nb, H, W, C, act, slope);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -73,6 +73,9 @@ struct SgParams {
   unsigned tpy[4], tpx[4];     // per group, tap t: offset = ((word >> 2t) & 3) - 1  (in -1 .. 2)
   unsigned oyx;                // per group g: output parity (bits 2g: oy, 2g+1: ox) when os == 2
   long long gstrideB;          // floats between the groups' B operands
+  // grouped GEMMs (rk_sgemm_grp: k same-shape problems in one launch, e.g. the k models of an
+  // inference ensemble): per-group operand / output / bias offsets in floats
+  long long gstrideA, gstrideO, gstrideBias;
 };
 
 RK_DEV __amdgpu_buffer_rsrc_t s_rsrc(const void* base, unsigned long long bytes) {
@@ -349,18 +352,18 @@ RK_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 // PA / PB: the A (rows) / B (columns) fragments were read interleaved (frag_pair)
 template <int MI, int NI, bool PA, bool PB, bool OMAP = false>
 RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int nbase, int lane, int split,
-                       int grp = 0) {
+                       int grp, float* outp, const float* biasp) {
   const int fl = p.flags;
   const int h = lane >> 5;
-  float* C = p.out + (long long)split * p.slabStride;
+  float* C = outp + (long long)split * p.slabStride;
   const bool want_sums = fl & (SF_STATS | SF_BNB | SF_BNP);
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
     const int n = PB ? nbase + 2 * (lane & 31) + ni : nbase + ni * 32 + (lane & 31);
     const bool nok = n < p.N;
     float b = 0.f, sh = 0.f;
-    if ((fl & (SF_BIAS | SF_BNB | SF_BNP)) && nok) b = p.bias[n];
-    if ((fl & (SF_BNB | SF_BNP)) && nok) sh = p.bias[p.N + n];
+    if ((fl & (SF_BIAS | SF_BNB | SF_BNP)) && nok) b = biasp[n];
+    if ((fl & (SF_BNB | SF_BNP)) && nok) sh = biasp[p.N + n];
     float s = 0.f, ss = 0.f;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
@@ -428,8 +431,9 @@ RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int 
 }
 
 // Workgroup = WGM x WGN waves, each owning (32*MI) x (32*NI) outputs: block tile BM x BN.
-template <int WGM, int WGN, int MI, int NI, int AM, int BMD, int NST>
+template <int WGM, int WGN, int MI, int NI, int AM, int BMD, int NST, bool GRP = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p) {
+  constexpr bool GR = GRP || AM == SM_KIN_CONVG;  // grid = groups x splits x tiles
   constexpr int NW = WGM * WGN;
   constexpr int WMT = 32 * MI, WNT = 32 * NI;  // wave tile
   constexpr int BM = WGM * WMT, BN = WGN * WNT;
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
   // weight gradient) run on one XCD and hit one L2
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   int grp = 0, rem = lin;
-  if constexpr (AM == SM_KIN_CONVG) {   // parity groups: grid = groups x splits x tiles
+  if constexpr (GR) {
     const int per = (int)(gridDim.x / p.groups);
     grp = lin / per;
     rem = lin - grp * per;
@@ -461,8 +465,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
 
   SOperand<AM, BM, NW> A;
   SOperand<BMD, BN, NW> B;
-  A.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane, grp);
-  if constexpr (AM == SM_KIN_CONVG)
+  if constexpr (GRP)
+    A.init(p, p.A + grp * p.gstrideA, p.bytesA - (unsigned long long)(grp * p.gstrideA) * 4ull, p.lda, m0, p.M,
+           wid, lane, grp);
+  else
+    A.init(p, p.A, p.bytesA, p.lda, m0, p.M, wid, lane, grp);
+  if constexpr (GR)
     B.init(p, p.B + grp * p.gstrideB, p.bytesB - (unsigned long long)(grp * p.gstrideB) * 4ull, p.ldb, n0, p.N,
            wid, lane);
   else
@@ -544,21 +552,23 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
   }
   s_wait_vmcnt<0>();  // the trailing zero-DMAs land before the workgroup's LDS is released
   s_epilogue<MI, NI, !SOperand<AM, BM, NW>::KIN && MI == 2, !SOperand<BMD, BN, NW>::KIN && NI == 2,
-             AM == SM_KIN_CONVG>(p, acc, m0 + wm * WMT, n0 + wn * WNT, lane, split, grp);
+             AM == SM_KIN_CONVG>(p, acc, m0 + wm * WMT, n0 + wn * WNT, lane, split, grp,
+                                 GRP ? p.out + grp * p.gstrideO : p.out,
+                                 GRP && p.bias ? p.bias + grp * p.gstrideBias : p.bias);
 }
 
-template <int WGM, int WGN, int MI, int NI, int AM, int BMD>
+template <int WGM, int WGN, int MI, int NI, int AM, int BMD, bool GRP = false>
 int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
   const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
-  dim3 grid(tiles * splits * (AM == SM_KIN_CONVG ? p.groups : 1));
+  dim3 grid(tiles * splits * ((GRP || AM == SM_KIN_CONVG) ? p.groups : 1));
   if (nst == 3) {
     if constexpr (WGM * WGN == 4)  // 3-stage rings only for the 4-wave tiles (8-wave ones fill LDS at 2)
-      hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3>), grid, dim3(64 * WGM * WGN), 0, st, p);
+      hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3, GRP>), grid, dim3(64 * WGM * WGN), 0, st, p);
     else
       return RK_EUNSUPPORTED;
   } else {
-    hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 2>), grid, dim3(64 * WGM * WGN), 0, st, p);
+    hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 2, GRP>), grid, dim3(64 * WGM * WGN), 0, st, p);
   }
   RK_LAUNCH_CHECK();
   return RK_OK;
@@ -567,13 +577,13 @@ int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
 // tile codes (block tile, waves): 0 128x128 (2x2), 1 128x64 (2x2), 2 64x128 (2x2), 3 64x64 (2x2),
 // 4 256x64 (4x1), 5 256x128 (4x2, 512 threads), 6 128x256 (2x4, 512 threads), 7 64x256 (1x4).
 // BIG = false instantiates only tiles 0-3 (dense layers, the general conv gather).
-template <int AM, int BMD, bool BIG>
+template <int AM, int BMD, bool BIG, bool GRP = false>
 int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t st) {
   switch (tile) {
-    case 0: return s_launch<2, 2, 2, 2, AM, BMD>(p, nst, splits, st);
-    case 1: return s_launch<2, 2, 2, 1, AM, BMD>(p, nst, splits, st);
-    case 2: return s_launch<2, 2, 1, 2, AM, BMD>(p, nst, splits, st);
-    case 3: return s_launch<2, 2, 1, 1, AM, BMD>(p, nst, splits, st);
+    case 0: return s_launch<2, 2, 2, 2, AM, BMD, GRP>(p, nst, splits, st);
+    case 1: return s_launch<2, 2, 2, 1, AM, BMD, GRP>(p, nst, splits, st);
+    case 2: return s_launch<2, 2, 1, 2, AM, BMD, GRP>(p, nst, splits, st);
+    case 3: return s_launch<2, 2, 1, 1, AM, BMD, GRP>(p, nst, splits, st);
   }
   if constexpr (BIG) {
     switch (tile) {
@@ -694,4 +704,43 @@ extern "C" int rk_sgemm_g(int kind, int tile, int nst, const float* A, const flo
   hipStream_t st = (hipStream_t)stream;
   if (kind == 6) return s_launch_tile<SM_KIN_CONVG, SM_KIN_DENSE, false>(tile, p, nst, splits, st);
   return s_launch_tile<SM_KOUT_DENSE, SM_KOUT_CONVG, false>(tile, p, nst, splits, st);
+}
+
+// Grouped GEMMs: `groups` same-shape problems in ONE launch (grid groups x splits x tiles) — the k models
+// of an inference ensemble run each layer as one kernel.  Group g reads A + g*gstrideA (0: a shared
+// input, e.g. the request batch), B + g*gstrideB, writes out + g*gstrideO and uses bias + g*gstrideBias.
+// kind 0 (conv forward) and 3 (dense A.B^T); flags: bias / ReLU / leaky-ReLU (no statistics).
+// bytesA / bytesB cover every group's operand.
+extern "C" int rk_sgemm_grp(int kind, int tile, int nst, const float* A, const float* B, float* C, const float* bias,
+                            int M, int N, int K, int lda, int ldb, int ldc, int H, int W, int Cch, int taps, int splits,
+                            long long slabStride, int flags, float alpha, float slope, long long bytesA,
+                            long long bytesB, int groups, long long gstrideA, long long gstrideB, long long gstrideO,
+                            long long gstrideBias, void* stream) {
+  if (kind != 0 && kind != 3) return RK_EBADARG;
+  if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 3) return RK_EBADARG;
+  if (groups < 1 || gstrideA < 0 || gstrideB < 0 || gstrideO < 0 || gstrideBias < 0) return RK_EBADARG;
+  if (taps != 1 && taps != 9) return RK_EBADARG;
+  if (K % 4 || lda % 4 || ldb % 4) return RK_EUNSUPPORTED;
+  if (kind == 0 && (Cch % 4 || Cch <= 0 || H <= 0 || W <= 0)) return RK_EUNSUPPORTED;
+  if (flags & ~(SF_BIAS | SF_RELU | SF_LRELU)) return RK_EUNSUPPORTED;
+  if (splits > 1 && flags) return RK_EBADARG;
+  SgParams p{};
+  p.A = A; p.B = B; p.out = C; p.bias = bias;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.H = H; p.W = W; p.C = Cch; p.taps = taps;
+  p.log2H = rk_log2(H); p.log2W = rk_log2(W); p.log2C = rk_log2(Cch);
+  p.invC = 1.0f / (float)Cch; p.invH = 1.0f / (float)H; p.invW = 1.0f / (float)W;
+  if (kind == 0 && (p.log2H < 0 || p.log2W < 0) && (long long)M + (long long)W * (H + 2) >= (1ll << 22))
+    return RK_EUNSUPPORTED;
+  p.ktPer = rk_cdiv(rk_cdiv(K, SBK), splits);
+  p.slabStride = splits > 1 ? slabStride : 0;
+  p.flags = flags; p.alpha = alpha; p.slope = slope;
+  p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
+  p.groups = groups; p.gstrideA = gstrideA; p.gstrideB = gstrideB; p.gstrideO = gstrideO; p.gstrideBias = gstrideBias;
+  p.Ho = H; p.Wo = W; p.log2Ho = p.log2H; p.log2Wo = p.log2W; p.invHo = p.invH; p.invWo = p.invW;
+  hipStream_t st = (hipStream_t)stream;
+  if (kind == 3) return s_launch_tile<SM_KIN_DENSE, SM_KIN_DENSE, false, true>(tile, p, nst, splits, st);
+  if (Cch % SBK == 0) return s_launch_tile<SM_KIN_CONVF, SM_KIN_DENSE, false, true>(tile, p, nst, splits, st);
+  return s_launch_tile<SM_KIN_CONV, SM_KIN_DENSE, false, true>(tile, p, nst, splits, st);
 }

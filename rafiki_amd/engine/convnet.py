@@ -839,3 +839,63 @@ class ConvNetEngine:
         if '__running__' in d:
             self.running.copy_(torch.as_tensor(d['__running__']))
         self._eval_coeffs = None
+
+
+class GroupedConvNets:
+    """k trained fp32 ConvNetEngines of ONE architecture evaluated as a single network: every layer
+    of all k models is one grouped kernel (ops.f32 *_grp) over weights stacked [k, ...] at build
+    time, so an ensemble forward costs the launches of one model with k x the work per launch (the
+    small-batch serving latency of k models ~ that of one).  The request batch is packed once and
+    shared by every group's first layer.  Inference only (BN folded into scale / shift)."""
+
+    @staticmethod
+    def arch_key(eng):
+        if not isinstance(eng, ConvNetEngine) or not eng.f32 or eng.input_bn or eng.flat_input:
+            return None
+        return (tuple(eng.blocks), tuple(eng.fcs), eng.num_classes, eng.ncls_p, eng.cin_p, eng.image_size,
+                eng.feat_dim, str(eng.device))
+
+    def __init__(self, engines):
+        keys = {self.arch_key(e) for e in engines}
+        if len(keys) != 1 or None in keys:
+            raise ValueError('GroupedConvNets needs fp32 conv engines of one architecture')
+        self.engines = list(engines)
+        e0 = self.engines[0]
+        self.k, self.proto = len(engines), e0
+        self.device = e0.device
+        self.refresh()
+
+    @torch.no_grad()
+    def refresh(self):
+        """(Re)stack the current weights and folded BN coefficients of the k engines."""
+        e0 = self.proto
+        for e in self.engines:
+            if e._eval_coeffs is None:
+                e.prepare_eval()
+
+        def stack(fn):
+            return torch.stack([fn(e) for e in self.engines]).contiguous()
+        self.conv_w = [stack(lambda e, n=name: e.flat.w(n + '.w').reshape(e.flat.w(n + '.w').shape[0], -1))
+                       for (name, _, _, _, _) in e0.blocks]
+        self.scale = [stack(lambda e, i=bi: e._eval_coeffs[i][2]) for bi in range(len(e0.blocks))]
+        self.shift = [stack(lambda e, i=bi: e._eval_coeffs[i][3]) for bi in range(len(e0.blocks))]
+        self.fc_w = [stack(lambda e, n=name: e.flat.w(n + '.w')) for (name, _, _, _) in e0.fcs]
+        self.fc_b = [stack(lambda e, n=name: e.flat.w(n + '.b')) for (name, _, _, _) in e0.fcs]
+        self.out_w = stack(lambda e: e.flat.w('out.w'))
+        self.out_b = stack(lambda e: e.flat.w('out.b'))
+
+    @torch.no_grad()
+    def forward_into(self, x, out_probs):
+        """x: the engines' input layout [B, H, W, cin_p] fp32 (shared); out_probs [k, B, num_classes]."""
+        e0, k = self.proto, self.k
+        B = x.shape[0]
+        h = x
+        for bi, (name, cin, cout, pool, hw) in enumerate(e0.blocks):
+            y = S.conv_fwd_grp(h, self.conv_w[bi])
+            h = S.bn_eval_grp(y, self.scale[bi], self.shift[bi], pool=pool, act=F.ACT_RELU)
+        z = h.reshape(k, B, e0.feat_dim)
+        for i in range(len(e0.fcs)):
+            z = S.linear_grp(z, self.fc_w[i], self.fc_b[i], act=F.ACT_RELU)
+        logits = S.linear_grp(z, self.out_w, self.out_b)
+        S.softmax_xent(logits.view(k * B, -1), None, e0.num_classes, probs=out_probs.view(k * B, -1))
+        return out_probs

@@ -201,6 +201,10 @@ class NativeImageClassifier(BaseModel):
     def num_classes(self):
         return int(self._meta['num_classes'])
 
+    def serving_engine(self):
+        """The trained engine (the predictor groups same-architecture engines into one network)."""
+        return self._engine
+
     def release_training(self):
         """Keep only the inference state (trainer -> predictor HBM handoff, predictor.resident)."""
         if self._engine is not None:

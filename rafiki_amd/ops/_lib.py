@@ -71,7 +71,10 @@ _SIGS = {
     "rk_bnf_colstats": [vp, vp, i32, i32, vp, vp],
     "rk_swt": [vp, vp, vp, i32, vp, vp],
     "rk_colsum_f32": [vp, i32, i32, i32, vp, i32, i32, vp],
-    "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, vp],
+    "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, i32, vp],
+    "rk_sgemm_grp": [i32, i32, i32, vp, vp, vp, vp] + [i32] * 10 + [i32, i64, i32, f32, f32, i64, i64, i32, i64, i64,
+                                                                     i64, i64, vp],
+    "rk_bnf_eval_grp": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
     "rk_pack_nhwc_f32": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
     "rk_softmax_xent_f32": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],
     # table-driven gathers (PG-GAN up / down convs), resampling, fp32 PG-GAN side kernels

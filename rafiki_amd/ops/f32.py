@@ -332,9 +332,11 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, *, out=None, accumulate=False):
     return out
 
 
-def sreduce_epi(slab, M, N, out, *, bias=None, act=ACT_NONE, slope=0.2, alpha=1.0, gate=None):
+def sreduce_epi(slab, M, N, out, *, bias=None, act=ACT_NONE, slope=0.2, alpha=1.0, gate=None, bias_rows=0):
+    """out = act(alpha * sum_s slab[s] + bias) (gated); bias_rows > 0: row block g uses bias[g]."""
     _lib.call("rk_sreduce_epi", _p(slab), slab.shape[0], int(M), int(N), _p(bias), int(act), float(slope),
-              float(alpha), _p(gate), 0 if gate is None else gate.stride(0), _p(out), out.stride(0), _s())
+              float(alpha), _p(gate), 0 if gate is None else gate.stride(0), _p(out), out.stride(0), int(bias_rows),
+              _s())
     return out
 
 
@@ -612,4 +614,78 @@ def conv_wt(w, taps=9):
     Cin = w.numel() // (taps * Cout)
     out = torch.empty((Cin, taps * Cout), device=w.device, dtype=torch.float32)
     _lib.call("rk_wflip_t", _p(w.contiguous()), _p(out), int(Cout), int(Cin), int(taps), _s())
+    return out
+
+
+# ------------------------------------------------------------------------------ grouped GEMMs
+# k same-shape problems per launch (rk_sgemm_grp): the k models of an inference ensemble run each layer
+# as ONE kernel (k x the workgroups of one model: small-batch layers fill the chip, launches / k).
+def sgemm_grp(kind, A, B, out, M, N, K, lda, ldb, ldc, groups, gstride_a, gstride_b, gstride_o, gstride_bias=0, *,
+              tile=0, nst=2, splits=1, slab_stride=0, bias=None, flags=0, alpha=1.0, slope=0.2, H=1, W=1, C=4,
+              taps=1):
+    _lib.call("rk_sgemm_grp", int(kind), int(tile), int(nst), _p(A), _p(B), _p(out), _p(bias), int(M), int(N), int(K),
+              int(lda), int(ldb), int(ldc), int(H), int(W), int(C), int(taps), int(splits), int(slab_stride),
+              int(flags), float(alpha), float(slope), _nbytes(A), _nbytes(B), int(groups), int(gstride_a),
+              int(gstride_b), int(gstride_o), int(gstride_bias), _s())
+    return out
+
+
+def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=ACT_NONE, slope=0.2, geo=None):
+    """Autotuned grouped launch: out [G, M, N]; split-K slabs [s, G*M, N] combined by sreduce_epi with
+    per-group bias."""
+    flags = _act_flags(bias, act)
+    geo = geo or {}
+
+    def run(cfg):
+        tile, nst, s = cfg
+        if s == 1:
+            sgemm_grp(kind, A, B, out, M, N, K, lda, ldb, N, G, gsa, N * K, M * N, N, tile=tile, nst=nst,
+                      bias=bias, flags=flags, slope=slope, **geo)
+            return
+        slab = torch.empty((s, G * M, N), device=out.device, dtype=torch.float32)
+        sgemm_grp(kind, A, B, slab, M, N, K, lda, ldb, N, G, gsa, N * K, M * N, 0, tile=tile, nst=nst, splits=s,
+                  slab_stride=G * M * N, **geo)
+        sreduce_epi(slab, G * M, N, out.view(G * M, N), bias=bias, act=act, slope=slope, bias_rows=M)
+    cands = [c for c in _cands(M * G, N, splittable=N % 4 == 0, K=K) if c[0] < 4]
+    run(_pick(key, cands, run))
+    return out
+
+
+def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None):
+    """k convs in one launch: x [G, Nb, H, W, Cin] (or [Nb, H, W, Cin] shared by every group),
+    W [G, Cout, taps*Cin], bias [G, Cout] -> [G, Nb, H, W, Cout] (3x3 stride-1 or 1x1)."""
+    G, Cout, K = W.shape
+    shared = x.dim() == 4
+    Nb, H, Wd, Cin = x.shape[-4:]
+    taps = K // Cin
+    assert taps in (1, 9) and K == taps * Cin and (shared or x.shape[0] == G), (x.shape, W.shape)
+    _check(x, 'conv_fwd_grp x')
+    M = Nb * H * Wd
+    if out is None:
+        out = torch.empty((G, Nb, H, Wd, Cout), device=x.device, dtype=torch.float32)
+    return _grp_run(0, x, W, out, M, Cout, K, Cin, K, G, 0 if shared else M * Cin,
+                    ('sfg', G, M, Cout, K, H, Wd, Cin, shared, bias is not None, act), bias=bias, act=act,
+                    slope=slope, geo=dict(H=H, W=Wd, C=Cin, taps=taps))
+
+
+def linear_grp(x, w, bias=None, *, act=ACT_NONE, slope=0.2, out=None):
+    """k dense layers in one launch: x [G, M, K] (or [M, K] shared), w [G, N, K], bias [G, N] -> [G, M, N]."""
+    G, N, K = w.shape
+    shared = x.dim() == 2
+    M = x.shape[-2]
+    _check(x, 'linear_grp x')
+    if out is None:
+        out = torch.empty((G, M, N), device=x.device, dtype=torch.float32)
+    return _grp_run(3, x, w, out, M, N, K, K, K, G, 0 if shared else M * K,
+                    ('slg', G, M, N, K, shared, bias is not None, act), bias=bias, act=act, slope=slope)
+
+
+def bn_eval_grp(y, scale, shift, *, pool=False, act=ACT_RELU, slope=0.2, out=None):
+    """eval BN(+act, +2x2 max-pool) of G stacked batches y [G, Nb, H, W, C] with per-group scale / shift [G, C]."""
+    G, Nb, H, W, C = y.shape
+    if out is None:
+        out = torch.empty((G, Nb, H // 2 if pool else H, W // 2 if pool else W, C), device=y.device,
+                          dtype=torch.float32)
+    _lib.call("rk_bnf_eval_grp", _p(y), _p(scale.contiguous()), _p(shift.contiguous()), _p(out), G, Nb, H, W, C,
+              int(pool), int(act), float(slope), _s())
     return out

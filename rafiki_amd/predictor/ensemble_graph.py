@@ -12,18 +12,23 @@ holds
 
 so a request costs one host memcpy into the pinned buffer, ONE graph launch and one stream sync —
 independent of k and of the model depth (at batch 1 the per-model graphs + stack + ensemble of the
-previous design were launch-bound at ~0.9 ms for 4 fp32 models).  The k branches run concurrently
-on the GPU.  Buckets are captured lazily on first use; a replica's graphs are serialised by a lock
-(each replica owns its models, buffers and stream, so replicas run concurrently).
+previous design were launch-bound at ~0.9 ms for 4 fp32 models).  Models of one architecture are
+evaluated as ONE grouped network (engine.convnet.GroupedConvNets: every layer of all of them is a
+single grouped kernel), so the graph holds the launches of one model, not k; other models get their
+own captured stream branch.  Buckets are captured lazily on first use; a replica's graphs are
+serialised by a lock (each replica owns its models, buffers and stream, so replicas run concurrently).
 """
 from __future__ import annotations
 
+import os
 import threading
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
+from ..ops.graphs import LOCK as _GRAPH_LOCK
 from ..ops.graphs import capture as _capture
 
 BUCKETS = (1, 8, 32, 64, 128, 256, 512)
@@ -50,9 +55,40 @@ class _Entry:
     __slots__ = ('graph', 'h_in', 'd_in', 'slots', 'out', 'h_out', 'bucket', 'host')
 
 
+def _plan_groups(models):
+    """[(member indices, GroupedConvNets or None)]: same-architecture native fp32 engines share one
+    grouped network; everything else runs alone."""
+    from ..engine.convnet import GroupedConvNets
+    by = OrderedDict()
+    for i, m in enumerate(models):
+        fn = getattr(m, 'serving_engine', None)
+        eng = fn() if callable(fn) else None
+        key = GroupedConvNets.arch_key(eng) if eng is not None else None
+        if key is None or os.environ.get('RAFIKI_ENSEMBLE_GROUPED', '1') == '0':
+            key = ('single', i)
+        by.setdefault(key, []).append(i)
+    plan = []
+    for key, idx in by.items():
+        grouped = None
+        if len(idx) > 1 and key[0] != 'single':
+            grouped = GroupedConvNets([models[i].serving_engine() for i in idx])
+        plan.append((idx, grouped))
+    return plan
+
+
 class EnsembleGraphs:
     def __init__(self, models: Sequence[object], weights: Optional[Sequence[float]] = None):
-        self.models = list(models)
+        for m in models:
+            m.prepare_serving()
+        plan = _plan_groups(list(models))
+        order = [i for idx, _ in plan for i in idx]   # slot order: group members contiguous
+        self.models = [models[i] for i in order]
+        if weights is not None:
+            weights = [weights[i] for i in order]
+        self.plan, pos = [], 0
+        for idx, grouped in plan:
+            self.plan.append((pos, pos + len(idx), grouped))
+            pos += len(idx)
         self.device = torch.device(getattr(self.models[0], 'device'))
         self.num_classes = int(self.models[0].num_classes)
         self.sigs: List[Tuple] = []
@@ -64,12 +100,10 @@ class EnsembleGraphs:
                                                                    device=self.device)
         self.lock = threading.Lock()
         self.stream = torch.cuda.Stream(device=self.device)
-        self._branches = [torch.cuda.Stream(device=self.device) for _ in self.models]
+        self._branches = [torch.cuda.Stream(device=self.device) for _ in self.plan]
         self._graphs: Dict[Tuple[int, bool], _Entry] = {}
         self._shapes: Dict[Tuple, Tuple] = {}
         self.replays = 0
-        for m in self.models:
-            m.prepare_serving()
 
     # ------------------------------------------------------------------ capture
     def _body(self, e: _Entry):
@@ -78,10 +112,15 @@ class EnsembleGraphs:
         if e.host:
             for s in self.sigs:
                 e.d_in[s].copy_(e.h_in[s], non_blocking=True)
-        for i, (m, br) in enumerate(zip(self.models, self._branches)):
+        for (lo, hi, grouped), br in zip(self.plan, self._branches):
             br.wait_stream(main)
             with torch.cuda.stream(br):
-                m.forward_into(e.d_in[m.input_signature()], e.slots[i])
+                m = self.models[lo]
+                xin = e.d_in[m.input_signature()]
+                if grouped is not None:
+                    grouped.forward_into(grouped.proto.prepare_inputs(xin), e.slots[lo:hi])
+                else:
+                    m.forward_into(xin, e.slots[lo])
         for br in self._branches:
             main.wait_stream(br)
         F.ensemble_mean(e.slots, self.weights, out=e.out)
@@ -92,6 +131,12 @@ class EnsembleGraphs:
         e = self._graphs.get((bucket, host))
         if e is not None:
             return e
+        # warm-up (autotuning, allocator growth, device syncs) and capture of a new bucket are
+        # serialised process-wide: another replica's thread may be capturing at the same moment
+        with _GRAPH_LOCK:
+            return self._build_entry(bucket, host)
+
+    def _build_entry(self, bucket: int, host: bool) -> _Entry:
         e = _Entry()
         e.bucket, e.host = bucket, host
         e.h_in = {s: torch.zeros((bucket,) + self._shapes[s], dtype=torch.uint8).pin_memory()

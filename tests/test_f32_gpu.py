@@ -314,3 +314,28 @@ def test_prepare_inputs_nhwc_pack():
     assert torch.allclose(got, ref, atol=1e-6)
     got_host = eng.prepare_inputs(imgs.numpy()).cpu()
     assert torch.allclose(got_host, ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("shared", [True, False])
+def test_grouped_conv_linear_bn_match_per_group(shared):
+    """rk_sgemm_grp / rk_bnf_eval_grp: k same-shape problems in one launch == k separate launches."""
+    from rafiki_amd.ops import f32 as S
+    G, Nb, H, Cin, Cout = 3, 2, 8, 32, 64
+    x = (_rand(Nb, H, H, Cin, seed=1) if shared else _rand(G, Nb, H, H, Cin, seed=1)).to(DEV)
+    W = _rand(G, Cout, 9 * Cin, seed=2, scale=0.05).to(DEV)
+    b = _rand(G, Cout, seed=3, scale=0.1).to(DEV)
+    y = S.conv_fwd_grp(x, W, bias=b, act=S.ACT_RELU)
+    for g in range(G):
+        ref = S.conv_fwd(x if shared else x[g].contiguous(), W[g].contiguous(), bias=b[g].contiguous(), act=S.ACT_RELU)
+        assert rel(y[g], ref) < 1e-6
+    sc, sh = _rand(G, Cout, seed=4).to(DEV), _rand(G, Cout, seed=5).to(DEV)
+    z = S.bn_eval_grp(y, sc, sh, pool=True)
+    for g in range(G):
+        assert rel(z[g], S.bn_eval(y[g].contiguous(), sc[g].contiguous(), sh[g].contiguous(), pool=True)) < 1e-6
+    M, K, N = 5, 256, 40
+    xa = (_rand(M, K, seed=6) if shared else _rand(G, M, K, seed=6)).to(DEV)
+    wl, bl = _rand(G, N, K, seed=7, scale=0.05).to(DEV), _rand(G, N, seed=8).to(DEV)
+    o = S.linear_grp(xa, wl, bl, act=S.ACT_RELU)
+    for g in range(G):
+        ref = torch.relu((xa if shared else xa[g]).double().cpu() @ wl[g].double().cpu().t() + bl[g].double().cpu())
+        assert rel(o[g], ref) < 1e-5

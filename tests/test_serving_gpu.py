@@ -258,6 +258,25 @@ def test_one_graph_ensemble_matches_per_model_path(ensemble, monkeypatch):
     g = p.replicas[0].graphs
     assert g is not None and g.replays >= 8 and ref_p.replicas[0].graphs is None
     assert {b for b, _ in g._graphs} >= {1, 8, 64, 512}
+    # the 4 same-architecture models run as ONE grouped network
+    assert len(g.plan) == 1 and g.plan[0][2] is not None and g.plan[0][2].k == 4
+
+
+def test_ensemble_graph_mixed_architectures(ensemble):
+    """A different-width model joins the graph as its own branch next to the grouped network."""
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.models.vgg_small import VggSmall
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    from rafiki_amd.predictor.predictor import Predictor
+    with use_context(TrialContext(device=torch.device(DEV))):
+        wide = VggSmall(epochs=1, learning_rate=0.05, momentum=0.9, weight_decay=5e-4, batch_size=128, width_mult=1.0,
+                        image_size=32, seed=9)
+        wide.train(TRAIN)
+    models = _copy_ensemble(ensemble[:2]) + [('wide', wide)] + _copy_ensemble(ensemble[2:3])
+    imgs, _ = synthetic_images(9, size=32, channels=3, classes=10, seed=21)
+    got = Predictor(models).predict_array(imgs)
+    ref = torch.stack([m.predict_proba(imgs.tolist()).float().cpu() for _, m in models]).mean(0).numpy()
+    assert np.allclose(got, ref, atol=1e-5)
 
 
 def test_replicas_serve_concurrent_requests(ensemble):
