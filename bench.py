@@ -206,20 +206,26 @@ def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30):
     top = trials[:k]
     if len(top) < k:
         return None
+    from rafiki_amd.predictor.resident import STORE
     models = []
+    from_hbm = 0
     t_load = time.perf_counter()
     for t in top:
-        mrec = db.get_model(db.get_sub_train_job(t.sub_train_job_id).model_id)
-        clazz = load_model_class(mrec.model_file_bytes, mrec.model_class)
-        inst = clazz(**(t.knobs or {}))
-        with open(t.params_file_path, 'rb') as f:
-            inst.load_parameters(pickle.loads(f.read()))
+        inst = STORE.take(t.id)   # trained in this process: still resident in HBM (no params-file read)
+        if inst is not None and str(getattr(inst, 'device', '')) == str(dev):
+            from_hbm += 1
+        else:
+            mrec = db.get_model(db.get_sub_train_job(t.sub_train_job_id).model_id)
+            clazz = load_model_class(mrec.model_file_bytes, mrec.model_class)
+            inst = clazz(**(t.knobs or {}))
+            with open(t.params_file_path, 'rb') as f:
+                inst.load_parameters(pickle.loads(f.read()))
         models.append((t.id, inst))
     t_load = time.perf_counter() - t_load
     pred = Predictor(models, max_batch=512)
     rng = np.random.default_rng(0)
     sig = models[0][1].input_signature()
-    out = {'models': k, 'load_s': round(t_load, 3)}
+    out = {'models': k, 'load_s': round(t_load, 3), 'loaded_from_hbm': from_hbm}
 
     def timed(fn, n):
         fn()
