@@ -72,7 +72,7 @@ def config2(n_train, n_test, epochs):
         t_trial = time.perf_counter() - t0
     return {'config': 'TfFeedForward-style MLP, 1 trial on 1 {}'.format('MI355X' if dev.type == 'cuda' else 'CPU'),
             'metric': 'training images/s (incl. data decode + upload)', 'value': round(n_train * epochs / t_train, 1),
-            'trial_seconds': round(t_trial, 3), 'score': s, 'knobs': knobs, 'dtype': 'bf16',
+            'trial_seconds': round(t_trial, 3), 'score': s, 'knobs': knobs, 'dtype': m._meta.get('dtype', 'fp32'),
             'data': 'synthetic Fashion-MNIST-shaped {}+{} 28x28'.format(n_train, n_test)}
 
 
@@ -100,6 +100,7 @@ def config3(trials, epochs):
             m = clazz(**knobs)
             m.train(train)
             torch.cuda.synchronize()
+            dtype = m._meta.get('dtype', 'fp32')
             t1 = time.perf_counter()
             s = m.evaluate(test)
             t2 = time.perf_counter()
@@ -118,7 +119,7 @@ def config3(trials, epochs):
             'value': round(3600.0 / per, 1), 'seconds_per_trial': round(per, 3),
             'first_trial_seconds': round(times[0], 3), 'trials': trials, 'phases_last_trial': phases[-1],
             'trial_definition': '{} epochs x 50000 images, batch 256, + eval 10000 + dump'.format(epochs),
-            'best_score': max(scores), 'dtype': 'bf16',
+            'best_score': max(scores), 'dtype': dtype,
             'data': 'synthetic CIFAR-shaped 50000+10000 32x32x3 (class-conditional), random-init weights'}
 
 
