@@ -26,6 +26,8 @@ OBJ_DIR = ROOT / "build" / "obj"
 NATIVE_DIR = Path(__file__).resolve().parent / "_native"
 KERNEL_LIB = NATIVE_DIR / "librafiki_kernels.so"
 RUNTIME_LIB = NATIVE_DIR / "librafiki_runtime.so"
+PYEXT_SRC = ROOT / "csrc" / "pyext"
+PYLIST_LIB = NATIVE_DIR / "librafiki_pylist.so"
 
 ARCH = os.environ.get("RAFIKI_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -87,13 +89,30 @@ def build_runtime(verbose: bool = False) -> Path | None:
     return RUNTIME_LIB
 
 
+def build_pyext(verbose: bool = False) -> Path | None:
+    """``csrc/pyext/*.cpp`` -> librafiki_pylist.so: C++ against the CPython headers, loaded with
+    ctypes.PyDLL (GIL held), no libpython link (symbols resolve in the host interpreter)."""
+    import sysconfig
+    srcs = sorted(PYEXT_SRC.glob("*.cpp"))
+    if not srcs:
+        return None
+    NATIVE_DIR.mkdir(parents=True, exist_ok=True)
+    if _stale(PYLIST_LIB, srcs):
+        tmp = PYLIST_LIB.with_suffix(".so.tmp")
+        _run([CXX, *CXX_FLAGS, "-shared", f"-I{sysconfig.get_paths()['include']}", *srcs, "-o", tmp], verbose)
+        os.replace(tmp, PYLIST_LIB)
+    return PYLIST_LIB
+
+
 def build(verbose: bool = False) -> None:
     if shutil.which(HIPCC) is None and not Path(HIPCC).exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
     build_kernels(verbose=verbose)
     build_runtime(verbose=verbose)
+    build_pyext(verbose=verbose)
 
 
 if __name__ == "__main__":
     build(verbose="-v" in sys.argv)
-    print(f"built {KERNEL_LIB}" + (f" and {RUNTIME_LIB}" if RUNTIME_LIB.exists() else ""))
+    print(f"built {KERNEL_LIB}" + (f" and {RUNTIME_LIB}" if RUNTIME_LIB.exists() else "")
+          + (f" and {PYLIST_LIB}" if PYLIST_LIB.exists() else ""))

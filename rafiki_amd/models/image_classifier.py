@@ -1,6 +1,6 @@
 """Shared machinery for the native image-classification models (VGG-small, FeedForward MLP).
 
-A trial uploads its whole train split to HBM once (uint8 -> packed bf16 by one gfx950 kernel),
+A trial uploads its whole train split to HBM once (uint8 -> packed fp32 / bf16 NHWC by one gfx950 kernel),
 captures the training step into a hipGraph and replays it per batch; shuffling and batching are
 device-side index_selects.  evaluate/predict use hipGraph-captured forwards per batch bucket.
 Task I/O contract (reference docs/src/user/tasks.rst:23-63): a query is an HxW (grayscale) or
@@ -171,7 +171,11 @@ class NativeImageClassifier(BaseModel):
         return float((pred == np.asarray(labels)).mean())
 
     def _queries_to_images(self, queries):
-        arr = np.asarray(queries)
+        from .. import runtime
+        # nested-list queries (the JSON query format) through the native walker (~10x numpy)
+        arr = runtime.pylist_u8(queries) if isinstance(queries, (list, tuple)) else None
+        if arr is None:
+            arr = np.asarray(queries)
         if arr.dtype != np.uint8:
             arr = np.clip(arr, 0, 255).astype(np.uint8)
         if arr.ndim == 2:

@@ -74,3 +74,38 @@ def json_u8_array(body: bytes, key: str, max_elems: int = 1 << 26):
     if n < 0:
         return None
     return out[:n].reshape([int(shape[i]) for i in range(nd.value)])
+
+
+# ------------------------------------------------------------------- nested lists -> uint8 (GIL held)
+_PYLIST = Path(__file__).resolve().parent / "_native" / "librafiki_pylist.so"
+_py = None
+
+
+def _pylib():
+    global _py
+    if _py is None and _PYLIST.exists():
+        h = ctypes.PyDLL(str(_PYLIST))
+        h.rk_pylist_shape.restype, h.rk_pylist_shape.argtypes = ctypes.c_int, [ctypes.py_object, ctypes.c_void_p]
+        h.rk_pylist_u8.restype = ctypes.c_int
+        h.rk_pylist_u8.argtypes = [ctypes.py_object, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        _py = h
+    return _py
+
+
+def pylist_u8(obj):
+    """A rectangular nest of Python lists / tuples of ints or floats -> uint8 numpy array (clipped to
+    [0, 255], floats truncated) by the native walker; None when the library is missing or the nest
+    is ragged / non-numeric (callers then fall back to numpy)."""
+    h = _pylib()
+    if h is None or not isinstance(obj, (list, tuple)):
+        return None
+    import numpy as np
+    shape = (ctypes.c_longlong * 8)()
+    nd = h.rk_pylist_shape(obj, shape)
+    if nd < 0:
+        return None
+    dims = [int(shape[i]) for i in range(nd)]
+    out = np.empty(dims, dtype=np.uint8)
+    if out.size and h.rk_pylist_u8(obj, shape, nd, out.ctypes.data) != 0:
+        return None
+    return out

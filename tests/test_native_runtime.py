@@ -22,3 +22,18 @@ def test_runtime_asan_ubsan(tmp_path):
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert 'runtime tests ok' in r.stdout
+
+
+def test_pylist_u8_matches_numpy():
+    import numpy as np
+    from rafiki_amd import runtime
+    rng = np.random.default_rng(0)
+    q = rng.integers(-20, 300, (5, 7, 3)).tolist()
+    got = runtime.pylist_u8(q)
+    assert got is not None and got.dtype == np.uint8
+    assert (got == np.clip(np.asarray(q), 0, 255).astype(np.uint8)).all()
+    f = (rng.random((4, 6)) * 400 - 50).tolist()
+    assert (runtime.pylist_u8(f) == np.clip(np.asarray(f), 0, 255).astype(np.uint8)).all()
+    assert runtime.pylist_u8([[1, 2], [3]]) is None          # ragged
+    assert runtime.pylist_u8([['a', 'b']]) is None           # non-numeric
+    assert runtime.pylist_u8(((1, 2), (3, 4))).tolist() == [[1, 2], [3, 4]]
