@@ -15,6 +15,7 @@ import numpy as np
 from rafiki_amd.constants import TaskType  # noqa: F401
 from rafiki_amd.model import (BaseModel, CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, dataset_utils,
                               logger)
+from rafiki_amd.engine.convnet import default_dtype
 from rafiki_amd.parallel.context import current as trial_context
 from rafiki_amd.utils import faults
 
@@ -148,10 +149,11 @@ class PyBiLstm(BaseModel):
                 s.lstm = nn.LSTM(int(k.get('word_embed_dims', 64)), int(k.get('word_rnn_hidden_size', 64)),
                                  batch_first=True, bidirectional=True)
                 s.out = nn.Linear(2 * int(k.get('word_rnn_hidden_size', 64)), self._tag_count)
+                s.rec_dtype = k.get('dtype') or default_dtype()   # fp32 (reference precision) unless opted into bf16
 
             def forward(s, x):
                 # gfx950 persistent-recurrence BiLSTM kernels on GPU (rafiki_amd.ops.lstm)
-                h = bilstm(s.drop(s.emb(x)), s.lstm)
+                h = bilstm(s.drop(s.emb(x)), s.lstm, dtype=s.rec_dtype)
                 return s.out(h)
 
         return Net().to(self.device)

@@ -7,7 +7,9 @@ bidirectional=True)`` over a padded batch, zero initial state).  Split of the wo
   plain GEMM (hipBLASLt through torch), as are the three weight/input-gradient GEMMs of the
   backward — they have no time dependence;
 * the sequential part (T steps of ``h @ W_hh^T`` + the cell) is ONE kernel launch per direction
-  pair, forward and backward (``rk_lstm_fwd`` / ``rk_lstm_bwd``).
+  pair, forward and backward: ``rk_lstm_fwd32`` / ``rk_lstm_bwd32`` (exact fp32 on
+  v_mfma_f32_16x16x4_f32, the reference's precision, default) or ``rk_lstm_fwd`` / ``rk_lstm_bwd``
+  (bf16 W_hh and h operands, fp32 cell state and accumulation; opt-in with ``dtype='bf16'``).
 
 Hidden sizes are zero-padded per gate block to HP in {64, 128}; padded units stay exactly zero,
 so the result equals the unpadded LSTM.  On CPU (or hidden > 128) ``bilstm`` runs torch's LSTM.
@@ -33,37 +35,45 @@ def _pad_gate_rows(w: torch.Tensor, H: int, HP: int) -> torch.Tensor:
 
 
 class BiLstmFn(torch.autograd.Function):
-    """x [T, B, E] fp32, w_ih [2, 4H, E], w_hh [2, 4H, H], b [2, 4H] (b_ih + b_hh) -> [T, B, 2H]."""
+    """x [T, B, E] fp32, w_ih [2, 4H, E], w_hh [2, 4H, H], b [2, 4H] (b_ih + b_hh) -> [T, B, 2H].
+    ``dtype`` picks the recurrence kernels: 'fp32' (default) or 'bf16'."""
 
     @staticmethod
-    def forward(ctx, x, w_ih, w_hh, b):
+    def forward(ctx, x, w_ih, w_hh, b, dtype='fp32'):
         T, B, E = x.shape
         H = w_hh.shape[-1]
         HP = _hp(H)
         w_ih_p = _pad_gate_rows(w_ih.detach().float(), H, HP)                          # [2, 4HP, E]
         w_hh_p = torch.zeros((2, 4 * HP, HP), device=x.device, dtype=torch.float32)
         w_hh_p[:, :, :H] = _pad_gate_rows(w_hh.detach().float(), H, HP)
-        w_hh_b = w_hh_p.to(torch.bfloat16).contiguous()
+        f32 = dtype != 'bf16'
+        # fp32: W_hh as is for the forward, W_hh^T [2, HP, 4HP] for the BPTT (float4 along k)
+        w_rec = w_hh_p.contiguous() if f32 else w_hh_p.to(torch.bfloat16).contiguous()
         b_p = _pad_gate_rows(b.detach().float(), H, HP)                                  # [2, 4HP]
         x2 = x.detach().float().reshape(T * B, E)
         gin = torch.addmm(b_p.reshape(1, -1), x2, w_ih_p.reshape(2 * 4 * HP, E).t()).contiguous()
         hout = torch.empty((T, B, 2, HP), device=x.device, dtype=torch.float32)
         gsave = torch.empty((T, B, 2, 4 * HP), device=x.device, dtype=torch.float32)
         csave = torch.empty((T, B, 2, HP), device=x.device, dtype=torch.float32)
-        _lib.call("rk_lstm_fwd", _p(gin), _p(w_hh_b), T, B, HP, _p(hout), _p(gsave), _p(csave), _s())
-        ctx.save_for_backward(x2, w_ih_p, w_hh_b, hout, gsave, csave)
+        _lib.call("rk_lstm_fwd32" if f32 else "rk_lstm_fwd", _p(gin), _p(w_rec), T, B, HP, _p(hout), _p(gsave),
+                  _p(csave), _s())
+        if f32:
+            w_rec = w_hh_p.transpose(1, 2).contiguous()
+        ctx.save_for_backward(x2, w_ih_p, w_rec, hout, gsave, csave)
         ctx.dims = (T, B, E, H, HP)
+        ctx.f32 = f32
         return hout[..., :H].reshape(T, B, 2 * H)
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, gy):
-        x2, w_ih_p, w_hh_b, hout, gsave, csave = ctx.saved_tensors
+        x2, w_ih_p, w_rec, hout, gsave, csave = ctx.saved_tensors
         T, B, E, H, HP = ctx.dims
         dh = torch.zeros((T, B, 2, HP), device=gy.device, dtype=torch.float32)
         dh[..., :H] = gy.reshape(T, B, 2, H)
         dg = torch.empty((T, B, 2, 4 * HP), device=gy.device, dtype=torch.float32)
-        _lib.call("rk_lstm_bwd", _p(w_hh_b), T, B, HP, _p(dh), _p(gsave), _p(csave), _p(dg), _s())
+        _lib.call("rk_lstm_bwd32" if ctx.f32 else "rk_lstm_bwd", _p(w_rec), T, B, HP, _p(dh), _p(gsave), _p(csave),
+                  _p(dg), _s())
         dg2 = dg.reshape(T * B, 2 * 4 * HP)
         gx = gw_ih = gw_hh = gb = None
         if ctx.needs_input_grad[0]:
@@ -80,10 +90,10 @@ class BiLstmFn(torch.autograd.Function):
             gw_hh = gw.reshape(2, 4, HP, HP)[:, :, :H, :H].reshape(2, 4 * H, H)
         if ctx.needs_input_grad[3]:
             gb = dg.sum((0, 1)).reshape(2, 4, HP)[:, :, :H].reshape(2, 4 * H)
-        return gx, gw_ih, gw_hh, gb
+        return gx, gw_ih, gw_hh, gb, None
 
 
-def bilstm(x, lstm: torch.nn.LSTM):
+def bilstm(x, lstm: torch.nn.LSTM, dtype='fp32'):
     """Run a 1-layer bidirectional ``nn.LSTM`` (batch_first) on the gfx950 kernels; returns
     [B, T, 2H] like ``lstm(x)[0]``.  CPU tensors and hidden > 128 use torch's own LSTM."""
     H = lstm.hidden_size
@@ -92,5 +102,5 @@ def bilstm(x, lstm: torch.nn.LSTM):
     w_ih = torch.stack([lstm.weight_ih_l0, lstm.weight_ih_l0_reverse])
     w_hh = torch.stack([lstm.weight_hh_l0, lstm.weight_hh_l0_reverse])
     b = torch.stack([lstm.bias_ih_l0 + lstm.bias_hh_l0, lstm.bias_ih_l0_reverse + lstm.bias_hh_l0_reverse])
-    y = BiLstmFn.apply(x.transpose(0, 1).contiguous(), w_ih, w_hh, b)
+    y = BiLstmFn.apply(x.transpose(0, 1).contiguous(), w_ih, w_hh, b, dtype)
     return y.transpose(0, 1)

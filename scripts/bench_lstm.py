@@ -24,7 +24,9 @@ def main():
         x = torch.randn(B, T, E, device='cuda', requires_grad=True)
         gy = torch.randn(B, T, 2 * H, device='cuda')
         row = {'B': B, 'T': T, 'E': E, 'H': H}
-        for name, fn in (('rafiki_hip', lambda: bilstm(x, lstm)), ('torch_miopen', lambda: lstm(x)[0])):
+        for name, fn in (('rafiki_hip_fp32', lambda: bilstm(x, lstm, dtype='fp32')),
+                         ('rafiki_hip_bf16', lambda: bilstm(x, lstm, dtype='bf16')),
+                         ('torch_miopen', lambda: lstm(x)[0])):
             for _ in range(3):
                 (fn() * gy).sum().backward()
             torch.cuda.synchronize()
@@ -33,7 +35,8 @@ def main():
                 (fn() * gy).sum().backward()
             torch.cuda.synchronize()
             row[name + '_ms'] = round((time.perf_counter() - t0) * 1e3 / a.reps, 3)
-        row['speedup'] = round(row['torch_miopen_ms'] / row['rafiki_hip_ms'], 2)
+        row['speedup_fp32'] = round(row['torch_miopen_ms'] / row['rafiki_hip_fp32_ms'], 2)
+        row['speedup_bf16'] = round(row['torch_miopen_ms'] / row['rafiki_hip_bf16_ms'], 2)
         res['cases'].append(row)
     print(json.dumps(res))
 
