@@ -151,7 +151,8 @@ def _tune_locked(key, candidates, run):
         try:
             with open(log, 'a') as f:
                 f.write(json.dumps({'key': [str(k) for k in key], 'best': list(best), 'us': round(best_t * 1e3, 2),
-                                    'first_us': round(times.get(candidates[0], float('inf')) * 1e3, 2)}) + '\n')
+                                    'first_us': round(times.get(candidates[0], float('inf')) * 1e3, 2),
+                                    'all': {str(list(c)): round(t * 1e3, 2) for c, t in times.items()}}) + '\n')
         except OSError:
             pass
     with _lock:
