@@ -1,0 +1,380 @@
+// Winograd F(2x2, 3x3) fp32 convolution for gfx950: stride 1, pad 1, NHWC, even H and W, C % 8 == 0.
+//
+// A 3x3 conv needs 9 MACs per output pixel and channel pair; F(2x2,3x3) needs 16 per 2x2 output tile,
+// i.e. 4 — 2.25x fewer v_mfma_f32_16x16x4_f32 cycles on exactly the same fp32 data type (all
+// transforms are fp32 adds / halvings).  The whole transform-GEMM-transform chain is fused in one
+// kernel, so the 4x larger transformed tensors never touch HBM:
+//   * weights: U = G g G^T, [16][Cout][Cin] (channel-contiguous), transformed once per weight
+//     update by rk_wino_weights, which also emits the flipped / transposed set of the data gradient
+//     (dgrad = forward conv of dy with flip(w)^T, whose transform is a transpose of U with the
+//     Winograd positions 0 <-> 3 swapped in both dimensions, since G J = P G);
+//   * workgroup = 8 waves, block tile = 64 output tiles (2x2 px each: 256 pixels) x 64 output
+//     channels; the K loop walks Cin in chunks of 8 through a 2-stage LDS ring (64 + 64 KiB):
+//     every thread loads one (tile, channel) 4x4 input window (raw buffer loads at fixed offsets,
+//     zeros outside the image via the buffer range check), applies B^T d B in registers and writes
+//     the 16 transformed values to LDS, and 4 float4 of U; the next chunk's global loads are in
+//     flight while the current chunk's MFMAs run; LDS column pairs are XOR-swizzled per row so
+//     the 64-bit fragment reads are bank-conflict-free;
+//   * wave (wm, wn) owns tiles 16 wm .. 16 wm + 15 and channels 32 wn .. 32 wn + 31 for ALL 16
+//     Winograd positions (32 16x16 accumulators, 128 fp32 registers), so the output transform
+//     A^T M A is lane-local — no cross-wave reduction — and each lane ends up holding whole 2x2
+//     output tiles of one channel;
+//   * K order inside a chunk is permuted (lane group q supplies channels 2q, 2q+1 over the two MFMA
+//     steps) so A and B fragments are single ds_read_b64s of contiguous LDS;
+//   * epilogues as in the direct kernels (csrc/kernels/sgemm.hip): bias, ReLU, BN statistics
+//     (fp64 slot atomics), and for the data gradient FLAG_BNB / FLAG_BNP (ReLU mask + BN-backward
+//     sums of the BN+ReLU(+2x2 max-pool) layer below).
+#include "common.h"
+
+namespace {
+
+constexpr int WT = 64;    // output tiles per block
+constexpr int WN = 64;    // output channels per block
+constexpr int WKC = 8;    // input channels per K chunk
+enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_BNB = 512, WF_BNP = 1024 };
+
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+struct WgParams {
+  const float* x;       // NHWC [Nb][H][W][C]
+  const float* u;       // [16][N][C]
+  float* y;             // NHWC [Nb][H][W][N]
+  const float* bias;    // [N] bias; BNB / BNP: BN scale [N] then shift [N] of the gated layer
+  double* stats;        // fp64 slots [slotMask+1][2][N]
+  const float* gate;    // BNB: BN input y of the gated layer [Nb][H][W][N]; BNP: at [Nb][2H][2W][N]
+  int Nb, H, W, C, N;
+  int TW, THW, ntiles, ncb, slotMask, flags;
+  unsigned long long xbytes, ubytes, ybytes;
+};
+
+constexpr unsigned WOOB = 0x80000000u;
+
+// LDS rows hold 8 channels (4 column pairs); row r stores column pair c at c ^ ((r >> 2) & 3): the 16
+// rows x one pair of a ds_read2st64_b64 lane group (banks mod 32) and the 16 rows x two pairs of a
+// ds_read_b64 group (banks mod 64) then hit distinct banks
+RK_DEV int w_swz(int row) { return ((row >> 2) & 3) << 1; }
+
+RK_DEV __amdgpu_buffer_rsrc_t w_rsrc(const float* base, unsigned long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)(unsigned)bytes, 0x00020000);
+}
+
+// tile t -> (image, 2x2 tile origin)
+RK_DEV void w_tile(const WgParams& p, int t, int& n, int& oy, int& ox) {
+  n = t / p.THW;
+  const int r = t - n * p.THW;
+  const int ty = r / p.TW;
+  oy = 2 * ty;
+  ox = 2 * (r - ty * p.TW);
+}
+
+__global__ __launch_bounds__(512) void wino_fwd_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) float Vs[2][16][WT][WKC];
+  __shared__ __attribute__((aligned(16))) float Us[2][16][WN][WKC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 3, wn = w >> 2;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = b % p.ncb, tb = b / p.ncb;
+  const int tbase = tb * WT, cbase = cb * WN;
+
+  // loader role: one (tile, channel) input window + 4 float4 of U per thread and chunk, as raw buffer
+  // loads whose byte offsets are fixed for the whole K loop (the chunk advances the descriptors'
+  // base in SGPRs); window pixels outside the image carry an offset past the buffer -> zeros
+  const int lt = tid >> 3, lc = tid & 7;
+  int ln, loy, lox;
+  w_tile(p, tbase + lt, ln, loy, lox);
+  const bool lok = tbase + lt < p.ntiles;
+  unsigned xo[16];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int yy = loy - 1 + a, xx = lox - 1 + bb;
+      const bool ok = lok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+      xo[a * 4 + bb] = ok ? (unsigned)((((ln * p.H + yy) * p.W + xx) * p.C + lc) * 4) : WOOB;
+    }
+  unsigned uo[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int f = tid + 512 * k;            // float4 index in [16][64][2]
+    const int pos = f >> 7, co = (f >> 1) & 63, half = f & 1;
+    uo[k] = cbase + co < p.N ? (unsigned)(((pos * p.N + cbase + co) * p.C + half * 4) * 4) : WOOB;
+  }
+  const int vsw = w_swz(lt);
+
+  float raw[16];
+  f32x4 ur[4];
+  auto load = [&](int c0) {
+    const __amdgpu_buffer_rsrc_t xr = w_rsrc(p.x + c0, p.xbytes - 4ull * c0);
+    const __amdgpu_buffer_rsrc_t urs = w_rsrc(p.u + c0, p.ubytes - 4ull * c0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      raw[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)xo[i], 0, 0));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ur[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, (int)uo[k], 0, 0));
+  };
+  auto store = [&](int st) {
+    float t[16];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {       // B^T d: rows
+      t[0 * 4 + bb] = raw[0 * 4 + bb] - raw[2 * 4 + bb];
+      t[1 * 4 + bb] = raw[1 * 4 + bb] + raw[2 * 4 + bb];
+      t[2 * 4 + bb] = raw[2 * 4 + bb] - raw[1 * 4 + bb];
+      t[3 * 4 + bb] = raw[1 * 4 + bb] - raw[3 * 4 + bb];
+    }
+    const int c = lc ^ vsw;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {          // (B^T d) B: columns
+      Vs[st][a * 4 + 0][lt][c] = t[a * 4 + 0] - t[a * 4 + 2];
+      Vs[st][a * 4 + 1][lt][c] = t[a * 4 + 1] + t[a * 4 + 2];
+      Vs[st][a * 4 + 2][lt][c] = t[a * 4 + 2] - t[a * 4 + 1];
+      Vs[st][a * 4 + 3][lt][c] = t[a * 4 + 1] - t[a * 4 + 3];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int f = tid + 512 * k, co = (f >> 1) & 63, c0 = (f & 1) * 4, sw = w_swz(co);
+      *(f32x2*)&Us[st][f >> 7][co][c0 ^ sw] = f32x2{ur[k][0], ur[k][1]};
+      *(f32x2*)&Us[st][f >> 7][co][(c0 + 2) ^ sw] = f32x2{ur[k][2], ur[k][3]};
+    }
+  };
+
+  f32x4 acc[16][2];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q][0] = acc[q][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = p.C / WKC;
+  load(0);
+  store(0);
+  __syncthreads();
+  const int ar = wm * 16 + (lane & 15), br = wn * 32 + (lane & 15);
+  const int ka = (2 * (lane >> 4)) ^ w_swz(ar), kb = (2 * (lane >> 4)) ^ w_swz(br);
+  for (int c = 0; c < nch; ++c) {
+    const int st = c & 1;
+    if (c + 1 < nch) load((c + 1) * WKC);
+    // two positions at a time: 4 independent MFMAs between dependent ones (32-cycle issue, ~40 latency)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      f32x2 a[2], bv[2][2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        a[e] = *(const f32x2*)&Vs[st][q + e][ar][ka];
+        bv[e][0] = *(const f32x2*)&Us[st][q + e][br][kb];
+        bv[e][1] = *(const f32x2*)&Us[st][q + e][br + 16][kb];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+            acc[q + e][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][nb][s], acc[q + e][nb], 0, 0, 0);
+    }
+    if (c + 1 < nch) store(st ^ 1);
+    __syncthreads();
+  }
+
+  // ---- output transform + epilogue: lane owns channels n0, n0 + 16 of 4 consecutive tiles; 32-bit
+  // element indices (the host checks the sizes), one tile decode per lane
+  const int fl = p.flags;
+  const bool sums = fl & (WF_STATS | WF_BNB | WF_BNP);
+  int nn[2];
+  bool nok[2];
+  float bs[2], sh[2], s[2], ss[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    nn[nb] = cbase + wn * 32 + nb * 16 + (lane & 15);
+    nok[nb] = nn[nb] < p.N;
+    bs[nb] = ((fl & (WF_BIAS | WF_BNB | WF_BNP)) && nok[nb]) ? p.bias[nn[nb]] : 0.f;
+    sh[nb] = ((fl & (WF_BNB | WF_BNP)) && nok[nb]) ? p.bias[p.N + nn[nb]] : 0.f;
+    s[nb] = ss[nb] = 0.f;
+  }
+  const int t0 = tbase + wm * 16 + (lane >> 4) * 4;
+  int im, oy, ox;
+  w_tile(p, t0, im, oy, ox);
+  const __amdgpu_buffer_rsrc_t yr = w_rsrc(p.y, p.ybytes);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool tok = t0 + r < p.ntiles;
+    const int pix = (im * p.H + oy) * p.W + ox;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      float tt[4][2];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {        // M A: columns
+        const f32x4 m0 = acc[a * 4 + 0][nb], m1 = acc[a * 4 + 1][nb], m2 = acc[a * 4 + 2][nb], m3 = acc[a * 4 + 3][nb];
+        tt[a][0] = m0[r] + m1[r] + m2[r];
+        tt[a][1] = m1[r] - m2[r] - m3[r];
+      }
+      if (!(tok && nok[nb])) continue;
+      const int n = nn[nb];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          // A^T (M A): rows
+          float v = i == 0 ? tt[0][j] + tt[1][j] + tt[2][j] : tt[1][j] - tt[2][j] - tt[3][j];
+          const int idx = (pix + i * p.W + j) * p.N + n;
+          if (fl & WF_BIAS) v += bs[nb];
+          if (fl & WF_STATS) {
+            s[nb] += v;
+            ss[nb] += v * v;
+          }
+          if (fl & WF_RELU) v = fmaxf(v, 0.f);
+          if (fl & WF_BNB) {
+            const float g = p.gate[idx];
+            v = g * bs[nb] + sh[nb] > 0.f ? v : 0.f;
+            s[nb] += v;
+            ss[nb] += v * g;
+          }
+          if (fl & WF_BNP) {
+            // pooled pixel (im, oy+i, ox+j) of an H x W map; its 2x2 window sits at 2H x 2W
+            const int W2 = 2 * p.W;
+            const int b0 = ((im * 2 * p.H + 2 * (oy + i)) * W2 + 2 * (ox + j)) * p.N + n;
+            const float y4[4] = {p.gate[b0], p.gate[b0 + p.N], p.gate[b0 + W2 * p.N], p.gate[b0 + W2 * p.N + p.N]};
+            float best = -INFINITY, zb = 0.f, yb = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // first maximal relu(z) of the window (torch max_pool2d rule)
+              const float z = y4[e] * bs[nb] + sh[nb];
+              const float av = fmaxf(z, 0.f);
+              if (av > best) { best = av; zb = z; yb = y4[e]; }
+            }
+            const float dz = zb > 0.f ? v : 0.f;
+            s[nb] += dz;
+            ss[nb] += dz * yb;
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), yr, idx * 4, 0, 0);
+        }
+    }
+    ox += 2;                               // next tile: (im, oy, ox) in row-major tile order
+    if (ox >= p.W) {
+      ox = 0;
+      oy += 2;
+      if (oy >= p.H) {
+        oy = 0;
+        ++im;
+      }
+    }
+  }
+  if (sums) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      float a = s[nb], b2 = ss[nb];
+      a += __shfl_xor(a, 16, 64);
+      b2 += __shfl_xor(b2, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b2 += __shfl_xor(b2, 32, 64);
+      if (nok[nb] && lane < 32) {
+        double* slot = p.stats + (long long)(blockIdx.x & p.slotMask) * 2 * p.N;
+        unsafeAtomicAdd(slot + (lane >= 16 ? p.N : 0) + nn[nb], (double)(lane >= 16 ? b2 : a));
+      }
+    }
+  }
+}
+
+// U = G g G^T of every (co, ci) 3x3 filter g = w[co][ky*3+kx][ci]: u[pos][co][ci]; optionally the
+// data-gradient set ut[pos][ci][co] = U[p(pos)][co][ci] with p swapping positions 0 and 3 per axis.
+// Block = 32 co x 32 ci filters staged through LDS (coalesced both ways).
+RK_DEV void w_transform(const float (&g)[9], float (&U)[16]) {
+  float t[4][3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const float g0 = g[kx], g1 = g[3 + kx], g2 = g[6 + kx];
+    t[0][kx] = g0;
+    t[1][kx] = 0.5f * (g0 + g1 + g2);
+    t[2][kx] = 0.5f * (g0 - g1 + g2);
+    t[3][kx] = g2;
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    U[a * 4 + 0] = t[a][0];
+    U[a * 4 + 1] = 0.5f * (t[a][0] + t[a][1] + t[a][2]);
+    U[a * 4 + 2] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
+    U[a * 4 + 3] = t[a][2];
+  }
+}
+
+__global__ __launch_bounds__(256) void wino_wt_kernel(const float* __restrict__ w, float* __restrict__ u,
+                                                      float* __restrict__ ut, int Co, int Ci) {
+  __shared__ float g[32][9][33];
+  const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+  float st[36];   // all loads in flight before the first LDS store
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    const int ci = i & 31, t = (i >> 5) % 9, co = i / (9 * 32);
+    st[k] = (co0 + co < Co && ci0 + ci < Ci) ? w[((long long)(co0 + co) * 9 + t) * Ci + ci0 + ci] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    g[i / (9 * 32)][(i >> 5) % 9][i & 31] = st[k];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    const int ci = i & 31, co = i >> 5;
+    if (co0 + co >= Co || ci0 + ci >= Ci) continue;
+    float gg[9], U[16];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
+    w_transform(gg, U);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u[((long long)q * Co + co0 + co) * Ci + ci0 + ci] = U[q];
+  }
+  if (ut == nullptr) return;
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    const int co = i & 31, ci = i >> 5;
+    if (co0 + co >= Co || ci0 + ci >= Ci) continue;
+    float gg[9], U[16];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
+    w_transform(gg, U);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int a = q >> 2, bq = q & 3;
+      const int pa = a == 0 ? 3 : a == 3 ? 0 : a, pb = bq == 0 ? 3 : bq == 3 ? 0 : bq;
+      ut[((long long)q * Ci + ci0 + ci) * Co + co0 + co] = U[pa * 4 + pb];
+    }
+  }
+}
+
+}  // namespace
+
+// Winograd-domain weights of a 3x3 conv w [Co][9][Ci]: u [16][Co][Ci], ut (nullable) [16][Ci][Co]
+extern "C" int rk_wino_weights(const float* w, float* u, float* ut, int Co, int Ci, void* stream) {
+  if (Co <= 0 || Ci <= 0) return RK_EBADARG;
+  const dim3 grid(rk_cdiv(Ci, 32), rk_cdiv(Co, 32));
+  hipLaunchKernelGGL(wino_wt_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, u, ut, Co, Ci);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// y = conv3x3(x, w) via F(2x2,3x3) with u = rk_wino_weights(w); flags WF_* (BNB/BNP: ``gate`` and the
+// scale/shift pair in ``bias``; BNP: H x W is the pooled map and gate is at 2H x 2W)
+extern "C" int rk_wino_conv(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
+                            const float* gate, int Nb, int H, int W, int C, int N, int flags, void* stream) {
+  if (Nb <= 0 || (H & 1) || (W & 1) || H <= 0 || W <= 0 || C <= 0 || (C % WKC) || N <= 0) return RK_EBADARG;
+  if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
+  if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
+  if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
+  WgParams p;
+  p.x = x; p.u = u; p.y = y; p.bias = bias; p.stats = stats; p.gate = gate;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.N = N;
+  p.TW = W / 2;
+  p.THW = (H / 2) * (W / 2);
+  const long long nt = (long long)Nb * p.THW;
+  if (nt >= (1LL << 30)) return RK_EBADARG;
+  p.ntiles = (int)nt;
+  p.ncb = rk_cdiv(N, WN);
+  // raw-buffer byte offsets are 32-bit with 0x80000000 as the out-of-range marker
+  p.xbytes = 4ull * Nb * H * W * C;
+  p.ubytes = 64ull * N * C;
+  p.ybytes = 4ull * Nb * H * W * N;
+  const unsigned long long gbytes = (flags & WF_BNP) ? 4 * p.ybytes : p.ybytes;
+  if (p.xbytes >= 0x7fffffffull || p.ubytes >= 0x7fffffffull || gbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
+  p.slotMask = slotMask;
+  p.flags = flags;
+  const long long blocks = (long long)rk_cdiv(p.ntiles, WT) * p.ncb;
+  if (blocks >= (1LL << 31)) return RK_EBADARG;
+  hipLaunchKernelGGL(wino_fwd_kernel, dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}

@@ -264,6 +264,87 @@ class SConvWT:
         return self.buf[off:off + Cin * self.taps * Cout].view(Cin, self.taps * Cout)
 
 
+# -------------------------------------------------------------------- Winograd F(2x2, 3x3) convs
+WF_RELU, WF_BIAS, WF_STATS, WF_BNB, WF_BNP = 1, 2, 4, 512, 1024
+WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
+WINO_CFG = (-1, 0, 1)   # the autotune candidate that runs rk_wino_conv
+
+
+def wino_ok(H: int, W: int, C: int) -> bool:
+    """Shapes the fused Winograd kernel takes: stride-1 3x3, even maps, C % 8 == 0."""
+    return WINO and H % 2 == 0 and W % 2 == 0 and C % 8 == 0 and C > 0
+
+
+def wino_weights(w: torch.Tensor, u: torch.Tensor, ut: Optional[torch.Tensor] = None):
+    """u [16][Cout][Cin] = G g G^T of w [Cout][9*Cin]; ut [16][Cin][Cout]: the data-gradient set."""
+    Cout = w.shape[0]
+    Cin = w.numel() // (9 * Cout)
+    assert u.numel() == 16 * Cout * Cin and (ut is None or ut.numel() == 16 * Cout * Cin)
+    _lib.call("rk_wino_weights", _p(w), _p(u), _p(ut), Cout, Cin, _s())
+    return u, ut
+
+
+def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None, bnp=None):
+    """y = conv3x3(x, w) (stride 1, pad 1) from u = wino_weights(w): x [Nb, H, W, C] fp32 NHWC.
+    ``stats``: fp64 BN slots (sum y, sum y^2); ``bnb`` / ``bnp`` = (y, coeffs, acc) as in conv_dgrad."""
+    _check(x, 'wino_conv x')
+    Nb, H, W, C = x.shape
+    N = u.shape[1]
+    assert u.shape == (16, N, C) and u.is_contiguous(), (u.shape, x.shape)
+    if out is None:
+        out = torch.empty((Nb, H, W, N), device=x.device, dtype=torch.float32)
+    assert out.shape == (Nb, H, W, N) and out.is_contiguous()
+    flags, gate = 0, None
+    if bias is not None:
+        flags |= WF_BIAS
+    if relu:
+        flags |= WF_RELU
+    if stats is not None:
+        flags |= WF_STATS
+    if bnb is not None:
+        gate, coeffs, stats = bnb
+        assert gate.shape == out.shape
+        bias, flags = coeffs[2:4].reshape(-1), WF_BNB
+    elif bnp is not None:
+        gate, coeffs, stats = bnp
+        assert gate.shape == (Nb, 2 * H, 2 * W, N)
+        bias, flags = coeffs[2:4].reshape(-1), WF_BNP
+    if stats is not None:
+        assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
+    _lib.call("rk_wino_conv", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
+              Nb, H, W, C, N, flags, _s())
+    return out
+
+
+class WinoWeights:
+    """Winograd-domain weights of several 3x3 convs in one buffer, refreshed once per weight update:
+    u_l [16][Cout][Cin] for the forward conv and (dgrad=True) ut_l [16][Cin][Cout] for the data
+    gradient (a forward conv of dy)."""
+
+    def __init__(self, weights, dgrad=True):
+        self.weights = list(weights)
+        self.dgrad = dgrad
+        self._off, off = [], 0
+        for w in self.weights:
+            n = 16 * w.numel() // 9
+            self._off.append((off, n, w.shape[0], w.numel() // (9 * w.shape[0])))
+            off += n * (2 if dgrad else 1)
+        dev = self.weights[0].device if self.weights else 'cpu'
+        self.buf = torch.zeros(max(off, 1), dtype=torch.float32, device=dev)
+
+    def refresh(self):
+        for l, w in enumerate(self.weights):
+            wino_weights(w, self.u(l), self.ut(l) if self.dgrad else None)
+
+    def u(self, l):
+        off, n, Cout, Cin = self._off[l]
+        return self.buf[off:off + n].view(16, Cout, Cin)
+
+    def ut(self, l):
+        off, n, Cout, Cin = self._off[l]
+        return self.buf[off + n:off + 2 * n].view(16, Cin, Cout)
+
+
 # ----------------------------------------------------------------------------------------- dense
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0.2, out=None, alpha=1.0):
     """out = act(alpha * x @ w.T + bias), fp32; small-M layers autotune split-K + a fused combine."""

@@ -1,0 +1,120 @@
+"""Fused Winograd F(2x2,3x3) fp32 conv (csrc/kernels/winograd.hip) vs fp64 PyTorch references.
+
+F(2x2,3x3) adds a few fp32 roundings in the input / output transforms (values up to 4x the inputs),
+measured ~1e-7 relative; the gate is the same 1e-5 relative Frobenius error as the direct kernels."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _rand(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).float()
+
+
+def _conv_ref(x_nhwc, w_ohwi):
+    return TF.conv2d(x_nhwc.double().permute(0, 3, 1, 2), w_ohwi.double().permute(0, 3, 1, 2),
+                     padding=1).permute(0, 2, 3, 1)
+
+
+def _u(w):
+    from rafiki_amd.ops import f32 as S
+    Cout, Cin = w.shape[0], w.shape[-1]
+    u = torch.empty((16, Cout, Cin), device=DEV)
+    ut = torch.empty((16, Cin, Cout), device=DEV)
+    S.wino_weights(w.to(DEV).reshape(Cout, -1).contiguous(), u, ut)
+    return u, ut
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [
+    (2, 8, 8, 16, 32), (3, 6, 10, 24, 40), (4, 32, 32, 64, 64), (8, 4, 4, 512, 512), (2, 2, 2, 8, 72),
+    (5, 16, 16, 128, 128), (1, 12, 20, 8, 8)])
+def test_wino_fwd_and_stats(N, H, W, Cin, Cout):
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=1)
+    w = _rand(Cout, 3, 3, Cin, seed=2, scale=1.0 / math.sqrt(9 * Cin))
+    u, _ = _u(w)
+    acc = torch.zeros((S.bn_slots(Cout), 2, Cout), dtype=torch.float64, device=DEV)
+    y = S.wino_conv(x.to(DEV), u, stats=acc)
+    torch.cuda.synchronize()
+    ref = _conv_ref(x, w)
+    assert rel(y, ref) < 1e-5
+    s = acc.sum(0).cpu()
+    r = ref.reshape(-1, Cout)
+    assert rel(s[0], r.sum(0)) < 1e-5 and rel(s[1], (r * r).sum(0)) < 1e-5
+
+
+def test_wino_bias_relu():
+    from rafiki_amd.ops import f32 as S
+    x = _rand(3, 8, 8, 32, seed=3)
+    w = _rand(48, 3, 3, 32, seed=4, scale=0.1)
+    b = _rand(48, seed=5)
+    u, _ = _u(w)
+    y = S.wino_conv(x.to(DEV), u, bias=b.to(DEV), relu=True)
+    torch.cuda.synchronize()
+    assert rel(y, torch.relu(_conv_ref(x, w) + b.double())) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 16, 16, 64, 64), (8, 4, 4, 512, 256),
+                                            (2, 6, 6, 24, 16)])
+def test_wino_dgrad_from_transposed_set(N, H, W, Cin, Cout):
+    """dx = conv(dy, flip(w)^T) from the ut set (transpose of u with positions 0 <-> 3 swapped)."""
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=6)
+    w = _rand(Cout, 3, 3, Cin, seed=7, scale=0.1)
+    dy = _rand(N, H, W, Cout, seed=8)
+    _, ut = _u(w)
+    dx = S.wino_conv(dy.to(DEV), ut)
+    torch.cuda.synchronize()
+    xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    out = TF.conv2d(xd, w.double().permute(0, 3, 1, 2), padding=1)
+    (gx,) = torch.autograd.grad(out, xd, dy.double().permute(0, 3, 1, 2))
+    assert rel(dx, gx.permute(0, 2, 3, 1)) < 1e-5
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_wino_dgrad_bn_epilogues_match_direct(pool):
+    """The BNB / BNP epilogues (ReLU mask / pool routing + BN-backward sums of the layer below) give
+    the same dx and sums as the direct kernel's."""
+    from rafiki_amd.ops import f32 as S
+    N, H, W, Cin, Cout = 4, 8, 8, 64, 128
+    Hy, Wy = (2 * H, 2 * W) if pool else (H, W)
+    y = _rand(N, Hy, Wy, Cin, seed=17) + 0.2
+    gamma, beta = torch.ones(Cin) * 1.3, _rand(Cin, seed=18) * 0.1
+    acc = torch.zeros((S.bn_slots(Cin), 2, Cin), dtype=torch.float64, device=DEV)
+    S.col_stats(y.to(DEV).view(-1, Cin), acc)
+    _, coeffs = S.bn_fwd(y.to(DEV), acc, N * Hy * Wy, gamma.to(DEV), beta.to(DEV), 1e-5, pool=pool, act=1)
+    w = _rand(Cout, 3, 3, Cin, seed=19, scale=0.05)
+    arena = w.reshape(-1).to(DEV).contiguous()
+    wt = S.SConvWT(arena, [arena.view(Cout, 3, 3, Cin)])
+    wt.refresh()
+    _, ut = _u(w)
+    dyo = _rand(N, H, W, Cout, seed=20).to(DEV)
+    acc_w, acc_d = torch.zeros_like(acc), torch.zeros_like(acc)
+    key = 'bnp' if pool else 'bnb'
+    d_w = S.wino_conv(dyo, ut, **{key: (y.to(DEV), coeffs, acc_w)})
+    d_d = S.conv_dgrad(dyo, wt.view(0), **{key: (y.to(DEV), coeffs, acc_d)})
+    torch.cuda.synchronize()
+    assert rel(d_w, d_d) < 1e-5
+    assert rel(acc_w.sum(0), acc_d.sum(0)) < 1e-5
+
+
+def test_wino_weights_arena_refresh():
+    from rafiki_amd.ops import f32 as S
+    ws = [_rand(64, 3, 3, 32, seed=21).to(DEV).reshape(64, -1).contiguous(),
+          _rand(16, 3, 3, 64, seed=22).to(DEV).reshape(16, -1).contiguous()]
+    ww = S.WinoWeights(ws)
+    ww.refresh()
+    for l, w in enumerate(ws):
+        u, ut = _u(w.view(w.shape[0], 3, 3, -1).cpu())
+        assert torch.equal(ww.u(l), u) and torch.equal(ww.ut(l), ut)
