@@ -8,9 +8,10 @@
 //     update by rk_wino_weights, which also emits the flipped / transposed set of the data gradient
 //     (dgrad = forward conv of dy with flip(w)^T, whose transform is a transpose of U with the
 //     Winograd positions 0 <-> 3 swapped in both dimensions, since G J = P G);
-//   * workgroup = 8 waves, block tile = 64 output tiles (2x2 px each: 256 pixels) x 64 output
-//     channels; the K loop walks Cin in chunks of 8 through a 2-stage LDS ring (64 + 64 KiB):
-//     every thread loads one (tile, channel) 4x4 input window (raw buffer loads at fixed offsets,
+//   * block tile = 64 output tiles (2x2 px each: 256 pixels) x 32 output channels on 4 waves (one
+//     48 KiB LDS stage, two workgroups per CU) or x 64 channels on 8 waves (2-stage 128 KiB ring),
+//     picked per layer by the autotuner; the K loop walks Cin in chunks of 8: every thread loads its
+//     (tile, channel) 4x4 input windows (raw buffer loads at fixed offsets,
 //     zeros outside the image via the buffer range check), applies B^T d B in registers and writes
 //     the 16 transformed values to LDS, and 4 float4 of U; the next chunk's global loads are in
 //     flight while the current chunk's MFMAs run; LDS column pairs are XOR-swizzled per row so
@@ -29,7 +30,6 @@
 namespace {
 
 constexpr int WT = 64;    // output tiles per block
-constexpr int WN = 64;    // output channels per block
 constexpr int WKC = 8;    // input channels per K chunk
 enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_BNB = 512, WF_BNP = 1024 };
 
@@ -67,73 +67,94 @@ RK_DEV void w_tile(const WgParams& p, int t, int& n, int& oy, int& ox) {
   ox = 2 * (r - ty * p.TW);
 }
 
-__global__ __launch_bounds__(512) void wino_fwd_kernel(const WgParams p) {
-  __shared__ __attribute__((aligned(16))) float Vs[2][16][WT][WKC];
-  __shared__ __attribute__((aligned(16))) float Us[2][16][WN][WKC];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w & 3, wn = w >> 2;
+// NWN = 1: 4 waves, 64 tiles x 32 channels, one 48 KiB LDS stage, two workgroups per CU (small
+// grids, overlapping epilogues); NWN = 2: 8 waves, 64 x 64, a 2-stage 128 KiB ring (one barrier per
+// chunk, V loaded once for 64 channels).  The autotuner picks per layer.
+template <int NWN>
+__global__ __launch_bounds__(256 * NWN, 3 - NWN) void wino_fwd_kernel(const WgParams p) {
+  constexpr int NT = 256 * NWN;            // threads
+  constexpr int BNC = 32 * NWN;            // output channels per block
+  constexpr int NSTG = NWN == 2 ? 2 : 1;   // LDS stages
+  constexpr int IT = 2 / NWN;              // input windows per thread and chunk
+  __shared__ __attribute__((aligned(16))) float Vs[NSTG][16][WT][WKC];
+  __shared__ __attribute__((aligned(16))) float Us[NSTG][16][BNC][WKC];
+  const int tid = threadIdx.x, lane = tid & 63, wm = (tid >> 6) & 3, wn = tid >> 8;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int cb = b % p.ncb, tb = b / p.ncb;
-  const int tbase = tb * WT, cbase = cb * WN;
+  const int tbase = tb * WT, cbase = cb * BNC;
 
-  // loader role: one (tile, channel) input window + 4 float4 of U per thread and chunk, as raw buffer
-  // loads whose byte offsets are fixed for the whole K loop (the chunk advances the descriptors'
-  // base in SGPRs); window pixels outside the image carry an offset past the buffer -> zeros
+  // loader role per thread and chunk: the (tile, channel) 4x4 input windows of tiles lt + NT/8 * h
+  // and 4 float4 of U, as raw buffer loads whose byte offsets are fixed for the whole K loop (the
+  // chunk advances the descriptors' base in SGPRs); window pixels outside the image carry an
+  // offset past the buffer -> zeros
   const int lt = tid >> 3, lc = tid & 7;
-  int ln, loy, lox;
-  w_tile(p, tbase + lt, ln, loy, lox);
-  const bool lok = tbase + lt < p.ntiles;
-  unsigned xo[16];
+  // per window: byte offset of its centre pixel (1, 1) and a 16-bit in-image mask; pixel (a, bb)
+  // sits at a wave-uniform delta from the centre
+  unsigned vb[IT], vm[IT];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int h = 0; h < IT; ++h) {
+    int ln, loy, lox;
+    w_tile(p, tbase + lt + NT / 8 * h, ln, loy, lox);
+    const bool lok = tbase + lt + NT / 8 * h < p.ntiles;
+    vb[h] = lok ? (unsigned)((((ln * p.H + loy) * p.W + lox) * p.C + lc) * 4) : 0u;
+    vm[h] = 0;
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      const int yy = loy - 1 + a, xx = lox - 1 + bb;
-      const bool ok = lok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
-      xo[a * 4 + bb] = ok ? (unsigned)((((ln * p.H + yy) * p.W + xx) * p.C + lc) * 4) : WOOB;
-    }
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int yy = loy - 1 + a, xx = lox - 1 + bb;
+        if (lok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) vm[h] |= 1u << (a * 4 + bb);
+      }
+  }
   unsigned uo[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int f = tid + 512 * k;            // float4 index in [16][64][2]
-    const int pos = f >> 7, co = (f >> 1) & 63, half = f & 1;
+    const int f = tid + NT * k;             // float4 index in [16][BNC][2]
+    const int pos = f / (2 * BNC), co = (f >> 1) & (BNC - 1), half = f & 1;
     uo[k] = cbase + co < p.N ? (unsigned)(((pos * p.N + cbase + co) * p.C + half * 4) * 4) : WOOB;
   }
-  const int vsw = w_swz(lt);
 
-  float raw[16];
+  float raw[IT][16];
   f32x4 ur[4];
   auto load = [&](int c0) {
     const __amdgpu_buffer_rsrc_t xr = w_rsrc(p.x + c0, p.xbytes - 4ull * c0);
     const __amdgpu_buffer_rsrc_t urs = w_rsrc(p.u + c0, p.ubytes - 4ull * c0);
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      raw[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)xo[i], 0, 0));
+    for (int h = 0; h < IT; ++h)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int d = (((i >> 2) - 1) * p.W + (i & 3) - 1) * p.C * 4;
+        const unsigned off = ((vm[h] >> i) & 1u) ? vb[h] + (unsigned)d : WOOB;
+        raw[h][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, 0, 0));
+      }
 #pragma unroll
     for (int k = 0; k < 4; ++k) ur[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, (int)uo[k], 0, 0));
   };
   auto store = [&](int st) {
-    float t[16];
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {       // B^T d: rows
-      t[0 * 4 + bb] = raw[0 * 4 + bb] - raw[2 * 4 + bb];
-      t[1 * 4 + bb] = raw[1 * 4 + bb] + raw[2 * 4 + bb];
-      t[2 * 4 + bb] = raw[2 * 4 + bb] - raw[1 * 4 + bb];
-      t[3 * 4 + bb] = raw[1 * 4 + bb] - raw[3 * 4 + bb];
-    }
-    const int c = lc ^ vsw;
+    for (int h = 0; h < IT; ++h) {
+      const int row = lt + NT / 8 * h, c = lc ^ w_swz(row);
+      float t[16];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {          // (B^T d) B: columns
-      Vs[st][a * 4 + 0][lt][c] = t[a * 4 + 0] - t[a * 4 + 2];
-      Vs[st][a * 4 + 1][lt][c] = t[a * 4 + 1] + t[a * 4 + 2];
-      Vs[st][a * 4 + 2][lt][c] = t[a * 4 + 2] - t[a * 4 + 1];
-      Vs[st][a * 4 + 3][lt][c] = t[a * 4 + 1] - t[a * 4 + 3];
+      for (int bb = 0; bb < 4; ++bb) {     // B^T d: rows
+        t[0 * 4 + bb] = raw[h][0 * 4 + bb] - raw[h][2 * 4 + bb];
+        t[1 * 4 + bb] = raw[h][1 * 4 + bb] + raw[h][2 * 4 + bb];
+        t[2 * 4 + bb] = raw[h][2 * 4 + bb] - raw[h][1 * 4 + bb];
+        t[3 * 4 + bb] = raw[h][1 * 4 + bb] - raw[h][3 * 4 + bb];
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {        // (B^T d) B: columns
+        Vs[st][a * 4 + 0][row][c] = t[a * 4 + 0] - t[a * 4 + 2];
+        Vs[st][a * 4 + 1][row][c] = t[a * 4 + 1] + t[a * 4 + 2];
+        Vs[st][a * 4 + 2][row][c] = t[a * 4 + 2] - t[a * 4 + 1];
+        Vs[st][a * 4 + 3][row][c] = t[a * 4 + 1] - t[a * 4 + 3];
+      }
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int f = tid + 512 * k, co = (f >> 1) & 63, c0 = (f & 1) * 4, sw = w_swz(co);
-      *(f32x2*)&Us[st][f >> 7][co][c0 ^ sw] = f32x2{ur[k][0], ur[k][1]};
-      *(f32x2*)&Us[st][f >> 7][co][(c0 + 2) ^ sw] = f32x2{ur[k][2], ur[k][3]};
+      const int f = tid + NT * k, pos = f / (2 * BNC), co = (f >> 1) & (BNC - 1), c0 = (f & 1) * 4, sw = w_swz(co);
+      *(f32x2*)&Us[st][pos][co][c0 ^ sw] = f32x2{ur[k][0], ur[k][1]};
+      *(f32x2*)&Us[st][pos][co][(c0 + 2) ^ sw] = f32x2{ur[k][2], ur[k][3]};
     }
   };
 
@@ -148,7 +169,7 @@ __global__ __launch_bounds__(512) void wino_fwd_kernel(const WgParams p) {
   const int ar = wm * 16 + (lane & 15), br = wn * 32 + (lane & 15);
   const int ka = (2 * (lane >> 4)) ^ w_swz(ar), kb = (2 * (lane >> 4)) ^ w_swz(br);
   for (int c = 0; c < nch; ++c) {
-    const int st = c & 1;
+    const int st = NSTG == 2 ? (c & 1) : 0;
     if (c + 1 < nch) load((c + 1) * WKC);
     // two positions at a time: 4 independent MFMAs between dependent ones (32-cycle issue, ~40 latency)
 #pragma unroll
@@ -168,7 +189,12 @@ __global__ __launch_bounds__(512) void wino_fwd_kernel(const WgParams p) {
           for (int nb = 0; nb < 2; ++nb)
             acc[q + e][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][nb][s], acc[q + e][nb], 0, 0, 0);
     }
-    if (c + 1 < nch) store(st ^ 1);
+    if constexpr (NSTG == 2) {             // the other stage is free: one barrier per chunk
+      if (c + 1 < nch) store(st ^ 1);
+    } else if (c + 1 < nch) {              // one stage: wait for every wave's reads first
+      __syncthreads();
+      store(0);
+    }
     __syncthreads();
   }
 
@@ -292,10 +318,9 @@ RK_DEV void w_transform(const float (&g)[9], float (&U)[16]) {
   }
 }
 
-__global__ __launch_bounds__(256) void wino_wt_kernel(const float* __restrict__ w, float* __restrict__ u,
-                                                      float* __restrict__ ut, int Co, int Ci) {
-  __shared__ float g[32][9][33];
-  const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+// one 32 co x 32 ci block of filters: LDS-staged so both output layouts are written coalesced
+RK_DEV void wt_block(const float* __restrict__ w, float* __restrict__ u, float* __restrict__ ut, int Co, int Ci,
+                     int co0, int ci0, float (&g)[32][9][33]) {
   float st[36];   // all loads in flight before the first LDS store
 #pragma unroll
   for (int k = 0; k < 36; ++k) {
@@ -336,6 +361,23 @@ __global__ __launch_bounds__(256) void wino_wt_kernel(const float* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(256) void wino_wt_kernel(const float* __restrict__ w, float* __restrict__ u,
+                                                      float* __restrict__ ut, int Co, int Ci) {
+  __shared__ float g[32][9][33];
+  wt_block(w, u, ut, Co, Ci, blockIdx.y * 32, blockIdx.x * 32, g);
+}
+
+// every layer of a network in one launch: desc[block] = (layer, co0, ci0, -); meta[layer] = (weight
+// offset in the arena, u offset, ut offset or -1, Co, Ci) in floats
+__global__ __launch_bounds__(256) void wino_wt_multi_kernel(const float* __restrict__ arena, float* __restrict__ dst,
+                                                            const int4* __restrict__ desc,
+                                                            const long long* __restrict__ meta) {
+  __shared__ float g[32][9][33];
+  const int4 d = desc[blockIdx.x];
+  const long long* m = meta + 5 * d.x;
+  wt_block(arena + m[0], dst + m[1], m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4], d.y, d.z, g);
+}
+
 }  // namespace
 
 // Winograd-domain weights of a 3x3 conv w [Co][9][Ci]: u [16][Co][Ci], ut (nullable) [16][Ci][Co]
@@ -347,10 +389,22 @@ extern "C" int rk_wino_weights(const float* w, float* u, float* ut, int Co, int 
   return RK_OK;
 }
 
+extern "C" int rk_wino_weights_multi(const float* arena, float* dst, const int* desc, int nblocks, const long long* meta,
+                                     void* stream) {
+  if (nblocks <= 0) return RK_OK;
+  hipLaunchKernelGGL(wino_wt_multi_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, arena, dst,
+                     (const int4*)desc, meta);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
 // y = conv3x3(x, w) via F(2x2,3x3) with u = rk_wino_weights(w); flags WF_* (BNB/BNP: ``gate`` and the
 // scale/shift pair in ``bias``; BNP: H x W is the pooled map and gate is at 2H x 2W)
 extern "C" int rk_wino_conv(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
-                            const float* gate, int Nb, int H, int W, int C, int N, int flags, void* stream) {
+                            const float* gate, int Nb, int H, int W, int C, int N, int flags, int variant,
+                            void* stream) {
+  if (variant != 0 && variant != 1) return RK_EBADARG;
+  const int BNC = variant ? 64 : 32;
   if (Nb <= 0 || (H & 1) || (W & 1) || H <= 0 || W <= 0 || C <= 0 || (C % WKC) || N <= 0) return RK_EBADARG;
   if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
   if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
@@ -363,7 +417,7 @@ extern "C" int rk_wino_conv(const float* x, const float* u, float* y, const floa
   const long long nt = (long long)Nb * p.THW;
   if (nt >= (1LL << 30)) return RK_EBADARG;
   p.ntiles = (int)nt;
-  p.ncb = rk_cdiv(N, WN);
+  p.ncb = rk_cdiv(N, BNC);
   // raw-buffer byte offsets are 32-bit with 0x80000000 as the out-of-range marker
   p.xbytes = 4ull * Nb * H * W * C;
   p.ubytes = 64ull * N * C;
@@ -374,7 +428,10 @@ extern "C" int rk_wino_conv(const float* x, const float* u, float* y, const floa
   p.flags = flags;
   const long long blocks = (long long)rk_cdiv(p.ntiles, WT) * p.ncb;
   if (blocks >= (1LL << 31)) return RK_EBADARG;
-  hipLaunchKernelGGL(wino_fwd_kernel, dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
+  if (variant)
+    hipLaunchKernelGGL(wino_fwd_kernel<2>, dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(wino_fwd_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -370,10 +370,14 @@ class ConvNetEngine:
         accs = self._bn_accumulators()
         if not self._acc_zeroed_by_prologue:
             self._bn_acc_flat.zero_()  # one memset node for every layer's fp64 statistic slots
+        ww = self._wino_train()
+        if ww is not None:
+            ww.refresh()   # one launch: Winograd-domain weights (forward + data-gradient sets) of blocks 1..
         acts, saved, h = [x], [], x
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             rm, rv = self.running_stats(bi)
-            y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0])
+            y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0],
+                           wino=ww.u(bi - 1) if ww is not None and bi > 0 else None)
             h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
                                  self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
             saved.append((y, coeffs))
@@ -430,17 +434,29 @@ class ConvNetEngine:
                 break
             py, pco = saved[bi - 1]
             pname, pcin, pcout, ppool, phw = self.blocks[bi - 1]
+            wu = ww.ut(bi - 1) if ww is not None else None
             if not ppool:
                 # the input block is BN+ReLU: its mask and BN-backward sums ride in this dgrad's epilogue
-                d = S.conv_dgrad(dy, wt.view(bi - 1), bnb=(py, pco, accs[bi - 1][1]))
+                d = S.conv_dgrad(dy, wt.view(bi - 1), bnb=(py, pco, accs[bi - 1][1]), wino=wu)
                 reduced = True
             elif phw == 2 * hw and not (hw & (hw - 1)):
                 # BN+ReLU+max-pool input (even power-of-two geometry): pool routing + sums in the epilogue
-                d = S.conv_dgrad(dy, wt.view(bi - 1), bnp=(py, pco, accs[bi - 1][1]))
+                d = S.conv_dgrad(dy, wt.view(bi - 1), bnp=(py, pco, accs[bi - 1][1]), wino=wu)
                 reduced = True
             else:
-                d = S.conv_dgrad(dy, wt.view(bi - 1))
+                d = S.conv_dgrad(dy, wt.view(bi - 1), wino=wu)
                 reduced = False
+
+    def _wino_train(self):
+        """WinoWeights over blocks 1.. (fp32 path): the fused F(2x2,3x3) kernel becomes an autotune
+        candidate of every forward / data-gradient conv it fits (RAFIKI_WINOGRAD=0 turns it off)."""
+        if not (self.f32 and S.WINO and len(self.blocks) > 1 and self.device.type == 'cuda'):
+            return None
+        ww = getattr(self, '_ww', None)
+        if ww is None:
+            fl = self.flat
+            ww = self._ww = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]])
+        return ww
 
     def _conv_wt(self):
         """ConvWT over the weights of blocks 1.. (block 0 has no data gradient), built once."""
@@ -725,6 +741,10 @@ class ConvNetEngine:
             coeffs.append(c)
         self._eval_coeffs = coeffs
         self._eval_graphs = {}
+        self._eval_wino = None
+        if self.f32 and S.WINO and len(self.blocks) > 1 and self.device.type == 'cuda':
+            self._eval_wino = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]], dgrad=False)
+            self._eval_wino.refresh()
         return coeffs
 
     @torch.no_grad()
@@ -732,8 +752,9 @@ class ConvNetEngine:
         fl = self.flat
         h = x
         B = x.shape[0]
+        ew = getattr(self, '_eval_wino', None)
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
-            y = S.conv_fwd(h, fl.w(name + '.w'))
+            y = S.conv_fwd(h, fl.w(name + '.w'), wino=ew.u(bi - 1) if ew is not None and bi > 0 else None)
             c = self._eval_coeffs[bi]
             h = S.bn_eval(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
         if self.input_bn:
@@ -817,13 +838,15 @@ class ConvNetEngine:
         return so[:B]
 
     def resident_bytes(self):
-        return self.flat.total * (4 + (0 if self.f32 else 2) + 4) + self.running.numel() * 4
+        ew = getattr(self, '_eval_wino', None)
+        extra = ew.buf.numel() * 4 if ew is not None else 0
+        return self.flat.total * (4 + (0 if self.f32 else 2) + 4) + self.running.numel() * 4 + extra
 
     def release_training(self):
         """Drop what only training needs — the captured step graphs (and with them their private
         activation pools), static batch buffers, the step schedule and the optimizer state — so a
         finished trial can stay resident in HBM for serving at its inference footprint."""
-        for a in ('_graph', '_sched_graph', '_static_x', '_static_y', '_sched', '_ctr'):
+        for a in ('_graph', '_sched_graph', '_static_x', '_static_y', '_sched', '_ctr', '_ww', '_wt'):
             if hasattr(self, a):
                 setattr(self, a, None)
         self.opt = None

@@ -132,9 +132,11 @@ def _slots_flags(acc):
 
 # ------------------------------------------------------------------------------------------ conv
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None, bias=None, act=ACT_NONE,
-             slope=0.2, out=None):
+             slope=0.2, out=None, wino=None):
     """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
-    [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue."""
+    [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue.
+    ``wino``: the layer's Winograd weights (WinoWeights.u) -> the fused F(2x2,3x3) kernel is one more
+    autotune candidate."""
     _check(x, 'conv_fwd x')
     Nb, H, W, Cin = x.shape
     Cout = w.shape[0]
@@ -145,8 +147,13 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     flags = (F_STATS if stats_acc is not None else 0) | (F_BIAS if bias is not None else 0)
     flags |= F_RELU if act == ACT_RELU else F_LRELU if act == ACT_LRELU else 0
 
+    use_w = wino is not None and taps == 9 and wino_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
+
     def run(cfg):
         tile, nst, s = cfg
+        if cfg in WINO_CFGS:
+            wino_conv(x, wino, out=out, bias=bias, stats=stats_acc, relu=act == ACT_RELU, variant=-1 - cfg[0])
+            return
         if s == 1:
             sgemm(KIND_CONV, x, w, out, M, Cout, K, Cin, K, Cout, tile=tile, nst=nst, bias=bias, stats=stats_acc,
                   H=H, W=W, C=Cin, taps=taps, flags=flags, slope=slope)
@@ -158,14 +165,17 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
               H=H, W=W, C=Cin, taps=taps)
         sreduce_epi(slab, M, Cout, out.view(M, Cout), bias=bias, act=act, slope=slope)
     cands = _cands(M, Cout, splittable=stats_acc is None and Cout % 4 == 0, K=K, big=Cin % 32 == 0)
-    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags), cands, run)
+    if use_w:
+        cands.extend(WINO_CFGS)
+    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, use_w), cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
     return out
 
 
-def conv_dgrad(dy: torch.Tensor, wt: torch.Tensor, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None):
+def conv_dgrad(dy: torch.Tensor, wt: torch.Tensor, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None,
+               wino=None):
     """dx = data gradient of a 3x3 conv as conv3x3(dy, wt) with wt = SConvWT.view() [Cin][taps*Cout].
     Epilogue options: ``gate`` (ReLU mask of the input activation), ``bnb = (y, coeffs, acc)`` (the input
     is BN+ReLU(y): mask + BN-backward sums into acc), ``bnp = (y, coeffs, acc)`` (the input is
@@ -189,11 +199,19 @@ def conv_dgrad(dy: torch.Tensor, wt: torch.Tensor, *, taps: int = 9, out=None, g
         gate, bias, flags = y, coeffs[2:4].reshape(-1), F_BNP
     elif gate is not None:
         flags = F_GATE
+    # ``wino``: the layer's Winograd data-gradient weights (WinoWeights.ut), one more candidate
+    use_w = wino is not None and taps == 9 and wino_ok(H, W, Cout) and not (flags & F_GATE)
 
     def run(cfg):
+        if cfg in WINO_CFGS:
+            wino_conv(dy, wino, out=out, bnb=bnb, bnp=bnp, variant=-1 - cfg[0])
+            return
         sgemm(KIND_CONV, dy, wt, out, M, Cin, K, Cout, K, Cin, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats,
               gate=gate, H=H, W=W, C=Cout, taps=taps, flags=flags)
-    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags), _cands(M, Cin, big=Cout % 32 == 0), run)
+    cands = _cands(M, Cin, big=Cout % 32 == 0)
+    if use_w:
+        cands.extend(WINO_CFGS)
+    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, use_w), cands, run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -267,7 +285,8 @@ class SConvWT:
 # -------------------------------------------------------------------- Winograd F(2x2, 3x3) convs
 WF_RELU, WF_BIAS, WF_STATS, WF_BNB, WF_BNP = 1, 2, 4, 512, 1024
 WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
-WINO_CFG = (-1, 0, 1)   # the autotune candidate that runs rk_wino_conv
+# autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1)
+WINO_CFGS = ((-1, 0, 1), (-2, 0, 1))
 
 
 def wino_ok(H: int, W: int, C: int) -> bool:
@@ -284,7 +303,8 @@ def wino_weights(w: torch.Tensor, u: torch.Tensor, ut: Optional[torch.Tensor] = 
     return u, ut
 
 
-def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None, bnp=None):
+def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None, bnp=None,
+              variant=0):
     """y = conv3x3(x, w) (stride 1, pad 1) from u = wino_weights(w): x [Nb, H, W, C] fp32 NHWC.
     ``stats``: fp64 BN slots (sum y, sum y^2); ``bnb`` / ``bnp`` = (y, coeffs, acc) as in conv_dgrad."""
     _check(x, 'wino_conv x')
@@ -312,29 +332,41 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
     if stats is not None:
         assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
     _lib.call("rk_wino_conv", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
-              Nb, H, W, C, N, flags, _s())
+              Nb, H, W, C, N, flags, int(variant), _s())
     return out
 
 
 class WinoWeights:
-    """Winograd-domain weights of several 3x3 convs in one buffer, refreshed once per weight update:
-    u_l [16][Cout][Cin] for the forward conv and (dgrad=True) ut_l [16][Cin][Cout] for the data
-    gradient (a forward conv of dy)."""
+    """Winograd-domain weights of several 3x3 convs whose fp32 weights live in one arena, refreshed by
+    ONE launch per weight update: u_l [16][Cout][Cin] for the forward conv and (dgrad=True) ut_l
+    [16][Cin][Cout] for the data gradient (a forward conv of dy)."""
 
-    def __init__(self, weights, dgrad=True):
+    def __init__(self, arena: torch.Tensor, weights, dgrad=True):
+        self.arena = arena
         self.weights = list(weights)
         self.dgrad = dgrad
-        self._off, off = [], 0
-        for w in self.weights:
-            n = 16 * w.numel() // 9
-            self._off.append((off, n, w.shape[0], w.numel() // (9 * w.shape[0])))
+        self._off, meta, desc, off = [], [], [], 0
+        for l, w in enumerate(self.weights):
+            Cout = w.shape[0]
+            Cin = w.numel() // (9 * Cout)
+            n = 16 * Cout * Cin
+            so = (w.data_ptr() - arena.data_ptr()) // 4
+            assert 0 <= so and so + w.numel() <= arena.numel() and w.is_contiguous()
+            self._off.append((off, n, Cout, Cin))
+            meta.append([so, off, off + n if dgrad else -1, Cout, Cin])
+            for co0 in range(0, Cout, 32):
+                for ci0 in range(0, Cin, 32):
+                    desc.append([l, co0, ci0, 0])
             off += n * (2 if dgrad else 1)
-        dev = self.weights[0].device if self.weights else 'cpu'
+        dev = arena.device
         self.buf = torch.zeros(max(off, 1), dtype=torch.float32, device=dev)
+        self.meta = torch.tensor(meta, dtype=torch.int64, device=dev).reshape(-1)
+        self.desc = torch.tensor(desc, dtype=torch.int32, device=dev).reshape(-1)
+        self.nblocks = len(desc)
 
     def refresh(self):
-        for l, w in enumerate(self.weights):
-            wino_weights(w, self.u(l), self.ut(l) if self.dgrad else None)
+        _lib.call("rk_wino_weights_multi", _p(self.arena), _p(self.buf), _p(self.desc), self.nblocks, _p(self.meta),
+                  _s())
 
     def u(self, l):
         off, n, Cout, Cin = self._off[l]
@@ -342,6 +374,7 @@ class WinoWeights:
 
     def ut(self, l):
         off, n, Cout, Cin = self._off[l]
+        assert self.dgrad
         return self.buf[off + n:off + 2 * n].view(16, Cin, Cout)
 
 

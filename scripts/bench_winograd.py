@@ -19,10 +19,12 @@ for (N, H, C, K) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128),
         for _ in range(reps): fn()
         e.record(); e.synchronize()
         return s.elapsed_time(e) / reps * 1e3
-    tw = t(lambda: S.wino_conv(x, u, stats=acc))
+    tw0 = t(lambda: S.wino_conv(x, u, stats=acc, variant=0))
+    tw1 = t(lambda: S.wino_conv(x, u, stats=acc, variant=1))
+    tw = min(tw0, tw1)
     td = t(lambda: S.conv_fwd(x, w.view(K, 3, 3, C), stats_acc=acc))
     tt = t(lambda: S.wino_weights(w, u, ut))
     fl = 2.0 * N * H * H * K * 9 * C
-    res.append(dict(N=N, H=H, C=C, K=K, wino_us=round(tw, 1), direct_us=round(td, 1), wt_us=round(tt, 1),
+    res.append(dict(N=N, H=H, C=C, K=K, wino4_us=round(tw0, 1), wino8_us=round(tw1, 1), direct_us=round(td, 1), wt_us=round(tt, 1),
                     speedup=round(td / tw, 2), wino_eff_tflops=round(fl / tw / 1e6, 1)))
     print(json.dumps(res[-1]), flush=True)

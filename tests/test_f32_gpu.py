@@ -215,10 +215,17 @@ def test_engine_grads_match_fp64_reference():
     _grad_check(eng, x, y, 1e-4)
 
 
-def test_engine_grads_vgg_small_full_width():
+@pytest.mark.parametrize("wino", [False, True])
+def test_engine_grads_vgg_small_full_width(wino, monkeypatch):
+    """Direct convs: 1e-4 (or 2x torch fp32).  With the fused Winograd convs as autotune candidates
+    the conv outputs are as accurate (scripts/wino_error.py: 2.6e-7..7.4e-7 vs fp64, direct
+    4.2e-7..5.9e-7) but round differently from torch, so a ReLU-boundary sign in the 4x4 layers can
+    flip where torch's does not — one flipped element moves a BN dgamma by ~1e-4 relative: gate 1e-3."""
+    from rafiki_amd.ops import f32 as S
+    monkeypatch.setattr(S, 'WINO', wino)
     eng = _engine(image_size=32, cfg=(64, 64, 'M', 128, 128, 'M', 256, 256, 'M', 512, 512, 'M'), fc_dims=(512,))
     x, y = _batch(32, hw=32, seed=1)
-    _grad_check(eng, x, y, 1e-4)
+    _grad_check(eng, x, y, 1e-3 if wino else 1e-4)
 
 
 def test_engine_grads_non_pow2_and_odd_pool():

@@ -39,13 +39,14 @@ def _u(w):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [
     (2, 8, 8, 16, 32), (3, 6, 10, 24, 40), (4, 32, 32, 64, 64), (8, 4, 4, 512, 512), (2, 2, 2, 8, 72),
     (5, 16, 16, 128, 128), (1, 12, 20, 8, 8)])
-def test_wino_fwd_and_stats(N, H, W, Cin, Cout):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino_fwd_and_stats(N, H, W, Cin, Cout, variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=1)
     w = _rand(Cout, 3, 3, Cin, seed=2, scale=1.0 / math.sqrt(9 * Cin))
     u, _ = _u(w)
     acc = torch.zeros((S.bn_slots(Cout), 2, Cout), dtype=torch.float64, device=DEV)
-    y = S.wino_conv(x.to(DEV), u, stats=acc)
+    y = S.wino_conv(x.to(DEV), u, stats=acc, variant=variant)
     torch.cuda.synchronize()
     ref = _conv_ref(x, w)
     assert rel(y, ref) < 1e-5
@@ -67,14 +68,15 @@ def test_wino_bias_relu():
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 16, 16, 64, 64), (8, 4, 4, 512, 256),
                                             (2, 6, 6, 24, 16)])
-def test_wino_dgrad_from_transposed_set(N, H, W, Cin, Cout):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino_dgrad_from_transposed_set(N, H, W, Cin, Cout, variant):
     """dx = conv(dy, flip(w)^T) from the ut set (transpose of u with positions 0 <-> 3 swapped)."""
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=6)
     w = _rand(Cout, 3, 3, Cin, seed=7, scale=0.1)
     dy = _rand(N, H, W, Cout, seed=8)
     _, ut = _u(w)
-    dx = S.wino_conv(dy.to(DEV), ut)
+    dx = S.wino_conv(dy.to(DEV), ut, variant=variant)
     torch.cuda.synchronize()
     xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
     out = TF.conv2d(xd, w.double().permute(0, 3, 1, 2), padding=1)
@@ -83,11 +85,13 @@ def test_wino_dgrad_from_transposed_set(N, H, W, Cin, Cout):
 
 
 @pytest.mark.parametrize("pool", [False, True])
-def test_wino_dgrad_bn_epilogues_match_direct(pool):
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("H", [8, 4])
+def test_wino_dgrad_bn_epilogues_match_direct(pool, variant, H):
     """The BNB / BNP epilogues (ReLU mask / pool routing + BN-backward sums of the layer below) give
     the same dx and sums as the direct kernel's."""
     from rafiki_amd.ops import f32 as S
-    N, H, W, Cin, Cout = 4, 8, 8, 64, 128
+    N, W, Cin, Cout = 4, H, 64, 128
     Hy, Wy = (2 * H, 2 * W) if pool else (H, W)
     y = _rand(N, Hy, Wy, Cin, seed=17) + 0.2
     gamma, beta = torch.ones(Cin) * 1.3, _rand(Cin, seed=18) * 0.1
@@ -102,7 +106,7 @@ def test_wino_dgrad_bn_epilogues_match_direct(pool):
     dyo = _rand(N, H, W, Cout, seed=20).to(DEV)
     acc_w, acc_d = torch.zeros_like(acc), torch.zeros_like(acc)
     key = 'bnp' if pool else 'bnb'
-    d_w = S.wino_conv(dyo, ut, **{key: (y.to(DEV), coeffs, acc_w)})
+    d_w = S.wino_conv(dyo, ut, variant=variant, **{key: (y.to(DEV), coeffs, acc_w)})
     d_d = S.conv_dgrad(dyo, wt.view(0), **{key: (y.to(DEV), coeffs, acc_d)})
     torch.cuda.synchronize()
     assert rel(d_w, d_d) < 1e-5
@@ -111,9 +115,15 @@ def test_wino_dgrad_bn_epilogues_match_direct(pool):
 
 def test_wino_weights_arena_refresh():
     from rafiki_amd.ops import f32 as S
-    ws = [_rand(64, 3, 3, 32, seed=21).to(DEV).reshape(64, -1).contiguous(),
-          _rand(16, 3, 3, 64, seed=22).to(DEV).reshape(16, -1).contiguous()]
-    ww = S.WinoWeights(ws)
+    shapes = [(64, 32), (16, 64), (40, 24)]
+    arena = torch.zeros(sum(co * 9 * ci for co, ci in shapes) + 7, device=DEV)
+    ws, off = [], 3
+    for k, (co, ci) in enumerate(shapes):
+        w = arena[off:off + co * 9 * ci].view(co, 9 * ci)
+        w.copy_(_rand(co, 9 * ci, seed=21 + k))
+        ws.append(w)
+        off += co * 9 * ci
+    ww = S.WinoWeights(arena, ws)
     ww.refresh()
     for l, w in enumerate(ws):
         u, ut = _u(w.view(w.shape[0], 3, 3, -1).cpu())
