@@ -296,6 +296,176 @@ __global__ __launch_bounds__(256 * NWN, 3 - NWN) void wino_fwd_kernel(const WgPa
   }
 }
 
+// ------------------------------------------------------------------------- weight gradient
+// dW = sum over 2x2 output tiles of G^T [ (A dY A^T) (.) (B^T d B) ] G: per Winograd position a GEMM
+// dU[pos][co][ci] = sum_t Mdy[pos][t][co] * V[pos][t][ci] with the reduction over tiles, 2.25x fewer
+// MFMA cycles than the direct weight gradient.  Block = 8 waves, 64 co x 64 ci x 16 positions
+// (wave (wm, wn): 16 co x 32 ci); the tile range is split over gridDim (split-K) and each block
+// applies G^T . G in registers, so it writes plain dW taps [Co][9][Ci] (slab per split, summed by
+// rk_reduce_slabs).  Every thread transforms one (tile, co) 2x2 output-gradient patch and one
+// (tile, ci) 4x4 input window per chunk of 8 tiles.
+struct WwParams {
+  const float* dy;      // NHWC [Nb][H][W][Co]
+  const float* x;       // NHWC [Nb][H][W][Ci]
+  float* out;           // [splits][Co][9][Ci]
+  int Nb, H, W, Co, Ci;
+  int TW, THW, ntiles, tps, nco, nci, accumulate;
+  float invTW, invTHW;
+  unsigned long long dybytes, xbytes;
+  long long slab;       // floats per split
+};
+
+__global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
+  __shared__ __attribute__((aligned(16))) float Ms[2][16][64][WKC];   // [stage][pos][co][tile]
+  __shared__ __attribute__((aligned(16))) float Vs[2][16][64][WKC];   // [stage][pos][ci][tile]
+  const int tid = threadIdx.x, lane = tid & 63, wm = (tid >> 6) & 3, wn = tid >> 8;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = p.nco * p.nci;
+  const int split = b / per, r0 = b - split * per;
+  const int co0 = (r0 / p.nci) * 64, ci0 = (r0 % p.nci) * 64;
+  const int t_begin = split * p.tps;
+  const int t_end = min(t_begin + p.tps, p.ntiles);
+  const int nch = (t_end - t_begin + WKC - 1) / WKC;
+  const int tt = tid & 7, ch = tid >> 3;   // tile within the chunk, channel within the block
+  const bool cok = co0 + ch < p.Co, iok = ci0 + ch < p.Ci;
+  const __amdgpu_buffer_rsrc_t dyr = w_rsrc(p.dy, p.dybytes), xr = w_rsrc(p.x, p.xbytes);
+
+  float gy[4], raw[16];
+  auto load = [&](int c) {
+    const int t = t_begin + c * WKC + tt;
+    // branch-free validity: (tile in range) x (channel in range) x (window row / column in image)
+    const unsigned okm = (t < t_end ? 1u : 0u);
+    // tile -> (n, oy, ox) by fp32 reciprocals (exact below 2^22 tiles)
+    const int n = (int)(((float)t + 0.5f) * p.invTHW);
+    const int rr = t - n * p.THW;
+    const int ty = (int)(((float)rr + 0.5f) * p.invTW);
+    const int oy = 2 * ty, ox = 2 * (rr - ty * p.TW);
+    const int pix = (n * p.H + oy) * p.W + ox;
+    const unsigned gm = okm & (cok ? 1u : 0u);
+    const unsigned ob = (unsigned)((pix * p.Co + co0 + ch) * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // invalid -> bit 31 set: past any buffer (a select here makes hipcc branch around the loads)
+      const unsigned off = (ob + (unsigned)((((i >> 1) * p.W) + (i & 1)) * p.Co * 4)) | ((gm ^ 1u) << 31);
+      gy[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dyr, (int)off, 0, 0));
+    }
+    // rows / columns 1, 2 of a window are always inside an even-sized map; 0 and 3 at the borders
+    const unsigned xm = okm & (iok ? 1u : 0u);
+    const unsigned rm = (xm * 6u) | ((oy > 0 ? xm : 0u) << 0) | ((oy + 2 < p.H ? xm : 0u) << 3);
+    const unsigned cm = 6u | ((ox > 0 ? 1u : 0u) << 0) | ((ox + 2 < p.W ? 1u : 0u) << 3);
+    const unsigned xb = (unsigned)((pix * p.Ci + ci0 + ch) * 4);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int a = i >> 2, bb = i & 3;
+      const unsigned in = (rm >> a) & (cm >> bb) & 1u;
+      const unsigned off = (xb + (unsigned)((((a - 1) * p.W) + bb - 1) * p.Ci * 4)) | ((in ^ 1u) << 31);
+      raw[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, 0, 0));
+    }
+  };
+  auto store = [&](int st) {
+    const int c = tt ^ w_swz(ch);
+    // A dY A^T (4x4 from 2x2): rows (y0, y0 + y1, y0 - y1, -y1), then the same on columns
+    float rw[4][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      rw[0][j] = gy[j];
+      rw[1][j] = gy[j] + gy[2 + j];
+      rw[2][j] = gy[j] - gy[2 + j];
+      rw[3][j] = -gy[2 + j];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      Ms[st][a * 4 + 0][ch][c] = rw[a][0];
+      Ms[st][a * 4 + 1][ch][c] = rw[a][0] + rw[a][1];
+      Ms[st][a * 4 + 2][ch][c] = rw[a][0] - rw[a][1];
+      Ms[st][a * 4 + 3][ch][c] = -rw[a][1];
+    }
+    float t[16];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {       // B^T d: rows
+      t[0 * 4 + bb] = raw[0 * 4 + bb] - raw[2 * 4 + bb];
+      t[1 * 4 + bb] = raw[1 * 4 + bb] + raw[2 * 4 + bb];
+      t[2 * 4 + bb] = raw[2 * 4 + bb] - raw[1 * 4 + bb];
+      t[3 * 4 + bb] = raw[1 * 4 + bb] - raw[3 * 4 + bb];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {          // (B^T d) B: columns
+      Vs[st][a * 4 + 0][ch][c] = t[a * 4 + 0] - t[a * 4 + 2];
+      Vs[st][a * 4 + 1][ch][c] = t[a * 4 + 1] + t[a * 4 + 2];
+      Vs[st][a * 4 + 2][ch][c] = t[a * 4 + 2] - t[a * 4 + 1];
+      Vs[st][a * 4 + 3][ch][c] = t[a * 4 + 1] - t[a * 4 + 3];
+    }
+  };
+
+  f32x4 acc[16][2];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q][0] = acc[q][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nch > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  const int ar = wm * 16 + (lane & 15), br = wn * 32 + (lane & 15);
+  const int ka = (2 * (lane >> 4)) ^ w_swz(ar), kb = (2 * (lane >> 4)) ^ w_swz(br);
+  for (int c = 0; c < nch; ++c) {
+    const int st = c & 1;
+    if (c + 1 < nch) load(c + 1);
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      f32x2 a[2], bv[2][2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        a[e] = *(const f32x2*)&Ms[st][q + e][ar][ka];
+        bv[e][0] = *(const f32x2*)&Vs[st][q + e][br][kb];
+        bv[e][1] = *(const f32x2*)&Vs[st][q + e][br + 16][kb];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+            acc[q + e][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][nb][s], acc[q + e][nb], 0, 0, 0);
+    }
+    if (c + 1 < nch) store(st ^ 1);
+    __syncthreads();
+  }
+
+  // G^T dU G per (co, ci) in registers -> the 9 taps
+  float* outp = p.out + (long long)split * p.slab;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int ci = ci0 + wn * 32 + nb * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + wm * 16 + (lane >> 4) * 4 + r;
+      float tq[3][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {        // rows: G^T X
+        const float x0 = acc[0 * 4 + q][nb][r], x1 = acc[1 * 4 + q][nb][r];
+        const float x2 = acc[2 * 4 + q][nb][r], x3 = acc[3 * 4 + q][nb][r];
+        tq[0][q] = x0 + 0.5f * (x1 + x2);
+        tq[1][q] = 0.5f * (x1 - x2);
+        tq[2][q] = 0.5f * (x1 + x2) + x3;
+      }
+      if (co >= p.Co || ci >= p.Ci) continue;
+      float* o = outp + (long long)co * 9 * p.Ci + ci;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {     // columns: (G^T X) G
+        float v[3];
+        v[0] = tq[ky][0] + 0.5f * (tq[ky][1] + tq[ky][2]);
+        v[1] = 0.5f * (tq[ky][1] - tq[ky][2]);
+        v[2] = 0.5f * (tq[ky][1] + tq[ky][2]) + tq[ky][3];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          float* d = o + (ky * 3 + kx) * p.Ci;
+          *d = p.accumulate ? *d + v[kx] : v[kx];
+        }
+      }
+    }
+  }
+}
+
 // U = G g G^T of every (co, ci) 3x3 filter g = w[co][ky*3+kx][ci]: u[pos][co][ci]; optionally the
 // data-gradient set ut[pos][ci][co] = U[p(pos)][co][ci] with p swapping positions 0 and 3 per axis.
 // Block = 32 co x 32 ci filters staged through LDS (coalesced both ways).
@@ -379,6 +549,38 @@ __global__ __launch_bounds__(256) void wino_wt_multi_kernel(const float* __restr
 }
 
 }  // namespace
+
+// dW [Co][9][Ci] (splits == 1, optionally accumulated) or per-split slabs [splits][Co][9][Ci] of the
+// weight gradient of a 3x3 stride-1 pad-1 conv, by F(2x2,3x3); tiles_per_split % 8 == 0
+extern "C" int rk_wino_wgrad(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
+                             int splits, int accumulate, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 1) || (W & 1) || Co <= 0 || Ci <= 0 || splits <= 0) return RK_EBADARG;
+  if (splits > 1 && accumulate) return RK_EBADARG;
+  WwParams p;
+  p.dy = dy; p.x = x; p.out = out;
+  p.Nb = Nb; p.H = H; p.W = W; p.Co = Co; p.Ci = Ci;
+  p.TW = W / 2;
+  p.THW = (H / 2) * (W / 2);
+  const long long nt = (long long)Nb * p.THW;
+  if (nt >= (1LL << 22)) return RK_EUNSUPPORTED;    // fp32-reciprocal tile decode
+  p.ntiles = (int)nt;
+  p.tps = ((p.ntiles + splits - 1) / splits + WKC - 1) / WKC * WKC;
+  p.nco = rk_cdiv(Co, 64);
+  p.nci = rk_cdiv(Ci, 64);
+  p.accumulate = accumulate;
+  p.invTW = 1.0f / (float)p.TW;
+  p.invTHW = 1.0f / (float)p.THW;
+  p.dybytes = 4ull * Nb * H * W * Co;
+  p.xbytes = 4ull * Nb * H * W * Ci;
+  if (p.dybytes >= 0x7fffffffull || p.xbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
+  p.slab = 9LL * Co * Ci;
+  const int used = rk_cdiv(p.ntiles, p.tps);        // splits that own tiles (the rest would be empty)
+  if (used != splits) return RK_EBADARG;
+  const long long blocks = (long long)splits * p.nco * p.nci;
+  hipLaunchKernelGGL(wino_wgrad_kernel, dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
 
 // Winograd-domain weights of a 3x3 conv w [Co][9][Ci]: u [16][Co][Ci], ut (nullable) [16][Ci][Co]
 extern "C" int rk_wino_weights(const float* w, float* u, float* ut, int Co, int Ci, void* stream) {

@@ -230,6 +230,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
 
     def run(cfg):
         tile, nst, s = cfg
+        if tile == WINO_WGRAD:
+            wino_wgrad(dy, x, out, splits=s, accumulate=accumulate)
+            return
         if s == 1:
             sgemm(KIND_WGRAD, dy, x, out, M, N, K, Cout, Cin, N, tile=tile, nst=nst, H=H, W=W, C=Cin, taps=taps,
                   flags=F_ACCUM if accumulate else 0)
@@ -244,7 +247,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
     if split:
         cands = [max(split, key=lambda c: min(cdiv(M, TILES[c[0]][0]) * cdiv(N, TILES[c[0]][1]) * c[2],
                                               2 * NUM_CU))] + cands
-    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate)), cands, run)
+    wcands = _wino_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
+    cands += wcands
+    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands)), cands, run)
     run(cfg)
     return out
 
@@ -333,6 +338,49 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
         assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
     _lib.call("rk_wino_conv", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
               Nb, H, W, C, N, flags, int(variant), _s())
+    return out
+
+
+WINO_WGRAD = -3   # autotune tile id of the Winograd weight gradient (cfg = (-3, 0, splits))
+
+
+def _wino_wgrad_cands(Nb, H, W, Cout, Cin):
+    """Split-K choices of rk_wino_wgrad that fill the chip: 128..4096 blocks, >= 8 chunks of 8 tiles per
+    block, slabs <= 256 MiB."""
+    if not (WINO and H % 2 == 0 and W % 2 == 0 and Cin >= 16 and Cout >= 16):
+        return []
+    nt = Nb * (H // 2) * (W // 2)
+    if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
+        return []
+    base = cdiv(Cout, 64) * cdiv(Cin, 64)
+    out = []
+    for s in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512):
+        tps = cdiv(cdiv(nt, s), 8) * 8
+        s_eff = cdiv(nt, tps)
+        if tps < 64 or base * s_eff > 4096 or (s_eff > 1 and s_eff * 9 * Cout * Cin * 4 > (256 << 20)):
+            continue
+        if base * s_eff < 128 and s != 1:
+            continue
+        c = (WINO_WGRAD, 0, s_eff)
+        if c not in out:
+            out.append(c)
+    return out
+
+
+def wino_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1, accumulate=False):
+    """out [Cout][9*Cin] (+)= weight gradient of a 3x3 stride-1 conv by F(2x2,3x3); splits > 1: per-split
+    slabs summed by reduce_slabs."""
+    _check(dy, 'wino_wgrad dy')
+    _check(x, 'wino_wgrad x')
+    Nb, H, W, Cout = dy.shape
+    Cin = x.shape[-1]
+    assert x.shape[:3] == dy.shape[:3] and out.numel() == Cout * 9 * Cin and out.is_contiguous()
+    if splits == 1:
+        _lib.call("rk_wino_wgrad", _p(dy), _p(x), _p(out), Nb, H, W, Cout, Cin, 1, int(bool(accumulate)), _s())
+        return out
+    slab = torch.empty((splits, Cout, 9 * Cin), device=dy.device, dtype=torch.float32)
+    _lib.call("rk_wino_wgrad", _p(dy), _p(x), _p(slab), Nb, H, W, Cout, Cin, int(splits), 0, _s())
+    reduce_slabs(slab, out.view(Cout, 9 * Cin), accumulate=accumulate)
     return out
 
 

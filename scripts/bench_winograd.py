@@ -24,7 +24,14 @@ for (N, H, C, K) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128),
     tw = min(tw0, tw1)
     td = t(lambda: S.conv_fwd(x, w.view(K, 3, 3, C), stats_acc=acc))
     tt = t(lambda: S.wino_weights(w, u, ut))
+    dy = torch.randn(N, H, H, K, device='cuda')
+    dw = torch.empty(K, 9 * C, device='cuda')
+    tww = {c[2]: t(lambda: S.wino_wgrad(dy, x, dw, splits=c[2])) for c in S._wino_wgrad_cands(N, H, H, K, C)}
+    s_best = min(tww, key=tww.get) if tww else None
+    twd = t(lambda: S.conv_wgrad(dy, x, out=dw))
     fl = 2.0 * N * H * H * K * 9 * C
     res.append(dict(N=N, H=H, C=C, K=K, wino4_us=round(tw0, 1), wino8_us=round(tw1, 1), direct_us=round(td, 1), wt_us=round(tt, 1),
-                    speedup=round(td / tw, 2), wino_eff_tflops=round(fl / tw / 1e6, 1)))
+                    speedup=round(td / tw, 2), wino_eff_tflops=round(fl / tw / 1e6, 1),
+                    wgrad_wino_us=round(tww[s_best], 1) if tww else None, wgrad_splits=s_best,
+                    wgrad_direct_us=round(twd, 1)))
     print(json.dumps(res[-1]), flush=True)

@@ -1,4 +1,5 @@
-"""One Winograd conv shape in a loop (for rocprofv3 PMC passes): python scripts/prof_wino_one.py N H C K reps"""
+"""One Winograd conv shape in a loop (for rocprofv3 PMC passes):
+python scripts/prof_wino_one.py N H C K reps [fwd|wgrad [splits]]"""
 import sys
 
 sys.path.insert(0, '.')
@@ -7,12 +8,20 @@ import torch
 from rafiki_amd.ops import _lib, f32 as S
 
 N, H, C, K, reps = (int(v) for v in sys.argv[1:6])
+mode = sys.argv[6] if len(sys.argv) > 6 else 'fwd'
 _lib.lib()
 x = torch.randn(N, H, H, C, device='cuda')
-w = torch.randn(K, 9 * C, device='cuda') * 0.05
-u = torch.empty(16, K, C, device='cuda')
-S.wino_weights(w, u)
-acc = torch.zeros((S.bn_slots(K), 2, K), dtype=torch.float64, device='cuda')
-for _ in range(reps):
-    S.wino_conv(x, u, stats=acc)
+if mode == 'wgrad':
+    dy = torch.randn(N, H, H, K, device='cuda')
+    dw = torch.empty(K, 9 * C, device='cuda')
+    splits = int(sys.argv[7]) if len(sys.argv) > 7 else S._wino_wgrad_cands(N, H, H, K, C)[-1][2]
+    for _ in range(reps):
+        S.wino_wgrad(dy, x, dw, splits=splits)
+else:
+    w = torch.randn(K, 9 * C, device='cuda') * 0.05
+    u = torch.empty(16, K, C, device='cuda')
+    S.wino_weights(w, u)
+    acc = torch.zeros((S.bn_slots(K), 2, K), dtype=torch.float64, device='cuda')
+    for _ in range(reps):
+        S.wino_conv(x, u, stats=acc)
 torch.cuda.synchronize()

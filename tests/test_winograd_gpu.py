@@ -128,3 +128,27 @@ def test_wino_weights_arena_refresh():
     for l, w in enumerate(ws):
         u, ut = _u(w.view(w.shape[0], 3, 3, -1).cpu())
         assert torch.equal(ww.u(l), u) and torch.equal(ww.ut(l), ut)
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 32, 32, 64, 64), (16, 4, 4, 256, 512),
+                                            (3, 6, 10, 24, 40), (2, 2, 2, 16, 16)])
+@pytest.mark.parametrize("splits", [1, 2, 5])
+def test_wino_wgrad(N, H, W, Cin, Cout, splits):
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=30)
+    dy = _rand(N, H, W, Cout, seed=31)
+    nt = N * (H // 2) * (W // 2)
+    tps = -(-(-(-nt // splits)) // 8) * 8
+    s_eff = -(-nt // tps)
+    dw = torch.empty(Cout, 9 * Cin, device=DEV)
+    S.wino_wgrad(dy.to(DEV), x.to(DEV), dw, splits=s_eff)
+    prev = _rand(Cout, 9 * Cin, seed=32).to(DEV)
+    acc = prev.clone()
+    S.wino_wgrad(dy.to(DEV), x.to(DEV), acc, splits=s_eff, accumulate=True)
+    torch.cuda.synchronize()
+    wd = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    out = TF.conv2d(x.double().permute(0, 3, 1, 2), wd, padding=1)
+    (gw,) = torch.autograd.grad(out, wd, dy.double().permute(0, 3, 1, 2))
+    ref = gw.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+    assert rel(dw, ref) < 1e-5
+    assert rel(acc, ref + prev.double().cpu()) < 1e-5
