@@ -140,8 +140,10 @@ class ConvFn(torch.autograd.Function):
         x = x.contiguous()
         bd = None if b is None else b.detach().float().contiguous()
         if x.dtype == F32:
-            y = S.conv_fwd(x, w.detach().contiguous(), taps=taps, bias=bd, act=_act(slope),
-                           slope=0.2 if slope is None else slope)
+            wd = w.detach().contiguous()
+            # 3x3: the fused Winograd kernels (weights transformed inside the candidate) compete in the tuner
+            y = S.conv_fwd(x, wd, taps=taps, bias=bd, act=_act(slope), slope=0.2 if slope is None else slope,
+                           wino=(lambda: S.wino_u(wd)) if taps == 9 else None)
         else:
             y = F.conv_fwd(x, _wshadow(w, wb), taps=taps, bias=bd, act=_act(slope),
                            slope=0.2 if slope is None else slope)
@@ -176,7 +178,9 @@ class ConvDgradFn(torch.autograd.Function):
     def forward(ctx, gy, w, wb, taps):
         gy = gy.contiguous()
         if gy.dtype == F32:
-            dx = S.conv_dgrad(gy, S.conv_wt(w.detach(), taps), taps=taps)
+            wd = w.detach().contiguous()
+            dx = S.conv_dgrad(gy, lambda: S.conv_wt(wd, taps), taps=taps, cin=wd.numel() // (taps * wd.shape[0]),
+                              wino=(lambda: S.wino_ut(wd)) if taps == 9 else None)
         else:
             dx = F.conv_dgrad(gy, _wshadow(w, wb), taps=taps)
         ctx.save_for_backward(gy, w)

@@ -135,8 +135,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
              slope=0.2, out=None, wino=None):
     """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
     [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue.
-    ``wino``: the layer's Winograd weights (WinoWeights.u) -> the fused F(2x2,3x3) kernel is one more
-    autotune candidate."""
+    ``wino``: the layer's Winograd weights (WinoWeights.u), or a callable producing them (run only
+    when a Winograd candidate runs, so the tuner times transform + conv) -> the fused F(2x2,3x3)
+    kernels are more autotune candidates."""
     _check(x, 'conv_fwd x')
     Nb, H, W, Cin = x.shape
     Cout = w.shape[0]
@@ -152,7 +153,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     def run(cfg):
         tile, nst, s = cfg
         if cfg in WINO_CFGS:
-            wino_conv(x, wino, out=out, bias=bias, stats=stats_acc, relu=act == ACT_RELU, variant=-1 - cfg[0])
+            wino_conv(x, wino() if callable(wino) else wino, out=out, bias=bias, stats=stats_acc,
+                      relu=act == ACT_RELU, variant=-1 - cfg[0])
             return
         if s == 1:
             sgemm(KIND_CONV, x, w, out, M, Cout, K, Cin, K, Cout, tile=tile, nst=nst, bias=bias, stats=stats_acc,
@@ -167,24 +169,25 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     cands = _cands(M, Cout, splittable=stats_acc is None and Cout % 4 == 0, K=K, big=Cin % 32 == 0)
     if use_w:
         cands.extend(WINO_CFGS)
-    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, use_w), cands, run)
+    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w), cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
     return out
 
 
-def conv_dgrad(dy: torch.Tensor, wt: torch.Tensor, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None,
-               wino=None):
+def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None,
+               wino=None, cin=None):
     """dx = data gradient of a 3x3 conv as conv3x3(dy, wt) with wt = SConvWT.view() [Cin][taps*Cout].
     Epilogue options: ``gate`` (ReLU mask of the input activation), ``bnb = (y, coeffs, acc)`` (the input
     is BN+ReLU(y): mask + BN-backward sums into acc), ``bnp = (y, coeffs, acc)`` (the input is
     maxpool(BN+ReLU(y)), y at 2x resolution: routing + sums; dx stays the pooled gradient)."""
     _check(dy, 'conv_dgrad dy')
     Nb, H, W, Cout = dy.shape
-    Cin = wt.shape[0]
+    # wt / wino may be callables (weights prepared per call, inside the timed candidate): then ``cin``
+    Cin = cin if callable(wt) else wt.shape[0]
     M, K = Nb * H * W, taps * Cout
-    assert wt.numel() == Cin * K
+    assert callable(wt) or wt.numel() == Cin * K
     if out is None:
         out = torch.empty((Nb, H, W, Cin), device=dy.device, dtype=torch.float32)
     flags, bias, stats = 0, None, None
@@ -204,14 +207,14 @@ def conv_dgrad(dy: torch.Tensor, wt: torch.Tensor, *, taps: int = 9, out=None, g
 
     def run(cfg):
         if cfg in WINO_CFGS:
-            wino_conv(dy, wino, out=out, bnb=bnb, bnp=bnp, variant=-1 - cfg[0])
+            wino_conv(dy, wino() if callable(wino) else wino, out=out, bnb=bnb, bnp=bnp, variant=-1 - cfg[0])
             return
-        sgemm(KIND_CONV, dy, wt, out, M, Cin, K, Cout, K, Cin, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats,
+        sgemm(KIND_CONV, dy, wt() if callable(wt) else wt, out, M, Cin, K, Cout, K, Cin, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats,
               gate=gate, H=H, W=W, C=Cout, taps=taps, flags=flags)
     cands = _cands(M, Cin, big=Cout % 32 == 0)
     if use_w:
         cands.extend(WINO_CFGS)
-    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, use_w), cands, run)
+    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w), cands, run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -306,6 +309,24 @@ def wino_weights(w: torch.Tensor, u: torch.Tensor, ut: Optional[torch.Tensor] = 
     assert u.numel() == 16 * Cout * Cin and (ut is None or ut.numel() == 16 * Cout * Cin)
     _lib.call("rk_wino_weights", _p(w), _p(u), _p(ut), Cout, Cin, _s())
     return u, ut
+
+
+def wino_u(w: torch.Tensor) -> torch.Tensor:
+    """Forward Winograd weights [16][Cout][Cin] of one conv weight [Cout, 3, 3, Cin] (fresh buffer)."""
+    Cout = w.shape[0]
+    u = torch.empty((16, Cout, w.numel() // (9 * Cout)), device=w.device, dtype=torch.float32)
+    _lib.call("rk_wino_weights", _p(w), _p(u), None, Cout, u.shape[2], _s())
+    return u
+
+
+def wino_ut(w: torch.Tensor) -> torch.Tensor:
+    """Data-gradient Winograd weights [16][Cin][Cout] of one conv weight [Cout, 3, 3, Cin]."""
+    Cout = w.shape[0]
+    Cin = w.numel() // (9 * Cout)
+    u = torch.empty((16, Cout, Cin), device=w.device, dtype=torch.float32)
+    ut = torch.empty((16, Cin, Cout), device=w.device, dtype=torch.float32)
+    _lib.call("rk_wino_weights", _p(w), _p(u), _p(ut), Cout, Cin, _s())
+    return ut
 
 
 def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None, bnp=None,
