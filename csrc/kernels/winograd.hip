@@ -45,6 +45,10 @@ struct WgParams {
   int Nb, H, W, C, N;
   int TW, THW, ntiles, ncb, slotMask, flags;
   unsigned long long xbytes, ubytes, ybytes;
+  // grouped launches (the k models of a serving ensemble): group g of gridDim = groups x bpg blocks
+  // reads x + g*gx (gx = 0: shared input), u + g*gu and writes y + g*gy, bias + g*gbias
+  int bpg;
+  long long gx, gu, gy, gbias;
 };
 
 constexpr unsigned WOOB = 0x80000000u;
@@ -79,9 +83,14 @@ __global__ __launch_bounds__(256 * NWN, 3 - NWN) void wino_fwd_kernel(const WgPa
   __shared__ __attribute__((aligned(16))) float Vs[NSTG][16][WT][WKC];
   __shared__ __attribute__((aligned(16))) float Us[NSTG][16][BNC][WKC];
   const int tid = threadIdx.x, lane = tid & 63, wm = (tid >> 6) & 3, wn = tid >> 8;
-  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int b0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = b0 / p.bpg, b = b0 - grp * p.bpg;
   const int cb = b % p.ncb, tb = b / p.ncb;
   const int tbase = tb * WT, cbase = cb * BNC;
+  const float* const gxp = p.x + grp * p.gx;
+  const float* const gup = p.u + grp * p.gu;
+  float* const gyp = p.y + grp * p.gy;
+  const float* const gbp = p.bias ? p.bias + grp * p.gbias : nullptr;
 
   // loader role per thread and chunk: the (tile, channel) 4x4 input windows of tiles lt + NT/8 * h
   // and 4 float4 of U, as raw buffer loads whose byte offsets are fixed for the whole K loop (the
@@ -117,8 +126,8 @@ __global__ __launch_bounds__(256 * NWN, 3 - NWN) void wino_fwd_kernel(const WgPa
   float raw[IT][16];
   f32x4 ur[4];
   auto load = [&](int c0) {
-    const __amdgpu_buffer_rsrc_t xr = w_rsrc(p.x + c0, p.xbytes - 4ull * c0);
-    const __amdgpu_buffer_rsrc_t urs = w_rsrc(p.u + c0, p.ubytes - 4ull * c0);
+    const __amdgpu_buffer_rsrc_t xr = w_rsrc(gxp + c0, p.xbytes - 4ull * c0);
+    const __amdgpu_buffer_rsrc_t urs = w_rsrc(gup + c0, p.ubytes - 4ull * c0);
 #pragma unroll
     for (int h = 0; h < IT; ++h)
 #pragma unroll
@@ -209,14 +218,14 @@ __global__ __launch_bounds__(256 * NWN, 3 - NWN) void wino_fwd_kernel(const WgPa
   for (int nb = 0; nb < 2; ++nb) {
     nn[nb] = cbase + wn * 32 + nb * 16 + (lane & 15);
     nok[nb] = nn[nb] < p.N;
-    bs[nb] = ((fl & (WF_BIAS | WF_BNB | WF_BNP)) && nok[nb]) ? p.bias[nn[nb]] : 0.f;
-    sh[nb] = ((fl & (WF_BNB | WF_BNP)) && nok[nb]) ? p.bias[p.N + nn[nb]] : 0.f;
+    bs[nb] = ((fl & (WF_BIAS | WF_BNB | WF_BNP)) && nok[nb]) ? gbp[nn[nb]] : 0.f;
+    sh[nb] = ((fl & (WF_BNB | WF_BNP)) && nok[nb]) ? gbp[p.N + nn[nb]] : 0.f;
     s[nb] = ss[nb] = 0.f;
   }
   const int t0 = tbase + wm * 16 + (lane >> 4) * 4;
   int im, oy, ox;
   w_tile(p, t0, im, oy, ox);
-  const __amdgpu_buffer_rsrc_t yr = w_rsrc(p.y, p.ybytes);
+  const __amdgpu_buffer_rsrc_t yr = w_rsrc(gyp, p.ybytes);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const bool tok = t0 + r < p.ntiles;
@@ -601,16 +610,21 @@ extern "C" int rk_wino_weights_multi(const float* arena, float* dst, const int* 
 }
 
 // y = conv3x3(x, w) via F(2x2,3x3) with u = rk_wino_weights(w); flags WF_* (BNB/BNP: ``gate`` and the
-// scale/shift pair in ``bias``; BNP: H x W is the pooled map and gate is at 2H x 2W)
-extern "C" int rk_wino_conv(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
-                            const float* gate, int Nb, int H, int W, int C, int N, int flags, int variant,
-                            void* stream) {
+// scale/shift pair in ``bias``; BNP: H x W is the pooled map and gate is at 2H x 2W).  groups > 1:
+// k independent convs in one grid (x / u / y / bias strided by gx / gu / gy / gbias floats; gx = 0
+// shares x), plain or bias / ReLU epilogues only.
+extern "C" int rk_wino_conv_grp(const float* x, const float* u, float* y, const float* bias, double* stats,
+                                int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
+                                int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
+                                void* stream) {
   if (variant != 0 && variant != 1) return RK_EBADARG;
   const int BNC = variant ? 64 : 32;
-  if (Nb <= 0 || (H & 1) || (W & 1) || H <= 0 || W <= 0 || C <= 0 || (C % WKC) || N <= 0) return RK_EBADARG;
+  if (Nb <= 0 || (H & 1) || (W & 1) || H <= 0 || W <= 0 || C <= 0 || (C % WKC) || N <= 0 || groups <= 0)
+    return RK_EBADARG;
   if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
   if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
   if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
+  if (groups > 1 && (flags & (WF_STATS | WF_BNB | WF_BNP))) return RK_EUNSUPPORTED;
   WgParams p;
   p.x = x; p.u = u; p.y = y; p.bias = bias; p.stats = stats; p.gate = gate;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.N = N;
@@ -628,12 +642,22 @@ extern "C" int rk_wino_conv(const float* x, const float* u, float* y, const floa
   if (p.xbytes >= 0x7fffffffull || p.ubytes >= 0x7fffffffull || gbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
   p.slotMask = slotMask;
   p.flags = flags;
-  const long long blocks = (long long)rk_cdiv(p.ntiles, WT) * p.ncb;
+  p.gx = gx; p.gu = gu; p.gy = gy; p.gbias = gbias;
+  const long long bpg = (long long)rk_cdiv(p.ntiles, WT) * p.ncb;
+  const long long blocks = bpg * groups;
   if (blocks >= (1LL << 31)) return RK_EBADARG;
+  p.bpg = (int)bpg;
   if (variant)
     hipLaunchKernelGGL(wino_fwd_kernel<2>, dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
   else
     hipLaunchKernelGGL(wino_fwd_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
   RK_LAUNCH_CHECK();
   return RK_OK;
+}
+
+extern "C" int rk_wino_conv(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
+                            const float* gate, int Nb, int H, int W, int C, int N, int flags, int variant,
+                            void* stream) {
+  return rk_wino_conv_grp(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, variant, 1, 0, 0, 0, 0,
+                          stream);
 }

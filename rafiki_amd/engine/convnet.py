@@ -900,6 +900,13 @@ class GroupedConvNets:
             return torch.stack([fn(e) for e in self.engines]).contiguous()
         self.conv_w = [stack(lambda e, n=name: e.flat.w(n + '.w').reshape(e.flat.w(n + '.w').shape[0], -1))
                        for (name, _, _, _, _) in e0.blocks]
+        # Winograd-domain weights [k, 16, Cout, Cin] of the 3x3 layers the fused kernel takes
+        self.conv_u = [None] * len(e0.blocks)
+        if S.WINO and self.device.type == 'cuda':
+            for bi, (name, cin, cout, pool, hw) in enumerate(e0.blocks):
+                w = self.conv_w[bi]
+                if bi > 0 and w.shape[2] % 9 == 0 and (w.shape[2] // 9) % 8 == 0 and hw % 2 == 0:
+                    self.conv_u[bi] = torch.stack([S.wino_u(w[g]) for g in range(self.k)]).contiguous()
         self.scale = [stack(lambda e, i=bi: e._eval_coeffs[i][2]) for bi in range(len(e0.blocks))]
         self.shift = [stack(lambda e, i=bi: e._eval_coeffs[i][3]) for bi in range(len(e0.blocks))]
         self.fc_w = [stack(lambda e, n=name: e.flat.w(n + '.w')) for (name, _, _, _) in e0.fcs]
@@ -914,7 +921,7 @@ class GroupedConvNets:
         B = x.shape[0]
         h = x
         for bi, (name, cin, cout, pool, hw) in enumerate(e0.blocks):
-            y = S.conv_fwd_grp(h, self.conv_w[bi])
+            y = S.conv_fwd_grp(h, self.conv_w[bi], wino=self.conv_u[bi])
             h = S.bn_eval_grp(y, self.scale[bi], self.shift[bi], pool=pool, act=F.ACT_RELU)
         z = h.reshape(k, B, e0.feat_dim)
         for i in range(len(e0.fcs)):

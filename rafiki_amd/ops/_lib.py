@@ -66,6 +66,7 @@ _SIGS = {
     "rk_lstm_bwd32": [vp, i32, i32, i32, vp, vp, vp, vp, vp],
     "rk_wino_weights": [vp, vp, vp, i32, i32, vp],
     "rk_wino_weights_multi": [vp, vp, vp, i32, vp, vp],
+    "rk_wino_conv_grp": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, vp],
     "rk_wino_wgrad": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "rk_wino_conv": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     # fp32 path (sgemm.hip, bnf.hip)

@@ -405,6 +405,22 @@ def wino_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1
     return out
 
 
+def wino_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
+    """k Winograd convs in one grid: x [G, Nb, H, W, C] (or [Nb, H, W, C] shared), u [G, 16, N, C],
+    bias [G, N] -> out [G, Nb, H, W, N]."""
+    G, _, N, C = u.shape
+    shared = x.dim() == 4
+    Nb, H, W, Cx = x.shape[-4:]
+    assert Cx == C and (shared or x.shape[0] == G) and u.is_contiguous() and x.is_contiguous()
+    if out is None:
+        out = torch.empty((G, Nb, H, W, N), device=x.device, dtype=torch.float32)
+    M = Nb * H * W
+    flags = (WF_BIAS if bias is not None else 0) | (WF_RELU if relu else 0)
+    _lib.call("rk_wino_conv_grp", _p(x), _p(u), _p(out), _p(bias), None, 0, None, Nb, H, W, C, N, flags,
+              int(variant), G, 0 if shared else M * C, 16 * N * C, M * N, N if bias is not None else 0, _s())
+    return out
+
+
 class WinoWeights:
     """Winograd-domain weights of several 3x3 convs whose fp32 weights live in one arena, refreshed by
     ONE launch per weight update: u_l [16][Cout][Cin] for the forward conv and (dgrad=True) ut_l
@@ -813,14 +829,18 @@ def sgemm_grp(kind, A, B, out, M, N, K, lda, ldb, ldc, groups, gstride_a, gstrid
     return out
 
 
-def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=ACT_NONE, slope=0.2, geo=None):
+def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=ACT_NONE, slope=0.2, geo=None,
+             extra=None):
     """Autotuned grouped launch: out [G, M, N]; split-K slabs [s, G*M, N] combined by sreduce_epi with
-    per-group bias."""
+    per-group bias.  ``extra(cfg)``: runs the WINO_CFGS candidates (grouped Winograd convs)."""
     flags = _act_flags(bias, act)
     geo = geo or {}
 
     def run(cfg):
         tile, nst, s = cfg
+        if cfg in WINO_CFGS:
+            extra(cfg)
+            return
         if s == 1:
             sgemm_grp(kind, A, B, out, M, N, K, lda, ldb, N, G, gsa, N * K, M * N, N, tile=tile, nst=nst,
                       bias=bias, flags=flags, slope=slope, **geo)
@@ -830,13 +850,16 @@ def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=
                   slab_stride=G * M * N, **geo)
         sreduce_epi(slab, G * M, N, out.view(G * M, N), bias=bias, act=act, slope=slope, bias_rows=M)
     cands = [c for c in _cands(M * G, N, splittable=N % 4 == 0, K=K) if c[0] < 4]
+    if extra is not None:
+        cands.extend(WINO_CFGS)
     run(_pick(key, cands, run))
     return out
 
 
-def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None):
+def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=None):
     """k convs in one launch: x [G, Nb, H, W, Cin] (or [Nb, H, W, Cin] shared by every group),
-    W [G, Cout, taps*Cin], bias [G, Cout] -> [G, Nb, H, W, Cout] (3x3 stride-1 or 1x1)."""
+    W [G, Cout, taps*Cin], bias [G, Cout] -> [G, Nb, H, W, Cout] (3x3 stride-1 or 1x1).
+    ``wino``: stacked Winograd weights [G, 16, Cout, Cin] -> grouped fused F(2x2,3x3) candidates."""
     G, Cout, K = W.shape
     shared = x.dim() == 4
     Nb, H, Wd, Cin = x.shape[-4:]
@@ -846,9 +869,14 @@ def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None):
     M = Nb * H * Wd
     if out is None:
         out = torch.empty((G, Nb, H, Wd, Cout), device=x.device, dtype=torch.float32)
+    extra = None
+    if wino is not None and taps == 9 and wino_ok(H, Wd, Cin) and act in (ACT_NONE, ACT_RELU):
+        assert wino.shape == (G, 16, Cout, Cin) and wino.is_contiguous()
+        def extra(cfg):
+            wino_conv_grp(x, wino, out=out, bias=bias, relu=act == ACT_RELU, variant=-1 - cfg[0])
     return _grp_run(0, x, W, out, M, Cout, K, Cin, K, G, 0 if shared else M * Cin,
-                    ('sfg', G, M, Cout, K, H, Wd, Cin, shared, bias is not None, act), bias=bias, act=act,
-                    slope=slope, geo=dict(H=H, W=Wd, C=Cin, taps=taps))
+                    ('sfg', G, M, Cout, K, H, Wd, Cin, shared, bias is not None, act, extra is not None), bias=bias,
+                    act=act, slope=slope, geo=dict(H=H, W=Wd, C=Cin, taps=taps), extra=extra)
 
 
 def linear_grp(x, w, bias=None, *, act=ACT_NONE, slope=0.2, out=None):

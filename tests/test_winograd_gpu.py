@@ -152,3 +152,21 @@ def test_wino_wgrad(N, H, W, Cin, Cout, splits):
     ref = gw.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
     assert rel(dw, ref) < 1e-5
     assert rel(acc, ref + prev.double().cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("shared", [True, False])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino_conv_grouped(shared, variant):
+    """k convs in one grid (the serving ensemble's layers) == k separate convs."""
+    from rafiki_amd.ops import f32 as S
+    G, Nb, H, Cin, Cout = 3, 5, 8, 32, 48
+    x = (_rand(Nb, H, H, Cin, seed=40) if shared else _rand(G, Nb, H, H, Cin, seed=40)).to(DEV)
+    w = [_rand(Cout, 3, 3, Cin, seed=41 + g, scale=0.1) for g in range(G)]
+    u = torch.stack([_u(wg)[0] for wg in w]).contiguous()
+    b = _rand(G, Cout, seed=45).to(DEV)
+    y = S.wino_conv_grp(x, u, bias=b, relu=True, variant=variant)
+    torch.cuda.synchronize()
+    for g in range(G):
+        xg = x if shared else x[g]
+        ref = torch.relu(_conv_ref(xg.cpu(), w[g]) + b[g].double().cpu())
+        assert rel(y[g], ref) < 1e-5
