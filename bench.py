@@ -133,7 +133,7 @@ def phase_throughput(args, info, dev):
         for r in range(world):  # training accuracy over the timed window as the trial signal
             advisor.feedback(proposals[r], float(table[r, 1]))
     out = dict(elapsed=elapsed, loss=loss, acc=acc, knobs=proposals[0], dtype=eng.dtype,
-               flops_per_image=eng.flops_per_image(), use_graph=use_graph)
+               train_flops_per_image=eng.train_flops_per_image(), use_graph=use_graph)
     del eng, data, y_all
     torch.cuda.empty_cache()
     return out
@@ -298,7 +298,8 @@ def main():
             'backend': info.backend,
             'n_devices': n_devices,
             'images_per_sec_per_trial': round(ips_trial, 1),
-            'model_tflops': round(th['flops_per_image'] * 3 * ips_trial * n_devices / 1e12, 2),
+            # direct-computation model FLOPs / time (the Winograd convs execute 4/9 of the conv MACs)
+            'model_tflops': round(th['train_flops_per_image'] * ips_trial * n_devices / 1e12, 2),
             'train_loss': round(th['loss'], 4),
             'train_acc': round(th['acc'], 4),
             'knobs_rank0': th['knobs'],

@@ -206,6 +206,13 @@ class ConvNetEngine:
             o, c = self._roff[bi], self.blocks[bi][2]
         return self.running[0, o:o + c], self.running[1, o:o + c]
 
+    def train_flops_per_image(self) -> float:
+        """Model FLOPs of one training image as a direct computation: forward + data gradient +
+        weight gradient of every layer, minus the stem's data gradient (never computed).  The
+        Winograd kernels execute 4/9 of the 3x3 conv MACs counted here."""
+        stem = 2.0 * self.blocks[0][4] ** 2 * self.blocks[0][2] * 9 * self.blocks[0][1] if self.blocks else 0.0
+        return 3.0 * self.flops_per_image() - stem
+
     def flops_per_image(self) -> float:
         """Forward MACs*2 of the conv + FC layers (train step = 3x)."""
         fl = 0.0
