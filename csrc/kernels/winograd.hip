@@ -513,16 +513,17 @@ RK_DEV void wt_block(const float* __restrict__ w, float* __restrict__ u, float* 
     g[i / (9 * 32)][(i >> 5) % 9][i & 31] = st[k];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 1024; i += 256) {
-    const int ci = i & 31, co = i >> 5;
-    if (co0 + co >= Co || ci0 + ci >= Ci) continue;
-    float gg[9], U[16];
+  if (u != nullptr)
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+      const int ci = i & 31, co = i >> 5;
+      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
+      float gg[9], U[16];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
-    w_transform(gg, U);
+      for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
+      w_transform(gg, U);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) u[((long long)q * Co + co0 + co) * Ci + ci0 + ci] = U[q];
-  }
+      for (int q = 0; q < 16; ++q) u[((long long)q * Co + co0 + co) * Ci + ci0 + ci] = U[q];
+    }
   if (ut == nullptr) return;
   for (int i = threadIdx.x; i < 1024; i += 256) {
     const int co = i & 31, ci = i >> 5;
@@ -547,14 +548,15 @@ __global__ __launch_bounds__(256) void wino_wt_kernel(const float* __restrict__ 
 }
 
 // every layer of a network in one launch: desc[block] = (layer, co0, ci0, -); meta[layer] = (weight
-// offset in the arena, u offset, ut offset or -1, Co, Ci) in floats
+// offset in the arena, u offset or -1, ut offset or -1, Co, Ci) in floats
 __global__ __launch_bounds__(256) void wino_wt_multi_kernel(const float* __restrict__ arena, float* __restrict__ dst,
                                                             const int4* __restrict__ desc,
                                                             const long long* __restrict__ meta) {
   __shared__ float g[32][9][33];
   const int4 d = desc[blockIdx.x];
   const long long* m = meta + 5 * d.x;
-  wt_block(arena + m[0], dst + m[1], m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4], d.y, d.z, g);
+  wt_block(arena + m[0], m[1] >= 0 ? dst + m[1] : nullptr, m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4],
+           d.y, d.z, g);
 }
 
 }  // namespace
@@ -591,9 +593,9 @@ extern "C" int rk_wino_wgrad(const float* dy, const float* x, float* out, int Nb
   return RK_OK;
 }
 
-// Winograd-domain weights of a 3x3 conv w [Co][9][Ci]: u [16][Co][Ci], ut (nullable) [16][Ci][Co]
+// Winograd-domain weights of a 3x3 conv w [Co][9][Ci]: u (nullable) [16][Co][Ci], ut (nullable) [16][Ci][Co]
 extern "C" int rk_wino_weights(const float* w, float* u, float* ut, int Co, int Ci, void* stream) {
-  if (Co <= 0 || Ci <= 0) return RK_EBADARG;
+  if (Co <= 0 || Ci <= 0 || (!u && !ut)) return RK_EBADARG;
   const dim3 grid(rk_cdiv(Ci, 32), rk_cdiv(Co, 32));
   hipLaunchKernelGGL(wino_wt_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, u, ut, Co, Ci);
   RK_LAUNCH_CHECK();

@@ -1,0 +1,689 @@
+// Winograd F(4x4, 3x3) fp32 convolution for gfx950: stride 1, pad 1, NHWC, H and W multiples of 4,
+// C % 8 == 0.
+//
+// F(4x4,3x3) multiplies 36 transformed values per 4x4 output tile: 2.25 MACs per output pixel and
+// channel pair against 9 for the direct conv and 4 for F(2x2,3x3) (csrc/kernels/winograd.hip), so
+// 1.78x fewer v_mfma_f32_16x16x4_f32 cycles than the F(2x2) kernel on the same fp32 data; the 6x6
+// input windows overlap less (2.25 loads per output against 4).  The transforms use the
+// interpolation points 0, +-1, +-2 (Lavin & Gray): B^T d B, G g G^T and A^T M A, all fp32; their
+// larger coefficients cost about one decimal digit of accuracy against F(2x2) (measured in
+// profiles/winograd_error_r2.jsonl, still at fp32 round-off scale).
+//
+//   * weights: U = G g G^T [36][Cout][Cin] for the forward conv and, for the data gradient (a forward
+//     conv of dy with the flipped, transposed filters), UT = G flip(g) G^T [36][Cin][Cout] — computed
+//     directly (the F(2x2) position-swap identity has no F(4x4) counterpart: G J is not a row
+//     permutation of G), all layers of a network in one launch;
+//   * block tile = 16 WM tiles (4x4 px each) x 16 WN output channels on WM x WN waves; each wave owns
+//     16 tiles x 16 channels for ALL 36 positions (36 16x16 accumulators, 144 fp32 registers), so the
+//     output transform is lane-local and every lane ends up with whole 4x4 output tiles of one
+//     channel; per position one 64-bit A read and one 64-bit B read feed two MFMAs;
+//   * K loop over Cin in chunks of 8 channels through one LDS stage: every thread loads the 6x6 window
+//     of one (tile, channel) (raw buffer loads at fixed offsets, zeros outside the image via an
+//     out-of-range offset), transforms it in registers and writes 36 values; the next chunk's global
+//     loads are in flight while the current chunk's MFMAs run; XOR-swizzled column pairs keep the
+//     fragment reads bank-conflict-free (the same layout as the F(2x2) kernel);
+//   * epilogues identical to the F(2x2) kernel: bias, ReLU, BN statistics (fp64 slot atomics) and
+//     the data-gradient FLAG_BNB / FLAG_BNP fusions; grouped launches for the serving ensemble.
+#include "common.h"
+
+namespace {
+
+constexpr int KC = 8;     // input channels per K chunk
+enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_BNB = 512, WF_BNP = 1024 };
+
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+struct W4Params {
+  const float* x;       // NHWC [Nb][H][W][C]
+  const float* u;       // [36][N][C]
+  float* y;             // NHWC [Nb][H][W][N]
+  const float* bias;    // [N] bias; BNB / BNP: BN scale [N] then shift [N] of the gated layer
+  double* stats;        // fp64 slots [slotMask+1][2][N]
+  const float* gate;    // BNB: BN input of the gated layer [Nb][H][W][N]; BNP: at [Nb][2H][2W][N]
+  int Nb, H, W, C, N;
+  int TW, THW, ntiles, ncb, slotMask, flags;
+  unsigned long long xbytes, ubytes, ybytes;
+  int bpg;
+  long long gx, gu, gy, gbias;
+};
+
+constexpr unsigned OOB = 0x80000000u;
+
+RK_DEV int swz(int row) { return ((row >> 2) & 3) << 1; }
+
+RK_DEV __amdgpu_buffer_rsrc_t rsrc(const float* base, unsigned long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)(unsigned)bytes, 0x00020000);
+}
+
+// B^T d of a 6-vector (interpolation points 0, 1, -1, 2, -2, inf)
+RK_DEV void bt6(float d0, float d1, float d2, float d3, float d4, float d5, float (&t)[6]) {
+  t[0] = 4.f * d0 - 5.f * d2 + d4;
+  t[1] = d3 + d4 - 4.f * (d1 + d2);
+  t[2] = d4 - d3 + 4.f * (d1 - d2);
+  t[3] = d4 - d2 + 2.f * (d3 - d1);
+  t[4] = d4 - d2 - 2.f * (d3 - d1);
+  t[5] = 4.f * d1 - 5.f * d3 + d5;
+}
+
+// A^T m of a 6-vector -> 4 outputs
+RK_DEV void at6(float m0, float m1, float m2, float m3, float m4, float m5, float (&o)[4]) {
+  const float s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
+  o[0] = m0 + s12 + s34;
+  o[1] = d12 + 2.f * d34;
+  o[2] = s12 + 4.f * s34;
+  o[3] = d12 + 8.f * d34 + m5;
+}
+
+// G g of a 3-vector -> 6 values
+RK_DEV void g6(float g0, float g1, float g2, float (&u)[6]) {
+  const float s = g0 + g2;
+  u[0] = 0.25f * g0;
+  u[1] = -(s + g1) * (1.f / 6.f);
+  u[2] = -(s - g1) * (1.f / 6.f);
+  u[3] = g0 * (1.f / 24.f) + g1 * (1.f / 12.f) + g2 * (1.f / 6.f);
+  u[4] = g0 * (1.f / 24.f) - g1 * (1.f / 12.f) + g2 * (1.f / 6.f);
+  u[5] = g2;
+}
+
+RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) {
+  n = t / p.THW;
+  const int r = t - n * p.THW;
+  const int ty = r / p.TW;
+  oy = 4 * ty;
+  ox = 4 * (r - ty * p.TW);
+}
+
+template <int WM, int WN, int MINW>
+__global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4Params p) {
+  constexpr int NT = 64 * WM * WN;         // threads
+  constexpr int T = 16 * WM;               // tiles per block
+  constexpr int BNC = 16 * WN;             // output channels per block
+  constexpr int IT = T * KC / NT;          // input windows per thread and chunk
+  constexpr int UL = 36 * BNC * 4 / NT;    // f32x2 weight loads per thread and chunk
+  static_assert(IT >= 1 && IT * NT == T * KC && UL * NT == 36 * BNC * 4, "tile shape");
+  __shared__ __attribute__((aligned(16))) float Vs[36][T][KC];
+  __shared__ __attribute__((aligned(16))) float Us[36][BNC][KC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int b0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = b0 / p.bpg, b = b0 - grp * p.bpg;
+  const int cb = b % p.ncb, tb = b / p.ncb;
+  const int tbase = tb * T, cbase = cb * BNC;
+  const float* const gxp = p.x + grp * p.gx;
+  const float* const gup = p.u + grp * p.gu;
+  float* const gyp = p.y + grp * p.gy;
+  const float* const gbp = p.bias ? p.bias + grp * p.gbias : nullptr;
+
+  // loader role: windows (tile lt + NT/8 h, channel lc); byte offset of the tile origin pixel and the
+  // in-image row / column masks of the 6x6 window (rows oy-1 .. oy+4)
+  const int lt = tid >> 3, lc = tid & 7;
+  unsigned vb[IT], rmk[IT], cmk[IT];
+#pragma unroll
+  for (int h = 0; h < IT; ++h) {
+    int ln, loy, lox;
+    const int t = tbase + lt + NT / 8 * h;
+    w4_tile(p, t, ln, loy, lox);
+    const bool lok = t < p.ntiles;
+    vb[h] = lok ? (unsigned)((((ln * p.H + loy) * p.W + lox) * p.C + lc) * 4) : 0u;
+    rmk[h] = cmk[h] = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      if (lok && loy - 1 + a >= 0 && loy - 1 + a < p.H) rmk[h] |= 1u << a;
+      if (lox - 1 + a >= 0 && lox - 1 + a < p.W) cmk[h] |= 1u << a;
+    }
+  }
+  // weight loads: thread tid covers (co, column pair) of positions pos0 + k * UPK, k < UL — one vector
+  // offset, the position stride rides in the scalar offset
+  constexpr int UPK = NT / (4 * BNC);
+  static_assert(UPK * 4 * BNC == NT, "weight loader shape");
+  const int uco = (tid >> 2) & (BNC - 1), upr = tid & 3, upos = tid / (4 * BNC);
+  const unsigned ub = cbase + uco < p.N ? (unsigned)(((upos * p.N + cbase + uco) * p.C + 2 * upr) * 4) : OOB;
+  const int ustride = UPK * p.N * p.C * 4;
+
+  float raw[IT][36];
+  f32x2 ur[UL];
+  auto load = [&](int c0) {
+    const __amdgpu_buffer_rsrc_t xr = rsrc(gxp + c0, p.xbytes - 4ull * c0);
+    const __amdgpu_buffer_rsrc_t urs = rsrc(gup + c0, p.ubytes - 4ull * c0);
+#pragma unroll
+    for (int h = 0; h < IT; ++h) {
+      // opaque copies: the 36 window offsets are rebuilt per chunk from 3 registers instead of being
+      // hoisted out of the K loop into 36 live registers
+      unsigned b = vb[h], rm = rmk[h], cm = cmk[h];
+      asm volatile("" : "+v"(b), "+v"(rm), "+v"(cm));
+#pragma unroll
+      for (int i = 0; i < 36; ++i) {
+        const int a = i / 6, bb = i % 6;
+        const int d = (((a - 1) * p.W) + bb - 1) * p.C * 4;
+        const unsigned in = (rm >> a) & (cm >> bb) & 1u;
+        const unsigned off = (b + (unsigned)d) | ((in ^ 1u) << 31);
+        raw[h][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UL; ++k)
+      ur[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(urs, (int)ub, k * ustride, 0));
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int h = 0; h < IT; ++h) {
+      const int row = lt + NT / 8 * h, c = lc ^ swz(row);
+      float* const r = raw[h];
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {     // B^T d along rows, in place
+        float o[6];
+        bt6(r[bb], r[6 + bb], r[12 + bb], r[18 + bb], r[24 + bb], r[30 + bb], o);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) r[a * 6 + bb] = o[a];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {        // (B^T d) B along columns, straight to LDS
+        float o[6];
+        bt6(r[a * 6 + 0], r[a * 6 + 1], r[a * 6 + 2], r[a * 6 + 3], r[a * 6 + 4], r[a * 6 + 5], o);
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) Vs[a * 6 + bb][row][c] = o[bb];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UL; ++k) *(f32x2*)&Us[upos + UPK * k][uco][(2 * upr) ^ swz(uco)] = ur[k];
+  };
+
+  f32x4 acc[36];
+#pragma unroll
+  for (int q = 0; q < 36; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = p.C / KC;
+  load(0);
+  store();
+  __syncthreads();
+  const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
+  const int ka = (2 * (lane >> 4)) ^ swz(ar), kb = (2 * (lane >> 4)) ^ swz(br);
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load((c + 1) * KC);
+    // four positions at a time: 4 independent MFMAs between dependent ones
+#pragma unroll
+    for (int q = 0; q < 36; q += 4) {
+      f32x2 a[4], bv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = *(const f32x2*)&Vs[q + e][ar][ka];
+        bv[e] = *(const f32x2*)&Us[q + e][br][kb];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s], acc[q + e], 0, 0, 0);
+    }
+    if (c + 1 < nch) {
+      __syncthreads();                     // every wave is done reading the stage
+      store();
+    }
+    __syncthreads();
+  }
+
+  // ---- output transform + epilogue: lane owns channel n of 4 consecutive tiles
+  const int fl = p.flags;
+  const bool sums = fl & (WF_STATS | WF_BNB | WF_BNP);
+  const int n = cbase + wn * 16 + (lane & 15);
+  const bool nok = n < p.N;
+  const float bs = ((fl & (WF_BIAS | WF_BNB | WF_BNP)) && nok) ? gbp[n] : 0.f;
+  const float sh = ((fl & (WF_BNB | WF_BNP)) && nok) ? gbp[p.N + n] : 0.f;
+  float s = 0.f, ss = 0.f;
+  const int t0 = tbase + wm * 16 + (lane >> 4) * 4;
+  int im, oy, ox;
+  w4_tile(p, t0, im, oy, ox);
+  const __amdgpu_buffer_rsrc_t yr = rsrc(gyp, p.ybytes);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool tok = t0 + r < p.ntiles;
+    float tt[6][4];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)            // M A: along columns
+      at6(acc[a * 6 + 0][r], acc[a * 6 + 1][r], acc[a * 6 + 2][r], acc[a * 6 + 3][r], acc[a * 6 + 4][r],
+          acc[a * 6 + 5][r], tt[a]);
+    if (tok && nok) {
+      const int pix = (im * p.H + oy) * p.W + ox;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float o[4];                        // A^T (M A): along rows
+        at6(tt[0][j], tt[1][j], tt[2][j], tt[3][j], tt[4][j], tt[5][j], o);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = o[i];
+          const int idx = (pix + i * p.W + j) * p.N + n;
+          if (fl & WF_BIAS) v += bs;
+          if (fl & WF_STATS) {
+            s += v;
+            ss += v * v;
+          }
+          if (fl & WF_RELU) v = fmaxf(v, 0.f);
+          if (fl & WF_BNB) {
+            const float g = p.gate[idx];
+            v = g * bs + sh > 0.f ? v : 0.f;
+            s += v;
+            ss += v * g;
+          }
+          if (fl & WF_BNP) {
+            const int W2 = 2 * p.W;
+            const int q0 = ((im * 2 * p.H + 2 * (oy + i)) * W2 + 2 * (ox + j)) * p.N + n;
+            const float y4[4] = {p.gate[q0], p.gate[q0 + p.N], p.gate[q0 + W2 * p.N], p.gate[q0 + W2 * p.N + p.N]};
+            float best = -INFINITY, zb = 0.f, yb = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // first maximal relu(z) of the window (torch max_pool2d rule)
+              const float z = y4[e] * bs + sh;
+              const float av = fmaxf(z, 0.f);
+              if (av > best) { best = av; zb = z; yb = y4[e]; }
+            }
+            const float dz = zb > 0.f ? v : 0.f;
+            s += dz;
+            ss += dz * yb;
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), yr, idx * 4, 0, 0);
+        }
+      }
+    }
+    ox += 4;                               // next tile in row-major tile order
+    if (ox >= p.W) {
+      ox = 0;
+      oy += 4;
+      if (oy >= p.H) {
+        oy = 0;
+        ++im;
+      }
+    }
+  }
+  if (sums) {
+    s += __shfl_xor(s, 16, 64);
+    ss += __shfl_xor(ss, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (nok && lane < 32) {
+      double* slot = p.stats + (long long)(blockIdx.x & p.slotMask) * 2 * p.N;
+      unsafeAtomicAdd(slot + (lane >= 16 ? p.N : 0) + n, (double)(lane >= 16 ? ss : s));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ weight gradient
+// dW = sum over 4x4 output tiles of G^T [ (A dY A^T) (.) (B^T d B) ] G: per Winograd position a GEMM
+// dU[pos][co][ci] = sum_t M[pos][t][co] * V[pos][t][ci] reduced over tiles (K), 1.78x fewer MFMA cycles
+// than the F(2x2) weight gradient.  Block = WM x WN waves, 16 WM co x 16 WN ci x 36 positions (wave:
+// 16 co x 16 ci); the tile range is split over gridDim (split-K); each block applies G^T . G in
+// registers and writes plain dW taps [Co][9][Ci] (a slab per split, summed by rk_reduce_slabs).  Per
+// chunk of 8 tiles every thread transforms (tile, co) 4x4 output-gradient patches and (tile, ci) 6x6
+// input windows.
+struct W4wParams {
+  const float* dy;      // NHWC [Nb][H][W][Co]
+  const float* x;       // NHWC [Nb][H][W][Ci]
+  float* out;           // [splits][Co][9][Ci]
+  int Nb, H, W, Co, Ci;
+  int TW, THW, ntiles, tps, nco, nci, accumulate;
+  float invTW, invTHW;
+  unsigned long long dybytes, xbytes;
+  long long slab;       // floats per split
+};
+
+// A y of a 4-vector -> 6 values (the adjoint of A^T)
+RK_DEV void a6(float y0, float y1, float y2, float y3, float (&m)[6]) {
+  const float e = y0 + y2, o = y1 + y3, e4 = y0 + 4.f * y2, o8 = 2.f * y1 + 8.f * y3;
+  m[0] = y0;
+  m[1] = e + o;
+  m[2] = e - o;
+  m[3] = e4 + o8;
+  m[4] = e4 - o8;
+  m[5] = y3;
+}
+
+// G^T x of a 6-vector -> 3 values (the adjoint of G)
+RK_DEV void gt6(float x0, float x1, float x2, float x3, float x4, float x5, float (&g)[3]) {
+  const float s12 = x1 + x2, s34 = x3 + x4;
+  g[0] = 0.25f * x0 - s12 * (1.f / 6.f) + s34 * (1.f / 24.f);
+  g[1] = (x2 - x1) * (1.f / 6.f) + (x3 - x4) * (1.f / 12.f);
+  g[2] = (s34 - s12) * (1.f / 6.f) + x5;
+}
+
+template <int WM, int WN, int MINW>
+__global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W4wParams p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BCO = 16 * WM, BCI = 16 * WN;
+  constexpr int PY = BCO * KC / NT;        // dy patches per thread and chunk
+  constexpr int PX = BCI * KC / NT;        // x windows per thread and chunk
+  static_assert(PY >= 1 && PX >= 1 && PY * NT == BCO * KC && PX * NT == BCI * KC, "wgrad tile shape");
+  __shared__ __attribute__((aligned(16))) float Ms[36][BCO][KC];   // [pos][co][tile]
+  __shared__ __attribute__((aligned(16))) float Vs[36][BCI][KC];   // [pos][ci][tile]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = p.nco * p.nci;
+  const int split = b / per, r0 = b - split * per;
+  const int co0 = (r0 / p.nci) * BCO, ci0 = (r0 % p.nci) * BCI;
+  const int t_begin = split * p.tps;
+  const int t_end = min(t_begin + p.tps, p.ntiles);
+  const int nch = (t_end - t_begin + KC - 1) / KC;
+  const int tt = tid & 7, ch = tid >> 3;   // tile within the chunk, channel (+ NT/8 h) within the block
+  const __amdgpu_buffer_rsrc_t dyr = rsrc(p.dy, p.dybytes), xr = rsrc(p.x, p.xbytes);
+
+  float gy[PY][16], raw[PX][36];
+  auto load = [&](int c) {
+    const int t = t_begin + c * KC + tt;
+    const unsigned okm = t < t_end ? 1u : 0u;
+    const int n = (int)(((float)t + 0.5f) * p.invTHW);   // exact below 2^22 tiles
+    const int rr = t - n * p.THW;
+    const int ty = (int)(((float)rr + 0.5f) * p.invTW);
+    const int oy = 4 * ty, ox = 4 * (rr - ty * p.TW);
+    const int pix = (n * p.H + oy) * p.W + ox;
+#pragma unroll
+    for (int h = 0; h < PY; ++h) {
+      const int co = co0 + ch + NT / 8 * h;
+      const unsigned bad = (okm & (co < p.Co ? 1u : 0u)) ^ 1u;
+      const unsigned ob = (unsigned)((pix * p.Co + co) * 4);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {       // the 4x4 patch lies inside the map (H, W multiples of 4)
+        const unsigned off = (ob + (unsigned)((((i >> 2) * p.W) + (i & 3)) * p.Co * 4)) | (bad << 31);
+        gy[h][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dyr, (int)off, 0, 0));
+      }
+    }
+    // window rows / columns 1..4 are inside the map; row / column 0 and 5 only away from the border
+    const unsigned rm = 30u | (oy > 0 ? 1u : 0u) | (oy + 4 < p.H ? 32u : 0u);
+    const unsigned cm = 30u | (ox > 0 ? 1u : 0u) | (ox + 4 < p.W ? 32u : 0u);
+#pragma unroll
+    for (int h = 0; h < PX; ++h) {
+      const int ci = ci0 + ch + NT / 8 * h;
+      const unsigned xm = okm & (ci < p.Ci ? 1u : 0u);
+      const unsigned xb = (unsigned)((pix * p.Ci + ci) * 4);
+#pragma unroll
+      for (int i = 0; i < 36; ++i) {
+        const int a = i / 6, bb = i % 6;
+        const unsigned in = xm & (rm >> a) & (cm >> bb) & 1u;
+        const unsigned off = (xb + (unsigned)((((a - 1) * p.W) + bb - 1) * p.Ci * 4)) | ((in ^ 1u) << 31);
+        raw[h][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, 0, 0));
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int h = 0; h < PY; ++h) {
+      const int row = ch + NT / 8 * h, c = tt ^ swz(row);
+      float m[6][4];                       // A dY: along rows
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float o[6];
+        a6(gy[h][j], gy[h][4 + j], gy[h][8 + j], gy[h][12 + j], o);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) m[a][j] = o[a];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {        // (A dY) A^T: along columns
+        float o[6];
+        a6(m[a][0], m[a][1], m[a][2], m[a][3], o);
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) Ms[a * 6 + bb][row][c] = o[bb];
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < PX; ++h) {
+      const int row = ch + NT / 8 * h, c = tt ^ swz(row);
+      float* const r = raw[h];
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        float o[6];
+        bt6(r[bb], r[6 + bb], r[12 + bb], r[18 + bb], r[24 + bb], r[30 + bb], o);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) r[a * 6 + bb] = o[a];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        float o[6];
+        bt6(r[a * 6 + 0], r[a * 6 + 1], r[a * 6 + 2], r[a * 6 + 3], r[a * 6 + 4], r[a * 6 + 5], o);
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) Vs[a * 6 + bb][row][c] = o[bb];
+      }
+    }
+  };
+
+  f32x4 acc[36];
+#pragma unroll
+  for (int q = 0; q < 36; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nch > 0) {
+    load(0);
+    store();
+  }
+  __syncthreads();
+  const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
+  const int ka = (2 * (lane >> 4)) ^ swz(ar), kb = (2 * (lane >> 4)) ^ swz(br);
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load(c + 1);
+#pragma unroll
+    for (int q = 0; q < 36; q += 4) {
+      f32x2 a[4], bv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = *(const f32x2*)&Ms[q + e][ar][ka];
+        bv[e] = *(const f32x2*)&Vs[q + e][br][kb];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s], acc[q + e], 0, 0, 0);
+    }
+    if (c + 1 < nch) {
+      __syncthreads();
+      store();
+    }
+    __syncthreads();
+  }
+
+  // G^T dU G per (co, ci) in registers -> the 9 taps
+  float* outp = p.out + (long long)split * p.slab;
+  const int ci = ci0 + wn * 16 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = co0 + wm * 16 + (lane >> 4) * 4 + r;
+    float tq[3][6];
+#pragma unroll
+    for (int bb = 0; bb < 6; ++bb) {       // rows: G^T X
+      float g[3];
+      gt6(acc[0 * 6 + bb][r], acc[1 * 6 + bb][r], acc[2 * 6 + bb][r], acc[3 * 6 + bb][r], acc[4 * 6 + bb][r],
+          acc[5 * 6 + bb][r], g);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) tq[ky][bb] = g[ky];
+    }
+    if (co >= p.Co || ci >= p.Ci) continue;
+    float* o = outp + (long long)co * 9 * p.Ci + ci;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {       // columns: (G^T X) G
+      float v[3];
+      gt6(tq[ky][0], tq[ky][1], tq[ky][2], tq[ky][3], tq[ky][4], tq[ky][5], v);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        float* d = o + (ky * 3 + kx) * p.Ci;
+        *d = p.accumulate ? *d + v[kx] : v[kx];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ weight transform
+// U = G g G^T (36 values) of a 3x3 filter g[ky*3+kx]
+RK_DEV void w4_transform(const float (&g)[9], float (&U)[36]) {
+  float t[6][3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    float o[6];
+    g6(g[kx], g[3 + kx], g[6 + kx], o);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) t[a][kx] = o[a];
+  }
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float o[6];
+    g6(t[a][0], t[a][1], t[a][2], o);
+#pragma unroll
+    for (int bb = 0; bb < 6; ++bb) U[a * 6 + bb] = o[bb];
+  }
+}
+
+// one 32 co x 32 ci block of filters, LDS-staged so both layouts are written coalesced:
+// u [36][Co][Ci] of w, ut [36][Ci][Co] of the flipped filters (either may be null)
+RK_DEV void w4_block(const float* __restrict__ w, float* __restrict__ u, float* __restrict__ ut, int Co, int Ci,
+                     int co0, int ci0, float (&g)[32][9][33]) {
+  float st[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    const int ci = i & 31, t = (i >> 5) % 9, co = i / (9 * 32);
+    st[k] = (co0 + co < Co && ci0 + ci < Ci) ? w[((long long)(co0 + co) * 9 + t) * Ci + ci0 + ci] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    g[i / (9 * 32)][(i >> 5) % 9][i & 31] = st[k];
+  }
+  __syncthreads();
+  if (u != nullptr)
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+      const int ci = i & 31, co = i >> 5;
+      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
+      float gg[9], U[36];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
+      w4_transform(gg, U);
+#pragma unroll
+      for (int q = 0; q < 36; ++q) u[((long long)q * Co + co0 + co) * Ci + ci0 + ci] = U[q];
+    }
+  if (ut != nullptr)
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+      const int co = i & 31, ci = i >> 5;
+      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
+      float gg[9], U[36];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) gg[t] = g[co][8 - t][ci];
+      w4_transform(gg, U);
+#pragma unroll
+      for (int q = 0; q < 36; ++q) ut[((long long)q * Ci + ci0 + ci) * Co + co0 + co] = U[q];
+    }
+}
+
+__global__ __launch_bounds__(256) void wino4_wt_kernel(const float* __restrict__ w, float* __restrict__ u,
+                                                       float* __restrict__ ut, int Co, int Ci) {
+  __shared__ float g[32][9][33];
+  w4_block(w, u, ut, Co, Ci, blockIdx.y * 32, blockIdx.x * 32, g);
+}
+
+// every layer in one launch: desc[block] = (layer, co0, ci0, -); meta[layer] = (weight offset in the
+// arena, u offset or -1, ut offset or -1, Co, Ci) in floats
+__global__ __launch_bounds__(256) void wino4_wt_multi_kernel(const float* __restrict__ arena, float* __restrict__ dst,
+                                                             const int4* __restrict__ desc,
+                                                             const long long* __restrict__ meta) {
+  __shared__ float g[32][9][33];
+  const int4 d = desc[blockIdx.x];
+  const long long* m = meta + 5 * d.x;
+  w4_block(arena + m[0], m[1] >= 0 ? dst + m[1] : nullptr, m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4],
+           d.y, d.z, g);
+}
+
+}  // namespace
+
+// u [36][Co][Ci] (nullable) / ut [36][Ci][Co] (nullable) of a 3x3 conv weight w [Co][9][Ci]
+extern "C" int rk_wino4_weights(const float* w, float* u, float* ut, int Co, int Ci, void* stream) {
+  if (Co <= 0 || Ci <= 0 || (!u && !ut)) return RK_EBADARG;
+  const dim3 grid(rk_cdiv(Ci, 32), rk_cdiv(Co, 32));
+  hipLaunchKernelGGL(wino4_wt_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, u, ut, Co, Ci);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_wino4_weights_multi(const float* arena, float* dst, const int* desc, int nblocks,
+                                      const long long* meta, void* stream) {
+  if (nblocks <= 0) return RK_OK;
+  hipLaunchKernelGGL(wino4_wt_multi_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, arena, dst,
+                     (const int4*)desc, meta);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// y = conv3x3(x, w) via F(4x4,3x3) with u = rk_wino4_weights(w); flags / grouping as rk_wino_conv_grp.
+// variant 0: 8 waves, 64 tiles x 32 channels (1 block per CU); 1: 4 waves, 32 x 32 (2 per CU)
+extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const float* bias, double* stats,
+                                 int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
+                                 int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
+                                 void* stream) {
+  if (variant != 0 && variant != 1) return RK_EBADARG;
+  const int T = variant ? 32 : 64, BNC = 32;
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || C <= 0 || (C % KC) || N <= 0 || groups <= 0)
+    return RK_EBADARG;
+  if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
+  if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
+  if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
+  if (groups > 1 && (flags & (WF_STATS | WF_BNB | WF_BNP))) return RK_EUNSUPPORTED;
+  W4Params p;
+  p.x = x; p.u = u; p.y = y; p.bias = bias; p.stats = stats; p.gate = gate;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.N = N;
+  p.TW = W / 4;
+  p.THW = (H / 4) * (W / 4);
+  const long long nt = (long long)Nb * p.THW;
+  if (nt >= (1LL << 30)) return RK_EBADARG;
+  p.ntiles = (int)nt;
+  p.ncb = rk_cdiv(N, BNC);
+  p.xbytes = 4ull * Nb * H * W * C;
+  p.ubytes = 144ull * N * C;
+  p.ybytes = 4ull * Nb * H * W * N;
+  const unsigned long long gbytes = (flags & WF_BNP) ? 4 * p.ybytes : p.ybytes;
+  if (p.xbytes >= 0x7fffffffull || p.ubytes >= 0x7fffffffull || gbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
+  p.slotMask = slotMask;
+  p.flags = flags;
+  p.gx = gx; p.gu = gu; p.gy = gy; p.gbias = gbias;
+  const long long bpg = (long long)rk_cdiv(p.ntiles, T) * p.ncb;
+  const long long blocks = bpg * groups;
+  if (blocks >= (1LL << 31)) return RK_EBADARG;
+  p.bpg = (int)bpg;
+  if (variant)
+    hipLaunchKernelGGL((wino4_fwd_kernel<2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL((wino4_fwd_kernel<4, 2, 1>), dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_wino4_conv(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
+                             const float* gate, int Nb, int H, int W, int C, int N, int flags, int variant,
+                             void* stream) {
+  return rk_wino4_conv_grp(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, variant, 1, 0, 0, 0, 0,
+                           stream);
+}
+
+// dW [Co][9][Ci] (splits == 1, optionally accumulated) or per-split slabs [splits][Co][9][Ci] of the
+// weight gradient of a 3x3 stride-1 pad-1 conv by F(4x4,3x3); H, W multiples of 4; tiles_per_split % 8 == 0
+extern "C" int rk_wino4_wgrad(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
+                              int splits, int accumulate, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0 || splits <= 0) return RK_EBADARG;
+  if (splits > 1 && accumulate) return RK_EBADARG;
+  constexpr int BCO = 32, BCI = 32;
+  W4wParams p;
+  p.dy = dy; p.x = x; p.out = out;
+  p.Nb = Nb; p.H = H; p.W = W; p.Co = Co; p.Ci = Ci;
+  p.TW = W / 4;
+  p.THW = (H / 4) * (W / 4);
+  const long long nt = (long long)Nb * p.THW;
+  if (nt >= (1LL << 22)) return RK_EUNSUPPORTED;    // fp32-reciprocal tile decode
+  p.ntiles = (int)nt;
+  p.tps = ((p.ntiles + splits - 1) / splits + KC - 1) / KC * KC;
+  p.nco = rk_cdiv(Co, BCO);
+  p.nci = rk_cdiv(Ci, BCI);
+  p.accumulate = accumulate;
+  p.invTW = 1.0f / (float)p.TW;
+  p.invTHW = 1.0f / (float)p.THW;
+  p.dybytes = 4ull * Nb * H * W * Co;
+  p.xbytes = 4ull * Nb * H * W * Ci;
+  if (p.dybytes >= 0x7fffffffull || p.xbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
+  p.slab = 9LL * Co * Ci;
+  const int used = rk_cdiv(p.ntiles, p.tps);
+  if (used != splits) return RK_EBADARG;
+  const long long blocks = (long long)splits * p.nco * p.nci;
+  hipLaunchKernelGGL((wino4_wgrad_kernel<2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+

@@ -384,7 +384,8 @@ class ConvNetEngine:
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             rm, rv = self.running_stats(bi)
             y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0],
-                           wino=ww.u(bi - 1) if ww is not None and bi > 0 else None)
+                           wino=ww.lazy('u2', bi - 1) if ww is not None and bi > 0 else None,
+                           wino4=ww.lazy('u4', bi - 1) if ww is not None and bi > 0 else None)
             h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
                                  self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
             saved.append((y, coeffs))
@@ -441,28 +442,33 @@ class ConvNetEngine:
                 break
             py, pco = saved[bi - 1]
             pname, pcin, pcout, ppool, phw = self.blocks[bi - 1]
-            wu = ww.ut(bi - 1) if ww is not None else None
+            wu = ww.lazy('ut2', bi - 1) if ww is not None else None
+            wu4 = ww.lazy('ut4', bi - 1) if ww is not None else None
             if not ppool:
                 # the input block is BN+ReLU: its mask and BN-backward sums ride in this dgrad's epilogue
-                d = S.conv_dgrad(dy, wt.view(bi - 1), bnb=(py, pco, accs[bi - 1][1]), wino=wu)
+                d = S.conv_dgrad(dy, wt.view(bi - 1), bnb=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4)
                 reduced = True
             elif phw == 2 * hw and not (hw & (hw - 1)):
                 # BN+ReLU+max-pool input (even power-of-two geometry): pool routing + sums in the epilogue
-                d = S.conv_dgrad(dy, wt.view(bi - 1), bnp=(py, pco, accs[bi - 1][1]), wino=wu)
+                d = S.conv_dgrad(dy, wt.view(bi - 1), bnp=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4)
                 reduced = True
             else:
-                d = S.conv_dgrad(dy, wt.view(bi - 1), wino=wu)
+                d = S.conv_dgrad(dy, wt.view(bi - 1), wino=wu, wino4=wu4)
                 reduced = False
+        if ww is not None:
+            ww.end_step()   # only the Winograd sets the tuned convs use are transformed from now on
 
     def _wino_train(self):
-        """WinoWeights over blocks 1.. (fp32 path): the fused F(2x2,3x3) kernel becomes an autotune
-        candidate of every forward / data-gradient conv it fits (RAFIKI_WINOGRAD=0 turns it off)."""
+        """WinoWeights over blocks 1.. (fp32 path): the fused F(2x2,3x3) and F(4x4,3x3) kernels become
+        autotune candidates of every forward / data-gradient conv they fit (RAFIKI_WINOGRAD=0 turns
+        both off, RAFIKI_WINOGRAD4=0 the F(4x4) ones)."""
         if not (self.f32 and S.WINO and len(self.blocks) > 1 and self.device.type == 'cuda'):
             return None
         ww = getattr(self, '_ww', None)
         if ww is None:
             fl = self.flat
-            ww = self._ww = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]])
+            ww = self._ww = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]],
+                                          hw=[b[4] for b in self.blocks[1:]])
         return ww
 
     def _conv_wt(self):
@@ -750,7 +756,8 @@ class ConvNetEngine:
         self._eval_graphs = {}
         self._eval_wino = None
         if self.f32 and S.WINO and len(self.blocks) > 1 and self.device.type == 'cuda':
-            self._eval_wino = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]], dgrad=False)
+            self._eval_wino = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]], dgrad=False,
+                                            hw=[b[4] for b in self.blocks[1:]])
             self._eval_wino.refresh()
         return coeffs
 
@@ -761,7 +768,8 @@ class ConvNetEngine:
         B = x.shape[0]
         ew = getattr(self, '_eval_wino', None)
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
-            y = S.conv_fwd(h, fl.w(name + '.w'), wino=ew.u(bi - 1) if ew is not None and bi > 0 else None)
+            y = S.conv_fwd(h, fl.w(name + '.w'), wino=ew.u(bi - 1) if ew is not None and bi > 0 else None,
+                           wino4=ew.u4(bi - 1) if ew is not None and bi > 0 else None)
             c = self._eval_coeffs[bi]
             h = S.bn_eval(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
         if self.input_bn:
@@ -909,11 +917,14 @@ class GroupedConvNets:
                        for (name, _, _, _, _) in e0.blocks]
         # Winograd-domain weights [k, 16, Cout, Cin] of the 3x3 layers the fused kernel takes
         self.conv_u = [None] * len(e0.blocks)
+        self.conv_u4 = [None] * len(e0.blocks)   # F(4x4) sets [k, 36, Cout, Cin] (maps in multiples of 4)
         if S.WINO and self.device.type == 'cuda':
             for bi, (name, cin, cout, pool, hw) in enumerate(e0.blocks):
                 w = self.conv_w[bi]
                 if bi > 0 and w.shape[2] % 9 == 0 and (w.shape[2] // 9) % 8 == 0 and hw % 2 == 0:
                     self.conv_u[bi] = torch.stack([S.wino_u(w[g]) for g in range(self.k)]).contiguous()
+                    if S.WINO4 and hw % 4 == 0:
+                        self.conv_u4[bi] = torch.stack([S.wino4_u(w[g]) for g in range(self.k)]).contiguous()
         self.scale = [stack(lambda e, i=bi: e._eval_coeffs[i][2]) for bi in range(len(e0.blocks))]
         self.shift = [stack(lambda e, i=bi: e._eval_coeffs[i][3]) for bi in range(len(e0.blocks))]
         self.fc_w = [stack(lambda e, n=name: e.flat.w(n + '.w')) for (name, _, _, _) in e0.fcs]
@@ -928,7 +939,7 @@ class GroupedConvNets:
         B = x.shape[0]
         h = x
         for bi, (name, cin, cout, pool, hw) in enumerate(e0.blocks):
-            y = S.conv_fwd_grp(h, self.conv_w[bi], wino=self.conv_u[bi])
+            y = S.conv_fwd_grp(h, self.conv_w[bi], wino=self.conv_u[bi], wino4=self.conv_u4[bi])
             h = S.bn_eval_grp(y, self.scale[bi], self.shift[bi], pool=pool, act=F.ACT_RELU)
         z = h.reshape(k, B, e0.feat_dim)
         for i in range(len(e0.fcs)):

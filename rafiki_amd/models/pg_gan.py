@@ -437,8 +437,9 @@ class GraphedRounds:
     device counter, the Adam step count lives on the device, and the loss accumulators are
     persistent buffers, so replays need no host input."""
 
-    def __init__(self, enabled):
+    def __init__(self, enabled, collectives=False):
         self.enabled = enabled
+        self.collectives = collectives
         self.graphs = {}
         self.seen = set()
         self.captures = 0
@@ -461,6 +462,10 @@ class GraphedRounds:
             return
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
+        if self.collectives:
+            # let the process group's watchdog retire the eager rounds' (completed) all-reduce works
+            # before the capture starts, so it never polls their events while this thread captures
+            time.sleep(0.3)
         with _capture(g):
             fn()
         self.graphs[key] = g
@@ -620,7 +625,7 @@ class PgGan(BaseModel):
         # one-box multi-rank rehearsal: eager)
         capturable = g_ar is None or self.ctx.dist.backend == 'nccl'
         graphs = GraphedRounds(dev.type == 'cuda' and capturable and bool(knobs.get('cuda_graph', True))
-                               and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0')
+                               and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0', collectives=g_ar is not None)
         self.graphs = graphs
         acc = torch.zeros(6, dtype=torch.float32, device=dev)
         level_cache = {}

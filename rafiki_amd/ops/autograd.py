@@ -143,7 +143,8 @@ class ConvFn(torch.autograd.Function):
             wd = w.detach().contiguous()
             # 3x3: the fused Winograd kernels (weights transformed inside the candidate) compete in the tuner
             y = S.conv_fwd(x, wd, taps=taps, bias=bd, act=_act(slope), slope=0.2 if slope is None else slope,
-                           wino=(lambda: S.wino_u(wd)) if taps == 9 else None)
+                           wino=(lambda: S.wino_u(wd)) if taps == 9 else None,
+                           wino4=(lambda: S.wino4_u(wd)) if taps == 9 else None)
         else:
             y = F.conv_fwd(x, _wshadow(w, wb), taps=taps, bias=bd, act=_act(slope),
                            slope=0.2 if slope is None else slope)
@@ -180,7 +181,8 @@ class ConvDgradFn(torch.autograd.Function):
         if gy.dtype == F32:
             wd = w.detach().contiguous()
             dx = S.conv_dgrad(gy, lambda: S.conv_wt(wd, taps), taps=taps, cin=wd.numel() // (taps * wd.shape[0]),
-                              wino=(lambda: S.wino_ut(wd)) if taps == 9 else None)
+                              wino=(lambda: S.wino_ut(wd)) if taps == 9 else None,
+                              wino4=(lambda: S.wino4_ut(wd)) if taps == 9 else None)
         else:
             dx = F.conv_dgrad(gy, _wshadow(w, wb), taps=taps)
         ctx.save_for_backward(gy, w)

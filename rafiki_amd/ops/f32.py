@@ -132,12 +132,12 @@ def _slots_flags(acc):
 
 # ------------------------------------------------------------------------------------------ conv
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None, bias=None, act=ACT_NONE,
-             slope=0.2, out=None, wino=None):
+             slope=0.2, out=None, wino=None, wino4=None):
     """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
     [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue.
     ``wino``: the layer's Winograd weights (WinoWeights.u), or a callable producing them (run only
     when a Winograd candidate runs, so the tuner times transform + conv) -> the fused F(2x2,3x3)
-    kernels are more autotune candidates."""
+    kernels are more autotune candidates; ``wino4`` likewise for the F(4x4,3x3) kernels (WinoWeights.u4)."""
     _check(x, 'conv_fwd x')
     Nb, H, W, Cin = x.shape
     Cout = w.shape[0]
@@ -149,9 +149,14 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     flags |= F_RELU if act == ACT_RELU else F_LRELU if act == ACT_LRELU else 0
 
     use_w = wino is not None and taps == 9 and wino_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
+    use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
 
     def run(cfg):
         tile, nst, s = cfg
+        if cfg in WINO4_CFGS:
+            wino4_conv(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
+                       relu=act == ACT_RELU, variant=-5 - cfg[0])
+            return
         if cfg in WINO_CFGS:
             wino_conv(x, wino() if callable(wino) else wino, out=out, bias=bias, stats=stats_acc,
                       relu=act == ACT_RELU, variant=-1 - cfg[0])
@@ -169,7 +174,10 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     cands = _cands(M, Cout, splittable=stats_acc is None and Cout % 4 == 0, K=K, big=Cin % 32 == 0)
     if use_w:
         cands.extend(WINO_CFGS)
-    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w), cands, run)
+    if use_w4:
+        cands.extend(WINO4_CFGS)
+    cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w,
+                 'lazy' if callable(wino4) else use_w4), cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -177,7 +185,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
 
 
 def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None,
-               wino=None, cin=None):
+               wino=None, wino4=None, cin=None):
     """dx = data gradient of a 3x3 conv as conv3x3(dy, wt) with wt = SConvWT.view() [Cin][taps*Cout].
     Epilogue options: ``gate`` (ReLU mask of the input activation), ``bnb = (y, coeffs, acc)`` (the input
     is BN+ReLU(y): mask + BN-backward sums into acc), ``bnp = (y, coeffs, acc)`` (the input is
@@ -204,8 +212,12 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
         flags = F_GATE
     # ``wino``: the layer's Winograd data-gradient weights (WinoWeights.ut), one more candidate
     use_w = wino is not None and taps == 9 and wino_ok(H, W, Cout) and not (flags & F_GATE)
+    use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cout) and not (flags & F_GATE)
 
     def run(cfg):
+        if cfg in WINO4_CFGS:
+            wino4_conv(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, variant=-5 - cfg[0])
+            return
         if cfg in WINO_CFGS:
             wino_conv(dy, wino() if callable(wino) else wino, out=out, bnb=bnb, bnp=bnp, variant=-1 - cfg[0])
             return
@@ -214,7 +226,10 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
     cands = _cands(M, Cin, big=Cout % 32 == 0)
     if use_w:
         cands.extend(WINO_CFGS)
-    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w), cands, run)
+    if use_w4:
+        cands.extend(WINO4_CFGS)
+    cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w,
+                 'lazy' if callable(wino4) else use_w4), cands, run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -236,6 +251,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
         if tile == WINO_WGRAD:
             wino_wgrad(dy, x, out, splits=s, accumulate=accumulate)
             return
+        if tile == WINO4_WGRAD:
+            wino4_wgrad(dy, x, out, splits=s, accumulate=accumulate)
+            return
         if s == 1:
             sgemm(KIND_WGRAD, dy, x, out, M, N, K, Cout, Cin, N, tile=tile, nst=nst, H=H, W=W, C=Cin, taps=taps,
                   flags=F_ACCUM if accumulate else 0)
@@ -251,8 +269,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
         cands = [max(split, key=lambda c: min(cdiv(M, TILES[c[0]][0]) * cdiv(N, TILES[c[0]][1]) * c[2],
                                               2 * NUM_CU))] + cands
     wcands = _wino_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
-    cands += wcands
-    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands)), cands, run)
+    w4cands = _wino4_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
+    cands += wcands + w4cands
+    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands), bool(w4cands)), cands, run)
     run(cfg)
     return out
 
@@ -362,6 +381,125 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
     return out
 
 
+# ----------------------------------------------------------------- Winograd F(4x4, 3x3) forward
+# autotune candidates that run rk_wino4_conv: 8-wave 64 tiles x 32 channels (variant 0) / 4-wave 32 x 32
+WINO4_CFGS = ((-5, 0, 1), (-6, 0, 1))
+WINO4 = os.environ.get('RAFIKI_WINOGRAD4', '1') != '0'
+
+
+def wino4_ok(H: int, W: int, C: int) -> bool:
+    """Shapes the fused F(4x4,3x3) kernel takes: stride-1 3x3, maps in multiples of 4, C % 8 == 0."""
+    return WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and C % 8 == 0 and C > 0
+
+
+def wino4_u(w: torch.Tensor) -> torch.Tensor:
+    """Forward F(4x4) weights [36][Cout][Cin] of one conv weight [Cout, 3, 3, Cin] (fresh buffer)."""
+    Cout = w.shape[0]
+    Cin = w.numel() // (9 * Cout)
+    u = torch.empty((36, Cout, Cin), device=w.device, dtype=torch.float32)
+    _lib.call("rk_wino4_weights", _p(w), _p(u), None, Cout, Cin, _s())
+    return u
+
+
+def wino4_ut(w: torch.Tensor) -> torch.Tensor:
+    """Data-gradient F(4x4) weights [36][Cin][Cout] (flipped, transposed filters) of w [Cout, 3, 3, Cin]."""
+    Cout = w.shape[0]
+    Cin = w.numel() // (9 * Cout)
+    ut = torch.empty((36, Cin, Cout), device=w.device, dtype=torch.float32)
+    _lib.call("rk_wino4_weights", _p(w), None, _p(ut), Cout, Cin, _s())
+    return ut
+
+
+def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None, bnp=None,
+               variant=0):
+    """y = conv3x3(x, w) (stride 1, pad 1) by F(4x4,3x3) from u = wino4_u(w); options as wino_conv."""
+    _check(x, 'wino4_conv x')
+    Nb, H, W, C = x.shape
+    N = u.shape[1]
+    assert u.shape == (36, N, C) and u.is_contiguous(), (u.shape, x.shape)
+    if out is None:
+        out = torch.empty((Nb, H, W, N), device=x.device, dtype=torch.float32)
+    assert out.shape == (Nb, H, W, N) and out.is_contiguous()
+    flags, gate = 0, None
+    if bias is not None:
+        flags |= WF_BIAS
+    if relu:
+        flags |= WF_RELU
+    if stats is not None:
+        flags |= WF_STATS
+    if bnb is not None:
+        gate, coeffs, stats = bnb
+        assert gate.shape == out.shape
+        bias, flags = coeffs[2:4].reshape(-1), WF_BNB
+    elif bnp is not None:
+        gate, coeffs, stats = bnp
+        assert gate.shape == (Nb, 2 * H, 2 * W, N)
+        bias, flags = coeffs[2:4].reshape(-1), WF_BNP
+    if stats is not None:
+        assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
+    _lib.call("rk_wino4_conv", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
+              Nb, H, W, C, N, flags, int(variant), _s())
+    return out
+
+
+def wino4_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
+    """k F(4x4) convs in one grid: x [G, Nb, H, W, C] (or shared [Nb, H, W, C]), u [G, 36, N, C]."""
+    G, _, N, C = u.shape
+    shared = x.dim() == 4
+    Nb, H, W, Cx = x.shape[-4:]
+    assert Cx == C and (shared or x.shape[0] == G) and u.is_contiguous() and x.is_contiguous()
+    if out is None:
+        out = torch.empty((G, Nb, H, W, N), device=x.device, dtype=torch.float32)
+    M = Nb * H * W
+    flags = (WF_BIAS if bias is not None else 0) | (WF_RELU if relu else 0)
+    _lib.call("rk_wino4_conv_grp", _p(x), _p(u), _p(out), _p(bias), None, 0, None, Nb, H, W, C, N, flags,
+              int(variant), G, 0 if shared else M * C, 36 * N * C, M * N, N if bias is not None else 0, _s())
+    return out
+
+
+WINO4_WGRAD = -7  # autotune tile id of the F(4x4) weight gradient (cfg = (-7, 0, splits))
+
+
+def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
+    """Split-K choices of rk_wino4_wgrad (32 co x 32 ci blocks): 128..4096 blocks, >= 4 chunks of 8 tiles
+    per block, slabs <= 256 MiB."""
+    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and Cin >= 16 and Cout >= 16):
+        return []
+    nt = Nb * (H // 4) * (W // 4)
+    if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
+        return []
+    base = cdiv(Cout, 32) * cdiv(Cin, 32)
+    out = []
+    for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+        tps = cdiv(cdiv(nt, s), 8) * 8
+        s_eff = cdiv(nt, tps)
+        if tps < 32 or base * s_eff > 4096 or (s_eff > 1 and s_eff * 9 * Cout * Cin * 4 > (256 << 20)):
+            continue
+        if base * s_eff < 128 and s != 1:
+            continue
+        c = (WINO4_WGRAD, 0, s_eff)
+        if c not in out:
+            out.append(c)
+    return out
+
+
+def wino4_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1, accumulate=False):
+    """out [Cout][9*Cin] (+)= weight gradient of a 3x3 stride-1 conv by F(4x4,3x3); splits > 1: per-split
+    slabs summed by reduce_slabs."""
+    _check(dy, 'wino4_wgrad dy')
+    _check(x, 'wino4_wgrad x')
+    Nb, H, W, Cout = dy.shape
+    Cin = x.shape[-1]
+    assert x.shape[:3] == dy.shape[:3] and out.numel() == Cout * 9 * Cin and out.is_contiguous()
+    if splits == 1:
+        _lib.call("rk_wino4_wgrad", _p(dy), _p(x), _p(out), Nb, H, W, Cout, Cin, 1, int(bool(accumulate)), _s())
+        return out
+    slab = torch.empty((splits, Cout, 9 * Cin), device=dy.device, dtype=torch.float32)
+    _lib.call("rk_wino4_wgrad", _p(dy), _p(x), _p(slab), Nb, H, W, Cout, Cin, int(splits), 0, _s())
+    reduce_slabs(slab, out.view(Cout, 9 * Cin), accumulate=accumulate)
+    return out
+
+
 WINO_WGRAD = -3   # autotune tile id of the Winograd weight gradient (cfg = (-3, 0, splits))
 
 
@@ -422,45 +560,132 @@ def wino_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
 
 
 class WinoWeights:
-    """Winograd-domain weights of several 3x3 convs whose fp32 weights live in one arena, refreshed by
-    ONE launch per weight update: u_l [16][Cout][Cin] for the forward conv and (dgrad=True) ut_l
-    [16][Cin][Cout] for the data gradient (a forward conv of dy)."""
+    """Winograd-domain weights of several 3x3 convs whose fp32 weights live in one arena: per layer the
+    F(2x2) sets u2 [16][Cout][Cin] (forward) and ut2 [16][Cin][Cout] (data gradient, ``dgrad=True``)
+    and, for maps in multiples of 4 (``f4``), the F(4x4) sets u4 [36][Cout][Cin] / ut4 [36][Cin][Cout].
 
-    def __init__(self, arena: torch.Tensor, weights, dgrad=True):
+    ``refresh()`` transforms every LIVE set in at most two launches per weight update.  The convs take
+    the sets through ``lazy(kind, l)`` callables, which the autotuned conv calls only when a Winograd
+    candidate of that kind runs: a set that is not fresh this step is transformed on demand (always
+    correct), and ``end_step()`` narrows the live sets to the ones the tuned convs actually used, so a
+    step pays only for the transforms it needs (outside graph capture; the captured step replays the
+    narrowed refresh)."""
+
+    KINDS = ('u2', 'ut2', 'u4', 'ut4')
+
+    def __init__(self, arena: torch.Tensor, weights, dgrad=True, f4=None, hw=None):
+        """hw[l]: the layer's map size (F(4x4) sets only where it is a multiple of 4; None: every layer)."""
         self.arena = arena
         self.weights = list(weights)
         self.dgrad = dgrad
-        self._off, meta, desc, off = [], [], [], 0
+        f4 = WINO4 if f4 is None else f4
+        self._layers, self._sets, off = [], {}, 0
         for l, w in enumerate(self.weights):
             Cout = w.shape[0]
             Cin = w.numel() // (9 * Cout)
-            n = 16 * Cout * Cin
             so = (w.data_ptr() - arena.data_ptr()) // 4
             assert 0 <= so and so + w.numel() <= arena.numel() and w.is_contiguous()
-            self._off.append((off, n, Cout, Cin))
-            meta.append([so, off, off + n if dgrad else -1, Cout, Cin])
-            for co0 in range(0, Cout, 32):
-                for ci0 in range(0, Cin, 32):
-                    desc.append([l, co0, ci0, 0])
-            off += n * (2 if dgrad else 1)
+            self._layers.append((so, Cout, Cin))
+            kinds = ['u2'] + (['ut2'] if dgrad else [])
+            if f4 and (hw is None or hw[l] % 4 == 0):
+                kinds += ['u4'] + (['ut4'] if dgrad else [])
+            for k in kinds:
+                n = (16 if k.endswith('2') else 36) * Cout * Cin
+                self._sets[(k, l)] = (off, n)
+                off += n
         dev = arena.device
         self.buf = torch.zeros(max(off, 1), dtype=torch.float32, device=dev)
-        self.meta = torch.tensor(meta, dtype=torch.int64, device=dev).reshape(-1)
-        self.desc = torch.tensor(desc, dtype=torch.int32, device=dev).reshape(-1)
-        self.nblocks = len(desc)
+        self._tables = {}
+        self.live = frozenset(self._sets)
+        self._fresh = set()
+        self._used = set()
+        self._prepare(self.live)
+
+    # ---- transform tables: one (desc, meta) pair per kernel family for a set of live sets
+    def _prepare(self, live):
+        if live in self._tables:
+            return self._tables[live]
+        out = []
+        for fam, width in (('2', 16), ('4', 36)):
+            meta, desc, idx = [], [], {}
+            for l, (so, Cout, Cin) in enumerate(self._layers):
+                u = self._sets.get(('u' + fam, l)) if ('u' + fam, l) in live else None
+                ut = self._sets.get(('ut' + fam, l)) if ('ut' + fam, l) in live else None
+                if u is None and ut is None:
+                    continue
+                idx[l] = len(meta)
+                meta.append([so, u[0] if u else -1, ut[0] if ut else -1, Cout, Cin])
+                for co0 in range(0, Cout, 32):
+                    for ci0 in range(0, Cin, 32):
+                        desc.append([idx[l], co0, ci0, 0])
+            if desc:
+                dev = self.arena.device
+                out.append((fam, torch.tensor(desc, dtype=torch.int32, device=dev).reshape(-1),
+                            torch.tensor(meta, dtype=torch.int64, device=dev).reshape(-1), len(desc)))
+        self._tables[live] = out
+        return out
 
     def refresh(self):
-        _lib.call("rk_wino_weights_multi", _p(self.arena), _p(self.buf), _p(self.desc), self.nblocks, _p(self.meta),
-                  _s())
+        for fam, desc, meta, nb in self._prepare(self.live):
+            name = "rk_wino_weights_multi" if fam == '2' else "rk_wino4_weights_multi"
+            _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
+        self._fresh = set(self.live)
+
+    def end_step(self):
+        """Narrow the live sets to the ones this step's convs used (no-op inside graph capture)."""
+        used, self._used = frozenset(self._used), set()
+        if not used or used == self.live:
+            return
+        try:
+            capturing = torch.cuda.is_current_stream_capturing()
+        except Exception:
+            capturing = False
+        if not capturing:
+            self._prepare(used)
+            self.live = used
+
+    def _view(self, kind, l):
+        off, n = self._sets[(kind, l)]
+        _, Cout, Cin = self._layers[l]
+        pos = 16 if kind.endswith('2') else 36
+        shape = (pos, Cout, Cin) if kind.startswith('u') and not kind.startswith('ut') else (pos, Cin, Cout)
+        return self.buf[off:off + n].view(shape)
+
+    def _ensure(self, kind, l):
+        if (kind, l) not in self._fresh:   # not refreshed this step: transform this layer's set now
+            so, Cout, Cin = self._layers[l]
+            w = self.arena[so:so + 9 * Cout * Cin]
+            v = self._view(kind, l)
+            name = "rk_wino_weights" if kind.endswith('2') else "rk_wino4_weights"
+            if kind.startswith('ut'):
+                _lib.call(name, _p(w), None, _p(v), Cout, Cin, _s())
+            else:
+                _lib.call(name, _p(w), _p(v), None, Cout, Cin, _s())
+            self._fresh.add((kind, l))
+        self._used.add((kind, l))
+        return self._view(kind, l)
+
+    def has(self, kind, l):
+        return (kind, l) in self._sets
+
+    def lazy(self, kind, l):
+        """Callable returning the fresh set (or None when the layer has no such set)."""
+        if (kind, l) not in self._sets:
+            return None
+        return lambda: self._ensure(kind, l)
 
     def u(self, l):
-        off, n, Cout, Cin = self._off[l]
-        return self.buf[off:off + n].view(16, Cout, Cin)
+        return self._view('u2', l)
 
     def ut(self, l):
-        off, n, Cout, Cin = self._off[l]
         assert self.dgrad
-        return self.buf[off + n:off + 2 * n].view(16, Cin, Cout)
+        return self._view('ut2', l)
+
+    def u4(self, l):
+        return self._view('u4', l) if ('u4', l) in self._sets else None
+
+    def ut4(self, l):
+        return self._view('ut4', l) if ('ut4', l) in self._sets else None
 
 
 # ----------------------------------------------------------------------------------------- dense
@@ -838,7 +1063,7 @@ def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=
 
     def run(cfg):
         tile, nst, s = cfg
-        if cfg in WINO_CFGS:
+        if cfg in WINO_CFGS or cfg in WINO4_CFGS:
             extra(cfg)
             return
         if s == 1:
@@ -851,15 +1076,16 @@ def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=
         sreduce_epi(slab, G * M, N, out.view(G * M, N), bias=bias, act=act, slope=slope, bias_rows=M)
     cands = [c for c in _cands(M * G, N, splittable=N % 4 == 0, K=K) if c[0] < 4]
     if extra is not None:
-        cands.extend(WINO_CFGS)
+        cands.extend(getattr(extra, 'cfgs', WINO_CFGS))
     run(_pick(key, cands, run))
     return out
 
 
-def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=None):
+def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=None, wino4=None):
     """k convs in one launch: x [G, Nb, H, W, Cin] (or [Nb, H, W, Cin] shared by every group),
     W [G, Cout, taps*Cin], bias [G, Cout] -> [G, Nb, H, W, Cout] (3x3 stride-1 or 1x1).
-    ``wino``: stacked Winograd weights [G, 16, Cout, Cin] -> grouped fused F(2x2,3x3) candidates."""
+    ``wino``: stacked Winograd weights [G, 16, Cout, Cin] -> grouped fused F(2x2,3x3) candidates;
+    ``wino4``: [G, 36, Cout, Cin] -> grouped F(4x4,3x3) candidates."""
     G, Cout, K = W.shape
     shared = x.dim() == 4
     Nb, H, Wd, Cin = x.shape[-4:]
@@ -870,12 +1096,20 @@ def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=Non
     if out is None:
         out = torch.empty((G, Nb, H, Wd, Cout), device=x.device, dtype=torch.float32)
     extra = None
-    if wino is not None and taps == 9 and wino_ok(H, Wd, Cin) and act in (ACT_NONE, ACT_RELU):
-        assert wino.shape == (G, 16, Cout, Cin) and wino.is_contiguous()
+    w2 = wino is not None and taps == 9 and wino_ok(H, Wd, Cin) and act in (ACT_NONE, ACT_RELU)
+    w4 = wino4 is not None and taps == 9 and wino4_ok(H, Wd, Cin) and act in (ACT_NONE, ACT_RELU)
+    if w2 or w4:
+        assert not w2 or (wino.shape == (G, 16, Cout, Cin) and wino.is_contiguous())
+        assert not w4 or (wino4.shape == (G, 36, Cout, Cin) and wino4.is_contiguous())
+
         def extra(cfg):
-            wino_conv_grp(x, wino, out=out, bias=bias, relu=act == ACT_RELU, variant=-1 - cfg[0])
+            if cfg in WINO4_CFGS:
+                wino4_conv_grp(x, wino4, out=out, bias=bias, relu=act == ACT_RELU, variant=-5 - cfg[0])
+            else:
+                wino_conv_grp(x, wino, out=out, bias=bias, relu=act == ACT_RELU, variant=-1 - cfg[0])
+        extra.cfgs = (WINO_CFGS if w2 else ()) + (WINO4_CFGS if w4 else ())
     return _grp_run(0, x, W, out, M, Cout, K, Cin, K, G, 0 if shared else M * Cin,
-                    ('sfg', G, M, Cout, K, H, Wd, Cin, shared, bias is not None, act, extra is not None), bias=bias,
+                    ('sfg', G, M, Cout, K, H, Wd, Cin, shared, bias is not None, act, w2, w4), bias=bias,
                     act=act, slope=slope, geo=dict(H=H, W=Wd, C=Cin, taps=taps), extra=extra)
 
 

@@ -1,0 +1,188 @@
+"""Fused Winograd F(4x4,3x3) fp32 conv (csrc/kernels/winograd4.hip) vs fp64 PyTorch references.
+
+F(4x4,3x3)'s transforms have coefficients up to 8 (A^T) and 5 (B^T), so its fp32 round-off is about
+ten times F(2x2)'s (profiles/winograd_error_r2.jsonl); the gate is 3e-5 relative Frobenius error,
+against ~1e-6 measured."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+TOL = 3e-5
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _rand(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).float()
+
+
+def _conv_ref(x_nhwc, w_ohwi):
+    return TF.conv2d(x_nhwc.double().permute(0, 3, 1, 2), w_ohwi.double().permute(0, 3, 1, 2),
+                     padding=1).permute(0, 2, 3, 1)
+
+
+def _w2(w):
+    return w.to(DEV).reshape(w.shape[0], -1).contiguous()
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [
+    (2, 8, 8, 16, 32), (3, 4, 12, 24, 40), (4, 32, 32, 64, 64), (8, 4, 4, 512, 512), (2, 4, 4, 8, 72),
+    (5, 16, 16, 128, 128), (1, 12, 20, 8, 8), (3, 8, 8, 256, 96)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino4_fwd_and_stats(N, H, W, Cin, Cout, variant):
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=1)
+    w = _rand(Cout, 3, 3, Cin, seed=2, scale=1.0 / math.sqrt(9 * Cin))
+    u = S.wino4_u(_w2(w))
+    acc = torch.zeros((S.bn_slots(Cout), 2, Cout), dtype=torch.float64, device=DEV)
+    y = S.wino4_conv(x.to(DEV), u, stats=acc, variant=variant)
+    torch.cuda.synchronize()
+    ref = _conv_ref(x, w)
+    assert rel(y, ref) < TOL
+    s = acc.sum(0).cpu()
+    r = ref.reshape(-1, Cout)
+    assert rel(s[0], r.sum(0)) < TOL and rel(s[1], (r * r).sum(0)) < TOL
+
+
+def test_wino4_bias_relu():
+    from rafiki_amd.ops import f32 as S
+    x = _rand(3, 8, 8, 32, seed=3)
+    w = _rand(48, 3, 3, 32, seed=4, scale=0.1)
+    b = _rand(48, seed=5)
+    y = S.wino4_conv(x.to(DEV), S.wino4_u(_w2(w)), bias=b.to(DEV), relu=True)
+    torch.cuda.synchronize()
+    assert rel(y, torch.relu(_conv_ref(x, w) + b.double())) < TOL
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 16, 16, 64, 64), (8, 4, 4, 512, 256),
+                                            (2, 4, 8, 24, 16)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino4_dgrad_from_flipped_set(N, H, W, Cin, Cout, variant):
+    """dx = conv(dy, flip(w)^T) from the ut set."""
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=6)
+    w = _rand(Cout, 3, 3, Cin, seed=7, scale=0.1)
+    dy = _rand(N, H, W, Cout, seed=8)
+    dx = S.wino4_conv(dy.to(DEV), S.wino4_ut(_w2(w)), variant=variant)
+    torch.cuda.synchronize()
+    xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    out = TF.conv2d(xd, w.double().permute(0, 3, 1, 2), padding=1)
+    (gx,) = torch.autograd.grad(out, xd, dy.double().permute(0, 3, 1, 2))
+    assert rel(dx, gx.permute(0, 2, 3, 1)) < TOL
+
+
+@pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("H", [8, 4])
+def test_wino4_dgrad_bn_epilogues_match_direct(pool, variant, H):
+    """The BNB / BNP epilogues give the same dx and BN-backward sums as the direct kernel's."""
+    from rafiki_amd.ops import f32 as S
+    N, W, Cin, Cout = 4, H, 64, 128
+    Hy, Wy = (2 * H, 2 * W) if pool else (H, W)
+    y = _rand(N, Hy, Wy, Cin, seed=17) + 0.2
+    gamma, beta = torch.ones(Cin) * 1.3, _rand(Cin, seed=18) * 0.1
+    acc = torch.zeros((S.bn_slots(Cin), 2, Cin), dtype=torch.float64, device=DEV)
+    S.col_stats(y.to(DEV).view(-1, Cin), acc)
+    _, coeffs = S.bn_fwd(y.to(DEV), acc, N * Hy * Wy, gamma.to(DEV), beta.to(DEV), 1e-5, pool=pool, act=1)
+    w = _rand(Cout, 3, 3, Cin, seed=19, scale=0.05)
+    arena = w.reshape(-1).to(DEV).contiguous()
+    wt = S.SConvWT(arena, [arena.view(Cout, 3, 3, Cin)])
+    wt.refresh()
+    ut = S.wino4_ut(_w2(w))
+    dyo = _rand(N, H, W, Cout, seed=20).to(DEV)
+    acc_w, acc_d = torch.zeros_like(acc), torch.zeros_like(acc)
+    key = 'bnp' if pool else 'bnb'
+    d_w = S.wino4_conv(dyo, ut, variant=variant, **{key: (y.to(DEV), coeffs, acc_w)})
+    d_d = S.conv_dgrad(dyo, wt.view(0), **{key: (y.to(DEV), coeffs, acc_d)})
+    torch.cuda.synchronize()
+    assert rel(d_w, d_d) < TOL
+    assert rel(acc_w.sum(0), acc_d.sum(0)) < TOL
+
+
+@pytest.mark.parametrize("shared", [True, False])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino4_conv_grouped(shared, variant):
+    """k convs in one grid (the serving ensemble's layers) == k separate convs."""
+    from rafiki_amd.ops import f32 as S
+    G, Nb, H, Cin, Cout = 3, 5, 8, 32, 48
+    x = (_rand(Nb, H, H, Cin, seed=40) if shared else _rand(G, Nb, H, H, Cin, seed=40)).to(DEV)
+    w = [_rand(Cout, 3, 3, Cin, seed=41 + g, scale=0.1) for g in range(G)]
+    u = torch.stack([S.wino4_u(_w2(wg)) for wg in w]).contiguous()
+    b = _rand(G, Cout, seed=45).to(DEV)
+    y = S.wino4_conv_grp(x, u, bias=b, relu=True, variant=variant)
+    torch.cuda.synchronize()
+    for g in range(G):
+        xg = x if shared else x[g]
+        ref = torch.relu(_conv_ref(xg.cpu(), w[g]) + b[g].double().cpu())
+        assert rel(y[g], ref) < TOL
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 32, 32, 64, 64), (16, 4, 4, 256, 512),
+                                            (3, 4, 12, 24, 40), (2, 4, 4, 16, 16)])
+@pytest.mark.parametrize("splits", [1, 2, 5])
+def test_wino4_wgrad(N, H, W, Cin, Cout, splits):
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=30)
+    dy = _rand(N, H, W, Cout, seed=31)
+    nt = N * (H // 4) * (W // 4)
+    tps = -(-(-(-nt // splits)) // 8) * 8
+    s_eff = -(-nt // tps)
+    dw = torch.empty(Cout, 9 * Cin, device=DEV)
+    S.wino4_wgrad(dy.to(DEV), x.to(DEV), dw, splits=s_eff)
+    prev = _rand(Cout, 9 * Cin, seed=32).to(DEV)
+    acc = prev.clone()
+    S.wino4_wgrad(dy.to(DEV), x.to(DEV), acc, splits=s_eff, accumulate=True)
+    torch.cuda.synchronize()
+    wd = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    out = TF.conv2d(x.double().permute(0, 3, 1, 2), wd, padding=1)
+    (gw,) = torch.autograd.grad(out, wd, dy.double().permute(0, 3, 1, 2))
+    ref = gw.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+    assert rel(dw, ref) < TOL
+    assert rel(acc, ref + prev.double().cpu()) < TOL
+
+
+def test_wino_weights_live_sets_and_on_demand_transform():
+    """WinoWeights narrows its per-step refresh to the sets the convs used; a set outside the live
+    group is transformed on demand, so every lazy() read sees the current weights."""
+    from rafiki_amd.ops import f32 as S
+    shapes = [(64, 32), (16, 64), (40, 24)]
+    arena = torch.zeros(sum(co * 9 * ci for co, ci in shapes) + 5, device=DEV)
+    ws, off = [], 5
+    for k, (co, ci) in enumerate(shapes):
+        w = arena[off:off + co * 9 * ci].view(co, 9 * ci)
+        w.copy_(_rand(co, 9 * ci, seed=50 + k).to(DEV))
+        ws.append(w)
+        off += co * 9 * ci
+    ww = S.WinoWeights(arena, ws, hw=[8, 6, 4])
+    assert not ww.has('u4', 1) and ww.has('ut4', 2)
+    ww.refresh()
+    for l, w in enumerate(ws):
+        assert torch.equal(ww.lazy('u2', l)(), S.wino_u(w))
+        assert torch.equal(ww.lazy('ut2', l)(), S.wino_ut(w))
+        if ww.has('u4', l):
+            assert torch.equal(ww.lazy('u4', l)(), S.wino4_u(w))
+            assert torch.equal(ww.lazy('ut4', l)(), S.wino4_ut(w))
+    ww.end_step()
+    # a step that only uses layer 0's F(4x4) forward set and layer 2's F(2x2) gradient set
+    ww.refresh()
+    ww.lazy('u4', 0)()
+    ww.lazy('ut2', 2)()
+    ww.end_step()
+    assert ww.live == frozenset({('u4', 0), ('ut2', 2)})
+    for w in ws:
+        w.mul_(-0.5).add_(0.25)
+    ww.refresh()
+    torch.cuda.synchronize()
+    assert torch.equal(ww.u4(0), S.wino4_u(ws[0]))
+    assert torch.equal(ww.ut(2), S.wino_ut(ws[2]))
+    assert not torch.equal(ww.u(1), S.wino_u(ws[1]))          # not live: stale until asked for
+    assert torch.equal(ww.lazy('u2', 1)(), S.wino_u(ws[1]))   # on-demand transform
+    assert torch.equal(ww.lazy('ut4', 2)(), S.wino4_ut(ws[2]))
