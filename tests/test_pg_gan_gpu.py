@@ -279,7 +279,23 @@ def test_colsum_tall(fn):
 def test_dp_round_with_rccl_allreduce_is_graph_captured():
     """Single-GPU rehearsal of the data-parallel round: a 1-rank RCCL group with the bucketed
     all-reduce forced on.  The rounds (backward hooks launching async all-reduces, waits, averaging,
-    Adam) are captured into hipGraphs and replayed, and training matches the no-collective run."""
+    Adam) are captured into hipGraphs and replayed, and training matches the no-collective run.
+
+    Runs in a fresh child process: the RCCL communicator, its watchdog thread and the graph pools
+    then start from a clean state instead of inheriting the rest of the suite's (one extra process
+    on the GPU, bounded by a timeout)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = "import sys; sys.path.insert(0, {!r}); import test_pg_gan_gpu as t; t._dp_round_child(); print('DP-OK')"
+    r = subprocess.run([sys.executable, '-c', code.format(here)], cwd=os.path.dirname(here), capture_output=True,
+                       text=True, timeout=100)
+    assert r.returncode == 0 and 'DP-OK' in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def _dp_round_child():
+    """Body of test_dp_round_with_rccl_allreduce_is_graph_captured (runs in a child process)."""
     import socket
     import torch.distributed as dist
     from rafiki_amd.models.pg_gan import PgGan
