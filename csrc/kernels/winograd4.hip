@@ -85,24 +85,58 @@ RK_DEV void g6(float g0, float g1, float g2, float (&u)[6]) {
   u[5] = g2;
 }
 
-RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) {
+// F(2x2,3x3) counterparts (interpolation points 0, 1, -1, inf): B^T d of a 4-vector, A^T m -> 2 outputs
+RK_DEV void bt4(float d0, float d1, float d2, float d3, float (&t)[4]) {
+  t[0] = d0 - d2;
+  t[1] = d1 + d2;
+  t[2] = d2 - d1;
+  t[3] = d1 - d3;
+}
+RK_DEV void at4(float m0, float m1, float m2, float m3, float (&o)[2]) {
+  o[0] = m0 + m1 + m2;
+  o[1] = m1 - m2 - m3;
+}
+
+// B^T / A^T of one window line (A = MO + 2 values, stride-strided in r) for output tile size MO
+template <int MO>
+RK_DEV void bt_line(const float* r, int stride, float (&o)[MO + 2]) {
+  if constexpr (MO == 4)
+    bt6(r[0], r[stride], r[2 * stride], r[3 * stride], r[4 * stride], r[5 * stride], o);
+  else
+    bt4(r[0], r[stride], r[2 * stride], r[3 * stride], o);
+}
+template <int MO>
+RK_DEV void at_line(const float (&m)[MO + 2], float (&o)[MO]) {
+  if constexpr (MO == 4)
+    at6(m[0], m[1], m[2], m[3], m[4], m[5], o);
+  else
+    at4(m[0], m[1], m[2], m[3], o);
+}
+
+template <int MO>
+RK_DEV void w_tile_of(const W4Params& p, int t, int& n, int& oy, int& ox) {
   n = t / p.THW;
   const int r = t - n * p.THW;
   const int ty = r / p.TW;
-  oy = 4 * ty;
-  ox = 4 * (r - ty * p.TW);
+  oy = MO * ty;
+  ox = MO * (r - ty * p.TW);
 }
+RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) { w_tile_of<4>(p, t, n, oy, ox); }
 
-template <int WM, int WN, int MINW>
-__global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4Params p) {
+// MO = 4: F(4x4,3x3), u [36][N][C]; MO = 2: F(2x2,3x3) on the same small-wave-tile layout (16 tiles x 16
+// channels per wave, 16 accumulators), u [16][N][C] — the variant for small grids (deep 8x8 / 4x4 maps)
+template <int MO, int WM, int WN, int MINW>
+__global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4Params p) {
+  constexpr int A = MO + 2;                // window / transformed tile side
+  constexpr int P = A * A;                 // Winograd positions
   constexpr int NT = 64 * WM * WN;         // threads
   constexpr int T = 16 * WM;               // tiles per block
   constexpr int BNC = 16 * WN;             // output channels per block
   constexpr int IT = T * KC / NT;          // input windows per thread and chunk
-  constexpr int UL = 36 * BNC * 4 / NT;    // f32x2 weight loads per thread and chunk
-  static_assert(IT >= 1 && IT * NT == T * KC && UL * NT == 36 * BNC * 4, "tile shape");
-  __shared__ __attribute__((aligned(16))) float Vs[36][T][KC];
-  __shared__ __attribute__((aligned(16))) float Us[36][BNC][KC];
+  constexpr int UL = P * BNC * 4 / NT;    // f32x2 weight loads per thread and chunk
+  static_assert(IT >= 1 && IT * NT == T * KC && UL * NT == P * BNC * 4, "tile shape");
+  __shared__ __attribute__((aligned(16))) float Vs[P][T][KC];
+  __shared__ __attribute__((aligned(16))) float Us[P][BNC][KC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int b0 = xcd_remap(blockIdx.x, gridDim.x);
@@ -115,19 +149,19 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4P
   const float* const gbp = p.bias ? p.bias + grp * p.gbias : nullptr;
 
   // loader role: windows (tile lt + NT/8 h, channel lc); byte offset of the tile origin pixel and the
-  // in-image row / column masks of the 6x6 window (rows oy-1 .. oy+4)
+  // in-image row / column masks of the A x A window (rows oy-1 .. oy+A-2)
   const int lt = tid >> 3, lc = tid & 7;
   unsigned vb[IT], rmk[IT], cmk[IT];
 #pragma unroll
   for (int h = 0; h < IT; ++h) {
     int ln, loy, lox;
     const int t = tbase + lt + NT / 8 * h;
-    w4_tile(p, t, ln, loy, lox);
+    w_tile_of<MO>(p, t, ln, loy, lox);
     const bool lok = t < p.ntiles;
     vb[h] = lok ? (unsigned)((((ln * p.H + loy) * p.W + lox) * p.C + lc) * 4) : 0u;
     rmk[h] = cmk[h] = 0;
 #pragma unroll
-    for (int a = 0; a < 6; ++a) {
+    for (int a = 0; a < A; ++a) {
       if (lok && loy - 1 + a >= 0 && loy - 1 + a < p.H) rmk[h] |= 1u << a;
       if (lox - 1 + a >= 0 && lox - 1 + a < p.W) cmk[h] |= 1u << a;
     }
@@ -140,20 +174,20 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4P
   const unsigned ub = cbase + uco < p.N ? (unsigned)(((upos * p.N + cbase + uco) * p.C + 2 * upr) * 4) : OOB;
   const int ustride = UPK * p.N * p.C * 4;
 
-  float raw[IT][36];
+  float raw[IT][P];
   f32x2 ur[UL];
   auto load = [&](int c0) {
     const __amdgpu_buffer_rsrc_t xr = rsrc(gxp + c0, p.xbytes - 4ull * c0);
     const __amdgpu_buffer_rsrc_t urs = rsrc(gup + c0, p.ubytes - 4ull * c0);
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
-      // opaque copies: the 36 window offsets are rebuilt per chunk from 3 registers instead of being
+      // opaque copies: the P window offsets are rebuilt per chunk from 3 registers instead of being
       // hoisted out of the K loop into 36 live registers
       unsigned b = vb[h], rm = rmk[h], cm = cmk[h];
       asm volatile("" : "+v"(b), "+v"(rm), "+v"(cm));
 #pragma unroll
-      for (int i = 0; i < 36; ++i) {
-        const int a = i / 6, bb = i % 6;
+      for (int i = 0; i < P; ++i) {
+        const int a = i / A, bb = i % A;
         const int d = (((a - 1) * p.W) + bb - 1) * p.C * 4;
         const unsigned in = (rm >> a) & (cm >> bb) & 1u;
         const unsigned off = (b + (unsigned)d) | ((in ^ 1u) << 31);
@@ -170,27 +204,27 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4P
       const int row = lt + NT / 8 * h, c = lc ^ swz(row);
       float* const r = raw[h];
 #pragma unroll
-      for (int bb = 0; bb < 6; ++bb) {     // B^T d along rows, in place
-        float o[6];
-        bt6(r[bb], r[6 + bb], r[12 + bb], r[18 + bb], r[24 + bb], r[30 + bb], o);
+      for (int bb = 0; bb < A; ++bb) {     // B^T d along rows, in place
+        float o[A];
+        bt_line<MO>(r + bb, A, o);
 #pragma unroll
-        for (int a = 0; a < 6; ++a) r[a * 6 + bb] = o[a];
+        for (int a = 0; a < A; ++a) r[a * A + bb] = o[a];
       }
 #pragma unroll
-      for (int a = 0; a < 6; ++a) {        // (B^T d) B along columns, straight to LDS
-        float o[6];
-        bt6(r[a * 6 + 0], r[a * 6 + 1], r[a * 6 + 2], r[a * 6 + 3], r[a * 6 + 4], r[a * 6 + 5], o);
+      for (int a = 0; a < A; ++a) {        // (B^T d) B along columns, straight to LDS
+        float o[A];
+        bt_line<MO>(r + a * A, 1, o);
 #pragma unroll
-        for (int bb = 0; bb < 6; ++bb) Vs[a * 6 + bb][row][c] = o[bb];
+        for (int bb = 0; bb < A; ++bb) Vs[a * A + bb][row][c] = o[bb];
       }
     }
 #pragma unroll
     for (int k = 0; k < UL; ++k) *(f32x2*)&Us[upos + UPK * k][uco][(2 * upr) ^ swz(uco)] = ur[k];
   };
 
-  f32x4 acc[36];
+  f32x4 acc[P];
 #pragma unroll
-  for (int q = 0; q < 36; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < P; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nch = p.C / KC;
   load(0);
@@ -202,7 +236,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4P
     if (c + 1 < nch) load((c + 1) * KC);
     // four positions at a time: 4 independent MFMAs between dependent ones
 #pragma unroll
-    for (int q = 0; q < 36; q += 4) {
+    for (int q = 0; q < P; q += 4) {
       f32x2 a[4], bv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -232,24 +266,29 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4P
   float s = 0.f, ss = 0.f;
   const int t0 = tbase + wm * 16 + (lane >> 4) * 4;
   int im, oy, ox;
-  w4_tile(p, t0, im, oy, ox);
+  w_tile_of<MO>(p, t0, im, oy, ox);
   const __amdgpu_buffer_rsrc_t yr = rsrc(gyp, p.ybytes);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const bool tok = t0 + r < p.ntiles;
-    float tt[6][4];
+    float tt[A][MO];
 #pragma unroll
-    for (int a = 0; a < 6; ++a)            // M A: along columns
-      at6(acc[a * 6 + 0][r], acc[a * 6 + 1][r], acc[a * 6 + 2][r], acc[a * 6 + 3][r], acc[a * 6 + 4][r],
-          acc[a * 6 + 5][r], tt[a]);
+    for (int a = 0; a < A; ++a) {          // M A: along columns
+      float m[A];
+#pragma unroll
+      for (int bb = 0; bb < A; ++bb) m[bb] = acc[a * A + bb][r];
+      at_line<MO>(m, tt[a]);
+    }
     if (tok && nok) {
       const int pix = (im * p.H + oy) * p.W + ox;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float o[4];                        // A^T (M A): along rows
-        at6(tt[0][j], tt[1][j], tt[2][j], tt[3][j], tt[4][j], tt[5][j], o);
+      for (int j = 0; j < MO; ++j) {
+        float m[A], o[MO];                 // A^T (M A): along rows
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int a = 0; a < A; ++a) m[a] = tt[a][j];
+        at_line<MO>(m, o);
+#pragma unroll
+        for (int i = 0; i < MO; ++i) {
           float v = o[i];
           const int idx = (pix + i * p.W + j) * p.N + n;
           if (fl & WF_BIAS) v += bs;
@@ -283,10 +322,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_fwd_kernel(const W4P
         }
       }
     }
-    ox += 4;                               // next tile in row-major tile order
+    ox += MO;                              // next tile in row-major tile order
     if (ox >= p.W) {
       ox = 0;
-      oy += 4;
+      oy += MO;
       if (oy >= p.H) {
         oy = 0;
         ++im;
@@ -604,15 +643,15 @@ extern "C" int rk_wino4_weights_multi(const float* arena, float* dst, const int*
   return RK_OK;
 }
 
-// y = conv3x3(x, w) via F(4x4,3x3) with u = rk_wino4_weights(w); flags / grouping as rk_wino_conv_grp.
-// variant 0: 8 waves, 64 tiles x 32 channels (1 block per CU); 1: 4 waves, 32 x 32 (2 per CU)
-extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const float* bias, double* stats,
-                                 int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
-                                 int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
-                                 void* stream) {
-  if (variant != 0 && variant != 1) return RK_EBADARG;
-  const int T = variant ? 32 : 64, BNC = 32;
-  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || C <= 0 || (C % KC) || N <= 0 || groups <= 0)
+namespace {
+// shared launcher of the small-wave-tile Winograd forward kernels: MO = 4 (u [36][N][C], H, W multiples
+// of 4) or MO = 2 (u [16][N][C], even H, W); T tiles x BNC channels per block of NT threads
+template <int MO, int WM, int WN, int MINW>
+int launch_gfwd(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
+                const float* gate, int Nb, int H, int W, int C, int N, int flags, int groups, long long gx,
+                long long gu, long long gy, long long gbias, void* stream) {
+  constexpr int T = 16 * WM, BNC = 16 * WN, P = (MO + 2) * (MO + 2);
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H % MO) || (W % MO) || C <= 0 || (C % KC) || N <= 0 || groups <= 0)
     return RK_EBADARG;
   if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
   if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
@@ -621,14 +660,14 @@ extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const
   W4Params p;
   p.x = x; p.u = u; p.y = y; p.bias = bias; p.stats = stats; p.gate = gate;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.N = N;
-  p.TW = W / 4;
-  p.THW = (H / 4) * (W / 4);
+  p.TW = W / MO;
+  p.THW = (H / MO) * (W / MO);
   const long long nt = (long long)Nb * p.THW;
   if (nt >= (1LL << 30)) return RK_EBADARG;
   p.ntiles = (int)nt;
   p.ncb = rk_cdiv(N, BNC);
   p.xbytes = 4ull * Nb * H * W * C;
-  p.ubytes = 144ull * N * C;
+  p.ubytes = 4ull * P * N * C;
   p.ybytes = 4ull * Nb * H * W * N;
   const unsigned long long gbytes = (flags & WF_BNP) ? 4 * p.ybytes : p.ybytes;
   if (p.xbytes >= 0x7fffffffull || p.ubytes >= 0x7fffffffull || gbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
@@ -639,12 +678,41 @@ extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const
   const long long blocks = bpg * groups;
   if (blocks >= (1LL << 31)) return RK_EBADARG;
   p.bpg = (int)bpg;
-  if (variant)
-    hipLaunchKernelGGL((wino4_fwd_kernel<2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
-  else
-    hipLaunchKernelGGL((wino4_fwd_kernel<4, 2, 1>), dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
+  hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW>), dim3((unsigned)blocks), dim3(64 * WM * WN), 0,
+                     (hipStream_t)stream, p);
   RK_LAUNCH_CHECK();
   return RK_OK;
+}
+}  // namespace
+
+// y = conv3x3(x, w) via F(4x4,3x3) with u = rk_wino4_weights(w); flags / grouping as rk_wino_conv_grp.
+// variant 0: 8 waves, 64 tiles x 32 channels (1 block per CU); 1: 4 waves, 32 x 32 (2 per CU)
+extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const float* bias, double* stats,
+                                 int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
+                                 int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
+                                 void* stream) {
+  if (variant == 0)
+    return launch_gfwd<4, 4, 2, 1>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
+                                   gbias, stream);
+  if (variant == 1)
+    return launch_gfwd<4, 2, 2, 2>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
+                                   gbias, stream);
+  return RK_EBADARG;
+}
+
+// F(2x2,3x3) with u = rk_wino_weights(w) [16][N][C] on small wave tiles (many blocks for small grids):
+// variant 0: 4 waves, 32 tiles x 32 channels (32 KiB LDS, 3 blocks per CU); 1: 2 waves, 16 x 32
+extern "C" int rk_wino2s_conv_grp(const float* x, const float* u, float* y, const float* bias, double* stats,
+                                  int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
+                                  int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
+                                  void* stream) {
+  if (variant == 0)
+    return launch_gfwd<2, 2, 2, 3>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
+                                   gbias, stream);
+  if (variant == 1)
+    return launch_gfwd<2, 1, 2, 3>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
+                                   gbias, stream);
+  return RK_EBADARG;
 }
 
 extern "C" int rk_wino4_conv(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,

@@ -159,7 +159,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
             return
         if cfg in WINO_CFGS:
             wino_conv(x, wino() if callable(wino) else wino, out=out, bias=bias, stats=stats_acc,
-                      relu=act == ACT_RELU, variant=-1 - cfg[0])
+                      relu=act == ACT_RELU, variant=_wino_variant(cfg))
             return
         if s == 1:
             sgemm(KIND_CONV, x, w, out, M, Cout, K, Cin, K, Cout, tile=tile, nst=nst, bias=bias, stats=stats_acc,
@@ -219,7 +219,7 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
             wino4_conv(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, variant=-5 - cfg[0])
             return
         if cfg in WINO_CFGS:
-            wino_conv(dy, wino() if callable(wino) else wino, out=out, bnb=bnb, bnp=bnp, variant=-1 - cfg[0])
+            wino_conv(dy, wino() if callable(wino) else wino, out=out, bnb=bnb, bnp=bnp, variant=_wino_variant(cfg))
             return
         sgemm(KIND_CONV, dy, wt() if callable(wt) else wt, out, M, Cin, K, Cout, K, Cin, tile=cfg[0], nst=cfg[1], bias=bias, stats=stats,
               gate=gate, H=H, W=W, C=Cout, taps=taps, flags=flags)
@@ -312,8 +312,13 @@ class SConvWT:
 # -------------------------------------------------------------------- Winograd F(2x2, 3x3) convs
 WF_RELU, WF_BIAS, WF_STATS, WF_BNB, WF_BNP = 1, 2, 4, 512, 1024
 WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
-# autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1)
-WINO_CFGS = ((-1, 0, 1), (-2, 0, 1))
+# autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1),
+# and the small-wave-tile kernels for small grids: 4-wave 32x32 (variant 2) / 2-wave 16x32 (variant 3)
+WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1))
+
+
+def _wino_variant(cfg):
+    return {-1: 0, -2: 1, -8: 2, -9: 3}[cfg[0]]
 
 
 def wino_ok(H: int, W: int, C: int) -> bool:
@@ -376,6 +381,10 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
         bias, flags = coeffs[2:4].reshape(-1), WF_BNP
     if stats is not None:
         assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
+    if variant >= 2:   # the small-wave-tile F(2x2) kernels (csrc/kernels/winograd4.hip): small grids
+        _lib.call("rk_wino2s_conv_grp", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
+                  Nb, H, W, C, N, flags, int(variant) - 2, 1, 0, 0, 0, 0, _s())
+        return out
     _lib.call("rk_wino_conv", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
               Nb, H, W, C, N, flags, int(variant), _s())
     return out
@@ -554,8 +563,9 @@ def wino_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
         out = torch.empty((G, Nb, H, W, N), device=x.device, dtype=torch.float32)
     M = Nb * H * W
     flags = (WF_BIAS if bias is not None else 0) | (WF_RELU if relu else 0)
-    _lib.call("rk_wino_conv_grp", _p(x), _p(u), _p(out), _p(bias), None, 0, None, Nb, H, W, C, N, flags,
-              int(variant), G, 0 if shared else M * C, 16 * N * C, M * N, N if bias is not None else 0, _s())
+    name, v = ("rk_wino2s_conv_grp", int(variant) - 2) if variant >= 2 else ("rk_wino_conv_grp", int(variant))
+    _lib.call(name, _p(x), _p(u), _p(out), _p(bias), None, 0, None, Nb, H, W, C, N, flags,
+              v, G, 0 if shared else M * C, 16 * N * C, M * N, N if bias is not None else 0, _s())
     return out
 
 
@@ -1106,7 +1116,7 @@ def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=Non
             if cfg in WINO4_CFGS:
                 wino4_conv_grp(x, wino4, out=out, bias=bias, relu=act == ACT_RELU, variant=-5 - cfg[0])
             else:
-                wino_conv_grp(x, wino, out=out, bias=bias, relu=act == ACT_RELU, variant=-1 - cfg[0])
+                wino_conv_grp(x, wino, out=out, bias=bias, relu=act == ACT_RELU, variant=_wino_variant(cfg))
         extra.cfgs = (WINO_CFGS if w2 else ()) + (WINO4_CFGS if w4 else ())
     return _grp_run(0, x, W, out, M, Cout, K, Cin, K, G, 0 if shared else M * Cin,
                     ('sfg', G, M, Cout, K, H, Wd, Cin, shared, bias is not None, act, w2, w4), bias=bias,
