@@ -125,7 +125,9 @@ RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) { w_tile
 
 // MO = 4: F(4x4,3x3), u [36][N][C]; MO = 2: F(2x2,3x3) on the same small-wave-tile layout (16 tiles x 16
 // channels per wave, 16 accumulators), u [16][N][C] — the variant for small grids (deep 8x8 / 4x4 maps)
-template <int MO, int WM, int WN, int MINW>
+// FL >= 0: the epilogue flags as a compile-time constant (branch-free per-element epilogue for the
+// combinations the engine uses); FL = -1 reads p.flags
+template <int MO, int WM, int WN, int MINW, int FL>
 __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4Params p) {
   constexpr int A = MO + 2;                // window / transformed tile side
   constexpr int P = A * A;                 // Winograd positions
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   static_assert(UPK * 4 * BNC == NT, "weight loader shape");
   const int uco = (tid >> 2) & (BNC - 1), upr = tid & 3, upos = tid / (4 * BNC);
   const unsigned ub = cbase + uco < p.N ? (unsigned)(((upos * p.N + cbase + uco) * p.C + 2 * upr) * 4) : OOB;
-  const int ustride = UPK * p.N * p.C * 4;
+  const int ustride = __builtin_amdgcn_readfirstlane(UPK * p.N * p.C * 4);
 
   float raw[IT][P];
   f32x2 ur[UL];
@@ -181,22 +183,32 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
     const __amdgpu_buffer_rsrc_t urs = rsrc(gup + c0, p.ubytes - 4ull * c0);
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
-      // opaque copies: the P window offsets are rebuilt per chunk from 3 registers instead of being
-      // hoisted out of the K loop into 36 live registers
+      // opaque copies: the window offsets are rebuilt per chunk from 3 registers instead of being
+      // hoisted out of the K loop into P live registers.  One vector offset per window row and edge
+      // column (interior columns are always inside the map); the column step rides in the scalar
+      // offset, so a load costs no vector ALU
       unsigned b = vb[h], rm = rmk[h], cm = cmk[h];
       asm volatile("" : "+v"(b), "+v"(rm), "+v"(cm));
+      const unsigned cl = cm & 1u, cr = (cm >> (A - 1)) & 1u;
 #pragma unroll
-      for (int i = 0; i < P; ++i) {
-        const int a = i / A, bb = i % A;
-        const int d = (((a - 1) * p.W) + bb - 1) * p.C * 4;
-        const unsigned in = (rm >> a) & (cm >> bb) & 1u;
-        const unsigned off = (b + (unsigned)d) | ((in ^ 1u) << 31);
-        raw[h][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, 0, 0));
+      for (int a = 0; a < A; ++a) {
+        const unsigned r = b + (unsigned)((a - 1) * p.W * p.C * 4);   // pixel (oy - 1 + a, ox)
+        const unsigned rok = (rm >> a) & 1u;
+        const unsigned mid = r | ((rok ^ 1u) << 31);
+        const unsigned lft = (r - (unsigned)(p.C * 4)) | (((rok & cl) ^ 1u) << 31);
+        const unsigned rgt = r | (((rok & cr) ^ 1u) << 31);
+#pragma unroll
+        for (int bb = 0; bb < A; ++bb) {
+          const unsigned off = bb == 0 ? lft : bb == A - 1 ? rgt : mid;
+          const int so = __builtin_amdgcn_readfirstlane(bb == 0 ? 0 : (bb - 1) * p.C * 4);   // keep it in an SGPR
+          raw[h][a * A + bb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, so, 0));
+        }
       }
     }
 #pragma unroll
     for (int k = 0; k < UL; ++k)
-      ur[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(urs, (int)ub, k * ustride, 0));
+      ur[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(urs, (int)ub,
+                                                                           __builtin_amdgcn_readfirstlane(k * ustride), 0));
   };
   auto store = [&]() {
 #pragma unroll
@@ -257,7 +269,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   }
 
   // ---- output transform + epilogue: lane owns channel n of 4 consecutive tiles
-  const int fl = p.flags;
+  const int fl = FL >= 0 ? FL : p.flags;
   const bool sums = fl & (WF_STATS | WF_BNB | WF_BNP);
   const int n = cbase + wn * 16 + (lane & 15);
   const bool nok = n < p.N;
@@ -418,9 +430,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
       const unsigned bad = (okm & (co < p.Co ? 1u : 0u)) ^ 1u;
       const unsigned ob = (unsigned)((pix * p.Co + co) * 4);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {       // the 4x4 patch lies inside the map (H, W multiples of 4)
-        const unsigned off = (ob + (unsigned)((((i >> 2) * p.W) + (i & 3)) * p.Co * 4)) | (bad << 31);
-        gy[h][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dyr, (int)off, 0, 0));
+      for (int i = 0; i < 4; ++i) {        // the 4x4 patch lies inside the map (H, W multiples of 4)
+        const unsigned off = (ob + (unsigned)(i * p.W * p.Co * 4)) | (bad << 31);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          gy[h][i * 4 + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+              dyr, (int)off, __builtin_amdgcn_readfirstlane(j * p.Co * 4), 0));
       }
     }
     // window rows / columns 1..4 are inside the map; row / column 0 and 5 only away from the border
@@ -431,12 +446,20 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
       const int ci = ci0 + ch + NT / 8 * h;
       const unsigned xm = okm & (ci < p.Ci ? 1u : 0u);
       const unsigned xb = (unsigned)((pix * p.Ci + ci) * 4);
+      const unsigned cl = cm & 1u, cr = (cm >> 5) & 1u;
 #pragma unroll
-      for (int i = 0; i < 36; ++i) {
-        const int a = i / 6, bb = i % 6;
-        const unsigned in = xm & (rm >> a) & (cm >> bb) & 1u;
-        const unsigned off = (xb + (unsigned)((((a - 1) * p.W) + bb - 1) * p.Ci * 4)) | ((in ^ 1u) << 31);
-        raw[h][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, 0, 0));
+      for (int a = 0; a < 6; ++a) {        // row / edge-column vector offsets, column step in soffset
+        const unsigned r = xb + (unsigned)((a - 1) * p.W * p.Ci * 4);
+        const unsigned rok = xm & (rm >> a) & 1u;
+        const unsigned mid = r | ((rok ^ 1u) << 31);
+        const unsigned lft = (r - (unsigned)(p.Ci * 4)) | (((rok & cl) ^ 1u) << 31);
+        const unsigned rgt = r | (((rok & cr) ^ 1u) << 31);
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) {
+          const unsigned off = bb == 0 ? lft : bb == 5 ? rgt : mid;
+          const int so = __builtin_amdgcn_readfirstlane(bb == 0 ? 0 : (bb - 1) * p.Ci * 4);
+          raw[h][a * 6 + bb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, so, 0));
+        }
       }
     }
   };
@@ -678,8 +701,18 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   const long long blocks = bpg * groups;
   if (blocks >= (1LL << 31)) return RK_EBADARG;
   p.bpg = (int)bpg;
-  hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW>), dim3((unsigned)blocks), dim3(64 * WM * WN), 0,
-                     (hipStream_t)stream, p);
+  const dim3 grid((unsigned)blocks), block(64 * WM * WN);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0>), grid, block, 0, st, p); break;
+    case WF_STATS: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS>), grid, block, 0, st, p); break;
+    case WF_BNB: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNB>), grid, block, 0, st, p); break;
+    case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP>), grid, block, 0, st, p); break;
+    case WF_BIAS | WF_RELU:
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU>), grid, block, 0, st, p);
+      break;
+    default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1>), grid, block, 0, st, p); break;
+  }
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
