@@ -280,8 +280,45 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   int im, oy, ox;
   w_tile_of<MO>(p, t0, im, oy, ox);
   const __amdgpu_buffer_rsrc_t yr = rsrc(gyp, p.ybytes);
+  // BNB (compile-time): the gate values of two tiles are requested at a time, ahead of their use (tiles
+  // 0-1 before the loop, 2-3 while tile 1 is transformed) instead of a dependent load per element
+  constexpr bool GPRE = FL == WF_BNB;
+  float gpre[GPRE ? 4 : 1][GPRE ? MO * MO : 1];
+  int gim = im, goy = oy, gox = ox;
+  auto gate_fetch = [&](int r) {           // tile t0 + r; (gim, goy, gox) walks the tiles in order
+    const __amdgpu_buffer_rsrc_t gr = rsrc(p.gate, p.ybytes);
+    const unsigned bad = (t0 + r < p.ntiles && nok) ? 0u : 1u;
+    const unsigned gb = (unsigned)((((gim * p.H + goy) * p.W + gox) * p.N + n) * 4);
+#pragma unroll
+    for (int i = 0; i < MO; ++i) {
+      const unsigned off = (gb + (unsigned)(i * p.W * p.N * 4)) | (bad << 31);
+#pragma unroll
+      for (int j = 0; j < MO; ++j)
+        gpre[r][i * MO + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            gr, (int)off, __builtin_amdgcn_readfirstlane(j * p.N * 4), 0));
+    }
+    gox += MO;
+    if (gox >= p.W) {
+      gox = 0;
+      goy += MO;
+      if (goy >= p.H) {
+        goy = 0;
+        ++gim;
+      }
+    }
+  };
+  if constexpr (GPRE) {
+    gate_fetch(0);
+    gate_fetch(1);
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
+    if constexpr (GPRE) {
+      if (r == 1) {
+        gate_fetch(2);
+        gate_fetch(3);
+      }
+    }
     const bool tok = t0 + r < p.ntiles;
     float tt[A][MO];
 #pragma unroll
@@ -310,7 +347,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
           }
           if (fl & WF_RELU) v = fmaxf(v, 0.f);
           if (fl & WF_BNB) {
-            const float g = p.gate[idx];
+            float g;
+            if constexpr (GPRE) g = gpre[r][i * MO + j];
+            else g = p.gate[idx];
             v = g * bs + sh > 0.f ? v : 0.f;
             s += v;
             ss += v * g;
@@ -398,9 +437,13 @@ template <int WM, int WN, int MINW>
 __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W4wParams p) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BCO = 16 * WM, BCI = 16 * WN;
-  constexpr int PY = BCO * KC / NT;        // dy patches per thread and chunk
-  constexpr int PX = BCI * KC / NT;        // x windows per thread and chunk
-  static_assert(PY >= 1 && PX >= 1 && PY * NT == BCO * KC && PX * NT == BCI * KC, "wgrad tile shape");
+  // dy patches / x windows per thread and chunk; with fewer items than threads (the 64 co x 32 ci
+  // block) only the first waves take that role
+  constexpr bool YALL = BCO * KC >= NT, XALL = BCI * KC >= NT;
+  constexpr int PY = YALL ? BCO * KC / NT : 1;
+  constexpr int PX = XALL ? BCI * KC / NT : 1;
+  static_assert((YALL ? PY * NT == BCO * KC : (BCO * KC) % 64 == 0) &&
+                (XALL ? PX * NT == BCI * KC : (BCI * KC) % 64 == 0), "wgrad tile shape");
   __shared__ __attribute__((aligned(16))) float Ms[36][BCO][KC];   // [pos][co][tile]
   __shared__ __attribute__((aligned(16))) float Vs[36][BCI][KC];   // [pos][ci][tile]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -424,8 +467,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
     const int ty = (int)(((float)rr + 0.5f) * p.invTW);
     const int oy = 4 * ty, ox = 4 * (rr - ty * p.TW);
     const int pix = (n * p.H + oy) * p.W + ox;
+    const bool yact = YALL || threadIdx.x < BCO * KC, xact = XALL || threadIdx.x < BCI * KC;
 #pragma unroll
-    for (int h = 0; h < PY; ++h) {
+    for (int h = 0; h < PY && yact; ++h) {
       const int co = co0 + ch + NT / 8 * h;
       const unsigned bad = (okm & (co < p.Co ? 1u : 0u)) ^ 1u;
       const unsigned ob = (unsigned)((pix * p.Co + co) * 4);
@@ -442,7 +486,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
     const unsigned rm = 30u | (oy > 0 ? 1u : 0u) | (oy + 4 < p.H ? 32u : 0u);
     const unsigned cm = 30u | (ox > 0 ? 1u : 0u) | (ox + 4 < p.W ? 32u : 0u);
 #pragma unroll
-    for (int h = 0; h < PX; ++h) {
+    for (int h = 0; h < PX && xact; ++h) {
       const int ci = ci0 + ch + NT / 8 * h;
       const unsigned xm = okm & (ci < p.Ci ? 1u : 0u);
       const unsigned xb = (unsigned)((pix * p.Ci + ci) * 4);
@@ -464,8 +508,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
     }
   };
   auto store = [&]() {
+    const bool yact = YALL || threadIdx.x < BCO * KC, xact = XALL || threadIdx.x < BCI * KC;
 #pragma unroll
-    for (int h = 0; h < PY; ++h) {
+    for (int h = 0; h < PY && yact; ++h) {
       const int row = ch + NT / 8 * h, c = tt ^ swz(row);
       float m[6][4];                       // A dY: along rows
 #pragma unroll
@@ -484,7 +529,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
       }
     }
 #pragma unroll
-    for (int h = 0; h < PX; ++h) {
+    for (int h = 0; h < PX && xact; ++h) {
       const int row = ch + NT / 8 * h, c = tt ^ swz(row);
       float* const r = raw[h];
 #pragma unroll
@@ -757,11 +802,14 @@ extern "C" int rk_wino4_conv(const float* x, const float* u, float* y, const flo
 
 // dW [Co][9][Ci] (splits == 1, optionally accumulated) or per-split slabs [splits][Co][9][Ci] of the
 // weight gradient of a 3x3 stride-1 pad-1 conv by F(4x4,3x3); H, W multiples of 4; tiles_per_split % 8 == 0
-extern "C" int rk_wino4_wgrad(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
-                              int splits, int accumulate, void* stream) {
+// variant 0: 4 waves, 32 co x 32 ci blocks (two per CU); 1: 8 waves, 64 co x 32 ci (a quarter less
+// transform work and LDS writes per MFMA)
+extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
+                                int splits, int accumulate, int variant, void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0 || splits <= 0) return RK_EBADARG;
   if (splits > 1 && accumulate) return RK_EBADARG;
-  constexpr int BCO = 32, BCI = 32;
+  if (variant != 0 && variant != 1) return RK_EBADARG;
+  const int BCO = variant ? 64 : 32, BCI = 32;
   W4wParams p;
   p.dy = dy; p.x = x; p.out = out;
   p.Nb = Nb; p.H = H; p.W = W; p.Co = Co; p.Ci = Ci;
@@ -783,8 +831,16 @@ extern "C" int rk_wino4_wgrad(const float* dy, const float* x, float* out, int N
   const int used = rk_cdiv(p.ntiles, p.tps);
   if (used != splits) return RK_EBADARG;
   const long long blocks = (long long)splits * p.nco * p.nci;
-  hipLaunchKernelGGL((wino4_wgrad_kernel<2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
+  if (variant)
+    hipLaunchKernelGGL((wino4_wgrad_kernel<4, 2, 1>), dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL((wino4_wgrad_kernel<2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
   RK_LAUNCH_CHECK();
   return RK_OK;
+}
+
+extern "C" int rk_wino4_wgrad(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
+                              int splits, int accumulate, void* stream) {
+  return rk_wino4_wgrad_v(dy, x, out, Nb, H, W, Co, Ci, splits, accumulate, 0, stream);
 }
 

@@ -252,7 +252,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
             wino_wgrad(dy, x, out, splits=s, accumulate=accumulate)
             return
         if tile == WINO4_WGRAD:
-            wino4_wgrad(dy, x, out, splits=s, accumulate=accumulate)
+            wino4_wgrad(dy, x, out, splits=s, accumulate=accumulate, variant=nst)
             return
         if s == 1:
             sgemm(KIND_WGRAD, dy, x, out, M, N, K, Cout, Cin, N, tile=tile, nst=nst, H=H, W=W, C=Cin, taps=taps,
@@ -470,29 +470,32 @@ WINO4_WGRAD = -7  # autotune tile id of the F(4x4) weight gradient (cfg = (-7, 0
 
 
 def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
-    """Split-K choices of rk_wino4_wgrad (32 co x 32 ci blocks): 128..4096 blocks, >= 4 chunks of 8 tiles
-    per block, slabs <= 256 MiB."""
+    """Split-K choices of rk_wino4_wgrad_v (variant 0: 32 co x 32 ci blocks, 1: 64 co x 32 ci): 128..4096
+    blocks, >= 4 chunks of 8 tiles per block, slabs <= 256 MiB.  cfg = (WINO4_WGRAD, variant, splits)."""
     if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and Cin >= 16 and Cout >= 16):
         return []
     nt = Nb * (H // 4) * (W // 4)
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
         return []
-    base = cdiv(Cout, 32) * cdiv(Cin, 32)
     out = []
-    for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
-        tps = cdiv(cdiv(nt, s), 8) * 8
-        s_eff = cdiv(nt, tps)
-        if tps < 32 or base * s_eff > 4096 or (s_eff > 1 and s_eff * 9 * Cout * Cin * 4 > (256 << 20)):
+    for v, bco in ((0, 32), (1, 64)):
+        if v == 1 and Cout < 64:
             continue
-        if base * s_eff < 128 and s != 1:
-            continue
-        c = (WINO4_WGRAD, 0, s_eff)
-        if c not in out:
-            out.append(c)
+        base = cdiv(Cout, bco) * cdiv(Cin, 32)
+        for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+            tps = cdiv(cdiv(nt, s), 8) * 8
+            s_eff = cdiv(nt, tps)
+            if tps < 32 or base * s_eff > 4096 or (s_eff > 1 and s_eff * 9 * Cout * Cin * 4 > (256 << 20)):
+                continue
+            if base * s_eff < 128 and s != 1:
+                continue
+            c = (WINO4_WGRAD, v, s_eff)
+            if c not in out:
+                out.append(c)
     return out
 
 
-def wino4_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1, accumulate=False):
+def wino4_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1, accumulate=False, variant=0):
     """out [Cout][9*Cin] (+)= weight gradient of a 3x3 stride-1 conv by F(4x4,3x3); splits > 1: per-split
     slabs summed by reduce_slabs."""
     _check(dy, 'wino4_wgrad dy')
@@ -501,10 +504,11 @@ def wino4_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=
     Cin = x.shape[-1]
     assert x.shape[:3] == dy.shape[:3] and out.numel() == Cout * 9 * Cin and out.is_contiguous()
     if splits == 1:
-        _lib.call("rk_wino4_wgrad", _p(dy), _p(x), _p(out), Nb, H, W, Cout, Cin, 1, int(bool(accumulate)), _s())
+        _lib.call("rk_wino4_wgrad_v", _p(dy), _p(x), _p(out), Nb, H, W, Cout, Cin, 1, int(bool(accumulate)),
+                  int(variant), _s())
         return out
     slab = torch.empty((splits, Cout, 9 * Cin), device=dy.device, dtype=torch.float32)
-    _lib.call("rk_wino4_wgrad", _p(dy), _p(x), _p(slab), Nb, H, W, Cout, Cin, int(splits), 0, _s())
+    _lib.call("rk_wino4_wgrad_v", _p(dy), _p(x), _p(slab), Nb, H, W, Cout, Cin, int(splits), 0, int(variant), _s())
     reduce_slabs(slab, out.view(Cout, 9 * Cin), accumulate=accumulate)
     return out
 

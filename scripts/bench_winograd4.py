@@ -45,12 +45,16 @@ for (N, H, C, K) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128),
     r['wt4_us'] = round(t(lambda: S.wino4_u(w)), 1)
     dy = torch.randn(N, H, H, K, device='cuda')
     dw = torch.empty(K, 9 * C, device='cuda')
-    for name, cands, fn in (('wg2', S._wino_wgrad_cands(N, H, H, K, C), S.wino_wgrad),
-                            ('wg4', S._wino4_wgrad_cands(N, H, H, K, C), S.wino4_wgrad)):
-        tw = {c[2]: t(lambda: fn(dy, x, dw, splits=c[2])) for c in cands}
+    tw = {c[2]: t(lambda: S.wino_wgrad(dy, x, dw, splits=c[2])) for c in S._wino_wgrad_cands(N, H, H, K, C)}
+    if tw:
+        sb = min(tw, key=tw.get)
+        r['wg2_us'], r['wg2_splits'] = round(tw[sb], 1), sb
+    for v in (0, 1):
+        tw = {c[2]: t(lambda: S.wino4_wgrad(dy, x, dw, splits=c[2], variant=v))
+              for c in S._wino4_wgrad_cands(N, H, H, K, C) if c[1] == v}
         if tw:
             sb = min(tw, key=tw.get)
-            r[name + '_us'], r[name + '_splits'] = round(tw[sb], 1), sb
+            r['wg4_v%d_us' % v], r['wg4_v%d_splits' % v] = round(tw[sb], 1), sb
     fl = 2.0 * N * H * H * K * 9 * C
     best2 = min(r['w2_v%d_us' % v] for v in range(4))
     best4 = min(r['w4_v0_us'], r['w4_v1_us'])

@@ -128,7 +128,8 @@ def test_wino4_conv_grouped(shared, variant):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 32, 32, 64, 64), (16, 4, 4, 256, 512),
                                             (3, 4, 12, 24, 40), (2, 4, 4, 16, 16)])
 @pytest.mark.parametrize("splits", [1, 2, 5])
-def test_wino4_wgrad(N, H, W, Cin, Cout, splits):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino4_wgrad(N, H, W, Cin, Cout, splits, variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=30)
     dy = _rand(N, H, W, Cout, seed=31)
@@ -136,10 +137,10 @@ def test_wino4_wgrad(N, H, W, Cin, Cout, splits):
     tps = -(-(-(-nt // splits)) // 8) * 8
     s_eff = -(-nt // tps)
     dw = torch.empty(Cout, 9 * Cin, device=DEV)
-    S.wino4_wgrad(dy.to(DEV), x.to(DEV), dw, splits=s_eff)
+    S.wino4_wgrad(dy.to(DEV), x.to(DEV), dw, splits=s_eff, variant=variant)
     prev = _rand(Cout, 9 * Cin, seed=32).to(DEV)
     acc = prev.clone()
-    S.wino4_wgrad(dy.to(DEV), x.to(DEV), acc, splits=s_eff, accumulate=True)
+    S.wino4_wgrad(dy.to(DEV), x.to(DEV), acc, splits=s_eff, accumulate=True, variant=variant)
     torch.cuda.synchronize()
     wd = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
     out = TF.conv2d(x.double().permute(0, 3, 1, 2), wd, padding=1)
