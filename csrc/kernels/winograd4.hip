@@ -790,6 +790,9 @@ extern "C" int rk_wino2s_conv_grp(const float* x, const float* u, float* y, cons
   if (variant == 1)
     return launch_gfwd<2, 1, 2, 3>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
                                    gbias, stream);
+  if (variant == 2)   // 8 waves, 64 tiles x 32 channels (48 KiB LDS)
+    return launch_gfwd<2, 4, 2, 2>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
+                                   gbias, stream);
   return RK_EBADARG;
 }
 

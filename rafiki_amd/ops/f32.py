@@ -313,12 +313,13 @@ class SConvWT:
 WF_RELU, WF_BIAS, WF_STATS, WF_BNB, WF_BNP = 1, 2, 4, 512, 1024
 WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
 # autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1),
-# and the small-wave-tile kernels for small grids: 4-wave 32x32 (variant 2) / 2-wave 16x32 (variant 3)
-WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1))
+# and the 16x16-wave-tile kernels of winograd4.hip: 4-wave 32x32 (variant 2), 2-wave 16x32 (variant 3),
+# 8-wave 64x32 (variant 4)
+WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1), (-10, 0, 1))
 
 
 def _wino_variant(cfg):
-    return {-1: 0, -2: 1, -8: 2, -9: 3}[cfg[0]]
+    return {-1: 0, -2: 1, -8: 2, -9: 3, -10: 4}[cfg[0]]
 
 
 def wino_ok(H: int, W: int, C: int) -> bool:
