@@ -227,6 +227,7 @@ class ConvNetEngine:
     # 11% SLOWER (1.161 -> 1.289 ms; the concurrent GEMMs and split-K slab traffic interfere) and,
     # re-measured with the current kernels, still 5-6% slower (258k -> 243-245k img/s), so it is off
     # by default (RAFIKI_OVERLAP_WGRAD=1) and kept as an option for layer shapes where it pays.
+    # fp32 path (Winograd kernels, one or two LDS-heavy workgroups per CU): 2.27 -> 2.46 ms, 8% slower.
     overlap_wgrad = os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') == '1'
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
@@ -430,31 +431,46 @@ class ConvNetEngine:
         d = d.view(B, self.feat_hw, self.feat_hw, -1)
         wt = self._conv_wt()
         if wt is not None:
-            wt.refresh()  # one launch: flipped/transposed fp32 weights of every dgrad layer
+            # flipped/transposed fp32 weights of every dgrad layer, refreshed (one launch) on first use
+            wt.begin_step()
         reduced = False
+        # RAFIKI_OVERLAP_WGRAD=1: weight gradients on a side stream (fork / join become graph edges),
+        # so a weight gradient and the next data gradient share the CUs
+        main = torch.cuda.current_stream(self.device)
+        side = self._side_stream() if self.overlap_wgrad else None
         for bi in range(len(self.blocks) - 1, -1, -1):
             name, cin, cout, pool, hw = self.blocks[bi]
             y, coeffs = saved[bi]
             dy = S.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), accs[bi][1], pool=pool, act=F.ACT_RELU,
                           dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'), reduced=reduced)
-            S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
+            if side is not None:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
+                dy.record_stream(side)
+                acts[bi].record_stream(side)
+            else:
+                S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
             if bi == 0:
                 break
             py, pco = saved[bi - 1]
             pname, pcin, pcout, ppool, phw = self.blocks[bi - 1]
             wu = ww.lazy('ut2', bi - 1) if ww is not None else None
             wu4 = ww.lazy('ut4', bi - 1) if ww is not None else None
+            wl = wt.lazy(bi - 1)
             if not ppool:
                 # the input block is BN+ReLU: its mask and BN-backward sums ride in this dgrad's epilogue
-                d = S.conv_dgrad(dy, wt.view(bi - 1), bnb=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4)
+                d = S.conv_dgrad(dy, wl, bnb=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin)
                 reduced = True
             elif phw == 2 * hw and not (hw & (hw - 1)):
                 # BN+ReLU+max-pool input (even power-of-two geometry): pool routing + sums in the epilogue
-                d = S.conv_dgrad(dy, wt.view(bi - 1), bnp=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4)
+                d = S.conv_dgrad(dy, wl, bnp=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin)
                 reduced = True
             else:
-                d = S.conv_dgrad(dy, wt.view(bi - 1), wino=wu, wino4=wu4)
+                d = S.conv_dgrad(dy, wl, wino=wu, wino4=wu4, cin=cin)
                 reduced = False
+        if side is not None:
+            main.wait_stream(side)
         if ww is not None:
             ww.end_step()   # only the Winograd sets the tuned convs use are transformed from now on
 

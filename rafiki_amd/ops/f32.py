@@ -301,8 +301,24 @@ class SConvWT:
         self.meta = torch.tensor(meta, dtype=torch.int64, device=dev)
         self.desc = torch.tensor(desc, dtype=torch.int32, device=dev)
 
+    _fresh = False
+
     def refresh(self):
         _lib.call("rk_swt", _p(self.arena), _p(self.buf), _p(self.desc), self.desc.shape[0], _p(self.meta), _s())
+        self._fresh = True
+
+    def begin_step(self):
+        """The weights change every step: the next lazy() read refreshes (one launch) first."""
+        self._fresh = False
+
+    def lazy(self, l: int):
+        """Callable view for conv_dgrad's direct candidates: the refresh launch runs only in steps whose
+        tuned data gradients use the direct kernel (Winograd ones read WinoWeights instead)."""
+        def get():
+            if not self._fresh:
+                self.refresh()
+            return self.view(l)
+        return get
 
     def view(self, l: int) -> torch.Tensor:
         off, Cin, Cout = self._views[l]
