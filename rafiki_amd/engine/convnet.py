@@ -123,11 +123,14 @@ class ConvNetEngine:
         self.f32 = self.dtype == 'fp32'
         self.act_dtype = torch.float32 if self.f32 else torch.bfloat16
         self.num_classes, self.in_channels, self.image_size = num_classes, in_channels, image_size
-        # fp32 K-inner operands move 16-B = 4-channel chunks, bf16 ones 8-channel chunks
-        self.cin_p = _pad4(in_channels) if self.f32 else _pad8(in_channels)
+        self.flat_input = not any(v != 'M' for v in cfg)
+        # fp32 K-inner operands move 16-B = 4-channel chunks, bf16 ones 8-channel chunks; with the
+        # Winograd kernels (C % 8 == 0) the fp32 stem is padded to 8 channels too, so the first conv
+        # and its weight gradient get the fused Winograd candidates (zero channels, zero weights)
+        self.cin_p = ((_pad8(in_channels) if S.WINO and not self.flat_input else _pad4(in_channels)) if self.f32
+                      else _pad8(in_channels))
         self.ncls_p = _pad8(num_classes)
         self.bn_eps, self.bn_momentum = bn_eps, bn_momentum
-        self.flat_input = not any(v != 'M' for v in cfg)
         self.input_bn = bool(input_bn)
         if self.input_bn and not self.flat_input:
             raise ValueError('input_bn is for fully-connected nets (no conv blocks)')
@@ -380,13 +383,13 @@ class ConvNetEngine:
             self._bn_acc_flat.zero_()  # one memset node for every layer's fp64 statistic slots
         ww = self._wino_train()
         if ww is not None:
-            ww.refresh()   # one launch: Winograd-domain weights (forward + data-gradient sets) of blocks 1..
+            ww.refresh()   # one launch per family: the live Winograd-domain weight sets of every block
         acts, saved, h = [x], [], x
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             rm, rv = self.running_stats(bi)
             y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0],
-                           wino=ww.lazy('u2', bi - 1) if ww is not None and bi > 0 else None,
-                           wino4=ww.lazy('u4', bi - 1) if ww is not None and bi > 0 else None)
+                           wino=ww.lazy('u2', bi) if ww is not None else None,
+                           wino4=ww.lazy('u4', bi) if ww is not None else None)
             h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
                                  self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
             saved.append((y, coeffs))
@@ -455,8 +458,8 @@ class ConvNetEngine:
                 break
             py, pco = saved[bi - 1]
             pname, pcin, pcout, ppool, phw = self.blocks[bi - 1]
-            wu = ww.lazy('ut2', bi - 1) if ww is not None else None
-            wu4 = ww.lazy('ut4', bi - 1) if ww is not None else None
+            wu = ww.lazy('ut2', bi) if ww is not None else None
+            wu4 = ww.lazy('ut4', bi) if ww is not None else None
             wl = wt.lazy(bi - 1)
             if not ppool:
                 # the input block is BN+ReLU: its mask and BN-backward sums ride in this dgrad's epilogue
@@ -478,13 +481,13 @@ class ConvNetEngine:
         """WinoWeights over blocks 1.. (fp32 path): the fused F(2x2,3x3) and F(4x4,3x3) kernels become
         autotune candidates of every forward / data-gradient conv they fit (RAFIKI_WINOGRAD=0 turns
         both off, RAFIKI_WINOGRAD4=0 the F(4x4) ones)."""
-        if not (self.f32 and S.WINO and len(self.blocks) > 1 and self.device.type == 'cuda'):
+        if not (self.f32 and S.WINO and self.blocks and self.device.type == 'cuda'):
             return None
         ww = getattr(self, '_ww', None)
         if ww is None:
             fl = self.flat
-            ww = self._ww = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]],
-                                          hw=[b[4] for b in self.blocks[1:]])
+            ww = self._ww = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks],
+                                          hw=[b[4] for b in self.blocks])
         return ww
 
     def _conv_wt(self):
@@ -771,9 +774,9 @@ class ConvNetEngine:
         self._eval_coeffs = coeffs
         self._eval_graphs = {}
         self._eval_wino = None
-        if self.f32 and S.WINO and len(self.blocks) > 1 and self.device.type == 'cuda':
-            self._eval_wino = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks[1:]], dgrad=False,
-                                            hw=[b[4] for b in self.blocks[1:]])
+        if self.f32 and S.WINO and self.blocks and self.device.type == 'cuda':
+            self._eval_wino = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks], dgrad=False,
+                                            hw=[b[4] for b in self.blocks])
             self._eval_wino.refresh()
         return coeffs
 
@@ -784,8 +787,8 @@ class ConvNetEngine:
         B = x.shape[0]
         ew = getattr(self, '_eval_wino', None)
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
-            y = S.conv_fwd(h, fl.w(name + '.w'), wino=ew.u(bi - 1) if ew is not None and bi > 0 else None,
-                           wino4=ew.u4(bi - 1) if ew is not None and bi > 0 else None)
+            y = S.conv_fwd(h, fl.w(name + '.w'), wino=ew.u(bi) if ew is not None else None,
+                           wino4=ew.u4(bi) if ew is not None else None)
             c = self._eval_coeffs[bi]
             h = S.bn_eval(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
         if self.input_bn:
@@ -937,7 +940,7 @@ class GroupedConvNets:
         if S.WINO and self.device.type == 'cuda':
             for bi, (name, cin, cout, pool, hw) in enumerate(e0.blocks):
                 w = self.conv_w[bi]
-                if bi > 0 and w.shape[2] % 9 == 0 and (w.shape[2] // 9) % 8 == 0 and hw % 2 == 0:
+                if w.shape[2] % 9 == 0 and (w.shape[2] // 9) % 8 == 0 and hw % 2 == 0:
                     self.conv_u[bi] = torch.stack([S.wino_u(w[g]) for g in range(self.k)]).contiguous()
                     if S.WINO4 and hw % 4 == 0:
                         self.conv_u4[bi] = torch.stack([S.wino4_u(w[g]) for g in range(self.k)]).contiguous()

@@ -489,7 +489,7 @@ WINO4_WGRAD = -7  # autotune tile id of the F(4x4) weight gradient (cfg = (-7, 0
 def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     """Split-K choices of rk_wino4_wgrad_v (variant 0: 32 co x 32 ci blocks, 1: 64 co x 32 ci): 128..4096
     blocks, >= 4 chunks of 8 tiles per block, slabs <= 256 MiB.  cfg = (WINO4_WGRAD, variant, splits)."""
-    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and Cin >= 16 and Cout >= 16):
+    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and Cin >= 8 and Cout >= 16):
         return []
     nt = Nb * (H // 4) * (W // 4)
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
@@ -536,7 +536,7 @@ WINO_WGRAD = -3   # autotune tile id of the Winograd weight gradient (cfg = (-3,
 def _wino_wgrad_cands(Nb, H, W, Cout, Cin):
     """Split-K choices of rk_wino_wgrad that fill the chip: 128..4096 blocks, >= 8 chunks of 8 tiles per
     block, slabs <= 256 MiB."""
-    if not (WINO and H % 2 == 0 and W % 2 == 0 and Cin >= 16 and Cout >= 16):
+    if not (WINO and H % 2 == 0 and W % 2 == 0 and Cin >= 8 and Cout >= 16):
         return []
     nt = Nb * (H // 2) * (W // 2)
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:

@@ -174,7 +174,10 @@ def _engine(**kw):
     return ConvNetEngine(**args)
 
 
-def _batch(B, hw=16, seed=0, c=4):
+def _batch(B, hw=16, seed=0, c=None):
+    if c is None:   # the fp32 engine's input padding: 8 channels with the Winograd stem, else 4
+        from rafiki_amd.ops import f32 as S
+        c = 8 if S.WINO else 4
     g = torch.Generator().manual_seed(seed)
     x = torch.zeros(B, hw, hw, c)
     x[..., :3] = torch.randn(B, hw, hw, 3, generator=g)
