@@ -127,7 +127,10 @@ RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) { w_tile
 // channels per wave, 16 accumulators), u [16][N][C] — the variant for small grids (deep 8x8 / 4x4 maps)
 // FL >= 0: the epilogue flags as a compile-time constant (branch-free per-element epilogue for the
 // combinations the engine uses); FL = -1 reads p.flags
-template <int MO, int WM, int WN, int MINW, int FL>
+// NS = 2: two LDS stages and two register sets — the transform of chunk c+1 (loaded during chunk c-1)
+// is written to one stage while the MFMAs of chunk c read the other, in the same wave (software
+// pipelining; one barrier per chunk; chunks past Cin load zeros, so the body is branch-free)
+template <int MO, int WM, int WN, int MINW, int FL, int NS = 1>
 __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4Params p) {
   constexpr int A = MO + 2;                // window / transformed tile side
   constexpr int P = A * A;                 // Winograd positions
@@ -137,8 +140,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   constexpr int IT = T * KC / NT;          // input windows per thread and chunk
   constexpr int UL = P * BNC * 4 / NT;    // f32x2 weight loads per thread and chunk
   static_assert(IT >= 1 && IT * NT == T * KC && UL * NT == P * BNC * 4, "tile shape");
-  __shared__ __attribute__((aligned(16))) float Vs[P][T][KC];
-  __shared__ __attribute__((aligned(16))) float Us[P][BNC][KC];
+  __shared__ __attribute__((aligned(16))) float Vs[NS][P][T][KC];
+  __shared__ __attribute__((aligned(16))) float Us[NS][P][BNC][KC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int b0 = xcd_remap(blockIdx.x, gridDim.x);
@@ -176,11 +179,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   const unsigned ub = cbase + uco < p.N ? (unsigned)(((upos * p.N + cbase + uco) * p.C + 2 * upr) * 4) : OOB;
   const int ustride = __builtin_amdgcn_readfirstlane(UPK * p.N * p.C * 4);
 
-  float raw[IT][P];
-  f32x2 ur[UL];
-  auto load = [&](int c0) {
-    const __amdgpu_buffer_rsrc_t xr = rsrc(gxp + c0, p.xbytes - 4ull * c0);
-    const __amdgpu_buffer_rsrc_t urs = rsrc(gup + c0, p.ubytes - 4ull * c0);
+  auto load = [&](int c0, float (&raw)[IT][P], f32x2 (&ur)[UL]) {
+    // a chunk past Cin (the pipelined tail) reads zeros: empty buffer ranges
+    const bool live = c0 < p.C;
+    const __amdgpu_buffer_rsrc_t xr = rsrc(gxp + c0, live ? p.xbytes - 4ull * c0 : 0ull);
+    const __amdgpu_buffer_rsrc_t urs = rsrc(gup + c0, live ? p.ubytes - 4ull * c0 : 0ull);
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
       // opaque copies: the window offsets are rebuilt per chunk from 3 registers instead of being
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
       ur[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(urs, (int)ub,
                                                                            __builtin_amdgcn_readfirstlane(k * ustride), 0));
   };
-  auto store = [&]() {
+  auto store = [&](int st, float (&raw)[IT][P], const f32x2 (&ur)[UL]) {
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
       const int row = lt + NT / 8 * h, c = lc ^ swz(row);
@@ -227,11 +230,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
         float o[A];
         bt_line<MO>(r + a * A, 1, o);
 #pragma unroll
-        for (int bb = 0; bb < A; ++bb) Vs[a * A + bb][row][c] = o[bb];
+        for (int bb = 0; bb < A; ++bb) Vs[st][a * A + bb][row][c] = o[bb];
       }
     }
 #pragma unroll
-    for (int k = 0; k < UL; ++k) *(f32x2*)&Us[upos + UPK * k][uco][(2 * upr) ^ swz(uco)] = ur[k];
+    for (int k = 0; k < UL; ++k) *(f32x2*)&Us[st][upos + UPK * k][uco][(2 * upr) ^ swz(uco)] = ur[k];
   };
 
   f32x4 acc[P];
@@ -239,21 +242,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   for (int q = 0; q < P; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nch = p.C / KC;
-  load(0);
-  store();
-  __syncthreads();
   const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
   const int ka = (2 * (lane >> 4)) ^ swz(ar), kb = (2 * (lane >> 4)) ^ swz(br);
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) load((c + 1) * KC);
+  auto mfma = [&](int st) {
     // four positions at a time: 4 independent MFMAs between dependent ones
 #pragma unroll
     for (int q = 0; q < P; q += 4) {
       f32x2 a[4], bv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        a[e] = *(const f32x2*)&Vs[q + e][ar][ka];
-        bv[e] = *(const f32x2*)&Us[q + e][br][kb];
+        a[e] = *(const f32x2*)&Vs[st][q + e][ar][ka];
+        bv[e] = *(const f32x2*)&Us[st][q + e][br][kb];
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -261,11 +260,39 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
         for (int e = 0; e < 4; ++e)
           acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s], acc[q + e], 0, 0, 0);
     }
-    if (c + 1 < nch) {
-      __syncthreads();                     // every wave is done reading the stage
-      store();
-    }
+  };
+  float rA[IT][P];
+  f32x2 uA[UL];
+  if constexpr (NS == 1) {
+    load(0, rA, uA);
+    store(0, rA, uA);
     __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) load((c + 1) * KC, rA, uA);
+      mfma(0);
+      if (c + 1 < nch) {
+        __syncthreads();                   // every wave is done reading the stage
+        store(0, rA, uA);
+      }
+      __syncthreads();
+    }
+  } else {
+    float rB[IT][P];
+    f32x2 uB[UL];
+    load(0, rA, uA);
+    load(KC, rB, uB);
+    store(0, rA, uA);
+    __syncthreads();
+    for (int c = 0; c < nch; c += 2) {
+      load((c + 2) * KC, rA, uA);
+      mfma(0);                             // chunk c
+      store(1, rB, uB);                    // chunk c + 1, in the MFMAs' shadow
+      __syncthreads();
+      load((c + 3) * KC, rB, uB);
+      mfma(1);                             // chunk c + 1 (zeros past the end)
+      store(0, rA, uA);                    // chunk c + 2
+      __syncthreads();
+    }
   }
 
   // ---- output transform + epilogue: lane owns channel n of 4 consecutive tiles
@@ -612,6 +639,169 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   }
 }
 
+// Software-pipelined weight gradient: 32 co x 32 ci blocks of 4 waves with TWO LDS stages (147 KiB, one
+// block and one wave per SIMD, accumulators in AGPRs).  While the MFMAs of chunk c read one stage, the
+// same wave transforms chunk c+1 (loaded during chunk c-1) into the other, so the transform VALU and
+// LDS writes issue in the shadow of the 32-cycle MFMAs instead of in a phase of their own; one barrier
+// per chunk.  Chunks past the end load zeros (out-of-range offsets), so the body is branch-free.
+__global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParams p) {
+  constexpr int BCO = 32, BCI = 32;
+  __shared__ __attribute__((aligned(16))) float Ms[2][36][BCO][KC];
+  __shared__ __attribute__((aligned(16))) float Vs[2][36][BCI][KC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = p.nco * p.nci;
+  const int split = b / per, r0 = b - split * per;
+  const int co0 = (r0 / p.nci) * BCO, ci0 = (r0 % p.nci) * BCI;
+  const int t_begin = split * p.tps;
+  const int t_end = min(t_begin + p.tps, p.ntiles);
+  const int nch = (t_end - t_begin + KC - 1) / KC;
+  const int tt = tid & 7, ch = tid >> 3;
+  const __amdgpu_buffer_rsrc_t dyr = rsrc(p.dy, p.dybytes), xr = rsrc(p.x, p.xbytes);
+  const int co = co0 + ch, ci = ci0 + ch;
+
+  auto load = [&](int c, float (&gy)[16], float (&raw)[36]) {
+    const int t = t_begin + c * KC + tt;
+    const unsigned okm = t < t_end ? 1u : 0u;
+    const int tq = t < t_end ? t : t_begin;            // decode a valid tile; masks zero the data
+    const int n = (int)(((float)tq + 0.5f) * p.invTHW);
+    const int rr = tq - n * p.THW;
+    const int ty = (int)(((float)rr + 0.5f) * p.invTW);
+    const int oy = 4 * ty, ox = 4 * (rr - ty * p.TW);
+    const int pix = (n * p.H + oy) * p.W + ox;
+    const unsigned bad = (okm & (co < p.Co ? 1u : 0u)) ^ 1u;
+    const unsigned ob = (unsigned)((pix * p.Co + co) * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned off = (ob + (unsigned)(i * p.W * p.Co * 4)) | (bad << 31);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        gy[i * 4 + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            dyr, (int)off, __builtin_amdgcn_readfirstlane(j * p.Co * 4), 0));
+    }
+    const unsigned rm = 30u | (oy > 0 ? 1u : 0u) | (oy + 4 < p.H ? 32u : 0u);
+    const unsigned cm = 30u | (ox > 0 ? 1u : 0u) | (ox + 4 < p.W ? 32u : 0u);
+    const unsigned xm = okm & (ci < p.Ci ? 1u : 0u);
+    const unsigned xb = (unsigned)((pix * p.Ci + ci) * 4);
+    const unsigned cl = cm & 1u, cr = (cm >> 5) & 1u;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const unsigned r = xb + (unsigned)((a - 1) * p.W * p.Ci * 4);
+      const unsigned rok = xm & (rm >> a) & 1u;
+      const unsigned mid = r | ((rok ^ 1u) << 31);
+      const unsigned lft = (r - (unsigned)(p.Ci * 4)) | (((rok & cl) ^ 1u) << 31);
+      const unsigned rgt = r | (((rok & cr) ^ 1u) << 31);
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        const unsigned off = bb == 0 ? lft : bb == 5 ? rgt : mid;
+        const int so = __builtin_amdgcn_readfirstlane(bb == 0 ? 0 : (bb - 1) * p.Ci * 4);
+        raw[a * 6 + bb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, so, 0));
+      }
+    }
+  };
+  const int srow = ch, scol = tt ^ swz(ch);
+  auto store = [&](int st, const float (&gy)[16], float (&raw)[36]) {
+    float m[6][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o[6];
+      a6(gy[j], gy[4 + j], gy[8 + j], gy[12 + j], o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) m[a][j] = o[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      float o[6];
+      a6(m[a][0], m[a][1], m[a][2], m[a][3], o);
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) Ms[st][a * 6 + bb][srow][scol] = o[bb];
+    }
+#pragma unroll
+    for (int bb = 0; bb < 6; ++bb) {
+      float o[6];
+      bt6(raw[bb], raw[6 + bb], raw[12 + bb], raw[18 + bb], raw[24 + bb], raw[30 + bb], o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) raw[a * 6 + bb] = o[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      float o[6];
+      bt6(raw[a * 6 + 0], raw[a * 6 + 1], raw[a * 6 + 2], raw[a * 6 + 3], raw[a * 6 + 4], raw[a * 6 + 5], o);
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) Vs[st][a * 6 + bb][srow][scol] = o[bb];
+    }
+  };
+
+  f32x4 acc[36];
+#pragma unroll
+  for (int q = 0; q < 36; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
+  const int ka = (2 * (lane >> 4)) ^ swz(ar), kb = (2 * (lane >> 4)) ^ swz(br);
+  auto mfma = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < 36; q += 4) {
+      f32x2 a[4], bv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = *(const f32x2*)&Ms[st][q + e][ar][ka];
+        bv[e] = *(const f32x2*)&Vs[st][q + e][br][kb];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s], acc[q + e], 0, 0, 0);
+    }
+  };
+
+  float gA[16], rA[36], gB[16], rB[36];
+  if (nch > 0) {
+    load(0, gA, rA);
+    load(1, gB, rB);
+    store(0, gA, rA);
+    __syncthreads();
+    for (int c = 0; c < nch; c += 2) {
+      load(c + 2, gA, rA);
+      mfma(0);                             // chunk c
+      store(1, gB, rB);                    // chunk c + 1, in the MFMAs' shadow
+      __syncthreads();
+      load(c + 3, gB, rB);
+      mfma(1);                             // chunk c + 1 (zeros past the end)
+      store(0, gA, rA);                    // chunk c + 2
+      __syncthreads();
+    }
+  }
+
+  float* outp = p.out + (long long)split * p.slab;
+  const int oci = ci0 + wn * 16 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int oco = co0 + wm * 16 + (lane >> 4) * 4 + r;
+    float tq[3][6];
+#pragma unroll
+    for (int bb = 0; bb < 6; ++bb) {
+      float g[3];
+      gt6(acc[0 * 6 + bb][r], acc[1 * 6 + bb][r], acc[2 * 6 + bb][r], acc[3 * 6 + bb][r], acc[4 * 6 + bb][r],
+          acc[5 * 6 + bb][r], g);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) tq[ky][bb] = g[ky];
+    }
+    if (oco >= p.Co || oci >= p.Ci) continue;
+    float* o = outp + (long long)oco * 9 * p.Ci + oci;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      float v[3];
+      gt6(tq[ky][0], tq[ky][1], tq[ky][2], tq[ky][3], tq[ky][4], tq[ky][5], v);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        float* d = o + (ky * 3 + kx) * p.Ci;
+        *d = p.accumulate ? *d + v[kx] : v[kx];
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ weight transform
 // U = G g G^T (36 values) of a 3x3 filter g[ky*3+kx]
 RK_DEV void w4_transform(const float (&g)[9], float (&U)[36]) {
@@ -714,7 +904,7 @@ extern "C" int rk_wino4_weights_multi(const float* arena, float* dst, const int*
 namespace {
 // shared launcher of the small-wave-tile Winograd forward kernels: MO = 4 (u [36][N][C], H, W multiples
 // of 4) or MO = 2 (u [16][N][C], even H, W); T tiles x BNC channels per block of NT threads
-template <int MO, int WM, int WN, int MINW>
+template <int MO, int WM, int WN, int MINW, int NS = 1>
 int launch_gfwd(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
                 const float* gate, int Nb, int H, int W, int C, int N, int flags, int groups, long long gx,
                 long long gu, long long gy, long long gbias, void* stream) {
@@ -749,14 +939,14 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   const dim3 grid((unsigned)blocks), block(64 * WM * WN);
   const hipStream_t st = (hipStream_t)stream;
   switch (flags) {
-    case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0>), grid, block, 0, st, p); break;
-    case WF_STATS: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS>), grid, block, 0, st, p); break;
-    case WF_BNB: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNB>), grid, block, 0, st, p); break;
-    case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP>), grid, block, 0, st, p); break;
+    case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0, NS>), grid, block, 0, st, p); break;
+    case WF_STATS: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS, NS>), grid, block, 0, st, p); break;
+    case WF_BNB: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNB, NS>), grid, block, 0, st, p); break;
+    case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP, NS>), grid, block, 0, st, p); break;
     case WF_BIAS | WF_RELU:
-      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU, NS>), grid, block, 0, st, p);
       break;
-    default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1>), grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1, NS>), grid, block, 0, st, p); break;
   }
   RK_LAUNCH_CHECK();
   return RK_OK;
@@ -775,6 +965,9 @@ extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const
   if (variant == 1)
     return launch_gfwd<4, 2, 2, 2>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
                                    gbias, stream);
+  if (variant == 2)   // 4 waves, 32 x 32, two LDS stages (147 KiB), software-pipelined
+    return launch_gfwd<4, 2, 2, 1, 2>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu,
+                                      gy, gbias, stream);
   return RK_EBADARG;
 }
 
@@ -793,6 +986,9 @@ extern "C" int rk_wino2s_conv_grp(const float* x, const float* u, float* y, cons
   if (variant == 2)   // 8 waves, 64 tiles x 32 channels (48 KiB LDS)
     return launch_gfwd<2, 4, 2, 2>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
                                    gbias, stream);
+  if (variant == 3)   // 8 waves, 64 x 32, two LDS stages (96 KiB), software-pipelined
+    return launch_gfwd<2, 4, 2, 1, 2>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu,
+                                      gy, gbias, stream);
   return RK_EBADARG;
 }
 
@@ -806,13 +1002,13 @@ extern "C" int rk_wino4_conv(const float* x, const float* u, float* y, const flo
 // dW [Co][9][Ci] (splits == 1, optionally accumulated) or per-split slabs [splits][Co][9][Ci] of the
 // weight gradient of a 3x3 stride-1 pad-1 conv by F(4x4,3x3); H, W multiples of 4; tiles_per_split % 8 == 0
 // variant 0: 4 waves, 32 co x 32 ci blocks (two per CU); 1: 8 waves, 64 co x 32 ci (a quarter less
-// transform work and LDS writes per MFMA)
+// transform work and LDS writes per MFMA); 2: 32 x 32, two LDS stages, transform in the MFMA shadow
 extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
                                 int splits, int accumulate, int variant, void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0 || splits <= 0) return RK_EBADARG;
   if (splits > 1 && accumulate) return RK_EBADARG;
-  if (variant != 0 && variant != 1) return RK_EBADARG;
-  const int BCO = variant ? 64 : 32, BCI = 32;
+  if (variant < 0 || variant > 2) return RK_EBADARG;
+  const int BCO = variant == 1 ? 64 : 32, BCI = 32;
   W4wParams p;
   p.dy = dy; p.x = x; p.out = out;
   p.Nb = Nb; p.H = H; p.W = W; p.Co = Co; p.Ci = Ci;
@@ -834,7 +1030,9 @@ extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int
   const int used = rk_cdiv(p.ntiles, p.tps);
   if (used != splits) return RK_EBADARG;
   const long long blocks = (long long)splits * p.nco * p.nci;
-  if (variant)
+  if (variant == 2)
+    hipLaunchKernelGGL(wino4_wgrad_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
+  else if (variant == 1)
     hipLaunchKernelGGL((wino4_wgrad_kernel<4, 2, 1>), dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);
   else
     hipLaunchKernelGGL((wino4_wgrad_kernel<2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);

@@ -155,7 +155,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         tile, nst, s = cfg
         if cfg in WINO4_CFGS:
             wino4_conv(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
-                       relu=act == ACT_RELU, variant=-5 - cfg[0])
+                       relu=act == ACT_RELU, variant=_wino4_variant(cfg))
             return
         if cfg in WINO_CFGS:
             wino_conv(x, wino() if callable(wino) else wino, out=out, bias=bias, stats=stats_acc,
@@ -216,7 +216,8 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
 
     def run(cfg):
         if cfg in WINO4_CFGS:
-            wino4_conv(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, variant=-5 - cfg[0])
+            wino4_conv(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp,
+                       variant=_wino4_variant(cfg))
             return
         if cfg in WINO_CFGS:
             wino_conv(dy, wino() if callable(wino) else wino, out=out, bnb=bnb, bnp=bnp, variant=_wino_variant(cfg))
@@ -331,11 +332,14 @@ WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
 # autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1),
 # and the 16x16-wave-tile kernels of winograd4.hip: 4-wave 32x32 (variant 2), 2-wave 16x32 (variant 3),
 # 8-wave 64x32 (variant 4)
-WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1), (-10, 0, 1))
+# RAFIKI_WINO_PIPE=0 drops the software-pipelined (two LDS stage) variants from the candidate lists
+WINO_PIPE = os.environ.get('RAFIKI_WINO_PIPE', '0') != '0'
+WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1), (-10, 0, 1)) + (((-12, 0, 1),) if WINO_PIPE else ())
+_WINO_VARIANT = {-1: 0, -2: 1, -8: 2, -9: 3, -10: 4, -12: 5}   # -12: 8-wave 64x32, two-stage pipelined
 
 
 def _wino_variant(cfg):
-    return {-1: 0, -2: 1, -8: 2, -9: 3, -10: 4}[cfg[0]]
+    return _WINO_VARIANT[cfg[0]]
 
 
 def wino_ok(H: int, W: int, C: int) -> bool:
@@ -409,7 +413,13 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
 
 # ----------------------------------------------------------------- Winograd F(4x4, 3x3) forward
 # autotune candidates that run rk_wino4_conv: 8-wave 64 tiles x 32 channels (variant 0) / 4-wave 32 x 32
-WINO4_CFGS = ((-5, 0, 1), (-6, 0, 1))
+# (variant 1) / 4-wave 32 x 32 over two LDS stages, software-pipelined (variant 2)
+WINO4_CFGS = ((-5, 0, 1), (-6, 0, 1)) + (((-11, 0, 1),) if WINO_PIPE else ())
+_WINO4_VARIANT = {-5: 0, -6: 1, -11: 2}
+
+
+def _wino4_variant(cfg):
+    return _WINO4_VARIANT[cfg[0]]
 WINO4 = os.environ.get('RAFIKI_WINOGRAD4', '1') != '0'
 
 
@@ -487,7 +497,8 @@ WINO4_WGRAD = -7  # autotune tile id of the F(4x4) weight gradient (cfg = (-7, 0
 
 
 def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
-    """Split-K choices of rk_wino4_wgrad_v (variant 0: 32 co x 32 ci blocks, 1: 64 co x 32 ci): 128..4096
+    """Split-K choices of rk_wino4_wgrad_v (variant 0: 32 co x 32 ci blocks, 1: 64 co x 32 ci, 2: 32 x 32
+    software-pipelined over two LDS stages): 128..4096
     blocks, >= 4 chunks of 8 tiles per block, slabs <= 256 MiB.  cfg = (WINO4_WGRAD, variant, splits)."""
     if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and Cin >= 8 and Cout >= 16):
         return []
@@ -495,7 +506,7 @@ def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
         return []
     out = []
-    for v, bco in ((0, 32), (1, 64)):
+    for v, bco in ((0, 32), (1, 64)) + (((2, 32),) if WINO_PIPE else ()):
         if v == 1 and Cout < 64:
             continue
         base = cdiv(Cout, bco) * cdiv(Cin, 32)
@@ -1135,7 +1146,7 @@ def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=Non
 
         def extra(cfg):
             if cfg in WINO4_CFGS:
-                wino4_conv_grp(x, wino4, out=out, bias=bias, relu=act == ACT_RELU, variant=-5 - cfg[0])
+                wino4_conv_grp(x, wino4, out=out, bias=bias, relu=act == ACT_RELU, variant=_wino4_variant(cfg))
             else:
                 wino_conv_grp(x, wino, out=out, bias=bias, relu=act == ACT_RELU, variant=_wino_variant(cfg))
         extra.cfgs = (WINO_CFGS if w2 else ()) + (WINO4_CFGS if w4 else ())

@@ -37,9 +37,9 @@ for (N, H, C, K) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128),
     u4 = S.wino4_u(w)
     acc = torch.zeros((S.bn_slots(K), 2, K), dtype=torch.float64, device='cuda')
     r = dict(N=N, H=H, C=C, K=K)
-    for v in (0, 1, 2, 3, 4):
+    for v in (0, 1, 2, 3, 4, 5):
         r['w2_v%d_us' % v] = round(t(lambda: S.wino_conv(x, u, stats=acc, variant=v)), 1)
-    for v in (0, 1):
+    for v in (0, 1, 2):
         r['w4_v%d_us' % v] = round(t(lambda: S.wino4_conv(x, u4, stats=acc, variant=v)), 1)
     r['wt2_us'] = round(t(lambda: S.wino_weights(w, u, ut)), 1)
     r['wt4_us'] = round(t(lambda: S.wino4_u(w)), 1)
@@ -49,15 +49,15 @@ for (N, H, C, K) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128),
     if tw:
         sb = min(tw, key=tw.get)
         r['wg2_us'], r['wg2_splits'] = round(tw[sb], 1), sb
-    for v in (0, 1):
+    for v in (0, 1, 2):
         tw = {c[2]: t(lambda: S.wino4_wgrad(dy, x, dw, splits=c[2], variant=v))
               for c in S._wino4_wgrad_cands(N, H, H, K, C) if c[1] == v}
         if tw:
             sb = min(tw, key=tw.get)
             r['wg4_v%d_us' % v], r['wg4_v%d_splits' % v] = round(tw[sb], 1), sb
     fl = 2.0 * N * H * H * K * 9 * C
-    best2 = min(r['w2_v%d_us' % v] for v in range(5))
-    best4 = min(r['w4_v0_us'], r['w4_v1_us'])
+    best2 = min(r['w2_v%d_us' % v] for v in range(6))
+    best4 = min(r['w4_v%d_us' % v] for v in range(3))
     r['speedup_4_over_2'] = round(best2 / best4, 3)
     r['w4_direct_equiv_tflops'] = round(fl / best4 / 1e6, 1)
     # accuracy on the first 8 images

@@ -4,6 +4,7 @@ F(4x4,3x3)'s transforms have coefficients up to 8 (A^T) and 5 (B^T), so its fp32
 ten times F(2x2)'s (profiles/winograd_error_r2.jsonl); the gate is 3e-5 relative Frobenius error,
 against ~1e-6 measured."""
 import math
+import os
 
 import pytest
 import torch
@@ -12,6 +13,9 @@ import torch.nn.functional as TF
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 TOL = 3e-5
+# the software-pipelined variants (2) are exercised with the candidate switch that enables them
+PIPE = os.environ.get('RAFIKI_WINO_PIPE', '0') != '0'
+VARIANTS = [0, 1, 2] if PIPE else [0, 1]
 
 
 def rel(a, b):
@@ -36,7 +40,7 @@ def _w2(w):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [
     (2, 8, 8, 16, 32), (3, 4, 12, 24, 40), (4, 32, 32, 64, 64), (8, 4, 4, 512, 512), (2, 4, 4, 8, 72),
     (5, 16, 16, 128, 128), (1, 12, 20, 8, 8), (3, 8, 8, 256, 96)])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_wino4_fwd_and_stats(N, H, W, Cin, Cout, variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=1)
@@ -64,7 +68,7 @@ def test_wino4_bias_relu():
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 16, 16, 64, 64), (8, 4, 4, 512, 256),
                                             (2, 4, 8, 24, 16)])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_wino4_dgrad_from_flipped_set(N, H, W, Cin, Cout, variant):
     """dx = conv(dy, flip(w)^T) from the ut set."""
     from rafiki_amd.ops import f32 as S
@@ -80,7 +84,7 @@ def test_wino4_dgrad_from_flipped_set(N, H, W, Cin, Cout, variant):
 
 
 @pytest.mark.parametrize("pool", [False, True])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("H", [8, 4])
 def test_wino4_dgrad_bn_epilogues_match_direct(pool, variant, H):
     """The BNB / BNP epilogues give the same dx and BN-backward sums as the direct kernel's."""
@@ -108,7 +112,7 @@ def test_wino4_dgrad_bn_epilogues_match_direct(pool, variant, H):
 
 
 @pytest.mark.parametrize("shared", [True, False])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_wino4_conv_grouped(shared, variant):
     """k convs in one grid (the serving ensemble's layers) == k separate convs."""
     from rafiki_amd.ops import f32 as S
@@ -128,7 +132,7 @@ def test_wino4_conv_grouped(shared, variant):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 32, 32, 64, 64), (16, 4, 4, 256, 512),
                                             (3, 4, 12, 24, 40), (2, 4, 4, 16, 16)])
 @pytest.mark.parametrize("splits", [1, 2, 5])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_wino4_wgrad(N, H, W, Cin, Cout, splits, variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=30)

@@ -4,6 +4,7 @@ kernels of csrc/kernels/winograd4.hip) vs fp64 PyTorch references.
 F(2x2,3x3) adds a few fp32 roundings in the input / output transforms (values up to 4x the inputs),
 measured ~1e-7 relative; the gate is the same 1e-5 relative Frobenius error as the direct kernels."""
 import math
+import os
 
 import pytest
 import torch
@@ -11,6 +12,8 @@ import torch.nn.functional as TF
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
+# variant 5 (software-pipelined) is exercised with the candidate switch that enables it
+VARIANTS = [0, 1, 2, 3, 4, 5] if os.environ.get('RAFIKI_WINO_PIPE', '0') != '0' else [0, 1, 2, 3, 4]
 
 
 def rel(a, b):
@@ -40,7 +43,7 @@ def _u(w):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [
     (2, 8, 8, 16, 32), (3, 6, 10, 24, 40), (4, 32, 32, 64, 64), (8, 4, 4, 512, 512), (2, 2, 2, 8, 72),
     (5, 16, 16, 128, 128), (1, 12, 20, 8, 8)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_wino_fwd_and_stats(N, H, W, Cin, Cout, variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=1)
@@ -69,7 +72,7 @@ def test_wino_bias_relu():
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 16, 16, 64, 64), (8, 4, 4, 512, 256),
                                             (2, 6, 6, 24, 16)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_wino_dgrad_from_transposed_set(N, H, W, Cin, Cout, variant):
     """dx = conv(dy, flip(w)^T) from the ut set (transpose of u with positions 0 <-> 3 swapped)."""
     from rafiki_amd.ops import f32 as S
@@ -86,7 +89,7 @@ def test_wino_dgrad_from_transposed_set(N, H, W, Cin, Cout, variant):
 
 
 @pytest.mark.parametrize("pool", [False, True])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("H", [8, 4])
 def test_wino_dgrad_bn_epilogues_match_direct(pool, variant, H):
     """The BNB / BNP epilogues (ReLU mask / pool routing + BN-backward sums of the layer below) give
@@ -156,7 +159,7 @@ def test_wino_wgrad(N, H, W, Cin, Cout, splits):
 
 
 @pytest.mark.parametrize("shared", [True, False])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_wino_conv_grouped(shared, variant):
     """k convs in one grid (the serving ensemble's layers) == k separate convs."""
     from rafiki_amd.ops import f32 as S
