@@ -332,9 +332,12 @@ WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
 # autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1),
 # and the 16x16-wave-tile kernels of winograd4.hip: 4-wave 32x32 (variant 2), 2-wave 16x32 (variant 3),
 # 8-wave 64x32 (variant 4)
-# RAFIKI_WINO_PIPE=0 drops the software-pipelined (two LDS stage) variants from the candidate lists
+# software-pipelined (two LDS stage) variants: the F(2x2) 8-wave one wins the 4x4-map layers and is a
+# default candidate; the F(4x4) ones (one wave per SIMD) measured 1.3-1.5x slower than the single-stage
+# kernels on every VGG-small layer (profiles/winograd_variants_r2e.jsonl) and join the candidates only
+# with RAFIKI_WINO_PIPE=1
 WINO_PIPE = os.environ.get('RAFIKI_WINO_PIPE', '0') != '0'
-WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1), (-10, 0, 1)) + (((-12, 0, 1),) if WINO_PIPE else ())
+WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1), (-10, 0, 1), (-12, 0, 1))
 _WINO_VARIANT = {-1: 0, -2: 1, -8: 2, -9: 3, -10: 4, -12: 5}   # -12: 8-wave 64x32, two-stage pipelined
 
 

@@ -4,7 +4,6 @@ kernels of csrc/kernels/winograd4.hip) vs fp64 PyTorch references.
 F(2x2,3x3) adds a few fp32 roundings in the input / output transforms (values up to 4x the inputs),
 measured ~1e-7 relative; the gate is the same 1e-5 relative Frobenius error as the direct kernels."""
 import math
-import os
 
 import pytest
 import torch
@@ -12,8 +11,7 @@ import torch.nn.functional as TF
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
-# variant 5 (software-pipelined) is exercised with the candidate switch that enables it
-VARIANTS = [0, 1, 2, 3, 4, 5] if os.environ.get('RAFIKI_WINO_PIPE', '0') != '0' else [0, 1, 2, 3, 4]
+VARIANTS = [0, 1, 2, 3, 4, 5]   # 2-5: winograd4.hip's 16x16-wave-tile kernels (5: two-stage pipelined)
 
 
 def rel(a, b):
