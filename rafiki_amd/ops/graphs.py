@@ -11,6 +11,7 @@ never interleave.
 from __future__ import annotations
 
 import contextlib
+import gc
 import threading
 
 import torch
@@ -18,8 +19,24 @@ import torch
 LOCK = threading.RLock()
 
 
+_depth = [0, False]   # [nesting depth of capture() in this process, gc enabled before the outermost]
+
+
 @contextlib.contextmanager
 def capture(graph: "torch.cuda.CUDAGraph", pool=None, stream=None):
+    # Python's cyclic GC must not run while a capture is open: a collection can destroy an unreachable
+    # CUDAGraph / event whose destructor calls into HIP, which is illegal on a capturing thread, and a
+    # C++ destructor cannot report the error (the process aborts).  torch.cuda.graph collects once
+    # before the capture begins; further collections wait until the outermost capture has ended.
     with LOCK:
-        with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode='thread_local'):
-            yield
+        if _depth[0] == 0:
+            _depth[1] = gc.isenabled()
+            gc.disable()
+        _depth[0] += 1
+        try:
+            with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode='thread_local'):
+                yield
+        finally:
+            _depth[0] -= 1
+            if _depth[0] == 0 and _depth[1]:
+                gc.enable()
