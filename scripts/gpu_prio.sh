@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+rm -f gpurun_out/*.log
+timeout -k 10 400 python -u -m pytest tests/test_winograd_gpu.py tests/test_winograd4_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/w_tests.log 2>&1 && \
+timeout -k 10 180 python -u scripts/bench_winograd4.py gpurun_out/w_bench.jsonl > gpurun_out/w_bench.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --trials 0 --no-serving > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --trials 0 --no-serving > gpurun_out/bench2.log 2>&1
+rc=$?
+tail -2 gpurun_out/w_tests.log; cut -c1-400 gpurun_out/w_bench.log; tail -1 gpurun_out/bench.log | cut -c1-250; tail -1 gpurun_out/bench2.log | cut -c1-250
+exit $rc
