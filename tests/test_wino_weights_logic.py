@@ -1,0 +1,105 @@
+"""CPU test of WinoWeights' live-set bookkeeping (rafiki_amd/ops/f32.py): which Winograd weight sets a
+step refreshes, the on-demand transform of a set outside the live group, and that narrowing never
+happens while a hipGraph capture is open.  The kernel launcher is replaced by a recorder, so this
+runs without a GPU; the GPU test test_winograd4_gpu.py checks the transformed values themselves."""
+import torch
+
+from rafiki_amd.ops import f32 as S
+
+
+class Recorder:
+    def __init__(self):
+        self.calls = []
+
+    def __call__(self, name, *args):
+        self.calls.append((name, args))
+        return 0
+
+    def names(self):
+        return [c[0] for c in self.calls]
+
+
+def _setup(monkeypatch, capturing=False):
+    rec = Recorder()
+    monkeypatch.setattr(S._lib, 'call', rec)
+    monkeypatch.setattr(S, '_s', lambda: None)
+    monkeypatch.setattr(S, '_p', lambda t: None if t is None else t.data_ptr())   # host tensors are fine here
+    monkeypatch.setattr(torch.cuda, 'is_current_stream_capturing', lambda: capturing)
+    shapes = [(64, 32), (16, 64), (40, 24)]
+    arena = torch.zeros(sum(co * 9 * ci for co, ci in shapes) + 3)
+    ws, off = [], 3
+    for co, ci in shapes:
+        ws.append(arena[off:off + co * 9 * ci].view(co, 9 * ci))
+        off += co * 9 * ci
+    ww = S.WinoWeights(arena, ws, hw=[8, 6, 4], f4=True)
+    return rec, ww
+
+
+def _tables(ww):
+    """{family: {layer: (u_offset, ut_offset)}} of the tables refresh() launches with."""
+    out = {}
+    layer_of = {so: l for l, (so, _, _) in enumerate(ww._layers)}
+    for fam, desc, meta, nb in ww._prepare(ww.live):
+        m = meta.view(-1, 5)
+        rows = sorted({int(x) for x in desc.view(-1, 4)[:, 0]})   # meta rows the blocks point at
+        assert rows == list(range(m.shape[0])) and nb == desc.view(-1, 4).shape[0]
+        out[fam] = {layer_of[int(m[r, 0])]: (int(m[r, 1]), int(m[r, 2])) for r in rows}
+    return out
+
+
+def test_sets_per_layer_follow_map_size(monkeypatch):
+    _, ww = _setup(monkeypatch)
+    assert ww.has('u2', 1) and ww.has('ut2', 1) and not ww.has('u4', 1)   # 6x6 map: no F(4x4) set
+    assert ww.has('u4', 0) and ww.has('ut4', 2)
+    assert ww.u4(1) is None and ww.u4(0).shape == (36, 64, 32) and ww.ut(2).shape == (16, 24, 40)
+
+
+def test_refresh_narrows_to_the_sets_a_step_used(monkeypatch):
+    rec, ww = _setup(monkeypatch)
+    ww.refresh()
+    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi']   # everything live
+    ww.end_step()                      # nothing read: keep everything
+    assert len(ww.live) == 10
+    ww.refresh()
+    ww.lazy('u4', 0)()
+    ww.lazy('ut2', 2)()
+    ww.end_step()
+    assert ww.live == frozenset({('u4', 0), ('ut2', 2)})
+    t = _tables(ww)
+    assert set(t) == {'2', '4'}
+    assert t['2'] == {2: (-1, ww._sets[('ut2', 2)][0])}          # gradient set only
+    assert t['4'] == {0: (ww._sets[('u4', 0)][0], -1)}           # forward set only
+    rec.calls.clear()
+    ww.refresh()
+    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi']
+    # a set outside the live group is transformed on demand, once per step
+    ww.lazy('u2', 1)()
+    ww.lazy('u2', 1)()
+    assert rec.names()[2:] == ['rk_wino_weights']
+    _, args = rec.calls[2]
+    assert args[1] is not None and args[2] is None                 # forward set, no gradient set
+
+
+def test_no_narrowing_inside_capture(monkeypatch):
+    rec, ww = _setup(monkeypatch, capturing=True)
+    ww.refresh()
+    ww.lazy('u2', 0)()
+    ww.end_step()
+    assert len(ww.live) == 10                                      # tables cannot be rebuilt in a capture
+
+
+def test_sconvwt_refresh_is_lazy(monkeypatch):
+    rec = Recorder()
+    monkeypatch.setattr(S._lib, 'call', rec)
+    monkeypatch.setattr(S, '_s', lambda: None)
+    monkeypatch.setattr(S, '_p', lambda t: None if t is None else t.data_ptr())
+    arena = torch.zeros(16 * 9 * 8 + 8 * 9 * 16)
+    wt = S.SConvWT(arena, [arena[:16 * 72].view(16, 3, 3, 8), arena[16 * 72:].view(8, 3, 3, 16)])
+    wt.begin_step()
+    assert rec.names() == []                                       # no tuned dgrad used it yet
+    v = wt.lazy(1)()
+    wt.lazy(0)()
+    assert rec.names() == ['rk_swt'] and v.shape == (16, 9 * 8)
+    wt.begin_step()
+    wt.lazy(0)()
+    assert rec.names() == ['rk_swt', 'rk_swt']
