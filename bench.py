@@ -124,7 +124,8 @@ def phase_throughput(args, info, dev):
     torch.cuda.synchronize()
     D.barrier(info)
     torch.cuda.synchronize()
-    elapsed = D.all_reduce_max(info, time.perf_counter() - t0)
+    own = time.perf_counter() - t0
+    elapsed = D.all_reduce_max(info, own)
     seen = max(1, int(eng.seen.item()))
     loss = float(eng.loss_sum.item()) / seen
     acc = float(eng.correct.item()) / seen
@@ -132,7 +133,7 @@ def phase_throughput(args, info, dev):
     if info.is_main:
         for r in range(world):  # training accuracy over the timed window as the trial signal
             advisor.feedback(proposals[r], float(table[r, 1]))
-    out = dict(elapsed=elapsed, loss=loss, acc=acc, knobs=proposals[0], dtype=eng.dtype,
+    out = dict(elapsed=elapsed, own_elapsed=own, loss=loss, acc=acc, knobs=proposals[0], dtype=eng.dtype,
                train_flops_per_image=eng.train_flops_per_image(), use_graph=use_graph)
     del eng, data, y_all
     torch.cuda.empty_cache()
@@ -249,10 +250,24 @@ def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30):
 
 def main():
     args = parse()
+    from rafiki_amd.config import NodeConfig
     from rafiki_amd.parallel import dist as D
+    from rafiki_amd.parallel import launch as L
+
+    backend = NodeConfig().dist_backend
+    if not L.under_launcher():
+        if args.gpus > 1:
+            # started without torchrun: spawn one rank per GPU before this process touches HIP
+            L.check_devices(args.gpus, backend)
+            sys.exit(L.spawn([sys.executable, '-u', os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+    elif int(os.environ['WORLD_SIZE']) != args.gpus:
+        raise SystemExit('bench: WORLD_SIZE={} but --gpus {}'.format(os.environ['WORLD_SIZE'], args.gpus))
+    elif args.gpus > 1:
+        L.check_devices(args.gpus, backend)
 
     info = D.init_distributed()
     world = info.world_size
+    assert world == args.gpus, (world, args.gpus)
     ndev = max(1, torch.cuda.device_count())
     # one GPU per rank; the gloo rehearsal backend wraps ranks onto the GPUs present
     gpu = info.local_rank if info.backend == 'nccl' else info.local_rank % ndev
@@ -265,6 +280,8 @@ def main():
     ms = th['elapsed'] * 1000.0 / args.steps
     ips_trial = B * args.steps / th['elapsed']
     ips_total = ips_trial * world if n_devices == world else None  # no aggregate when ranks share a GPU
+    # per-rank rates from each rank's own timed window (the headline uses the max-over-ranks time)
+    per_rank = D.gather_floats(info, [B * args.steps / th['own_elapsed']])[:, 0].tolist()
 
     trials = None
     serving = None
@@ -296,7 +313,10 @@ def main():
                        'optimizer': 'SGD nesterov momentum + wd (fused flat-arena kernel)',
                        'hipgraph': th['use_graph']},
             'backend': info.backend,
+            'world_size': D.world_size(info),
             'n_devices': n_devices,
+            'images_per_sec_per_rank_min': round(min(per_rank), 1),
+            'images_per_sec_per_rank_max': round(max(per_rank), 1),
             'images_per_sec_per_trial': round(ips_trial, 1),
             # direct-computation model FLOPs / time (the Winograd convs execute 4/9 of the conv MACs)
             'model_tflops': round(th['train_flops_per_image'] * ips_trial * n_devices / 1e12, 2),

@@ -146,6 +146,13 @@ def broadcast_object(info: DistInfo, obj):
     return lst[0]
 
 
+def world_size(info: DistInfo) -> int:
+    """The process group's own size (not the env's claim); 1 without a group."""
+    if info.world_size > 1 and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
 def destroy(info: DistInfo):
     if info.world_size > 1 and dist.is_initialized():
         dist.destroy_process_group()
