@@ -37,24 +37,31 @@ def _simplify(v):
     return v
 
 
+PROPOSALS = [0]   # knob sets proposed by any advisor in this process (tests assert where GPs run)
+
+
 class BaseAdvisor:
     def __init__(self, knob_config, seed=None):
         self.knob_config = dict(knob_config)
         self.rng = np.random.default_rng(seed)
-        self._lock = threading.Lock()
+        self._lock = threading.Lock()    # history / pending
+        self._plock = threading.Lock()   # one proposal computation at a time (rng, GP state)
         self.history = []  # (knobs, score)
         self._pending = []
 
     def propose(self):
-        with self._lock:
-            knobs = self._propose_locked(1)[0]
-            self._pending.append(knobs)
-            return knobs
+        return self.propose_batch(1)[0]
 
     def propose_batch(self, q):
-        with self._lock:
-            out = self._propose_locked(q)
-            self._pending.extend(out)
+        # the GP fit runs on a snapshot, outside the lock: feedback() from another thread never waits
+        # behind a fit; proposals of concurrent callers are serialised by the proposal lock only
+        with self._plock:
+            with self._lock:
+                PROPOSALS[0] += q
+                history, pending = list(self.history), list(self._pending)
+            out = self._propose_from(q, history, pending)
+            with self._lock:
+                self._pending.extend(out)
             return out
 
     def feedback(self, knobs, score):
@@ -80,7 +87,7 @@ class BaseAdvisor:
                 raise TypeError('unknown knob type {}'.format(type(k)))
         return knobs
 
-    def _propose_locked(self, q):
+    def _propose_from(self, q, history, pending):
         return [self._random_knobs() for _ in range(q)]
 
     @property
@@ -106,7 +113,9 @@ class _GP:
 
     @staticmethod
     def _dist(A, B):
-        return np.sqrt(np.maximum(((A[:, None, :] - B[None, :, :]) ** 2).sum(-1), 0.0))
+        # |a|^2 + |b|^2 - 2 a.b: one GEMM instead of an [n, m, d] broadcast
+        d2 = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2.0 * (A @ B.T)
+        return np.sqrt(np.maximum(d2, 0.0))
 
     def _kd(self, D):
         d = D / self.ls
@@ -216,13 +225,14 @@ class GpAdvisor(BaseAdvisor):
                 keep = ~flip
                 u[keep, c:c + d] = self._encode(knobs)[c:c + d]
             parts.append(u)
-        return self._snap(np.concatenate(parts))
+        # discrete knobs snap many samples onto the same point: score each distinct point once
+        return np.unique(self._snap(np.concatenate(parts)), axis=0)
 
-    def _propose_locked(self, q):
+    def _propose_from(self, q, history, pending_in):
         if self.dims == 0:
             return [self._random_knobs() for _ in range(q)]
         out = []
-        obs = list(self.history)
+        obs = list(history)
         if len(obs) < self.n_init:
             n_rand = min(q, self.n_init - len(obs))
             out.extend(self._random_knobs() for _ in range(n_rand))
@@ -232,7 +242,7 @@ class GpAdvisor(BaseAdvisor):
                 return out
         scores = np.array([s for _, s in obs])
         lie = float(scores.mean())
-        pending = [p for p in self._pending] + list(out)
+        pending = list(pending_in) + list(out)
         top = [k for k, _ in sorted(obs, key=lambda t: -t[1])[:3]]
         X = np.stack([self._encode(k) for k, _ in obs] + [self._encode(p) for p in pending])
         y = np.concatenate([scores, np.full(len(pending), lie)])
@@ -244,8 +254,8 @@ class GpAdvisor(BaseAdvisor):
             z = (mu - best - self.xi) / sd
             ei = (mu - best - self.xi) * _norm_cdf(z) + sd * _norm_pdf(z)
             # never re-propose an observed or pending point
-            d2 = ((C[:, None, :] - X[None, :, :]) ** 2).sum(-1).min(1)
-            ei[d2 < 1e-12] = -np.inf
+            d2 = _GP._dist(C, X).min(1)
+            ei[d2 < 1e-6] = -np.inf
             i = int(np.argmax(ei))
             pick = decode_knobs(self.knob_config, C[i]) if np.isfinite(ei[i]) else self._random_knobs()
             pick = {k: _simplify(v) for k, v in pick.items()}

@@ -5,11 +5,15 @@ Reference parity: rafiki/worker/train.py (``TrainWorker.start`` :37-132, ``stop`
 train/evaluate -> pickle params to ``<workdir>/params/<trial_id>.model`` -> report score.
 
 MI355X-native redesign:
-  * rank 0 owns the sub-train-job's advisor (GP-EI) and the budget; each round it proposes one knob
-    set per rank and broadcasts them as one packed fp64 tensor over RCCL (gloo on CPU); every rank
-    trains its own trial on its own GPU; (score, ok, seconds) come back by all_gather and rank 0
-    feeds the GP.  No HTTP in the loop, one shared GP posterior, and the budget is decided by one
-    process (fixes the reference's budget race, train.py:50 / SURVEY §5.2);
+  * rank 0 owns the sub-train-job's ONE advisor (GP-EI); every rank trains its own trial on its own
+    GPU.  Default (``async``) scheduling: a rank that finishes a trial claims the next budget slot
+    atomically in the SQLite store, then exchanges one packed fp64 row with rank 0 over RCCL
+    point-to-point — its (score, ok, seconds) in, its next knob set out, proposed with every
+    in-flight trial as a constant-liar point (``parallel/exchange.py``).  No round barrier, no HTTP
+    in the loop, one GP posterior, and the budget can never overshoot (the reference's budget race,
+    train.py:50 / SURVEY §5.2);
+  * ``rounds`` scheduling (lock-step): rank 0 proposes one knob set per rank per round, broadcast as
+    one packed tensor over RCCL; scores come back by all_gather;
   * models that declare ``DATA_PARALLEL = True`` train ONE trial per round on all ranks jointly
     (bucketed gradient all-reduce inside the model), e.g. the PG-GAN;
   * a failed trial is marked ERRORED and the loop continues (bounded by ``max_trial_errors``)
@@ -64,10 +68,10 @@ class TrainWorker:
         os.makedirs(self._params_dir, exist_ok=True)
         self._max_trial_errors = max_trial_errors
         self._ckpt_every = checkpoint_every_epochs
-        # 'async' : ranks pull trials independently — an atomic budget claim in the store + a GP-EI
-        #           proposal over the shared history with in-flight trials as constant-liar points;
-        #           no round barrier, so heterogeneous trial lengths (epochs / batch size / width
-        #           knobs) never idle a GPU.  The default ('auto') for every non-data-parallel model.
+        # 'async' : ranks pull trials independently — an atomic budget claim in the store, then the
+        #           knobs from rank 0's single GP-EI advisor over RCCL (in-flight trials as constant-
+        #           liar points); no round barrier, so heterogeneous trial lengths (epochs / batch size /
+        #           width knobs) never idle a GPU.  The default ('auto') for every non-data-parallel model.
         # 'rounds': rank 0 proposes one knob set per rank per round, broadcast over RCCL (lock-step;
         #           every round waits for its slowest trial).  Data-parallel models always use it.
         self._scheduling = scheduling or os.environ.get('RAFIKI_TRIAL_SCHEDULING', 'auto')
@@ -98,10 +102,10 @@ class TrainWorker:
         clazz = load_model_class(model.model_file_bytes, model.model_class)
         knob_config = clazz.get_knob_config()
         data_parallel = bool(getattr(clazz, 'DATA_PARALLEL', False)) and info.world_size > 1
-        advisor = make_advisor(knob_config, self._advisor_type, self._seed) if info.is_main else None
         device = default_device()
         if self._scheduling in ('async', 'auto') and not data_parallel:
             return self._start_async(clazz, model, sub, train_job, knob_config, max_trials, deadline, device)
+        advisor = make_advisor(knob_config, self._advisor_type, self._seed) if info.is_main else None
         errors = 0
         # trials this worker was running when its previous incarnation died, with a checkpoint to
         # resume from; re-run first, under their original ids and knobs
@@ -158,47 +162,39 @@ class TrainWorker:
         """Asynchronous trial scheduling: every rank pulls its next trial as
         soon as its GPU is free — no round barrier, so one slow trial never idles the other GPUs.
 
-        * budget: an atomic claim in the store (``Database.claim_trial``);
-        * knobs: each rank fits the GP-EI advisor on the SHARED history (completed trials of the
-          sub-train-job) with every in-flight trial's knobs as constant-liar pending points, so
-          concurrent proposals spread out exactly as in a batched proposal;
-        * end: when the budget is exhausted, a last barrier and rank 0 closes the sub-train-job."""
-        import concurrent.futures as cf
+        * budget: an atomic claim in the store (``Database.claim_trial``), taken BEFORE asking for knobs;
+        * knobs/scores: ONE GP-EI advisor on rank 0 (``parallel.exchange.KnobExchange``).  A rank that
+          finishes a trial rings a doorbell in the rendezvous store and exchanges one packed fp64 row
+          with rank 0 over RCCL point-to-point (its score in, its next knob set out); rank 0 proposes
+          with every in-flight trial as a constant-liar pending point;
+        * end: a failed claim reports the last score and leaves; rank 0's server exits once every
+          peer has left, then a last barrier and rank 0 closes the sub-train-job."""
+        from ..parallel.exchange import KnobExchange
         info = self._dist
         errors = 0
-        n_local = 0
-        # propose-ahead: the knobs of this rank's NEXT trial are computed on a helper thread while the
-        # current trial runs (the current trial is one of the constant-liar pending points, exactly as
-        # in a batched proposal), so the GP fit never sits between two trials on the GPU
-        pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix='rafiki-advisor')
-
-        def propose(trial_id, extra_pending, salt):
-            history, pending = [], list(extra_pending)
-            for t in self._db.get_trials_of_sub_train_job(sub.id):
-                if t.id == trial_id or not t.knobs:
-                    continue
-                if t.status == TrialStatus.COMPLETED:
-                    history.append((dict(t.knobs), float(t.score)))
-                elif t.status in (TrialStatus.STARTED, TrialStatus.RUNNING):
-                    pending.append(dict(t.knobs))
-            seed = None if self._seed is None else int(self._seed) * 1000003 + info.rank * 7919 + salt
-            adv = make_advisor(knob_config, self._advisor_type, seed)
-            adv.history.extend(history)
-            adv._pending.extend(pending)
-            return adv.propose()
-
-        ahead = None
-        # trials this worker was running when its previous incarnation died, with a checkpoint to
-        # resume from (SURVEY §5.4): they keep their ids, knobs and budget slot, and run first
-        for tid, knobs in self._orphaned_trials(sub.id):
-            if self._stop:
-                break
-            ctx = TrialContext(device=device, dist=info, data_parallel=False)
-            t0 = time.perf_counter()
-            score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, True, resume_id=tid)
-            self.busy_s += time.perf_counter() - t0
-            errors = errors + 1 if not ok else 0
+        history = []
+        if info.is_main:   # a restarted job's GP starts from the durable record
+            history = [(dict(t.knobs), float(t.score)) for t in self._db.get_trials_of_sub_train_job(sub.id)
+                       if t.status == TrialStatus.COMPLETED and t.knobs]
+        ex = KnobExchange(info, knob_config, lambda: make_advisor(knob_config, self._advisor_type, self._seed),
+                          tag=str(sub.id), history=history)
+        self.exchange = ex
+        prev = None
         try:
+            # trials this worker was running when its previous incarnation died, with a checkpoint to
+            # resume from (SURVEY §5.4): they keep their ids, knobs and budget slot, and run first
+            for tid, knobs in self._orphaned_trials(sub.id):
+                if self._stop:
+                    break
+                ctx = TrialContext(device=device, dist=info, data_parallel=False)
+                t0 = time.perf_counter()
+                score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, True, resume_id=tid)
+                secs = time.perf_counter() - t0
+                self.busy_s += secs
+                errors = errors + 1 if not ok else 0
+                if prev is not None:   # fold the previous orphan's score in without asking for knobs
+                    ex.report(prev)
+                prev = (knobs, score, ok > 0, secs)
             while not self._stop and errors < self._max_trial_errors:
                 if deadline is not None and time.time() > deadline:
                     break
@@ -208,24 +204,25 @@ class TrainWorker:
                 if trial is None:
                     break
                 th = time.perf_counter()
-                knobs = ahead.result() if ahead is not None else propose(trial.id, [], n_local)
+                knobs = ex.request(prev)
                 self.gap_parts['propose'] += time.perf_counter() - th
-                ahead = pool.submit(propose, None, [dict(knobs)], n_local + 1)
                 ctx = TrialContext(device=device, dist=info, data_parallel=False)
                 t0 = time.perf_counter()
                 if self.first_trial_t is None:
                     self.first_trial_t = t0
                 score, ok = self._run_trial(clazz, model, sub, knobs, train_job, ctx, True, resume_id=trial.id)
                 self.last_trial_end_t = time.perf_counter()
-                self.busy_s += self.last_trial_end_t - t0
+                secs = self.last_trial_end_t - t0
+                self.busy_s += secs
                 errors = errors + 1 if not ok else 0
-                n_local += 1
+                prev = (knobs, score, ok > 0, secs)
         finally:
-            pool.shutdown(wait=True)
+            ex.finish(prev)
+            ex.close()
         if info.world_size > 1:
             D.barrier(info)
         if info.is_main:
-            logger.info('sub-train-job %s budget reached (async)', sub.id)
+            logger.info('sub-train-job %s budget reached (async, %s)', sub.id, ex.stats)
             self._db.mark_sub_train_job_as_stopped(self._db.get_sub_train_job(sub.id))
 
     def _orphaned_trials(self, sub_id):

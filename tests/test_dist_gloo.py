@@ -174,6 +174,7 @@ def _sleepy_group(rank, world, port, db_path, service_id, workdir, scheduling, o
     from rafiki_amd.db.database import Database
     from rafiki_amd.parallel import dist as D
     from rafiki_amd.worker.train import TrainWorker
+    from rafiki_amd.advisor import advisor as advisor_mod
     info = D.init_distributed(backend='gloo')
     D.barrier(info)
     w = TrainWorker(service_id, 'w{}'.format(rank), db=Database(db_path), dist_info=info, seed=rank,
@@ -183,7 +184,8 @@ def _sleepy_group(rank, world, port, db_path, service_id, workdir, scheduling, o
     wall = time.perf_counter() - t0
     with open(os.path.join(out_dir, 'idle{}.txt'.format(rank)), 'w') as f:
         f.write(repr((wall, w.busy_s, len(w.completed_trials), w.first_trial_t - t0 if w.first_trial_t else 0.0,
-                      time.perf_counter() - (w.last_trial_end_t or t0), w.gap_parts)))
+                      time.perf_counter() - (w.last_trial_end_t or t0), w.gap_parts,
+                      getattr(getattr(w, 'exchange', None), 'stats', None), advisor_mod.PROPOSALS[0])))
     D.destroy(info)
 
 
@@ -205,8 +207,12 @@ def _idle_fraction(scheduling, world=4, budget=48):
         res = [eval(open(os.path.join(d, 'idle{}.txt'.format(r))).read()) for r in range(world)]
         wall = max(r[0] for r in res)
         idle = 1.0 - sum(r[1] for r in res) / (world * wall)
-        print(scheduling, ['wall {:.2f} busy {:.2f} n {} start {:.3f} tail {:.3f} {}'.format(*r) for r in res])
+        print(scheduling, ['wall {:.2f} busy {:.2f} n {} start {:.3f} tail {:.3f} {} {} {}'.format(*r) for r in res])
         units = [t.knobs['units'] for t in trials]
+        if scheduling == 'auto':
+            # every proposal came from rank 0's single advisor: no GP was ever fit on another rank
+            assert all(r[7] == 0 for r in res[1:]), [r[7] for r in res]
+            assert res[0][7] >= budget and res[0][6]['remote_requests'] > 0, res[0][6:]
         return idle, trials, units
 
 
@@ -223,3 +229,46 @@ def test_async_scheduling_keeps_gpus_busy_with_unequal_trials():
     assert len(trials_r) == 48
     print('rounds idle fraction {:.3f}'.format(idle_rounds))
     assert idle_rounds > idle
+
+
+def _knobx(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rafiki_amd.advisor.advisor import GpAdvisor
+    from rafiki_amd.model.knob import FloatKnob, IntegerKnob
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.parallel.exchange import KnobExchange
+    info = D.init_distributed(backend='gloo')
+    kc = {'x': FloatKnob(0.0, 1.0), 'n': IntegerKnob(1, 4)}
+    ex = KnobExchange(info, kc, lambda: GpAdvisor(kc, seed=0), tag='t')
+    got, prev = [], None
+    for i in range(5):
+        k = ex.request(prev)
+        got.append(k)
+        prev = (k, 100.0 * rank + i, True, 0.01)   # a score that names its sender
+    ex.report((got[0], -1.0, False, 0.0))           # an errored trial: no score enters the GP
+    ex.finish(prev)
+    ex.close()
+    hist = sorted(s for _, s in ex.advisor.history) if info.is_main else None
+    with open(os.path.join(out_dir, 'x{}.txt'.format(rank)), 'w') as f:
+        f.write(repr((got, hist, ex.stats if info.is_main else None)))
+    D.destroy(info)
+
+
+def test_knob_exchange_scores_reach_rank0_advisor():
+    """Async exchange (parallel/exchange.py): each rank's scores arrive at rank 0's single GP over the
+    control group, every request is answered with a valid knob set, and errored trials add nothing."""
+    port = _free_port()
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_knobx, args=(world, port, d), nprocs=world, join=True)
+        res = [eval(open(os.path.join(d, 'x{}.txt'.format(r))).read()) for r in range(world)]
+        for got, _, _ in res:
+            assert len(got) == 5
+            for k in got:
+                assert 0.0 <= k['x'] <= 1.0 and k['n'] in (1, 2, 3, 4)
+        hist, stats = res[0][1], res[0][2]
+        assert hist == sorted(100.0 * r + i for r in range(world) for i in range(5))
+        assert stats['remote_requests'] == (world - 1) * (5 + 1 + 1)
+        # no two in-flight proposals were identical (constant-liar pending points)
+        firsts = [tuple(sorted(r[0][0].items())) for r in res]
+        assert len(set(firsts)) == world
