@@ -772,7 +772,9 @@ class ConvNetEngine:
                 c = torch.stack([rm, r, sc, fl.w(name + '.beta') - rm * sc])
             coeffs.append(c)
         self._eval_coeffs = coeffs
-        self._eval_graphs = {}
+        from ..ops.graphs import quiesced
+        with quiesced():
+            self._eval_graphs = {}
         self._eval_wino = None
         if self.f32 and S.WINO and self.blocks and self.device.type == 'cuda':
             self._eval_wino = S.WinoWeights(fl.master, [fl.w(b[0] + '.w') for b in self.blocks], dgrad=False,
@@ -880,10 +882,12 @@ class ConvNetEngine:
         """Drop what only training needs — the captured step graphs (and with them their private
         activation pools), static batch buffers, the step schedule and the optimizer state — so a
         finished trial can stay resident in HBM for serving at its inference footprint."""
-        for a in ('_graph', '_sched_graph', '_static_x', '_static_y', '_sched', '_ctr', '_ww', '_wt'):
-            if hasattr(self, a):
-                setattr(self, a, None)
-        self.opt = None
+        from ..ops.graphs import quiesced
+        with quiesced():
+            for a in ('_graph', '_sched_graph', '_static_x', '_static_y', '_sched', '_ctr', '_ww', '_wt'):
+                if hasattr(self, a):
+                    setattr(self, a, None)
+            self.opt = None
 
     # ---------------------------------------------------------------------------- state I/O
     def state_dict(self):

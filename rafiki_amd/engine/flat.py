@@ -157,8 +157,20 @@ class FlatParams:
 
     def load_state_dict(self, d):
         for s in self.specs:
-            if s.name in d:
-                self.w(s.name).copy_(torch.as_tensor(d[s.name], dtype=torch.float32).reshape(s.shape))
+            if s.name not in d:
+                continue
+            v = torch.as_tensor(d[s.name], dtype=torch.float32)
+            if v.numel() != math.prod(s.shape) and v.dim() == len(s.shape) and \
+                    tuple(v.shape[:-1]) == tuple(s.shape[:-1]):
+                # a conv stem saved with another input-channel padding (4 vs 8 fp32 channels,
+                # RAFIKI_WINOGRAD on/off, or a bf16 save): the padding channels are zero either way
+                out = torch.zeros(s.shape, dtype=torch.float32)
+                c = min(v.shape[-1], s.shape[-1])
+                if v.shape[-1] > c and bool(v[..., c:].any()):
+                    raise ValueError('{}: cannot drop non-zero input channels {}..{}'.format(s.name, c, v.shape[-1]))
+                out[..., :c] = v[..., :c]
+                v = out
+            self.w(s.name).copy_(v.reshape(s.shape))
         self.sync_bf16()
 
 

@@ -248,4 +248,6 @@ class NativeImageClassifier(BaseModel):
         return self._engine.resident_bytes() if self._engine is not None else 0
 
     def destroy(self):
-        self._engine = None
+        from ..ops.graphs import quiesced
+        with quiesced():   # the engine's captured graphs die here
+            self._engine = None

@@ -445,7 +445,9 @@ class GraphedRounds:
         self.captures = 0
 
     def clear(self):
-        self.graphs.clear()
+        from ..ops.graphs import quiesced
+        with quiesced():
+            self.graphs.clear()
         self.seen.clear()
 
     def run(self, key, fn):
@@ -463,8 +465,9 @@ class GraphedRounds:
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
         if self.collectives:
-            # let the process group's watchdog retire the eager rounds' (completed) all-reduce works
-            # before the capture starts, so it never polls their events while this thread captures
+            # opt-in path (see the RAFIKI_PGGAN_GRAPH_COLLECTIVES note in PgGan.train): give the process
+            # group's watchdog ~3 poll periods to retire the eager rounds' completed works before the
+            # capture starts.  Residual race: a stalled watchdog thread could still poll during it.
             time.sleep(0.3)
         with _capture(g):
             fn()
@@ -623,7 +626,13 @@ class PgGan(BaseModel):
         rng = TrialRng(dev, self.seed * 7919)   # one stream for all ranks; each keeps its shard
         # RCCL collectives are graph-capturable, gloo ones are not (a gloo group on GPUs is the
         # one-box multi-rank rehearsal: eager)
-        capturable = g_ar is None or self.ctx.dist.backend == 'nccl'
+        # Capturing rounds WITH collectives is opt-in (RAFIKI_PGGAN_GRAPH_COLLECTIVES=1): the process
+        # group's watchdog thread polls the events of the eager rounds' completed works on its own
+        # schedule, and torch exposes no hook to wait until it has retired them, so a capture could
+        # still overlap such a poll (GraphedRounds.run waits 0.3 s, ~3 watchdog periods: a residual
+        # race, not a guarantee).  Default: data-parallel rounds run eager, single-GPU ones captured.
+        capturable = g_ar is None or (self.ctx.dist.backend == 'nccl'
+                                      and os.environ.get('RAFIKI_PGGAN_GRAPH_COLLECTIVES', '0') == '1')
         graphs = GraphedRounds(dev.type == 'cuda' and capturable and bool(knobs.get('cuda_graph', True))
                                and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0', collectives=g_ar is not None)
         self.graphs = graphs
@@ -892,7 +901,10 @@ class PgGan(BaseModel):
         self.nets.load_state({k: pickle.loads(params[k]) for k in ('G', 'D', 'Gs')})
 
     def destroy(self):
-        self.nets = None
+        from ..ops.graphs import quiesced
+        with quiesced():
+            self.graphs = None
+            self.nets = None
 
 
 # ============================================================================== eval helpers

@@ -19,6 +19,15 @@ import torch
 LOCK = threading.RLock()
 
 
+@contextlib.contextmanager
+def quiesced():
+    """Hold while dropping the last reference to captured graphs (engine teardown, trainer ->
+    predictor handoff): a graph's destructor frees its exec and private memory pool, which must not
+    run while another thread of this process is capturing."""
+    with LOCK:
+        yield
+
+
 _depth = [0, False]   # [nesting depth of capture() in this process, gc enabled before the outermost]
 
 

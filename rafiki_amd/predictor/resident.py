@@ -24,10 +24,12 @@ logger = logging.getLogger(__name__)
 
 
 def _destroy(model):
-    try:
-        model.destroy()
-    except Exception:
-        pass
+    from ..ops.graphs import quiesced
+    with quiesced():
+        try:
+            model.destroy()
+        except Exception:
+            pass
 
 
 class ResidentStore:

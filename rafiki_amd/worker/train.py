@@ -307,10 +307,13 @@ class TrainWorker:
             return float('nan'), 0.0
         finally:
             if inst is not None:
-                try:
-                    inst.destroy()
-                except Exception:
-                    pass
+                from ..ops.graphs import quiesced
+                with quiesced():   # no other thread may be capturing while the model's graphs die
+                    try:
+                        inst.destroy()
+                    except Exception:
+                        pass
+                    inst = None
             model_logger.set_logger(prev_logger)
             if handler:
                 trial_logger.removeHandler(handler)

@@ -289,8 +289,9 @@ def test_dp_round_with_rccl_allreduce_is_graph_captured():
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     code = "import sys; sys.path.insert(0, {!r}); import test_pg_gan_gpu as t; t._dp_round_child(); print('DP-OK')"
+    env = dict(os.environ, RAFIKI_PGGAN_GRAPH_COLLECTIVES='1')   # capture of collective rounds is opt-in
     r = subprocess.run([sys.executable, '-c', code.format(here)], cwd=os.path.dirname(here), capture_output=True,
-                       text=True, timeout=100)
+                       text=True, timeout=100, env=env)
     assert r.returncode == 0 and 'DP-OK' in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
