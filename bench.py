@@ -12,10 +12,13 @@ Every part of it is measured in this run, none extrapolated:
            synthetic dataset; W untimed warmup steps, then K timed steps bracketed by barrier +
            synchronize on both sides, max over ranks.
   phase 2  trials/hour: the real AutoML loop — ``TrainWorker`` (async trial scheduling, atomic budget
-           claims in the SQLite store, GP-EI proposals with constant-liar pending points) runs
-           propose -> train -> evaluate -> pickle params -> record score for ``--trials`` trials per
-           GPU of the ``VggSmallTrial`` definition (2 epochs over 8192 non-separable synthetic images,
-           evaluated on 2048), after one untimed warm-up trial per GPU; wall time max over ranks.
+           claims in the SQLite store, knobs/scores exchanged with rank 0's single GP-EI advisor over
+           RCCL, constant-liar pending points) runs propose -> train -> evaluate -> pickle params ->
+           record score for ``--trials`` trials per GPU of the ``VggSmallTrial`` definition (10 epochs
+           over 50k non-separable synthetic CIFAR-shaped images, evaluated on 10k), after one untimed
+           warm-up trial per GPU; wall time max over ranks; per-trial breakdown of rank 0.
+  phase 2b overhead probe: ``--probe-trials`` trials per GPU of ``VggSmallProbe`` (2 epochs x 8192
+           images), where per-trial fixed costs dominate.
   phase 3  predictor ensemble QPS (rank 0, 1 GPU): the top-4 trials of phase 2 loaded from their
            params files into one ``Predictor``; hipGraph-captured forwards on 4 HIP streams + the
            on-device ensemble mean, device-resident uint8 batches of 256 (plus the batch-1 latency
@@ -40,8 +43,12 @@ import torch  # noqa: E402
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-TRAIN_URI = 'synthetic://image?n=8192&size=32&channels=3&classes=10&seed=0&noise=64&flip=0.1'
-TEST_URI = 'synthetic://image?n=2048&size=32&channels=3&classes=10&seed=1&noise=64&flip=0.1'
+# phase 2 headline trial: CIFAR-10-sized synthetic splits (50k train / 10k test, 32x32x3, 10 classes)
+TRAIN_URI = 'synthetic://image?n=50000&size=32&channels=3&classes=10&seed=0&noise=64&flip=0.1'
+TEST_URI = 'synthetic://image?n=10000&size=32&channels=3&classes=10&seed=1&noise=64&flip=0.1'
+# phase 2b overhead probe: ~64 training steps per trial
+PROBE_TRAIN_URI = 'synthetic://image?n=8192&size=32&channels=3&classes=10&seed=0&noise=64&flip=0.1'
+PROBE_TEST_URI = 'synthetic://image?n=2048&size=32&channels=3&classes=10&seed=1&noise=64&flip=0.1'
 
 
 def parse():
@@ -51,7 +58,8 @@ def parse():
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--batch', type=int, default=256, help='per-trial (per-GPU) batch size')
     ap.add_argument('--dataset-size', type=int, default=50000)
-    ap.add_argument('--trials', type=int, default=4, help='timed trials per GPU in phase 2 (0: skip)')
+    ap.add_argument('--trials', type=int, default=2, help='timed VggSmallTrial trials per GPU in phase 2 (0: skip)')
+    ap.add_argument('--probe-trials', type=int, default=4, help='timed overhead-probe trials per GPU (0: skip)')
     ap.add_argument('--no-serving', action='store_true', help='skip phase 3')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
@@ -140,7 +148,7 @@ def phase_throughput(args, info, dev):
     return out
 
 
-def _setup_job(db, budget, model_name, model_class):
+def _setup_job(db, budget, model_name, model_class, train_uri, test_uri):
     from rafiki_amd.models import model_file
     from rafiki_amd.utils.auth import hash_password
     u = db.get_user_by_email('bench@rafiki') or db.create_user('bench@rafiki', hash_password('bench'), 'ADMIN')
@@ -148,15 +156,32 @@ def _setup_job(db, budget, model_name, model_class):
     with open(model_file(model_name), 'rb') as f:
         m = db.create_model(u.id, model_class + '_' + tag, 'IMAGE_CLASSIFICATION', f.read(), model_class,
                             'rafiki_amd', {}, 'PRIVATE')
-    tj = db.create_train_job(u.id, 'bench_' + tag, 1, 'IMAGE_CLASSIFICATION', budget, TRAIN_URI, TEST_URI)
+    tj = db.create_train_job(u.id, 'bench_' + tag, 1, 'IMAGE_CLASSIFICATION', budget, train_uri, test_uri)
     sub = db.create_sub_train_job(tj.id, m.id, u.id)
     svc = db.create_service('TRAIN', 'bench', 'rafiki_amd', 1, 1)
     db.create_train_job_worker(svc.id, sub.id)
     return svc.id, sub.id
 
 
-def phase_trials(args, info, root):
-    """Run a warm-up sub-train-job (one trial per GPU) then a timed one (``--trials`` per GPU)."""
+def _mean_breakdown(records):
+    """Mean per-trial seconds: worker phases + the model's own phases (build / capture / loop / ...)."""
+    if not records:
+        return {}
+    out = {}
+    for k in ('claim', 'propose', 'train', 'evaluate', 'dump', 'record'):
+        vals = [r[k] for r in records if k in r]
+        if vals:
+            out[k] = round(sum(vals) / len(vals), 4)
+    mk = sorted({k for r in records for k in r.get('model', {})})
+    for k in mk:
+        vals = [r['model'][k] for r in records if k in r.get('model', {})]
+        out['train.' + k] = round(sum(vals) / len(vals), 4)
+    return out
+
+
+def phase_trials(args, info, root, model_class, per_gpu, train_uri, test_uri, warm=True):
+    """Timed sub-train-job of ``per_gpu`` trials per GPU (after an untimed warm-up one: one trial per
+    GPU).  Returns wall time (max over ranks), completed count, scores and rank 0's breakdown."""
     from rafiki_amd.db.database import Database
     from rafiki_amd.parallel import dist as D
     from rafiki_amd.worker.train import TrainWorker
@@ -169,30 +194,38 @@ def phase_trials(args, info, root):
     if info.is_main:
         os.makedirs(params, exist_ok=True)
         db = Database(db_path)
-        warm = _setup_job(db, {'MODEL_TRIAL_COUNT': world}, 'VggSmallTrial', 'VggSmallTrial')
-        timed = _setup_job(db, {'MODEL_TRIAL_COUNT': world * args.trials}, 'VggSmallTrial', 'VggSmallTrial')
-        ids = [warm[0], warm[1], timed[0], timed[1]]
+        w_ids = _setup_job(db, {'MODEL_TRIAL_COUNT': world}, model_class, model_class, train_uri, test_uri) \
+            if warm else (None, None)
+        timed = _setup_job(db, {'MODEL_TRIAL_COUNT': world * per_gpu}, model_class, model_class, train_uri, test_uri)
+        ids = [w_ids[0], w_ids[1], timed[0], timed[1]]
     ids = D.broadcast_object(info, ids)
     db = Database(db_path)
-    w = TrainWorker(ids[0], 'bench-w{}'.format(info.rank), db=db, dist_info=info, seed=args.seed,
-                    scheduling='async', params_dir=params)
-    w.start()
+    first = None
+    if warm:
+        t0 = time.perf_counter()
+        w = TrainWorker(ids[0], 'bench-w{}'.format(info.rank), db=db, dist_info=info, seed=args.seed,
+                        scheduling='async', params_dir=params, offer_resident=True)
+        w.start()
+        first = dict(_mean_breakdown(w.trial_records), wall=round(time.perf_counter() - t0, 3))
     D.barrier(info)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     w = TrainWorker(ids[2], 'bench-w{}'.format(info.rank), db=db, dist_info=info, seed=args.seed + 1,
-                    scheduling='async', params_dir=params)
+                    scheduling='async', params_dir=params, offer_resident=True)
     w.start()
     torch.cuda.synchronize()
     mine = time.perf_counter() - t0
     D.barrier(info)
     wall = D.all_reduce_max(info, mine)
-    busy = D.gather_floats(info, [mine])
+    busy = D.gather_floats(info, [mine, w.busy_s, len(w.completed_trials)])
     trials = db.get_trials_of_sub_train_job(ids[3])
     done = [t for t in trials if t.status == 'COMPLETED']
     scores = sorted((float(t.score) for t in done), reverse=True)
+    steady = _mean_breakdown(w.trial_records)
+    ex = getattr(w, 'exchange', None)
     return dict(wall=wall, n=len(done), errored=len(trials) - len(done), scores=scores, sub=ids[3], db=db,
-                busy=[float(b) for b in busy[:, 0]])
+                busy=[float(b) for b in busy[:, 1]], per_rank=[int(c) for c in busy[:, 2]], first=first,
+                steady=steady, exchange=dict(ex.stats) if (ex is not None and info.is_main) else None)
 
 
 def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30):
@@ -283,14 +316,18 @@ def main():
     # per-rank rates from each rank's own timed window (the headline uses the max-over-ranks time)
     per_rank = D.gather_floats(info, [B * args.steps / th['own_elapsed']])[:, 0].tolist()
 
-    trials = None
+    trials = probe = None
     serving = None
+    tag = os.environ.get('MASTER_PORT', '0') if world > 1 else str(os.getpid())
+    root = os.path.join(tempfile.gettempdir(), 'rafiki_bench_{}'.format(tag))
     if args.trials > 0:
-        tag = os.environ.get('MASTER_PORT', '0') if world > 1 else str(os.getpid())
-        root = os.path.join(tempfile.gettempdir(), 'rafiki_bench_{}'.format(tag))
-        trials = phase_trials(args, info, root)
-        if info.is_main and not args.no_serving:
-            serving = phase_serving(trials['db'], trials['sub'], dev)
+        trials = phase_trials(args, info, root, 'VggSmallTrial', args.trials, TRAIN_URI, TEST_URI)
+    if args.probe_trials > 0:
+        probe = phase_trials(args, info, root, 'VggSmallProbe', args.probe_trials, PROBE_TRAIN_URI, PROBE_TEST_URI,
+                             warm=False)
+    src = probe or trials
+    if src is not None and info.is_main and not args.no_serving:
+        serving = phase_serving(src['db'], src['sub'], dev)
 
     if info.is_main:
         out = {
@@ -329,10 +366,21 @@ def main():
             out['trials_measured'] = trials['n']
             out['trials_errored'] = trials['errored']
             out['trials_wall_s'] = round(trials['wall'], 3)
+            out['trials_per_rank'] = trials['per_rank']
             out['trial_busy_s_per_rank'] = [round(b, 3) for b in trials['busy']]
-            out['trial_definition'] = ('VggSmallTrial: GP-EI knobs (lr, momentum, wd), 2 epochs x 8192 images '
-                                       'batch 256 + eval on 2048, params pickled; async scheduling')
+            out['trial_definition'] = ('VggSmallTrial: GP-EI knobs (lr, momentum, wd) from rank 0 over RCCL, '
+                                       '10 epochs x 50000 synthetic CIFAR-shaped images, batch 256 + eval on '
+                                       '10000, params pickled; async scheduling; after 1 untimed warm-up trial/GPU')
             out['trial_scores'] = [round(s, 4) for s in trials['scores']]
+            out['trial_breakdown_s'] = {'first_trial_rank0': trials['first'], 'steady_mean_rank0': trials['steady']}
+            if trials['exchange'] is not None:
+                out['knob_exchange'] = {k: (round(v, 4) if isinstance(v, float) else v)
+                                        for k, v in trials['exchange'].items()}
+        if probe is not None:
+            out['probe_trials_per_hour'] = round(probe['n'] * 3600.0 / probe['wall'], 1)
+            out['probe_trials_measured'] = probe['n']
+            out['probe_definition'] = 'VggSmallProbe: 2 epochs x 8192 images + eval 2048 (~64 steps; overhead probe)'
+            out['probe_breakdown_s'] = probe['steady']
         if serving is not None:
             out['ensemble_qps'] = serving['device_b256']['qps']
             out['ensemble'] = serving

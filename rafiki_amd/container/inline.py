@@ -29,7 +29,7 @@ class InlineServiceRunner:
                 from ..parallel.dist import DistInfo
                 from ..worker.train import TrainWorker
                 db.mark_service_as_running(db.get_service(sid))
-                TrainWorker(sid, 'inline', db=db, dist_info=DistInfo()).start()
+                TrainWorker(sid, 'inline', db=db, dist_info=DistInfo(), offer_resident=True).start()
                 db.mark_service_as_stopped(db.get_service(sid))
                 w = db.get_train_job_worker(sid)
                 if w is not None:

@@ -13,6 +13,7 @@ MODELS_DIR = os.path.dirname(os.path.abspath(__file__))
 ZOO = {
     'VggSmall': ('vgg_small.py', 'IMAGE_CLASSIFICATION'),
     'VggSmallTrial': ('vgg_small.py', 'IMAGE_CLASSIFICATION'),
+    'VggSmallProbe': ('vgg_small.py', 'IMAGE_CLASSIFICATION'),
     'Vgg16': ('vgg16.py', 'IMAGE_CLASSIFICATION'),
     'FeedForward': ('feed_forward.py', 'IMAGE_CLASSIFICATION'),
     'SkDt': ('sk_models.py', 'IMAGE_CLASSIFICATION'),

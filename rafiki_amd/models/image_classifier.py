@@ -101,6 +101,7 @@ class NativeImageClassifier(BaseModel):
                 self._restore_ckpt(saved['state'], gen)
                 step, epoch = int(saved['state']['step']), int(saved['epoch']) + 1
                 logger.log('resumed from checkpoint after epoch {} (step {})'.format(saved['epoch'], step))
+        t_loop = time.perf_counter()
         while step < total:
             perm = torch.randperm(n, device=eng.device, generator=gen)
             eng.reset_metrics()
@@ -130,6 +131,9 @@ class NativeImageClassifier(BaseModel):
                 ck.save(self._ckpt_state(step, gen), epoch)
             faults.maybe_fail('crash', epoch=epoch, rank=ctx.rank)
             epoch += 1
+        if eng.device.type == 'cuda':
+            torch.cuda.synchronize(eng.device)
+        tm['loop'] = time.perf_counter() - t_loop
         if eng.device.type == 'cuda':
             logger.log(hbm_peak_bytes=int(torch.cuda.max_memory_allocated(eng.device)))
         t_pe = time.perf_counter()

@@ -3,12 +3,24 @@
 The best (tile shape, staging variant, split-K) differs per layer shape (measured on MI355X with
 scripts/bench_igemm.py: e.g. the LDS-DMA 2-stage ring wins on 16x16/8x8 layers, 64x64 register
 staging on the 4x4x512 layers).  The first time a shape is seen outside hipGraph capture, every
-candidate runs a few times under HIP events and the fastest is cached (in memory and, if
-``RAFIKI_TUNE_CACHE`` points to a file, on disk).  During capture only cached/heuristic configs
-are used, so captured graphs never contain tuning launches.
+candidate runs a few times under HIP events and the fastest is cached.  During capture only
+cached/heuristic configs are used, so captured graphs never contain tuning launches.
+
+The cache is a node-wide tuning database (MIOpen's perf-db idea), keyed by what the timings depend on:
+
+* file ``<WORKDIR>/tune/<gfx arch>-<kernel library hash>.json`` (``RAFIKI_TUNE_CACHE`` overrides the
+  path, ``RAFIKI_TUNE_CACHE=off`` keeps it in memory only).  A rebuilt kernel library or another GPU
+  architecture starts a fresh file, so stale picks are never replayed;
+* every worker process of the node shares it: a miss re-reads the file if another rank wrote it
+  since, and writes are merged under an exclusive ``flock`` (read + merge + atomic replace), so
+  concurrent ranks never drop each other's entries;
+* a read-only database shipped in the package (``rafiki_amd/tune/<arch>-<hash>.json``) seeds it,
+  so a fresh node whose kernel library matches starts warm.
 """
 from __future__ import annotations
 
+import fcntl
+import hashlib
 import json
 import os
 import threading
@@ -20,14 +32,52 @@ from .graphs import LOCK as _GRAPH_LOCK, capture as _capture
 _lock = threading.Lock()
 _cache = {}
 _loaded = False
-stats = {'tuned': 0, 'seconds': 0.0, 'candidates': 0}
+_disk_mtime = [None]
+stats = {'tuned': 0, 'seconds': 0.0, 'candidates': 0, 'loaded': 0, 'reloads': 0}
 ENABLED = os.environ.get('RAFIKI_AUTOTUNE', '1') != '0'
 REPS = int(os.environ.get('RAFIKI_AUTOTUNE_REPS', '3'))
 PASSES = int(os.environ.get('RAFIKI_AUTOTUNE_PASSES', '2'))
+SHIPPED_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tune')
+_ident = {}
+
+
+def _arch() -> str:
+    if 'arch' not in _ident:
+        try:
+            name = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+            _ident['arch'] = name.split(':')[0]
+        except Exception:
+            _ident['arch'] = os.environ.get('RAFIKI_OFFLOAD_ARCH', 'gfx950')
+    return _ident['arch']
+
+
+def lib_hash() -> str:
+    """Content hash of the kernel library the picks were timed with (12 hex digits)."""
+    if 'lib' not in _ident:
+        from ._lib import loaded_path as lib_path
+        h = hashlib.sha1()
+        try:
+            with open(lib_path(), 'rb') as f:
+                for chunk in iter(lambda: f.read(1 << 20), b''):
+                    h.update(chunk)
+            _ident['lib'] = h.hexdigest()[:12]
+        except OSError:
+            _ident['lib'] = 'nolib'
+    return _ident['lib']
+
+
+def db_name() -> str:
+    return '{}-{}.json'.format(_arch(), lib_hash())
 
 
 def _path():
-    return os.environ.get('RAFIKI_TUNE_CACHE', '')
+    p = os.environ.get('RAFIKI_TUNE_CACHE')
+    if p is not None and p.lower() in ('off', '0', 'none', ''):
+        return ''
+    if p:
+        return p
+    from ..config import get_config
+    return os.path.join(get_config().workdir, 'tune', db_name())
 
 
 def _tup(v):
@@ -35,19 +85,44 @@ def _tup(v):
     return tuple(_tup(x) for x in v) if isinstance(v, list) else v
 
 
+def _read(path):
+    try:
+        with open(path) as f:
+            return {_tup(json.loads(k)): _tup(v) for k, v in json.load(f).items()}
+    except (OSError, ValueError):
+        return {}
+
+
 def _load():
     global _loaded
     if _loaded:
         return
     _loaded = True
+    shipped = os.path.join(SHIPPED_DIR, db_name())
+    if os.path.exists(shipped):
+        got = _read(shipped)
+        _cache.update(got)
+        stats['loaded'] += len(got)
+    _refresh(force=True)
+
+
+def _refresh(force=False):
+    """Merge entries other processes wrote to the node database since we last looked."""
     p = _path()
-    if p and os.path.exists(p):
-        try:
-            with open(p) as f:
-                for k, v in json.load(f).items():
-                    _cache[_tup(json.loads(k))] = _tup(v)
-        except (OSError, ValueError):
-            pass
+    if not p:
+        return
+    try:
+        m = os.stat(p).st_mtime_ns
+    except OSError:
+        return
+    if not force and m == _disk_mtime[0]:
+        return
+    _disk_mtime[0] = m
+    got = _read(p)
+    for k, v in got.items():
+        _cache.setdefault(k, v)
+    stats['loaded'] += len(got)
+    stats['reloads'] += 1
 
 
 def _save():
@@ -55,10 +130,21 @@ def _save():
     if not p:
         return
     try:
-        tmp = p + '.tmp'
-        with open(tmp, 'w') as f:
-            json.dump({json.dumps(k): v for k, v in _cache.items()}, f)
-        os.replace(tmp, p)
+        os.makedirs(os.path.dirname(p) or '.', exist_ok=True)
+        with open(p + '.lock', 'a+') as lf:
+            fcntl.flock(lf, fcntl.LOCK_EX)
+            try:
+                merged = _read(p)
+                merged.update(_cache)       # this process's fresh timings win on a clash
+                tmp = '{}.{}.tmp'.format(p, os.getpid())
+                with open(tmp, 'w') as f:
+                    json.dump({json.dumps(k): v for k, v in merged.items()}, f)
+                os.replace(tmp, p)
+                _disk_mtime[0] = os.stat(p).st_mtime_ns
+                for k, v in merged.items():
+                    _cache.setdefault(k, v)
+            finally:
+                fcntl.flock(lf, fcntl.LOCK_UN)
     except OSError:
         pass
 
@@ -66,7 +152,11 @@ def _save():
 def lookup(key):
     with _lock:
         _load()
-        return _cache.get(key)
+        hit = _cache.get(key)
+        if hit is None:
+            _refresh()
+            hit = _cache.get(key)
+        return hit
 
 
 def can_tune():

@@ -56,7 +56,8 @@ class _TrialLogHandler(logging.Handler):
 
 class TrainWorker:
     def __init__(self, service_id, worker_id, db=None, dist_info: D.DistInfo = None, params_dir=None,
-                 max_trial_errors=3, advisor_type=None, seed=None, checkpoint_every_epochs=1, scheduling=None):
+                 max_trial_errors=3, advisor_type=None, seed=None, checkpoint_every_epochs=1, scheduling=None,
+                 offer_resident=None):
         from ..config import get_config
         from ..db.database import Database
         self._service_id = service_id
@@ -75,6 +76,10 @@ class TrainWorker:
         # 'rounds': rank 0 proposes one knob set per rank per round, broadcast over RCCL (lock-step;
         #           every round waits for its slowest trial).  Data-parallel models always use it.
         self._scheduling = scheduling or os.environ.get('RAFIKI_TRIAL_SCHEDULING', 'auto')
+        # keep finished models resident in HBM for a predictor IN THIS PROCESS (inline services, the
+        # bench, notebooks); a service-mode worker's predictor runs elsewhere and could never take them
+        self._offer_resident = (os.environ.get('RAFIKI_OFFER_RESIDENT', '0') == '1' if offer_resident is None
+                                else bool(offer_resident))
         self._advisor_type = advisor_type
         self._seed = seed
         self._trial_id = None
@@ -84,6 +89,7 @@ class TrainWorker:
         self.first_trial_t = None   # perf_counter at the first / after the last trial (idle accounting)
         self.last_trial_end_t = None
         self.gap_parts = {'claim': 0.0, 'propose': 0.0}  # async-loop seconds outside trials
+        self.trial_records = []   # per completed trial: claim / propose / train / evaluate / dump seconds
 
     # ------------------------------------------------------------------------------ main loop
     def start(self):
@@ -200,12 +206,15 @@ class TrainWorker:
                     break
                 tc = time.perf_counter()
                 trial = self._db.claim_trial(sub.id, model.id, self._worker_id, max_trials)
-                self.gap_parts['claim'] += time.perf_counter() - tc
+                claim_s = time.perf_counter() - tc
+                self.gap_parts['claim'] += claim_s
                 if trial is None:
                     break
                 th = time.perf_counter()
                 knobs = ex.request(prev)
-                self.gap_parts['propose'] += time.perf_counter() - th
+                propose_s = time.perf_counter() - th
+                self.gap_parts['propose'] += propose_s
+                self._next_gap = {'claim': claim_s, 'propose': propose_s}
                 ctx = TrialContext(device=device, dist=info, data_parallel=False)
                 t0 = time.perf_counter()
                 if self.first_trial_t is None:
@@ -271,12 +280,17 @@ class TrainWorker:
         model_logger.set_logger(trial_logger)
         inst = None
         try:
+            rec = dict(getattr(self, '_next_gap', None) or {})
+            self._next_gap = None
+            t_start = time.perf_counter()
             with use_context(ctx):
                 inst = clazz(**knobs)
                 with model_logger.phase('train'):
                     inst.train(train_job.train_dataset_uri)
+                t_train = time.perf_counter()
                 with model_logger.phase('evaluate'):
                     score = float(inst.evaluate(train_job.test_dataset_uri))
+                t_eval = time.perf_counter()
                 if not math.isfinite(score):
                     raise ValueError('non-finite score {}'.format(score))
                 params_path = None
@@ -288,14 +302,20 @@ class TrainWorker:
                     with open(tmp, 'wb') as f:
                         f.write(blob)
                     os.replace(tmp, params_path)
+            t_dump = time.perf_counter()
             if record:
                 self._db.mark_trial_as_complete(trial, score, params_path)
                 self.completed_trials.append((trial.id, score))
+                # per-trial breakdown (bench phase 2): the model's own phases (load / build / upload /
+                # capture / train loop / prepare_eval) when it reports them
+                rec.update(train=t_train - t_start, evaluate=t_eval - t_train, dump=t_dump - t_eval,
+                           record=time.perf_counter() - t_dump, model=dict(getattr(inst, 'timings', {}) or {}))
+                self.trial_records.append(rec)
                 ctx.checkpoint.remove()
                 # in-process trainer -> predictor handoff: a kept model stays resident in HBM (the
                 # params file above remains the durable copy)
                 from ..predictor.resident import STORE
-                if not ctx.data_parallel and STORE.offer(trial.id, inst, score):
+                if self._offer_resident and not ctx.data_parallel and STORE.offer(trial.id, inst, score):
                     inst = None
             return score, 1.0
         except Exception:
