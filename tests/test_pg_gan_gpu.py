@@ -242,8 +242,11 @@ def test_graphed_rounds_match_eager():
         outs.append((nets.G.master.clone(), nets.D.master.clone(), acc.clone()))
     (g0, d0, a0), (g1, d1, a1) = outs
     assert torch.isfinite(a1).all()
-    assert cos(g0, g1) > 0.9999 and cos(d0, d1) > 0.9999
-    assert rel_err(a1, a0) < 5e-2
+    # fp32, same kernels, same RNG stream: only reduction-order noise may separate the two runs
+    print('graphed vs eager frob G {:.2e} D {:.2e} acc rel {:.2e}'.format(frob(g1, g0), frob(d1, d0),
+                                                                          rel_err(a1, a0)))
+    assert frob(g1, g0) <= 1e-5 and frob(d1, d0) <= 1e-5
+    assert rel_err(a1, a0) < 1e-4
 
 
 @pytest.mark.parametrize("N,H,C,segs", [(8, 4, 24, 1), (16, 4, 512, 2), (12, 2, 40, 3), (8, 4, 12, 2)])
