@@ -37,10 +37,10 @@ class InlineServiceRunner:
                     sub = db.get_sub_train_job(w.sub_train_job_id)
                     ServicesManager(db, None).refresh_train_job_status(sub.train_job_id)
             elif stype == ServiceType.PREDICT:
-                from ..predictor.fastserve import FastPredictorServer
+                from ..predictor.nativeserve import make_server
                 from ..predictor.predictor import Predictor
                 predictor = Predictor.from_inference_job(env['RAFIKI_INFERENCE_JOB_ID'], db=db)
-                srv = FastPredictorServer(predictor, '127.0.0.1', int(env['RAFIKI_SERVICE_PORT'])).start()
+                srv = make_server(predictor, '127.0.0.1', int(env['RAFIKI_SERVICE_PORT'])).start()
                 self.servers[sid] = srv
                 db.mark_service_as_running(db.get_service(sid))
         except Exception:

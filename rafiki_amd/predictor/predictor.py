@@ -117,6 +117,9 @@ class _Replica:
         self.streams = None
         self.graphs = None
         self.graphs_failed = False
+        # the per-model path writes each model's static bucket buffers and replays its graphs:
+        # two threads on one replica must not interleave there (the ensemble graph has its own lock)
+        self.lock = threading.RLock()
 
 
 class Predictor:
@@ -258,6 +261,10 @@ class Predictor:
             return self._predict_models(r, queries)
 
     def _predict_models(self, r, queries):
+        with r.lock:
+            return self._predict_models_locked(r, queries)
+
+    def _predict_models_locked(self, r, queries):
         preds, ok = [], []
         for name, m in r.models:
             try:
@@ -346,6 +353,10 @@ class Predictor:
 
     def _proba_device_on(self, r, inputs, queries=None):
         """Per-model path: each model's bucketed graph on its own HIP stream, then the ensemble kernel."""
+        with r.lock:
+            return self._proba_device_on_locked(r, inputs, queries)
+
+    def _proba_device_on_locked(self, r, inputs, queries=None):
         import torch
         dev = next(iter(inputs.values())).device if inputs else torch.device('cuda')
         if r.streams is None or len(r.streams) != len(r.models):
@@ -375,14 +386,93 @@ class Predictor:
     # ------------------------------------------------------------------- dynamic batching
     def start(self):
         """One batching consumer per replica over the shared request queue (the reference's
-        replicas each pop from the same Redis queue)."""
+        replicas each pop from the same Redis queue).  For native image ensembles each consumer is
+        a two-stage pipeline: a collector thread batches and decodes queries (nested lists -> uint8)
+        while the device thread runs the previous batch's hipGraph, through a 2-deep hand-off."""
         if not self._threads:
             self._stop.clear()
-            for i in range(len(self.replicas)):
+            for i, r in enumerate(self.replicas):
+                if self._pipelined(r):
+                    hand = queue.Queue(maxsize=2)
+                    for fn, nm in ((self._collect_loop, 'collect'), (self._device_loop, 'device')):
+                        t = threading.Thread(target=fn, args=(r, hand), name='rafiki-batcher-{}-{}'.format(nm, i),
+                                             daemon=True)
+                        t.start()
+                        self._threads.append(t)
+                    continue
                 t = threading.Thread(target=self._batch_loop, name='rafiki-batcher-{}'.format(i), daemon=True)
                 t.start()
                 self._threads.append(t)
         return self
+
+    def _pipelined(self, r):
+        from . import ensemble_graph as EG
+        return (self._fast_path() and os.environ.get('RAFIKI_BATCHER_PIPELINE', '1') != '0'
+                and all(callable(getattr(m, 'input_signature', None)) for _, m in r.models)
+                and EG.supports([m for _, m in r.models]))
+
+    def _take_batch(self):
+        try:
+            first = self._q.get(timeout=0.05)
+        except queue.Empty:
+            return None
+        batch = [first]
+        deadline = time.perf_counter() + self.max_wait_s
+        while len(batch) < self.max_batch:
+            rem = deadline - time.perf_counter()
+            try:
+                batch.append(self._q.get(timeout=max(0.0, rem)) if rem > 0 else self._q.get_nowait())
+            except queue.Empty:
+                break
+        return batch
+
+    def _collect_loop(self, r, hand):
+        while not self._stop.is_set():
+            batch = self._take_batch()
+            if batch is None:
+                continue
+            futs = [f for _, f in batch]
+            try:
+                host = _decode_once(r.models, [q for q, _ in batch])
+            except Exception as e:
+                for f in futs:
+                    f.set_exception(e)
+                continue
+            while not self._stop.is_set():
+                try:
+                    hand.put((host, futs), timeout=0.05)
+                    break
+                except queue.Full:
+                    continue
+
+    def _device_loop(self, r, hand):
+        while not self._stop.is_set():
+            try:
+                host, futs = hand.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            with self._rlock:
+                r.inflight += 1
+            try:
+                out = self._graph_call(r, lambda g: g.run_host(host))
+                if out is None:
+                    import torch
+                    dev = _cuda_device_of(r.models)
+                    inputs = {s: torch.from_numpy(a).to(dev) for s, a in host.items()}
+                    out = self._proba_device_on(r, inputs).cpu().numpy()
+                rows = out.tolist()
+                for f, p in zip(futs, rows):
+                    f.set_result(p)
+            except Exception as e:
+                for f in futs:
+                    if not f.done():
+                        f.set_exception(e)
+            finally:
+                with self._rlock:
+                    r.inflight -= 1
+                    r.served += 1
+            self.stats['batches'] += 1
+            self.stats['queries'] += len(futs)
 
     def stop(self):
         self._stop.set()

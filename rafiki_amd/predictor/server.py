@@ -4,8 +4,8 @@ rafiki/predictor/app.py:23-30) plus ``POST /predict_batch {"queries": [...]}`` (
 
 Run as a service: ``python -m rafiki_amd.predictor.server`` with RAFIKI_INFERENCE_JOB_ID,
 RAFIKI_SERVICE_ID and RAFIKI_SERVICE_PORT in the environment.  The service serves through the
-event-loop front end (``fastserve.FastPredictorServer``, same routes); RAFIKI_PREDICTOR_SERVER=flask
-selects this Flask app instead.
+native C++ front end (``nativeserve.NativePredictorServer``, same routes); RAFIKI_PREDICTOR_SERVER=fast
+selects the asyncio one (``fastserve``) and RAFIKI_PREDICTOR_SERVER=flask this Flask app.
 """
 from __future__ import annotations
 
@@ -99,8 +99,8 @@ def main():
             db.mark_service_as_running(db.get_service(sid))
         app.run(host='0.0.0.0', port=port, threaded=True)
         return 0
-    from .fastserve import FastPredictorServer
-    srv = FastPredictorServer(predictor, '0.0.0.0', port)
+    from .nativeserve import make_server
+    srv = make_server(predictor, '0.0.0.0', port)
     if sid:
         db.mark_service_as_running(db.get_service(sid))
     srv.serve_forever()

@@ -50,19 +50,43 @@ def timed(fn, iters):
 
 
 def _client_proc(url, kind, threads, seconds, q, payload):
-    import requests
+    """Load generator process: ``threads`` keep-alive connections, each sending one request at a time.
+    json1: pre-encoded single-query JSON bodies over a raw socket (the client must not be the
+    bottleneck: requests + json.dumps of 3072 ints costs ~1 ms per call); npy: batch bodies."""
+    import socket
+    host, port = url.split('//')[1].split(':')
+    port = int(port)
+    if kind == 'json1':
+        body = json.dumps({'query': payload}).encode()
+        path, per = b'/predict', 1
+    else:
+        body, path, per = payload, b'/predict_batch_npy', 128
+    req = b'POST %s HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n' % (path, len(body)) + body
     stop = threading.Event()
     counts = [0] * threads
+    lats = [[] for _ in range(threads)]
 
     def worker(i):
-        s = requests.Session()
+        s = socket.create_connection((host, port))
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        buf = b''
         while not stop.is_set():
-            if kind == 'json1':
-                s.post(url + '/predict', json={'query': payload}, timeout=30).raise_for_status()
-                counts[i] += 1
-            else:
-                s.post(url + '/predict_batch_npy', data=payload, timeout=30).raise_for_status()
-                counts[i] += 128
+            t = time.perf_counter()
+            s.sendall(req)
+            while True:
+                h = buf.find(b'\r\n\r\n')
+                if h >= 0:
+                    head = buf[:h].lower()
+                    cl = int(head.split(b'content-length:')[1].split(b'\r\n')[0])
+                    if len(buf) >= h + 4 + cl:
+                        if not buf.startswith(b'HTTP/1.1 200'):
+                            raise RuntimeError(buf[:200])
+                        buf = buf[h + 4 + cl:]
+                        break
+                buf += s.recv(1 << 16)
+            lats[i].append(time.perf_counter() - t)
+            counts[i] += per
+        s.close()
     ths = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
     for t in ths:
         t.start()
@@ -70,14 +94,17 @@ def _client_proc(url, kind, threads, seconds, q, payload):
     stop.set()
     for t in ths:
         t.join()
-    q.put(sum(counts))
+    q.put((sum(counts), [x for lst in lats for x in lst]))
 
 
 def http_bench(pred, rng, args, server='fast'):
     import io
     from rafiki_amd.container.container_manager import free_port
     port = free_port()
-    if server == 'fast':
+    if server == 'native':
+        from rafiki_amd.predictor.nativeserve import NativePredictorServer
+        srv = NativePredictorServer(pred, '127.0.0.1', port).start()
+    elif server == 'fast':
         from rafiki_amd.predictor.fastserve import FastPredictorServer
         srv = FastPredictorServer(pred, '127.0.0.1', port).start()
     else:
@@ -103,15 +130,20 @@ def http_bench(pred, rng, args, server='fast'):
               for _ in range(procs)]
         for p in ps:
             p.start()
-        total = sum(q.get(timeout=120) for _ in ps)
+        got = [q.get(timeout=120) for _ in ps]
         for p in ps:
             p.join(30)
-        return round(total / seconds, 1)
+        lat = np.array([x for _, lst in got for x in lst]) * 1e3
+        return {'qps': round(sum(n for n, _ in got) / seconds, 1),
+                'p50_ms': round(float(np.percentile(lat, 50)), 3), 'p99_ms': round(float(np.percentile(lat, 99)), 3)}
     pred.start()
-    out['json_single_query_qps_8x8clients'] = run('json1', 8, 8)
-    out['npy_batch128_qps_4x2clients'] = run('npy', 4, 2)
-    if server == 'fast':
-        out['json_single_query_qps_16x16clients'] = run('json1', 16, 16)
+    out['json_single_query_64clients'] = run('json1', 8, 8)
+    out['npy_batch128_8clients'] = run('npy', 4, 2)
+    if server != 'flask':
+        out['json_single_query_256clients'] = run('json1', 16, 16)
+    if hasattr(srv, 'counters'):
+        c = srv.counters
+        out['server_counters'] = {k: c[k] for k in ('requests', 'batches', 'batched_queries') if k in c}
     srv.shutdown()
     return out
 
@@ -125,6 +157,7 @@ def main():
     ap.add_argument('--seconds', type=float, default=5.0)
     ap.add_argument('--replicas', type=int, default=1)
     ap.add_argument('--skip-http', action='store_true')
+    ap.add_argument('--flask', action='store_true', help='also measure the Flask app')
     ap.add_argument('--out', default='')
     args = ap.parse_args()
     from rafiki_amd.ops import _lib
@@ -162,8 +195,10 @@ def main():
         res['array'][b] = {'qps': round(b * it / dt, 1), 'ms_per_batch': round(1e3 * dt / it, 3)}
     # real HTTP: the predictor's Flask app on a local port, concurrent clients
     if not args.skip_http:
-        res['http'] = http_bench(pred, rng, args, 'fast')
-        res['http_flask'] = http_bench(pred, rng, args, 'flask')
+        res['http_native'] = http_bench(pred, rng, args, 'native')
+        res['http_asyncio'] = http_bench(pred, rng, args, 'fast')
+        if args.flask:
+            res['http_flask'] = http_bench(pred, rng, args, 'flask')
     # dynamic batcher under concurrent single-query clients
     pred.start()
     one = rng.integers(0, 256, (32, 32, 3)).tolist()

@@ -40,11 +40,18 @@ class FakePredictor:
         return [self._probs(np.asarray([q], dtype=np.uint8))[0].tolist() for q in queries]
 
 
-@pytest.fixture()
-def server():
-    from rafiki_amd.predictor.fastserve import FastPredictorServer
+@pytest.fixture(params=['fast', 'native'])
+def server(request):
+    """Both front ends: asyncio (fastserve) and the C++ epoll server (nativeserve)."""
     fake = FakePredictor()
-    srv = FastPredictorServer(fake, '127.0.0.1', 0).start()
+    if request.param == 'native':
+        from rafiki_amd.predictor import nativeserve
+        if not nativeserve.available():
+            pytest.skip('librafiki_runtime.so not built')
+        srv = nativeserve.NativePredictorServer(fake, '127.0.0.1', 0).start()
+    else:
+        from rafiki_amd.predictor.fastserve import FastPredictorServer
+        srv = FastPredictorServer(fake, '127.0.0.1', 0).start()
     yield srv, fake, 'http://127.0.0.1:{}'.format(srv.port)
     srv.shutdown()
 
