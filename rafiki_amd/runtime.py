@@ -92,10 +92,14 @@ def _pylib():
     return _py
 
 
-def pylist_u8(obj):
+def pylist_u8(obj, max_elems: int = 1 << 26):
     """A rectangular nest of Python lists / tuples of ints or floats -> uint8 numpy array (clipped to
     [0, 255], floats truncated) by the native walker; None when the library is missing or the nest
-    is ragged / non-numeric (callers then fall back to numpy)."""
+    is ragged / non-numeric (callers then fall back to numpy).
+
+    The shape comes from the first-element chain before the walk proves the nest rectangular, so
+    the allocation is capped (``max_elems`` bytes): a small adversarial query whose first children
+    are long and the rest empty cannot request a huge buffer."""
     h = _pylib()
     if h is None or not isinstance(obj, (list, tuple)):
         return None
@@ -105,7 +109,15 @@ def pylist_u8(obj):
     if nd < 0:
         return None
     dims = [int(shape[i]) for i in range(nd)]
-    out = np.empty(dims, dtype=np.uint8)
+    total = 1
+    for d in dims:
+        total *= d
+        if total > max_elems:
+            return None
+    try:
+        out = np.empty(dims, dtype=np.uint8)
+    except (MemoryError, ValueError):
+        return None
     if out.size and h.rk_pylist_u8(obj, shape, nd, out.ctypes.data) != 0:
         return None
     return out

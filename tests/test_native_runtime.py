@@ -37,3 +37,14 @@ def test_pylist_u8_matches_numpy():
     assert runtime.pylist_u8([[1, 2], [3]]) is None          # ragged
     assert runtime.pylist_u8([['a', 'b']]) is None           # non-numeric
     assert runtime.pylist_u8(((1, 2), (3, 4))).tolist() == [[1, 2], [3, 4]]
+
+
+def test_pylist_u8_caps_adversarial_shapes():
+    """the first-element chain of a small ragged query must not size a huge allocation."""
+    from rafiki_amd import runtime
+    if runtime._pylib() is None:
+        import pytest
+        pytest.skip('pylist extension not built')
+    q = [[list(range(3))] * 100000] + [[]] * 100000
+    assert runtime.pylist_u8(q) is None          # refused without allocating 3e10 bytes
+    assert runtime.pylist_u8([[1, 2], [3, 4]]).tolist() == [[1, 2], [3, 4]]
