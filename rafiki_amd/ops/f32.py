@@ -501,7 +501,8 @@ WINO4_WGRAD = -7  # autotune tile id of the F(4x4) weight gradient (cfg = (-7, 0
 
 def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     """Split-K choices of rk_wino4_wgrad_v (variant 0: 32 co x 32 ci blocks, 1: 64 co x 32 ci, 2: 32 x 32
-    software-pipelined over two LDS stages): 128..4096
+    software-pipelined over two LDS stages, 3: 32 x 32 with the 36 positions split over the waves on
+    32x32x2 MFMAs): 128..4096
     blocks, >= 4 chunks of 8 tiles per block, slabs <= 256 MiB.  cfg = (WINO4_WGRAD, variant, splits)."""
     if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and Cin >= 8 and Cout >= 16):
         return []
@@ -509,7 +510,7 @@ def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
         return []
     out = []
-    for v, bco in ((0, 32), (1, 64)) + (((2, 32),) if WINO_PIPE else ()):
+    for v, bco in ((0, 32), (1, 64), (3, 32)) + (((2, 32),) if WINO_PIPE else ()):
         if v == 1 and Cout < 64:
             continue
         base = cdiv(Cout, bco) * cdiv(Cin, 32)
