@@ -303,6 +303,55 @@ def test_replicas_serve_concurrent_requests(ensemble):
     assert all(r.graphs is not None for r in p.replicas)
 
 
+def test_per_model_path_is_thread_safe_on_one_replica(ensemble, monkeypatch):
+    """with the one-graph ensemble off, the per-model path writes each model's static
+    bucket buffers and replays its graphs; 6 threads sharing ONE replica must each get their own
+    batch's answer (the per-replica lock serialises them)."""
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor.predictor import Predictor
+    monkeypatch.setenv('RAFIKI_ENSEMBLE_GRAPH', '0')
+    p = Predictor(_copy_ensemble(ensemble))
+    imgs, _ = synthetic_images(60, size=32, channels=3, classes=10, seed=5)
+    ref = Predictor(ensemble).predict_array(imgs)
+    out = [None] * 15
+    errs = []
+
+    def worker(k):
+        try:
+            for j in range(5):
+                i = (k * 5 + j) % 15
+                out[i] = p.predict_array(imgs[i * 4:(i + 1) * 4])
+        except Exception as e:   # surfaced below
+            errs.append(e)
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errs, errs
+    assert p.replicas[0].graphs is None
+    assert np.allclose(np.concatenate(out), ref, atol=1e-5)
+
+
+def test_pipelined_batcher_matches_direct_path(ensemble):
+    """The two-stage in-process batcher (collector decodes batch n+1 while the device thread runs
+    batch n) answers every single query exactly as the direct array path."""
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor.predictor import Predictor
+    p = Predictor(_copy_ensemble(ensemble), max_batch=16, max_wait_ms=1.0)
+    assert p._pipelined(p.replicas[0])
+    imgs, _ = synthetic_images(64, size=32, channels=3, classes=10, seed=6)
+    ref = Predictor(ensemble).predict_array(imgs)
+    p.start()
+    try:
+        futs = [p.submit(imgs[i].tolist()) for i in range(len(imgs))]
+        got = np.asarray([f.result(timeout=60) for f in futs])
+    finally:
+        p.stop()
+    assert np.allclose(got, ref, atol=1e-5)
+    assert p.stats['batches'] < len(imgs)
+
+
 def test_resident_handoff_keeps_trained_model_in_hbm(ensemble):
     """A finished trial offered to the resident store drops its training state (step graphs,
     optimizer) but predicts exactly as before, and take() hands back the same object."""
@@ -317,3 +366,50 @@ def test_resident_handoff_keeps_trained_model_in_hbm(ensemble):
     got = store.take('trial-x')
     assert got is m and store.take('trial-x') is None
     assert torch.equal(got.predict_proba(imgs.tolist()).cpu(), before)
+
+
+def test_native_http_front_end_serves_the_gpu_ensemble(ensemble):
+    """The C++ front end (csrc/runtime/httpfront.cpp) in front of the real top-k ensemble: concurrent
+    single JSON queries are batched into device batches and every answer matches predict_array."""
+    import json as _json
+    import socket
+
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor import nativeserve
+    from rafiki_amd.predictor.predictor import Predictor
+    if not nativeserve.available():
+        pytest.skip('librafiki_runtime.so not built')
+    p = Predictor(_copy_ensemble(ensemble))
+    imgs, _ = synthetic_images(32, size=32, channels=3, classes=10, seed=8)
+    ref = Predictor(ensemble).predict_array(imgs)
+    srv = nativeserve.NativePredictorServer(p, '127.0.0.1', 0).start()
+    out = [None] * len(imgs)
+
+    def client(lo, hi):
+        s = socket.create_connection(('127.0.0.1', srv.port), timeout=60)
+        buf = b''
+        for i in range(lo, hi):
+            body = _json.dumps({'query': imgs[i].tolist()}).encode()
+            s.sendall(b'POST /predict HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n' % len(body) + body)
+            while True:
+                h = buf.find(b'\r\n\r\n')
+                if h >= 0:
+                    cl = int(buf[:h].lower().split(b'content-length:')[1].split(b'\r\n')[0])
+                    if len(buf) >= h + 4 + cl:
+                        assert buf.startswith(b'HTTP/1.1 200'), buf[:200]
+                        out[i] = _json.loads(buf[h + 4:h + 4 + cl])['prediction']
+                        buf = buf[h + 4 + cl:]
+                        break
+                buf += s.recv(65536)
+        s.close()
+    try:
+        ts = [threading.Thread(target=client, args=(k * 4, (k + 1) * 4)) for k in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        c = srv.counters
+    finally:
+        srv.shutdown()
+    assert np.allclose(np.asarray(out), ref, atol=1e-5)
+    assert c['batched_queries'] == len(imgs) and c['batches'] <= len(imgs)
