@@ -1219,3 +1219,133 @@ extern "C" int rk_wino4_wgrad(const float* dy, const float* x, float* out, int N
   return rk_wino4_wgrad_v(dy, x, out, Nb, H, W, Co, Ci, splits, accumulate, 0, stream);
 }
 
+
+// ------------------------------------------------------------- pre-transformed weight gradient (deep layers)
+// dW by F(4x4,3x3) as three launches: transform every 4x4 dy patch (M = A dY A^T) and every 6x6 x
+// window (V = B^T x B) ONCE into position-major buffers M [36][T][Co], V [36][T][Ci]; the 36 GEMMs
+// dU[q] = M[q]^T V[q] run as ONE split-K launch of the tuned sgemm (kind 5, splits = 36, slab q = dU[q]);
+// then dW = G^T dU G.  In the fused kernels each (co, ci) block re-transforms its whole dy / x range,
+// i.e. every x window Co/32 times — on the 8x8 / 4x4 maps (T = 1024 / 256 tiles, 256-512 channels) that
+// redundant transform work dominates, and here it is done once.
+namespace {
+
+__global__ __launch_bounds__(256) void w4pt_dy_kernel(const float* __restrict__ dy, float* __restrict__ m, int H,
+                                                      int W, int C, int TW, int THW, long long total, long long T) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  const long long t = i / C;
+  const int n = (int)(t / THW), r = (int)(t - (long long)n * THW), ty = r / TW;
+  const int oy = 4 * ty, ox = 4 * (r - ty * TW);
+  const float* src = dy + (((long long)n * H + oy) * W + ox) * C + c;
+  float g[16];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) g[a * 4 + b] = src[((long long)a * W + b) * C];
+  float mm[6][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float o[6];
+    a6(g[j], g[4 + j], g[8 + j], g[12 + j], o);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) mm[a][j] = o[a];
+  }
+  float* dst = m + t * C + c;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float o[6];
+    a6(mm[a][0], mm[a][1], mm[a][2], mm[a][3], o);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) dst[(long long)(a * 6 + b) * T * C] = o[b];
+  }
+}
+
+__global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x, float* __restrict__ v, int H,
+                                                     int W, int C, int TW, int THW, long long total, long long T) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  const long long t = i / C;
+  const int n = (int)(t / THW), r = (int)(t - (long long)n * THW), ty = r / TW;
+  const int oy = 4 * ty - 1, ox = 4 * (r - ty * TW) - 1;
+  float d[36];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int yy = oy + a, xx = ox + b;
+      d[a * 6 + b] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? x[(((long long)n * H + yy) * W + xx) * C + c] : 0.f;
+    }
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    float o[6];
+    bt6(d[b], d[6 + b], d[12 + b], d[18 + b], d[24 + b], d[30 + b], o);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) d[a * 6 + b] = o[a];
+  }
+  float* dst = v + t * C + c;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float o[6];
+    bt6(d[a * 6 + 0], d[a * 6 + 1], d[a * 6 + 2], d[a * 6 + 3], d[a * 6 + 4], d[a * 6 + 5], o);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) dst[(long long)(a * 6 + b) * T * C] = o[b];
+  }
+}
+
+// dU [36][Co][Ci] -> dW [Co][9][Ci] (+= with accumulate)
+__global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__ du, float* __restrict__ out, int Co,
+                                                       int Ci, int accumulate) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long plane = (long long)Co * Ci;
+  if (i >= plane) return;
+  const int co = (int)(i / Ci), ci = (int)(i - (long long)co * Ci);
+  float tq[3][6];
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    float g[3];
+    gt6(du[(0 * 6 + b) * plane + i], du[(1 * 6 + b) * plane + i], du[(2 * 6 + b) * plane + i],
+        du[(3 * 6 + b) * plane + i], du[(4 * 6 + b) * plane + i], du[(5 * 6 + b) * plane + i], g);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) tq[ky][b] = g[ky];
+  }
+  float* o = out + (long long)co * 9 * Ci + ci;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    float v[3];
+    gt6(tq[ky][0], tq[ky][1], tq[ky][2], tq[ky][3], tq[ky][4], tq[ky][5], v);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      float* d = o + (ky * 3 + kx) * Ci;
+      *d = accumulate ? *d + v[kx] : v[kx];
+    }
+  }
+}
+
+}  // namespace
+
+// M [36][T][Co] and V [36][T][Ci] (T = Nb * H/4 * W/4 tiles) of dy / x (NHWC, H and W multiples of 4)
+extern "C" int rk_wino4_pt_transform(const float* dy, const float* x, float* m, float* v, int Nb, int H, int W,
+                                     int Co, int Ci, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0) return RK_EBADARG;
+  const int TW = W / 4, THW = (H / 4) * (W / 4);
+  const long long T = (long long)Nb * THW;
+  const long long ty = T * Co, tx = T * Ci;
+  hipLaunchKernelGGL(w4pt_dy_kernel, dim3((unsigned)((ty + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy, m, H,
+                     W, Co, TW, THW, ty, T);
+  RK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(w4pt_x_kernel, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, v, H, W,
+                     Ci, TW, THW, tx, T);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_wino4_pt_output(const float* du, float* out, int Co, int Ci, int accumulate, void* stream) {
+  if (Co <= 0 || Ci <= 0) return RK_EBADARG;
+  const long long plane = (long long)Co * Ci;
+  hipLaunchKernelGGL(w4pt_out_kernel, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, (hipStream_t)stream, du,
+                     out, Co, Ci, accumulate);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}

@@ -255,6 +255,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
         if tile == WINO4_WGRAD:
             wino4_wgrad(dy, x, out, splits=s, accumulate=accumulate, variant=nst)
             return
+        if tile == WINO4_WGRAD_PT:
+            wino4_wgrad_pt(dy, x, out, accumulate=accumulate, tile=nst, nst=s)
+            return
         if s == 1:
             sgemm(KIND_WGRAD, dy, x, out, M, N, K, Cout, Cin, N, tile=tile, nst=nst, H=H, W=W, C=Cin, taps=taps,
                   flags=F_ACCUM if accumulate else 0)
@@ -271,8 +274,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
                                               2 * NUM_CU))] + cands
     wcands = _wino_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
     w4cands = _wino4_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
-    cands += wcands + w4cands
-    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands), bool(w4cands)), cands, run)
+    ptcands = _wino4_pt_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
+    cands += wcands + w4cands + ptcands
+    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands), bool(w4cands), bool(ptcands)),
+                cands, run)
     run(cfg)
     return out
 
@@ -542,6 +547,42 @@ def wino4_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=
     slab = torch.empty((splits, Cout, 9 * Cin), device=dy.device, dtype=torch.float32)
     _lib.call("rk_wino4_wgrad_v", _p(dy), _p(x), _p(slab), Nb, H, W, Cout, Cin, int(splits), 0, int(variant), _s())
     reduce_slabs(slab, out.view(Cout, 9 * Cin), accumulate=accumulate)
+    return out
+
+
+WINO4_WGRAD_PT = -13  # pre-transformed F(4x4) weight gradient: cfg = (-13, sgemm tile, sgemm nst)
+
+
+def _wino4_pt_cands(Nb, H, W, Cout, Cin):
+    """The pre-transformed F(4x4) weight gradient (transform once, 36 GEMMs as one split-K sgemm) on
+    maps of <= 16x16 where the fused kernels' redundant per-block transforms dominate."""
+    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= 16 and W <= 16 and Cin % 4 == 0
+            and Cout % 4 == 0 and Cin >= 32 and Cout >= 32):
+        return []
+    T = Nb * (H // 4) * (W // 4)
+    if T % 32 or 36 * T * max(Cin, Cout) * 4 >= (1 << 31) or 36 * Cout * Cin * 4 > (512 << 20):
+        return []
+    return [(WINO4_WGRAD_PT, t, n) for t in (0, 1, 2, 3) for n in ((2, 3) if t in _NST3 else (2,))]
+
+
+def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accumulate=False, tile=0, nst=2):
+    """out [Cout][9*Cin] (+)= the F(4x4,3x3) weight gradient through position-major transformed buffers:
+    M [36][T][Cout], V [36][T][Cin] (one transform launch each), dU[q] = M[q]^T V[q] as ONE sgemm with
+    36 K-splits (slab q = dU[q]), then dW = G^T dU G."""
+    _check(dy, 'wino4_wgrad_pt dy')
+    _check(x, 'wino4_wgrad_pt x')
+    Nb, H, W, Cout = dy.shape
+    Cin = x.shape[-1]
+    T = Nb * (H // 4) * (W // 4)
+    assert H % 4 == 0 and W % 4 == 0 and T % 32 == 0 and x.shape[:3] == dy.shape[:3], (dy.shape, x.shape)
+    assert out.numel() == Cout * 9 * Cin and out.is_contiguous()
+    m = torch.empty((36 * T, Cout), device=dy.device, dtype=torch.float32)
+    v = torch.empty((36 * T, Cin), device=dy.device, dtype=torch.float32)
+    _lib.call("rk_wino4_pt_transform", _p(dy), _p(x), _p(m), _p(v), Nb, H, W, Cout, Cin, _s())
+    du = torch.empty((36, Cout, Cin), device=dy.device, dtype=torch.float32)
+    sgemm(KIND_DENSE_DW, m, v, du, Cout, Cin, 36 * T, Cout, Cin, Cin, tile=tile, nst=nst, splits=36,
+          slab_stride=Cout * Cin)
+    _lib.call("rk_wino4_pt_output", _p(du), _p(out), Cout, Cin, int(bool(accumulate)), _s())
     return out
 
 

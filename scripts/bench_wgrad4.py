@@ -39,8 +39,14 @@ for (N, H, C, K) in [(256, 32, 8, 64), (256, 32, 64, 64), (256, 16, 64, 128), (2
             sb = min(tw, key=tw.get)
             r['v%d_us' % v], r['v%d_splits' % v] = round(tw[sb], 1), sb
             r['v%d_all' % v] = {s: round(u, 1) for s, u in sorted(tw.items())}
+    tp = {(c[1], c[2]): t(lambda: S.wino4_wgrad_pt(dy, x, dw, tile=c[1], nst=c[2]))
+          for c in S._wino4_pt_cands(N, H, H, K, C)}
+    if tp:
+        cb = min(tp, key=tp.get)
+        r['pt_us'], r['pt_cfg'] = round(tp[cb], 1), list(cb)
     fl = 2.0 * N * H * H * K * 9 * C
-    r['direct_equiv_tflops_best'] = round(fl / min(r.get('v%d_us' % v, 1e9) for v in (0, 1, 3)) / 1e6, 1)
+    r['direct_equiv_tflops_best'] = round(fl / min([r.get('v%d_us' % v, 1e9) for v in (0, 1, 3)] +
+                                                  [r.get('pt_us', 1e9)]) / 1e6, 1)
     print(json.dumps(r), flush=True)
     res.append(r)
 if len(sys.argv) > 1:

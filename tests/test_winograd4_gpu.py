@@ -192,3 +192,25 @@ def test_wino_weights_live_sets_and_on_demand_transform():
     assert not torch.equal(ww.u(1), S.wino_u(ws[1]))          # not live: stale until asked for
     assert torch.equal(ww.lazy('u2', 1)(), S.wino_u(ws[1]))   # on-demand transform
     assert torch.equal(ww.lazy('ut4', 2)(), S.wino4_ut(ws[2]))
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(16, 8, 8, 64, 128), (32, 4, 4, 256, 128), (8, 16, 16, 32, 64),
+                                            (64, 4, 4, 40, 36)])
+@pytest.mark.parametrize("tile", [0, 3])
+def test_wino4_wgrad_pretransformed(N, H, W, Cin, Cout, tile):
+    """Pre-transformed F(4x4) weight gradient (transform launch + 36-split sgemm + output transform)."""
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=40)
+    dy = _rand(N, H, W, Cout, seed=41)
+    dw = torch.empty(Cout, 9 * Cin, device=DEV)
+    S.wino4_wgrad_pt(dy.to(DEV), x.to(DEV), dw, tile=tile)
+    prev = _rand(Cout, 9 * Cin, seed=42).to(DEV)
+    acc = prev.clone()
+    S.wino4_wgrad_pt(dy.to(DEV), x.to(DEV), acc, accumulate=True, tile=tile)
+    torch.cuda.synchronize()
+    wd = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    out = TF.conv2d(x.double().permute(0, 3, 1, 2), wd, padding=1)
+    (gw,) = torch.autograd.grad(out, wd, dy.double().permute(0, 3, 1, 2))
+    ref = gw.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+    assert rel(dw, ref) < TOL
+    assert rel(acc, ref + prev.double().cpu()) < TOL
