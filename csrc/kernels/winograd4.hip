@@ -32,7 +32,6 @@ constexpr int KC = 8;     // input channels per K chunk
 enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_BNB = 512, WF_BNP = 1024 };
 
 typedef __attribute__((ext_vector_type(2))) float f32x2;
-typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 struct W4Params {
   const float* x;       // NHWC [Nb][H][W][C]
@@ -640,176 +639,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   }
 }
 
-// Position-split weight gradient (variant 3): 32 co x 32 ci blocks of 4 waves, each wave owning 9 of the
-// 36 Winograd positions for the WHOLE 32 x 32 (co, ci) tile on v_mfma_f32_32x32x2_f32 (9 x 16 = 144
-// accumulators).  Against the 16x16-per-wave layout every LDS fragment read feeds a 32x32 product instead
-// of a 16x16 one, halving LDS reads per MFMA cycle.  K order inside a chunk is permuted so each lane reads
-// its 4 k values of a position with ONE ds_read_b128 (lane half h takes tiles 4h..4h+3, step s pairs
-// k = 4h + s in A and B alike).  73.7 KiB of LDS: two blocks per CU, so one block's transform / LDS-write
-// phase runs in the other's MFMA shadow.  The G^T dU G output transform gathers the 36 positions of a
-// (co, ci) pair through LDS in four 8-ci slabs.
-__global__ __launch_bounds__(256, 2) void wino4_wgrad_ps_kernel(const W4wParams p) {
-  constexpr int BC = 32;
-  __shared__ __attribute__((aligned(16))) float lds[2 * 36 * BC * KC];
-  float (*Ms)[BC][KC] = (float (*)[BC][KC])lds;                   // [pos][co][tile]
-  float (*Vs)[BC][KC] = (float (*)[BC][KC])(lds + 36 * BC * KC);  // [pos][ci][tile]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = p.nco * p.nci;
-  const int split = b / per, r0 = b - split * per;
-  const int co0 = (r0 / p.nci) * BC, ci0 = (r0 % p.nci) * BC;
-  const int t_begin = split * p.tps;
-  const int t_end = min(t_begin + p.tps, p.ntiles);
-  const int nch = (t_end - t_begin + KC - 1) / KC;
-  const int tt = tid & 7, ch = tid >> 3;   // tile within the chunk, channel row within the block
-  const __amdgpu_buffer_rsrc_t dyr = rsrc(p.dy, p.dybytes), xr = rsrc(p.x, p.xbytes);
-
-  float gy[16], raw[36];
-  auto load = [&](int c) {
-    const int t = t_begin + c * KC + tt;
-    const unsigned okm = t < t_end ? 1u : 0u;
-    const int n = (int)(((float)t + 0.5f) * p.invTHW);   // exact below 2^22 tiles
-    const int rr = t - n * p.THW;
-    const int ty = (int)(((float)rr + 0.5f) * p.invTW);
-    const int oy = 4 * ty, ox = 4 * (rr - ty * p.TW);
-    const int pix = (n * p.H + oy) * p.W + ox;
-    {
-      const int co = co0 + ch;
-      const unsigned bad = (okm & (co < p.Co ? 1u : 0u)) ^ 1u;
-      const unsigned ob = (unsigned)((pix * p.Co + co) * 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const unsigned off = (ob + (unsigned)(i * p.W * p.Co * 4)) | (bad << 31);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          gy[i * 4 + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-              dyr, (int)off, __builtin_amdgcn_readfirstlane(j * p.Co * 4), 0));
-      }
-    }
-    const unsigned rm = 30u | (oy > 0 ? 1u : 0u) | (oy + 4 < p.H ? 32u : 0u);
-    const unsigned cm = 30u | (ox > 0 ? 1u : 0u) | (ox + 4 < p.W ? 32u : 0u);
-    {
-      const int ci = ci0 + ch;
-      const unsigned xm = okm & (ci < p.Ci ? 1u : 0u);
-      const unsigned xb = (unsigned)((pix * p.Ci + ci) * 4);
-      const unsigned cl = cm & 1u, cr = (cm >> 5) & 1u;
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const unsigned r = xb + (unsigned)((a - 1) * p.W * p.Ci * 4);
-        const unsigned rok = xm & (rm >> a) & 1u;
-        const unsigned mid = r | ((rok ^ 1u) << 31);
-        const unsigned lft = (r - (unsigned)(p.Ci * 4)) | (((rok & cl) ^ 1u) << 31);
-        const unsigned rgt = r | (((rok & cr) ^ 1u) << 31);
-#pragma unroll
-        for (int bb = 0; bb < 6; ++bb) {
-          const unsigned off = bb == 0 ? lft : bb == 5 ? rgt : mid;
-          const int so = __builtin_amdgcn_readfirstlane(bb == 0 ? 0 : (bb - 1) * p.Ci * 4);
-          raw[a * 6 + bb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)off, so, 0));
-        }
-      }
-    }
-  };
-  auto store = [&]() {
-    float m[6][4];                         // A dY: along rows
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float o[6];
-      a6(gy[j], gy[4 + j], gy[8 + j], gy[12 + j], o);
-#pragma unroll
-      for (int a = 0; a < 6; ++a) m[a][j] = o[a];
-    }
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {          // (A dY) A^T: along columns
-      float o[6];
-      a6(m[a][0], m[a][1], m[a][2], m[a][3], o);
-#pragma unroll
-      for (int bb = 0; bb < 6; ++bb) Ms[a * 6 + bb][ch][tt] = o[bb];
-    }
-#pragma unroll
-    for (int bb = 0; bb < 6; ++bb) {       // B^T x B
-      float o[6];
-      bt6(raw[bb], raw[6 + bb], raw[12 + bb], raw[18 + bb], raw[24 + bb], raw[30 + bb], o);
-#pragma unroll
-      for (int a = 0; a < 6; ++a) raw[a * 6 + bb] = o[a];
-    }
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      float o[6];
-      bt6(raw[a * 6 + 0], raw[a * 6 + 1], raw[a * 6 + 2], raw[a * 6 + 3], raw[a * 6 + 4], raw[a * 6 + 5], o);
-#pragma unroll
-      for (int bb = 0; bb < 6; ++bb) Vs[a * 6 + bb][ch][tt] = o[bb];
-    }
-  };
-
-  f32x16 acc[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
-  if (nch > 0) {
-    load(0);
-    store();
-  }
-  __syncthreads();
-  const int i32 = lane & 31, h4 = (lane >> 5) * 4;
-  const int q0 = wave * 9;
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) load(c + 1);
-#pragma unroll
-    for (int q = 0; q < 9; ++q) {
-      const f32x4 a = *(const f32x4*)&Ms[q0 + q][i32][h4];
-      const f32x4 bv = *(const f32x4*)&Vs[q0 + q][i32][h4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bv[s], acc[q], 0, 0, 0);
-    }
-    if (c + 1 < nch) {
-      __syncthreads();
-      store();
-    }
-    __syncthreads();
-  }
-
-  // G^T dU G: stage the 36 positions of 8 ci at a time ([pos][co][8]) and let every thread finish one
-  // (co, ci) pair; lane (i32, half) holds ci = i32 and co = 8 (r / 4) + 4 half + (r % 4)
-  float (*St)[BC][8] = (float (*)[BC][8])lds;
-  float* outp = p.out + (long long)split * p.slab;
-  const int oco = tid >> 3, oci = tid & 7;
-#pragma unroll
-  for (int sl = 0; sl < BC / 8; ++sl) {
-    if ((i32 >> 3) == sl) {
-#pragma unroll
-      for (int q = 0; q < 9; ++q)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) St[q0 + q][8 * (r >> 2) + h4 + (r & 3)][i32 & 7] = acc[q][r];
-    }
-    __syncthreads();
-    const int co = co0 + oco, ci = ci0 + sl * 8 + oci;
-    float tq[3][6];
-#pragma unroll
-    for (int bb = 0; bb < 6; ++bb) {       // rows: G^T X
-      float g[3];
-      gt6(St[0 * 6 + bb][oco][oci], St[1 * 6 + bb][oco][oci], St[2 * 6 + bb][oco][oci], St[3 * 6 + bb][oco][oci],
-          St[4 * 6 + bb][oco][oci], St[5 * 6 + bb][oco][oci], g);
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) tq[ky][bb] = g[ky];
-    }
-    if (co < p.Co && ci < p.Ci) {
-      float* o = outp + (long long)co * 9 * p.Ci + ci;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {     // columns: (G^T X) G
-        float v[3];
-        gt6(tq[ky][0], tq[ky][1], tq[ky][2], tq[ky][3], tq[ky][4], tq[ky][5], v);
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          float* d = o + (ky * 3 + kx) * p.Ci;
-          *d = p.accumulate ? *d + v[kx] : v[kx];
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // Software-pipelined weight gradient: 32 co x 32 ci blocks of 4 waves with TWO LDS stages (147 KiB, one
 // block and one wave per SIMD, accumulators in AGPRs).  While the MFMAs of chunk c read one stage, the
 // same wave transforms chunk c+1 (loaded during chunk c-1) into the other, so the transform VALU and
@@ -1173,13 +1002,15 @@ extern "C" int rk_wino4_conv(const float* x, const float* u, float* y, const flo
 // dW [Co][9][Ci] (splits == 1, optionally accumulated) or per-split slabs [splits][Co][9][Ci] of the
 // weight gradient of a 3x3 stride-1 pad-1 conv by F(4x4,3x3); H, W multiples of 4; tiles_per_split % 8 == 0
 // variant 0: 4 waves, 32 co x 32 ci blocks (two per CU); 1: 8 waves, 64 co x 32 ci (a quarter less
-// transform work and LDS writes per MFMA); 2: 32 x 32, two LDS stages, transform in the MFMA shadow;
-// 3: 32 x 32, positions split over the waves on 32x32x2 MFMAs (half the LDS reads per MFMA cycle)
+// transform work and LDS writes per MFMA); 2: 32 x 32, two LDS stages, transform in the MFMA shadow.
+// (A position-split variant — each wave 9 of the 36 positions for a whole 32x32 tile on 32x32x2 MFMAs,
+// half the LDS reads per MFMA cycle — measured 5-8% SLOWER than variant 1 on every VGG-small layer,
+// profiles/wgrad4_variants_r3.jsonl, and was removed: the LDS-write / transform phase bounds it.)
 extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
                                 int splits, int accumulate, int variant, void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0 || splits <= 0) return RK_EBADARG;
   if (splits > 1 && accumulate) return RK_EBADARG;
-  if (variant < 0 || variant > 3) return RK_EBADARG;
+  if (variant < 0 || variant > 2) return RK_EBADARG;
   const int BCO = variant == 1 ? 64 : 32, BCI = 32;
   W4wParams p;
   p.dy = dy; p.x = x; p.out = out;
@@ -1202,9 +1033,7 @@ extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int
   const int used = rk_cdiv(p.ntiles, p.tps);
   if (used != splits) return RK_EBADARG;
   const long long blocks = (long long)splits * p.nco * p.nci;
-  if (variant == 3)
-    hipLaunchKernelGGL(wino4_wgrad_ps_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
-  else if (variant == 2)
+  if (variant == 2)
     hipLaunchKernelGGL(wino4_wgrad_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
   else if (variant == 1)
     hipLaunchKernelGGL((wino4_wgrad_kernel<4, 2, 1>), dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, p);

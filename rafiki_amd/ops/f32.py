@@ -118,11 +118,19 @@ def _cands(M, N, splittable=False, K=0, big=False):
     return out
 
 
-def _pick(key, cands, run):
+def _pick(key, cands, run, protect=()):
+    """The tuned config for ``key``.  ``protect``: tensors the op accumulates into — a tuning sweep runs
+    every candidate several times, so their contents are saved first and restored afterwards."""
     if _PIN is not None:
         return (_PIN[0], _PIN[1], cands[0][2])
     if not autotune.ENABLED:
         return cands[0]
+    if protect and autotune.lookup(key) is None and autotune.can_tune():
+        saved = [t.clone() for t in protect]
+        cfg = autotune.tune(key, cands, run)
+        for t, v in zip(protect, saved):
+            t.copy_(v)
+        return cfg
     return autotune.tune(key, cands, run)
 
 
@@ -277,7 +285,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
     ptcands = _wino4_pt_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
     cands += wcands + w4cands + ptcands
     cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands), bool(w4cands), bool(ptcands)),
-                cands, run)
+                cands, run, protect=(out,) if accumulate else ())
     run(cfg)
     return out
 
@@ -506,8 +514,7 @@ WINO4_WGRAD = -7  # autotune tile id of the F(4x4) weight gradient (cfg = (-7, 0
 
 def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     """Split-K choices of rk_wino4_wgrad_v (variant 0: 32 co x 32 ci blocks, 1: 64 co x 32 ci, 2: 32 x 32
-    software-pipelined over two LDS stages, 3: 32 x 32 with the 36 positions split over the waves on
-    32x32x2 MFMAs): 128..4096
+    software-pipelined over two LDS stages): 128..4096
     blocks, >= 4 chunks of 8 tiles per block, slabs <= 256 MiB.  cfg = (WINO4_WGRAD, variant, splits)."""
     if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and Cin >= 8 and Cout >= 16):
         return []
@@ -515,7 +522,7 @@ def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
         return []
     out = []
-    for v, bco in ((0, 32), (1, 64), (3, 32)) + (((2, 32),) if WINO_PIPE else ()):
+    for v, bco in ((0, 32), (1, 64)) + (((2, 32),) if WINO_PIPE else ()):
         if v == 1 and Cout < 64:
             continue
         base = cdiv(Cout, bco) * cdiv(Cin, 32)
@@ -555,8 +562,10 @@ WINO4_WGRAD_PT = -13  # pre-transformed F(4x4) weight gradient: cfg = (-13, sgem
 
 def _wino4_pt_cands(Nb, H, W, Cout, Cin):
     """The pre-transformed F(4x4) weight gradient (transform once, 36 GEMMs as one split-K sgemm) on
-    maps of <= 16x16 where the fused kernels' redundant per-block transforms dominate."""
-    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= 16 and W <= 16 and Cin % 4 == 0
+    maps of <= 8x8, where the fused kernels' redundant per-block transforms dominate (VGG-small batch
+    256: 8x8x256x256 84.8 vs 101.7 us, 4x4x512x512 76.4 vs 96.3; it loses on 16x16 maps,
+    profiles/wgrad4_variants_r3.jsonl)."""
+    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= 8 and W <= 8 and Cin % 4 == 0
             and Cout % 4 == 0 and Cin >= 32 and Cout >= 32):
         return []
     T = Nb * (H // 4) * (W // 4)
@@ -839,7 +848,7 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, *, out=None, accumulate=False):
               splits=s, slab_stride=Nout * Nin)
         reduce_slabs(slab, out, accumulate=accumulate)
     cands = _cands(Nout, Nin, splittable=True, K=M)
-    run(_pick(('sdw', M, Nout, Nin, bool(accumulate)), cands, run))
+    run(_pick(('sdw', M, Nout, Nin, bool(accumulate)), cands, run, protect=(out,) if accumulate else ()))
     return out
 
 

@@ -1,7 +1,7 @@
 # Round-3 GPU pass: wgrad variant tests + per-layer bench, full GPU suite, bench (1 GPU), --gpus 2 fails fast
 set -o pipefail
 mkdir -p gpurun_out/r3c
-timeout -k 10 300 python -u -m pytest tests/test_winograd4_gpu.py -x -q -k wgrad --timeout 120 --timeout-method thread > gpurun_out/r3c/w4_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_winograd4_gpu.py -x -q -k "wgrad" --timeout 120 --timeout-method thread > gpurun_out/r3c/w4_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/r3c/w4_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u scripts/bench_wgrad4.py gpurun_out/r3c/wgrad4.jsonl > gpurun_out/r3c/wgrad4.log 2>&1 || exit $?
 cat gpurun_out/r3c/wgrad4.log | cut -c1-220

@@ -220,7 +220,9 @@ def test_graphed_rounds_match_eager():
     from rafiki_amd.engine.flat import FlatAdam
     from rafiki_amd.models.pg_gan import GraphedRounds, PgGan, TrialRng
     outs = []
-    for graphed in (False, True):
+    # run 0 autotunes every shape (its first round times candidate kernels); runs 1-2 (eager) and 3
+    # (graphed) then use identical cached kernel choices
+    for graphed in (False, False, False, True):
         m = PgGan(D_repeats=1, minibatch_base=16, fmap_base=1024, fmap_max=128, seed=3)
         m.device = torch.device(DEV)
         m._build([1, 16, 16], 0)
@@ -240,13 +242,15 @@ def test_graphed_rounds_match_eager():
         assert graphs.captures == (1 if graphed else 0)
         assert int(rng.step.item()) == 10
         outs.append((nets.G.master.clone(), nets.D.master.clone(), acc.clone()))
-    (g0, d0, a0), (g1, d1, a1) = outs
+    (gt, dt, at), (ge, de, ae), (ge2, de2, ae2), (g1, d1, a1) = outs
     assert torch.isfinite(a1).all()
-    # fp32, same kernels, same RNG stream: only reduction-order noise may separate the two runs
-    print('graphed vs eager frob G {:.2e} D {:.2e} acc rel {:.2e}'.format(frob(g1, g0), frob(d1, d0),
-                                                                          rel_err(a1, a0)))
-    assert frob(g1, g0) <= 1e-5 and frob(d1, d0) <= 1e-5
-    assert rel_err(a1, a0) < 1e-4
+    print('eager vs eager frob G {:.2e} D {:.2e}; tuning run vs eager G {:.2e} D {:.2e}'.format(
+        frob(ge2, ge), frob(de2, de), frob(gt, ge), frob(dt, de)))
+    print('graphed vs eager frob G {:.2e} D {:.2e} acc rel {:.2e}'.format(frob(g1, ge), frob(d1, de),
+                                                                          rel_err(a1, ae)))
+    # fp32, same kernels, same RNG stream
+    assert frob(g1, ge) <= 1e-5 and frob(d1, de) <= 1e-5
+    assert rel_err(a1, ae) < 1e-4
 
 
 @pytest.mark.parametrize("N,H,C,segs", [(8, 4, 24, 1), (16, 4, 512, 2), (12, 2, 40, 3), (8, 4, 12, 2)])
