@@ -1178,3 +1178,125 @@ extern "C" int rk_wino4_pt_output(const float* du, float* out, int Co, int Ci, i
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
+
+// ---------------------------------------------------------- pre-transformed F(4x4) conv (deep layers)
+// y = conv3x3(x, w) as V = B^T x B once per 6x6 window (rk_wino4_pt_transform's x half, [36][T][C]),
+// Y'[q] = V[q] U[q]^T as ONE 36-group sgemm (u = wino4_u(w) [36][N][C], kind 3), then this output
+// transform A^T Y' A per 4x4 tile with the fused kernels' epilogues (bias, ReLU, BN statistics, BNB /
+// BNP data-gradient gating).  On the 8x8 / 4x4 maps the fused kernels re-transform every input window
+// once per output-channel block; here each window is transformed once and the GEMMs run at sgemm speed.
+namespace {
+
+__global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restrict__ yt, float* __restrict__ y,
+                                                            const float* __restrict__ bp, double* stats, int slotMask,
+                                                            const float* __restrict__ gate, int Nb, int H, int W,
+                                                            int N, int TW, int THW, int T, int flags) {
+  constexpr int TPB = 16;                  // tiles per block: 4 tile groups x 4 tiles each
+  __shared__ float red[2][4][64];
+  const int nblk = (N + 63) / 64;
+  const int nb = blockIdx.x % nblk, tb = blockIdx.x / nblk;
+  const int lane = threadIdx.x & 63, tg = threadIdx.x >> 6;
+  const int n = nb * 64 + lane;
+  const bool nok = n < N;
+  const long long plane = (long long)T * N;
+  const float bs = ((flags & (WF_BIAS | WF_BNB | WF_BNP)) && nok) ? bp[n] : 0.f;
+  const float sh = ((flags & (WF_BNB | WF_BNP)) && nok) ? bp[N + n] : 0.f;
+  float s = 0.f, ss = 0.f;
+  for (int r = 0; r < 4; ++r) {
+    const int t = tb * TPB + tg * 4 + r;
+    if (t >= T || !nok) continue;
+    float m[36];
+#pragma unroll
+    for (int q = 0; q < 36; ++q) m[q] = yt[q * plane + (long long)t * N + n];
+    float tt[6][4];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {          // M A: along columns
+      float o[4];
+      at6(m[a * 6 + 0], m[a * 6 + 1], m[a * 6 + 2], m[a * 6 + 3], m[a * 6 + 4], m[a * 6 + 5], o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tt[a][j] = o[j];
+    }
+    const int im = t / THW, rr = t - im * THW, ty = rr / TW;
+    const int oy = 4 * ty, ox = 4 * (rr - ty * TW);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o[4];
+      at6(tt[0][j], tt[1][j], tt[2][j], tt[3][j], tt[4][j], tt[5][j], o);   // A^T (M A): along rows
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = o[i];
+        const long long idx = (((long long)im * H + oy + i) * W + ox + j) * N + n;
+        if (flags & WF_BIAS) v += bs;
+        if (flags & WF_STATS) {
+          s += v;
+          ss += v * v;
+        }
+        if (flags & WF_RELU) v = fmaxf(v, 0.f);
+        if (flags & WF_BNB) {
+          const float g = gate[idx];
+          v = g * bs + sh > 0.f ? v : 0.f;
+          s += v;
+          ss += v * g;
+        }
+        if (flags & WF_BNP) {
+          const long long W2 = 2LL * W;
+          const long long q0 = (((long long)im * 2 * H + 2 * (oy + i)) * W2 + 2 * (ox + j)) * N + n;
+          const float y4[4] = {gate[q0], gate[q0 + N], gate[q0 + W2 * N], gate[q0 + W2 * N + N]};
+          float best = -INFINITY, zb = 0.f, yb = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {    // first maximal relu(z) of the window (torch max_pool2d rule)
+            const float z = y4[e] * bs + sh;
+            const float av = fmaxf(z, 0.f);
+            if (av > best) { best = av; zb = z; yb = y4[e]; }
+          }
+          const float dz = zb > 0.f ? v : 0.f;
+          s += dz;
+          ss += dz * yb;
+        }
+        y[idx] = v;
+      }
+    }
+  }
+  if (flags & (WF_STATS | WF_BNB | WF_BNP)) {
+    red[0][tg][lane] = s;
+    red[1][tg][lane] = ss;
+    __syncthreads();
+    if (tg == 0 && nok) {
+      const float a = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+      const float b = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+      double* slot = stats + (long long)(blockIdx.x & slotMask) * 2 * N;
+      unsafeAtomicAdd(slot + n, (double)a);
+      unsafeAtomicAdd(slot + N + n, (double)b);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias, double* stats, int slotMask,
+                                    const float* gate, int Nb, int H, int W, int N, int flags, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || N <= 0) return RK_EBADARG;
+  if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
+  if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
+  if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
+  const int TW = W / 4, THW = (H / 4) * (W / 4);
+  const long long T = (long long)Nb * THW;
+  if (T * N >= (1LL << 31)) return RK_EUNSUPPORTED;
+  const long long blocks = ((N + 63) / 64) * ((T + 15) / 16);
+  hipLaunchKernelGGL(w4pt_conv_out_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, yt, y, bias,
+                     stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// V = B^T x B of every 6x6 window: [36][T][C] (the x half of rk_wino4_pt_transform)
+extern "C" int rk_wino4_pt_input(const float* x, float* v, int Nb, int H, int W, int C, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || C <= 0) return RK_EBADARG;
+  const int TW = W / 4, THW = (H / 4) * (W / 4);
+  const long long T = (long long)Nb * THW;
+  const long long tx = T * C;
+  hipLaunchKernelGGL(w4pt_x_kernel, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, v, H, W,
+                     C, TW, THW, tx, T);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}

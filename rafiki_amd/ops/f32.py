@@ -159,8 +159,14 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     use_w = wino is not None and taps == 9 and wino_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
 
+    use_pt = use_w4 and wino4_pt_ok(H, W, Cin, Cout)
+
     def run(cfg):
         tile, nst, s = cfg
+        if tile == WINO4_PT:
+            wino4_conv_pt(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
+                          relu=act == ACT_RELU, tile=nst, nst=s)
+            return
         if cfg in WINO4_CFGS:
             wino4_conv(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
                        relu=act == ACT_RELU, variant=_wino4_variant(cfg))
@@ -184,8 +190,10 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         cands.extend(WINO_CFGS)
     if use_w4:
         cands.extend(WINO4_CFGS)
+    if use_pt:
+        cands.extend(WINO4_PT_CFGS)
     cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt), cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -222,7 +230,13 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
     use_w = wino is not None and taps == 9 and wino_ok(H, W, Cout) and not (flags & F_GATE)
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cout) and not (flags & F_GATE)
 
+    use_pt = use_w4 and wino4_pt_ok(H, W, Cout, Cin)
+
     def run(cfg):
+        if cfg[0] == WINO4_PT:
+            wino4_conv_pt(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, tile=cfg[1],
+                          nst=cfg[2])
+            return
         if cfg in WINO4_CFGS:
             wino4_conv(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp,
                        variant=_wino4_variant(cfg))
@@ -237,8 +251,10 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
         cands.extend(WINO_CFGS)
     if use_w4:
         cands.extend(WINO4_CFGS)
+    if use_pt:
+        cands.extend(WINO4_PT_CFGS)
     cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt), cands, run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -491,6 +507,57 @@ def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=N
         assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
     _lib.call("rk_wino4_conv", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
               Nb, H, W, C, N, flags, int(variant), _s())
+    return out
+
+
+WINO4_PT = -14   # pre-transformed F(4x4) conv: cfg = (-14, sgemm tile, sgemm nst)
+
+
+def wino4_pt_ok(H, W, C, N):
+    """Deep maps (<= 8x8), where the fused kernels re-transform each input window once per output-channel
+    block: there the transform-once + grouped-GEMM path is a tuner candidate."""
+    return (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= 8 and W <= 8 and C % 4 == 0 and C >= 32
+            and N >= 32)
+
+
+WINO4_PT_CFGS = tuple((WINO4_PT, t, n) for t in (0, 1, 2, 3) for n in ((2, 3) if t in _NST3 else (2,)))
+
+
+def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None,
+                  bnp=None, tile=0, nst=2):
+    """wino4_conv through position-major buffers: V = B^T x B [36][T][C] (one launch), Y'[q] = V[q] u[q]^T
+    as one 36-group sgemm, then A^T Y' A with the same epilogues (bias / ReLU / BN statistics / BNB / BNP)."""
+    _check(x, 'wino4_conv_pt x')
+    Nb, H, W, C = x.shape
+    N = u.shape[1]
+    assert u.shape == (36, N, C) and u.is_contiguous() and H % 4 == 0 and W % 4 == 0, (u.shape, x.shape)
+    if out is None:
+        out = torch.empty((Nb, H, W, N), device=x.device, dtype=torch.float32)
+    assert out.shape == (Nb, H, W, N) and out.is_contiguous()
+    flags, gate = 0, None
+    if bias is not None:
+        flags |= WF_BIAS
+    if relu:
+        flags |= WF_RELU
+    if stats is not None:
+        flags |= WF_STATS
+    if bnb is not None:
+        gate, coeffs, stats = bnb
+        assert gate.shape == out.shape
+        bias, flags = coeffs[2:4].reshape(-1).contiguous(), WF_BNB
+    elif bnp is not None:
+        gate, coeffs, stats = bnp
+        assert gate.shape == (Nb, 2 * H, 2 * W, N)
+        bias, flags = coeffs[2:4].reshape(-1).contiguous(), WF_BNP
+    if stats is not None:
+        assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
+    T = Nb * (H // 4) * (W // 4)
+    v = torch.empty((36, T, C), device=x.device, dtype=torch.float32)
+    _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
+    yt = torch.empty((36, T, N), device=x.device, dtype=torch.float32)
+    sgemm_grp(KIND_DENSE, v, u, yt, T, N, C, C, C, N, 36, T * C, N * C, T * N, tile=tile, nst=nst)
+    _lib.call("rk_wino4_pt_conv_out", _p(yt), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
+              Nb, H, W, N, flags, _s())
     return out
 
 

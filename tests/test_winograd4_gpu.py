@@ -213,3 +213,49 @@ def test_wino4_wgrad_pretransformed(N, H, W, Cin, Cout, tile):
     ref = gw.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
     assert rel(dw, ref) < TOL
     assert rel(acc, ref + prev.double().cpu()) < TOL
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(8, 4, 4, 512, 512), (3, 8, 8, 256, 96), (16, 8, 8, 64, 128),
+                                            (5, 4, 8, 40, 36)])
+@pytest.mark.parametrize("tile", [0, 3])
+def test_wino4_conv_pretransformed_fwd_stats_bias_relu(N, H, W, Cin, Cout, tile):
+    """Pre-transformed F(4x4) conv (input transform + 36-group sgemm + output transform) vs fp64."""
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, W, Cin, seed=50)
+    w = _rand(Cout, 3, 3, Cin, seed=51, scale=1.0 / math.sqrt(9 * Cin))
+    u = S.wino4_u(_w2(w))
+    acc = torch.zeros((S.bn_slots(Cout), 2, Cout), dtype=torch.float64, device=DEV)
+    y = S.wino4_conv_pt(x.to(DEV), u, stats=acc, tile=tile)
+    b = _rand(Cout, seed=52)
+    yb = S.wino4_conv_pt(x.to(DEV), u, bias=b.to(DEV), relu=True, tile=tile)
+    torch.cuda.synchronize()
+    ref = _conv_ref(x, w)
+    assert rel(y, ref) < TOL
+    s = acc.sum(0).cpu()
+    r = ref.reshape(-1, Cout)
+    assert rel(s[0], r.sum(0)) < TOL and rel(s[1], (r * r).sum(0)) < TOL
+    assert rel(yb, torch.relu(ref + b.double())) < TOL
+
+
+@pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("H", [8, 4])
+def test_wino4_conv_pretransformed_bn_epilogues(pool, H):
+    """BNB / BNP data-gradient epilogues of the pre-transformed conv == the fused kernel's."""
+    from rafiki_amd.ops import f32 as S
+    N, W, Cin, Cout = 4, H, 64, 128
+    Hy, Wy = (2 * H, 2 * W) if pool else (H, W)
+    y = _rand(N, Hy, Wy, Cin, seed=57) + 0.2
+    gamma, beta = torch.ones(Cin) * 1.3, _rand(Cin, seed=58) * 0.1
+    acc = torch.zeros((S.bn_slots(Cin), 2, Cin), dtype=torch.float64, device=DEV)
+    S.col_stats(y.to(DEV).view(-1, Cin), acc)
+    _, coeffs = S.bn_fwd(y.to(DEV), acc, N * Hy * Wy, gamma.to(DEV), beta.to(DEV), 1e-5, pool=pool, act=1)
+    w = _rand(Cout, 3, 3, Cin, seed=59, scale=0.05)
+    ut = S.wino4_ut(_w2(w))
+    dyo = _rand(N, H, W, Cout, seed=60).to(DEV)
+    acc_f, acc_p = torch.zeros_like(acc), torch.zeros_like(acc)
+    key = 'bnp' if pool else 'bnb'
+    d_f = S.wino4_conv(dyo, ut, **{key: (y.to(DEV), coeffs, acc_f)})
+    d_p = S.wino4_conv_pt(dyo, ut, **{key: (y.to(DEV), coeffs, acc_p)})
+    torch.cuda.synchronize()
+    assert rel(d_p, d_f) < TOL
+    assert rel(acc_p.sum(0), acc_f.sum(0)) < TOL
