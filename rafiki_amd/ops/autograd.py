@@ -25,6 +25,7 @@ native library is mandatory (a missing extension raises, it never silently falls
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -278,12 +279,33 @@ def up_weights(w, cin):
     return _box4(w.reshape(co, 3, 3, cin).flip(1, 2)).permute(3, 1, 2, 0).reshape(cin, 16 * co)
 
 
+def resample_via_winograd(full_hw: int, channels: int) -> bool:
+    """Resampling conv by Winograd at full resolution instead of the direct stride-2 / transposed conv?
+
+    The fused stride-2 forms (S2: 4x4 taps at the low resolution, S2T: 4 parity groups of 2x2 taps) do
+    16 / 4 MACs per low-res / full-res output and channel pair; conv3x3 at full resolution by F(4x4,3x3)
+    does 2.25 per full-res pixel — 1.8x fewer MFMA cycles for the down conv, 1.8x fewer for the up conv
+    — at the price of one full-resolution activation round trip (upscale / box-filter pass).  On the
+    32x32x512 PG-GAN layers the resampling convs were a third of the lod-0 step
+    (profiles/pg_gan_lod0_f32_kernels_r3.txt).  RAFIKI_PGGAN_RESAMPLE = auto (Winograd on maps >= 16 with
+    >= 64 channels) | direct | wino."""
+    mode = os.environ.get('RAFIKI_PGGAN_RESAMPLE', 'auto')
+    if mode == 'direct':
+        return False
+    if mode == 'wino':
+        return S.WINO and S.WINO4 and full_hw % 4 == 0 and channels % 8 == 0
+    return S.WINO and S.WINO4 and full_hw >= 16 and full_hw % 4 == 0 and channels >= 64 and channels % 8 == 0
+
+
 def upscale_conv2d(x, w, b=None, *, wb=None, lrelu=None):
     """conv3x3(upscale2d(x), w) + b (pg_gans.py:1032-1039)."""
     if x.device.type != 'cuda':
         y = _conv_ref(upscale2d(x), w, b, 9)
         return y if lrelu is None else leaky_relu(y, lrelu)
     if x.dtype == F32:
+        if resample_via_winograd(2 * x.shape[1], x.shape[-1]):
+            # upscale (native kernel) then the Winograd-capable 3x3 conv with bias + leaky ReLU epilogue
+            return conv2d(upscale2d(x.contiguous()), w, b, lrelu=lrelu)
         return S2TFn.apply(x.contiguous(), up_weights(w, x.shape[-1]), b, None if lrelu is None else float(lrelu))
     y = UpConvFn.apply(x, w, b, wb)
     return y if lrelu is None else leaky_relu(y, lrelu)
@@ -292,6 +314,11 @@ def upscale_conv2d(x, w, b=None, *, wb=None, lrelu=None):
 def conv2d_downscale2d(x, w, b=None, *, wb=None, lrelu=None):
     """conv3x3 then 2x2 box downscale (+b) == the reference's fused 4x4 stride-2 conv (pg_gans.py:1053-1059)."""
     if x.device.type == 'cuda' and x.dtype == F32:
+        if resample_via_winograd(x.shape[1], x.shape[-1]):
+            # Winograd conv at full resolution (+bias in its epilogue: the box filter commutes with it),
+            # the native box-filter downscale, then the leaky ReLU on the quarter-size map
+            y = downscale2d(conv2d(x.contiguous(), w, b))
+            return y if lrelu is None else leaky_relu(y, lrelu)
         return S2Fn.apply(x.contiguous(), down_weights(w, x.shape[-1]), b, None if lrelu is None else float(lrelu))
     y = downscale2d(conv2d(x, w, b, taps=9, wb=wb))
     return y if lrelu is None else leaky_relu(y, lrelu)

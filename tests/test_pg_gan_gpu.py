@@ -333,3 +333,43 @@ def _dp_round_child():
         assert cos(g0, g1) > 0.9999 and cos(d0, d1) > 0.9999
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["direct", "wino"])
+@pytest.mark.parametrize("up", [False, True])
+def test_resampling_conv_paths_double_backward(mode, up, monkeypatch):
+    """Both implementations of the resampling convs (direct stride-2 / transposed gather vs Winograd at
+    full resolution) give the reference's values, gradients and WGAN-GP second derivatives."""
+    from rafiki_amd.ops import autograd as A
+    monkeypatch.setenv('RAFIKI_PGGAN_RESAMPLE', mode)
+    g = torch.Generator().manual_seed(5)
+    N, H, C = 2, (8 if up else 16), 64
+    x0 = torch.randn(N, H, H, C, generator=g, dtype=torch.float64)
+    w0 = torch.randn(C, 9 * C, generator=g, dtype=torch.float64) * (1.0 / (9 * C)) ** 0.5
+    b0 = torch.randn(C, generator=g, dtype=torch.float64) * 0.1
+
+    def ref(x, w, b):
+        xc = x.permute(0, 3, 1, 2)
+        wc = w.reshape(C, 3, 3, C).permute(0, 3, 1, 2)
+        if up:
+            y = TF.conv2d(TF.interpolate(xc, scale_factor=2, mode='nearest'), wc, b, padding=1)
+        else:
+            y = TF.avg_pool2d(TF.conv2d(xc, wc, None, padding=1), 2) + b.view(1, -1, 1, 1)
+        return TF.leaky_relu(y, 0.2).permute(0, 2, 3, 1)
+
+    def run(fn, x0, w0, b0, dt, dev):
+        x = x0.to(dev, dt).requires_grad_(True)
+        w = w0.to(dev, dt).requires_grad_(True)
+        b = b0.to(dev, dt).requires_grad_(True)
+        y = fn(x, w, b)
+        (gx,) = torch.autograd.grad(y.sum(), x, create_graph=True)
+        (gx.square().sum() + y.square().sum()).backward()
+        return y.detach(), gx.detach(), w.grad, b.grad
+
+    fn = (lambda x, w, b: A.upscale_conv2d(x, w, b, lrelu=0.2)) if up else \
+        (lambda x, w, b: A.conv2d_downscale2d(x, w, b, lrelu=0.2))
+    got = run(fn, x0, w0, b0, torch.float32, DEV)
+    exp = run(ref, x0, w0, b0, torch.float64, 'cpu')
+    torch.cuda.synchronize()
+    for a, e in zip(got, exp):
+        assert frob(a, e) < 1e-4, (mode, up, frob(a, e))
