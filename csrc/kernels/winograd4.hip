@@ -1191,7 +1191,8 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
                                                             const float* __restrict__ bp, double* stats, int slotMask,
                                                             const float* __restrict__ gate, int Nb, int H, int W,
                                                             int N, int TW, int THW, int T, int flags) {
-  constexpr int TPB = 16;                  // tiles per block: 4 tile groups x 4 tiles each
+  constexpr int TPB = 4;                   // tiles per block: one per 64-thread group (>= 2 blocks per CU
+                                           // on the 4x4 x 512 maps: T x N / 256 blocks)
   __shared__ float red[2][4][64];
   const int nblk = (N + 63) / 64;
   const int nb = blockIdx.x % nblk, tb = blockIdx.x / nblk;
@@ -1202,9 +1203,9 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
   const float bs = ((flags & (WF_BIAS | WF_BNB | WF_BNP)) && nok) ? bp[n] : 0.f;
   const float sh = ((flags & (WF_BNB | WF_BNP)) && nok) ? bp[N + n] : 0.f;
   float s = 0.f, ss = 0.f;
-  for (int r = 0; r < 4; ++r) {
-    const int t = tb * TPB + tg * 4 + r;
-    if (t >= T || !nok) continue;
+  {
+    const int t = tb * TPB + tg;
+    if (t < T && nok) {
     float m[36];
 #pragma unroll
     for (int q = 0; q < 36; ++q) m[q] = yt[q * plane + (long long)t * N + n];
@@ -1256,6 +1257,7 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
         y[idx] = v;
       }
     }
+    }
   }
   if (flags & (WF_STATS | WF_BNB | WF_BNP)) {
     red[0][tg][lane] = s;
@@ -1282,7 +1284,7 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
   const int TW = W / 4, THW = (H / 4) * (W / 4);
   const long long T = (long long)Nb * THW;
   if (T * N >= (1LL << 31)) return RK_EUNSUPPORTED;
-  const long long blocks = ((N + 63) / 64) * ((T + 15) / 16);
+  const long long blocks = ((N + 63) / 64) * ((T + 3) / 4);
   hipLaunchKernelGGL(w4pt_conv_out_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, yt, y, bias,
                      stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags);
   RK_LAUNCH_CHECK();

@@ -49,7 +49,7 @@ def stages(m, lod=2.0, mb=64):
     loss.mean().backward(retain_graph=True)
     out['D_grad'] = nets.D.grad.clone()
     nets.D.grad.zero_()
-    (mixed_s.sum()).backward()
+    (mixed_s.sum()).backward(retain_graph=True)
     out['D_grad_plain'] = nets.D.grad.clone()
     nets.D.grad.zero_()
     (norms.sum()).backward()
