@@ -352,6 +352,8 @@ def main():
             'backend': info.backend,
             'world_size': D.world_size(info),
             'n_devices': n_devices,
+            # ranks sharing GPUs (gloo rehearsal of the control path on a smaller box): no aggregate
+            'rehearsal': n_devices < world,
             'images_per_sec_per_rank_min': round(min(per_rank), 1),
             'images_per_sec_per_rank_max': round(max(per_rank), 1),
             'images_per_sec_per_trial': round(ips_trial, 1),
