@@ -11,6 +11,7 @@ import math
 
 import pytest
 import torch
+import torch.nn.functional as TF
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
