@@ -601,3 +601,61 @@ extern "C" int rk_lrelu_pixelnorm_f32(const void* x, const float* bias, const vo
                                       float eps, void* out, void* stream) {
   return lrelu_pn_launch<float>(x, bias, dz, P, C, slope, eps, out, (hipStream_t)stream);
 }
+
+// ------------------------------------------------------------------------------ leaky-ReLU gate
+// g = gy * (y > 0 ? 1 : slope): the gradient through a leaky ReLU read from its OUTPUT y (same sign as the
+// input).  Linear in gy, so the autograd Function applies the same gate to differentiate it again
+// (WGAN-GP double backward).  The _colsum form also reduces g over rows (the conv bias gradient) in
+// the same pass: 64 channels per block, gridDim.y row chunks write partial sums to part + y * C.
+namespace {
+
+__global__ __launch_bounds__(256) void lrelu_gate_kernel(const float4* __restrict__ gy, const float4* __restrict__ y,
+                                                         float4* __restrict__ out, long long n4, float slope) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 g = gy[i], v = y[i];
+    out[i] = make_float4(v.x > 0.f ? g.x : g.x * slope, v.y > 0.f ? g.y : g.y * slope,
+                         v.z > 0.f ? g.z : g.z * slope, v.w > 0.f ? g.w : g.w * slope);
+  }
+}
+
+__global__ __launch_bounds__(256) void lrelu_gate_colsum_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                                                                float* __restrict__ out, int R, int C, float slope,
+                                                                float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int q = threadIdx.x >> 6;
+  const int per = (R + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(R, r0 + per);
+  float s = 0.f;
+  if (c < C)
+    for (int r = r0 + q; r < r1; r += 4) {
+      const long long i = (long long)r * C + c;
+      const float g = y[i] > 0.f ? gy[i] : gy[i] * slope;
+      out[i] = g;
+      s += g;
+    }
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && c < C)
+    part[(long long)blockIdx.y * C + c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+}  // namespace
+
+extern "C" int rk_lrelu_gate_f32(const float* gy, const float* y, float* out, long long n, float slope, void* stream) {
+  if (n <= 0 || (n & 3)) return RK_EUNSUPPORTED;
+  const long long n4 = n / 4;
+  const unsigned blocks = (unsigned)std::min<long long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(lrelu_gate_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float4*)gy,
+                     (const float4*)y, (float4*)out, n4, slope);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_lrelu_gate_colsum_f32(const float* gy, const float* y, float* out, int R, int C, float slope,
+                                        float* part, int chunks, void* stream) {
+  if (R <= 0 || C <= 0 || chunks < 1) return RK_EBADARG;
+  hipLaunchKernelGGL(lrelu_gate_colsum_kernel, dim3(rk_cdiv(C, 64), chunks), dim3(256), 0, (hipStream_t)stream, gy, y,
+                     out, R, C, slope, part);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}

@@ -89,6 +89,8 @@ _SIGS = {
     "rk_bnf_colstats": [vp, vp, i32, i32, vp, vp],
     "rk_swt": [vp, vp, vp, i32, vp, vp],
     "rk_colsum_f32": [vp, i32, i32, i32, vp, i32, i32, vp],
+    "rk_lrelu_gate_f32": [vp, vp, vp, i64, f32, vp],
+    "rk_lrelu_gate_colsum_f32": [vp, vp, vp, i32, i32, f32, vp, i32, vp],
     "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, i32, vp],
     "rk_sgemm_grp": [i32, i32, i32, vp, vp, vp, vp] + [i32] * 10 + [i32, i64, i32, f32, f32, i64, i64, i32, i64, i64,
                                                                      i64, i64, vp],

@@ -125,10 +125,28 @@ def sumpool2(x):
 
 
 # ------------------------------------------------------------------------------------- conv
+class LReluGateFn(torch.autograd.Function):
+    """g = gy * (y > 0 ? 1 : slope) on the native kernel; linear in gy, so its derivative is the same
+    gate (WGAN-GP double backward).  The mask is piecewise constant: no gradient flows into y."""
+
+    @staticmethod
+    def forward(ctx, gy, y, slope):
+        ctx.save_for_backward(y)
+        ctx.slope = slope
+        return S.lrelu_gate(gy.contiguous(), y.detach().contiguous(), slope)
+
+    @staticmethod
+    def backward(ctx, gg):
+        (y,) = ctx.saved_tensors
+        return LReluGateFn.apply(gg, y, ctx.slope), None, None
+
+
 def _lrelu_gate(gy, y, slope):
     """gy * lrelu'(.) with the mask read from the activation OUTPUT y (same sign as its input);
-    linear in gy, so it differentiates again through torch (WGAN-GP double backward).  The mask is
-    piecewise constant, so y is detached: no (zero) gradient is routed back into y's producer."""
+    linear in gy, so it differentiates again (WGAN-GP double backward).  The mask is piecewise
+    constant, so y is detached: no (zero) gradient is routed back into y's producer."""
+    if gy.is_cuda and gy.dtype == F32 and y.dtype == F32 and gy.shape[-1] % 4 == 0:
+        return LReluGateFn.apply(gy, y, float(slope))
     return torch.ops.aten.leaky_relu_backward(gy, y.detach(), slope, True)
 
 
@@ -160,15 +178,22 @@ class ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors[:2]
+        gb = None
         if ctx.slope is not None:
-            gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
+            y = ctx.saved_tensors[2]
+            if (ctx.has_b and _needed(ctx, 2) and not torch.is_grad_enabled() and gy.is_cuda
+                    and gy.dtype == F32 and y.dtype == F32 and gy.is_contiguous()):
+                # outside a create_graph backward: gate + bias gradient in one pass over gy
+                gy, gb = S.lrelu_gate_colsum(gy, y.contiguous(), float(ctx.slope))
+            else:
+                gy = _lrelu_gate(gy, y, ctx.slope)
         gy = _as(gy, ctx.dt)
-        gx = gw = gb = None
+        gx = gw = None
         if _needed(ctx, 0):
             gx = ConvDgradFn.apply(gy, w, ctx.wb, ctx.taps)
         if _needed(ctx, 1):
             gw = ConvWgradFn.apply(x, gy, ctx.taps)
-        if ctx.has_b and _needed(ctx, 2):
+        if ctx.has_b and _needed(ctx, 2) and gb is None:
             gb = _bias_grad(gy)
         return gx, gw, gb, None, None, None
 
@@ -450,10 +475,17 @@ class DenseFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors[:2]
+        gb = None
         if ctx.slope is not None:
-            gy = _lrelu_gate(gy, ctx.saved_tensors[2], ctx.slope)
+            y = ctx.saved_tensors[2]
+            if (ctx.has_b and _needed(ctx, 2) and not torch.is_grad_enabled() and gy.is_cuda
+                    and gy.dtype == F32 and y.dtype == F32 and gy.is_contiguous()):
+                # outside a create_graph backward: gate + bias gradient in one pass over gy
+                gy, gb = S.lrelu_gate_colsum(gy, y.contiguous(), float(ctx.slope))
+            else:
+                gy = _lrelu_gate(gy, y, ctx.slope)
         gy = _as(gy, ctx.dt)
-        gx = gw = gb = None
+        gx = gw = None
         if _needed(ctx, 0):
             gx = DenseDxFn.apply(gy, w, ctx.wb)
         if _needed(ctx, 1):

@@ -932,6 +932,34 @@ def reduce_slabs(slab, out, *, accumulate=False, scale=1.0):
     return _rs(slab, out, accumulate=accumulate, scale=scale)
 
 
+def lrelu_gate(gy: torch.Tensor, y: torch.Tensor, slope: float, out=None):
+    """gy * (y > 0 ? 1 : slope) (fp32, contiguous, same shape)."""
+    _check(gy, 'lrelu_gate gy')
+    _check(y, 'lrelu_gate y')
+    assert gy.shape == y.shape
+    if out is None:
+        out = torch.empty_like(gy)
+    _lib.call("rk_lrelu_gate_f32", _p(gy), _p(y), _p(out), gy.numel(), float(slope), _s())
+    return out
+
+
+def lrelu_gate_colsum(gy: torch.Tensor, y: torch.Tensor, slope: float):
+    """(g, colsum(g)) with g = lrelu_gate(gy, y, slope) in one pass; gy / y [..., C] fp32."""
+    _check(gy, 'lrelu_gate_colsum gy')
+    _check(y, 'lrelu_gate_colsum y')
+    assert gy.shape == y.shape
+    Cc = gy.shape[-1]
+    R = gy.numel() // Cc
+    g = torch.empty_like(gy)
+    chunks = max(1, min(cdiv(R, 256), cdiv(2 * NUM_CU, cdiv(Cc, 64))))
+    part = torch.empty((chunks, Cc), device=gy.device, dtype=torch.float32)
+    _lib.call("rk_lrelu_gate_colsum_f32", _p(gy), _p(y), _p(g), R, Cc, float(slope), _p(part), chunks, _s())
+    if chunks == 1:
+        return g, part[0]
+    out = torch.empty(Cc, device=gy.device, dtype=torch.float32)
+    return g, reduce_slabs(part, out)
+
+
 def colsum(x2d, out, *, accumulate=False):
     """out[c] (+)= sum_r x2d[r, c] (fp32).  Tall inputs split the rows over ~2 blocks per CU, then fold
     the partial rows with reduce_slabs."""

@@ -374,3 +374,26 @@ def test_resampling_conv_paths_double_backward(mode, up, monkeypatch):
     torch.cuda.synchronize()
     for a, e in zip(got, exp):
         assert frob(a, e) < 1e-4, (mode, up, frob(a, e))
+
+
+def test_lrelu_gate_kernels_and_double_backward():
+    """Native leaky-ReLU gate: plain, fused with the bias column sum, and its own derivative."""
+    from rafiki_amd.ops import autograd as A
+    from rafiki_amd.ops import f32 as S
+    g = torch.Generator().manual_seed(9)
+    gy = torch.randn(3, 5, 7, 24, generator=g).to(DEV)
+    y = torch.randn(3, 5, 7, 24, generator=g).to(DEV)
+    ref = torch.where(y > 0, gy, gy * 0.2)
+    assert torch.equal(S.lrelu_gate(gy, y, 0.2), ref)
+    out, cs = S.lrelu_gate_colsum(gy, y, 0.2)
+    assert torch.equal(out, ref)
+    assert rel_err(cs, ref.reshape(-1, 24).double().sum(0).float()) < 1e-5
+    big = torch.randn(64, 32, 32, 64, generator=g).to(DEV)
+    yb = torch.randn(64, 32, 32, 64, generator=g).to(DEV)
+    _, csb = S.lrelu_gate_colsum(big, yb, 0.2)
+    refb = torch.where(yb > 0, big, big * 0.2).reshape(-1, 64).double().sum(0)
+    assert rel_err(csb, refb.float()) < 1e-5
+    a = gy.clone().requires_grad_(True)
+    o = A.LReluGateFn.apply(a, y, 0.2)
+    (ga,) = torch.autograd.grad((o * o).sum(), a, create_graph=True)
+    assert torch.allclose(ga, 2 * torch.where(y > 0, ref, ref * 0.2), atol=1e-6)
