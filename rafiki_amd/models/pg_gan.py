@@ -41,6 +41,7 @@ pseudo-classes).  The number is therefore NOT comparable to a published Inceptio
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import pickle
@@ -756,7 +757,10 @@ class PgGan(BaseModel):
         loss = loss + real_s.square() * wgan_epsilon
         if nets.label_size:
             loss = loss + _softmax_xent(real_l, labels) + _softmax_xent(fake_l, labels)
-        loss.mean().backward()
+        # data-parallel rounds launch their all-reduce buckets from post-accumulate-grad hooks, so
+        # they keep autograd's accumulation
+        with A.accumulate_weight_grads_in_place() if ar is None else contextlib.nullcontext():
+            loss.mean().backward()
         if ar is not None:
             ar.finish()
         self._finite_guard(nets.D, opt)
@@ -780,7 +784,10 @@ class PgGan(BaseModel):
             loss = loss + _softmax_xent(fake_l, labels)
         if ar is not None:
             ar.begin()
-        loss.mean().backward()
+        # data-parallel rounds launch their all-reduce buckets from post-accumulate-grad hooks, so
+        # they keep autograd's accumulation
+        with A.accumulate_weight_grads_in_place() if ar is None else contextlib.nullcontext():
+            loss.mean().backward()
         if ar is not None:
             ar.finish()
         self._finite_guard(nets.G, opt)

@@ -25,7 +25,9 @@ native library is mandatory (a missing extension raises, it never silently falls
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 from typing import Optional
 
 import torch
@@ -125,6 +127,38 @@ def sumpool2(x):
 
 
 # ------------------------------------------------------------------------------------- conv
+_direct = threading.local()
+
+
+@contextlib.contextmanager
+def accumulate_weight_grads_in_place():
+    """Within this context a plain ``loss.backward()`` (no create_graph) accumulates fp32 conv / dense
+    weight gradients straight into each leaf's persistent ``.grad`` buffer (the flat gradient arena)
+    and returns None for the weight, skipping autograd's AccumulateGrad add — one weight-sized
+    read-modify-write per use, and a weight is used several times per WGAN-GP step (real/fake, mixed,
+    the penalty's double backward).  Only for ``.backward()`` into ``.grad`` (not autograd.grad)."""
+    prev = getattr(_direct, 'on', False)
+    _direct.on = True
+    try:
+        yield
+    finally:
+        _direct.on = prev
+
+
+def _param_grad_buffer(w):
+    """The persistent fp32 gradient buffer of a weight (the leaf's .grad, or the viewed leaf's, in the
+    weight's shape), inside ``accumulate_weight_grads_in_place`` and outside a create_graph backward."""
+    if not getattr(_direct, 'on', False) or torch.is_grad_enabled() or w.dtype != F32 or not w.is_cuda:
+        return None
+    leaf = w if w.is_leaf else getattr(w, '_base', None)
+    if leaf is None or not leaf.is_leaf or not leaf.requires_grad:
+        return None
+    g = leaf.grad
+    if g is None or g.dtype != F32 or not g.is_contiguous() or g.numel() != w.numel() or leaf.numel() != w.numel():
+        return None
+    return g.view(w.shape)
+
+
 class LReluGateFn(torch.autograd.Function):
     """g = gy * (y > 0 ? 1 : slope) on the native kernel; linear in gy, so its derivative is the same
     gate (WGAN-GP double backward).  The mask is piecewise constant: no gradient flows into y."""
@@ -192,7 +226,12 @@ class ConvFn(torch.autograd.Function):
         if _needed(ctx, 0):
             gx = ConvDgradFn.apply(gy, w, ctx.wb, ctx.taps)
         if _needed(ctx, 1):
-            gw = ConvWgradFn.apply(x, gy, ctx.taps)
+            buf = _param_grad_buffer(w) if x.dtype == F32 else None
+            if buf is not None:
+                S.conv_wgrad(gy.contiguous(), x.contiguous(), taps=ctx.taps, out=buf.view(buf.shape[0], -1),
+                             accumulate=True)
+            else:
+                gw = ConvWgradFn.apply(x, gy, ctx.taps)
         if ctx.has_b and _needed(ctx, 2) and gb is None:
             gb = _bias_grad(gy)
         return gx, gw, gb, None, None, None
@@ -489,8 +528,12 @@ class DenseFn(torch.autograd.Function):
         if _needed(ctx, 0):
             gx = DenseDxFn.apply(gy, w, ctx.wb)
         if _needed(ctx, 1):
-            gw = DenseDwFn.apply(x, gy)
-        if ctx.has_b and _needed(ctx, 2):
+            buf = _param_grad_buffer(w) if x.dtype == F32 else None
+            if buf is not None:
+                S.linear_dw(gy.contiguous(), x.contiguous(), out=buf, accumulate=True)
+            else:
+                gw = DenseDwFn.apply(x, gy)
+        if ctx.has_b and _needed(ctx, 2) and gb is None:
             gb = _bias_grad(gy)
         return gx, gw, gb, None, None
 

@@ -397,3 +397,34 @@ def test_lrelu_gate_kernels_and_double_backward():
     o = A.LReluGateFn.apply(a, y, 0.2)
     (ga,) = torch.autograd.grad((o * o).sum(), a, create_graph=True)
     assert torch.allclose(ga, 2 * torch.where(y > 0, ref, ref * 0.2), atol=1e-6)
+
+
+def test_in_place_weight_grad_accumulation_matches_autograd():
+    """accumulate_weight_grads_in_place: conv / dense weight gradients written straight into the leaf's
+    .grad buffer equal autograd's accumulated ones (weight used twice, lrelu epilogues, bias)."""
+    from rafiki_amd.ops import autograd as A
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(8, 8, 8, 32, generator=g).to(DEV)
+    base_w = torch.randn(48, 3, 3, 32, generator=g).to(DEV) * 0.05
+    base_d = torch.randn(16, 8 * 8 * 48, generator=g).to(DEV) * 0.01
+    b = torch.zeros(48, device=DEV)
+
+    def grads(in_place):
+        w = torch.nn.Parameter(base_w.clone())
+        wd = torch.nn.Parameter(base_d.clone())
+        bb = torch.nn.Parameter(b.clone())
+        w.grad, wd.grad, bb.grad = torch.zeros_like(w), torch.zeros_like(wd), torch.zeros_like(bb)
+        y1 = A.conv2d(x, w.reshape(48, -1), bb, lrelu=0.2)
+        y2 = A.conv2d(x * 0.5, w.reshape(48, -1), bb, lrelu=0.2)
+        z = A.dense((y1 + y2).reshape(8, -1), wd, None)
+        ctx = A.accumulate_weight_grads_in_place() if in_place else contextlib.nullcontext()
+        with ctx:
+            z.square().mean().backward()
+        torch.cuda.synchronize()
+        return w.grad.clone(), wd.grad.clone(), bb.grad.clone()
+
+    import contextlib
+    a = grads(False)
+    c = grads(True)
+    for u, v in zip(a, c):
+        assert frob(v, u) < 1e-6, frob(v, u)
