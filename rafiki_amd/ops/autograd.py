@@ -350,15 +350,17 @@ def resample_via_winograd(full_hw: int, channels: int) -> bool:
     16 / 4 MACs per low-res / full-res output and channel pair; conv3x3 at full resolution by F(4x4,3x3)
     does 2.25 per full-res pixel — 1.8x fewer MFMA cycles for the down conv, 1.8x fewer for the up conv
     — at the price of one full-resolution activation round trip (upscale / box-filter pass).  On the
-    32x32x512 PG-GAN layers the resampling convs were a third of the lod-0 step
-    (profiles/pg_gan_lod0_f32_kernels_r3.txt).  RAFIKI_PGGAN_RESAMPLE = auto (Winograd on maps >= 16 with
-    >= 64 channels) | direct | wino."""
-    mode = os.environ.get('RAFIKI_PGGAN_RESAMPLE', 'auto')
-    if mode == 'direct':
-        return False
+    32x32x512 PG-GAN layers the resampling convs are a third of the lod-0 step
+    (profiles/pg_gan_lod0_f32_kernels_r3_direct.txt), yet measured end to end the Winograd route was
+    slower (lod 0: 73.0 vs 71.3 ms per D+G round, profiles/pg_gan_bench_r3e.jsonl): the direct gathers
+    run at high MFMA utilisation and the full-resolution round trips cost more than the saved MACs.
+    RAFIKI_PGGAN_RESAMPLE = direct (default) | wino | auto (Winograd on maps >= 16 with >= 64 channels)."""
+    mode = os.environ.get('RAFIKI_PGGAN_RESAMPLE', 'direct')
     if mode == 'wino':
         return S.WINO and S.WINO4 and full_hw % 4 == 0 and channels % 8 == 0
-    return S.WINO and S.WINO4 and full_hw >= 16 and full_hw % 4 == 0 and channels >= 64 and channels % 8 == 0
+    if mode == 'auto':
+        return S.WINO and S.WINO4 and full_hw >= 16 and full_hw % 4 == 0 and channels >= 64 and channels % 8 == 0
+    return False
 
 
 def upscale_conv2d(x, w, b=None, *, wb=None, lrelu=None):

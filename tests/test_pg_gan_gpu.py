@@ -234,7 +234,9 @@ def test_graphed_rounds_match_eager():
             o.skip_flag = torch.zeros(1, dtype=torch.int32, device=DEV)
         rng = TrialRng(m.device, 11)
         acc = torch.zeros(6, device=DEV)
-        level = torch.randint(0, 256, (256, 1, 4, 4), dtype=torch.uint8, device=DEV)
+        # the same reals in every run (a global-RNG draw here made the runs differ, not the kernels)
+        level = torch.randint(0, 256, (256, 1, 4, 4), dtype=torch.uint8,
+                              generator=torch.Generator().manual_seed(7)).to(DEV)
         labels = torch.zeros((256, 0), device=DEV)
         graphs = GraphedRounds(graphed)
         for _ in range(5):
@@ -249,7 +251,9 @@ def test_graphed_rounds_match_eager():
         frob(ge2, ge), frob(de2, de), frob(gt, ge), frob(dt, de)))
     print('graphed vs eager frob G {:.2e} D {:.2e} acc rel {:.2e}'.format(frob(g1, ge), frob(d1, de),
                                                                           rel_err(a1, ae)))
-    # fp32, same kernels, same RNG stream
+    # fp32, same kernels, same data and RNG stream: the kernels are deterministic (no float atomics on
+    # this path), so eager reruns agree bitwise and the replayed graph matches to round-off
+    assert frob(ge2, ge) <= 1e-6 and frob(de2, de) <= 1e-6
     assert frob(g1, ge) <= 1e-5 and frob(d1, de) <= 1e-5
     assert rel_err(a1, ae) < 1e-4
 
