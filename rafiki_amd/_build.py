@@ -104,12 +104,30 @@ def build_pyext(verbose: bool = False) -> Path | None:
     return PYLIST_LIB
 
 
+TOOLS_SRC = ROOT / "csrc" / "tools"
+
+
+def build_tools(verbose: bool = False) -> list:
+    """``csrc/tools/*.cpp`` -> executables in ``_native/`` (benchmark load generators)."""
+    out = []
+    NATIVE_DIR.mkdir(parents=True, exist_ok=True)
+    for src in sorted(TOOLS_SRC.glob("*.cpp")):
+        exe = NATIVE_DIR / src.stem
+        if _stale(exe, [src]):
+            tmp = exe.with_suffix(".tmp")
+            _run([CXX, *CXX_FLAGS, src, "-o", tmp], verbose)
+            os.replace(tmp, exe)
+        out.append(exe)
+    return out
+
+
 def build(verbose: bool = False) -> None:
     if shutil.which(HIPCC) is None and not Path(HIPCC).exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
     build_kernels(verbose=verbose)
     build_runtime(verbose=verbose)
     build_pyext(verbose=verbose)
+    build_tools(verbose=verbose)
 
 
 if __name__ == "__main__":

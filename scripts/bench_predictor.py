@@ -24,7 +24,8 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def build_models(k, device, classes=10):
@@ -118,11 +119,28 @@ def http_bench(pred, rng, args, server='fast'):
     batch = rng.integers(0, 256, (128, 32, 32, 3), dtype=np.uint8)
     buf = io.BytesIO()
     np.save(buf, batch, allow_pickle=False)
-    body = buf.getvalue()
+    body = npy_body = buf.getvalue()
+
+    httpload = os.path.join(ROOT, 'rafiki_amd', '_native', 'httpload')
 
     def run(kind, procs, threads, seconds=4.0):
-        """Load from separate client processes (a load generator sharing the server's GIL would
-        measure itself)."""
+        """Load from outside the server's process: the native closed-loop generator (csrc/tools/
+        httpload.cpp, ~microseconds per request) when built, else Python client processes (a load
+        generator sharing the server's GIL would measure itself)."""
+        if os.path.exists(httpload):
+            import subprocess
+            import tempfile
+            body = json.dumps({'query': one}).encode() if kind == 'json1' else npy_body
+            with tempfile.NamedTemporaryFile(suffix='.body') as bf:
+                bf.write(body)
+                bf.flush()
+                r = subprocess.run([httpload, '127.0.0.1', str(port), '/predict' if kind == 'json1' else
+                                    '/predict_batch_npy', bf.name, str(procs * threads), str(min(4, procs)),
+                                    str(seconds)], capture_output=True, text=True, timeout=seconds + 60)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            per = 1 if kind == 'json1' else 128
+            return {'qps': round(d['qps'] * per, 1), 'p50_ms': d['p50_ms'], 'p99_ms': d['p99_ms'],
+                    'errors': d['errors'], 'client': 'httpload'}
         import multiprocessing as mproc
         ctx = mproc.get_context('spawn')
         q = ctx.Queue()
@@ -158,6 +176,7 @@ def main():
     ap.add_argument('--replicas', type=int, default=1)
     ap.add_argument('--skip-http', action='store_true')
     ap.add_argument('--flask', action='store_true', help='also measure the Flask app')
+    ap.add_argument('--skip-http-asyncio', action='store_true')
     ap.add_argument('--out', default='')
     args = ap.parse_args()
     from rafiki_amd.ops import _lib
@@ -196,7 +215,8 @@ def main():
     # real HTTP: the predictor's Flask app on a local port, concurrent clients
     if not args.skip_http:
         res['http_native'] = http_bench(pred, rng, args, 'native')
-        res['http_asyncio'] = http_bench(pred, rng, args, 'fast')
+        if not args.skip_http_asyncio:
+            res['http_asyncio'] = http_bench(pred, rng, args, 'fast')
         if args.flask:
             res['http_flask'] = http_bench(pred, rng, args, 'flask')
     # dynamic batcher under concurrent single-query clients
