@@ -40,7 +40,7 @@ import torch.nn.functional as TF
 
 from ..ops import f32 as S
 from ..ops import functional as F
-from ..ops.graphs import capture as _capture
+from ..ops.graphs import capture as _capture, device_sync as _device_sync
 from .flat import FlatAdam, FlatParams, FlatSGD, init_const, init_kaiming
 
 VGG_SMALL_CFG = (64, 64, 'M', 128, 128, 'M', 256, 256, 'M', 512, 512, 'M')
@@ -630,7 +630,7 @@ class ConvNetEngine:
         g = torch.cuda.CUDAGraph()
         with _capture(g):
             self._train_step_gpu(self._static_x, self._static_y)
-        torch.cuda.synchronize()
+        _device_sync(self.device)
         self.flat.master.copy_(snap[0])
         self.flat.sync_bf16()
         self.running.copy_(snap[1])
@@ -685,7 +685,7 @@ class ConvNetEngine:
         g = torch.cuda.CUDAGraph()
         with _capture(g):
             body()
-        torch.cuda.synchronize()
+        _device_sync(self.device)
         self.flat.master.copy_(snap[0])
         self.flat.sync_bf16()
         self.running.copy_(snap[1])

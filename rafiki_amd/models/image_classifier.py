@@ -20,6 +20,7 @@ import torch
 from ..engine.convnet import ConvNetEngine, default_dtype
 from ..model import BaseModel, dataset_utils, logger
 from ..parallel.context import current as trial_context
+from ..ops.graphs import device_sync
 from ..utils import faults
 
 
@@ -132,7 +133,7 @@ class NativeImageClassifier(BaseModel):
             faults.maybe_fail('crash', epoch=epoch, rank=ctx.rank)
             epoch += 1
         if eng.device.type == 'cuda':
-            torch.cuda.synchronize(eng.device)
+            device_sync(eng.device)
         tm['loop'] = time.perf_counter() - t_loop
         if eng.device.type == 'cuda':
             logger.log(hbm_peak_bytes=int(torch.cuda.max_memory_allocated(eng.device)))

@@ -57,7 +57,7 @@ from rafiki_amd.engine.convnet import default_dtype
 from rafiki_amd.engine.flat import FlatAdam, FlatParams, init_const, init_normal
 from rafiki_amd.model import BaseModel, CategoricalKnob, FixedKnob, FloatKnob, IntegerKnob, logger
 from rafiki_amd.ops import autograd as A
-from rafiki_amd.ops.graphs import capture as _capture
+from rafiki_amd.ops.graphs import capture as _capture, device_sync
 from rafiki_amd.parallel.context import current as trial_context
 
 
@@ -464,7 +464,7 @@ class GraphedRounds:
             fn()
             return
         g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize()
+        device_sync()
         if self.collectives:
             # opt-in path (see the RAFIKI_PGGAN_GRAPH_COLLECTIVES note in PgGan.train): give the process
             # group's watchdog ~3 poll periods to retire the eager rounds' completed works before the

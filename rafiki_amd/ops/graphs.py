@@ -28,6 +28,17 @@ def quiesced():
         yield
 
 
+def device_sync(device=None):
+    """``torch.cuda.synchronize`` that never overlaps another thread's capture.  On ROCm a device-wide
+    synchronize walks every stream of the device, including one that another thread is capturing
+    into, and that invalidates the capture whatever its error mode (measured: an inline trainer's
+    end-of-loop synchronize failed with hipErrorStreamCaptureUnsupported and the concurrent trainer's
+    capture died in its next launch).  Captures hold LOCK for their whole duration, so taking it
+    here serialises the two."""
+    with LOCK:
+        torch.cuda.synchronize(device)
+
+
 _depth = [0, False]   # [nesting depth of capture() in this process, gc enabled before the outermost]
 
 

@@ -80,3 +80,24 @@ def test_quiesced_waits_for_an_open_capture(fake_graph):
         order.append('teardown')
     t.join()
     assert order == ['capture-end', 'teardown']
+
+
+def test_device_sync_waits_for_an_open_capture(fake_graph, monkeypatch):
+    """A device-wide synchronize invalidates another thread's open capture on ROCm, so the
+    trainers' synchronize goes through graphs.device_sync, which waits for the capture to end."""
+    order = []
+    entered = threading.Event()
+    monkeypatch.setattr(torch.cuda, 'synchronize', lambda device=None: order.append('sync'))
+
+    def capturer():
+        with graphs.capture(object()):
+            entered.set()
+            time.sleep(0.2)
+            order.append('capture-end')
+
+    t = threading.Thread(target=capturer)
+    t.start()
+    entered.wait(5)
+    graphs.device_sync()
+    t.join()
+    assert order == ['capture-end', 'sync']
