@@ -23,6 +23,15 @@
 //   * the accumulator layout puts one output channel per lane and 16 pixels in registers, so BN
 //     statistics are 16 in-register adds + one lane swap, and stores are 2 x 128-B rows per
 //     instruction.
+// X6 = true (tile code + 16): the same kernel with the products on the bf16 matrix cores at fp32
+// accuracy.  Every fp32 fragment value is split after its LDS read into three bf16 pieces,
+// x = hi + mid + lo (each the round-to-nearest bf16 of the remaining residual; the subtractions are
+// exact), and a 16-deep k chunk takes SIX v_mfma_f32_32x32x16_bf16 — hi*hi, hi*mid, mid*hi, hi*lo,
+// lo*hi, mid*mid — into the same fp32 accumulators.  The dropped terms (mid*lo, lo*mid, lo*lo) are
+// below 2^-25 of |x*y| and the pieces represent x to 2^-26, so every product is fp32-accurate
+// (below the unit roundoff of the fp32 accumulation that follows, which is unchanged): at the bf16
+// MFMA rate (16x the f32 one) six products cost 6/16 of the v_mfma_f32_32x32x2_f32 cycles.  The
+// error against fp64 is measured in tests/test_x6_gpu.py and profiles/ (equal to the f32 MFMA's).
 // Epilogues (runtime flags: the epilogue runs once per tile after K/32 x 4096 MFMA cycles, so its
 // VALU is noise): bias, ReLU / leaky-ReLU, ReLU gate (dense dX), BN statistics (fp64 atomic slots),
 // FLAG_BNB / FLAG_BNP (data-gradient into a BN+ReLU [+2x2 max-pool] layer: mask + BN-backward sums),
@@ -346,6 +355,32 @@ RK_DEV void s_group_sched() {
   __builtin_amdgcn_sched_group_barrier(0x002, 256, 0);  // leftover VALU after the MFMAs
 }
 
+// x = hi + mid + lo for 8 fp32 values (two 4-value fragments): bf16 round-to-nearest of x, then of
+// the residuals (x - hi and x - hi - mid are exact in fp32)
+RK_DEV void split3(const f32x4& v0, const f32x4& v1, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = e < 4 ? v0[e] : v1[e - 4];
+    const bf16 h = (bf16)x;
+    const float r = x - (float)h;
+    const bf16 m = (bf16)r;
+    hi[e] = h;
+    mid[e] = m;
+    lo[e] = (bf16)(r - (float)m);
+  }
+}
+
+RK_DEV f32x16 mfma6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh, const bf16x8& bm,
+                    const bf16x8& bl, f32x16 c) {
+  // small terms first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+}
+
 // accumulator register r of a 32x32 block: row (r&3) + 8(r>>2) + 4h, column lane&31
 RK_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -431,7 +466,7 @@ RK_DEV void s_epilogue(const SgParams& p, f32x16 (&acc)[MI][NI], int mbase, int 
 }
 
 // Workgroup = WGM x WGN waves, each owning (32*MI) x (32*NI) outputs: block tile BM x BN.
-template <int WGM, int WGN, int MI, int NI, int AM, int BMD, int NST, bool GRP = false>
+template <int WGM, int WGN, int MI, int NI, int AM, int BMD, int NST, bool GRP = false, bool X6 = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p) {
   constexpr bool GR = GRP || AM == SM_KIN_CONVG;  // grid = groups x splits x tiles
   constexpr int NW = WGM * WGN;
@@ -516,6 +551,33 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
     // LDS read instructions per group
     constexpr int RA = A.KIN ? MI : (MI == 2 ? 4 : 4 * MI), RB = B.KIN ? NI : (NI == 2 ? 4 : 4 * NI);
     constexpr int DA = BM / (8 * NW), DB = BN / (8 * NW);              // DMA instructions per wave
+    if constexpr (X6) {
+      // two 16-deep chunks per K-tile; chunk c = k-groups 2c, 2c+1: lane half h supplies
+      // k = 16c + {4h..4h+3, 8+4h..8+4h+3} of A and B alike (the MFMA sums over matched k-slots)
+#pragma unroll
+      for (int c = 0; c < SBK / 16; ++c) {
+        f32x4 a0[MI], a1[MI], b0[NI], b1[NI];
+        load_frags(A, As, wm * WMT, 2 * c, lane, a0);
+        load_frags(A, As, wm * WMT, 2 * c + 1, lane, a1);
+        load_frags(B, Bs, wn * WNT, 2 * c, lane, b0);
+        load_frags(B, Bs, wn * WNT, 2 * c + 1, lane, b1);
+        if (c == 0 && !(p.dbg & 1)) {
+          A.issue(p, nxt, kt + NST - 1, p.K, p.lda, wid, more);
+          B.issue(p, nxt + ABYTES, kt + NST - 1, p.K, p.ldb, wid, more);
+        }
+        bf16x8 ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) split3(b0[j], b1[j], bh[j], bm[j], bl[j]);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma6(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
+      }
+      st = st + 1 == NST ? 0 : st + 1;
+      continue;
+    }
     f32x4 a[2][MI], b[2][NI];
     load_frags(A, As, wm * WMT, 0, lane, a[0]);
     load_frags(B, Bs, wn * WNT, 0, lane, b[0]);
@@ -558,15 +620,21 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
 }
 
 template <int WGM, int WGN, int MI, int NI, int AM, int BMD, bool GRP = false>
-int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
+int s_launch(const SgParams& p, int nst, int splits, hipStream_t st, bool x6) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
   const int tiles = rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN);
   dim3 grid(tiles * splits * ((GRP || AM == SM_KIN_CONVG) ? p.groups : 1));
   if (nst == 3) {
-    if constexpr (WGM * WGN == 4)  // 3-stage rings only for the 4-wave tiles (8-wave ones fill LDS at 2)
-      hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3, GRP>), grid, dim3(64 * WGM * WGN), 0, st, p);
-    else
+    if constexpr (WGM * WGN == 4) {  // 3-stage rings only for the 4-wave tiles (8-wave ones fill LDS at 2)
+      if (x6)
+        hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3, GRP, true>), grid, dim3(64 * WGM * WGN), 0, st, p);
+      else
+        hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 3, GRP>), grid, dim3(64 * WGM * WGN), 0, st, p);
+    } else {
       return RK_EUNSUPPORTED;
+    }
+  } else if (x6) {
+    hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 2, GRP, true>), grid, dim3(64 * WGM * WGN), 0, st, p);
   } else {
     hipLaunchKernelGGL((sgemm_kernel<WGM, WGN, MI, NI, AM, BMD, 2, GRP>), grid, dim3(64 * WGM * WGN), 0, st, p);
   }
@@ -579,18 +647,19 @@ int s_launch(const SgParams& p, int nst, int splits, hipStream_t st) {
 // BIG = false instantiates only tiles 0-3 (dense layers, the general conv gather).
 template <int AM, int BMD, bool BIG, bool GRP = false>
 int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t st) {
-  switch (tile) {
-    case 0: return s_launch<2, 2, 2, 2, AM, BMD, GRP>(p, nst, splits, st);
-    case 1: return s_launch<2, 2, 2, 1, AM, BMD, GRP>(p, nst, splits, st);
-    case 2: return s_launch<2, 2, 1, 2, AM, BMD, GRP>(p, nst, splits, st);
-    case 3: return s_launch<2, 2, 1, 1, AM, BMD, GRP>(p, nst, splits, st);
+  const bool x6 = tile >= 16;  // tile code + 16: the split-bf16 (X6) K loop
+  switch (tile & 15) {
+    case 0: return s_launch<2, 2, 2, 2, AM, BMD, GRP>(p, nst, splits, st, x6);
+    case 1: return s_launch<2, 2, 2, 1, AM, BMD, GRP>(p, nst, splits, st, x6);
+    case 2: return s_launch<2, 2, 1, 2, AM, BMD, GRP>(p, nst, splits, st, x6);
+    case 3: return s_launch<2, 2, 1, 1, AM, BMD, GRP>(p, nst, splits, st, x6);
   }
   if constexpr (BIG) {
-    switch (tile) {
-      case 4: return s_launch<4, 1, 2, 2, AM, BMD>(p, nst, splits, st);
-      case 5: return s_launch<4, 2, 2, 2, AM, BMD>(p, nst, splits, st);
-      case 6: return s_launch<2, 4, 2, 2, AM, BMD>(p, nst, splits, st);
-      case 7: return s_launch<1, 4, 2, 2, AM, BMD>(p, nst, splits, st);
+    switch (tile & 15) {
+      case 4: return s_launch<4, 1, 2, 2, AM, BMD>(p, nst, splits, st, x6);
+      case 5: return s_launch<4, 2, 2, 2, AM, BMD>(p, nst, splits, st, x6);
+      case 6: return s_launch<2, 4, 2, 2, AM, BMD>(p, nst, splits, st, x6);
+      case 7: return s_launch<1, 4, 2, 2, AM, BMD>(p, nst, splits, st, x6);
     }
   }
   return RK_EUNSUPPORTED;
@@ -602,7 +671,8 @@ int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t 
 // B = weights [N][K]; the data gradient is kind 0 on dy with rk_swt-transposed weights), 2 conv weight
 // gradient (A = dy [K = pixels][M = Cout] K-outer, B = x gathered [K = pixels][N = taps*C]),
 // 3 dense A·Bᵀ (A [M][K], B [N][K]), 4 dense dX A·B (A [M][K], B [K][N]), 5 dense dW Aᵀ·B
-// (A [K][M], B [K][N]).  tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64.  nst: LDS ring stages (2, 3).
+// (A [K][M], B [K][N]).  tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64 (+16: the X6 split-bf16 K loop).
+// nst: LDS ring stages (2, 3).
 // splits > 1: fp32 slabs out + split * slabStride (combine with rk_reduce_slabs / rk_sreduce_epi).
 // flags: SF_* above; stats = fp64 slots [slotMask+1][2][N] (zeroed by the caller).
 extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float* B, float* C, const float* bias,
@@ -610,7 +680,9 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
                         int ldc, int H, int W, int Cch, int taps, int splits, long long slabStride, int flags,
                         float alpha, float slope, long long bytesA, long long bytesB, void* stream) {
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 7) return RK_EBADARG;
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 7 ||
+      tile > 23)
+    return RK_EBADARG;
   if (taps != 1 && taps != 9) return RK_EBADARG;
   const bool conv = kind == 0 || kind == 2;
   // 16-B chunks: K-inner operands need K % 4 == 0 (and 16-B aligned rows); K-outer ones need the
@@ -671,7 +743,9 @@ extern "C" int rk_sgemm_g(int kind, int tile, int nst, const float* A, const flo
                           float slope, long long bytesA, long long bytesB, void* stream) {
   if (kind != 6 && kind != 7) return RK_EBADARG;
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 3) return RK_EBADARG;
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 3 ||
+      tile > 19)
+    return RK_EBADARG;
   if (ntaps < 1 || ntaps > 16 || groups < 1 || groups > 4 || (stride != 1 && stride != 2) || (os != 1 && os != 2))
     return RK_EBADARG;
   if (kind == 7 && groups != 1) return RK_EBADARG;
@@ -718,7 +792,9 @@ extern "C" int rk_sgemm_grp(int kind, int tile, int nst, const float* A, const f
                             long long gstrideBias, void* stream) {
   if (kind != 0 && kind != 3) return RK_EBADARG;
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 3) return RK_EBADARG;
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 3 ||
+      tile > 19)
+    return RK_EBADARG;
   if (groups < 1 || gstrideA < 0 || gstrideB < 0 || gstrideO < 0 || gstrideBias < 0) return RK_EBADARG;
   if (taps != 1 && taps != 9) return RK_EBADARG;
   if (K % 4 || lda % 4 || ldb % 4) return RK_EUNSUPPORTED;

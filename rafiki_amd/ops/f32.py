@@ -29,6 +29,18 @@ F_RELU, F_BIAS, F_STATS, F_GATE, F_ACCUM, F_LRELU, F_BNB, F_BNP = 1, 2, 4, 8, 16
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 64), (256, 128), (128, 256), (64, 256)]
 _NST3 = (0, 1, 2, 3, 4, 7)
 NUM_CU = 256
+# tile code + X6: the split-bf16 K loop of rk_sgemm (fp32-accurate products on the bf16 MFMA: every
+# fp32 operand value = three bf16 pieces, six v_mfma_f32_32x32x16_bf16 per 16-deep chunk; see
+# sgemm.hip).  RAFIKI_X6=0 keeps every GEMM on v_mfma_f32_32x32x2_f32.
+X6 = 16
+USE_X6 = os.environ.get('RAFIKI_X6', '1') != '0'
+
+
+def tile_dims(t: int):
+    """(BM, BN) of a tile code (X6 codes included)."""
+    return TILES[t & 15]
+
+
 # RAFIKI_SGEMM_CFG="tile,nst" pins every sgemm launch (A/B runs without the tuner)
 _PIN = tuple(int(v) for v in os.environ['RAFIKI_SGEMM_CFG'].split(',')) if os.environ.get('RAFIKI_SGEMM_CFG') else None
 
@@ -115,6 +127,8 @@ def _cands(M, N, splittable=False, K=0, big=False):
                     c = (t, nst, s_eff)
                     if c not in out:
                         out.append(c)
+    if USE_X6:
+        out += [(t + X6, nst, s) for (t, nst, s) in out]
     return out
 
 
@@ -294,7 +308,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
     # the split-K configs fill the chip: lead with the best-filling heuristic one
     split = [c for c in cands if c[2] > 1]
     if split:
-        cands = [max(split, key=lambda c: min(cdiv(M, TILES[c[0]][0]) * cdiv(N, TILES[c[0]][1]) * c[2],
+        cands = [max(split, key=lambda c: min(cdiv(M, tile_dims(c[0])[0]) * cdiv(N, tile_dims(c[0])[1]) * c[2],
                                               2 * NUM_CU))] + cands
     wcands = _wino_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
     w4cands = _wino4_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
@@ -1194,7 +1208,7 @@ def s2_wgrad(x, g, *, out=None):
     cands = _cands(M, N, splittable=True, K=K)
     split = [c for c in cands if c[2] > 1]
     if split:
-        cands = [max(split, key=lambda c: min(cdiv(M, TILES[c[0]][0]) * cdiv(N, TILES[c[0]][1]) * c[2],
+        cands = [max(split, key=lambda c: min(cdiv(M, tile_dims(c[0])[0]) * cdiv(N, tile_dims(c[0])[1]) * c[2],
                                               2 * NUM_CU))] + cands
     run(_pick(('s2w', M, N, K, H, Wd, Ci), cands, run))
     return out
@@ -1265,7 +1279,7 @@ def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=
         sgemm_grp(kind, A, B, slab, M, N, K, lda, ldb, N, G, gsa, N * K, M * N, 0, tile=tile, nst=nst, splits=s,
                   slab_stride=G * M * N, **geo)
         sreduce_epi(slab, G * M, N, out.view(G * M, N), bias=bias, act=act, slope=slope, bias_rows=M)
-    cands = [c for c in _cands(M * G, N, splittable=N % 4 == 0, K=K) if c[0] < 4]
+    cands = [c for c in _cands(M * G, N, splittable=N % 4 == 0, K=K) if (c[0] & 15) < 4]
     if extra is not None:
         cands.extend(getattr(extra, 'cfgs', WINO_CFGS))
     run(_pick(key, cands, run))
