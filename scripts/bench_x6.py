@@ -113,10 +113,29 @@ def main():
                 wz = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, device=dev, requires_grad=True)
                 (gw,) = torch.autograd.grad(TF.conv2d(xd, wz, padding=1), wz, dy.double().permute(0, 3, 1, 2))
                 ref = gw.permute(0, 2, 3, 1).reshape(cout, 9 * cin)
+            # halo-tiled X6 conv (fwd / dgrad)
+            tx, cfgx, ex = float('inf'), None, None
+            if pas != 'wgrad' and S.xconv_ok(hw, hw, cin if pas == 'fwd' else cout, cout if pas == 'fwd' else cin, M):
+                if pas == 'fwd':
+                    planes = S.xconv_planes(w)
+                    xin, oshape = x, (B, hw, hw, cout)
+                else:
+                    wfull = wt.reshape(cin, 3, 3, cout).permute(3, 1, 2, 0).flip(1, 2).contiguous()  # [cout][3][3][cin]
+                    planes = S.xconv_planes(wfull, dgrad=True)
+                    xin, oshape = dy, (B, hw, hw, cin)
+                ox = torch.empty(oshape, device=dev)
+                xc = S._xconv_cands(hw, hw, xin.shape[-1], oshape[-1], M)
+                tx, cfgx = best(xc, lambda cfg: (lambda: S.xconv(xin, planes, cfg=S.XCONV - cfg[0], out=ox)), a.reps)
+                if cfgx is not None:
+                    S.xconv(xin, planes, cfg=S.XCONV - cfgx[0], out=ox)
+                    torch.cuda.synchronize()
+                    ex = rel(ox, ref)
             rec = {'layer': li, 'pass': pas, 'cin': cin, 'cout': cout, 'hw': hw,
                    'f32_us': round(t32, 2), 'f32_cfg': cfg32, 'f32_tflops': round(flop / t32 / 1e6, 1),
                    'x6_us': round(t6, 2), 'x6_cfg': cfg6, 'x6_tflops': round(flop / t6 / 1e6, 1),
-                   'speedup': round(t32 / t6, 3), 'err_f32': rel(r32, ref), 'err_x6': rel(r6, ref)}
+                   'speedup': round(t32 / t6, 3), 'err_f32': rel(r32, ref), 'err_x6': rel(r6, ref),
+                   'xconv_us': round(tx, 2), 'xconv_cfg': cfgx, 'err_xconv': ex,
+                   'xconv_tflops': round(flop / tx / 1e6, 1) if tx < float('inf') else None}
             print(json.dumps(rec), flush=True)
             if fout:
                 fout.write(json.dumps(rec) + '\n')
