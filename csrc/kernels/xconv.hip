@@ -44,7 +44,7 @@ RK_DEV void x_barrier() {
 }
 
 // IH > 0: an item is IMG whole IH x W images (small maps); IH == 0: TH = BM / W rows of one image
-template <int BM, int BN, int W, int IH>
+template <int BM, int BN, int WGM, int W, int IH>
 __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
   constexpr int TH = IH ? IH : BM / W;
   constexpr int IMG = IH ? BM / ((IH ? IH : 1) * W) : 1;
@@ -53,14 +53,15 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
   constexpr int P_BYTES = LP * 4 * 1024;
   constexpr int B_BYTES = 3 * BN * 64;        // 3 planes x BN rows x 32 bf16
   constexpr int LB = 3 * BN / 64;             // B DMA instructions per wave per tap
-  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
+  constexpr int WGN = 4 / WGM;                // 4 waves: WGM x WGN
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   static_assert(MI >= 1 && NI >= 1 && BM % W == 0 && (IH == 0 || BM % (IH * W) == 0), "tile");
   static_assert(LB * 256 == 3 * BN * 4, "B tile must split evenly over the waves");
   __shared__ __attribute__((aligned(16))) char smem[2 * P_BYTES + 3 * B_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid - (wid / WGN) * WGN;
   const int C = p.C, N = p.N, K = p.K;   // K = C (reduction channels of one tap)
   const int NCC = C / XKC;
   const int tilesN = N / BN;
@@ -173,31 +174,34 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
   s_epilogue<MI, NI, false, false>(p, acc, m0 + wm * WM, n0 + wn * WN, lane, 0, 0, p.out, p.bias);
 }
 
-template <int BM, int BN, int W>
+template <int BM, int BN, int WGM, int W>
 int x_launch_w(const SgParams& p, hipStream_t st) {
   const int items = (p.M / BM) * (p.N / BN);
   if (BM >= p.H * W) {
     if (BM % (p.H * W)) return RK_EUNSUPPORTED;
     switch (p.H) {  // whole images per item
-      case 4: if constexpr (BM % (4 * W) == 0) { hipLaunchKernelGGL((xconv_kernel<BM, BN, W, 4>), dim3(items), dim3(256), 0, st, p); break; } return RK_EUNSUPPORTED;
-      case 8: if constexpr (BM % (8 * W) == 0) { hipLaunchKernelGGL((xconv_kernel<BM, BN, W, 8>), dim3(items), dim3(256), 0, st, p); break; } return RK_EUNSUPPORTED;
+      case 4: if constexpr (BM % (4 * W) == 0) { hipLaunchKernelGGL((xconv_kernel<BM, BN, WGM, W, 4>), dim3(items), dim3(256), 0, st, p); break; } return RK_EUNSUPPORTED;
+      case 8: if constexpr (BM % (8 * W) == 0) { hipLaunchKernelGGL((xconv_kernel<BM, BN, WGM, W, 8>), dim3(items), dim3(256), 0, st, p); break; } return RK_EUNSUPPORTED;
+      case 16: if constexpr (BM % (16 * W) == 0) { hipLaunchKernelGGL((xconv_kernel<BM, BN, WGM, W, 16>), dim3(items), dim3(256), 0, st, p); break; } return RK_EUNSUPPORTED;
       default: return RK_EUNSUPPORTED;
     }
   } else {
     if (p.H % (BM / W)) return RK_EUNSUPPORTED;
-    hipLaunchKernelGGL((xconv_kernel<BM, BN, W, 0>), dim3(items), dim3(256), 0, st, p);
+    hipLaunchKernelGGL((xconv_kernel<BM, BN, WGM, W, 0>), dim3(items), dim3(256), 0, st, p);
   }
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WGM = 2>
 int x_launch(const SgParams& p, hipStream_t st) {
   switch (p.W) {
-    case 4: return x_launch_w<BM, BN, 4>(p, st);
-    case 8: return x_launch_w<BM, BN, 8>(p, st);
-    case 16: return x_launch_w<BM, BN, 16>(p, st);
-    case 32: return x_launch_w<BM, BN, 32>(p, st);
+    case 4:  // 16 whole 4x4 images per 256-pixel item: two patches would not fit in LDS
+      if constexpr (BM <= 128) return x_launch_w<BM, BN, WGM, 4>(p, st);
+      return RK_EUNSUPPORTED;
+    case 8: return x_launch_w<BM, BN, WGM, 8>(p, st);
+    case 16: return x_launch_w<BM, BN, WGM, 16>(p, st);
+    case 32: return x_launch_w<BM, BN, WGM, 32>(p, st);
   }
   return RK_EUNSUPPORTED;
 }
@@ -280,7 +284,9 @@ __global__ __launch_bounds__(256) void xconv_wt_multi_kernel(const float* __rest
 
 // y = conv3x3(x, w) (stride 1, pad 1): x [Nb][H][W][C] fp32 NHWC, wp = the bf16 planes [3][9][N][C] of
 // rk_xconv_weights (forward set: N = Cout; data-gradient set of the transposed conv: N = Cin, C = Cout),
-// out [Nb][H][W][N] fp32.  cfg bit 0: 64-pixel items (else 128), bit 1: 64-channel items (else 128).
+// out [Nb][H][W][N] fp32.  cfg 0-3: bit 0 64-pixel items (else 128), bit 1 64-channel items (else 128),
+// 2 x 2 waves; cfg 4: 256 x 64 items on 4 x 1 waves (a wave = 64 px x 64 channels: 4x less weight
+// traffic per FLOP than 64 x 64 items, the B ring three 1.5k-cycle steps deep).
 // flags: SF_BIAS / SF_RELU / SF_LRELU / SF_STATS (fp64 slots [slotMask+1][2][N]) / SF_BNB / SF_BNP
 // (gate = the gated layer's pre-BN input, bias = its BN scale [N] then shift [N]) / SF_ACCUM.
 // Square maps of 4, 8, 16 or 32; C % 32 == 0; N % (item channels) == 0.
@@ -288,9 +294,9 @@ extern "C" int rk_xconv(int cfg, const float* x, const void* wp, float* out, con
                         int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
                         long long bytesA, long long bytesB, void* stream) {
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (Nb <= 0 || C <= 0 || N <= 0 || cfg < 0 || cfg > 3) return RK_EBADARG;
+  if (Nb <= 0 || C <= 0 || N <= 0 || cfg < 0 || cfg > 4) return RK_EBADARG;
   if (H != W || (W != 4 && W != 8 && W != 16 && W != 32) || C % XKC) return RK_EUNSUPPORTED;
-  const int BM = (cfg & 1) ? 64 : 128, BN = (cfg & 2) ? 64 : 128;
+  const int BM = cfg == 4 ? 256 : (cfg & 1) ? 64 : 128, BN = cfg == 4 ? 64 : (cfg & 2) ? 64 : 128;
   const long long M = (long long)Nb * H * W;
   if (M % BM || N % BN || M >= (1ll << 30)) return RK_EUNSUPPORTED;
   if (flags & ~(SF_BIAS | SF_RELU | SF_LRELU | SF_STATS | SF_BNB | SF_BNP | SF_ACCUM)) return RK_EUNSUPPORTED;
@@ -313,6 +319,7 @@ extern "C" int rk_xconv(int cfg, const float* x, const void* wp, float* out, con
     case 1: return x_launch<64, 128>(p, st);
     case 2: return x_launch<128, 64>(p, st);
     case 3: return x_launch<64, 64>(p, st);
+    case 4: return x_launch<256, 64, 4>(p, st);   // 4 x 1 waves of 64 px x 64 channels
   }
   return RK_EBADARG;
 }

@@ -539,10 +539,17 @@ def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=N
 WINO4_PT = -14   # pre-transformed F(4x4) conv: cfg = (-14, sgemm tile, sgemm nst)
 
 
+# largest map the pre-transformed paths are offered on: 8 with the f32 GEMM (they lost on 16x16 maps,
+# profiles/wgrad4_variants_r3.jsonl); with the X6 GEMM loop their batched GEMM is 1.1-1.3x faster, so the
+# tuner also weighs them on 16x16 and 32x32 maps
+PT_MAX_HW = 32 if USE_X6 else 8
+
+
 def wino4_pt_ok(H, W, C, N):
     """Deep maps (<= 8x8), where the fused kernels re-transform each input window once per output-channel
     block: there the transform-once + grouped-GEMM path is a tuner candidate."""
-    return (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= 8 and W <= 8 and C % 4 == 0 and C >= 32
+    return (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= PT_MAX_HW and W <= PT_MAX_HW and C % 4 == 0
+            and C >= 32
             and N >= 32)
 
 
@@ -659,7 +666,7 @@ def _wino4_pt_cands(Nb, H, W, Cout, Cin):
     maps of <= 8x8, where the fused kernels' redundant per-block transforms dominate (VGG-small batch
     256: 8x8x256x256 84.8 vs 101.7 us, 4x4x512x512 76.4 vs 96.3; it loses on 16x16 maps,
     profiles/wgrad4_variants_r3.jsonl)."""
-    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= 8 and W <= 8 and Cin % 4 == 0
+    if not (WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and H <= PT_MAX_HW and W <= PT_MAX_HW and Cin % 4 == 0
             and Cout % 4 == 0 and Cin >= 32 and Cout >= 32):
         return []
     T = Nb * (H // 4) * (W // 4)
@@ -750,8 +757,8 @@ def wino_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
     return out
 
 
-XCONV = -30   # autotune tile ids -30 .. -33: the halo-tiled X6 conv (xconv.hip), cfg bits = 30 + (-id)
-XCONV_CFGS = tuple((XCONV - c, 0, 1) for c in range(4)) if USE_X6 else ()
+XCONV = -30   # autotune tile ids -30 .. -34: the halo-tiled X6 conv (xconv.hip), cfg = XCONV - id
+XCONV_ITEMS = ((128, 128), (64, 128), (128, 64), (64, 64), (256, 64))   # (pixels, channels) per cfg
 
 
 def xconv_ok(H: int, W: int, C: int, N: int, M: int) -> bool:
@@ -763,9 +770,8 @@ def _xconv_cands(H, W, C, N, M):
     if not xconv_ok(H, W, C, N, M):
         return []
     out = []
-    for c in range(4):
-        bm, bn = (64 if c & 1 else 128), (64 if c & 2 else 128)
-        if M % bm or N % bn:
+    for c, (bm, bn) in enumerate(XCONV_ITEMS):
+        if M % bm or N % bn or (bm > H * W and bm % (H * W)) or (bm == 256 and W == 4):
             continue
         out.append((XCONV - c, 0, 1))
     return out

@@ -8,5 +8,5 @@ python -c "
 import json
 for l in open('gpurun_out/xc/layers.jsonl'):
     r=json.loads(l); print(r['layer'],r['pass'],'f32',r['f32_us'],'x6',r['x6_us'],'xconv',r['xconv_us'],r['xconv_cfg'],r['err_xconv'])"
-RAFIKI_AUTOTUNE_LOG=$PWD/gpurun_out/xc/tune.jsonl timeout -k 10 300 python -u bench.py --trials 0 --probe-trials 0 --no-serving > gpurun_out/xc/bench.log 2>&1 || exit $?
-tail -1 gpurun_out/xc/bench.log | cut -c1-300
+true
+
