@@ -12,9 +12,9 @@
 // taps out of it (the tap is a constant shift of the patch pixel a lane reads).  The weights are
 // split ONCE per weight update by xconv_wt_kernel into bf16 planes [3][9][N][K] (K permuted inside
 // each 16-group so a lane's eight k values are one 16-byte read) and stream per (tap, chunk) through
-// a 3-stage LDS-DMA ring; only the activation fragments are split in registers (2 of every 6*MI*NI
-// MFMAs' operands).  Patches are double buffered: the next chunk's patch is in flight during the nine
-// taps of the current one.  One barrier per tap.
+// a 3-stage LDS-DMA ring; the activation patch is split once per block and chunk (register-staged:
+// loaded during the previous chunk's nine taps, split and written at the chunk boundary), so the
+// tap loop is ds_read_b128 + MFMA only.  One barrier per tap.
 //
 // The data gradient is the same kernel on dy with the flipped, transposed weight planes (xconv_wt
 // writes both sets), so the BN-backward epilogues (FLAG_BNB / FLAG_BNP) of sgemm_core.h apply as is.
@@ -26,7 +26,8 @@ namespace {
 
 #include "sgemm_core.h"
 
-constexpr int XKC = 32;  // input channels per chunk (one 128-byte patch row per pixel)
+constexpr int XKC = 32;  // input channels per chunk (one 64-byte row per pixel and plane)
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 RK_DEV void x_dma16(__amdgpu_buffer_rsrc_t r, char* dst, int off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, off, 0, 0, 0);
@@ -44,20 +45,31 @@ RK_DEV void x_barrier() {
 }
 
 // IH > 0: an item is IMG whole IH x W images (small maps); IH == 0: TH = BM / W rows of one image
+//
+// LDS images (every ds_read_b128 conflict-free for the four 16-lane groups of that instruction,
+// MI355X_MICROARCH.md §LDS, whatever the tap shift of the start pixel):
+//   patch: 3 bf16 planes x NPP pixels x 64 B (32 channels); 16-B piece q of pixel pp (channels
+//          {16(q>>1) + 4(q&1) .. +3} U {16(q>>1) + 8 + 4(q&1) .. +3}: a lane's eight k values) stored at
+//          q ^ ((pp >> 2) & 3);
+//   B:     3 planes x BN rows x 64 B, piece q of row n at q ^ ((n >> 2) & 3).
+// The patch is split into its planes ONCE per block and chunk: its fp32 chunk is loaded into registers
+// during the nine taps of the previous chunk and written (split, ds_write_b64) at the chunk boundary.
 template <int BM, int BN, int WGM, int W, int IH>
 __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
   constexpr int TH = IH ? IH : BM / W;
   constexpr int IMG = IH ? BM / ((IH ? IH : 1) * W) : 1;
   constexpr int PC = W + 2, PIMG = (TH + 2) * PC, NPP = IMG * PIMG;
-  constexpr int LP = (NPP * 8 + 255) / 256;   // patch DMA instructions per wave
-  constexpr int P_BYTES = LP * 4 * 1024;
+  constexpr int LQ = (NPP * 8 + 255) / 256;   // 16-B patch loads per thread (4 fp32 channels each)
+  constexpr int PLANE = NPP * 64;             // bytes per patch plane
+  constexpr int P_BYTES = 3 * PLANE;
   constexpr int B_BYTES = 3 * BN * 64;        // 3 planes x BN rows x 32 bf16
   constexpr int LB = 3 * BN / 64;             // B DMA instructions per wave per tap
   constexpr int WGN = 4 / WGM;                // 4 waves: WGM x WGN
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   static_assert(MI >= 1 && NI >= 1 && BM % W == 0 && (IH == 0 || BM % (IH * W) == 0), "tile");
   static_assert(LB * 256 == 3 * BN * 4, "B tile must split evenly over the waves");
-  __shared__ __attribute__((aligned(16))) char smem[2 * P_BYTES + 3 * B_BYTES];
+  static_assert(2 * LB + LQ <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[P_BYTES + 3 * B_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -75,18 +87,21 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
   const __amdgpu_buffer_rsrc_t rA = s_rsrc(p.A, p.bytesA);
   const __amdgpu_buffer_rsrc_t rB = s_rsrc(p.B, p.bytesB);
 
-  // ---- patch DMA lane constants (byte offset of chunk 0, or SOOB)
-  unsigned poff[LP];
+  // ---- patch load slots: thread t, load q -> slot t + 256 q = (pixel, 4-channel chunk c); source byte
+  // offset of chunk 0 (or SOOB) and the LDS byte offset (plane 0) of its 8-byte half-piece
+  unsigned poff[LQ];
+  int pdst[LQ];
 #pragma unroll
-  for (int q = 0; q < LP; ++q) {
-    const int slot = (wid * LP + q) * 64 + lane;
-    const int pp = slot >> 3;
-    const int lc = (slot & 7) ^ (pp & 7);
+  for (int q = 0; q < LQ; ++q) {
+    const int slot = tid + 256 * q;
+    const int pp = slot >> 3, c = slot & 7;
     const int img = pp / PIMG, rem = pp - img * PIMG;
     const int pr = rem / PC, pc = rem - pr * PC;
     const int row = r0 - 1 + pr;
     const bool ok = pp < NPP && pc >= 1 && pc <= W && (unsigned)row < (unsigned)p.H && (IH == 0 || (pr >= 1 && pr <= TH));
-    poff[q] = ok ? (unsigned)((((img0 + img) * p.H + row) * W + pc - 1) * C) * 4u + (unsigned)lc * 16u : SOOB;
+    poff[q] = ok ? (unsigned)((((img0 + img) * p.H + row) * W + pc - 1) * C) * 4u + (unsigned)c * 16u : SOOB;
+    const int piece = 2 * (c >> 2) + (c & 1), half = (c >> 1) & 1;
+    pdst[q] = pp < NPP ? pp * 64 + ((piece ^ ((pp >> 2) & 3)) << 4) + half * 8 : -1;
   }
   // ---- B DMA lane constants: planes [3][9][N][K] bf16, rows n0.., 64-byte k-chunk pieces
   unsigned boff[LB];
@@ -95,7 +110,7 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
     const int slot = (wid * LB + q) * 64 + lane;
     const int pl = slot / (BN * 4), rem = slot - pl * (BN * 4);
     const int n = rem >> 2;
-    const int pc = (rem & 3) ^ ((n >> 1) & 3);
+    const int pc = (rem & 3) ^ ((n >> 2) & 3);
     boff[q] = ((unsigned)(pl * 9) * (unsigned)N * (unsigned)K + (unsigned)(n0 + n) * (unsigned)K) * 2u + (unsigned)pc * 16u;
   }
   const unsigned tstep = (unsigned)N * (unsigned)K * 2u;  // bytes between taps of one plane
@@ -108,15 +123,36 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
     ppb[i] = img * PIMG + (rem / W + 1) * PC + (rem % W) + 1;
   }
 
-  auto issue_patch = [&](int cc, int buf) {
-    char* dst = smem + buf * P_BYTES + wid * LP * 1024;
+  u32x4 pv[LQ];
+  auto load_patch = [&](int cc) {
 #pragma unroll
-    for (int j = 0; j < LP; ++j) x_dma16(rA, dst + j * 1024, (int)(poff[j] == SOOB ? SOOB : poff[j] + (unsigned)cc * 128u));
+    for (int q = 0; q < LQ; ++q)
+      pv[q] = __builtin_amdgcn_raw_buffer_load_b128(rA, (int)(poff[q] == SOOB ? SOOB : poff[q] + (unsigned)cc * 128u), 0, 0);
+  };
+  auto write_patch = [&]() {   // split the registers' fp32 chunk into the three bf16 planes
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+      if (pdst[q] < 0) continue;
+      const f32x4 v = __builtin_bit_cast(f32x4, pv[q]);
+      bf16x4 ph, pm, pl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16 a = (bf16)v[e];
+        const float r = v[e] - (float)a;
+        const bf16 b = (bf16)r;
+        ph[e] = a;
+        pm[e] = b;
+        pl[e] = (bf16)(r - (float)b);
+      }
+      *(bf16x4*)(smem + pdst[q]) = ph;
+      *(bf16x4*)(smem + PLANE + pdst[q]) = pm;
+      *(bf16x4*)(smem + 2 * PLANE + pdst[q]) = pl;
+    }
   };
   auto issue_b = [&](int s, int stage) {  // step s = cc * 9 + tap
     const int cc = s / 9, tap = s - cc * 9;
     const unsigned src = (unsigned)tap * tstep + (unsigned)cc * 64u;
-    char* dst = smem + 2 * P_BYTES + stage * B_BYTES + wid * LB * 1024;
+    char* dst = smem + P_BYTES + stage * B_BYTES + wid * LB * 1024;
 #pragma unroll
     for (int j = 0; j < LB; ++j) x_dma16(rB, dst + j * 1024, (int)(boff[j] + src));
   };
@@ -130,23 +166,24 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int S = NCC * 9;
-  issue_patch(0, 0);
+  load_patch(0);
   issue_b(0, 0);
-  if (S > 1) issue_b(1, 1);
+  issue_b(1, 1);
+  x_wait_vmcnt<2 * LB>();
+  write_patch();
   for (int cc = 0; cc < NCC; ++cc) {
     const bool last = cc == NCC - 1;
-    const char* pt = smem + (cc & 1) * P_BYTES;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int s = cc * 9 + tap;
-      // DMAs issued after B(s): B(s+1), plus the next patch when it went out at tap 0 of this chunk
+      // loads issued after B(s): B(s+1), plus the next patch when it went out at tap 0 of this chunk
       if (last && tap == 8) x_wait_vmcnt<0>();
-      else if ((tap == 1 || tap == 2) && !last) x_wait_vmcnt<LB + LP>();
+      else if ((tap == 1 || tap == 2) && !last) x_wait_vmcnt<LB + LQ>();
       else x_wait_vmcnt<LB>();
       x_barrier();
       if (s + 2 < S) issue_b(s + 2, (s + 2) % 3);
-      if (tap == 0 && !last) issue_patch(cc + 1, (cc + 1) & 1);
-      const char* lb = smem + 2 * P_BYTES + (s % 3) * B_BYTES;
+      if (tap == 0 && !last) load_patch(cc + 1);
+      const char* lb = smem + P_BYTES + (s % 3) * B_BYTES;
       const int shift = ((tap * 11) >> 5) * PC + (tap - 3 * ((tap * 11) >> 5)) - PC - 1;  // (dy, dx) in -1..1
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -154,14 +191,15 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int pp = ppb[i] + shift;
-          const f32x4 v0 = *(const f32x4*)(pt + pp * 128 + (((4 * ks + h) ^ (pp & 7)) << 4));
-          const f32x4 v1 = *(const f32x4*)(pt + pp * 128 + (((4 * ks + 2 + h) ^ (pp & 7)) << 4));
-          split3(v0, v1, ah[i], am[i], al[i]);
+          const int o = pp * 64 + (((2 * ks + h) ^ ((pp >> 2) & 3)) << 4);
+          ah[i] = *(const bf16x8*)(smem + o);
+          am[i] = *(const bf16x8*)(smem + PLANE + o);
+          al[i] = *(const bf16x8*)(smem + 2 * PLANE + o);
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int n = wn * WN + j * 32 + (lane & 31);
-          const int o = n * 64 + (((2 * ks + h) ^ ((n >> 1) & 3)) << 4);
+          const int o = n * 64 + (((2 * ks + h) ^ ((n >> 2) & 3)) << 4);
           const bf16x8 bh = *(const bf16x8*)(lb + o);
           const bf16x8 bm = *(const bf16x8*)(lb + BN * 64 + o);
           const bf16x8 bl = *(const bf16x8*)(lb + 2 * BN * 64 + o);
@@ -169,6 +207,13 @@ __global__ __launch_bounds__(256, 1) void xconv_kernel(const SgParams p) {
           for (int i = 0; i < MI; ++i) acc[i][j] = mfma6(ah[i], am[i], al[i], bh, bm, bl, acc[i][j]);
         }
       }
+    }
+    if (!last) {
+      // the next chunk's patch: loaded before B(s+1), B(s+2) of taps 7, 8; every wave is done with
+      // this chunk's patch once it passes the barrier
+      x_wait_vmcnt<2 * LB>();
+      x_barrier();
+      write_patch();
     }
   }
   s_epilogue<MI, NI, false, false>(p, acc, m0 + wm * WM, n0 + wn * WN, lane, 0, 0, p.out, p.bias);
@@ -196,7 +241,7 @@ int x_launch_w(const SgParams& p, hipStream_t st) {
 template <int BM, int BN, int WGM = 2>
 int x_launch(const SgParams& p, hipStream_t st) {
   switch (p.W) {
-    case 4:  // 16 whole 4x4 images per 256-pixel item: two patches would not fit in LDS
+    case 4:  // 16 whole 4x4 images per 256-pixel item: the patch registers would spill
       if constexpr (BM <= 128) return x_launch_w<BM, BN, WGM, 4>(p, st);
       return RK_EUNSUPPORTED;
     case 8: return x_launch_w<BM, BN, WGM, 8>(p, st);
