@@ -1058,97 +1058,127 @@ extern "C" int rk_wino4_wgrad(const float* dy, const float* x, float* out, int N
 // redundant transform work dominates, and here it is done once.
 namespace {
 
+// one thread per (tile, 4-channel group): float4 loads / stores (coalesced across the channel groups of
+// a tile), 32-bit index math (the launchers check T * C < 2^31); the transforms run componentwise
 __global__ __launch_bounds__(256) void w4pt_dy_kernel(const float* __restrict__ dy, float* __restrict__ m, int H,
-                                                      int W, int C, int TW, int THW, long long total, long long T) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int c = (int)(i % C);
-  const long long t = i / C;
-  const int n = (int)(t / THW), r = (int)(t - (long long)n * THW), ty = r / TW;
+                                                      int W, int C, int TW, int THW, int total4, int T) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int C4 = C >> 2;
+  const int c4 = i % C4, t = i / C4;
+  const int n = t / THW, r = t - n * THW, ty = r / TW;
   const int oy = 4 * ty, ox = 4 * (r - ty * TW);
-  const float* src = dy + (((long long)n * H + oy) * W + ox) * C + c;
-  float g[16];
+  const float* src = dy + ((n * H + oy) * W + ox) * C + 4 * c4;
+  f32x4 g[16];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) g[a * 4 + b] = src[((long long)a * W + b) * C];
-  float mm[6][4];
+    for (int b = 0; b < 4; ++b) g[a * 4 + b] = *(const f32x4*)(src + (a * W + b) * C);
+  f32x4 res[36];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float o[6];
-    a6(g[j], g[4 + j], g[8 + j], g[12 + j], o);
+  for (int e = 0; e < 4; ++e) {
+    float mm[6][4];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) mm[a][j] = o[a];
+    for (int j = 0; j < 4; ++j) {
+      float o[6];
+      a6(g[j][e], g[4 + j][e], g[8 + j][e], g[12 + j][e], o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) mm[a][j] = o[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      float o[6];
+      a6(mm[a][0], mm[a][1], mm[a][2], mm[a][3], o);
+#pragma unroll
+      for (int b = 0; b < 6; ++b) res[a * 6 + b][e] = o[b];
+    }
   }
-  float* dst = m + t * C + c;
+  float* dst = m + t * C + 4 * c4;
+  const int ps = T * C;
 #pragma unroll
-  for (int a = 0; a < 6; ++a) {
-    float o[6];
-    a6(mm[a][0], mm[a][1], mm[a][2], mm[a][3], o);
-#pragma unroll
-    for (int b = 0; b < 6; ++b) dst[(long long)(a * 6 + b) * T * C] = o[b];
-  }
+  for (int q = 0; q < 36; ++q) *(f32x4*)(dst + q * ps) = res[q];
 }
 
 __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x, float* __restrict__ v, int H,
-                                                     int W, int C, int TW, int THW, long long total, long long T) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int c = (int)(i % C);
-  const long long t = i / C;
-  const int n = (int)(t / THW), r = (int)(t - (long long)n * THW), ty = r / TW;
+                                                     int W, int C, int TW, int THW, int total4, int T) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int C4 = C >> 2;
+  const int c4 = i % C4, t = i / C4;
+  const int n = t / THW, r = t - n * THW, ty = r / TW;
   const int oy = 4 * ty - 1, ox = 4 * (r - ty * TW) - 1;
-  float d[36];
+  f32x4 d[36];
 #pragma unroll
   for (int a = 0; a < 6; ++a)
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
       const int yy = oy + a, xx = ox + b;
-      d[a * 6 + b] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? x[(((long long)n * H + yy) * W + xx) * C + c] : 0.f;
+      d[a * 6 + b] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                         ? *(const f32x4*)(x + ((n * H + yy) * W + xx) * C + 4 * c4)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-  for (int b = 0; b < 6; ++b) {
-    float o[6];
-    bt6(d[b], d[6 + b], d[12 + b], d[18 + b], d[24 + b], d[30 + b], o);
+  for (int b = 0; b < 6; ++b)
 #pragma unroll
-    for (int a = 0; a < 6; ++a) d[a * 6 + b] = o[a];
-  }
-  float* dst = v + t * C + c;
+    for (int e = 0; e < 4; ++e) {
+      float o[6];
+      bt6(d[b][e], d[6 + b][e], d[12 + b][e], d[18 + b][e], d[24 + b][e], d[30 + b][e], o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) d[a * 6 + b][e] = o[a];
+    }
+  float* dst = v + t * C + 4 * c4;
+  const int ps = T * C;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    float o[6];
-    bt6(d[a * 6 + 0], d[a * 6 + 1], d[a * 6 + 2], d[a * 6 + 3], d[a * 6 + 4], d[a * 6 + 5], o);
+    f32x4 o4[6];
 #pragma unroll
-    for (int b = 0; b < 6; ++b) dst[(long long)(a * 6 + b) * T * C] = o[b];
+    for (int e = 0; e < 4; ++e) {
+      float o[6];
+      bt6(d[a * 6 + 0][e], d[a * 6 + 1][e], d[a * 6 + 2][e], d[a * 6 + 3][e], d[a * 6 + 4][e], d[a * 6 + 5][e], o);
+#pragma unroll
+      for (int b = 0; b < 6; ++b) o4[b][e] = o[b];
+    }
+#pragma unroll
+    for (int b = 0; b < 6; ++b) *(f32x4*)(dst + (a * 6 + b) * ps) = o4[b];
   }
 }
 
-// dU [36][Co][Ci] -> dW [Co][9][Ci] (+= with accumulate)
+// dU [36][Co][Ci] -> dW [Co][9][Ci] (+= with accumulate); one thread per (co, 4-channel group)
 __global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__ du, float* __restrict__ out, int Co,
                                                        int Ci, int accumulate) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long plane = (long long)Co * Ci;
-  if (i >= plane) return;
-  const int co = (int)(i / Ci), ci = (int)(i - (long long)co * Ci);
-  float tq[3][6];
+  const int i = blockIdx.x * 256 + threadIdx.x;   // 4-channel group index in [Co][Ci/4]
+  const int plane = Co * Ci;
+  if (i * 4 >= plane) return;
+  const int C4 = Ci >> 2;
+  const int co = i / C4, ci = 4 * (i - co * C4);
+  const float* src = du + co * Ci + ci;
+  f32x4 u[36];
 #pragma unroll
-  for (int b = 0; b < 6; ++b) {
-    float g[3];
-    gt6(du[(0 * 6 + b) * plane + i], du[(1 * 6 + b) * plane + i], du[(2 * 6 + b) * plane + i],
-        du[(3 * 6 + b) * plane + i], du[(4 * 6 + b) * plane + i], du[(5 * 6 + b) * plane + i], g);
+  for (int q = 0; q < 36; ++q) u[q] = *(const f32x4*)(src + q * plane);
+  float* o = out + co * 9 * Ci + ci;
+  f32x4 w[9];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) tq[ky][b] = g[ky];
-  }
-  float* o = out + (long long)co * 9 * Ci + ci;
+  for (int e = 0; e < 4; ++e) {
+    float tq[3][6];
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    float v[3];
-    gt6(tq[ky][0], tq[ky][1], tq[ky][2], tq[ky][3], tq[ky][4], tq[ky][5], v);
+    for (int b = 0; b < 6; ++b) {
+      float g[3];
+      gt6(u[b][e], u[6 + b][e], u[12 + b][e], u[18 + b][e], u[24 + b][e], u[30 + b][e], g);
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      float* d = o + (ky * 3 + kx) * Ci;
-      *d = accumulate ? *d + v[kx] : v[kx];
+      for (int ky = 0; ky < 3; ++ky) tq[ky][b] = g[ky];
     }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      float v[3];
+      gt6(tq[ky][0], tq[ky][1], tq[ky][2], tq[ky][3], tq[ky][4], tq[ky][5], v);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) w[ky * 3 + kx][e] = v[kx];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    f32x4* d = (f32x4*)(o + k * Ci);
+    *d = accumulate ? *d + w[k] : w[k];
   }
 }
 
@@ -1158,22 +1188,25 @@ __global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__
 extern "C" int rk_wino4_pt_transform(const float* dy, const float* x, float* m, float* v, int Nb, int H, int W,
                                      int Co, int Ci, void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0) return RK_EBADARG;
+  if ((Co & 3) || (Ci & 3)) return RK_EUNSUPPORTED;
   const int TW = W / 4, THW = (H / 4) * (W / 4);
   const long long T = (long long)Nb * THW;
-  const long long ty = T * Co, tx = T * Ci;
+  if (36 * T * Co >= (1ll << 31) || 36 * T * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const long long ty = T * Co / 4, tx = T * Ci / 4;
   hipLaunchKernelGGL(w4pt_dy_kernel, dim3((unsigned)((ty + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy, m, H,
-                     W, Co, TW, THW, ty, T);
+                     W, Co, TW, THW, (int)ty, (int)T);
   RK_LAUNCH_CHECK();
   hipLaunchKernelGGL(w4pt_x_kernel, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, v, H, W,
-                     Ci, TW, THW, tx, T);
+                     Ci, TW, THW, (int)tx, (int)T);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
 extern "C" int rk_wino4_pt_output(const float* du, float* out, int Co, int Ci, int accumulate, void* stream) {
   if (Co <= 0 || Ci <= 0) return RK_EBADARG;
-  const long long plane = (long long)Co * Ci;
-  hipLaunchKernelGGL(w4pt_out_kernel, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, (hipStream_t)stream, du,
+  if ((Ci & 3) || 36ll * Co * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const long long g4 = (long long)Co * Ci / 4;
+  hipLaunchKernelGGL(w4pt_out_kernel, dim3((unsigned)((g4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, du,
                      out, Co, Ci, accumulate);
   RK_LAUNCH_CHECK();
   return RK_OK;
@@ -1294,11 +1327,13 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
 // V = B^T x B of every 6x6 window: [36][T][C] (the x half of rk_wino4_pt_transform)
 extern "C" int rk_wino4_pt_input(const float* x, float* v, int Nb, int H, int W, int C, void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || C <= 0) return RK_EBADARG;
+  if (C & 3) return RK_EUNSUPPORTED;
   const int TW = W / 4, THW = (H / 4) * (W / 4);
   const long long T = (long long)Nb * THW;
-  const long long tx = T * C;
+  if (36 * T * C >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const long long tx = T * C / 4;
   hipLaunchKernelGGL(w4pt_x_kernel, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, v, H, W,
-                     C, TW, THW, tx, T);
+                     C, TW, THW, (int)tx, (int)T);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -195,7 +195,7 @@ def test_wino_weights_live_sets_and_on_demand_transform():
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(16, 8, 8, 64, 128), (32, 4, 4, 256, 128), (8, 16, 16, 32, 64),
                                             (64, 4, 4, 40, 36)])   # (16x16 works too; the tuner skips it)
-@pytest.mark.parametrize("tile", [0, 3])
+@pytest.mark.parametrize("tile", [0, 3, 16, 19])   # 16, 19: the X6 K loop
 def test_wino4_wgrad_pretransformed(N, H, W, Cin, Cout, tile):
     """Pre-transformed F(4x4) weight gradient (transform launch + 36-split sgemm + output transform)."""
     from rafiki_amd.ops import f32 as S
@@ -217,7 +217,7 @@ def test_wino4_wgrad_pretransformed(N, H, W, Cin, Cout, tile):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(8, 4, 4, 512, 512), (3, 8, 8, 256, 96), (16, 8, 8, 64, 128),
                                             (5, 4, 8, 40, 36)])
-@pytest.mark.parametrize("tile", [0, 3])
+@pytest.mark.parametrize("tile", [0, 3, 16, 19])   # 16, 19: the X6 K loop
 def test_wino4_conv_pretransformed_fwd_stats_bias_relu(N, H, W, Cin, Cout, tile):
     """Pre-transformed F(4x4) conv (input transform + 36-group sgemm + output transform) vs fp64."""
     from rafiki_amd.ops import f32 as S
