@@ -66,8 +66,16 @@ def lib_hash() -> str:
     return _ident['lib']
 
 
+# switches that change the candidate sets (not the kernels): a non-default setting tunes into its own
+# database file, so a pick made among more candidates is never replayed where they are switched off
+_CAND_SWITCHES = ('RAFIKI_X6', 'RAFIKI_XCONV', 'RAFIKI_PT_MAX_HW', 'RAFIKI_WINOGRAD', 'RAFIKI_WINOGRAD4',
+                  'RAFIKI_WINO_PIPE')
+
+
 def db_name() -> str:
-    return '{}-{}.json'.format(_arch(), lib_hash())
+    tag = ','.join('{}={}'.format(k, os.environ[k]) for k in _CAND_SWITCHES if k in os.environ)
+    suffix = '-' + hashlib.sha1(tag.encode()).hexdigest()[:8] if tag else ''
+    return '{}-{}{}.json'.format(_arch(), lib_hash(), suffix)
 
 
 def _path():

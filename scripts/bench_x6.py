@@ -115,7 +115,7 @@ def main():
                 ref = gw.permute(0, 2, 3, 1).reshape(cout, 9 * cin)
             # halo-tiled X6 conv (fwd / dgrad)
             tx, cfgx, ex = float('inf'), None, None
-            if pas != 'wgrad' and S.xconv_ok(hw, hw, cin if pas == 'fwd' else cout, cout if pas == 'fwd' else cin, M):
+            if pas != 'wgrad' and S.xconv_ok(hw, hw, cin if pas == 'fwd' else cout, cout if pas == 'fwd' else cin, M, True):
                 if pas == 'fwd':
                     planes = S.xconv_planes(w)
                     xin, oshape = x, (B, hw, hw, cout)
@@ -124,7 +124,7 @@ def main():
                     planes = S.xconv_planes(wfull, dgrad=True)
                     xin, oshape = dy, (B, hw, hw, cin)
                 ox = torch.empty(oshape, device=dev)
-                xc = S._xconv_cands(hw, hw, xin.shape[-1], oshape[-1], M)
+                xc = S._xconv_cands(hw, hw, xin.shape[-1], oshape[-1], M, True)
                 tx, cfgx = best(xc, lambda cfg: (lambda: S.xconv(xin, planes, cfg=S.XCONV - cfg[0], out=ox)), a.reps)
                 if cfgx is not None:
                     S.xconv(xin, planes, cfg=S.XCONV - cfgx[0], out=ox)

@@ -25,6 +25,7 @@ def _setup(monkeypatch, capturing=False):
     monkeypatch.setattr(S, '_s', lambda: None)
     monkeypatch.setattr(S, '_p', lambda t: None if t is None else t.data_ptr())   # host tensors are fine here
     monkeypatch.setattr(torch.cuda, 'is_current_stream_capturing', lambda: capturing)
+    monkeypatch.setattr(S, 'USE_XCONV', True)     # the X6 plane sets exist when the halo conv is a candidate
     shapes = [(64, 32), (16, 64), (40, 24)]
     arena = torch.zeros(sum(co * 9 * ci for co, ci in shapes) + 3)
     ws, off = [], 3
