@@ -454,6 +454,11 @@ int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t 
     case 1: return s_launch<2, 2, 2, 1, AM, BMD, GRP>(p, nst, splits, st, x6);
     case 2: return s_launch<2, 2, 1, 2, AM, BMD, GRP>(p, nst, splits, st, x6);
     case 3: return s_launch<2, 2, 1, 1, AM, BMD, GRP>(p, nst, splits, st, x6);
+    // few-wave tiles with 64 x 64 wave tiles (twice the MFMAs per split fragment of the 2x2-wave
+    // tiles: the X6 loop's split VALU per MFMA halves) for small grids of many groups
+    case 8: return s_launch<1, 1, 2, 2, AM, BMD, GRP>(p, nst, splits, st, x6);
+    case 9: return s_launch<2, 1, 2, 2, AM, BMD, GRP>(p, nst, splits, st, x6);
+    case 10: return s_launch<1, 2, 2, 2, AM, BMD, GRP>(p, nst, splits, st, x6);
   }
   if constexpr (BIG) {
     switch (tile & 15) {
@@ -472,7 +477,8 @@ int s_launch_tile(int tile, const SgParams& p, int nst, int splits, hipStream_t 
 // B = weights [N][K]; the data gradient is kind 0 on dy with rk_swt-transposed weights), 2 conv weight
 // gradient (A = dy [K = pixels][M = Cout] K-outer, B = x gathered [K = pixels][N = taps*C]),
 // 3 dense A·Bᵀ (A [M][K], B [N][K]), 4 dense dX A·B (A [M][K], B [K][N]), 5 dense dW Aᵀ·B
-// (A [K][M], B [K][N]).  tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64 (+16: the X6 split-bf16 K loop).
+// (A [K][M], B [K][N]).  tile: 0 128x128, 1 128x64, 2 64x128, 3 64x64 (2x2 waves), 8 64x64 (1 wave),
+// 9 128x64 (2x1), 10 64x128 (1x2); +16: the X6 split-bf16 K loop.
 // nst: LDS ring stages (2, 3).
 // splits > 1: fp32 slabs out + split * slabStride (combine with rk_reduce_slabs / rk_sreduce_epi).
 // flags: SF_* above; stats = fp64 slots [slotMask+1][2][N] (zeroed by the caller).
@@ -481,8 +487,8 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
                         int ldc, int H, int W, int Cch, int taps, int splits, long long slabStride, int flags,
                         float alpha, float slope, long long bytesA, long long bytesB, void* stream) {
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 7 ||
-      tile > 23)
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 10 ||
+      tile > 26)
     return RK_EBADARG;
   if (taps != 1 && taps != 9) return RK_EBADARG;
   const bool conv = kind == 0 || kind == 2;
@@ -544,8 +550,8 @@ extern "C" int rk_sgemm_g(int kind, int tile, int nst, const float* A, const flo
                           float slope, long long bytesA, long long bytesB, void* stream) {
   if (kind != 6 && kind != 7) return RK_EBADARG;
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 3 ||
-      tile > 19)
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 ||
+      ((tile & 15) > 3 && (tile & 15) < 8) || (tile & 15) > 10 || tile > 26)
     return RK_EBADARG;
   if (ntaps < 1 || ntaps > 16 || groups < 1 || groups > 4 || (stride != 1 && stride != 2) || (os != 1 && os != 2))
     return RK_EBADARG;
@@ -593,8 +599,8 @@ extern "C" int rk_sgemm_grp(int kind, int tile, int nst, const float* A, const f
                             long long gstrideBias, void* stream) {
   if (kind != 0 && kind != 3) return RK_EBADARG;
   if (bytesA <= 0 || bytesB <= 0 || bytesA >= (1ll << 31) || bytesB >= (1ll << 31)) return RK_EUNSUPPORTED;
-  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 3 ||
-      tile > 19)
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0 || (nst != 2 && nst != 3) || tile < 0 ||
+      ((tile & 15) > 3 && (tile & 15) < 8) || (tile & 15) > 10 || tile > 26)
     return RK_EBADARG;
   if (groups < 1 || gstrideA < 0 || gstrideB < 0 || gstrideO < 0 || gstrideBias < 0) return RK_EBADARG;
   if (taps != 1 && taps != 9) return RK_EBADARG;

@@ -26,8 +26,10 @@ KIND_CONV, KIND_WGRAD, KIND_DENSE, KIND_DENSE_DX, KIND_DENSE_DW = 0, 2, 3, 4, 5
 F_RELU, F_BIAS, F_STATS, F_GATE, F_ACCUM, F_LRELU, F_BNB, F_BNP = 1, 2, 4, 8, 16, 32, 512, 1024
 # block tiles (see rk_sgemm): 0-3 four-wave 2x2, 4 256x64 (4x1 waves), 5 256x128 / 6 128x256 (8 waves),
 # 7 64x256 (1x4).  Tiles 4-7 exist for the conv kinds with C % 32 == 0 and the weight gradient.
-TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 64), (256, 128), (128, 256), (64, 256)]
-_NST3 = (0, 1, 2, 3, 4, 7)
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 64), (256, 128), (128, 256), (64, 256),
+         (64, 64), (128, 64), (64, 128)]   # 8-10: 1- / 2-wave tiles of 64x64 wave tiles (X6 candidates)
+_NST3 = (0, 1, 2, 3, 4, 7, 8, 9, 10)
+_FEW_WAVE = (8, 9, 10)
 NUM_CU = 256
 # tile code + X6: the split-bf16 K loop of rk_sgemm (fp32-accurate products on the bf16 MFMA: every
 # fp32 operand value = three bf16 pieces, six v_mfma_f32_32x32x16_bf16 per 16-deep chunk; see
@@ -128,7 +130,15 @@ def _cands(M, N, splittable=False, K=0, big=False):
                     if c not in out:
                         out.append(c)
     if USE_X6:
-        out += [(t + X6, nst, s) for (t, nst, s) in out]
+        x6 = [(t + X6, nst, s) for (t, nst, s) in out if t < 4 or t >= 4]
+        # the few-wave 64x64-wave-tile shapes, X6 only (their point is the split VALU per MFMA)
+        for t in _FEW_WAVE:
+            bm, bn = TILES[t]
+            if (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N) > 1.3:
+                continue
+            for nst in (2, 3):
+                x6.append((t + X6, nst, 1))
+        out += x6
     return out
 
 
@@ -554,7 +564,8 @@ def wino4_pt_ok(H, W, C, N):
 
 
 WINO4_PT_CFGS = tuple((WINO4_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)) for t in (0, 1, 2, 3)
-                      for n in ((2, 3) if t in _NST3 else (2,)))
+                      for n in ((2, 3) if t in _NST3 else (2,))) + \
+    (tuple((WINO4_PT, t + X6, n) for t in _FEW_WAVE for n in (2, 3)) if USE_X6 else ())
 
 
 def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None,
@@ -673,7 +684,8 @@ def _wino4_pt_cands(Nb, H, W, Cout, Cin):
     if T % 32 or 36 * T * max(Cin, Cout) * 4 >= (1 << 31) or 36 * Cout * Cin * 4 > (512 << 20):
         return []
     return [(WINO4_WGRAD_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)) for t in (0, 1, 2, 3)
-            for n in ((2, 3) if t in _NST3 else (2,))]
+            for n in ((2, 3) if t in _NST3 else (2,))] + \
+        ([(WINO4_WGRAD_PT, t + X6, n) for t in _FEW_WAVE for n in (2, 3)] if USE_X6 else [])
 
 
 def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accumulate=False, tile=0, nst=2):
@@ -1384,7 +1396,7 @@ def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=
         sgemm_grp(kind, A, B, slab, M, N, K, lda, ldb, N, G, gsa, N * K, M * N, 0, tile=tile, nst=nst, splits=s,
                   slab_stride=G * M * N, **geo)
         sreduce_epi(slab, G * M, N, out.view(G * M, N), bias=bias, act=act, slope=slope, bias_rows=M)
-    cands = [c for c in _cands(M * G, N, splittable=N % 4 == 0, K=K) if (c[0] & 15) < 4]
+    cands = [c for c in _cands(M * G, N, splittable=N % 4 == 0, K=K) if (c[0] & 15) < 4 or (c[0] & 15) in _FEW_WAVE]
     if extra is not None:
         cands.extend(getattr(extra, 'cfgs', WINO_CFGS))
     run(_pick(key, cands, run))

@@ -29,7 +29,7 @@ def _both(run, ref):
     """run(tile) -> output tensor; returns (err f32 loop, err X6 loop) for tiles 0..3."""
     from rafiki_amd.ops import f32 as S
     out = []
-    for t in (0, 3):
+    for t in (0, 3, 8, 9, 10):   # 8-10: the 1- / 2-wave tiles
         e32 = rel(run(t), ref)
         e6 = rel(run(t + S.X6), ref)
         out.append((t, e32, e6))
