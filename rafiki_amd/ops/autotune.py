@@ -8,7 +8,7 @@ cached/heuristic configs are used, so captured graphs never contain tuning launc
 
 The cache is a node-wide tuning database (MIOpen's perf-db idea), keyed by what the timings depend on:
 
-* file ``<WORKDIR>/tune/<gfx arch>-<kernel library hash>.json`` (``RAFIKI_TUNE_CACHE`` overrides the
+* file ``<WORKDIR>/tune/<gfx arch>-<kernel source hash>.json`` (``RAFIKI_TUNE_CACHE`` overrides the
   path, ``RAFIKI_TUNE_CACHE=off`` keeps it in memory only).  A rebuilt kernel library or another GPU
   architecture starts a fresh file, so stale picks are never replayed;
 * every worker process of the node shares it: a miss re-reads the file if another rank wrote it
@@ -51,16 +51,33 @@ def _arch() -> str:
     return _ident['arch']
 
 
+_SRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), 'csrc',
+                        'kernels')
+
+
 def lib_hash() -> str:
-    """Content hash of the kernel library the picks were timed with (12 hex digits)."""
+    """Hash of the kernel library the picks were timed with (12 hex digits): of the kernel SOURCES when the
+    tree has them (hipcc output is not byte-reproducible — it embeds temporary file names — so a rebuild
+    of unchanged sources keeps its database), else of the library bytes."""
     if 'lib' not in _ident:
-        from ._lib import loaded_path as lib_path
         h = hashlib.sha1()
         try:
-            with open(lib_path(), 'rb') as f:
-                for chunk in iter(lambda: f.read(1 << 20), b''):
-                    h.update(chunk)
-            _ident['lib'] = h.hexdigest()[:12]
+            srcs = sorted(f for f in os.listdir(_SRC_DIR) if f.endswith(('.hip', '.h')))
+        except OSError:
+            srcs = []
+        try:
+            if srcs:
+                for f in srcs:
+                    h.update(f.encode())
+                    with open(os.path.join(_SRC_DIR, f), 'rb') as fh:
+                        h.update(fh.read())
+                _ident['lib'] = 's' + h.hexdigest()[:11]
+            else:
+                from ._lib import loaded_path as lib_path
+                with open(lib_path(), 'rb') as f:
+                    for chunk in iter(lambda: f.read(1 << 20), b''):
+                        h.update(chunk)
+                _ident['lib'] = h.hexdigest()[:12]
         except OSError:
             _ident['lib'] = 'nolib'
     return _ident['lib']
