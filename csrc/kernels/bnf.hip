@@ -10,6 +10,12 @@
 
 namespace {
 
+RK_DEV int rk_log2_dev(int v) { return (v > 0 && (v & (v - 1)) == 0) ? 31 - __builtin_clz(v) : -1; }
+
+// a / d for the launch-constant d (shift when d is a power of two: log2d >= 0); 32-bit index math
+// (the launchers check that every element offset fits in an int)
+RK_DEV int idiv(int a, int d, int log2d) { return log2d >= 0 ? a >> log2d : a / d; }
+
 RK_DEV float act_f(float z, int act, float slope) {
   return act == 1 ? fmaxf(z, 0.f) : act == 2 ? (z > 0.f ? z : z * slope) : z;
 }
@@ -65,10 +71,11 @@ __global__ __launch_bounds__(256) void bnf_fwd_kernel(const float* __restrict__ 
   __syncthreads();
   const int G = C >> 2;
   const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
-  const long long total = (long long)Nb * Ho * Wo * G;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int cg = (int)(i % G);
-    const long long pix = i / G;
+  const int lG = rk_log2_dev(G), lWo = rk_log2_dev(Wo), lHo = rk_log2_dev(Ho);
+  const int total = Nb * Ho * Wo * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = idiv(i, G, lG);
+    const int cg = i - pix * G;
     const int c = cg * 4;
     const f32x4 sc = *(const f32x4*)(s_sc + c), sh = *(const f32x4*)(s_sh + c);
     f32x4 o;
@@ -77,13 +84,13 @@ __global__ __launch_bounds__(256) void bnf_fwd_kernel(const float* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = act_f(v[e] * sc[e] + sh[e], act, slope);
     } else {
-      const int wo = (int)(pix % Wo);
-      const long long t = pix / Wo;
-      const int ho = (int)(t % Ho);
-      const long long n = t / Ho;
-      const long long b0 = ((n * H + 2 * ho) * W + 2 * wo) * C + c;
+      const int t = idiv(pix, Wo, lWo);
+      const int wo = pix - t * Wo;
+      const int n = idiv(t, Ho, lHo);
+      const int ho = t - n * Ho;
+      const int b0 = ((n * H + 2 * ho) * W + 2 * wo) * C + c;
       const f32x4 v0 = *(const f32x4*)(y + b0), v1 = *(const f32x4*)(y + b0 + C);
-      const f32x4 v2 = *(const f32x4*)(y + b0 + (long long)W * C), v3 = *(const f32x4*)(y + b0 + (long long)W * C + C);
+      const f32x4 v2 = *(const f32x4*)(y + b0 + W * C), v3 = *(const f32x4*)(y + b0 + W * C + C);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float a0 = act_f(v0[e] * sc[e] + sh[e], act, slope), a1 = act_f(v1[e] * sc[e] + sh[e], act, slope);
@@ -216,10 +223,11 @@ __global__ __launch_bounds__(256) void bnf_bwd_apply_kernel(const float* __restr
   // holds positions no (floor-mode) window covers: dz = 0 there, dy = B*y + Cc still has to be written
   const int Hc = POOL ? (H + 1) >> 1 : H, Wc = POOL ? (W + 1) >> 1 : W;
   const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
-  const long long total = (long long)Nb * Hc * Wc * G;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int cg = (int)(i % G);
-    const long long pix = i / G;
+  const int lG = rk_log2_dev(G), lWc = rk_log2_dev(Wc), lHc = rk_log2_dev(Hc);
+  const int total = Nb * Hc * Wc * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = idiv(i, G, lG);
+    const int cg = i - pix * G;
     const int c = cg * 4;
     const f32x4 a = *(const f32x4*)(kA + c), b = *(const f32x4*)(kB + c), cc = *(const f32x4*)(kC + c);
     const f32x4 sc = *(const f32x4*)(coeffs + 2 * C + c), sh = *(const f32x4*)(coeffs + 3 * C + c);
@@ -231,12 +239,12 @@ __global__ __launch_bounds__(256) void bnf_bwd_apply_kernel(const float* __restr
       for (int e = 0; e < 4; ++e) o[e] = a[e] * (d[e] * act_d(v[e] * sc[e] + sh[e], act, slope)) + b[e] * v[e] + cc[e];
       *(f32x4*)(dy + pix * C + c) = o;
     } else {
-      const int wc = (int)(pix % Wc);
-      const long long t = pix / Wc;
-      const int hc = (int)(t % Hc);
-      const long long n = t / Hc;
-      const long long b0 = ((n * H + 2 * hc) * W + 2 * wc) * C + c;
-      const long long offs[4] = {b0, b0 + C, b0 + (long long)W * C, b0 + (long long)W * C + C};
+      const int t = idiv(pix, Wc, lWc);
+      const int wc = pix - t * Wc;
+      const int n = idiv(t, Hc, lHc);
+      const int hc = t - n * Hc;
+      const int b0 = ((n * H + 2 * hc) * W + 2 * wc) * C + c;
+      const int offs[4] = {b0, b0 + C, b0 + W * C, b0 + W * C + C};
       if (hc < Ho && wc < Wo) {
         const f32x4 d = *(const f32x4*)(dout + ((n * Ho + hc) * Wo + wc) * C + c);
         f32x4 v[4], o[4];
@@ -445,6 +453,7 @@ extern "C" int rk_bnf_fwd(const float* y, const double* slots, int SL, double co
   if (slots && (!gamma || !beta || !coeffs)) return RK_EBADARG;
   if (!slots && (!scale || !shift)) return RK_EBADARG;
   const long long work = (long long)Nb * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
+  if ((long long)Nb * H * W * C >= (1ll << 31)) return RK_EUNSUPPORTED;   // 32-bit element offsets
   const dim3 grid(grid_cap(work, 2048));
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = 2 * (size_t)C * sizeof(float);
@@ -478,6 +487,7 @@ extern "C" int rk_bnf_bwd_apply(const float* dout, const float* y, const float* 
                                 float* dy, int Nb, int H, int W, int C, int pool, int act, float slope, void* stream) {
   if (C % 4 || C > BN_MAX_C || (pool && (H < 2 || W < 2))) return RK_EUNSUPPORTED;
   const long long work = (long long)Nb * (pool ? (H + 1) / 2 : H) * (pool ? (W + 1) / 2 : W) * (C / 4);
+  if ((long long)Nb * H * W * C >= (1ll << 31)) return RK_EUNSUPPORTED;   // 32-bit element offsets
   const dim3 grid(grid_cap(work, 2048));
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = 3 * (size_t)C * sizeof(float);
