@@ -88,3 +88,38 @@ def test_xconv_dgrad_bn_epilogues():
         torch.cuda.synchronize()
         assert rel(d1, d2) < 1e-5, mode
         assert rel(a1.sum(0), a2.sum(0)) < 1e-5, mode
+
+
+@pytest.mark.parametrize("mode", ["fwd", "bnb", "bnp"])
+def test_xconv_writes_only_its_outputs(mode):
+    """Canaries around the output and the fp64 statistic slots: nothing outside them changes."""
+    from rafiki_amd.ops import f32 as S
+    N, H, Cin, Cout = 8, 8, 64, 128
+    g = torch.Generator().manual_seed(11)
+    if mode == 'fwd':
+        x = torch.randn(N, H, H, Cin, generator=g).to(DEV)
+        planes = S.xconv_planes((torch.randn(Cout, 3, 3, Cin, generator=g) * 0.05).to(DEV))
+        No = Cout
+    else:
+        x = torch.randn(N, H, H, Cout, generator=g).to(DEV)
+        planes = S.xconv_planes((torch.randn(Cout, 3, 3, Cin, generator=g) * 0.05).to(DEV), dgrad=True)
+        No = Cin
+    n_out = N * H * H * No
+    big = torch.full((n_out + 2 * 4096,), 7.0, device=DEV)
+    out = big[4096:4096 + n_out].view(N, H, H, No)
+    SL = S.bn_slots(No)
+    sbig = torch.full((SL * 2 * No + 2 * 512,), 3.0, dtype=torch.float64, device=DEV)
+    stats = sbig[512:512 + SL * 2 * No].view(SL, 2, No)
+    stats.zero_()
+    for cfg in [c[0] for c in S._xconv_cands(H, H, x.shape[-1], No, N * H * H, force=True)]:
+        if mode == 'fwd':
+            S.xconv(x, planes, cfg=S.XCONV - cfg, out=out, stats=stats)
+        else:
+            coeffs = torch.stack([torch.zeros(No), torch.ones(No), torch.randn(No, generator=g),
+                                  torch.randn(No, generator=g)]).to(DEV)
+            ys = (N, H, H, No) if mode == 'bnb' else (N, 2 * H, 2 * H, No)
+            y = torch.randn(*ys, generator=g).to(DEV)
+            S.xconv(x, planes, cfg=S.XCONV - cfg, out=out, **{mode: (y, coeffs, stats)})
+        torch.cuda.synchronize()
+        assert bool((big[:4096] == 7.0).all()) and bool((big[4096 + n_out:] == 7.0).all()), cfg
+        assert bool((sbig[:512] == 3.0).all()) and bool((sbig[512 + SL * 2 * No:] == 3.0).all()), cfg
