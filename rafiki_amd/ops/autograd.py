@@ -331,16 +331,44 @@ def _box4(w3):
     return wp[:, 1:, 1:] + wp[:, :-1, 1:] + wp[:, 1:, :-1] + wp[:, :-1, :-1]
 
 
+_BOX_MATS = {}
+
+
+def _box_mat(device, flip: bool, scale: float):
+    """[16, 9] 0/1 (x scale) matrix of _box4: W4[a][b] = sum of w3[ky][kx] over ky in {a-1, a}, kx in {b-1, b}
+    (flip: of the 180-degree-rotated kernel)."""
+    key = (str(device), flip, scale)
+    m = _BOX_MATS.get(key)
+    if m is None:
+        m = torch.zeros(16, 9)
+        for a in range(4):
+            for b in range(4):
+                for ky in (a - 1, a):
+                    for kx in (b - 1, b):
+                        if 0 <= ky < 3 and 0 <= kx < 3:
+                            q = ky * 3 + kx
+                            m[a * 4 + b, 8 - q if flip else q] = scale
+        m = _BOX_MATS[key] = m.to(device)
+    return m
+
+
 def down_weights(w, cin):
-    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cout, 16*Cin] of conv3x3 + 2x2 box downscale."""
+    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cout, 16*Cin] of conv3x3 + 2x2 box downscale: one batched
+    GEMM ([16, 9] box matrix x every output channel's [9, Cin] taps) forward and one backward, instead of
+    pad + four shifted adds + scale (and their adjoints) per call."""
     co = w.shape[0]
-    return (_box4(w.reshape(co, 3, 3, cin)) * 0.25).reshape(co, 16 * cin)
+    if w.device.type != 'cuda':
+        return (_box4(w.reshape(co, 3, 3, cin)) * 0.25).reshape(co, 16 * cin)
+    return torch.matmul(_box_mat(w.device, False, 0.25), w.reshape(co, 9, cin)).reshape(co, 16 * cin)
 
 
 def up_weights(w, cin):
-    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cin, 16*Cout] whose adjoint S2T is upscale2d + conv3x3."""
+    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cin, 16*Cout] whose adjoint S2T is upscale2d + conv3x3 (the
+    tap flip folded into the box matrix; one batched GEMM + one transposing copy)."""
     co = w.shape[0]
-    return _box4(w.reshape(co, 3, 3, cin).flip(1, 2)).permute(3, 1, 2, 0).reshape(cin, 16 * co)
+    if w.device.type != 'cuda':
+        return _box4(w.reshape(co, 3, 3, cin).flip(1, 2)).permute(3, 1, 2, 0).reshape(cin, 16 * co)
+    return torch.matmul(_box_mat(w.device, True, 1.0), w.reshape(co, 9, cin)).permute(2, 1, 0).reshape(cin, 16 * co)
 
 
 def resample_via_winograd(full_hw: int, channels: int) -> bool:
