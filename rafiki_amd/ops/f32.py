@@ -185,7 +185,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
 
     use_pt = use_w4 and wino4_pt_ok(H, W, Cin, Cout)
-    xc = _xconv_cands(H, W, Cin, Cout, M) if xw is not None and taps == 9 else []
+    xc = _xconv_cands(H, W, Cin, Cout, M) if xw is not None and taps == 9 and 'fwd' in _XCONV_PASSES else []
 
     def run(cfg):
         tile, nst, s = cfg
@@ -262,7 +262,8 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
 
     use_pt = use_w4 and wino4_pt_ok(H, W, Cout, Cin)
     # ``xw``: the layer's X6 data-gradient planes (WinoWeights 'xt'): the halo-tiled X6 conv of dy
-    xc = _xconv_cands(H, W, Cout, Cin, M) if xw is not None and taps == 9 and not (flags & F_GATE) else []
+    xc = (_xconv_cands(H, W, Cout, Cin, M) if xw is not None and taps == 9 and not (flags & F_GATE)
+          and 'dgrad' in _XCONV_PASSES else [])
 
     def run(cfg):
         if cfg[0] <= XCONV:
@@ -778,6 +779,7 @@ XCONV_ITEMS = ((128, 128), (64, 128), (128, 64), (64, 64), (256, 64))   # (pixel
 # (tests/test_f32_gpu.py::test_engine_grads_vgg_small_full_width) although every unit test of it holds
 # 1e-5 — under investigation (scripts/diag_xconv_engine.py), so it is not an autotune candidate by default
 USE_XCONV = USE_X6 and os.environ.get('RAFIKI_XCONV', '0') != '0'
+_XCONV_PASSES = {'1': ('fwd', 'dgrad'), 'fwd': ('fwd',), 'dgrad': ('dgrad',)}.get(os.environ.get('RAFIKI_XCONV', '0'), ())
 
 
 def xconv_ok(H: int, W: int, C: int, N: int, M: int, force: bool = False) -> bool:
