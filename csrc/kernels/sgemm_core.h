@@ -1,5 +1,5 @@
-// Shared core of the fp32 GEMM kernels (sgemm.hip: implicit-GEMM convs / dense; xconv.hip: halo-tiled
-// 3x3 convs): parameter block, flag bits, geometry decoders, the X6 split-bf16 product helpers and the
+// Shared core of the fp32 GEMM kernels (sgemm.hip: implicit-GEMM convs / dense; x6p.hip: pre-split X6
+// GEMMs): parameter block, flag bits, geometry decoders, the X6 split-bf16 product helpers and the
 // 32x32-accumulator epilogue (bias / activation / BN statistics / BNB / BNP fusions / split-K slabs).
 // Included inside each translation unit's anonymous namespace.
 #pragma once

@@ -105,10 +105,6 @@ _SIGS = {
     "rk_wflip_t": [vp, vp, i32, i32, i32, vp],
     "rk_mbstd_f32": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_lrelu_pixelnorm_f32": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
-    # halo-tiled X6 3x3 conv (xconv.hip)
-    "rk_xconv": [i32, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, i64, vp],
-    "rk_xconv_weights": [vp, vp, vp, i32, i32, vp],
-    "rk_xconv_weights_multi": [vp, vp, vp, i32, vp, vp],
 }
 
 _OPTIONAL: set[str] = set()

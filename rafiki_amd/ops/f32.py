@@ -164,13 +164,12 @@ def _slots_flags(acc):
 
 # ------------------------------------------------------------------------------------------ conv
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None, bias=None, act=ACT_NONE,
-             slope=0.2, out=None, wino=None, wino4=None, xw=None):
+             slope=0.2, out=None, wino=None, wino4=None):
     """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
     [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue.
     ``wino``: the layer's Winograd weights (WinoWeights.u), or a callable producing them (run only
     when a Winograd candidate runs, so the tuner times transform + conv) -> the fused F(2x2,3x3)
-    kernels are more autotune candidates; ``wino4`` likewise for the F(4x4,3x3) kernels (WinoWeights.u4),
-    ``xw`` for the halo-tiled X6 conv (WinoWeights 'x' planes)."""
+    kernels are more autotune candidates; ``wino4`` likewise for the F(4x4,3x3) kernels (WinoWeights.u4)."""
     _check(x, 'conv_fwd x')
     Nb, H, W, Cin = x.shape
     Cout = w.shape[0]
@@ -185,13 +184,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
 
     use_pt = use_w4 and wino4_pt_ok(H, W, Cin, Cout)
-    xc = _xconv_cands(H, W, Cin, Cout, M) if xw is not None and taps == 9 and 'fwd' in _XCONV_PASSES else []
 
     def run(cfg):
         tile, nst, s = cfg
-        if tile <= XCONV:
-            xconv(x, xw() if callable(xw) else xw, cfg=XCONV - tile, out=out, bias=bias, stats=stats_acc, act=act)
-            return
         if tile == WINO4_PT:
             wino4_conv_pt(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
                           relu=act == ACT_RELU, tile=nst, nst=s)
@@ -221,9 +216,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         cands.extend(WINO4_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
-    cands.extend(xc)
     cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4, use_pt, bool(xc)), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt), cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -231,7 +225,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
 
 
 def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None,
-               wino=None, wino4=None, cin=None, xw=None):
+               wino=None, wino4=None, cin=None):
     """dx = data gradient of a 3x3 conv as conv3x3(dy, wt) with wt = SConvWT.view() [Cin][taps*Cout].
     Epilogue options: ``gate`` (ReLU mask of the input activation), ``bnb = (y, coeffs, acc)`` (the input
     is BN+ReLU(y): mask + BN-backward sums into acc), ``bnp = (y, coeffs, acc)`` (the input is
@@ -261,14 +255,8 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cout) and not (flags & F_GATE)
 
     use_pt = use_w4 and wino4_pt_ok(H, W, Cout, Cin)
-    # ``xw``: the layer's X6 data-gradient planes (WinoWeights 'xt'): the halo-tiled X6 conv of dy
-    xc = (_xconv_cands(H, W, Cout, Cin, M) if xw is not None and taps == 9 and not (flags & F_GATE)
-          and 'dgrad' in _XCONV_PASSES else [])
 
     def run(cfg):
-        if cfg[0] <= XCONV:
-            xconv(dy, xw() if callable(xw) else xw, cfg=XCONV - cfg[0], out=out, bnb=bnb, bnp=bnp)
-            return
         if cfg[0] == WINO4_PT:
             wino4_conv_pt(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, tile=cfg[1],
                           nst=cfg[2])
@@ -289,9 +277,8 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
         cands.extend(WINO4_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
-    cands.extend(xc)
     cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4, use_pt, bool(xc)), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt), cands, run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -770,77 +757,6 @@ def wino_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
     return out
 
 
-XCONV = -30   # autotune tile ids -30 .. -34: the halo-tiled X6 conv (xconv.hip), cfg = XCONV - id
-XCONV_ITEMS = ((128, 128), (64, 128), (128, 64), (64, 64), (256, 64))   # (pixels, channels) per cfg
-
-
-# opt-in: it rarely beats the F(4x4) / pre-transformed paths (profiles/xconv_layers_r3.jsonl) and, as a
-# forward candidate inside the full-width fp32 engine, it moved the top layers' gradients by ~3e-3 vs fp64
-# (tests/test_f32_gpu.py::test_engine_grads_vgg_small_full_width) although every unit test of it holds
-# 1e-5 — under investigation (scripts/diag_xconv_engine.py), so it is not an autotune candidate by default
-USE_XCONV = USE_X6 and os.environ.get('RAFIKI_XCONV', '0') != '0'
-_XCONV_PASSES = {'1': ('fwd', 'dgrad'), 'fwd': ('fwd',), 'dgrad': ('dgrad',)}.get(os.environ.get('RAFIKI_XCONV', '0'), ())
-
-
-def xconv_ok(H: int, W: int, C: int, N: int, M: int, force: bool = False) -> bool:
-    """Shapes the halo-tiled X6 conv takes: square 4/8/16/32 maps, C % 32 == 0, N % 64 == 0."""
-    return (USE_XCONV or force) and H == W and W in (4, 8, 16, 32) and C % 32 == 0 and N % 64 == 0 and M % 64 == 0
-
-
-def _xconv_cands(H, W, C, N, M, force=False):
-    if not xconv_ok(H, W, C, N, M, force):
-        return []
-    out = []
-    for c, (bm, bn) in enumerate(XCONV_ITEMS):
-        if M % bm or N % bn or (bm > H * W and bm % (H * W)) or (bm == 256 and W == 4):
-            continue
-        out.append((XCONV - c, 0, 1))
-    return out
-
-
-def xconv_planes(w: torch.Tensor, dgrad: bool = False) -> torch.Tensor:
-    """bf16 weight planes of a [Cout][3][3][Cin] fp32 weight for rk_xconv: forward [3][9][Cout][Cin],
-    or (``dgrad``) those of the flipped transposed conv [3][9][Cin][Cout]."""
-    Cout = w.shape[0]
-    Cin = w.numel() // (9 * Cout)
-    planes = torch.empty((3, 9, Cin if dgrad else Cout, Cout if dgrad else Cin), dtype=torch.bfloat16,
-                         device=w.device)
-    _lib.call("rk_xconv_weights", _p(w), None if dgrad else _p(planes), _p(planes) if dgrad else None, Cout, Cin,
-              _s())
-    return planes
-
-
-def xconv(x: torch.Tensor, planes: torch.Tensor, *, cfg=0, out=None, bias=None, stats=None, act=ACT_NONE,
-          bnb=None, bnp=None, accumulate=False):
-    """Halo-tiled 3x3 conv of x [Nb, H, W, C] fp32 with the X6 weight planes [3][9][N][C] (see
-    xconv_planes / WinoWeights 'x' / 'xt'): y [Nb, H, W, N] fp32, epilogues as sgemm's."""
-    _check(x, 'xconv x')
-    Nb, H, W, C = x.shape
-    N = planes.shape[2]
-    assert planes.shape == (3, 9, N, C) and planes.is_contiguous(), (planes.shape, x.shape)
-    if out is None:
-        out = torch.empty((Nb, H, W, N), device=x.device, dtype=torch.float32)
-    flags = (F_BIAS if bias is not None else 0) | (F_RELU if act == ACT_RELU else F_LRELU if act == ACT_LRELU else 0)
-    gate = None
-    if stats is not None:
-        flags |= F_STATS
-    if bnb is not None:
-        gate, coeffs, stats = bnb
-        bias, flags = coeffs[2:4].reshape(-1).contiguous(), F_BNB
-    elif bnp is not None:
-        gate, coeffs, stats = bnp
-        bias, flags = coeffs[2:4].reshape(-1).contiguous(), F_BNP
-    if accumulate:
-        flags |= F_ACCUM
-    slot_mask = 0
-    if stats is not None:
-        assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
-        slot_mask = stats.shape[0] - 1
-    _lib.call("rk_xconv", int(cfg), _p(x), _p(planes), _p(out), _p(bias), _p(stats), int(slot_mask), _p(gate),
-              Nb, H, W, C, N, int(flags), _nbytes(x), _nbytes(planes), _s())
-    return out
-
-
 class WinoWeights:
     """Winograd-domain weights of several 3x3 convs whose fp32 weights live in one arena: per layer the
     F(2x2) sets u2 [16][Cout][Cin] (forward) and ut2 [16][Cin][Cout] (data gradient, ``dgrad=True``)
@@ -853,7 +769,7 @@ class WinoWeights:
     step pays only for the transforms it needs (outside graph capture; the captured step replays the
     narrowed refresh)."""
 
-    KINDS = ('u2', 'ut2', 'u4', 'ut4', 'x', 'xt')
+    KINDS = ('u2', 'ut2', 'u4', 'ut4')
 
     def __init__(self, arena: torch.Tensor, weights, dgrad=True, f4=None, hw=None):
         """hw[l]: the layer's map size (F(4x4) sets only where it is a multiple of 4; None: every layer)."""
@@ -871,14 +787,8 @@ class WinoWeights:
             kinds = ['u2'] + (['ut2'] if dgrad else [])
             if f4 and (hw is None or hw[l] % 4 == 0):
                 kinds += ['u4'] + (['ut4'] if dgrad else [])
-            # X6 planes (bf16 [3][9][N][K], 13.5 floats per weight) where the halo-tiled conv takes the shape
-            if USE_XCONV and (hw is None or hw[l] in (4, 8, 16, 32)):
-                if Cin % 32 == 0 and Cout % 64 == 0:
-                    kinds.append('x')
-                if dgrad and Cout % 32 == 0 and Cin % 64 == 0:
-                    kinds.append('xt')
             for k in kinds:
-                n = (27 * Cout * Cin) // 2 if k in ('x', 'xt') else (16 if k.endswith('2') else 36) * Cout * Cin
+                n = (16 if k.endswith('2') else 36) * Cout * Cin
                 self._sets[(k, l)] = (off, n)
                 off += n
         dev = arena.device
@@ -894,7 +804,7 @@ class WinoWeights:
         if live in self._tables:
             return self._tables[live]
         out = []
-        for fam, (ka, kb) in (('2', ('u2', 'ut2')), ('4', ('u4', 'ut4')), ('x', ('x', 'xt'))):
+        for fam, (ka, kb) in (('2', ('u2', 'ut2')), ('4', ('u4', 'ut4'))):
             meta, desc, idx = [], [], {}
             for l, (so, Cout, Cin) in enumerate(self._layers):
                 u = self._sets.get((ka, l)) if (ka, l) in live else None
@@ -915,7 +825,7 @@ class WinoWeights:
 
     def refresh(self):
         for fam, desc, meta, nb in self._prepare(self.live):
-            name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi", 'x': "rk_xconv_weights_multi"}[fam]
+            name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi"}[fam]
             _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
         self._fresh = set(self.live)
 
@@ -935,9 +845,6 @@ class WinoWeights:
     def _view(self, kind, l):
         off, n = self._sets[(kind, l)]
         _, Cout, Cin = self._layers[l]
-        if kind in ('x', 'xt'):
-            flat = self.buf[off:off + n].view(torch.bfloat16)
-            return flat.view((3, 9, Cout, Cin) if kind == 'x' else (3, 9, Cin, Cout))
         pos = 16 if kind.endswith('2') else 36
         shape = (pos, Cout, Cin) if kind.startswith('u') and not kind.startswith('ut') else (pos, Cin, Cout)
         return self.buf[off:off + n].view(shape)
@@ -948,9 +855,7 @@ class WinoWeights:
             w = self.arena[so:so + 9 * Cout * Cin]
             v = self._view(kind, l)
             name = "rk_wino_weights" if kind.endswith('2') else "rk_wino4_weights"
-            if kind in ('x', 'xt'):
-                name = "rk_xconv_weights"
-            if kind.startswith('ut') or kind == 'xt':
+            if kind.startswith('ut'):
                 _lib.call(name, _p(w), None, _p(v), Cout, Cin, _s())
             else:
                 _lib.call(name, _p(w), _p(v), None, Cout, Cin, _s())
@@ -979,9 +884,6 @@ class WinoWeights:
 
     def ut4(self, l):
         return self._view('ut4', l) if ('ut4', l) in self._sets else None
-
-    def x(self, l):
-        return self._view('x', l) if ('x', l) in self._sets else None
 
 
 # ----------------------------------------------------------------------------------------- dense

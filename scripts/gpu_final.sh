@@ -6,4 +6,3 @@ rc=$?; tail -3 gpurun_out/final/pytest_gpu.log | cut -c1-300; [ $rc -eq 0 ] || e
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1
 timeout -k 10 400 python -u bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/final/bench.log 2>&1 || exit $?
 tail -1 gpurun_out/final/bench.log | cut -c1-300
-RAFIKI_TUNE_CACHE=off timeout -k 10 200 python -u scripts/diag_xplanes.py 2>&1 | grep -v amdgpu.ids | tail -40

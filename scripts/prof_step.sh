@@ -9,7 +9,7 @@ mkdir -p $OUT
 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/t -o run -- \
   python3 bench.py --steps 20 --warmup 5 --trials 0 "$@" > $OUT/t.log 2>&1
 python3 scripts/trace_steps.py $(find $OUT/t -name '*kernel_trace.csv' | head -1) --steps 20 \
-  --csv $OUT/durations.csv > $OUT/durations.txt
+  --csv $OUT/durations.csv --seq $OUT/seq.txt > $OUT/durations.txt
 rm -rf $OUT/t
 tail -1 $OUT/t.log
 cat $OUT/durations.txt | head -60

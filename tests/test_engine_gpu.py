@@ -55,7 +55,7 @@ def test_bf16_bn_backward_is_exact_given_its_inputs(monkeypatch):
     gradient) to < 1% (measured 0.2%).  The oracle's inputs differ from the engine's by ~1% (another
     bf16 rounding realisation of the same network: measured 1.3% on the last block's incoming
     gradient), and the BN backward's cancelling projection dz = k1*(g - mean g - xhat*mean(g*xhat))
-    amplifies that ~4x (measured 5.4% on its output, scripts/diag_bf16_layers.py) — so the end-to-end
+    amplifies that ~4x (measured 5.4% on its output) — so the end-to-end
     gate above stays loose by construction while the kernels are pinned tightly here."""
     import torch.nn.functional as TF
     from rafiki_amd.ops import functional as F
@@ -154,7 +154,7 @@ def test_grads_match_reference_non_pow2_vgg16_layout():
         fro = ((got - g).norm() / g.norm().clamp_min(1e-12)).item()
         cos = torch.nn.functional.cosine_similarity(got.flatten(), g.flatten(), 0).item()
         # 5 BN stages down to 1x1 at batch 32 amplify the bf16 dy rounding; the same net at 32x32 (the
-        # power-of-two path) measures fro 0.18 / cos 0.983 on conv0 (scripts/diag_grads48.py)
+        # power-of-two path) measures fro 0.18 / cos 0.983 on conv0
         print('bf16-grad48-vs-emulated', n, round(fro, 4), round(cos, 5))
         assert fro < 0.2 and cos > 0.98, (n, fro, cos)
 

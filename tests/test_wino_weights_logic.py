@@ -25,7 +25,6 @@ def _setup(monkeypatch, capturing=False):
     monkeypatch.setattr(S, '_s', lambda: None)
     monkeypatch.setattr(S, '_p', lambda t: None if t is None else t.data_ptr())   # host tensors are fine here
     monkeypatch.setattr(torch.cuda, 'is_current_stream_capturing', lambda: capturing)
-    monkeypatch.setattr(S, 'USE_XCONV', True)     # the X6 plane sets exist when the halo conv is a candidate
     shapes = [(64, 32), (16, 64), (40, 24)]
     arena = torch.zeros(sum(co * 9 * ci for co, ci in shapes) + 3)
     ws, off = [], 3
@@ -50,9 +49,6 @@ def _tables(ww):
 
 def test_sets_per_layer_follow_map_size(monkeypatch):
     _, ww = _setup(monkeypatch)
-    # X6 planes: forward where Cin % 32 == 0 and Cout % 64 == 0 on a 4/8/16/32 map, gradient with the roles swapped
-    assert ww.has('x', 0) and not ww.has('xt', 0) and not ww.has('x', 1) and not ww.has('x', 2)
-    assert ww.x(0).shape == (3, 9, 64, 32) and ww.x(0).dtype == torch.bfloat16
     assert ww.has('u2', 1) and ww.has('ut2', 1) and not ww.has('u4', 1)   # 6x6 map: no F(4x4) set
     assert ww.has('u4', 0) and ww.has('ut4', 2)
     assert ww.u4(1) is None and ww.u4(0).shape == (36, 64, 32) and ww.ut(2).shape == (16, 24, 40)
@@ -61,10 +57,9 @@ def test_sets_per_layer_follow_map_size(monkeypatch):
 def test_refresh_narrows_to_the_sets_a_step_used(monkeypatch):
     rec, ww = _setup(monkeypatch)
     ww.refresh()
-    # everything live (the 64x32 layer on its 8x8 map also has the X6 forward planes)
-    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi', 'rk_xconv_weights_multi']
+    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi']
     ww.end_step()                      # nothing read: keep everything
-    assert len(ww.live) == 11
+    assert len(ww.live) == 10
     ww.refresh()
     ww.lazy('u4', 0)()
     ww.lazy('ut2', 2)()
@@ -90,7 +85,7 @@ def test_no_narrowing_inside_capture(monkeypatch):
     ww.refresh()
     ww.lazy('u2', 0)()
     ww.end_step()
-    assert len(ww.live) == 11                                      # tables cannot be rebuilt in a capture
+    assert len(ww.live) == 10                                      # tables cannot be rebuilt in a capture
 
 
 def test_sconvwt_refresh_is_lazy(monkeypatch):
