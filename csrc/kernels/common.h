@@ -54,6 +54,15 @@ RK_DEV int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// x = hi + mid + lo: bf16 round-to-nearest of x, then of the residuals (x - hi and x - hi - mid are exact
+// in fp32) — the operand pieces of the X6 (fp32-accurate split-bf16) GEMMs, written once by producers
+RK_DEV void split3v(float x, bf16& h, bf16& m, bf16& l) {
+  h = (bf16)x;
+  const float r = x - (float)h;
+  m = (bf16)r;
+  l = (bf16)(r - (float)m);
+}
+
 static inline int rk_cdiv(int a, int b) { return (a + b - 1) / b; }
 static inline int rk_log2(int v) {
   int l = 0;

@@ -238,17 +238,6 @@ RK_DEV void load_frags(const OP& op, const char* tile, int r0, int g, int lane, 
   }
 }
 
-template <int N>
-RK_DEV void s_wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-RK_DEV void s_barrier_lds() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 // Scheduling pattern of one 8-deep k-group (NMF MFMAs): one MFMA, the NR LDS reads of the next
 // group's fragments, then ND (MFMA, DMA) pairs, then the remaining MFMAs.
 template <int NMF, int NR, int ND>

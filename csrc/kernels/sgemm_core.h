@@ -123,6 +123,17 @@ RK_DEV f32x16 mfma6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const 
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
 }
 
+template <int N>
+RK_DEV void s_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+RK_DEV void s_barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // accumulator register r of a 32x32 block: row (r&3) + 8(r>>2) + 4h, column lane&31
 RK_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 

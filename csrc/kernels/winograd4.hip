@@ -823,8 +823,10 @@ RK_DEV void w4_transform(const float (&g)[9], float (&U)[36]) {
 }
 
 // one 32 co x 32 ci block of filters, LDS-staged so both layouts are written coalesced:
-// u [36][Co][Ci] of w, ut [36][Ci][Co] of the flipped filters (either may be null)
-RK_DEV void w4_block(const float* __restrict__ w, float* __restrict__ u, float* __restrict__ ut, int Co, int Ci,
+// u [36][Co][Ci] of w, ut [36][Ci][Co] of the flipped filters (either may be null).  PL: the X6 planes
+// instead, bf16 u [36][3][Co][Ci] / ut [36][3][Ci][Co] (hi, mid, lo of every value; x6p.hip)
+template <bool PL = false>
+RK_DEV void w4_block(const float* __restrict__ w, void* __restrict__ u, void* __restrict__ ut, int Co, int Ci,
                      int co0, int ci0, float (&g)[32][9][33]) {
   float st[36];
 #pragma unroll
@@ -839,6 +841,18 @@ RK_DEV void w4_block(const float* __restrict__ w, float* __restrict__ u, float* 
     g[i / (9 * 32)][(i >> 5) % 9][i & 31] = st[k];
   }
   __syncthreads();
+  auto put = [&](void* dst, long long q, long long rows, long long r, long long cols, long long c, float v) {
+    if constexpr (PL) {
+      bf16* d = (bf16*)dst + (q * 3 * rows + r) * cols + c;
+      bf16 h, m, l;
+      split3v(v, h, m, l);
+      d[0] = h;
+      d[rows * cols] = m;
+      d[2 * rows * cols] = l;
+    } else {
+      ((float*)dst)[(q * rows + r) * cols + c] = v;
+    }
+  };
   if (u != nullptr)
     for (int i = threadIdx.x; i < 1024; i += 256) {
       const int ci = i & 31, co = i >> 5;
@@ -848,7 +862,7 @@ RK_DEV void w4_block(const float* __restrict__ w, float* __restrict__ u, float* 
       for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
       w4_transform(gg, U);
 #pragma unroll
-      for (int q = 0; q < 36; ++q) u[((long long)q * Co + co0 + co) * Ci + ci0 + ci] = U[q];
+      for (int q = 0; q < 36; ++q) put(u, q, Co, co0 + co, Ci, ci0 + ci, U[q]);
     }
   if (ut != nullptr)
     for (int i = threadIdx.x; i < 1024; i += 256) {
@@ -859,7 +873,7 @@ RK_DEV void w4_block(const float* __restrict__ w, float* __restrict__ u, float* 
       for (int t = 0; t < 9; ++t) gg[t] = g[co][8 - t][ci];
       w4_transform(gg, U);
 #pragma unroll
-      for (int q = 0; q < 36; ++q) ut[((long long)q * Ci + ci0 + ci) * Co + co0 + co] = U[q];
+      for (int q = 0; q < 36; ++q) put(ut, q, Ci, ci0 + ci, Co, co0 + co, U[q]);
     }
 }
 
@@ -881,6 +895,23 @@ __global__ __launch_bounds__(256) void wino4_wt_multi_kernel(const float* __rest
            d.y, d.z, g);
 }
 
+// the X6 planes of every layer in one launch: as wino4_wt_multi_kernel, offsets in bf16 elements of dst
+__global__ __launch_bounds__(256) void x6p_wt_multi_kernel(const float* __restrict__ arena, bf16* __restrict__ dst,
+                                                           const int4* __restrict__ desc,
+                                                           const long long* __restrict__ meta) {
+  __shared__ float g[32][9][33];
+  const int4 d = desc[blockIdx.x];
+  const long long* m = meta + 5 * d.x;
+  w4_block<true>(arena + m[0], m[1] >= 0 ? dst + m[1] : nullptr, m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3],
+                 (int)m[4], d.y, d.z, g);
+}
+
+__global__ __launch_bounds__(256) void x6p_wt_kernel(const float* __restrict__ w, bf16* __restrict__ u,
+                                                     bf16* __restrict__ ut, int Co, int Ci) {
+  __shared__ float g[32][9][33];
+  w4_block<true>(w, u, ut, Co, Ci, blockIdx.y * 32, blockIdx.x * 32, g);
+}
+
 }  // namespace
 
 // u [36][Co][Ci] (nullable) / ut [36][Ci][Co] (nullable) of a 3x3 conv weight w [Co][9][Ci]
@@ -888,6 +919,25 @@ extern "C" int rk_wino4_weights(const float* w, float* u, float* ut, int Co, int
   if (Co <= 0 || Ci <= 0 || (!u && !ut)) return RK_EBADARG;
   const dim3 grid(rk_cdiv(Ci, 32), rk_cdiv(Co, 32));
   hipLaunchKernelGGL(wino4_wt_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, u, ut, Co, Ci);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// X6 planes u [36][3][Co][Ci] (nullable) / ut [36][3][Ci][Co] (nullable), bf16, of w [Co][9][Ci]
+extern "C" int rk_x6p_w4_weights(const float* w, void* u, void* ut, int Co, int Ci, void* stream) {
+  if (Co <= 0 || Ci <= 0 || (!u && !ut)) return RK_EBADARG;
+  if (108ll * Co * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const dim3 grid(rk_cdiv(Ci, 32), rk_cdiv(Co, 32));
+  hipLaunchKernelGGL(x6p_wt_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, (bf16*)u, (bf16*)ut, Co, Ci);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_x6p_w4_weights_multi(const float* arena, void* dst, const int* desc, int nblocks,
+                                       const long long* meta, void* stream) {
+  if (nblocks <= 0) return RK_OK;
+  hipLaunchKernelGGL(x6p_wt_multi_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, arena, (bf16*)dst,
+                     (const int4*)desc, meta);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -1099,7 +1149,9 @@ __global__ __launch_bounds__(256) void w4pt_dy_kernel(const float* __restrict__ 
   for (int q = 0; q < 36; ++q) *(f32x4*)(dst + q * ps) = res[q];
 }
 
-__global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x, float* __restrict__ v, int H,
+// PL: bf16 X6 planes v [36][3][T][C] (hi, mid, lo) instead of fp32 v [36][T][C]
+template <bool PL = false>
+__global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x, void* __restrict__ v, int H,
                                                      int W, int C, int TW, int THW, int total4, int T) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total4) return;
@@ -1126,7 +1178,6 @@ __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x
 #pragma unroll
       for (int a = 0; a < 6; ++a) d[a * 6 + b][e] = o[a];
     }
-  float* dst = v + t * C + 4 * c4;
   const int ps = T * C;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
@@ -1139,13 +1190,115 @@ __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x
       for (int b = 0; b < 6; ++b) o4[b][e] = o[b];
     }
 #pragma unroll
-    for (int b = 0; b < 6; ++b) *(f32x4*)(dst + (a * 6 + b) * ps) = o4[b];
+    for (int b = 0; b < 6; ++b) {
+      if constexpr (PL) {
+        bf16x4 h4, m4, l4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bf16 hh, mm, ll;
+          split3v(o4[b][e], hh, mm, ll);
+          h4[e] = hh;
+          m4[e] = mm;
+          l4[e] = ll;
+        }
+        bf16x4* dst = (bf16x4*)((bf16*)v + (long long)(a * 6 + b) * 3 * ps + t * C + 4 * c4);
+        dst[0] = h4;
+        dst[ps / 4] = m4;
+        dst[ps / 2] = l4;
+      } else {
+        *(f32x4*)((float*)v + (long long)(a * 6 + b) * ps + t * C + 4 * c4) = o4[b];
+      }
+    }
   }
+}
+
+// Weight-gradient operands for the pre-split X6 GEMM (x6p.hip), K-inner over the tiles: M^T planes
+// [36][3][Co][T] of dy (A dY A^T per 4x4 patch) and V^T planes [36][3][Ci][T] of x (B^T d B per 6x6
+// window).  One thread per (tile, 4-channel group), tiles fastest, so every bf16 store of a wave writes
+// 64 consecutive tiles of one (position, plane, channel) row.
+RK_DEV void store_planes_t(bf16* dst, int q, int c, int C, int T, int t, float v) {
+  bf16 h, m, l;
+  split3v(v, h, m, l);
+  bf16* d = dst + ((long long)q * 3 * C + c) * T + t;
+  const long long ps = (long long)C * T;
+  d[0] = h;
+  d[ps] = m;
+  d[2 * ps] = l;
+}
+
+__global__ __launch_bounds__(256) void w4pt_dyT_kernel(const float* __restrict__ dy, bf16* __restrict__ m, int H,
+                                                       int W, int C, int TW, int THW, int total4, int T) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int t = i % T, c4 = i / T;
+  const int n = t / THW, r = t - n * THW, ty = r / TW;
+  const int oy = 4 * ty, ox = 4 * (r - ty * TW);
+  const float* src = dy + ((n * H + oy) * W + ox) * C + 4 * c4;
+  f32x4 g[16];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) g[a * 4 + b] = *(const f32x4*)(src + (a * W + b) * C);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float mm[6][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o[6];
+      a6(g[j][e], g[4 + j][e], g[8 + j][e], g[12 + j][e], o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) mm[a][j] = o[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      float o[6];
+      a6(mm[a][0], mm[a][1], mm[a][2], mm[a][3], o);
+#pragma unroll
+      for (int b = 0; b < 6; ++b) store_planes_t(m, a * 6 + b, 4 * c4 + e, C, T, t, o[b]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void w4pt_xT_kernel(const float* __restrict__ x, bf16* __restrict__ v, int H,
+                                                      int W, int C, int TW, int THW, int total4, int T) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int t = i % T, c4 = i / T;
+  const int n = t / THW, r = t - n * THW, ty = r / TW;
+  const int oy = 4 * ty - 1, ox = 4 * (r - ty * TW) - 1;
+  f32x4 d[36];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int yy = oy + a, xx = ox + b;
+      d[a * 6 + b] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                         ? *(const f32x4*)(x + ((n * H + yy) * W + xx) * C + 4 * c4)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+  for (int b = 0; b < 6; ++b)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float o[6];
+      bt6(d[b][e], d[6 + b][e], d[12 + b][e], d[18 + b][e], d[24 + b][e], d[30 + b][e], o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) d[a * 6 + b][e] = o[a];
+    }
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float o[6];
+      bt6(d[a * 6 + 0][e], d[a * 6 + 1][e], d[a * 6 + 2][e], d[a * 6 + 3][e], d[a * 6 + 4][e], d[a * 6 + 5][e], o);
+#pragma unroll
+      for (int b = 0; b < 6; ++b) store_planes_t(v, a * 6 + b, 4 * c4 + e, C, T, t, o[b]);
+    }
 }
 
 // dU [36][Co][Ci] -> dW [Co][9][Ci] (+= with accumulate); one thread per (co, 4-channel group)
 __global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__ du, float* __restrict__ out, int Co,
-                                                       int Ci, int accumulate) {
+                                                       int Ci, int accumulate, int nslab, long long slab) {
   const int i = blockIdx.x * 256 + threadIdx.x;   // 4-channel group index in [Co][Ci/4]
   const int plane = Co * Ci;
   if (i * 4 >= plane) return;
@@ -1155,6 +1308,9 @@ __global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__
   f32x4 u[36];
 #pragma unroll
   for (int q = 0; q < 36; ++q) u[q] = *(const f32x4*)(src + q * plane);
+  for (int k = 1; k < nslab; ++k)   // split-K partial slabs of the GEMM
+#pragma unroll
+    for (int q = 0; q < 36; ++q) u[q] += *(const f32x4*)(src + k * slab + q * plane);
   float* o = out + co * 9 * Ci + ci;
   f32x4 w[9];
 #pragma unroll
@@ -1196,18 +1352,20 @@ extern "C" int rk_wino4_pt_transform(const float* dy, const float* x, float* m, 
   hipLaunchKernelGGL(w4pt_dy_kernel, dim3((unsigned)((ty + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy, m, H,
                      W, Co, TW, THW, (int)ty, (int)T);
   RK_LAUNCH_CHECK();
-  hipLaunchKernelGGL(w4pt_x_kernel, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, v, H, W,
-                     Ci, TW, THW, (int)tx, (int)T);
+  hipLaunchKernelGGL(w4pt_x_kernel<false>, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     v, H, W, Ci, TW, THW, (int)tx, (int)T);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
-extern "C" int rk_wino4_pt_output(const float* du, float* out, int Co, int Ci, int accumulate, void* stream) {
-  if (Co <= 0 || Ci <= 0) return RK_EBADARG;
+// du: nslab slabs of [36][Co][Ci], slab floats apart (split-K partial sums), summed here
+extern "C" int rk_wino4_pt_output(const float* du, float* out, int Co, int Ci, int accumulate, int nslab,
+                                  long long slab, void* stream) {
+  if (Co <= 0 || Ci <= 0 || nslab <= 0 || (nslab > 1 && slab < 36ll * Co * Ci)) return RK_EBADARG;
   if ((Ci & 3) || 36ll * Co * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
   const long long g4 = (long long)Co * Ci / 4;
   hipLaunchKernelGGL(w4pt_out_kernel, dim3((unsigned)((g4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, du,
-                     out, Co, Ci, accumulate);
+                     out, Co, Ci, accumulate, nslab, slab);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -1223,7 +1381,8 @@ namespace {
 __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restrict__ yt, float* __restrict__ y,
                                                             const float* __restrict__ bp, double* stats, int slotMask,
                                                             const float* __restrict__ gate, int Nb, int H, int W,
-                                                            int N, int TW, int THW, int T, int flags) {
+                                                            int N, int TW, int THW, int T, int flags, int nslab,
+                                                            long long slab) {
   constexpr int TPB = 4;                   // tiles per block: one per 64-thread group (>= 2 blocks per CU
                                            // on the 4x4 x 512 maps: T x N / 256 blocks)
   __shared__ float red[2][4][64];
@@ -1242,6 +1401,9 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
     float m[36];
 #pragma unroll
     for (int q = 0; q < 36; ++q) m[q] = yt[q * plane + (long long)t * N + n];
+    for (int k = 1; k < nslab; ++k)   // split-K partial slabs of the GEMM
+#pragma unroll
+      for (int q = 0; q < 36; ++q) m[q] += yt[k * slab + q * plane + (long long)t * N + n];
     float tt[6][4];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {          // M A: along columns
@@ -1308,9 +1470,11 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
 
 }  // namespace
 
+// yt: nslab slabs of [36][T][N], slab floats apart (split-K partial sums of the GEMM), summed here
 extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias, double* stats, int slotMask,
-                                    const float* gate, int Nb, int H, int W, int N, int flags, void* stream) {
-  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || N <= 0) return RK_EBADARG;
+                                    const float* gate, int Nb, int H, int W, int N, int flags, int nslab,
+                                    long long slab, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || N <= 0 || nslab <= 0) return RK_EBADARG;
   if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
   if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
   if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
@@ -1318,8 +1482,9 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
   const long long T = (long long)Nb * THW;
   if (T * N >= (1LL << 31)) return RK_EUNSUPPORTED;
   const long long blocks = ((N + 63) / 64) * ((T + 3) / 4);
+  if (nslab > 1 && slab < 36 * T * N) return RK_EBADARG;
   hipLaunchKernelGGL(w4pt_conv_out_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, yt, y, bias,
-                     stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags);
+                     stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -1332,8 +1497,42 @@ extern "C" int rk_wino4_pt_input(const float* x, float* v, int Nb, int H, int W,
   const long long T = (long long)Nb * THW;
   if (36 * T * C >= (1ll << 31)) return RK_EUNSUPPORTED;
   const long long tx = T * C / 4;
-  hipLaunchKernelGGL(w4pt_x_kernel, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, v, H, W,
-                     C, TW, THW, (int)tx, (int)T);
+  hipLaunchKernelGGL(w4pt_x_kernel<false>, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     v, H, W, C, TW, THW, (int)tx, (int)T);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// V planes [36][3][T][C] (bf16 hi, mid, lo of B^T x B) for the pre-split X6 GEMM (x6p.hip)
+extern "C" int rk_x6p_w4_input(const float* x, void* v, int Nb, int H, int W, int C, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || C <= 0) return RK_EBADARG;
+  if (C & 3) return RK_EUNSUPPORTED;
+  const int TW = W / 4, THW = (H / 4) * (W / 4);
+  const long long T = (long long)Nb * THW;
+  if (108 * T * C >= (1ll << 31) || (long long)Nb * H * W * C >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const long long tx = T * C / 4;
+  hipLaunchKernelGGL(w4pt_x_kernel<true>, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     v, H, W, C, TW, THW, (int)tx, (int)T);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// M^T planes [36][3][Co][T] of dy and V^T planes [36][3][Ci][T] of x (bf16), the weight-gradient operands
+// of the pre-split X6 GEMM: dU[q] = M^T[q] (V^T[q])^T, K = T tiles
+extern "C" int rk_x6p_w4_wgrad_transform(const float* dy, const float* x, void* mt, void* vt, int Nb, int H, int W,
+                                         int Co, int Ci, void* stream) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0) return RK_EBADARG;
+  if ((Co & 3) || (Ci & 3)) return RK_EUNSUPPORTED;
+  const int TW = W / 4, THW = (H / 4) * (W / 4);
+  const long long T = (long long)Nb * THW;
+  if (108 * T * Co >= (1ll << 31) || 108 * T * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
+  if ((long long)Nb * H * W * (Co > Ci ? Co : Ci) >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const long long ty = T * Co / 4, tx = T * Ci / 4;
+  hipLaunchKernelGGL(w4pt_dyT_kernel, dim3((unsigned)((ty + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy,
+                     (bf16*)mt, H, W, Co, TW, THW, (int)ty, (int)T);
+  RK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(w4pt_xT_kernel, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     (bf16*)vt, H, W, Ci, TW, THW, (int)tx, (int)T);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

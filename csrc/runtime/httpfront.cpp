@@ -121,9 +121,13 @@ struct Server {
   std::atomic<long long> nconns{0};
   long long max_batch = 512;
   long long max_body = 256 << 20;
+  long long max_query = 1 << 20;  // bytes of ONE image query on the batch path; larger ones go to Python
   bool batching = true;
   std::mutex qmu;
-  std::condition_variable qcv;
+  // one condition variable per queue: a notify for an image query must never be consumed by the generic
+  // thread (whose predicate stays false) while the batch threads sleep out their timeout
+  std::condition_variable qcv;   // items (batch threads)
+  std::condition_variable gcv;   // generic requests (the Python request thread)
   std::deque<Item> items;
   std::deque<std::pair<uint64_t, Generic>> generic;
   std::unordered_map<uint64_t, std::vector<Ticket>> batches;
@@ -328,7 +332,7 @@ bool process(IoThread* io, Conn* c) {
       Item it;
       it.data.resize((size_t)clen);
       long long n = clen > 0 ? rt_json_u8_array(body, clen, "query", it.data.data(), clen, it.shape, &it.ndim) : -1;
-      if (n > 0) {
+      if (n > 0 && n <= s->max_query) {   // oversized queries take the generic path (bounded batch buffers)
         it.data.resize((size_t)n);
         it.conn = c->id;
         it.io = io->idx;
@@ -350,7 +354,7 @@ bool process(IoThread* io, Conn* c) {
       s->generic.emplace_back(gid, std::move(g));
     }
     s->ngeneric++;
-    s->qcv.notify_all();
+    s->gcv.notify_one();
     if (close_req) c->closing = true;
   }
   if (!ok) return false;  // the connection is gone
@@ -534,6 +538,13 @@ int rt_http_port(void* h) {
   return ntohs(a.sin_port);
 }
 
+// Largest single image query (bytes) the batch path accepts; larger ones are served by the generic path.
+void rt_http_set_max_query(void* h, long long bytes) {
+  auto* s = (Server*)h;
+  std::lock_guard<std::mutex> g(s->qmu);
+  s->max_query = bytes > 0 ? bytes : (1 << 20);
+}
+
 // Blocks up to timeout_ms for pending image queries; takes every pending query of the first
 // query's shape (<= max_batch, <= cap bytes) into `out`.  Returns the query count (0: timeout,
 // -1: stopped, -3: `out` cannot hold one query of `shape`); `shape`/`ndim` describe ONE query,
@@ -632,7 +643,7 @@ long long rt_http_next_request(void* h, int timeout_ms, unsigned long long* id, 
                                int pcap) {
   auto* s = (Server*)h;
   std::unique_lock<std::mutex> lk(s->qmu);
-  if (!s->qcv.wait_for(lk, std::chrono::milliseconds(timeout_ms),
+  if (!s->gcv.wait_for(lk, std::chrono::milliseconds(timeout_ms),
                        [s] { return s->stop.load() || !s->generic.empty(); }))
     return -1;
   if (s->stop.load()) return -2;
@@ -694,6 +705,7 @@ void rt_http_shutdown(void* h) {
     s->stop.store(true);
   }
   s->qcv.notify_all();
+  s->gcv.notify_all();
 }
 
 // Joins the server's threads, closes every connection and frees the server.

@@ -389,7 +389,8 @@ class ConvNetEngine:
             rm, rv = self.running_stats(bi)
             y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0],
                            wino=ww.lazy('u2', bi) if ww is not None else None,
-                           wino4=ww.lazy('u4', bi) if ww is not None else None)
+                           wino4=ww.lazy('u4', bi) if ww is not None else None,
+                           wino4p=ww.lazy('u4p', bi) if ww is not None else None)
             h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
                                  self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
             saved.append((y, coeffs))
@@ -460,17 +461,18 @@ class ConvNetEngine:
             pname, pcin, pcout, ppool, phw = self.blocks[bi - 1]
             wu = ww.lazy('ut2', bi) if ww is not None else None
             wu4 = ww.lazy('ut4', bi) if ww is not None else None
+            wu4p = ww.lazy('ut4p', bi) if ww is not None else None
             wl = wt.lazy(bi - 1)
             if not ppool:
                 # the input block is BN+ReLU: its mask and BN-backward sums ride in this dgrad's epilogue
-                d = S.conv_dgrad(dy, wl, bnb=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin)
+                d = S.conv_dgrad(dy, wl, bnb=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin, wino4p=wu4p)
                 reduced = True
             elif phw == 2 * hw and not (hw & (hw - 1)):
                 # BN+ReLU+max-pool input (even power-of-two geometry): pool routing + sums in the epilogue
-                d = S.conv_dgrad(dy, wl, bnp=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin)
+                d = S.conv_dgrad(dy, wl, bnp=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin, wino4p=wu4p)
                 reduced = True
             else:
-                d = S.conv_dgrad(dy, wl, wino=wu, wino4=wu4, cin=cin)
+                d = S.conv_dgrad(dy, wl, wino=wu, wino4=wu4, cin=cin, wino4p=wu4p)
                 reduced = False
         if side is not None:
             main.wait_stream(side)
@@ -790,7 +792,7 @@ class ConvNetEngine:
         ew = getattr(self, '_eval_wino', None)
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             y = S.conv_fwd(h, fl.w(name + '.w'), wino=ew.u(bi) if ew is not None else None,
-                           wino4=ew.u4(bi) if ew is not None else None)
+                           wino4=ew.u4(bi) if ew is not None else None, wino4p=ew.u4p(bi) if ew is not None else None)
             c = self._eval_coeffs[bi]
             h = S.bn_eval(y, c[2], c[3], pool=pool, act=F.ACT_RELU)
         if self.input_bn:

@@ -76,9 +76,9 @@ _SIGS = {
     "rk_wino4_wgrad": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "rk_wino4_wgrad_v": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "rk_wino4_pt_transform": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
-    "rk_wino4_pt_output": [vp, vp, i32, i32, i32, vp],
+    "rk_wino4_pt_output": [vp, vp, i32, i32, i32, i32, i64, vp],
     "rk_wino4_pt_input": [vp, vp, i32, i32, i32, i32, vp],
-    "rk_wino4_pt_conv_out": [vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp],
+    "rk_wino4_pt_conv_out": [vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, vp],
     "rk_wino2s_conv_grp": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, vp],
     # fp32 path (sgemm.hip, bnf.hip)
     "rk_sgemm": [i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
@@ -105,6 +105,14 @@ _SIGS = {
     "rk_wflip_t": [vp, vp, i32, i32, i32, vp],
     "rk_mbstd_f32": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_lrelu_pixelnorm_f32": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
+    # pre-split X6 GEMMs (x6p.hip) and their plane producers (winograd4.hip)
+    "rk_x6p_gemm": [i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i32, i32, i32, i64,
+                    i64, i64, vp],
+    "rk_x6p_split": [vp, vp, i32, i32, i32, i32, i64, vp],
+    "rk_x6p_w4_weights": [vp, vp, vp, i32, i32, vp],
+    "rk_x6p_w4_weights_multi": [vp, vp, vp, i32, vp, vp],
+    "rk_x6p_w4_input": [vp, vp, i32, i32, i32, i32, vp],
+    "rk_x6p_w4_wgrad_transform": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
 }
 
 _OPTIONAL: set[str] = set()

@@ -164,12 +164,13 @@ def _slots_flags(acc):
 
 # ------------------------------------------------------------------------------------------ conv
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None, bias=None, act=ACT_NONE,
-             slope=0.2, out=None, wino=None, wino4=None):
+             slope=0.2, out=None, wino=None, wino4=None, wino4p=None):
     """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
     [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue.
     ``wino``: the layer's Winograd weights (WinoWeights.u), or a callable producing them (run only
     when a Winograd candidate runs, so the tuner times transform + conv) -> the fused F(2x2,3x3)
-    kernels are more autotune candidates; ``wino4`` likewise for the F(4x4,3x3) kernels (WinoWeights.u4)."""
+    kernels are more autotune candidates; ``wino4`` likewise for the F(4x4,3x3) kernels (WinoWeights.u4),
+    ``wino4p`` the X6 weight planes (WinoWeights 'u4p') of the pre-split pre-transformed F(4x4) path."""
     _check(x, 'conv_fwd x')
     Nb, H, W, Cin = x.shape
     Cout = w.shape[0]
@@ -184,9 +185,14 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
 
     use_pt = use_w4 and wino4_pt_ok(H, W, Cin, Cout)
+    use_ptx = (wino4p is not None and taps == 9 and wino4_ptx_ok(H, W, Cin, Cout) and act in (ACT_NONE, ACT_RELU))
 
     def run(cfg):
         tile, nst, s = cfg
+        if tile == WINO4_PTX:
+            wino4_conv_pt(x, wino4p() if callable(wino4p) else wino4p, out=out, bias=bias, stats=stats_acc,
+                          relu=act == ACT_RELU, tile=nst // 4, nst=nst % 4, splits=s)
+            return
         if tile == WINO4_PT:
             wino4_conv_pt(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
                           relu=act == ACT_RELU, tile=nst, nst=s)
@@ -216,8 +222,10 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         cands.extend(WINO4_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
+    if use_ptx:
+        cands.extend(WINO4_PTX_CFGS)
     cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4, use_pt), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt, 'lazy' if callable(wino4p) else use_ptx), cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -225,7 +233,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
 
 
 def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None,
-               wino=None, wino4=None, cin=None):
+               wino=None, wino4=None, cin=None, wino4p=None):
     """dx = data gradient of a 3x3 conv as conv3x3(dy, wt) with wt = SConvWT.view() [Cin][taps*Cout].
     Epilogue options: ``gate`` (ReLU mask of the input activation), ``bnb = (y, coeffs, acc)`` (the input
     is BN+ReLU(y): mask + BN-backward sums into acc), ``bnp = (y, coeffs, acc)`` (the input is
@@ -255,8 +263,14 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cout) and not (flags & F_GATE)
 
     use_pt = use_w4 and wino4_pt_ok(H, W, Cout, Cin)
+    # ``wino4p``: the X6 planes of the data-gradient set (WinoWeights 'ut4p'): the pre-split PT path
+    use_ptx = wino4p is not None and taps == 9 and wino4_ptx_ok(H, W, Cout, Cin) and not (flags & F_GATE)
 
     def run(cfg):
+        if cfg[0] == WINO4_PTX:
+            wino4_conv_pt(dy, wino4p() if callable(wino4p) else wino4p, out=out, bnb=bnb, bnp=bnp, tile=cfg[1] // 4,
+                          nst=cfg[1] % 4, splits=cfg[2])
+            return
         if cfg[0] == WINO4_PT:
             wino4_conv_pt(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, tile=cfg[1],
                           nst=cfg[2])
@@ -277,8 +291,10 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
         cands.extend(WINO4_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
+    if use_ptx:
+        cands.extend(WINO4_PTX_CFGS)
     cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4, use_pt), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt, 'lazy' if callable(wino4p) else use_ptx), cands, run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -306,6 +322,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
         if tile == WINO4_WGRAD_PT:
             wino4_wgrad_pt(dy, x, out, accumulate=accumulate, tile=nst, nst=s)
             return
+        if tile == WINO4_WGRAD_PTX:
+            wino4_wgrad_pt(dy, x, out, accumulate=accumulate, tile=nst // 4, nst=nst % 4, planes=True, splits=s)
+            return
         if s == 1:
             sgemm(KIND_WGRAD, dy, x, out, M, N, K, Cout, Cin, N, tile=tile, nst=nst, H=H, W=W, C=Cin, taps=taps,
                   flags=F_ACCUM if accumulate else 0)
@@ -323,9 +342,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
     wcands = _wino_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
     w4cands = _wino4_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
     ptcands = _wino4_pt_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
-    cands += wcands + w4cands + ptcands
-    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands), bool(w4cands), bool(ptcands)),
-                cands, run, protect=(out,) if accumulate else ())
+    ptxcands = _wino4_ptx_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
+    cands += wcands + w4cands + ptcands + ptxcands
+    cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands), bool(w4cands), bool(ptcands),
+                 bool(ptxcands)), cands, run, protect=(out,) if accumulate else ())
     run(cfg)
     return out
 
@@ -557,13 +577,17 @@ WINO4_PT_CFGS = tuple((WINO4_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)
 
 
 def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None,
-                  bnp=None, tile=0, nst=2):
+                  bnp=None, tile=0, nst=2, splits=1):
     """wino4_conv through position-major buffers: V = B^T x B [36][T][C] (one launch), Y'[q] = V[q] u[q]^T
-    as one 36-group sgemm, then A^T Y' A with the same epilogues (bias / ReLU / BN statistics / BNB / BNP)."""
+    as one 36-group sgemm, then A^T Y' A with the same epilogues (bias / ReLU / BN statistics / BNB / BNP).
+    With bf16 X6 planes u [36][3][N][C] (WinoWeights 'u4p' / 'ut4p') the input transform writes V as planes
+    too and the GEMM is the pre-split X6 one (x6p_gemm; ``tile`` / ``nst`` are its configs)."""
     _check(x, 'wino4_conv_pt x')
     Nb, H, W, C = x.shape
-    N = u.shape[1]
-    assert u.shape == (36, N, C) and u.is_contiguous() and H % 4 == 0 and W % 4 == 0, (u.shape, x.shape)
+    planes = u.dtype == torch.bfloat16   # u4p / ut4p X6 planes [36][3][N][C]
+    N = u.shape[-2]
+    assert u.shape == ((36, 3, N, C) if planes else (36, N, C)) and u.is_contiguous() and H % 4 == 0 and W % 4 == 0, \
+        (u.shape, x.shape)
     if out is None:
         out = torch.empty((Nb, H, W, N), device=x.device, dtype=torch.float32)
     assert out.shape == (Nb, H, W, N) and out.is_contiguous()
@@ -585,12 +609,20 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
     if stats is not None:
         assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
     T = Nb * (H // 4) * (W // 4)
-    v = torch.empty((36, T, C), device=x.device, dtype=torch.float32)
-    _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
-    yt = torch.empty((36, T, N), device=x.device, dtype=torch.float32)
-    sgemm_grp(KIND_DENSE, v, u, yt, T, N, C, C, C, N, 36, T * C, N * C, T * N, tile=tile, nst=nst)
+    if planes:   # pre-split X6: V planes [36][3][T][C] once, then the plane GEMM (no split in the K loop)
+        splits = x6p_splits(C, splits)
+        yt = torch.empty((splits, 36, T, N), device=x.device, dtype=torch.float32)
+        v = torch.empty((36, 3, T, C), device=x.device, dtype=torch.bfloat16)
+        _lib.call("rk_x6p_w4_input", _p(x), _p(v), Nb, H, W, C, _s())
+        x6p_gemm(v, u, yt, T, N, C, groups=36, tile=tile, nst=nst, splits=splits)
+    else:
+        splits = 1
+        yt = torch.empty((36, T, N), device=x.device, dtype=torch.float32)
+        v = torch.empty((36, T, C), device=x.device, dtype=torch.float32)
+        _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
+        sgemm_grp(KIND_DENSE, v, u, yt, T, N, C, C, C, N, 36, T * C, N * C, T * N, tile=tile, nst=nst)
     _lib.call("rk_wino4_pt_conv_out", _p(yt), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
-              Nb, H, W, N, flags, _s())
+              Nb, H, W, N, flags, splits, 36 * T * N, _s())
     return out
 
 
@@ -676,10 +708,12 @@ def _wino4_pt_cands(Nb, H, W, Cout, Cin):
         ([(WINO4_WGRAD_PT, t + X6, n) for t in _FEW_WAVE for n in (2, 3)] if USE_X6 else [])
 
 
-def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accumulate=False, tile=0, nst=2):
+def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accumulate=False, tile=0, nst=2,
+                   planes=False, splits=1):
     """out [Cout][9*Cin] (+)= the F(4x4,3x3) weight gradient through position-major transformed buffers:
     M [36][T][Cout], V [36][T][Cin] (one transform launch each), dU[q] = M[q]^T V[q] as ONE sgemm with
-    36 K-splits (slab q = dU[q]), then dW = G^T dU G."""
+    36 K-splits (slab q = dU[q]), then dW = G^T dU G.  ``planes``: the operands as X6 planes transposed to
+    K-inner ([36][3][C][T]) and the 36 GEMMs as one grouped pre-split X6 launch (x6p_gemm configs)."""
     _check(dy, 'wino4_wgrad_pt dy')
     _check(x, 'wino4_wgrad_pt x')
     Nb, H, W, Cout = dy.shape
@@ -687,14 +721,85 @@ def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accu
     T = Nb * (H // 4) * (W // 4)
     assert H % 4 == 0 and W % 4 == 0 and T % 32 == 0 and x.shape[:3] == dy.shape[:3], (dy.shape, x.shape)
     assert out.numel() == Cout * 9 * Cin and out.is_contiguous()
-    m = torch.empty((36 * T, Cout), device=dy.device, dtype=torch.float32)
-    v = torch.empty((36 * T, Cin), device=dy.device, dtype=torch.float32)
-    _lib.call("rk_wino4_pt_transform", _p(dy), _p(x), _p(m), _p(v), Nb, H, W, Cout, Cin, _s())
-    du = torch.empty((36, Cout, Cin), device=dy.device, dtype=torch.float32)
-    sgemm(KIND_DENSE_DW, m, v, du, Cout, Cin, 36 * T, Cout, Cin, Cin, tile=tile, nst=nst, splits=36,
-          slab_stride=Cout * Cin)
-    _lib.call("rk_wino4_pt_output", _p(du), _p(out), Cout, Cin, int(bool(accumulate)), _s())
+    if planes:   # pre-split X6: M^T / V^T planes [36][3][C][T] (K = tiles inner), 36-group plane GEMM
+        splits = x6p_splits(T, splits)
+        du = torch.empty((splits, 36, Cout, Cin), device=dy.device, dtype=torch.float32)
+        m = torch.empty((36, 3, Cout, T), device=dy.device, dtype=torch.bfloat16)
+        v = torch.empty((36, 3, Cin, T), device=dy.device, dtype=torch.bfloat16)
+        _lib.call("rk_x6p_w4_wgrad_transform", _p(dy), _p(x), _p(m), _p(v), Nb, H, W, Cout, Cin, _s())
+        x6p_gemm(m, v, du, Cout, Cin, T, groups=36, tile=tile, nst=nst, splits=splits)
+    else:
+        splits = 1
+        du = torch.empty((36, Cout, Cin), device=dy.device, dtype=torch.float32)
+        m = torch.empty((36 * T, Cout), device=dy.device, dtype=torch.float32)
+        v = torch.empty((36 * T, Cin), device=dy.device, dtype=torch.float32)
+        _lib.call("rk_wino4_pt_transform", _p(dy), _p(x), _p(m), _p(v), Nb, H, W, Cout, Cin, _s())
+        sgemm(KIND_DENSE_DW, m, v, du, Cout, Cin, 36 * T, Cout, Cin, Cin, tile=tile, nst=nst, splits=36,
+              slab_stride=Cout * Cin)
+    _lib.call("rk_wino4_pt_output", _p(du), _p(out), Cout, Cin, int(bool(accumulate)), splits, 36 * Cout * Cin, _s())
     return out
+
+
+# ---------------------------------------------------------------- pre-split X6 GEMMs (x6p.hip)
+# The X6 products with the operands split into bf16 planes ONCE by their producers (the Winograd
+# transforms) instead of after every LDS read inside the K loop: the pre-transformed F(4x4) paths on
+# planes are autotune candidates next to their fp32-operand sgemm forms.  RAFIKI_X6P=0 turns them off.
+USE_X6P = USE_X6 and os.environ.get('RAFIKI_X6P', '1') != '0'
+XP_TILES = ((128, 128), (128, 64), (64, 128), (64, 64), (64, 64), (128, 64), (64, 128), (256, 128), (128, 256))
+XP_NST3 = (0, 1, 2, 3, 4, 5, 6)          # tiles 7-8 (8 waves, 72 KiB per stage) ring 2 stages only
+# (tile, nst, splits) of the x6p GEMM: every tile x ring depth unsplit; the big tiles also with 2 / 4 K-splits
+# (the 4x4-map GEMMs have T = 256 rows: 288 blocks of 128x128 for 256 CUs; the slabs are summed by the
+# output transforms that read Y' / dU anyway)
+_XP_CFGS = tuple((t, n, 1) for t in range(len(XP_TILES)) for n in ((2, 3) if t in XP_NST3 else (2,))) + \
+    tuple((t, 2, s) for t in (0, 1, 2, 7, 8) for s in (2, 4))
+WINO4_PTX = -15         # conv / data gradient: cfg = (-15, x6p code, splits), code = tile * 4 + nst
+WINO4_WGRAD_PTX = -16   # weight gradient: likewise
+WINO4_PTX_CFGS = tuple((WINO4_PTX, 4 * t + n, s) for t, n, s in _XP_CFGS) if USE_X6P else ()
+
+
+def x6p_split(src: torch.Tensor, out=None) -> torch.Tensor:
+    """bf16 X6 planes [3][rows][cols] (hi, mid, lo; x = hi + mid + lo) of an fp32 [rows][cols] matrix."""
+    _check(src, 'x6p_split src')
+    rows, cols = src.shape
+    if out is None:
+        out = torch.empty((3, rows, cols), dtype=torch.bfloat16, device=src.device)
+    _lib.call("rk_x6p_split", _p(src), _p(out), rows, cols, cols, cols, rows * cols, _s())
+    return out
+
+
+def x6p_gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, M: int, N: int, K: int, *, groups: int = 1,
+             tile: int = 0, nst: int = 2, accumulate: bool = False, splits: int = 1) -> torch.Tensor:
+    """out[g] (+)= A[g] . B[g]^T for g < groups: A bf16 planes [G][3][M][K], B [G][3][N][K] (contiguous),
+    out fp32 [G][M][N]; K % 32 == 0.  splits > 1: out is [splits][G][M][N] raw split-K partial sums."""
+    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and A.is_contiguous() and B.is_contiguous()
+    assert A.numel() == groups * 3 * M * K and B.numel() == groups * 3 * N * K
+    assert out.numel() == splits * groups * M * N and not (accumulate and splits > 1)
+    _lib.call("rk_x6p_gemm", int(tile), int(nst), _p(A), _p(B), _p(out), M, N, K, K, K, N, M * K, N * K, 3 * M * K,
+              3 * N * K, M * N, int(groups), int(bool(accumulate)), int(splits), groups * M * N, _nbytes(A),
+              _nbytes(B), _s())
+    return out
+
+
+def x6p_splits(K: int, s: int) -> int:
+    """The effective split count of ``s`` requested splits over K (every split gets >= one 32-deep K-tile)."""
+    nk = K // 32
+    per = cdiv(nk, max(1, s))
+    return cdiv(nk, per)
+
+
+def wino4_ptx_ok(H, W, C, N):
+    """Shapes the plane path of the pre-transformed F(4x4) conv takes (K = C channels, % 32)."""
+    return USE_X6P and wino4_pt_ok(H, W, C, N) and C % 32 == 0
+
+
+def _wino4_ptx_wgrad_cands(Nb, H, W, Cout, Cin):
+    """The plane path of the pre-transformed F(4x4) weight gradient: K = T tiles (% 32)."""
+    if not (USE_X6P and _wino4_pt_cands(Nb, H, W, Cout, Cin)):
+        return []
+    T = Nb * (H // 4) * (W // 4)
+    if T % 32 or 108 * T * max(Cin, Cout) >= (1 << 31):
+        return []
+    return [(WINO4_WGRAD_PTX, 4 * t + n, x6p_splits(T, s)) for t, n, s in _XP_CFGS]
 
 
 WINO_WGRAD = -3   # autotune tile id of the Winograd weight gradient (cfg = (-3, 0, splits))
@@ -769,7 +874,7 @@ class WinoWeights:
     step pays only for the transforms it needs (outside graph capture; the captured step replays the
     narrowed refresh)."""
 
-    KINDS = ('u2', 'ut2', 'u4', 'ut4')
+    KINDS = ('u2', 'ut2', 'u4', 'ut4', 'u4p', 'ut4p')
 
     def __init__(self, arena: torch.Tensor, weights, dgrad=True, f4=None, hw=None):
         """hw[l]: the layer's map size (F(4x4) sets only where it is a multiple of 4; None: every layer)."""
@@ -787,8 +892,13 @@ class WinoWeights:
             kinds = ['u2'] + (['ut2'] if dgrad else [])
             if f4 and (hw is None or hw[l] % 4 == 0):
                 kinds += ['u4'] + (['ut4'] if dgrad else [])
+                # X6 planes (bf16 [36][3][..], 54 floats per weight) where the pre-split PT path takes the shape
+                if hw is None or wino4_ptx_ok(hw[l], hw[l], Cin, Cout):
+                    kinds.append('u4p')
+                if dgrad and (hw is None or wino4_ptx_ok(hw[l], hw[l], Cout, Cin)):
+                    kinds.append('ut4p')
             for k in kinds:
-                n = (16 if k.endswith('2') else 36) * Cout * Cin
+                n = 54 * Cout * Cin if k.endswith('p') else (16 if k.endswith('2') else 36) * Cout * Cin
                 self._sets[(k, l)] = (off, n)
                 off += n
         dev = arena.device
@@ -804,7 +914,8 @@ class WinoWeights:
         if live in self._tables:
             return self._tables[live]
         out = []
-        for fam, (ka, kb) in (('2', ('u2', 'ut2')), ('4', ('u4', 'ut4'))):
+        for fam, (ka, kb) in (('2', ('u2', 'ut2')), ('4', ('u4', 'ut4')), ('p', ('u4p', 'ut4p'))):
+            scale = 2 if fam == 'p' else 1   # plane sets: offsets in bf16 elements
             meta, desc, idx = [], [], {}
             for l, (so, Cout, Cin) in enumerate(self._layers):
                 u = self._sets.get((ka, l)) if (ka, l) in live else None
@@ -812,7 +923,7 @@ class WinoWeights:
                 if u is None and ut is None:
                     continue
                 idx[l] = len(meta)
-                meta.append([so, u[0] if u else -1, ut[0] if ut else -1, Cout, Cin])
+                meta.append([so, scale * u[0] if u else -1, scale * ut[0] if ut else -1, Cout, Cin])
                 for co0 in range(0, Cout, 32):
                     for ci0 in range(0, Cin, 32):
                         desc.append([idx[l], co0, ci0, 0])
@@ -825,7 +936,7 @@ class WinoWeights:
 
     def refresh(self):
         for fam, desc, meta, nb in self._prepare(self.live):
-            name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi"}[fam]
+            name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi", 'p': "rk_x6p_w4_weights_multi"}[fam]
             _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
         self._fresh = set(self.live)
 
@@ -845,6 +956,9 @@ class WinoWeights:
     def _view(self, kind, l):
         off, n = self._sets[(kind, l)]
         _, Cout, Cin = self._layers[l]
+        if kind.endswith('p'):
+            flat = self.buf[off:off + n].view(torch.bfloat16)
+            return flat.view((36, 3, Cout, Cin) if kind == 'u4p' else (36, 3, Cin, Cout))
         pos = 16 if kind.endswith('2') else 36
         shape = (pos, Cout, Cin) if kind.startswith('u') and not kind.startswith('ut') else (pos, Cin, Cout)
         return self.buf[off:off + n].view(shape)
@@ -855,6 +969,8 @@ class WinoWeights:
             w = self.arena[so:so + 9 * Cout * Cin]
             v = self._view(kind, l)
             name = "rk_wino_weights" if kind.endswith('2') else "rk_wino4_weights"
+            if kind.endswith('p'):
+                name = "rk_x6p_w4_weights"
             if kind.startswith('ut'):
                 _lib.call(name, _p(w), None, _p(v), Cout, Cin, _s())
             else:
@@ -884,6 +1000,9 @@ class WinoWeights:
 
     def ut4(self, l):
         return self._view('ut4', l) if ('ut4', l) in self._sets else None
+
+    def u4p(self, l):
+        return self._view('u4p', l) if ('u4p', l) in self._sets else None
 
 
 # ----------------------------------------------------------------------------------------- dense

@@ -35,6 +35,10 @@ from .. import runtime
 logger = logging.getLogger(__name__)
 
 MAX_BODY = 256 << 20
+# one image query on the C++ batch path (larger ones are routed to the generic Python path) and the most
+# the batch buffer of a replica may grow to
+MAX_QUERY = 1 << 20
+MAX_BATCH_BUF = 64 << 20
 
 _SIGS = {
     'rt_http_start': (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
@@ -53,6 +57,7 @@ _SIGS = {
     'rt_http_stats': (None, [ctypes.c_void_p, ctypes.c_void_p]),
     'rt_http_shutdown': (None, [ctypes.c_void_p]),
     'rt_http_stop': (None, [ctypes.c_void_p]),
+    'rt_http_set_max_query': (None, [ctypes.c_void_p, ctypes.c_longlong]),
 }
 _STAT_KEYS = ('requests', 'batches', 'batched_queries', 'generic_requests', 'errors', 'connections_accepted',
               'connections_open', 'queued_queries')
@@ -150,15 +155,21 @@ class NativePredictorServer:
         nd = ctypes.c_int(0)
         bid = ctypes.c_ulonglong(0)
         while self._running.is_set():
-            n = h.rt_http_next_batch(self._h, 100, buf.ctypes.data, cap, shape, ctypes.byref(nd), ctypes.byref(bid))
-            if n == 0:
-                continue
-            if n == -1:
-                break
-            per = int(math.prod(int(shape[i]) for i in range(nd.value)))
-            if n == -3:   # one query of this shape does not fit: grow to max_batch of them
-                cap = max(cap, per * self.max_batch)
-                buf = np.empty(cap, dtype=np.uint8)
+            try:
+                n = h.rt_http_next_batch(self._h, 100, buf.ctypes.data, cap, shape, ctypes.byref(nd),
+                                         ctypes.byref(bid))
+                if n == 0:
+                    continue
+                if n == -1:
+                    break
+                per = int(math.prod(int(shape[i]) for i in range(nd.value)))
+                if n == -3:   # one query of this shape does not fit: grow (bounded; C++ caps a query at MAX_QUERY)
+                    cap = max(cap, per, min(per * self.max_batch, MAX_BATCH_BUF))
+                    buf = np.empty(cap, dtype=np.uint8)
+                    continue
+            except Exception:   # never let the replica's only batch thread die
+                self._base['python_errors'] += 1
+                logger.error('batch loop error:\n%s', traceback.format_exc())
                 continue
             q = tuple(int(shape[i]) for i in range(nd.value))
             arr = buf[:n * per].reshape((int(n),) + q)
@@ -210,6 +221,7 @@ class NativePredictorServer:
                                   1 if self.predictor._fast_path() else 0)
         if not self._h:
             raise OSError('cannot listen on {}:{}'.format(self.host, self.port))
+        h.rt_http_set_max_query(self._h, MAX_QUERY)
         self.port = int(h.rt_http_port(self._h))
         self._running.set()
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self.generic_threads,

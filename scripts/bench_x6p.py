@@ -1,0 +1,67 @@
+"""Pre-split X6 GEMM (x6p.hip) on the 36-group GEMMs of the VGG-small pre-transformed F(4x4) layers
+(batch 256): microseconds and fp32-equivalent TFLOP/s of every tile / ring depth, against the X6 bf16
+peak (2.5 PFLOP/s / 6 products = 417 TFLOP/s).  usage: python scripts/bench_x6p.py [out.jsonl]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, '.')
+import torch  # noqa: E402
+
+from rafiki_amd.ops import _lib, f32 as S  # noqa: E402
+
+_lib.lib()
+PEAK = 2.5e15 / 6
+
+
+def t(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    s.record()
+    g.replay()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+# (name, M, N, K): conv fwd/dgrad Y'[q] = V[q] U[q]^T (M = tiles, N = out channels, K = in channels) and
+# weight gradients dU[q] = M^T[q] V^T[q]^T (M = Cout, N = Cin, K = tiles)
+SHAPES = [('c5f', 1024, 256, 256), ('c6f', 256, 512, 256), ('c7f', 256, 512, 512), ('c4d', 1024, 128, 256),
+          ('c6d', 256, 256, 512), ('c5w', 256, 256, 1024), ('c7w', 512, 512, 256)]
+res = []
+for name, M, N, K in SHAPES:
+    a = torch.randn(36, 3, M, K, device='cuda').to(torch.bfloat16)
+    b = torch.randn(36, 3, N, K, device='cuda').to(torch.bfloat16)
+    out = torch.empty(4, 36, M, N, device='cuda')
+    fl = 2.0 * 36 * M * N * K
+    r = dict(name=name, M=M, N=N, K=K)
+    times = {}
+    cfgs = [(t + kt, n, sp) for (t, n, sp) in S._XP_CFGS for kt in (0, 16) if not (kt and K % 64)]
+    if os.environ.get('X6P_CFGS'):   # e.g. "3,2,1;16,3,1" (timing-diagnostic runs: RAFIKI_X6P_DBG)
+        cfgs = [tuple(int(v) for v in c.split(',')) for c in os.environ['X6P_CFGS'].split(';')]
+    for (tile, nst, sp) in cfgs:
+        sp = S.x6p_splits(K, sp)
+        try:
+            times[(tile, nst, sp)] = t(lambda: S.x6p_gemm(a, b, out[:sp], M, N, K, groups=36, tile=tile, nst=nst,
+                                                          splits=sp))
+        except Exception:  # noqa: BLE001
+            times[(tile, nst, sp)] = float('inf')
+    best = min(times, key=times.get)
+    r['best'] = list(best)
+    r['us'] = round(times[best], 2)
+    r['tflops'] = round(fl / times[best] / 1e6, 1)
+    r['pct_x6_peak'] = round(100 * fl / (times[best] * 1e-6) / PEAK, 1)
+    r['all'] = {'{},{},{}'.format(*k): round(v, 1) for k, v in times.items()}
+    print(json.dumps(r), flush=True)
+    res.append(r)
+if len(sys.argv) > 1:
+    with open(sys.argv[1], 'w') as f:
+        for r in res:
+            f.write(json.dumps(r) + '\n')

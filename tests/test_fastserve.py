@@ -118,3 +118,51 @@ def test_bad_and_oversized_content_length(server):
         s.close()
         assert resp.split(b' ')[1] == code, resp
     assert requests.get(url + '/').status_code == 200   # server still serving
+
+
+def test_native_single_query_latency_with_idle_generic_thread():
+    """An image query must wake a batch thread at once even while the generic thread waits on its own
+    queue (one shared condition variable let notify_one wake the wrong waiter: ~100 ms stalls)."""
+    import time
+    from rafiki_amd.predictor import nativeserve
+    if not nativeserve.available():
+        pytest.skip('librafiki_runtime.so not built')
+    fake = FakePredictor()
+    srv = nativeserve.NativePredictorServer(fake, '127.0.0.1', 0).start()
+    try:
+        url = 'http://127.0.0.1:{}/predict'.format(srv.port)
+        s = requests.Session()
+        s.post(url, json={'query': [[1, 2], [3, 4]]}).raise_for_status()
+        worst = 0.0
+        for i in range(20):
+            time.sleep(0.02)   # let every waiter go back to sleep
+            t = time.perf_counter()
+            r = s.post(url, json={'query': [[i, 2], [3, 4]]})
+            worst = max(worst, time.perf_counter() - t)
+            assert r.status_code == 200
+        assert worst < 0.05, worst
+    finally:
+        srv.shutdown()
+
+
+def test_native_oversized_query_takes_the_generic_path(monkeypatch):
+    """A query larger than the batch path's per-query limit is served by the generic (Python) path
+    instead of growing the replica's batch buffer without bound."""
+    from rafiki_amd.predictor import nativeserve
+    if not nativeserve.available():
+        pytest.skip('librafiki_runtime.so not built')
+    monkeypatch.setattr(nativeserve, 'MAX_QUERY', 64)
+    fake = FakePredictor()
+    srv = nativeserve.NativePredictorServer(fake, '127.0.0.1', 0).start()
+    try:
+        url = 'http://127.0.0.1:{}/predict'.format(srv.port)
+        big = np.arange(100, dtype=np.uint8).reshape(10, 10).tolist()
+        r = requests.post(url, json={'query': big})
+        assert r.status_code == 200
+        assert np.allclose(r.json()['prediction'], fake._probs(np.asarray([big], dtype=np.uint8))[0])
+        c = srv.counters
+        assert c['generic_requests'] == 1 and c['batched_queries'] == 0   # the generic path, not the batch path
+        small = requests.post(url, json={'query': [[1, 2], [3, 4]]})
+        assert small.status_code == 200 and srv.counters['batched_queries'] == 1
+    finally:
+        srv.shutdown()

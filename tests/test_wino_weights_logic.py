@@ -49,6 +49,9 @@ def _tables(ww):
 
 def test_sets_per_layer_follow_map_size(monkeypatch):
     _, ww = _setup(monkeypatch)
+    # X6 planes of the pre-split PT path where its GEMM takes the shape (K = channels % 32, both >= 32)
+    assert ww.has('u4p', 0) and ww.has('ut4p', 0) and not ww.has('u4p', 2) and not ww.has('ut4p', 2)
+    assert ww.u4p(0).shape == (36, 3, 64, 32) and ww.u4p(0).dtype == torch.bfloat16
     assert ww.has('u2', 1) and ww.has('ut2', 1) and not ww.has('u4', 1)   # 6x6 map: no F(4x4) set
     assert ww.has('u4', 0) and ww.has('ut4', 2)
     assert ww.u4(1) is None and ww.u4(0).shape == (36, 64, 32) and ww.ut(2).shape == (16, 24, 40)
@@ -57,9 +60,9 @@ def test_sets_per_layer_follow_map_size(monkeypatch):
 def test_refresh_narrows_to_the_sets_a_step_used(monkeypatch):
     rec, ww = _setup(monkeypatch)
     ww.refresh()
-    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi']
+    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi', 'rk_x6p_w4_weights_multi']
     ww.end_step()                      # nothing read: keep everything
-    assert len(ww.live) == 10
+    assert len(ww.live) == 12
     ww.refresh()
     ww.lazy('u4', 0)()
     ww.lazy('ut2', 2)()
@@ -67,6 +70,11 @@ def test_refresh_narrows_to_the_sets_a_step_used(monkeypatch):
     assert ww.live == frozenset({('u4', 0), ('ut2', 2)})
     t = _tables(ww)
     assert set(t) == {'2', '4'}
+    # the plane family's meta rows carry offsets in bf16 elements (twice the float offset)
+    ww.live = frozenset({('u4p', 0), ('ut4p', 0)})
+    tp = _tables(ww)['p']
+    assert tp == {0: (2 * ww._sets[('u4p', 0)][0], 2 * ww._sets[('ut4p', 0)][0])}
+    ww.live = frozenset({('u4', 0), ('ut2', 2)})
     assert t['2'] == {2: (-1, ww._sets[('ut2', 2)][0])}          # gradient set only
     assert t['4'] == {0: (ww._sets[('u4', 0)][0], -1)}           # forward set only
     rec.calls.clear()
@@ -85,7 +93,7 @@ def test_no_narrowing_inside_capture(monkeypatch):
     ww.refresh()
     ww.lazy('u2', 0)()
     ww.end_step()
-    assert len(ww.live) == 10                                      # tables cannot be rebuilt in a capture
+    assert len(ww.live) == 12                                      # tables cannot be rebuilt in a capture
 
 
 def test_sconvwt_refresh_is_lazy(monkeypatch):
