@@ -168,3 +168,66 @@ extern "C" int rk_wflip_t(const float* w, float* out, int Co, int Ci, int taps, 
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
+
+// ---- box-filter weights of the fused resampling convs (pg_gans.py:1035-1036 / 1055-1056) and their adjoints
+// The 4x4 kernel W4[a][b] = s * sum of w3[ky][kx] over ky in {a-1, a}, kx in {b-1, b} (the four 1-pixel shifts
+// of the zero-padded 3x3 kernel; flip: of the 180-degree-rotated kernel).  One thread per (co, ci):
+//   mode 0: down  w [Co][9][Ci]  -> W4 [Co][16][Ci]          (s = 1/4)
+//   mode 1: adjoint of mode 0: g4 [Co][16][Ci] -> g3 [Co][9][Ci]
+//   mode 2: up    w [Co][9][Ci]  -> W4^T [Ci][16][Co], flipped (s = 1)
+//   mode 3: adjoint of mode 2: g4 [Ci][16][Co] -> g3 [Co][9][Ci]
+namespace {
+__global__ __launch_bounds__(256) void box_weights_kernel(int mode, const float* __restrict__ src,
+                                                         float* __restrict__ dst, int Co, int Ci, float s) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)Co * Ci) return;
+  // modes 2 / 3 index the transposed [Ci][16][Co] layout with co fastest (coalesced on that side)
+  const bool tr = mode >= 2;
+  const int co = tr ? (int)(i % Co) : (int)(i / Ci);
+  const int ci = tr ? (int)(i / Co) : (int)(i % Ci);
+  const bool flip = mode >= 2;
+  if (mode == 0 || mode == 2) {
+    float g[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) g[q] = src[((long long)co * 9 + q) * Ci + ci];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        float v = 0.f;
+#pragma unroll
+        for (int ky = a - 1; ky <= a; ++ky)
+#pragma unroll
+          for (int kx = b - 1; kx <= b; ++kx)
+            if (ky >= 0 && ky < 3 && kx >= 0 && kx < 3) v += g[flip ? 8 - (ky * 3 + kx) : ky * 3 + kx];
+        const int t = a * 4 + b;
+        dst[tr ? ((long long)ci * 16 + t) * Co + co : ((long long)co * 16 + t) * Ci + ci] = s * v;
+      }
+  } else {
+    float g4[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      g4[t] = src[tr ? ((long long)ci * 16 + t) * Co + co : ((long long)co * 16 + t) * Ci + ci];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const int qq = flip ? 8 - q : q;   // the 3x3 tap this output is, before the flip
+      const int ky = qq / 3, kx = qq % 3;
+      float v = 0.f;
+#pragma unroll
+      for (int a = ky; a <= ky + 1; ++a)
+#pragma unroll
+        for (int b = kx; b <= kx + 1; ++b) v += g4[a * 4 + b];
+      dst[((long long)co * 9 + q) * Ci + ci] = s * v;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int rk_box_weights(int mode, const float* src, float* dst, int Co, int Ci, float scale, void* stream) {
+  if (mode < 0 || mode > 3 || Co <= 0 || Ci <= 0 || !src || !dst) return RK_EBADARG;
+  const long long n = (long long)Co * Ci;
+  hipLaunchKernelGGL(box_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mode,
+                     src, dst, Co, Ci, scale);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}

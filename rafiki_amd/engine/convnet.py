@@ -239,6 +239,8 @@ class ConvNetEngine:
     # data gradients as forward convs of dy with flipped/transposed weights (F.ConvWT, one transpose
     # launch per step): the forward kernels' K-inner weight operand and tiles are the faster ones
     dgrad_wt = os.environ.get('RAFIKI_DGRAD_WT', '1') != '0'
+    # fp32 path: the classifier head (output layer, softmax-xent, its gradients) as two fused launches
+    fused_head = os.environ.get('RAFIKI_FUSED_HEAD', '1') != '0'
 
     def _side_stream(self):
         st = getattr(self, '_wgrad_stream', None)
@@ -410,15 +412,32 @@ class ConvNetEngine:
         for (name, di, do, _) in self.fcs:
             z = S.linear(z, fl.w(name + '.w'), fl.w(name + '.b'), act=F.ACT_RELU)
             fc_in.append(z)
-        logits = S.linear(z, fl.w('out.w'), fl.w('out.b'))
         dlogits = torch.empty((B, self.ncls_p), dtype=torch.float32, device=self.device)
-        S.softmax_xent(logits, labels, self.num_classes, dlogits=dlogits, loss_sum=self.loss_sum,
-                       correct=self.correct, counted=self.seen)
-        # ---- backward
-        S.linear_dw(dlogits, fc_in[-1], out=fl.g('out.w'))
-        S.colsum(dlogits, fl.g('out.b'))
-        d, wname = dlogits, 'out'
-        for k in range(len(self.fcs) - 1, -1, -1):
+        k_top = len(self.fcs) - 1
+        if self.fused_head and S.head_ok(self.ncls_p, self.d_last):
+            # output layer + softmax-xent + d(hidden) in one launch, the output weight / bias and the top
+            # hidden layer's bias gradients in a second (csrc/kernels/head.hip)
+            gated = k_top >= 0
+            dz = torch.empty((B, self.d_last), dtype=torch.float32, device=self.device)
+            S.head_fwd_bwd(z, fl.w('out.w'), fl.w('out.b'), labels, self.num_classes, dlogits=dlogits, dz=dz,
+                           gated=gated, loss_sum=self.loss_sum, correct=self.correct, counted=self.seen)
+            S.head_dw(z, dlogits, dz, dw=fl.g('out.w'), db=fl.g('out.b'),
+                      dbh=fl.g(self.fcs[k_top][0] + '.b') if gated else None)
+            d = dz
+            if gated:
+                S.linear_dw(d, fc_in[k_top], out=fl.g(self.fcs[k_top][0] + '.w'))
+                wname, k_top = self.fcs[k_top][0], k_top - 1
+            else:
+                wname = None   # dz is already the gradient of the flattened features
+        else:
+            logits = S.linear(z, fl.w('out.w'), fl.w('out.b'))
+            S.softmax_xent(logits, labels, self.num_classes, dlogits=dlogits, loss_sum=self.loss_sum,
+                           correct=self.correct, counted=self.seen)
+            # ---- backward
+            S.linear_dw(dlogits, fc_in[-1], out=fl.g('out.w'))
+            S.colsum(dlogits, fl.g('out.b'))
+            d, wname = dlogits, 'out'
+        for k in range(k_top, -1, -1):
             name = self.fcs[k][0]
             d = S.linear_dx(d, fl.w(wname + '.w'), gate=fc_in[k + 1])
             S.linear_dw(d, fc_in[k], out=fl.g(name + '.w'))
@@ -426,7 +445,8 @@ class ConvNetEngine:
             wname = name
         if not self.blocks and not self.input_bn:
             return
-        d = S.linear_dx(d, fl.w(wname + '.w'))
+        if wname is not None:
+            d = S.linear_dx(d, fl.w(wname + '.w'))
         if self.input_bn:
             raw, coeffs = in_saved
             S.bn_bwd(d.view(B, 1, 1, self.feat_dim), raw, coeffs, fl.w('in_bn.gamma'), accs[-1][1], pool=False,

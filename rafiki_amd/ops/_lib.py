@@ -102,9 +102,13 @@ _SIGS = {
                                                                  f32, i64, i64, vp],
     "rk_resample2x": [i32, i32, vp, vp, i32, i32, i32, i32, f32, vp],
     "rk_s2t_weights": [vp, vp, i32, i32, vp],
+    "rk_box_weights": [i32, vp, vp, i32, i32, f32, vp],
     "rk_wflip_t": [vp, vp, i32, i32, i32, vp],
     "rk_mbstd_f32": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_lrelu_pixelnorm_f32": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
+    # fused classifier head (head.hip)
+    "rk_head_fwd_bwd": [vp, i32, i32, vp, vp, i32, vp, i32, f32, vp, vp, i32, vp, vp, vp, vp],
+    "rk_head_dw": [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp],
     # pre-split X6 GEMMs (x6p.hip) and their plane producers (winograd4.hip)
     "rk_x6p_gemm": [i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i32, i32, i32, i64,
                     i64, i64, vp],

@@ -33,6 +33,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as TF
 
+from . import _lib
 from . import f32 as S
 from . import functional as F
 
@@ -331,44 +332,57 @@ def _box4(w3):
     return wp[:, 1:, 1:] + wp[:, :-1, 1:] + wp[:, 1:, :-1] + wp[:, :-1, :-1]
 
 
-_BOX_MATS = {}
+def _box_launch(mode, src, co, cin):
+    """rk_box_weights (resample.hip): mode 0 down [Co,9Ci]->[Co,16Ci] (x1/4), 1 its adjoint, 2 up (flipped,
+    transposed) [Co,9Ci]->[Ci,16Co], 3 its adjoint."""
+    src = src.contiguous()
+    shape = {0: (co, 16 * cin), 1: (co, 9 * cin), 2: (cin, 16 * co), 3: (co, 9 * cin)}[mode]
+    out = torch.empty(shape, device=src.device, dtype=torch.float32)
+    _lib.call("rk_box_weights", int(mode), S._p(src), S._p(out), co, cin, 0.25 if mode < 2 else 1.0, S._s())
+    return out
 
 
-def _box_mat(device, flip: bool, scale: float):
-    """[16, 9] 0/1 (x scale) matrix of _box4: W4[a][b] = sum of w3[ky][kx] over ky in {a-1, a}, kx in {b-1, b}
-    (flip: of the 180-degree-rotated kernel)."""
-    key = (str(device), flip, scale)
-    m = _BOX_MATS.get(key)
-    if m is None:
-        m = torch.zeros(16, 9)
-        for a in range(4):
-            for b in range(4):
-                for ky in (a - 1, a):
-                    for kx in (b - 1, b):
-                        if 0 <= ky < 3 and 0 <= kx < 3:
-                            q = ky * 3 + kx
-                            m[a * 4 + b, 8 - q if flip else q] = scale
-        m = _BOX_MATS[key] = m.to(device)
-    return m
+class BoxWeightsFn(torch.autograd.Function):
+    """The resampling convs' 4x4 box-filter weights of a 3x3 kernel (linear in w) on one native kernel,
+    backward = the adjoint kernel (itself differentiable: WGAN-GP's double backward goes through it)."""
+
+    @staticmethod
+    def forward(ctx, w, co, cin, mode):
+        ctx.co, ctx.cin, ctx.mode = co, cin, mode
+        return _box_launch(mode, w, co, cin)
+
+    @staticmethod
+    def backward(ctx, g):
+        return BoxWeightsAdjFn.apply(g, ctx.co, ctx.cin, ctx.mode), None, None, None
+
+
+class BoxWeightsAdjFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, co, cin, mode):
+        ctx.co, ctx.cin, ctx.mode = co, cin, mode
+        return _box_launch(mode + 1, g, co, cin)
+
+    @staticmethod
+    def backward(ctx, gg):
+        return BoxWeightsFn.apply(gg, ctx.co, ctx.cin, ctx.mode), None, None, None
 
 
 def down_weights(w, cin):
-    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cout, 16*Cin] of conv3x3 + 2x2 box downscale: one batched
-    GEMM ([16, 9] box matrix x every output channel's [9, Cin] taps) forward and one backward, instead of
-    pad + four shifted adds + scale (and their adjoints) per call."""
+    """3x3 weights [Cout, 9*Cin] -> S2 weights [Cout, 16*Cin] of conv3x3 + 2x2 box downscale (one native
+    kernel forward, its adjoint backward: no pad + four shifted adds + scale, no vendor GEMM)."""
     co = w.shape[0]
-    if w.device.type != 'cuda':
+    if w.device.type != 'cuda' or w.dtype != F32:
         return (_box4(w.reshape(co, 3, 3, cin)) * 0.25).reshape(co, 16 * cin)
-    return torch.matmul(_box_mat(w.device, False, 0.25), w.reshape(co, 9, cin)).reshape(co, 16 * cin)
+    return BoxWeightsFn.apply(w.reshape(co, 9 * cin), co, cin, 0)
 
 
 def up_weights(w, cin):
     """3x3 weights [Cout, 9*Cin] -> S2 weights [Cin, 16*Cout] whose adjoint S2T is upscale2d + conv3x3 (the
-    tap flip folded into the box matrix; one batched GEMM + one transposing copy)."""
+    tap flip and the transpose folded into the same native kernel)."""
     co = w.shape[0]
-    if w.device.type != 'cuda':
+    if w.device.type != 'cuda' or w.dtype != F32:
         return _box4(w.reshape(co, 3, 3, cin).flip(1, 2)).permute(3, 1, 2, 0).reshape(cin, 16 * co)
-    return torch.matmul(_box_mat(w.device, True, 1.0), w.reshape(co, 9, cin)).permute(2, 1, 0).reshape(cin, 16 * co)
+    return BoxWeightsFn.apply(w.reshape(co, 9 * cin), co, cin, 2)
 
 
 def resample_via_winograd(full_hw: int, channels: int) -> bool:

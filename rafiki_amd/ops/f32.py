@@ -1200,6 +1200,34 @@ def softmax_xent(logits, labels, ncls, *, dlogits=None, probs=None, loss_sum=Non
               _p(correct), _p(counted), _s())
 
 
+HEAD_NC = (8, 16, 32)
+
+
+def head_ok(ncls_p: int, D: int) -> bool:
+    """Shapes the fused classifier head (csrc/kernels/head.hip) takes."""
+    return ncls_p in HEAD_NC and D % 32 == 0 and D > 0
+
+
+def head_fwd_bwd(z, w, bias, labels, ncls, *, dlogits, dz, gated, loss_sum=None, correct=None, counted=None,
+                 grad_scale=None):
+    """Output layer + softmax cross-entropy + its data gradient in one launch: z [B][D] -> dlogits [B][NC]
+    ((softmax - onehot) * grad_scale), dz [B][D] = dlogits W (gated by z > 0 when ``gated``)."""
+    _check(z, 'head z')
+    B, D = z.shape
+    NC = w.shape[0]
+    assert w.shape == (NC, D) and dlogits.shape == (B, NC) and dz.shape == (B, D)
+    _lib.call("rk_head_fwd_bwd", _p(z), B, D, _p(w), _p(bias), NC, _p(labels), int(ncls),
+              float(1.0 / max(1, B) if grad_scale is None else grad_scale), _p(dlogits), _p(dz), int(bool(gated)),
+              _p(loss_sum), _p(correct), _p(counted), _s())
+
+
+def head_dw(z, dlogits, dz, *, dw, db=None, dbh=None):
+    """dw [NC][D] = dlogits^T z, db = colsum(dlogits), dbh = colsum(dz) (the hidden layer's bias gradient)."""
+    B, D = z.shape
+    NC = dlogits.shape[1]
+    _lib.call("rk_head_dw", _p(z), _p(dlogits), _p(dz), B, D, NC, _p(dw), _p(db), _p(dbh), _s())
+
+
 def pack_nhwc(images, cpad=4, scale=1.0, shift=0.0, out=None, nhwc=False):
     """uint8/float32 NCHW (``nhwc``: NHWC) -> fp32 NHWC with channels padded to ``cpad``, x*scale+shift."""
     if nhwc:

@@ -432,3 +432,99 @@ def test_in_place_weight_grad_accumulation_matches_autograd():
     c = grads(True)
     for u, v in zip(a, c):
         assert frob(v, u) < 1e-6, frob(v, u)
+
+
+# ---- fp32 (the default PG-GAN precision) unit tests of the fused elementwise kernels against fp64 oracles
+def _rel64(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+@pytest.mark.parametrize("P,C,with_bias", [(64 * 16, 512, True), (4 * 16 * 16, 256, False), (300, 512, False),
+                                          (77, 256, True), (50, 1024, False), (33, 24, True)])
+def test_lrelu_pixelnorm_fp32_vs_fp64(P, C, with_bias):
+    """lrelu_pn_fwd / bwd kernels (fp32 instantiation, pg_gans.py:993-995 pixel norm after leaky ReLU), with
+    and without the fused bias, on lod-0 / lod-3 shaped rows: relative Frobenius error <= 1e-5."""
+    from rafiki_amd.ops import autograd as A
+    g = torch.Generator().manual_seed(P + C)
+    x = torch.randn(P, C, generator=g)
+    b = torch.randn(C, generator=g) * 0.3 if with_bias else None
+    dz = torch.randn(P, C, generator=g)
+    xg = x.to(DEV).requires_grad_(True)
+    bg = b.to(DEV).requires_grad_(True) if with_bias else None
+    z = A.lrelu_pixel_norm(xg, bg)
+    z.backward(dz.to(DEV))
+    xr = x.double().requires_grad_(True)
+    br = b.double().requires_grad_(True) if with_bias else None
+    y = F.leaky_relu(xr + br if with_bias else xr, 0.2)
+    zr = y * torch.rsqrt(y.square().mean(-1, keepdim=True) + 1e-8)
+    zr.backward(dz.double())
+    assert _rel64(z, zr) <= 1e-5
+    assert _rel64(xg.grad, xr.grad) <= 1e-5
+    if with_bias:
+        assert _rel64(bg.grad, br.grad) <= 1e-5
+
+
+def _mbstd64(x, g, segs, extra):
+    out = []
+    for t in x.chunk(segs):
+        N, H, W, C = t.shape
+        y = t.reshape(g, -1, H, W, C)
+        y = y - y.mean(0, keepdim=True)
+        y = (y.square().mean(0) + 1e-8).sqrt().mean((1, 2, 3))
+        y = y.reshape(1, -1, 1, 1, 1).expand(g, -1, H, W, 1).reshape(N, H, W, 1)
+        parts = [t, y] + ([t.new_zeros((N, H, W, extra))] if extra else [])
+        out.append(torch.cat(parts, -1))
+    return torch.cat(out, 0)
+
+
+@pytest.mark.parametrize("N,H,C,segs", [(64, 4, 512, 1), (16, 4, 512, 2), (8, 4, 24, 1), (12, 2, 40, 3),
+                                        (32, 4, 128, 2)])
+def test_minibatch_stddev_fp32_vs_fp64(N, H, C, segs):
+    """mbstd_vec_a / _b kernels (fp32 instantiation, pg_gans.py:1070-1082): forward, backward and
+    backward-of-backward (the WGAN-GP penalty differentiates through it) <= 1e-5 against fp64."""
+    from rafiki_amd.ops import autograd as A
+    g = torch.Generator().manual_seed(N * H + C)
+    x = torch.randn(N, H, H, C, generator=g)
+    cp = C + 1 + (-(C + 1)) % 8
+    Wt = torch.randn(N, H, H, cp, generator=g)
+    V = torch.randn(N, H, H, C, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    Wd = Wt.to(DEV).requires_grad_(True)
+    out = A.minibatch_stddev(xd, 4, pad_to=8, segs=segs)
+    (gx,) = torch.autograd.grad((out * Wd).sum(), xd, create_graph=True)
+    (gx * V.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    W64 = Wt.double().requires_grad_(True)
+    o64 = _mbstd64(x64, min(4, N // segs), segs, cp - C - 1)
+    (g64,) = torch.autograd.grad((o64 * W64).sum(), x64, create_graph=True)
+    (g64 * V.double()).sum().backward()
+    assert _rel64(out, o64) <= 1e-5
+    assert _rel64(gx, g64) <= 1e-5
+    assert _rel64(xd.grad, x64.grad) <= 1e-5
+    assert _rel64(Wd.grad, W64.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("co,cin", [(64, 32), (512, 512), (3, 40)])
+def test_box_weights_kernel_and_adjoints(co, cin):
+    """rk_box_weights (the resampling convs' 4x4 box weights) forward, backward and double backward vs the
+    fp64 pad + shifted-add composite (no vendor GEMM on this path any more)."""
+    from rafiki_amd.ops import autograd as A
+    g = torch.Generator().manual_seed(co + cin)
+    w = torch.randn(co, 9 * cin, generator=g)
+    for fn in (A.down_weights, A.up_weights):
+        wd = w.to(DEV).requires_grad_(True)
+        out = fn(wd, cin)
+        gy = torch.randn(out.shape, generator=g)
+        (gw,) = torch.autograd.grad(out, wd, gy.to(DEV), create_graph=True)
+        v = torch.randn(gw.shape, generator=g)
+        w64 = w.double().requires_grad_(True)
+        o64 = fn(w64, cin)            # CPU composite in fp64
+        (g64,) = torch.autograd.grad(o64, w64, gy.double())
+        assert _rel64(out, o64) <= 1e-6
+        assert _rel64(gw, g64) <= 1e-6
+        # the adjoint is linear and itself differentiable: d<gw, v>/d gy == fn(v)
+        gyd = gy.to(DEV).requires_grad_(True)
+        (gw2,) = torch.autograd.grad(fn(wd, cin), wd, gyd, create_graph=True)
+        (dgy,) = torch.autograd.grad((gw2 * v.to(DEV)).sum(), gyd)
+        assert _rel64(dgy, fn(v.double(), cin)) <= 1e-6
