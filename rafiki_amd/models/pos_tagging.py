@@ -136,8 +136,10 @@ class PyBiLstm(BaseModel):
         self.device = trial_context().device
 
     def _create(self):
+        import torch
         import torch.nn as nn
-        from rafiki_amd.ops.lstm import bilstm
+        from rafiki_amd.ops.autograd import dense
+        from rafiki_amd.ops.lstm import bilstm, embedding
         k = self._knobs
         V = len(self._word_dict) + 2  # 0 = pad, 1 = unknown
 
@@ -152,9 +154,13 @@ class PyBiLstm(BaseModel):
                 s.rec_dtype = k.get('dtype') or default_dtype()   # fp32 (reference precision) unless opted into bf16
 
             def forward(s, x):
-                # gfx950 persistent-recurrence BiLSTM kernels on GPU (rafiki_amd.ops.lstm)
-                h = bilstm(s.drop(s.emb(x)), s.lstm, dtype=s.rec_dtype)
-                return s.out(h)
+                # gfx950 kernels on GPU: embedding gather / sorted scatter-sum gradient, persistent-recurrence
+                # BiLSTM with its GEMMs on sgemm (rafiki_amd.ops.lstm), the output layer on sgemm
+                h = bilstm(s.drop(embedding(x, s.emb)), s.lstm, dtype=s.rec_dtype)
+                o = s.out
+                if h.is_cuda and h.dtype == torch.float32 and o.in_features % 4 == 0 and o.out_features % 4 == 0:
+                    return dense(h.reshape(-1, o.in_features), o.weight, o.bias).reshape(h.shape[:-1] + (-1,))
+                return o(h)
 
         return Net().to(self.device)
 

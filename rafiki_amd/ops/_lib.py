@@ -106,6 +106,9 @@ _SIGS = {
     "rk_wflip_t": [vp, vp, i32, i32, i32, vp],
     "rk_mbstd_f32": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_lrelu_pixelnorm_f32": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
+    # embedding gather / deterministic scatter-sum gradient (embed.hip)
+    "rk_embedding_fwd": [vp, vp, vp, i32, i32, vp],
+    "rk_embedding_bwd": [vp, vp, vp, i32, i32, i32, i32, vp, i64, vp],
     # fused classifier head (head.hip)
     "rk_head_fwd_bwd": [vp, i32, i32, vp, vp, i32, vp, i32, f32, vp, vp, i32, vp, vp, vp, vp],
     "rk_head_dw": [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp],
@@ -120,6 +123,8 @@ _SIGS = {
 }
 
 _OPTIONAL: set[str] = set()
+# non-int return types
+_RESTYPES = {"rk_embedding_bwd_ws": (C.c_longlong, [i32])}
 
 
 class NativeLibraryError(RuntimeError):
@@ -152,6 +157,10 @@ def lib():
                 raise NativeLibraryError(f"{KERNEL_LIB} lacks symbol {name}: rebuild it")
             fn.argtypes = args
             fn.restype = C.c_int
+        for name, (rt, args) in _RESTYPES.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = rt
         _lib = h
         return _lib
 

@@ -4,8 +4,12 @@ Reference: examples/models/pos_tagging/PyBiLstm.py:249-268 (``nn.LSTM(Ew, h, bat
 bidirectional=True)`` over a padded batch, zero initial state).  Split of the work:
 
 * the input projection ``x @ W_ih^T + b_ih + b_hh`` of every timestep and both directions is one
-  plain GEMM (hipBLASLt through torch), as are the three weight/input-gradient GEMMs of the
-  backward — they have no time dependence;
+  GEMM on the in-tree fp32 kernels (``ops.f32.linear``: sgemm.hip, f32 / X6 loops, autotuned, bias in
+  the epilogue), as are the backward's input gradient (``linear_dx``), the two weight gradients
+  (``linear_dw``, W_hh's per direction over strided views) and the bias gradient (``colsum``) — they
+  have no time dependence;
+* the word embedding (PyBiLstm.py:249) is ``embedding``: an in-tree gather kernel forward and a
+  deterministic sort + segmented-sum scatter backward (csrc/kernels/embed.hip);
 * the sequential part (T steps of ``h @ W_hh^T`` + the cell) is ONE kernel launch per direction
   pair, forward and backward: ``rk_lstm_fwd32`` / ``rk_lstm_bwd32`` (exact fp32 on
   v_mfma_f32_16x16x4_f32, the reference's precision, default) or ``rk_lstm_fwd`` / ``rk_lstm_bwd``
@@ -19,7 +23,48 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from . import f32 as S
 from .functional import _p, _s
+
+
+def _native_dense(*dims) -> bool:
+    """The in-tree fp32 GEMMs take 16-B (4-float) rows: every non-batch extent a multiple of 4."""
+    return all(d % 4 == 0 for d in dims)
+
+
+class EmbeddingFn(torch.autograd.Function):
+    """out = W[ids] (rk_embedding_fwd); dW by a stable sort of the token ids and an in-order segmented sum
+    per id (rk_embedding_bwd: bit-reproducible, no float atomics); padding_idx's row gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, ids, w, padding_idx):
+        ids = ids.contiguous().to(torch.int64)
+        n, (V, E) = ids.numel(), w.shape
+        out = torch.empty(ids.shape + (E,), device=w.device, dtype=torch.float32)
+        _lib.call("rk_embedding_fwd", _p(ids), _p(w.contiguous()), _p(out), n, E, _s())
+        ctx.save_for_backward(ids)
+        ctx.dims = (V, E, -1 if padding_idx is None else int(padding_idx))
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gy):
+        (ids,) = ctx.saved_tensors
+        V, E, pad = ctx.dims
+        n = ids.numel()
+        gw = torch.empty((V, E), device=gy.device, dtype=torch.float32)
+        nbytes = int(_lib.lib().rk_embedding_bwd_ws(n))
+        ws = torch.empty(nbytes, device=gy.device, dtype=torch.uint8)
+        _lib.call("rk_embedding_bwd", _p(ids), _p(gy.contiguous().float()), _p(gw), n, V, E, pad, _p(ws), nbytes, _s())
+        return None, gw, None
+
+
+def embedding(ids, emb: torch.nn.Embedding):
+    """``emb(ids)`` on the gfx950 kernels (fp32 weights, E % 4 == 0); torch's own elsewhere."""
+    w = emb.weight
+    if ids.device.type != 'cuda' or w.dtype != torch.float32 or w.shape[1] % 4 or emb.max_norm is not None:
+        return emb(ids)
+    return EmbeddingFn.apply(ids, w, emb.padding_idx)
 
 
 def _hp(H: int) -> int:
@@ -50,8 +95,11 @@ class BiLstmFn(torch.autograd.Function):
         # fp32: W_hh as is for the forward, W_hh^T [2, HP, 4HP] for the BPTT (float4 along k)
         w_rec = w_hh_p.contiguous() if f32 else w_hh_p.to(torch.bfloat16).contiguous()
         b_p = _pad_gate_rows(b.detach().float(), H, HP)                                  # [2, 4HP]
-        x2 = x.detach().float().reshape(T * B, E)
-        gin = torch.addmm(b_p.reshape(1, -1), x2, w_ih_p.reshape(2 * 4 * HP, E).t()).contiguous()
+        x2 = x.detach().float().reshape(T * B, E).contiguous()
+        if _native_dense(E):
+            gin = S.linear(x2, w_ih_p.reshape(2 * 4 * HP, E), b_p.reshape(-1).contiguous())
+        else:
+            gin = torch.addmm(b_p.reshape(1, -1), x2, w_ih_p.reshape(2 * 4 * HP, E).t()).contiguous()
         hout = torch.empty((T, B, 2, HP), device=x.device, dtype=torch.float32)
         gsave = torch.empty((T, B, 2, 4 * HP), device=x.device, dtype=torch.float32)
         csave = torch.empty((T, B, 2, HP), device=x.device, dtype=torch.float32)
@@ -75,21 +123,28 @@ class BiLstmFn(torch.autograd.Function):
         _lib.call("rk_lstm_bwd32" if ctx.f32 else "rk_lstm_bwd", _p(w_rec), T, B, HP, _p(dh), _p(gsave), _p(csave),
                   _p(dg), _s())
         dg2 = dg.reshape(T * B, 2 * 4 * HP)
+        native = _native_dense(E)
         gx = gw_ih = gw_hh = gb = None
         if ctx.needs_input_grad[0]:
-            gx = (dg2 @ w_ih_p.reshape(2 * 4 * HP, E)).reshape(T, B, E)
+            w2 = w_ih_p.reshape(2 * 4 * HP, E)
+            gx = (S.linear_dx(dg2, w2) if native else dg2 @ w2).reshape(T, B, E)
         if ctx.needs_input_grad[1]:
-            gw = torch.einsum('ndg,ne->dge', dg2.reshape(T * B, 2, 4 * HP), x2)          # [2, 4HP, E]
+            gw = S.linear_dw(dg2, x2) if native else \
+                torch.einsum('ndg,ne->dge', dg2.reshape(T * B, 2, 4 * HP), x2)            # [2, 4HP, E]
             gw_ih = gw.reshape(2, 4, HP, E)[:, :, :H].reshape(2, 4 * H, E)
         if ctx.needs_input_grad[2]:
             # h_{t-1} of the forward direction / h_{t+1} of the reverse one (zero initial state)
             hp = torch.zeros_like(hout)
             hp[1:, :, 0] = hout[:-1, :, 0]
             hp[:-1, :, 1] = hout[1:, :, 1]
-            gw = torch.einsum('tbdg,tbdh->dgh', dg, hp)                                     # [2, 4HP, HP]
+            gw = torch.empty((2, 4 * HP, HP), device=gy.device, dtype=torch.float32)
+            for d in range(2):   # per direction over strided row views: [TB, 4HP]^T [TB, HP]
+                S.linear_dw(dg.view(T * B, 2, 4 * HP)[:, d], hp.view(T * B, 2, HP)[:, d], out=gw[d])
             gw_hh = gw.reshape(2, 4, HP, HP)[:, :, :H, :H].reshape(2, 4 * H, H)
         if ctx.needs_input_grad[3]:
-            gb = dg.sum((0, 1)).reshape(2, 4, HP)[:, :, :H].reshape(2, 4 * H)
+            gsum = torch.empty(2 * 4 * HP, device=gy.device, dtype=torch.float32)
+            S.colsum(dg2, gsum)
+            gb = gsum.reshape(2, 4, HP)[:, :, :H].reshape(2, 4 * H)
         return gx, gw_ih, gw_hh, gb, None
 
 
