@@ -451,6 +451,45 @@ class GraphedRounds:
             self.graphs.clear()
         self.seen.clear()
 
+    def run_segments(self, key, segs):
+        """A round as a list of ('g', fn) compute segments and ('e', fn) eager collective segments
+        (data-parallel rounds: gradients -> all-reduce -> optimizer).  Each compute segment becomes its
+        own graph (one memory pool per key, segments replayed in capture order); the collectives run
+        eagerly between replays, so no collective is ever inside a capture and the process group's
+        watchdog has nothing of ours to race (no sleep, deterministic)."""
+        if not self.enabled:
+            for _, fn in segs:
+                fn()
+            return
+        gs = self.graphs.get(key)
+        if gs is not None:
+            for (kind, fn), g in zip(segs, gs):
+                if g is None:
+                    fn()
+                else:
+                    g.replay()
+            return
+        if key not in self.seen:
+            self.seen.add(key)
+            for _, fn in segs:
+                fn()
+            return
+        device_sync()
+        pool = torch.cuda.graph_pool_handle()
+        gs = []
+        for kind, fn in segs:
+            if kind == 'e':
+                fn()
+                gs.append(None)
+                continue
+            g = torch.cuda.CUDAGraph()
+            with _capture(g, pool=pool):
+                fn()
+            g.replay()   # a capture records, it does not execute: run it before the next segment
+            gs.append(g)
+            self.captures += 1
+        self.graphs[key] = gs
+
     def run(self, key, fn):
         if not self.enabled:
             fn()
@@ -632,10 +671,18 @@ class PgGan(BaseModel):
         # schedule, and torch exposes no hook to wait until it has retired them, so a capture could
         # still overlap such a poll (GraphedRounds.run waits 0.3 s, ~3 watchdog periods: a residual
         # race, not a guarantee).  Default: data-parallel rounds run eager, single-GPU ones captured.
-        capturable = g_ar is None or (self.ctx.dist.backend == 'nccl'
+        # Data-parallel rounds are captured by SEGMENTS: gradients (captured) -> bucketed all-reduce
+        # (eager, between replays) -> optimizer (captured), so no collective is inside a capture.  The
+        # older whole-round capture with the collectives inside stays an opt-in
+        # (RAFIKI_PGGAN_GRAPH_COLLECTIVES=1, nccl only: it waits 0.3 s for the watchdog).  With eager
+        # collective segments a gloo group (the one-box multi-rank rehearsal) is capturable too.
+        whole = g_ar is not None and (self.ctx.dist.backend == 'nccl'
                                       and os.environ.get('RAFIKI_PGGAN_GRAPH_COLLECTIVES', '0') == '1')
+        segmented = g_ar is not None and not whole
+        capturable = g_ar is None or whole or segmented
         graphs = GraphedRounds(dev.type == 'cuda' and capturable and bool(knobs.get('cuda_graph', True))
-                               and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0', collectives=g_ar is not None)
+                               and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0', collectives=whole)
+        self.segmented = segmented
         self.graphs = graphs
         acc = torch.zeros(6, dtype=torch.float32, device=dev)
         level_cache = {}
@@ -676,10 +723,18 @@ class PgGan(BaseModel):
             def round_fn():
                 self.train_round(sched.lod, mb, level, labels_all, rng, G_opt, D_opt, acc, D_repeats=D_repeats,
                                  G_smoothing=G_smoothing, d_ar=d_ar, g_ar=g_ar)
+            segs = (self.round_segments(sched.lod, mb, level, labels_all, rng, G_opt, D_opt, acc,
+                                        D_repeats=D_repeats, G_smoothing=G_smoothing, d_ar=d_ar, g_ar=g_ar)
+                    if segmented else None)
             for _ in range(minibatch_repeats):
-                if frac == 0:
+                if frac == 0 and segs is not None:
+                    graphs.run_segments(key, segs)
+                elif frac == 0:
                     graphs.run(key, round_fn)
-                else:   # LOD transition: the fade factor changes every tick, run eagerly
+                elif segs is not None:   # LOD transition: the fade factor changes every tick, run eagerly
+                    for _, fn in segs:
+                        fn()
+                else:
                     round_fn()
                 cur_nimg += sched.minibatch * D_repeats
                 nD += D_repeats
@@ -727,9 +782,50 @@ class PgGan(BaseModel):
         else:
             opt.skip_flag.fill_(0 if bool(torch.isfinite(flat.grad).all()) else 1)
 
+    def round_segments(self, lod, mb, level, labels_all, rng, G_opt, D_opt, acc, *, D_repeats=1, G_smoothing=0.99,
+                       d_ar=None, g_ar=None):
+        """train_round as segments for GraphedRounds.run_segments: per D step gradients ('g'), the
+        bucketed all-reduce of D.grad ('e'), then mean + finite guard + Adam + Gs EMA ('g'); likewise
+        the G step.  Adjacent compute segments are merged (D_repeats + 2 graphs per round)."""
+        nets = self.nets
+
+        def d_grads():
+            acc[:4] += self._d_step(lod, mb, level, labels_all, rng, D_opt, None, apply=False)
+
+        def d_apply():
+            d_ar.scale()
+            self._apply(nets.D, D_opt, rng)
+            nets.update_Gs(G_smoothing)
+
+        def g_grads():
+            acc[4] += self._g_step(lod, mb, labels_all, rng, G_opt, None, apply=False)
+
+        def g_apply():
+            g_ar.scale()
+            self._apply(nets.G, G_opt, rng)
+            nets.set_requires_grad(nets.d_params, True)
+
+        raw = []
+        for _ in range(D_repeats):
+            raw += [('g', d_grads), ('e', d_ar.allreduce_now), ('g', d_apply)]
+        raw += [('g', g_grads), ('e', g_ar.allreduce_now), ('g', g_apply)]
+        segs = []
+        for kind, fn in raw:
+            if segs and kind == 'g' and segs[-1][0] == 'g':
+                prev = segs[-1][1]
+                segs[-1] = ('g', (lambda a, b: (lambda: (a(), b())))(prev, fn))
+            else:
+                segs.append((kind, fn))
+        return segs
+
+    def _apply(self, flat, opt, rng):
+        self._finite_guard(flat, opt)
+        opt.step()
+        rng.advance()
+
     def _d_step(self, lod, mb, level, labels_all, rng, opt, ar, wgan_lambda=10.0, wgan_epsilon=0.001,
-                wgan_target=1.0):
-        """_D_wgangp_acgan (pg_gans.py:1291-1328) + D optimizer step."""
+                wgan_target=1.0, apply=True):
+        """_D_wgangp_acgan (pg_gans.py:1291-1328) + D optimizer step (``apply=False``: gradients only)."""
         nets = self.nets
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.g_params, False)
@@ -763,14 +859,13 @@ class PgGan(BaseModel):
             loss.mean().backward()
         if ar is not None:
             ar.finish()
-        self._finite_guard(nets.D, opt)
-        opt.step()
-        rng.advance()
+        if apply:
+            self._apply(nets.D, opt, rng)
         return torch.stack([loss.mean().detach(), real_s.mean().detach(), fake_s.mean().detach(),
                             norms.mean().detach()])
 
-    def _g_step(self, lod, mb, labels_all, rng, opt, ar):
-        """_G_wgan_acgan (pg_gans.py:1276-1289) + G optimizer step."""
+    def _g_step(self, lod, mb, labels_all, rng, opt, ar, apply=True):
+        """_G_wgan_acgan (pg_gans.py:1276-1289) + G optimizer step (``apply=False``: gradients only)."""
         nets = self.nets
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.d_params, False)
@@ -790,10 +885,9 @@ class PgGan(BaseModel):
             loss.mean().backward()
         if ar is not None:
             ar.finish()
-        self._finite_guard(nets.G, opt)
-        opt.step()
-        rng.advance()
-        nets.set_requires_grad(nets.d_params, True)
+        if apply:
+            self._apply(nets.G, opt, rng)
+            nets.set_requires_grad(nets.d_params, True)
         return loss.mean().detach()
 
     # ------------------------------------------------------------------ generation

@@ -123,6 +123,22 @@ class FlatGradAllReduce:
         if average:
             self.grad.mul_(1.0 / self.world)
 
+    def allreduce_now(self):
+        """Launch every bucket's all-reduce (sum) and make the current stream wait for them — the eager
+        collective segment between two captured segments of a data-parallel round (the 1/world mean is
+        ``scale()``, the first op of the next captured segment)."""
+        if self.world <= 1 and not self.force:
+            return
+        works = [dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                 for a, e in self.buckets]
+        for w in works:
+            w.wait()
+
+    def scale(self):
+        """grad *= 1/world (the all-reduce mean, pg_gans.py:1175-1179)."""
+        if self.world > 1:
+            self.grad.mul_(1.0 / self.world)
+
     def remove(self):
         for h in self._hooks:
             h.remove()

@@ -290,8 +290,9 @@ def test_colsum_tall(fn):
 
 def test_dp_round_with_rccl_allreduce_is_graph_captured():
     """Single-GPU rehearsal of the data-parallel round: a 1-rank RCCL group with the bucketed
-    all-reduce forced on.  The rounds (backward hooks launching async all-reduces, waits, averaging,
-    Adam) are captured into hipGraphs and replayed, and training matches the no-collective run.
+    all-reduce forced on.  On the DEFAULT path (no opt-in, no sleep) the rounds are captured by
+    segments — gradients (graph) -> bucketed all-reduce (eager, between replays) -> mean + Adam + EMA
+    (graph) — and replayed, and training matches the no-collective run.
 
     Runs in a fresh child process: the RCCL communicator, its watchdog thread and the graph pools
     then start from a clean state instead of inheriting the rest of the suite's (one extra process
@@ -301,7 +302,7 @@ def test_dp_round_with_rccl_allreduce_is_graph_captured():
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     code = "import sys; sys.path.insert(0, {!r}); import test_pg_gan_gpu as t; t._dp_round_child(); print('DP-OK')"
-    env = dict(os.environ, RAFIKI_PGGAN_GRAPH_COLLECTIVES='1')   # capture of collective rounds is opt-in
+    env = {k: v for k, v in os.environ.items() if k != 'RAFIKI_PGGAN_GRAPH_COLLECTIVES'}
     r = subprocess.run([sys.executable, '-c', code.format(here)], cwd=os.path.dirname(here), capture_output=True,
                        text=True, timeout=100, env=env)
     assert r.returncode == 0 and 'DP-OK' in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
@@ -331,7 +332,10 @@ def _dp_round_child():
                 m = PgGan(**dict(knobs, force_grad_allreduce=force))
                 m.train(data)
             torch.cuda.synchronize()
-            assert m.graphs.captures == 1, m.graphs.captures   # one stable-LOD key, replayed afterwards
+            # one stable-LOD key, replayed afterwards: one graph without collectives; with them the
+            # D_repeats + 2 = 3 compute segments around the 2 eager all-reduce segments
+            assert m.graphs.captures == (3 if force else 1), m.graphs.captures
+            assert m.segmented == force
             outs.append((m.nets.G.master.clone(), m.nets.D.master.clone()))
         (g0, d0), (g1, d1) = outs
         assert torch.isfinite(g1).all() and torch.isfinite(d1).all()
