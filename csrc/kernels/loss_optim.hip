@@ -216,8 +216,11 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restri
                                                            int* __restrict__ counter, int B,
                                                            uint4* __restrict__ out, int* __restrict__ out_y,
                                                            double* __restrict__ zero, long long zero_n,
-                                                           int* __restrict__ done) {
+                                                           int* __restrict__ done, const float* __restrict__ lr_table,
+                                                           float* __restrict__ lr_out) {
   const long long step = *counter;
+  // the step's learning-rate multiplier from a per-step table (a schedule inside the replayed graph)
+  if (lr_table && blockIdx.x == 0 && threadIdx.x == 0) *lr_out = lr_table[step];
   const long long total = (long long)B * row_vec;
   const long long gstride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gstride) {
@@ -610,13 +613,15 @@ extern "C" int rk_conv_wt(const void* src, void* dst, const int* desc, int nbloc
   return RK_OK;
 }
 
+// lr_table (nullable): *lr_out = lr_table[*counter] (the optimizer kernel later in the step reads lr_out)
 extern "C" int rk_gather_batch(const void* data, long long row_bytes, const int* labels, const long long* sched,
                                int* counter, int B, void* out, int* out_y, double* zero, long long zero_n, int* done,
-                               void* stream) {
-  if (row_bytes % 16 || zero_n < 0 || (zero_n && !zero)) return RK_EUNSUPPORTED;
+                               const float* lr_table, float* lr_out, void* stream) {
+  if (row_bytes % 16 || zero_n < 0 || (zero_n && !zero) || (lr_table && !lr_out)) return RK_EUNSUPPORTED;
   const long long rv = row_bytes / 16;
   hipLaunchKernelGGL(gather_batch_kernel, dim3(grid_for((long long)B * rv, 2048)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)data, rv, labels, sched, counter, B, (uint4*)out, out_y, zero, zero_n, done);
+                     (const uint4*)data, rv, labels, sched, counter, B, (uint4*)out, out_y, zero, zero_n, done,
+                     lr_table, lr_out);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -675,6 +675,9 @@ class ConvNetEngine:
         self._static_y = torch.zeros((batch_size,), dtype=torch.int32, device=self.device)
 
         self._done = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # per-step LR multipliers read by the prologue into the optimizer's device scalar (SGD)
+        self._lr_table = torch.ones(max_steps, dtype=torch.float32, device=self.device)
+        lr_out = getattr(self.opt, 'lr_scale', None)
         accs = self._bn_accumulators() if self._use_bn_acc() else None
 
         # the step counter advances inside the step's last kernel (SGD) or, for other optimizers, in
@@ -685,7 +688,8 @@ class ConvNetEngine:
             # one prologue launch: gather + zero the BN slot tables (+ counter)
             F.gather_batch(self._data, self._labels, self._sched, self._ctr, self._static_x, self._static_y,
                            zero=self._bn_acc_flat if accs is not None else None,
-                           done=None if opt_bumps else self._done)
+                           done=None if opt_bumps else self._done,
+                           lr_table=self._lr_table if lr_out is not None else None, lr_out=lr_out)
             self._acc_zeroed_by_prologue = accs is not None
             if opt_bumps:
                 self.opt.bump = self._ctr
@@ -718,10 +722,13 @@ class ConvNetEngine:
         self._sched_graph = g
         return g
 
-    def set_schedule(self, idx, start: int = 0):
-        """idx: [steps, B] row indices (device) -> schedule buffer; the next replay uses row ``start``."""
+    def set_schedule(self, idx, start: int = 0, lr_scales=None):
+        """idx: [steps, B] row indices (device) -> schedule buffer; the next replay uses row ``start``.
+        ``lr_scales`` [steps] (optional): the optimizer's LR multiplier of each step."""
         self._sched[:idx.shape[0]].copy_(idx)
         self._ctr.fill_(start)
+        if lr_scales is not None:
+            self._lr_table[:len(lr_scales)].copy_(torch.as_tensor(lr_scales, dtype=torch.float32))
 
     def replay(self):
         self._sched_graph.replay()

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from ..engine.convnet import ConvNetEngine, default_dtype
+from ..engine.flat import FlatSGD
 from ..model import BaseModel, dataset_utils, logger
 from ..parallel.context import current as trial_context
 from ..ops.graphs import device_sync
@@ -81,7 +82,12 @@ class NativeImageClassifier(BaseModel):
         total = max(1, int(math.ceil(epochs * steps_per_epoch)))
         use_graph = eng.device.type == 'cuda'
         t_cap = time.perf_counter()
-        if use_graph:
+        # one graph per step that also gathers its minibatch by a device-side counter from a per-epoch
+        # index schedule and reads its LR multiplier from a per-step table: a replay per step, no copies
+        scheduled = use_graph and isinstance(eng.opt, FlatSGD)
+        if scheduled:
+            eng.capture_scheduled(x_all, y_all, steps_per_epoch, bs)
+        elif use_graph:
             eng.capture(bs)
         tm['capture'] = time.perf_counter() - t_cap
         xb = torch.empty(eng.input_shape(bs), dtype=x_all.dtype, device=eng.device)
@@ -108,10 +114,20 @@ class NativeImageClassifier(BaseModel):
             eng.reset_metrics()
             t0 = time.perf_counter()
             done = 0
+            if scheduled:
+                cosine = hasattr(eng.opt, 'set_lr_scale') and sched == 'cosine'
+                lrs = [0.5 * (1.0 + math.cos(math.pi * (step + b) / total)) if cosine else 1.0
+                       for b in range(steps_per_epoch)]
+                eng.set_schedule(perm[:steps_per_epoch * bs].view(steps_per_epoch, bs), lr_scales=lrs)
             for b in range(steps_per_epoch):
                 if step >= total:
                     break
                 faults.maybe_fail('train_step', step=step, rank=ctx.rank)
+                if scheduled:
+                    eng.replay()
+                    step += 1
+                    done += 1
+                    continue
                 if hasattr(eng.opt, 'set_lr_scale') and sched == 'cosine':
                     eng.opt.set_lr_scale(0.5 * (1.0 + math.cos(math.pi * step / total)))
                 idx = perm[b * bs:(b + 1) * bs]

@@ -800,16 +800,17 @@ def ensemble_mean(probs, weights=None, out=None):
     return out
 
 
-def gather_batch(data, labels, sched, counter, out_x, out_y, *, zero=None, done=None):
+def gather_batch(data, labels, sched, counter, out_x, out_y, *, zero=None, done=None, lr_table=None, lr_out=None):
     """out_x[b] = data[sched[*counter][b]], out_y likewise — device-side step counter (graph-safe).
     ``zero``: an fp64 tensor zeroed in the same launch; ``done`` (int32 [1], zero-initialised): the
-    kernel also advances ``counter`` by one after every block has read it."""
+    kernel also advances ``counter`` by one after every block has read it; ``lr_table``: lr_out[0] =
+    lr_table[*counter] (a per-step learning-rate schedule inside the replayed graph)."""
     B = out_x.shape[0]
     row_bytes = data[0].numel() * data.element_size()
     if zero is not None:
         assert zero.dtype == torch.float64 and zero.is_contiguous()
     _lib.call("rk_gather_batch", _p(data), row_bytes, _p(labels), _p(sched), _p(counter), B, _p(out_x), _p(out_y),
-              _p(zero), 0 if zero is None else zero.numel(), _p(done), _s())
+              _p(zero), 0 if zero is None else zero.numel(), _p(done), _p(lr_table), _p(lr_out), _s())
     return out_x
 
 

@@ -97,6 +97,15 @@ def main():
         h, m = c.get('TCC_HIT_sum', 0), c.get('TCC_MISS_sum', 0)
         if h + m:
             r['l2_hit_pct'] = round(100.0 * h / (h + m), 1)
+        wc = c.get('SQ_WAVE_CYCLES', 0)
+        if wc:   # shares of wave lifetime: parked (waitcnt / barrier), issue-stalled, issuing VALU
+            r['wait_pct'] = round(100.0 * c.get('SQ_WAIT_ANY', 0) / wc, 1)
+            if 'SQ_WAIT_INST_ANY' in c:
+                r['stall_pct'] = round(100.0 * c['SQ_WAIT_INST_ANY'] / wc, 1)
+            if 'SQ_ACTIVE_INST_VALU' in c:
+                r['valu_pct'] = round(100.0 * c['SQ_ACTIVE_INST_VALU'] / wc, 1)
+        if c.get('SQ_INSTS_MFMA') and 'SQ_INSTS_VALU' in c:
+            r['valu_per_mfma'] = round(c['SQ_INSTS_VALU'] / c['SQ_INSTS_MFMA'], 2)
         r['gui_kcycles_per_step'] = round(gui / 1e3 / a.steps, 1)
         for key in ('SQ_VALU_MFMA_BUSY_CYCLES', 'FETCH_SIZE', 'WRITE_SIZE'):
             tot[key] += c.get(key, 0)
@@ -105,7 +114,7 @@ def main():
         rows.append(r)
     rows.sort(key=lambda r: -(r['us_per_step'] or 0) * 1e6 - r['gui_kcycles_per_step'])
     cols = ['kernel', 'launches_per_step', 'us_per_step', 'mfma_util_pct', 'lds_conflict_pct',
-            'fetch_MB', 'write_MB', 'GBps', 'l2_hit_pct']
+            'fetch_MB', 'write_MB', 'GBps', 'l2_hit_pct', 'wait_pct', 'stall_pct', 'valu_pct', 'valu_per_mfma']
     print(('%-60s' + '%11s' * (len(cols) - 1)) % tuple(c[:10] for c in cols))
     for r in rows:
         print(('%-60s' + '%11s' * (len(cols) - 1)) % tuple([r['kernel'][:60]] + [r.get(c, '') for c in cols[1:]]))
