@@ -29,6 +29,8 @@
 
 namespace {
 
+#include "wino_wt.h"
+
 constexpr int WT = 64;    // output tiles per block
 constexpr int WKC = 8;    // input channels per K chunk
 enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_BNB = 512, WF_BNP = 1024 };
@@ -471,72 +473,6 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
           *d = p.accumulate ? *d + v[kx] : v[kx];
         }
       }
-    }
-  }
-}
-
-// U = G g G^T of every (co, ci) 3x3 filter g = w[co][ky*3+kx][ci]: u[pos][co][ci]; optionally the
-// data-gradient set ut[pos][ci][co] = U[p(pos)][co][ci] with p swapping positions 0 and 3 per axis.
-// Block = 32 co x 32 ci filters staged through LDS (coalesced both ways).
-RK_DEV void w_transform(const float (&g)[9], float (&U)[16]) {
-  float t[4][3];
-#pragma unroll
-  for (int kx = 0; kx < 3; ++kx) {
-    const float g0 = g[kx], g1 = g[3 + kx], g2 = g[6 + kx];
-    t[0][kx] = g0;
-    t[1][kx] = 0.5f * (g0 + g1 + g2);
-    t[2][kx] = 0.5f * (g0 - g1 + g2);
-    t[3][kx] = g2;
-  }
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    U[a * 4 + 0] = t[a][0];
-    U[a * 4 + 1] = 0.5f * (t[a][0] + t[a][1] + t[a][2]);
-    U[a * 4 + 2] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
-    U[a * 4 + 3] = t[a][2];
-  }
-}
-
-// one 32 co x 32 ci block of filters: LDS-staged so both output layouts are written coalesced
-RK_DEV void wt_block(const float* __restrict__ w, float* __restrict__ u, float* __restrict__ ut, int Co, int Ci,
-                     int co0, int ci0, float (&g)[32][9][33]) {
-  float st[36];   // all loads in flight before the first LDS store
-#pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    const int i = threadIdx.x + 256 * k;
-    const int ci = i & 31, t = (i >> 5) % 9, co = i / (9 * 32);
-    st[k] = (co0 + co < Co && ci0 + ci < Ci) ? w[((long long)(co0 + co) * 9 + t) * Ci + ci0 + ci] : 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    const int i = threadIdx.x + 256 * k;
-    g[i / (9 * 32)][(i >> 5) % 9][i & 31] = st[k];
-  }
-  __syncthreads();
-  if (u != nullptr)
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-      const int ci = i & 31, co = i >> 5;
-      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
-      float gg[9], U[16];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
-      w_transform(gg, U);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) u[((long long)q * Co + co0 + co) * Ci + ci0 + ci] = U[q];
-    }
-  if (ut == nullptr) return;
-  for (int i = threadIdx.x; i < 1024; i += 256) {
-    const int co = i & 31, ci = i >> 5;
-    if (co0 + co >= Co || ci0 + ci >= Ci) continue;
-    float gg[9], U[16];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
-    w_transform(gg, U);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int a = q >> 2, bq = q & 3;
-      const int pa = a == 0 ? 3 : a == 3 ? 0 : a, pb = bq == 0 ? 3 : bq == 3 ? 0 : bq;
-      ut[((long long)q * Ci + ci0 + ci) * Co + co0 + co] = U[pa * 4 + pb];
     }
   }
 }

@@ -28,6 +28,8 @@
 
 namespace {
 
+#include "wino_wt.h"
+
 constexpr int KC = 8;     // input channels per K chunk
 enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_BNB = 512, WF_BNP = 1024 };
 
@@ -72,17 +74,6 @@ RK_DEV void at6(float m0, float m1, float m2, float m3, float m4, float m5, floa
   o[1] = d12 + 2.f * d34;
   o[2] = s12 + 4.f * s34;
   o[3] = d12 + 8.f * d34 + m5;
-}
-
-// G g of a 3-vector -> 6 values
-RK_DEV void g6(float g0, float g1, float g2, float (&u)[6]) {
-  const float s = g0 + g2;
-  u[0] = 0.25f * g0;
-  u[1] = -(s + g1) * (1.f / 6.f);
-  u[2] = -(s - g1) * (1.f / 6.f);
-  u[3] = g0 * (1.f / 24.f) + g1 * (1.f / 12.f) + g2 * (1.f / 6.f);
-  u[4] = g0 * (1.f / 24.f) - g1 * (1.f / 12.f) + g2 * (1.f / 6.f);
-  u[5] = g2;
 }
 
 // F(2x2,3x3) counterparts (interpolation points 0, 1, -1, inf): B^T d of a 4-vector, A^T m -> 2 outputs
@@ -803,80 +794,6 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
 }
 
 // ------------------------------------------------------------------------------ weight transform
-// U = G g G^T (36 values) of a 3x3 filter g[ky*3+kx]
-RK_DEV void w4_transform(const float (&g)[9], float (&U)[36]) {
-  float t[6][3];
-#pragma unroll
-  for (int kx = 0; kx < 3; ++kx) {
-    float o[6];
-    g6(g[kx], g[3 + kx], g[6 + kx], o);
-#pragma unroll
-    for (int a = 0; a < 6; ++a) t[a][kx] = o[a];
-  }
-#pragma unroll
-  for (int a = 0; a < 6; ++a) {
-    float o[6];
-    g6(t[a][0], t[a][1], t[a][2], o);
-#pragma unroll
-    for (int bb = 0; bb < 6; ++bb) U[a * 6 + bb] = o[bb];
-  }
-}
-
-// one 32 co x 32 ci block of filters, LDS-staged so both layouts are written coalesced:
-// u [36][Co][Ci] of w, ut [36][Ci][Co] of the flipped filters (either may be null).  PL: the X6 planes
-// instead, bf16 u [36][3][Co][Ci] / ut [36][3][Ci][Co] (hi, mid, lo of every value; x6p.hip)
-template <bool PL = false>
-RK_DEV void w4_block(const float* __restrict__ w, void* __restrict__ u, void* __restrict__ ut, int Co, int Ci,
-                     int co0, int ci0, float (&g)[32][9][33]) {
-  float st[36];
-#pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    const int i = threadIdx.x + 256 * k;
-    const int ci = i & 31, t = (i >> 5) % 9, co = i / (9 * 32);
-    st[k] = (co0 + co < Co && ci0 + ci < Ci) ? w[((long long)(co0 + co) * 9 + t) * Ci + ci0 + ci] : 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    const int i = threadIdx.x + 256 * k;
-    g[i / (9 * 32)][(i >> 5) % 9][i & 31] = st[k];
-  }
-  __syncthreads();
-  auto put = [&](void* dst, long long q, long long rows, long long r, long long cols, long long c, float v) {
-    if constexpr (PL) {
-      bf16* d = (bf16*)dst + (q * 3 * rows + r) * cols + c;
-      bf16 h, m, l;
-      split3v(v, h, m, l);
-      d[0] = h;
-      d[rows * cols] = m;
-      d[2 * rows * cols] = l;
-    } else {
-      ((float*)dst)[(q * rows + r) * cols + c] = v;
-    }
-  };
-  if (u != nullptr)
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-      const int ci = i & 31, co = i >> 5;
-      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
-      float gg[9], U[36];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
-      w4_transform(gg, U);
-#pragma unroll
-      for (int q = 0; q < 36; ++q) put(u, q, Co, co0 + co, Ci, ci0 + ci, U[q]);
-    }
-  if (ut != nullptr)
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-      const int co = i & 31, ci = i >> 5;
-      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
-      float gg[9], U[36];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) gg[t] = g[co][8 - t][ci];
-      w4_transform(gg, U);
-#pragma unroll
-      for (int q = 0; q < 36; ++q) put(ut, q, Ci, ci0 + ci, Co, co0 + co, U[q]);
-    }
-}
-
 __global__ __launch_bounds__(256) void wino4_wt_kernel(const float* __restrict__ w, float* __restrict__ u,
                                                        float* __restrict__ ut, int Co, int Ci) {
   __shared__ float g[32][9][33];
@@ -906,6 +823,24 @@ __global__ __launch_bounds__(256) void x6p_wt_multi_kernel(const float* __restri
                  (int)m[4], d.y, d.z, g);
 }
 
+__global__ __launch_bounds__(256) void wt_all_kernel(const float* __restrict__ arena, float* __restrict__ dst,
+                                                     const int4* __restrict__ desc, const long long* __restrict__ meta) {
+  __shared__ float g[32][9][33];
+  const int4 d = desc[blockIdx.x];
+  const long long* m = meta + 5 * d.x;
+  const float* w = arena + m[0];
+  if (d.w == 0) {
+    wt_block(w, m[1] >= 0 ? dst + m[1] : nullptr, m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4], d.y, d.z, g);
+  } else if (d.w == 1) {
+    w4_block<false>(w, m[1] >= 0 ? dst + m[1] : nullptr, m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4], d.y,
+                    d.z, g);
+  } else {
+    bf16* db = (bf16*)dst;
+    w4_block<true>(w, m[1] >= 0 ? db + m[1] : nullptr, m[2] >= 0 ? db + m[2] : nullptr, (int)m[3], (int)m[4], d.y,
+                   d.z, g);
+  }
+}
+
 __global__ __launch_bounds__(256) void x6p_wt_kernel(const float* __restrict__ w, bf16* __restrict__ u,
                                                      bf16* __restrict__ ut, int Co, int Ci) {
   __shared__ float g[32][9][33];
@@ -923,6 +858,13 @@ extern "C" int rk_wino4_weights(const float* w, float* u, float* ut, int Co, int
   return RK_OK;
 }
 
+// Every live Winograd weight set of a network, all families, in ONE launch: desc[block] = (meta row, co0,
+// ci0, family), family 0 F(2x2) fp32 sets, 1 F(4x4) fp32 sets, 2 F(4x4) X6 bf16 planes; meta rows as the
+// per-family kernels' (offsets in floats of dst, bf16 elements of dst for family 2).  Replaces three
+// launches, two of them a few dozen latency-bound blocks (profiles/vgg_small_f32_step_kernels_r4*).
+extern "C" int rk_wino_weights_all(const float* arena, float* dst, const int* desc, int nblocks,
+                                   const long long* meta, void* stream);
+
 // X6 planes u [36][3][Co][Ci] (nullable) / ut [36][3][Ci][Co] (nullable), bf16, of w [Co][9][Ci]
 extern "C" int rk_x6p_w4_weights(const float* w, void* u, void* ut, int Co, int Ci, void* stream) {
   if (Co <= 0 || Ci <= 0 || (!u && !ut)) return RK_EBADARG;
@@ -938,6 +880,15 @@ extern "C" int rk_x6p_w4_weights_multi(const float* arena, void* dst, const int*
   if (nblocks <= 0) return RK_OK;
   hipLaunchKernelGGL(x6p_wt_multi_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, arena, (bf16*)dst,
                      (const int4*)desc, meta);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_wino_weights_all(const float* arena, float* dst, const int* desc, int nblocks,
+                                   const long long* meta, void* stream) {
+  if (nblocks <= 0) return RK_OK;
+  hipLaunchKernelGGL(wt_all_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, arena, dst, (const int4*)desc,
+                     meta);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

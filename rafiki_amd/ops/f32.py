@@ -932,12 +932,37 @@ class WinoWeights:
                 out.append((fam, torch.tensor(desc, dtype=torch.int32, device=dev).reshape(-1),
                             torch.tensor(meta, dtype=torch.int64, device=dev).reshape(-1), len(desc)))
         self._tables[live] = out
+        # every family in one table for the single-launch refresh (rk_wino_weights_all): meta rows
+        # concatenated, each block's desc row = (meta row, co0, ci0, family)
+        fam_id = {'2': 0, '4': 1, 'p': 2}
+        adesc, ameta, base = [], [], 0
+        for fam, desc, meta, nb in out:
+            d = desc.view(-1, 4).cpu().clone()
+            d[:, 0] += base
+            d[:, 3] = fam_id[fam]
+            adesc.append(d)
+            ameta.append(meta.view(-1, 5).cpu())
+            base += ameta[-1].shape[0]
+        if adesc:
+            dev = self.arena.device
+            self._tables[('all', live)] = (torch.cat(adesc).to(dev).reshape(-1), torch.cat(ameta).to(dev).reshape(-1),
+                                           sum(int(t.shape[0]) for t in adesc))
         return out
 
+    # one launch for every family (RAFIKI_WT_ALL=0: one launch per family)
+    WT_ALL = os.environ.get('RAFIKI_WT_ALL', '1') != '0'
+
     def refresh(self):
-        for fam, desc, meta, nb in self._prepare(self.live):
-            name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi", 'p': "rk_x6p_w4_weights_multi"}[fam]
-            _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
+        tabs = self._prepare(self.live)
+        allt = self._tables.get(('all', self.live))
+        if self.WT_ALL and allt is not None:
+            desc, meta, nb = allt
+            _lib.call("rk_wino_weights_all", _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
+        else:
+            for fam, desc, meta, nb in tabs:
+                name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi",
+                        'p': "rk_x6p_w4_weights_multi"}[fam]
+                _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
         self._fresh = set(self.live)
 
     def end_step(self):

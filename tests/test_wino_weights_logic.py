@@ -25,6 +25,7 @@ def _setup(monkeypatch, capturing=False):
     monkeypatch.setattr(S, '_s', lambda: None)
     monkeypatch.setattr(S, '_p', lambda t: None if t is None else t.data_ptr())   # host tensors are fine here
     monkeypatch.setattr(torch.cuda, 'is_current_stream_capturing', lambda: capturing)
+    monkeypatch.setattr(S.WinoWeights, 'WT_ALL', False)   # one launch per family (the combined table: below)
     shapes = [(64, 32), (16, 64), (40, 24)]
     arena = torch.zeros(sum(co * 9 * ci for co, ci in shapes) + 3)
     ws, off = [], 3
@@ -111,3 +112,28 @@ def test_sconvwt_refresh_is_lazy(monkeypatch):
     wt.begin_step()
     wt.lazy(0)()
     assert rec.names() == ['rk_swt', 'rk_swt']
+
+
+def test_single_launch_refresh_table_covers_every_family(monkeypatch):
+    """RAFIKI_WT_ALL (default): one rk_wino_weights_all launch whose table is the per-family tables
+    concatenated — meta rows renumbered, the family id in each block's 4th field."""
+    rec, ww = _setup(monkeypatch)
+    monkeypatch.setattr(S.WinoWeights, 'WT_ALL', True)
+    ww.refresh()
+    assert rec.names() == ['rk_wino_weights_all']
+    fams = ww._prepare(ww.live)
+    desc, meta, nb = ww._tables[('all', ww.live)]
+    d, m = desc.view(-1, 4), meta.view(-1, 5)
+    assert nb == d.shape[0] == sum(f[3] for f in fams)
+    assert m.shape[0] == sum(f[2].numel() // 5 for f in fams)
+    fam_of = {'2': 0, '4': 1, 'p': 2}
+    row = 0
+    base = 0
+    for fam, fdesc, fmeta, fnb in fams:
+        fd = fdesc.view(-1, 4)
+        got = d[row:row + fnb]
+        assert (got[:, 0] == fd[:, 0] + base).all() and (got[:, 1:3] == fd[:, 1:3]).all()
+        assert (got[:, 3] == fam_of[fam]).all()
+        assert torch.equal(m[base:base + fmeta.numel() // 5], fmeta.view(-1, 5))
+        row += fnb
+        base += fmeta.numel() // 5
