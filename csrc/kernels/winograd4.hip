@@ -25,6 +25,7 @@
 //   * epilogues identical to the F(2x2) kernel: bias, ReLU, BN statistics (fp64 slot atomics) and
 //     the data-gradient FLAG_BNB / FLAG_BNP fusions; grouped launches for the serving ensemble.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -1419,6 +1420,126 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
   }
 }
 
+// The same with VW-channel vectors (VW = 2: 8-B, 4: 16-B accesses; the scalar kernel's 4-B accesses ran at
+// ~3.2 TB/s): one thread per (tile, VW channels) — 36 vector loads of Y', 16 vector stores, vector gate
+// loads; a 64-thread block = 64 / (64 / VW) tiles x 64 channels, many blocks even on the 4x4 maps.
+template <int VW>
+__global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restrict__ yt, float* __restrict__ y,
+                                                            const float* __restrict__ bp, double* stats, int slotMask,
+                                                            const float* __restrict__ gate, int Nb, int H, int W,
+                                                            int N, int TW, int THW, int T, int flags, int nslab,
+                                                            long long slab) {
+  constexpr int LPT = 64 / VW, TPB = 64 / LPT;   // lanes per tile, tiles per block
+  typedef __attribute__((ext_vector_type(VW))) float fv;
+  __shared__ float red[2][TPB][64];
+  const int nblk = (N + 63) / 64;
+  const int nb = blockIdx.x % nblk, tb = blockIdx.x / nblk;
+  const int qd = threadIdx.x % LPT, tg = threadIdx.x / LPT;
+  const int n = nb * 64 + VW * qd;
+  const bool nok = n < N;
+  const long long plane = (long long)T * N;
+  fv bs = {}, sh = {};
+  if ((flags & (WF_BIAS | WF_BNB | WF_BNP)) && nok) bs = *(const fv*)(bp + n);
+  if ((flags & (WF_BNB | WF_BNP)) && nok) sh = *(const fv*)(bp + N + n);
+  fv s = {}, ss = {};
+  const int t = tb * TPB + tg;
+  if (t < T && nok) {
+    fv m[36];
+    const float* src = yt + (long long)t * N + n;
+#pragma unroll
+    for (int q = 0; q < 36; ++q) m[q] = *(const fv*)(src + q * plane);
+    for (int k = 1; k < nslab; ++k)   // split-K partial slabs of the GEMM
+#pragma unroll
+      for (int q = 0; q < 36; ++q) m[q] += *(const fv*)(src + k * slab + q * plane);
+    const int im = t / THW, rr = t - im * THW, ty = rr / TW;
+    const int oy = 4 * ty, ox = 4 * (rr - ty * TW);
+    fv res[4][4];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      float tt[6][4];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {          // M A: along columns
+        float o[4];
+        at6(m[a * 6 + 0][e], m[a * 6 + 1][e], m[a * 6 + 2][e], m[a * 6 + 3][e], m[a * 6 + 4][e], m[a * 6 + 5][e], o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tt[a][j] = o[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float o[4];
+        at6(tt[0][j], tt[1][j], tt[2][j], tt[3][j], tt[4][j], tt[5][j], o);   // A^T (M A): along rows
+#pragma unroll
+        for (int i = 0; i < 4; ++i) res[i][j][e] = o[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fv v = res[i][j];
+        const long long idx = (((long long)im * H + oy + i) * W + ox + j) * N + n;
+        if (flags & WF_BIAS) v += bs;
+        if (flags & WF_STATS) {
+          s += v;
+          ss += v * v;
+        }
+        if (flags & WF_RELU) {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (flags & WF_BNB) {
+          const fv g = *(const fv*)(gate + idx);
+#pragma unroll
+          for (int e = 0; e < VW; ++e) {
+            v[e] = g[e] * bs[e] + sh[e] > 0.f ? v[e] : 0.f;
+            s[e] += v[e];
+            ss[e] += v[e] * g[e];
+          }
+        }
+        if (flags & WF_BNP) {
+          const long long W2 = 2LL * W;
+          const long long q0 = (((long long)im * 2 * H + 2 * (oy + i)) * W2 + 2 * (ox + j)) * N + n;
+          const fv y4[4] = {*(const fv*)(gate + q0), *(const fv*)(gate + q0 + N), *(const fv*)(gate + q0 + W2 * N),
+                            *(const fv*)(gate + q0 + W2 * N + N)};
+#pragma unroll
+          for (int e = 0; e < VW; ++e) {
+            float best = -INFINITY, zb = 0.f, yb = 0.f;
+#pragma unroll
+            for (int w4 = 0; w4 < 4; ++w4) {   // first maximal relu(z) of the window (torch max_pool2d rule)
+              const float z = y4[w4][e] * bs[e] + sh[e];
+              const float av = fmaxf(z, 0.f);
+              if (av > best) { best = av; zb = z; yb = y4[w4][e]; }
+            }
+            const float dz = zb > 0.f ? v[e] : 0.f;
+            s[e] += dz;
+            ss[e] += dz * yb;
+          }
+        }
+        *(fv*)(y + idx) = v;
+      }
+  }
+  if (flags & (WF_STATS | WF_BNB | WF_BNP)) {
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      red[0][tg][VW * qd + e] = s[e];
+      red[1][tg][VW * qd + e] = ss[e];
+    }
+    __syncthreads();
+    const int c = threadIdx.x;   // 64 threads: one channel of the block's 64 each
+    if (nb * 64 + c < N) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int r = 0; r < TPB; ++r) {
+        a += red[0][r][c];
+        b += red[1][r][c];
+      }
+      double* slot = stats + (long long)(blockIdx.x & slotMask) * 2 * N;
+      unsafeAtomicAdd(slot + nb * 64 + c, (double)a);
+      unsafeAtomicAdd(slot + N + nb * 64 + c, (double)b);
+    }
+  }
+}
+
 }  // namespace
 
 // yt: nslab slabs of [36][T][N], slab floats apart (split-K partial sums of the GEMM), summed here
@@ -1434,6 +1555,20 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
   if (T * N >= (1LL << 31)) return RK_EUNSUPPORTED;
   const long long blocks = ((N + 63) / 64) * ((T + 3) / 4);
   if (nslab > 1 && slab < 36 * T * N) return RK_EBADARG;
+  // vector widths: RAFIKI_PT_OUT_VW = 4 (16-B) | 2 (8-B, default: fewer registers) | 1 (the scalar kernel)
+  static const int vw = getenv("RAFIKI_PT_OUT_VW") ? atoi(getenv("RAFIKI_PT_OUT_VW")) : 2;
+  if ((vw == 2 || vw == 4) && N % vw == 0) {
+    const long long tpb = vw == 4 ? 4 : 2;
+    const long long blocksv = ((N + 63) / 64) * ((T + tpb - 1) / tpb);
+    if (vw == 4)
+      hipLaunchKernelGGL(w4pt_conv_outv_kernel<4>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab);
+    else
+      hipLaunchKernelGGL(w4pt_conv_outv_kernel<2>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab);
+    RK_LAUNCH_CHECK();
+    return RK_OK;
+  }
   hipLaunchKernelGGL(w4pt_conv_out_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, yt, y, bias,
                      stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab);
   RK_LAUNCH_CHECK();
