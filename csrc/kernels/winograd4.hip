@@ -1168,6 +1168,100 @@ __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x
 // [36][3][Co][T] of dy (A dY A^T per 4x4 patch) and V^T planes [36][3][Ci][T] of x (B^T d B per 6x6
 // window).  One thread per (tile, 4-channel group), tiles fastest, so every bf16 store of a wave writes
 // 64 consecutive tiles of one (position, plane, channel) row.
+// LDS-staged form (T % 32 == 0, C % 8 == 0): one wave per 32 tiles x 8 channels.  Lane (tile tl, 4-channel
+// group g) transforms its window, splits the 36 x 4 values and writes them as bf16 into an LDS image
+// [36][3][8][32 tiles]; the wave then stores 16-B pieces of its 864 (position, plane, channel) rows of 32
+// tiles — 54 vector stores per lane instead of 432 two-byte ones (the T-fastest kernels were store-issue
+// bound: 29.7 / 22.5 us for the 8x8x256 layer, profiles/vgg_small_f32_step_kernels_r4*).
+template <bool DY>
+__global__ __launch_bounds__(64) void w4pt_planesT_kernel(const float* __restrict__ src, bf16* __restrict__ dst,
+                                                          int H, int W, int C, int TW, int THW, int T) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[36 * 3 * 8 * 32];
+  const int lane = threadIdx.x;
+  const int g = lane & 1, tl = lane >> 1;
+  const int t = blockIdx.x * 32 + tl, c0 = blockIdx.y * 8 + 4 * g;
+  const int n = t / THW, r = t - n * THW, ty = r / TW;
+  f32x4 res[36];
+  if (DY) {
+    const int oy = 4 * ty, ox = 4 * (r - ty * TW);
+    const float* sp = src + ((n * H + oy) * W + ox) * C + c0;
+    f32x4 gy[16];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) gy[a * 4 + b] = *(const f32x4*)(sp + (a * W + b) * C);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float mm[6][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float o[6];
+        a6(gy[j][e], gy[4 + j][e], gy[8 + j][e], gy[12 + j][e], o);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) mm[a][j] = o[a];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        float o[6];
+        a6(mm[a][0], mm[a][1], mm[a][2], mm[a][3], o);
+#pragma unroll
+        for (int b = 0; b < 6; ++b) res[a * 6 + b][e] = o[b];
+      }
+    }
+  } else {
+    const int oy = 4 * ty - 1, ox = 4 * (r - ty * TW) - 1;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const int yy = oy + a, xx = ox + b;
+        res[a * 6 + b] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                             ? *(const f32x4*)(src + ((n * H + yy) * W + xx) * C + c0)
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int b = 0; b < 6; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float o[6];
+        bt6(res[b][e], res[6 + b][e], res[12 + b][e], res[18 + b][e], res[24 + b][e], res[30 + b][e], o);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) res[a * 6 + b][e] = o[a];
+      }
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float o[6];
+        bt6(res[a * 6][e], res[a * 6 + 1][e], res[a * 6 + 2][e], res[a * 6 + 3][e], res[a * 6 + 4][e],
+            res[a * 6 + 5][e], o);
+#pragma unroll
+        for (int b = 0; b < 6; ++b) res[a * 6 + b][e] = o[b];
+      }
+  }
+#pragma unroll
+  for (int q = 0; q < 36; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bf16 hh, mi, lo;
+      split3v(res[q][e], hh, mi, lo);
+      const int row = (q * 3) * 8 + 4 * g + e;   // (q, plane 0, channel)
+      sm[row * 32 + tl] = hh;
+      sm[(row + 8) * 32 + tl] = mi;
+      sm[(row + 16) * 32 + tl] = lo;
+    }
+  __syncthreads();
+  // 864 rows x 64 B = 3456 pieces of 16 B; row (q, p, c) -> dst[((q * 3 + p) * C + cbase + c) * T + tbase ..]
+  const uint4* sv = (const uint4*)sm;
+  const int tbase = blockIdx.x * 32, cbase = blockIdx.y * 8;
+  for (int i = lane; i < 864 * 4; i += 64) {
+    const int row = i >> 2, piece = i & 3;
+    const int qp = row >> 3, c = row & 7;
+    bf16* d = dst + ((long long)qp * C + cbase + c) * T + tbase + piece * 8;
+    *(uint4*)d = sv[i];
+  }
+}
+
 RK_DEV void store_planes_t(bf16* dst, int q, int c, int C, int T, int t, float v) {
   bf16 h, m, l;
   split3v(v, h, m, l);
@@ -1613,6 +1707,15 @@ extern "C" int rk_x6p_w4_wgrad_transform(const float* dy, const float* x, void* 
   const long long T = (long long)Nb * THW;
   if (108 * T * Co >= (1ll << 31) || 108 * T * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
   if ((long long)Nb * H * W * (Co > Ci ? Co : Ci) >= (1ll << 31)) return RK_EUNSUPPORTED;
+  if (T % 32 == 0 && Co % 8 == 0 && Ci % 8 == 0) {
+    hipLaunchKernelGGL(w4pt_planesT_kernel<true>, dim3((unsigned)(T / 32), Co / 8), dim3(64), 0, (hipStream_t)stream,
+                       dy, (bf16*)mt, H, W, Co, TW, THW, (int)T);
+    RK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(w4pt_planesT_kernel<false>, dim3((unsigned)(T / 32), Ci / 8), dim3(64), 0, (hipStream_t)stream,
+                       x, (bf16*)vt, H, W, Ci, TW, THW, (int)T);
+    RK_LAUNCH_CHECK();
+    return RK_OK;
+  }
   const long long ty = T * Co / 4, tx = T * Ci / 4;
   hipLaunchKernelGGL(w4pt_dyT_kernel, dim3((unsigned)((ty + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy,
                      (bf16*)mt, H, W, Co, TW, THW, (int)ty, (int)T);
