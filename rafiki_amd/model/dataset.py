@@ -143,16 +143,34 @@ class CorpusDataset(ModelDataset):
 
 
 # ------------------------------------------------------------------------------- synthetic data
+_BANKS = {}
+
+
+def _noise_bank(shape, nb):
+    """The unit-variance Gaussian noise bank of ``synthetic_images``: one fixed bank per image shape,
+    SHARED by every split and seed (so train and test noise come from the same distribution) and at
+    least as large as the image dimension (so the noise spans the full pixel space)."""
+    key = (tuple(shape), nb)
+    if key not in _BANKS:
+        _BANKS.clear()   # one resident bank (~50 MB for 4096 CIFAR-sized images)
+        _BANKS[key] = np.random.default_rng(4321).standard_normal(size=(nb, *shape), dtype=np.float32)
+    return _BANKS[key]
+
+
 def synthetic_images(n, size=32, channels=3, classes=10, seed=0, separable=True, noise=None, flip=0.0,
-                     chunk=4096, bank=1024):
+                     chunk=4096, bank=None):
     """Deterministic class-conditional images: a per-class template plus Gaussian noise (std ``noise``,
     default 48 / 96 for separable / not).  ``flip`` relabels that fraction of the images uniformly at
     random, so no classifier exceeds ~1 - flip*(1 - 1/classes) accuracy (a non-separable task).
 
-    The noise of image i is cos(t_i) B[j_i] + sin(t_i) B[k_i] over a bank B of ``bank`` Gaussian
-    images (random pair, random angle: still exactly N(0, std^2) per pixel), built chunk by chunk in
+    The noise of image i is std * (cos(t_i) B[j_i] + sin(t_i) B[k_i]) over a bank B of ``bank`` unit
+    Gaussian images (random pair, random angle: exactly N(0, std^2) per pixel), built chunk by chunk in
     float32 — a CIFAR-sized split (50k x 32x32x3) takes a fraction of a second instead of drawing 150M
-    normals, which dominated a benchmark trial's first dataset load."""
+    normals, which dominated a benchmark trial's first dataset load.  The bank is shared by all splits
+    and seeds and has at least as many images as pixels (default max(4096, dim)), so every split's noise
+    has the same full-rank distribution; the seed picks the labels, pairs and angles.  (Round 3 drew a
+    1024-image bank per seed — a rank-1024 noise subspace that differed between train and test — so
+    scores on this data are not comparable with that round's.)"""
     rng = np.random.default_rng(seed)
     shape = (size, size) if channels == 1 else (size, size, channels)
     tmpl_rng = np.random.default_rng(1234)
@@ -160,13 +178,12 @@ def synthetic_images(n, size=32, channels=3, classes=10, seed=0, separable=True,
     templates = templates * np.float32(0.6) + np.float32(50.0)
     labels = rng.integers(0, classes, size=n)
     std = np.float32(noise if noise is not None else (48.0 if separable else 96.0))
-    nb = max(1, min(int(bank), n))
-    B = rng.standard_normal(size=(nb, *shape), dtype=np.float32)
-    B *= std
+    nb = int(bank) if bank is not None else max(4096, int(np.prod(shape)))
+    B = _noise_bank(shape, nb)
     j1, j2 = rng.integers(0, nb, size=n), rng.integers(0, nb, size=n)
     th = rng.uniform(0.0, 2.0 * np.pi, size=n)
-    ca = np.cos(th).astype(np.float32).reshape((n,) + (1,) * len(shape))
-    sa = np.sin(th).astype(np.float32).reshape((n,) + (1,) * len(shape))
+    ca = (std * np.cos(th)).astype(np.float32).reshape((n,) + (1,) * len(shape))
+    sa = (std * np.sin(th)).astype(np.float32).reshape((n,) + (1,) * len(shape))
     imgs = np.empty((n, *shape), dtype=np.uint8)
     for i in range(0, n, chunk):
         sl = slice(i, i + chunk)

@@ -28,7 +28,7 @@ F_RELU, F_BIAS, F_STATS, F_GATE, F_ACCUM, F_LRELU, F_BNB, F_BNP = 1, 2, 4, 8, 16
 # 7 64x256 (1x4).  Tiles 4-7 exist for the conv kinds with C % 32 == 0 and the weight gradient.
 TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 64), (256, 128), (128, 256), (64, 256),
          (64, 64), (128, 64), (64, 128)]   # 8-10: 1- / 2-wave tiles of 64x64 wave tiles (X6 candidates)
-_NST3 = (0, 1, 2, 3, 4, 7, 8, 9, 10)
+_NST3 = (0, 1, 2, 3, 4, 7)   # 3-stage rings: 4-wave tiles only (sgemm.hip s_launch)
 _FEW_WAVE = (8, 9, 10)
 NUM_CU = 256
 # tile code + X6: the split-bf16 K loop of rk_sgemm (fp32-accurate products on the bf16 MFMA: every
@@ -136,8 +136,7 @@ def _cands(M, N, splittable=False, K=0, big=False):
             bm, bn = TILES[t]
             if (cdiv(M, bm) * bm * cdiv(N, bn) * bn) / float(M * N) > 1.3:
                 continue
-            for nst in (2, 3):
-                x6.append((t + X6, nst, 1))
+            x6.append((t + X6, 2, 1))
         out += x6
     return out
 
@@ -573,7 +572,7 @@ def wino4_pt_ok(H, W, C, N):
 
 WINO4_PT_CFGS = tuple((WINO4_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)) for t in (0, 1, 2, 3)
                       for n in ((2, 3) if t in _NST3 else (2,))) + \
-    (tuple((WINO4_PT, t + X6, n) for t in _FEW_WAVE for n in (2, 3)) if USE_X6 else ())
+    (tuple((WINO4_PT, t + X6, 2) for t in _FEW_WAVE) if USE_X6 else ())
 
 
 def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None,
@@ -705,7 +704,7 @@ def _wino4_pt_cands(Nb, H, W, Cout, Cin):
         return []
     return [(WINO4_WGRAD_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)) for t in (0, 1, 2, 3)
             for n in ((2, 3) if t in _NST3 else (2,))] + \
-        ([(WINO4_WGRAD_PT, t + X6, n) for t in _FEW_WAVE for n in (2, 3)] if USE_X6 else [])
+        ([(WINO4_WGRAD_PT, t + X6, 2) for t in _FEW_WAVE] if USE_X6 else [])
 
 
 def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accumulate=False, tile=0, nst=2,

@@ -255,13 +255,19 @@ class KnobExchange:
         if self.chan.dev.type == 'cuda':
             torch.cuda.set_device(self.chan.dev)
         done = set()
+        ahead_failed = False
         qkey = self.tag + '/q'
         while len(done) < self.info.world_size - 1:
             with self._cv:
                 r = self._ahead_work()
                 hv, old = self._hv, self._ahead.get(r)
-            if r is not None and self.store.queue_len(qkey) == 0:
-                self._propose_one(r, hv, old)
+            if r is not None and not ahead_failed and self.store.queue_len(qkey) == 0:
+                try:
+                    self._propose_one(r, hv, old)
+                except Exception as e:   # advisor failure: stop proposing ahead; requests get refusals
+                    logger.error('knob exchange: proposal for rank %d failed: %r', r, e)
+                    self._error = self._error or e
+                    ahead_failed = True
                 continue
             try:
                 peer = int(self.store.queue_pop(qkey, block=True))
@@ -275,10 +281,15 @@ class KnobExchange:
             op, has_prev, score, ok, secs = row[:_HDR]
             op = int(op)
             prev = (self._knobs(row[_HDR:]), score, ok > 0, secs) if has_prev > 0 else None
-            knobs = self._handle(peer, op, prev)
+            try:
+                knobs, valid = self._handle(peer, op, prev), 1.0
+            except Exception as e:   # advisor failure: the peer still gets a (refusing) reply, never a hang
+                logger.error('knob exchange: request of rank %d failed: %r', peer, e)
+                self._error = self._error or e
+                knobs, valid = None, 0.0
             if op == OP_REQUEST:
                 with graphs.LOCK:
-                    self.chan.send([1.0] + self._row(knobs), peer)
+                    self.chan.send([valid] + self._row(knobs), peer)
             elif op == OP_FINISH:
                 done.add(peer)
             with self._cv:
@@ -298,7 +309,9 @@ class KnobExchange:
         if op != OP_REQUEST:
             return None
         rep = self.chan.recv(1 + len(self.names), 0)
-        return self._knobs(rep[1:]) if rep[0] > 0 else None
+        if rep[0] <= 0:
+            raise RuntimeError('knob exchange: rank 0 could not propose knobs (advisor failed)')
+        return self._knobs(rep[1:])
 
     def request(self, prev=None) -> dict:
         if self.info.is_main:

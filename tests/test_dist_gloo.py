@@ -277,3 +277,46 @@ def test_knob_exchange_scores_reach_rank0_advisor():
         # no two in-flight proposals were identical (constant-liar pending points)
         firsts = [tuple(sorted(r[0][0].items())) for r in res]
         assert len(set(firsts)) == world
+
+
+def _knobx_fail(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rafiki_amd.advisor.advisor import GpAdvisor
+    from rafiki_amd.model.knob import FloatKnob
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.parallel.exchange import KnobExchange
+    info = D.init_distributed(backend='gloo')
+    kc = {'x': FloatKnob(0.0, 1.0)}
+
+    class Broken(GpAdvisor):
+        def propose(self):
+            raise ValueError('advisor down')
+
+    ex = KnobExchange(info, kc, lambda: Broken(kc, seed=0), tag='f')
+    err = []
+    try:
+        ex.request(None)
+    except RuntimeError as e:
+        err.append(type(e).__name__)
+    except ValueError as e:          # rank 0 proposes inline
+        err.append(type(e).__name__)
+    ex.finish(None)
+    try:
+        ex.close()
+    except RuntimeError:
+        err.append('close')
+    with open(os.path.join(out_dir, 'f{}.txt'.format(rank)), 'w') as f:
+        f.write(repr(err))
+    D.destroy(info)
+
+
+def test_knob_exchange_advisor_failure_does_not_hang_peers():
+    """An advisor that raises: every peer's request gets a refusal reply (RuntimeError) instead of
+    blocking in recv, every rank still finishes, and rank 0's close() reports the failure."""
+    port = _free_port()
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_knobx_fail, args=(world, port, d), nprocs=world, join=True)
+        res = [eval(open(os.path.join(d, 'f{}.txt'.format(r))).read()) for r in range(world)]
+        assert res[0] == ['ValueError', 'close']
+        assert res[1] == res[2] == ['RuntimeError']
