@@ -10,6 +10,8 @@
 //     * parse the request line + Content-Length, read the body;
 //     * `POST /predict` whose "query" is a rectangular uint8 integer array (an image): decoded
 //       straight to bytes and queued for batching;
+//     * `POST /predict_batch_npy` with a uint8 .npy body: its images join the same queue as one
+//       request and are answered with one .npy float32 [n, classes] array;
 //     * `GET /`: answered in place;
 //     * anything else: queued as a generic request for Python (same wire contract as before).
 //   Python batch threads (one per predictor replica) call rt_http_next_batch(): it blocks (ctypes
@@ -43,6 +45,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -54,14 +57,17 @@ namespace {
 
 constexpr size_t kMaxHeader = 64 << 10;
 constexpr size_t kMaxConns = 16384;
+constexpr long long kMaxNpyBatch = 64ll << 20;   // image bytes of one .npy request on the batch path
 
-struct Item {  // one batchable image query
+struct Item {  // one batchable request: a JSON image query (count 1) or an npy batch of `count` images
   uint64_t conn;
   int io;
   uint64_t seq;
   bool close;
+  bool npy;
+  long long count;
   int ndim;
-  long long shape[8];
+  long long shape[8];   // ONE image
   std::vector<uint8_t> data;
 };
 
@@ -70,6 +76,8 @@ struct Ticket {  // where a response goes
   int io;
   uint64_t seq;
   bool close;
+  bool npy = false;      // respond with an .npy float32 [count, ncls] array instead of {"prediction": [...]}
+  long long count = 1;   // images of the batch that belong to this request
 };
 
 struct Generic {  // a request Python answers
@@ -243,6 +251,83 @@ bool ieq(const char* a, size_t n, const char* b) {
   return true;
 }
 
+// `.npy` (format 1.x-3.x) uint8 C-order array of >= 2 dims: fills the shape of ONE image (dims 1..),
+// the image count and the data offset; false for anything else (the generic Python route serves it)
+bool parse_npy_u8(const char* b, long long n, long long* count, long long* shape, int* ndim, long long* data_off) {
+  if (n < 12 || memcmp(b, "\x93NUMPY", 6) != 0) return false;
+  const int major = (unsigned char)b[6];
+  long long hl, h0;
+  if (major == 1) {
+    hl = (unsigned char)b[8] | ((unsigned char)b[9] << 8);
+    h0 = 10;
+  } else if (major == 2 || major == 3) {
+    hl = (long long)(unsigned char)b[8] | ((long long)(unsigned char)b[9] << 8) |
+         ((long long)(unsigned char)b[10] << 16) | ((long long)(unsigned char)b[11] << 24);
+    h0 = 12;
+  } else {
+    return false;
+  }
+  if (h0 + hl > n) return false;
+  std::string_view hd(b + h0, (size_t)hl);
+  auto value_of = [&](const char* key) -> std::string_view {
+    size_t k = hd.find(key);
+    if (k == std::string_view::npos) return {};
+    size_t c = hd.find(':', k);
+    if (c == std::string_view::npos) return {};
+    size_t v = c + 1;
+    while (v < hd.size() && hd[v] == ' ') ++v;
+    return hd.substr(v);
+  };
+  std::string_view d = value_of("'descr'"), f = value_of("'fortran_order'"), sh = value_of("'shape'");
+  if (!(d.substr(0, 5) == "'|u1'" || d.substr(0, 5) == "'<u1'") || f.substr(0, 5) != "False" || sh.empty() ||
+      sh[0] != '(')
+    return false;
+  long long dims[9];
+  int nd = 0;
+  size_t i = 1;
+  while (i < sh.size() && sh[i] != ')') {
+    while (i < sh.size() && (sh[i] == ' ' || sh[i] == ',')) ++i;
+    if (i < sh.size() && sh[i] == ')') break;
+    long long v = 0;
+    bool any = false;
+    while (i < sh.size() && sh[i] >= '0' && sh[i] <= '9') {
+      v = v * 10 + (sh[i++] - '0');
+      any = true;
+      if (v > (1ll << 40)) return false;
+    }
+    if (!any || nd == 9) return false;
+    dims[nd++] = v;
+  }
+  if (nd < 2 || nd > 9) return false;
+  long long per = 1;
+  for (int k = 1; k < nd; ++k) {
+    if (dims[k] <= 0) return false;
+    per *= dims[k];
+    if (per > (1ll << 40)) return false;
+  }
+  if (dims[0] <= 0 || dims[0] * per != n - h0 - hl) return false;
+  *count = dims[0];
+  *ndim = nd - 1;
+  for (int k = 1; k < nd; ++k) shape[k - 1] = dims[k];
+  *data_off = h0 + hl;
+  return true;
+}
+
+// .npy float32 [n][ncls] (format 1.0, header padded to a 64-byte boundary)
+std::string npy_f32(const float* v, long long n, long long ncls) {
+  std::string hd = "{'descr': '<f4', 'fortran_order': False, 'shape': (" + std::to_string(n) + ", " +
+                   std::to_string(ncls) + "), }";
+  const size_t total = (10 + hd.size() + 1 + 63) / 64 * 64;
+  hd.append(total - 10 - hd.size() - 1, ' ');
+  hd += '\n';
+  std::string o("\x93NUMPY\x01\x00", 8);
+  o += (char)(hd.size() & 255);
+  o += (char)(hd.size() >> 8);
+  o += hd;
+  o.append((const char*)v, (size_t)(n * ncls) * sizeof(float));
+  return o;
+}
+
 // parse + dispatch every complete request in c->in; returns false if the connection was closed
 bool process(IoThread* io, Conn* c) {
   Server* s = io->srv;
@@ -338,6 +423,8 @@ bool process(IoThread* io, Conn* c) {
         it.io = io->idx;
         it.seq = seq;
         it.close = close_req;
+        it.npy = false;
+        it.count = 1;
         {
           std::lock_guard<std::mutex> g(s->qmu);
           s->items.push_back(std::move(it));
@@ -346,6 +433,28 @@ bool process(IoThread* io, Conn* c) {
         if (close_req) c->closing = true;  // stop parsing; close after this response
         continue;
       }
+    }
+    // an .npy uint8 image batch joins the image queue whole (one batch thread, one graph replay, one
+    // .npy response); batches beyond max_batch images or max_query bytes per image go to Python
+    long long cnt = 0, doff = 0;
+    Item nit;
+    if (s->batching && method == "POST" && path == "/predict_batch_npy" &&
+        parse_npy_u8(body, clen, &cnt, nit.shape, &nit.ndim, &doff) && cnt <= s->max_batch &&
+        (clen - doff) / cnt <= s->max_query && clen - doff <= kMaxNpyBatch) {
+      nit.data.assign((const uint8_t*)body + doff, (const uint8_t*)body + clen);
+      nit.conn = c->id;
+      nit.io = io->idx;
+      nit.seq = seq;
+      nit.close = close_req;
+      nit.npy = true;
+      nit.count = cnt;
+      {
+        std::lock_guard<std::mutex> g(s->qmu);
+        s->items.push_back(std::move(nit));
+      }
+      s->qcv.notify_one();
+      if (close_req) c->closing = true;
+      continue;
     }
     Generic g{t, method, path, std::string(body, (size_t)clen)};
     uint64_t gid = s->next_id++;
@@ -545,10 +654,10 @@ void rt_http_set_max_query(void* h, long long bytes) {
   s->max_query = bytes > 0 ? bytes : (1 << 20);
 }
 
-// Blocks up to timeout_ms for pending image queries; takes every pending query of the first
-// query's shape (<= max_batch, <= cap bytes) into `out`.  Returns the query count (0: timeout,
-// -1: stopped, -3: `out` cannot hold one query of `shape`); `shape`/`ndim` describe ONE query,
-// `batch_id` identifies the batch for completion.
+// Blocks up to timeout_ms for pending image requests; takes every pending request whose images have
+// the first one's shape (<= max_batch images, <= cap bytes; an .npy request's images stay together)
+// into `out`.  Returns the image count (0: timeout, -1: stopped, -3: `out` cannot hold the first
+// request); `shape`/`ndim` describe ONE image, `batch_id` identifies the batch for completion.
 long long rt_http_next_batch(void* h, int timeout_ms, uint8_t* out, long long cap, long long* shape, int* ndim,
                              unsigned long long* batch_id) {
   auto* s = (Server*)h;
@@ -561,24 +670,26 @@ long long rt_http_next_batch(void* h, int timeout_ms, uint8_t* out, long long ca
   int nd = first.ndim;
   long long sh[8];
   memcpy(sh, first.shape, sizeof(sh));
-  size_t per = first.data.size();
+  size_t per = first.data.size() / (size_t)first.count;   // bytes of one image
   std::vector<Ticket> tickets;
   std::deque<Item> rest;
   long long n = 0;
   while (!s->items.empty()) {
     Item it = std::move(s->items.front());
     s->items.pop_front();
-    bool same = it.ndim == nd && it.data.size() == per && !memcmp(it.shape, sh, sizeof(long long) * (size_t)nd);
-    if (same && n < s->max_batch && (long long)((n + 1) * per) <= cap) {
-      memcpy(out + n * per, it.data.data(), per);
-      tickets.push_back(Ticket{it.conn, it.io, it.seq, it.close});
-      ++n;
+    bool same = it.ndim == nd && it.data.size() == per * (size_t)it.count &&
+                !memcmp(it.shape, sh, sizeof(long long) * (size_t)nd);
+    // a request's images stay together; the first request of a batch may alone exceed max_batch
+    if (same && (n == 0 || n + it.count <= s->max_batch) && (long long)((n + it.count) * per) <= cap) {
+      memcpy(out + n * per, it.data.data(), it.data.size());
+      tickets.push_back(Ticket{it.conn, it.io, it.seq, it.close, it.npy, it.count});
+      n += it.count;
     } else {
       rest.push_back(std::move(it));
     }
   }
   s->items.swap(rest);
-  if (n == 0) {  // one query exceeds the caller's buffer: report its shape, the caller grows the buffer
+  if (n == 0) {  // the first request exceeds the caller's buffer: report its shape, the caller grows the buffer
     *ndim = nd;
     for (int i = 0; i < nd; ++i) shape[i] = sh[i];
     return -3;
@@ -605,9 +716,18 @@ int rt_http_complete(void* h, unsigned long long batch_id, const float* probs, l
     tickets.swap(it->second);
     s->batches.erase(it);
   }
-  if ((long long)tickets.size() != n) return -2;
+  long long total = 0;
+  for (auto& t : tickets) total += t.count;
+  if (total != n) return -2;
   std::string body;
-  for (long long i = 0; i < n; ++i) {
+  long long i = 0;
+  for (const Ticket& t : tickets) {
+    if (t.npy) {
+      body = npy_f32(probs + i * ncls, t.count, ncls);
+      post(s, t, http_response(200, "application/octet-stream", body.data(), body.size(), t.close));
+      i += t.count;
+      continue;
+    }
     body.clear();
     body += "{\"prediction\": [";
     for (long long j = 0; j < ncls; ++j) {
@@ -615,8 +735,8 @@ int rt_http_complete(void* h, unsigned long long batch_id, const float* probs, l
       append_double(body, (double)probs[i * ncls + j]);
     }
     body += "]}";
-    const Ticket& t = tickets[(size_t)i];
     post(s, t, http_response(200, "application/json", body.data(), body.size(), t.close));
+    ++i;
   }
   return 0;
 }
@@ -631,7 +751,7 @@ int rt_http_fail(void* h, unsigned long long batch_id, const char* msg) {
     tickets.swap(it->second);
     s->batches.erase(it);
   }
-  s->errors += (long long)tickets.size();
+  for (auto& t : tickets) s->errors += t.count;
   size_t n = strlen(msg);
   for (auto& t : tickets) post(s, t, http_response(500, "text/plain", msg, n, t.close));
   return 0;

@@ -101,8 +101,9 @@ class EnsembleGraphs:
         self.lock = threading.Lock()
         self.stream = torch.cuda.Stream(device=self.device)
         self._branches = [torch.cuda.Stream(device=self.device) for _ in self.plan]
-        self._graphs: Dict[Tuple[int, bool], _Entry] = {}
+        self._graphs: Dict[Tuple[int, object], _Entry] = {}
         self._shapes: Dict[Tuple, Tuple] = {}
+        self._stage = self._stage_out = None
         self.replays = 0
 
     # ------------------------------------------------------------------ capture
@@ -127,7 +128,8 @@ class EnsembleGraphs:
         if e.host:
             e.h_out.copy_(e.out, non_blocking=True)
 
-    def _entry(self, bucket: int, host: bool) -> _Entry:
+    def _entry(self, bucket: int, host) -> _Entry:
+        """host: False (device in/out), True (own pinned buffers) or ('stage', slot) (the staging slot's)."""
         e = self._graphs.get((bucket, host))
         if e is not None:
             return e
@@ -136,16 +138,22 @@ class EnsembleGraphs:
         with _GRAPH_LOCK:
             return self._build_entry(bucket, host)
 
-    def _build_entry(self, bucket: int, host: bool) -> _Entry:
+    def _build_entry(self, bucket: int, host) -> _Entry:
         e = _Entry()
-        e.bucket, e.host = bucket, host
-        e.h_in = {s: torch.zeros((bucket,) + self._shapes[s], dtype=torch.uint8).pin_memory()
-                  for s in self.sigs} if host else None
+        e.bucket, e.host = bucket, bool(host)
+        if isinstance(host, tuple):   # a staging slot: views of its shared max-bucket pinned buffers
+            e.h_in = {self.sigs[0]: self._stage[host[1]][:bucket]}
+        else:
+            e.h_in = {s: torch.zeros((bucket,) + self._shapes[s], dtype=torch.uint8).pin_memory()
+                      for s in self.sigs} if host else None
         e.d_in = {s: torch.zeros((bucket,) + self._shapes[s], dtype=torch.uint8, device=self.device)
                   for s in self.sigs}
         e.slots = torch.zeros((len(self.models), bucket, self.num_classes), dtype=torch.float32, device=self.device)
         e.out = torch.zeros((bucket, self.num_classes), dtype=torch.float32, device=self.device)
-        e.h_out = torch.zeros((bucket, self.num_classes), dtype=torch.float32).pin_memory() if host else None
+        if isinstance(host, tuple):
+            e.h_out = self._stage_out[host[1]][:bucket]
+        else:
+            e.h_out = torch.zeros((bucket, self.num_classes), dtype=torch.float32).pin_memory() if host else None
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             self._body(e)          # eager warm-up: autotunes every GEMM shape, sizes the allocator
@@ -211,3 +219,41 @@ class EnsembleGraphs:
             res.record_stream(cur)
             self.replays += 1
             return res
+
+    # ------------------------------------------------------------------ double-buffered host path
+    def staging(self, shape: Tuple[int, ...]):
+        """Two pinned uint8 staging slots [BUCKETS[-1], *shape] (returned as flat numpy views) with their
+        pinned fp32 outputs, for a single-signature ensemble (None otherwise).  The native front end
+        decodes batch n+1 into one slot while the graph of batch n replays from the other: per bucket
+        and slot one graph whose H2D reads the slot and whose D2H writes the slot's output."""
+        if len(self.sigs) != 1:
+            return None
+        shape = tuple(int(v) for v in shape)
+        with self.lock:
+            if self._shapes.setdefault(self.sigs[0], shape) != shape:
+                return None
+            if self._stage is None:
+                n = BUCKETS[-1]
+                self._stage = [torch.zeros((n,) + shape, dtype=torch.uint8).pin_memory() for _ in range(2)]
+                self._stage_out = [torch.zeros((n, self.num_classes), dtype=torch.float32).pin_memory()
+                                   for _ in range(2)]
+        return [t.numpy().reshape(-1) for t in self._stage]
+
+    def launch_staged(self, slot: int, B: int):
+        """Replay the graph of staging slot ``slot`` for its first B images (B <= BUCKETS[-1]); returns an
+        event the caller waits on before reading ``staged_out(slot)[:B]``.  No host sync here."""
+        if not 0 < B <= BUCKETS[-1]:
+            raise ValueError('staged batch of {} images'.format(B))
+        bucket = next(b for b in BUCKETS if b >= B)
+        with self.lock:
+            e = self._entry(bucket, ('stage', slot))
+            with torch.cuda.stream(self.stream):
+                e.graph.replay()
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            self.replays += 1
+        return ev
+
+    def staged_out(self, slot: int) -> np.ndarray:
+        return self._stage_out[slot].numpy()
+

@@ -8,11 +8,17 @@ Division of labour:
 
 * C++ I/O threads (epoll) own every socket: HTTP/1.1 keep-alive parsing, JSON image queries decoded
   straight to uint8, response formatting and writing.  No per-request Python.
-* One Python batch thread per predictor replica loops on ``rt_http_next_batch`` (blocking in C++,
-  GIL released): it receives every image query pending at that moment as ONE contiguous uint8
-  batch, runs ``Predictor.predict_array`` (one hipGraph for the whole ensemble) and hands the
-  probabilities back with ``rt_http_complete``; C++ writes one ``{"prediction": [...]}`` per query.
-  Queries that arrive while the GPU runs batch k become batch k+1 — no timer, no per-query futures.
+* One Python batch thread per predictor replica, bound to that replica, loops on
+  ``rt_http_next_batch`` (blocking in C++, GIL released): it receives every image request pending at
+  that moment — single JSON queries and whole ``.npy`` batches — as ONE contiguous uint8 batch and
+  hands the probabilities back with ``rt_http_complete``; C++ writes one ``{"prediction": [...]}``
+  per JSON query and one ``.npy`` float32 array per npy request.  Queries that arrive while the GPU
+  runs batch k become batch k+1 — no timer, no per-query futures.
+* Double buffering: for a one-graph ensemble (``EnsembleGraphs.staging``) C++ decodes straight into
+  one of two pinned staging slots; batch k+1 is collected into slot B and its graph queued right
+  behind batch k's (slot A) before the thread waits for batch k and completes it.  Each replica has
+  its own graphs, stream and slots, so R replicas take disjoint batches from the C++ queue and run
+  concurrently.  Other predictors go through ``Predictor.predict_array``.
 * Everything else (non-image queries, batch routes, stats) is a generic request answered by a
   small Python pool, exactly as ``fastserve`` answers it.
 """
@@ -147,7 +153,107 @@ class NativePredictorServer:
         return out
 
     # ------------------------------------------------------------------------------ loops
-    def _batch_loop(self):
+    def _batch_loop(self, idx=0):
+        fn = getattr(self.predictor, 'staged_graphs', None)
+        staged = None
+        if callable(fn):
+            try:
+                staged = fn(idx)
+            except Exception:
+                logger.error('replica %d: no staged ensemble graphs:\n%s', idx, traceback.format_exc())
+        if staged is not None:
+            bufs = staged[1].staging(staged[2])
+            if bufs is not None:
+                return self._staged_loop(staged[1], staged[2], bufs)
+        return self._plain_loop()
+
+    def _complete(self, bid, probs, n):
+        h = _lib()
+        try:
+            probs = np.ascontiguousarray(np.asarray(probs), dtype=np.float32)
+            if probs.ndim != 2 or probs.shape[0] < n:
+                raise ValueError('predictor returned shape {} for {} queries'.format(probs.shape, n))
+            h.rt_http_complete(self._h, bid, probs.ctypes.data, int(n), int(probs.shape[1]))
+            self._base['python_batches'] += 1
+        except Exception as e:
+            self._fail(bid, e)
+
+    def _fail(self, bid, e):
+        self._base['python_errors'] += 1
+        logger.error('predictor batch failed: %r', e)
+        _lib().rt_http_fail(self._h, bid, '{}: {}'.format(type(e).__name__, e).encode('utf-8', 'replace'))
+
+    def _staged_loop(self, g, img_shape, bufs):
+        """Double-buffered loop over one replica's ensemble graphs: collect batch k+1 into the free
+        staging slot and queue its replay before waiting for batch k."""
+        h = _lib()
+        cap = int(bufs[0].size)
+        shape = (ctypes.c_longlong * 8)()
+        nd = ctypes.c_int(0)
+        bid = ctypes.c_ulonglong(0)
+        pending = None   # (event, slot, batch id, images)
+        slot = 0
+        big = None       # fallback buffer for requests the staging slot cannot hold
+        while self._running.is_set():
+            launched = None
+            try:
+                n = h.rt_http_next_batch(self._h, 0 if pending else 100, bufs[slot].ctypes.data, cap, shape,
+                                         ctypes.byref(nd), ctypes.byref(bid))
+                if n == -1:
+                    break
+                if n == -3:   # larger than a staging slot: take it into the bounded fallback buffer
+                    pending = self._finish_staged(g, pending)
+                    if big is None:
+                        big = np.empty(MAX_BATCH_BUF, dtype=np.uint8)
+                    n = h.rt_http_next_batch(self._h, 0, big.ctypes.data, big.size, shape, ctypes.byref(nd),
+                                             ctypes.byref(bid))
+                    if n > 0:
+                        q = tuple(int(shape[i]) for i in range(nd.value))
+                        arr = big[:n * math.prod(q)].reshape((int(n),) + q)
+                        self._run_sync(bid.value, arr, n)
+                    continue
+                if n > 0:
+                    q = tuple(int(shape[i]) for i in range(nd.value))
+                    if q == tuple(img_shape):
+                        try:
+                            launched = (g.launch_staged(slot, int(n)), slot, bid.value, int(n))
+                        except Exception as e:
+                            self._fail(bid.value, e)
+                        slot ^= 1
+                    else:   # another image shape (resized by the models): the synchronous array path
+                        pending = self._finish_staged(g, pending)
+                        arr = bufs[slot][:n * math.prod(q)].reshape((int(n),) + q).copy()
+                        self._run_sync(bid.value, arr, n)
+            except Exception:   # never let the replica's only batch thread die
+                self._base['python_errors'] += 1
+                logger.error('batch loop error:\n%s', traceback.format_exc())
+            pending = self._finish_staged(g, pending)
+            pending = launched
+        self._finish_staged(g, pending)
+
+    def _finish_staged(self, g, pending):
+        """Wait for a launched staged batch and complete it; returns None (the new 'pending')."""
+        if pending is None:
+            return None
+        ev, slot, bid, n = pending
+        try:
+            ev.synchronize()
+        except Exception as e:
+            self._fail(bid, e)
+            return None
+        self.predictor.stats['queries'] = self.predictor.stats.get('queries', 0) + n
+        self._complete(bid, g.staged_out(slot), n)
+        return None
+
+    def _run_sync(self, bid, arr, n):
+        try:
+            probs = self.predictor.predict_array(arr)
+        except Exception as e:
+            self._fail(bid, e)
+            return
+        self._complete(bid, probs, n)
+
+    def _plain_loop(self):
         h = _lib()
         cap = max(1, self.max_batch) * 32 * 32 * 3
         buf = np.empty(cap, dtype=np.uint8)
@@ -163,8 +269,8 @@ class NativePredictorServer:
                 if n == -1:
                     break
                 per = int(math.prod(int(shape[i]) for i in range(nd.value)))
-                if n == -3:   # one query of this shape does not fit: grow (bounded; C++ caps a query at MAX_QUERY)
-                    cap = max(cap, per, min(per * self.max_batch, MAX_BATCH_BUF))
+                if n == -3:   # the first request does not fit: grow to the bound (C++ keeps requests below it)
+                    cap = max(cap, MAX_BATCH_BUF)
                     buf = np.empty(cap, dtype=np.uint8)
                     continue
             except Exception:   # never let the replica's only batch thread die
@@ -173,16 +279,7 @@ class NativePredictorServer:
                 continue
             q = tuple(int(shape[i]) for i in range(nd.value))
             arr = buf[:n * per].reshape((int(n),) + q)
-            try:
-                probs = np.ascontiguousarray(np.asarray(self.predictor.predict_array(arr)), dtype=np.float32)
-                if probs.ndim != 2 or probs.shape[0] != n:
-                    raise ValueError('predictor returned shape {} for {} queries'.format(probs.shape, n))
-                h.rt_http_complete(self._h, bid.value, probs.ctypes.data, int(n), int(probs.shape[1]))
-                self._base['python_batches'] += 1
-            except Exception as e:
-                self._base['python_errors'] += 1
-                logger.error('predictor batch failed:\n%s', traceback.format_exc())
-                h.rt_http_fail(self._h, bid.value, '{}: {}'.format(type(e).__name__, e).encode('utf-8', 'replace'))
+            self._run_sync(bid.value, arr, n)
 
     def _serve_generic(self, rid, method, path, body):
         h = _lib()
@@ -227,7 +324,8 @@ class NativePredictorServer:
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self.generic_threads,
                                                            thread_name_prefix='rafiki-http-py')
         for i in range(self.slots):
-            t = threading.Thread(target=self._batch_loop, name='rafiki-http-batch-{}'.format(i), daemon=True)
+            t = threading.Thread(target=self._batch_loop, args=(i,), name='rafiki-http-batch-{}'.format(i),
+                                 daemon=True)
             t.start()
             self._threads.append(t)
         t = threading.Thread(target=self._generic_loop, name='rafiki-http-generic', daemon=True)

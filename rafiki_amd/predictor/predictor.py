@@ -295,6 +295,24 @@ class Predictor:
                     return self._proba_device_on(r, inputs).cpu().numpy()
         return self.predict(arr.tolist())
 
+    def staged_graphs(self, idx):
+        """(replica, its ensemble graphs, the image shape they take) for replica ``idx`` — what the native
+        front end's double-buffered batch loop drives directly — or None when that replica has no
+        one-graph ensemble or takes several input signatures."""
+        if not self._fast_path() or idx >= len(self.replicas):
+            return None
+        r = self.replicas[idx]
+        if not all(callable(getattr(m, 'input_signature', None)) for _, m in r.models):
+            return None
+        g = self._ensemble_graphs(r)
+        if g is None or len(g.sigs) != 1:
+            return None
+        sig = g.sigs[0]
+        if not (isinstance(sig, tuple) and len(sig) == 3 and sig[0] == 'image_u8'):
+            return None
+        size, ch = int(sig[1]), int(sig[2])
+        return r, g, ((size, size) if ch == 1 else (size, size, ch))
+
     def _predict_remote(self, queries):
         """Fan the batch out to every worker first, then gather (workers run concurrently); a worker
         that misses the deadline is dropped from this batch's ensemble (partial-ensemble fallback)."""

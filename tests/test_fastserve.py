@@ -166,3 +166,77 @@ def test_native_oversized_query_takes_the_generic_path(monkeypatch):
         assert small.status_code == 200 and srv.counters['batched_queries'] == 1
     finally:
         srv.shutdown()
+
+
+def _npy(a):
+    buf = io.BytesIO()
+    np.save(buf, a, allow_pickle=False)
+    return buf.getvalue()
+
+
+def test_native_npy_batches_join_the_image_queue():
+    """POST /predict_batch_npy with a uint8 body is decoded in C++ and batched with concurrent JSON
+    queries of the same image shape (one predict_array call can serve both); the reply is an .npy
+    float32 array.  Non-uint8 arrays and batches above max_batch take the generic Python path."""
+    from rafiki_amd.predictor import nativeserve
+    if not nativeserve.available():
+        pytest.skip('librafiki_runtime.so not built')
+    fake = FakePredictor()
+    srv = nativeserve.NativePredictorServer(fake, '127.0.0.1', 0, max_batch=64).start()
+    try:
+        url = 'http://127.0.0.1:{}'.format(srv.port)
+        rng = np.random.default_rng(1)
+        qs = rng.integers(0, 200, (40, 3, 4), dtype=np.uint8)
+        r = requests.post(url + '/predict_batch_npy', data=_npy(qs))
+        assert r.status_code == 200 and r.headers['Content-Type'] == 'application/octet-stream'
+        got = np.load(io.BytesIO(r.content), allow_pickle=False)
+        assert got.dtype == np.float32 and np.array_equal(got, fake._probs(qs))
+        assert srv.counters['batched_queries'] == 40 and srv.counters['generic_requests'] == 0
+        # many npy batches and single JSON queries at once: every reply is its own slice
+        out, errs = {}, []
+
+        def npy_client(k):
+            try:
+                s = requests.Session()
+                for j in range(4):
+                    a = qs[(k + j) % 8 * 5:(k + j) % 8 * 5 + 5]
+                    out[('n', k, j)] = (np.load(io.BytesIO(s.post(url + '/predict_batch_npy', data=_npy(a)).content)),
+                                        fake._probs(a))
+            except Exception as e:
+                errs.append(e)
+
+        def json_client(k):
+            try:
+                s = requests.Session()
+                for j in range(6):
+                    q = qs[(k * 6 + j) % 40]
+                    out[('j', k, j)] = (np.asarray(s.post(url + '/predict', json={'query': q.tolist()}).json()
+                                                   ['prediction']), fake._probs(q[None])[0])
+            except Exception as e:
+                errs.append(e)
+        ts = [threading.Thread(target=npy_client, args=(k,)) for k in range(4)] + \
+             [threading.Thread(target=json_client, args=(k,)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not errs, errs
+        assert len(out) == 4 * 4 + 4 * 6
+        for got, want in out.values():
+            assert np.allclose(got, want)
+        g0 = srv.counters['generic_requests']
+        # float32 npy: generic path (np.load + predict_array), same wire format
+        r = requests.post(url + '/predict_batch_npy', data=_npy(qs[:3].astype(np.float32)))
+        assert r.status_code == 200 and np.allclose(np.load(io.BytesIO(r.content)), fake._probs(qs[:3]))
+        # above max_batch images: generic path
+        big = rng.integers(0, 200, (70, 3, 4), dtype=np.uint8)
+        r = requests.post(url + '/predict_batch_npy', data=_npy(big))
+        assert r.status_code == 200 and np.allclose(np.load(io.BytesIO(r.content)), fake._probs(big))
+        assert srv.counters['generic_requests'] == g0 + 2
+        # a poisoned npy batch fails as a whole with 500, the server keeps serving
+        bad = qs[:2].copy()
+        bad[1, 0, 0] = 255
+        assert requests.post(url + '/predict_batch_npy', data=_npy(bad)).status_code == 500
+        assert requests.post(url + '/predict', json={'query': qs[0].tolist()}).status_code == 200
+    finally:
+        srv.shutdown()

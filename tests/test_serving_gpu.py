@@ -413,3 +413,63 @@ def test_native_http_front_end_serves_the_gpu_ensemble(ensemble):
         srv.shutdown()
     assert np.allclose(np.asarray(out), ref, atol=1e-5)
     assert c['batched_queries'] == len(imgs) and c['batches'] <= len(imgs)
+    assert p.replicas[0].graphs is not None and p.replicas[0].graphs._stage is not None   # double-buffered path
+
+
+def test_native_front_end_npy_and_two_replicas_double_buffered(ensemble):
+    """Two replicas behind the C++ front end, each with its own batch thread, staging slots and graphs:
+    .npy batches and JSON queries from concurrent clients are answered exactly as predict_array, and both
+    replicas take batches (disjoint pulls from the C++ queue)."""
+    import io as _io
+
+    import requests
+
+    from rafiki_amd.model.dataset import synthetic_images
+    from rafiki_amd.predictor import nativeserve
+    from rafiki_amd.predictor.predictor import Predictor
+    if not nativeserve.available():
+        pytest.skip('librafiki_runtime.so not built')
+    p = Predictor(_copy_ensemble(ensemble), replicas=[_copy_ensemble(ensemble)])
+    imgs, _ = synthetic_images(96, size=32, channels=3, classes=10, seed=9)
+    ref = Predictor(ensemble).predict_array(imgs)
+    srv = nativeserve.NativePredictorServer(p, '127.0.0.1', 0).start()
+    url = 'http://127.0.0.1:{}'.format(srv.port)
+    out, errs = {}, []
+
+    def npy_client(k):
+        try:
+            s = requests.Session()
+            for j in range(3):
+                lo = ((k * 3 + j) % 12) * 8
+                buf = _io.BytesIO()
+                np.save(buf, imgs[lo:lo + 8], allow_pickle=False)
+                r = s.post(url + '/predict_batch_npy', data=buf.getvalue())
+                out[('n', lo)] = (np.load(_io.BytesIO(r.content), allow_pickle=False), ref[lo:lo + 8])
+        except Exception as e:
+            errs.append(e)
+
+    def json_client(k):
+        try:
+            s = requests.Session()
+            for j in range(6):
+                i = (k * 6 + j) % 96
+                r = s.post(url + '/predict', json={'query': imgs[i].tolist()})
+                out[('j', i)] = (np.asarray(r.json()['prediction']), ref[i])
+        except Exception as e:
+            errs.append(e)
+    try:
+        ts = [threading.Thread(target=npy_client, args=(k,)) for k in range(4)] + \
+             [threading.Thread(target=json_client, args=(k,)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        c = srv.counters
+    finally:
+        srv.shutdown()
+    assert not errs, errs
+    for got, want in out.values():
+        assert np.allclose(got, want, atol=1e-5)
+    assert c['generic_requests'] == 0 and c['errors'] == 0
+    assert all(r.graphs is not None and r.graphs._stage is not None for r in p.replicas)
+    assert all(r.graphs.replays > 0 for r in p.replicas), [r.graphs.replays for r in p.replicas]
