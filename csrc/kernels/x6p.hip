@@ -21,6 +21,7 @@
 //     XCD-aware remap (a group's tiles share their A / B panels in one XCD's L2).
 #include "common.h"
 #include <cstdlib>
+#include <utility>
 
 namespace {
 
@@ -39,7 +40,7 @@ struct XpParams {
   int groups, flags;            // flags: 1 = accumulate into C
   int splits, ktPer;            // split-K: split s covers K-tiles [s ktPer, (s+1) ktPer), writes slab s
   long long slabStride;         // elements between split-K slabs of C
-  int dbg;                      // timing diagnostics (RAFIKI_X6P_DBG): 1 no DMA in the K loop, 2 no MFMAs
+  int dbg;                      // unused
   unsigned long long bytesA, bytesB;
 };
 
@@ -78,10 +79,12 @@ struct XOp {
   // live = false: zeros (keeps the issue code branch-free at the end of the K loop)
   RK_DEV void issue(char* tile, int kt, int wid, bool live) const {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const unsigned o = (off[q] + (unsigned)kt * (unsigned)RB) | ((unsigned)!live << 31);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(tile + (wid * NQ + q) * 1024), 16, (int)o, 0, 0, 0);
-    }
+    for (int q = 0; q < NQ; ++q) issue_q(tile, kt, wid, live, q);
+  }
+  // one DMA wave-instruction (1 KiB) of this wave's share
+  RK_DEV void issue_q(char* tile, int kt, int wid, bool live, int q) const {
+    const unsigned o = (off[q] + (unsigned)kt * (unsigned)RB) | ((unsigned)!live << 31);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(tile + (wid * NQ + q) * 1024), 16, (int)o, 0, 0, 0);
   }
 
   // plane p, rows r0 .. r0+31, 16-deep chunk cc of the K-tile: lane (r, h) holds k = 16 cc + 8 h + j
@@ -91,6 +94,30 @@ struct XOp {
     return *(const bf16x8*)(tile + p * (T * RB) + r * RB + ((c ^ xswz<KT>(r)) << 4));
   }
 };
+
+// Schedule of one 16-deep chunk: NM MFMAs; the NR LDS reads of the next chunk's fragments go out one per
+// MFMA from the first; the NV DMA pieces of a later K-tile are spread evenly among the MFMAs (an LDS-DMA
+// wave-instruction costs ~60 issue cycles, two MFMA slots: issued in a cluster in front of the MFMAs they
+// left the matrix core idle for L x 60 cycles per K-tile)
+template <class F, int... I>
+RK_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+RK_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int NM, int NR, int NV>
+RK_DEV void xp_sched() {
+  static_assert(NR <= NM, "one fragment read per MFMA slot");
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (m < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    if ((m + 1) * NV / NM > m * NV / NM) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+  }
+}
 
 template <int WGM, int WGN, int MI, int NI, int NST, int KT>
 __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams p) {
@@ -138,6 +165,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
     }
   }
 
+  constexpr int NC = KT / 16;                 // 16-deep chunks per K-tile
+  constexpr int LA = XOp<BM, NW, KT>::NQ;
+  constexpr int NM = 6 * MI * NI;             // MFMAs per chunk
+  constexpr int NR = 3 * (MI + NI);           // fragment reads per chunk
   int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt has landed once only the younger tiles' DMAs are outstanding
@@ -152,44 +183,43 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
     const char* Bs = As + ABYTES;
     const bool more = kt + NST - 1 < nk;
     char* nxt = smem + (st == 0 ? NST - 1 : st - 1) * SB;   // stage of tile kt + NST - 1
-    // per 32-deep half of the K-tile both chunks' fragments are read up front (the second set lands while
-    // the first chunk's MFMAs run); the next tile's DMAs go out after the first half's reads
+    // fragments double-buffered in registers: chunk c+1's are read while chunk c's MFMAs run; the DMA
+    // pieces of tile kt + NST - 1 are spread over the tile's chunks and interleaved with the MFMAs
+    bf16x8 fa[2][3][MI], fb[2][3][NI];
 #pragma unroll
-    for (int hf = 0; hf < KT / 32; ++hf) {
-      bf16x8 a[2][3][MI], b[2][3][NI];
+    for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2)
+      for (int i = 0; i < MI; ++i) fa[0][pl][i] = A.frag(As, pl, wm * 32 * MI + i * 32, 0, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[0][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, 0, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<NC>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      constexpr int cur = c & 1, nx = cur ^ 1;
+      if constexpr (c + 1 < NC) {
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-          for (int i = 0; i < MI; ++i) a[c2][pl][i] = A.frag(As, pl, wm * 32 * MI + i * 32, 2 * hf + c2, lane);
+          for (int i = 0; i < MI; ++i) fa[nx][pl][i] = A.frag(As, pl, wm * 32 * MI + i * 32, c + 1, lane);
 #pragma unroll
-          for (int j = 0; j < NI; ++j) b[c2][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, 2 * hf + c2, lane);
+          for (int j = 0; j < NI; ++j) fb[nx][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, c + 1, lane);
         }
-      if (hf == 0 && !(p.dbg & 1)) {
-        A.issue(nxt, kt + NST - 1, wid, more);
-        B.issue(nxt + ABYTES, kt + NST - 1, wid, more);
       }
-      if (p.dbg & 2) {   // keep the fragment reads, drop the MFMAs
 #pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2)
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-            for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(a[c2][pl][i]));
-#pragma unroll
-            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(b[c2][pl][j]));
-          }
-      } else {
-#pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2)
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j)
-              acc[i][j] = mfma6(a[c2][0][i], a[c2][1][i], a[c2][2][i], b[c2][0][j], b[c2][1][j], b[c2][2][j], acc[i][j]);
+      for (int q = L * c / NC; q < L * (c + 1) / NC; ++q) {
+        if (q < LA) A.issue_q(nxt, kt + NST - 1, wid, more, q);
+        else B.issue_q(nxt + ABYTES, kt + NST - 1, wid, more, q - LA);
       }
-    }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = mfma6(fa[cur][0][i], fa[cur][1][i], fa[cur][2][i], fb[cur][0][j], fb[cur][1][j], fb[cur][2][j],
+                            acc[i][j]);
+      xp_sched<NM, (c + 1 < NC ? NR : 0), L * (c + 1) / NC - L * c / NC>();
+      __builtin_amdgcn_sched_barrier(0);
+    });
     st = st + 1 == NST ? 0 : st + 1;
   }
   s_wait_vmcnt<0>();   // the trailing zero-DMAs land before the workgroup's LDS is released
@@ -290,8 +320,7 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   p.splits = rk_cdiv(nk, p.ktPer);   // every split gets >= 1 K-tile
   if (p.splits != splits) return RK_EBADARG;
   p.slabStride = splits > 1 ? slabStride : 0;
-  static const int dbg = getenv("RAFIKI_X6P_DBG") ? atoi(getenv("RAFIKI_X6P_DBG")) : 0;
-  p.dbg = dbg;
+  p.dbg = 0;
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   const hipStream_t st = (hipStream_t)stream;
   switch (tile) {

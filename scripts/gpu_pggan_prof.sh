@@ -1,5 +1,6 @@
 #!/bin/bash
-# PG-GAN per-kernel steady-state time (kernel trace) + one PMC pass (MFMA utilisation) at one LOD.
+# PG-GAN per-kernel steady-state time (kernel trace) + PMC passes (MFMA utilisation; HBM fetch; HBM write)
+# at one LOD.
 #   scripts/gpu_pggan_prof.sh <lod> [steps]  -> gpurun_out/pgprof_lod<lod>/{kernels.txt,kernels.csv,pmc.txt}
 set -e -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -15,9 +16,15 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES S
   SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
   --output-format csv -d $OUT/p0 -o run -- python3 scripts/bench_pg_gan.py --lods $LOD --steps 2 --warmup 1 \
   > $OUT/p0.log 2>&1
-python3 scripts/pmc_summary.py $OUT/p0 --steps 2 --marker lerp_kernel --durations $OUT/kernels.csv \
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE \
+  --output-format csv -d $OUT/p1 -o run -- python3 scripts/bench_pg_gan.py --lods $LOD --steps 2 --warmup 1 \
+  > $OUT/p1.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE GRBM_GUI_ACTIVE \
+  --output-format csv -d $OUT/p2 -o run -- python3 scripts/bench_pg_gan.py --lods $LOD --steps 2 --warmup 1 \
+  > $OUT/p2.log 2>&1
+python3 scripts/pmc_summary.py $OUT/p0 $OUT/p1 $OUT/p2 --steps 2 --marker lerp_kernel --durations $OUT/kernels.csv \
   --csv $OUT/pmc.csv > $OUT/pmc.txt
-rm -rf $OUT/t $OUT/p0
+rm -rf $OUT/t $OUT/p0 $OUT/p1 $OUT/p2
 tail -1 $OUT/t.log | cut -c1-300
 head -40 $OUT/kernels.txt
 tail -3 $OUT/pmc.txt
