@@ -217,8 +217,10 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restri
                                                            uint4* __restrict__ out, int* __restrict__ out_y,
                                                            double* __restrict__ zero, long long zero_n,
                                                            int* __restrict__ done, const float* __restrict__ lr_table,
-                                                           float* __restrict__ lr_out) {
-  const long long step = *counter;
+                                                           float* __restrict__ lr_out, int nsteps, long long nrows) {
+  // the schedule holds nsteps rows: a counter past it wraps around (warm-up runs, extra replays) instead
+  // of reading beyond the buffers; row indices outside the dataset read row 0
+  const long long step = (long long)((unsigned)*counter % (unsigned)nsteps);
   // the step's learning-rate multiplier from a per-step table (a schedule inside the replayed graph)
   if (lr_table && blockIdx.x == 0 && threadIdx.x == 0) *lr_out = lr_table[step];
   const long long total = (long long)B * row_vec;
@@ -226,7 +228,8 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restri
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gstride) {
     const int b = (int)(i / row_vec);
     const long long c = i - (long long)b * row_vec;
-    const long long src = sched[step * B + b];
+    long long src = sched[step * B + b];
+    if ((unsigned long long)src >= (unsigned long long)nrows) src = 0;
     out[i] = data[src * row_vec + c];
     if (c == 0 && out_y) out_y[b] = labels[src];
   }
@@ -614,14 +617,16 @@ extern "C" int rk_conv_wt(const void* src, void* dst, const int* desc, int nbloc
 }
 
 // lr_table (nullable): *lr_out = lr_table[*counter] (the optimizer kernel later in the step reads lr_out)
+// sched [nsteps][B] row indices into data [nrows][row_bytes]; lr_table [nsteps]
 extern "C" int rk_gather_batch(const void* data, long long row_bytes, const int* labels, const long long* sched,
                                int* counter, int B, void* out, int* out_y, double* zero, long long zero_n, int* done,
-                               const float* lr_table, float* lr_out, void* stream) {
+                               const float* lr_table, float* lr_out, int nsteps, long long nrows, void* stream) {
   if (row_bytes % 16 || zero_n < 0 || (zero_n && !zero) || (lr_table && !lr_out)) return RK_EUNSUPPORTED;
+  if (nsteps <= 0 || nrows <= 0) return RK_EBADARG;
   const long long rv = row_bytes / 16;
   hipLaunchKernelGGL(gather_batch_kernel, dim3(grid_for((long long)B * rv, 2048)), dim3(256), 0, (hipStream_t)stream,
                      (const uint4*)data, rv, labels, sched, counter, B, (uint4*)out, out_y, zero, zero_n, done,
-                     lr_table, lr_out);
+                     lr_table, lr_out, nsteps, nrows);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

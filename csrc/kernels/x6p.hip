@@ -40,7 +40,7 @@ struct XpParams {
   int groups, flags;            // flags: 1 = accumulate into C
   int splits, ktPer;            // split-K: split s covers K-tiles [s ktPer, (s+1) ktPer), writes slab s
   long long slabStride;         // elements between split-K slabs of C
-  int dbg;                      // unused
+  int dbg;                      // DBG builds: 1 no DMA in the K loop, 2 no MFMAs
   unsigned long long bytesA, bytesB;
 };
 
@@ -119,7 +119,8 @@ RK_DEV void xp_sched() {
   }
 }
 
-template <int WGM, int WGN, int MI, int NI, int NST, int KT>
+// DBG: timing-diagnostic build (RAFIKI_X6P_DBG, tiles 0 and 3): p.dbg 1 = no DMA in the K loop, 2 = no MFMAs
+template <int WGM, int WGN, int MI, int NI, int NST, int KT, bool DBG = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams p) {
   constexpr int NW = WGM * WGN;
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
@@ -206,17 +207,29 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
           for (int j = 0; j < NI; ++j) fb[nx][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, c + 1, lane);
         }
       }
+      if (!DBG || !(p.dbg & 1)) {
 #pragma unroll
-      for (int q = L * c / NC; q < L * (c + 1) / NC; ++q) {
-        if (q < LA) A.issue_q(nxt, kt + NST - 1, wid, more, q);
-        else B.issue_q(nxt + ABYTES, kt + NST - 1, wid, more, q - LA);
+        for (int q = L * c / NC; q < L * (c + 1) / NC; ++q) {
+          if (q < LA) A.issue_q(nxt, kt + NST - 1, wid, more, q);
+          else B.issue_q(nxt + ABYTES, kt + NST - 1, wid, more, q - LA);
+        }
       }
+      if (DBG && (p.dbg & 2)) {   // keep the fragment reads, drop the MFMAs
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+        for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = mfma6(fa[cur][0][i], fa[cur][1][i], fa[cur][2][i], fb[cur][0][j], fb[cur][1][j], fb[cur][2][j],
-                            acc[i][j]);
+          for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[cur][pl][i]));
+#pragma unroll
+          for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fb[cur][pl][j]));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = mfma6(fa[cur][0][i], fa[cur][1][i], fa[cur][2][i], fb[cur][0][j], fb[cur][1][j],
+                              fb[cur][2][j], acc[i][j]);
+      }
       xp_sched<NM, (c + 1 < NC ? NR : 0), L * (c + 1) / NC - L * c / NC>();
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -244,7 +257,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
   }
 }
 
-template <int WGM, int WGN, int MI, int NI, int KT>
+template <int WGM, int WGN, int MI, int NI, int KT, bool DBG = false>
 int xp_launch(const XpParams& p, int nst, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
   constexpr int SB = 3 * (BM + BN) * 2 * KT;
@@ -253,12 +266,12 @@ int xp_launch(const XpParams& p, int nst, hipStream_t st) {
   const dim3 grid((unsigned)blocks), block(64 * WGM * WGN);
   if (nst == 3) {
     if constexpr (3 * SB <= 163840)
-      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 3, KT>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 3, KT, DBG>), grid, block, 0, st, p);
     else
       return RK_EUNSUPPORTED;
   } else {
     if constexpr (2 * SB <= 163840)
-      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 2, KT>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 2, KT, DBG>), grid, block, 0, st, p);
     else
       return RK_EUNSUPPORTED;
   }
@@ -308,7 +321,8 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   // every in-group byte offset must stay below the 2 GiB buffer range
   if ((2 * psA + (long long)M * lda) * 2 >= (1ll << 31) || (2 * psB + (long long)N * ldb) * 2 >= (1ll << 31))
     return RK_EUNSUPPORTED;
-  if (groups > 1 && (gsA < 3 * psA || gsB < 3 * psB || gsC < (long long)M * ldc)) return RK_EBADARG;
+  // gsA / gsB == 0: one operand shared by every group (broadcast)
+  if (groups > 1 && ((gsA && gsA < 3 * psA) || (gsB && gsB < 3 * psB) || gsC < (long long)M * ldc)) return RK_EBADARG;
   if (2 * (gsA * (groups - 1) + 3 * psA) > bytesA || 2 * (gsB * (groups - 1) + 3 * psB) > bytesB) return RK_EBADARG;
   XpParams p;
   p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = C;
@@ -320,9 +334,12 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   p.splits = rk_cdiv(nk, p.ktPer);   // every split gets >= 1 K-tile
   if (p.splits != splits) return RK_EBADARG;
   p.slabStride = splits > 1 ? slabStride : 0;
-  p.dbg = 0;
+  static const int dbg = getenv("RAFIKI_X6P_DBG") ? atoi(getenv("RAFIKI_X6P_DBG")) : 0;
+  p.dbg = dbg;
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   const hipStream_t st = (hipStream_t)stream;
+  if (dbg && kt == 32 && (tile == 0 || tile == 3))
+    return tile == 0 ? xp_launch<2, 2, 2, 2, 32, true>(p, nst, st) : xp_launch<2, 2, 1, 1, 32, true>(p, nst, st);
   switch (tile) {
     case 0: return xp_launch_kt<2, 2, 2, 2>(p, nst, kt, st);
     case 1: return xp_launch_kt<2, 2, 2, 1>(p, nst, kt, st);

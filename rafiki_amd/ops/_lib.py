@@ -38,7 +38,7 @@ _SIGS = {
     "rk_bn_act_fwd": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "rk_bn_bwd_reduce": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
     "rk_bn_bwd_rows": [i64, i32],
-    "rk_gather_batch": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i64, vp, vp, vp, vp],
+    "rk_gather_batch": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i64, vp, vp, vp, i32, i64, vp],
     "rk_reduce_slabs_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, vp, i32, vp],
     "rk_slab_epi": [vp, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp],
     "rk_conv_wt": [vp, vp, vp, i32, vp, vp],

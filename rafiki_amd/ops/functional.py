@@ -809,8 +809,13 @@ def gather_batch(data, labels, sched, counter, out_x, out_y, *, zero=None, done=
     row_bytes = data[0].numel() * data.element_size()
     if zero is not None:
         assert zero.dtype == torch.float64 and zero.is_contiguous()
+    if sched.dim() != 2 or sched.shape[1] != B or sched.dtype != torch.int64:
+        raise ValueError('sched must be int64 [steps, {}], got {} {}'.format(B, sched.dtype, tuple(sched.shape)))
+    if lr_table is not None and lr_table.numel() < sched.shape[0]:
+        raise ValueError('lr_table shorter than the schedule')
     _lib.call("rk_gather_batch", _p(data), row_bytes, _p(labels), _p(sched), _p(counter), B, _p(out_x), _p(out_y),
-              _p(zero), 0 if zero is None else zero.numel(), _p(done), _p(lr_table), _p(lr_out), _s())
+              _p(zero), 0 if zero is None else zero.numel(), _p(done), _p(lr_table), _p(lr_out), sched.shape[0],
+              data.shape[0], _s())
     return out_x
 
 

@@ -1,6 +1,9 @@
 """Pre-split X6 GEMM (x6p.hip) on the 36-group GEMMs of the VGG-small pre-transformed F(4x4) layers
 (batch 256): microseconds and fp32-equivalent TFLOP/s of every tile / ring depth, against the X6 bf16
-peak (2.5 PFLOP/s / 6 products = 417 TFLOP/s).  usage: python scripts/bench_x6p.py [out.jsonl]"""
+peak (2.5 PFLOP/s / 6 products = 417 TFLOP/s).  usage: python scripts/bench_x6p.py [out.jsonl]
+X6P_CFGS="tile,nst,splits;..." restricts the configs; X6P_SHARED=1 gives every group the SAME A and B (group
+strides 0: the operands stay L2-resident — separates L2/HBM supply from the CU-side intake); RAFIKI_X6P_DBG=1|2
+(tiles 0 / 3): no DMA in the K loop | no MFMAs."""
 import json
 import os
 import sys
@@ -36,12 +39,22 @@ def t(fn, reps=20):
 SHAPES = [('c5f', 1024, 256, 256), ('c6f', 256, 512, 256), ('c7f', 256, 512, 512), ('c4d', 1024, 128, 256),
           ('c6d', 256, 256, 512), ('c5w', 256, 256, 1024), ('c7w', 512, 512, 256)]
 res = []
+SHARED = os.environ.get('X6P_SHARED') == '1'
+
+
+def gemm(a, b, out, M, N, K, tile, nst, sp):
+    if not SHARED:
+        return S.x6p_gemm(a, b, out, M, N, K, groups=36, tile=tile, nst=nst, splits=sp)
+    _lib.call("rk_x6p_gemm", tile, nst, a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, K, K, N, M * K, N * K,
+              0, 0, M * N, 36, 0, sp, 36 * M * N, a.numel() * 2, b.numel() * 2, torch.cuda.current_stream().cuda_stream)
+
+
 for name, M, N, K in SHAPES:
-    a = torch.randn(36, 3, M, K, device='cuda').to(torch.bfloat16)
-    b = torch.randn(36, 3, N, K, device='cuda').to(torch.bfloat16)
+    a = torch.randn(1 if SHARED else 36, 3, M, K, device='cuda').to(torch.bfloat16)
+    b = torch.randn(1 if SHARED else 36, 3, N, K, device='cuda').to(torch.bfloat16)
     out = torch.empty(4, 36, M, N, device='cuda')
     fl = 2.0 * 36 * M * N * K
-    r = dict(name=name, M=M, N=N, K=K)
+    r = dict(name=name, M=M, N=N, K=K, shared=SHARED, dbg=os.environ.get('RAFIKI_X6P_DBG', '0'))
     times = {}
     cfgs = [(t + kt, n, sp) for (t, n, sp) in S._XP_CFGS for kt in (0, 16) if not (kt and K % 64)]
     if os.environ.get('X6P_CFGS'):   # e.g. "3,2,1;16,3,1" (timing-diagnostic runs: RAFIKI_X6P_DBG)
@@ -49,8 +62,7 @@ for name, M, N, K in SHAPES:
     for (tile, nst, sp) in cfgs:
         sp = S.x6p_splits(K, sp)
         try:
-            times[(tile, nst, sp)] = t(lambda: S.x6p_gemm(a, b, out[:sp], M, N, K, groups=36, tile=tile, nst=nst,
-                                                          splits=sp))
+            times[(tile, nst, sp)] = t(lambda: gemm(a, b, out[:sp], M, N, K, tile, nst, sp))
         except Exception:  # noqa: BLE001
             times[(tile, nst, sp)] = float('inf')
     best = min(times, key=times.get)

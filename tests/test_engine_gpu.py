@@ -121,6 +121,24 @@ def test_scheduled_graph_matches_eager_and_advances_counter(opt):
     assert abs(e1.loss_sum.item() - e2.loss_sum.item()) < 1e-3 * max(1.0, abs(e1.loss_sum.item()))
 
 
+def test_scheduled_graph_with_a_one_step_schedule():
+    """A dataset smaller than two batches gives a one-row schedule; the capture's warm-up steps (and any
+    replay past the schedule) must wrap around it, never read past the schedule or the dataset."""
+    e1, e2 = _engine(lr=0.05), _engine(lr=0.05)
+    data, labels = _batch(40, seed=3)
+    B = 32
+    e2.capture_scheduled(data, labels, 1, B)
+    g = torch.Generator('cuda').manual_seed(2)
+    for ep in range(3):
+        idx = torch.randperm(40, device='cuda', generator=g)[:B].view(1, B)
+        e2.set_schedule(idx)
+        e1.train_step(data[idx[0]].contiguous(), labels[idx[0]].contiguous())
+        e2.replay()
+    torch.cuda.synchronize()
+    assert int(e2._ctr.item()) == 1
+    assert torch.allclose(e1.flat.master, e2.flat.master, rtol=1e-5, atol=1e-6)
+
+
 def test_training_reduces_loss_and_eval():
     eng = _engine(lr=0.05)
     x, y = _batch(128, seed=5)
