@@ -95,22 +95,32 @@ __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ 
                                                       float* __restrict__ dw, float* __restrict__ db,
                                                       float* __restrict__ dbh) {
   __shared__ float red[8][NC + 1][32];
+  __shared__ float dbr[8][NC];
   const int kk = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int k = blockIdx.x * 32 + kk;
-  float acc[NC];
+  const bool dbl = blockIdx.x == 0 && kk == 0 && db;   // block 0 also sums dlogits' columns (the bias gradient)
+  float acc[NC], dba[NC];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+  for (int c = 0; c < NC; ++c) acc[c] = dba[c] = 0.f;
   float hs = 0.f;
   for (int b = rg; b < B; b += 8) {
     const float zv = z[(long long)b * D + k];
     const float* gr = dlogits + (long long)b * NC;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) acc[c] += gr[c] * zv;
+    for (int c = 0; c < NC; ++c) {
+      const float g = gr[c];
+      acc[c] += g * zv;
+      dba[c] += g;
+    }
     if (dbh) hs += dz[(long long)b * D + k];
   }
 #pragma unroll
   for (int c = 0; c < NC; ++c) red[rg][c][kk] = acc[c];
   red[rg][NC][kk] = hs;
+  if (dbl) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dbr[rg][c] = dba[c];
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < (NC + 1) * 32; i += 256) {
     const int c = i >> 5, col = i & 31;
@@ -121,12 +131,11 @@ __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ 
     if (c < NC) dw[(long long)c * D + kc] = s;
     else if (dbh) dbh[kc] = s;
   }
-  if (blockIdx.x == 0 && db) {   // the output bias gradient: column sums of dlogits (one thread per class)
-    if (threadIdx.x < NC) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += dlogits[(long long)b * NC + threadIdx.x];
-      db[threadIdx.x] = s;
-    }
+  if (blockIdx.x == 0 && db && threadIdx.x < NC) {   // 8 row-group partials of the bias gradient, in order
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s += dbr[r][threadIdx.x];
+    db[threadIdx.x] = s;
   }
 }
 
