@@ -257,6 +257,168 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
   }
 }
 
+// Warp-specialised variant: 2 x 2 compute waves (wave tile 32 MI x 32 NI) that only read fragments and
+// issue MFMAs, plus 4 loader waves that only issue the LDS-DMA pieces.  An LDS-DMA wave-instruction costs
+// its issuing wave ~60-185 cycles; issued by the compute waves (x6p_gemm_kernel) those cycles come out of
+// the MFMA stream (every tile shape measured at 25-30 % of the X6 peak).  Here a loader wave on each SIMD
+// issues while the compute wave beside it keeps the matrix core busy.  Per K-tile: loaders wait for
+// their pieces of tile kt, one workgroup barrier (tile kt landed; every compute wave is done with tile
+// kt-1), then the loaders issue tile kt+NST-1 into the freed stage while the compute waves consume kt.
+template <int MI, int NI, int NST, int KT>
+__global__ __launch_bounds__(512) void x6p_ws_kernel(const XpParams p) {
+  constexpr int BM = 64 * MI, BN = 64 * NI;
+  constexpr int ABYTES = 3 * BM * 2 * KT, SB = 3 * (BM + BN) * 2 * KT;
+  using OA = XOp<BM, 4, KT>;
+  using OB = XOp<BN, 4, KT>;
+  constexpr int L = OA::NQ + OB::NQ;   // DMA pieces per loader wave per K-tile
+  static_assert(L <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[NST * SB];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool loader = wv >= 4;
+  const int wid = loader ? wv - 4 : wv;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tilesN = (p.N + BN - 1) / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * tilesN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int gs = lin / tiles, bid = lin - gs * tiles;
+  const int grp = gs / p.splits, split = gs - grp * p.splits;
+  const int mt = bid / tilesN, nt = bid - mt * tilesN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kt0 = split * p.ktPer;
+  const int nk = min(p.K / KT - kt0, p.ktPer);
+
+  if (loader) {
+    OA A;
+    OB B;
+    const unsigned long long ka = 2ull * (unsigned long long)kt0 * KT;
+    A.init(p.A + grp * p.gsA + kt0 * KT, p.bytesA - 2ull * (unsigned long long)(grp * p.gsA) - ka, p.lda, p.psA, m0,
+           p.M, wid, lane);
+    B.init(p.B + grp * p.gsB + kt0 * KT, p.bytesB - 2ull * (unsigned long long)(grp * p.gsB) - ka, p.ldb, p.psB, n0,
+           p.N, wid, lane);
+#pragma unroll
+    for (int s = 0; s < NST - 1; ++s) {
+      if (s < nk) {
+        A.issue(smem + s * SB, s, wid, true);
+        B.issue(smem + s * SB + ABYTES, s, wid, true);
+      }
+    }
+    int st = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if constexpr (NST == 3) {
+        if (kt + 1 < nk) s_wait_vmcnt<L>();
+        else s_wait_vmcnt<0>();
+      } else {
+        s_wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + NST - 1 < nk) {
+        char* nxt = smem + (st == 0 ? NST - 1 : st - 1) * SB;
+        A.issue(nxt, kt + NST - 1, wid, true);
+        B.issue(nxt + ABYTES, kt + NST - 1, wid, true);
+      }
+      st = st + 1 == NST ? 0 : st + 1;
+    }
+    return;
+  }
+
+  OA A;   // fragment addressing only (the compute waves issue no DMA)
+  OB B;
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  constexpr int NC = KT / 16;
+  constexpr int NM = 6 * MI * NI;
+  constexpr int NR = 3 * (MI + NI);
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    s_barrier_lds();   // tile kt is in LDS; every compute wave is done reading tile kt-1
+    const char* As = smem + st * SB;
+    const char* Bs = As + ABYTES;
+    bf16x8 fa[2][3][MI], fb[2][3][NI];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[0][pl][i] = A.frag(As, pl, wm * 32 * MI + i * 32, 0, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[0][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, 0, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<NC>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      constexpr int cur = c & 1, nx = cur ^ 1;
+      if constexpr (c + 1 < NC) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) fa[nx][pl][i] = A.frag(As, pl, wm * 32 * MI + i * 32, c + 1, lane);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) fb[nx][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, c + 1, lane);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = mfma6(fa[cur][0][i], fa[cur][1][i], fa[cur][2][i], fb[cur][0][j], fb[cur][1][j], fb[cur][2][j],
+                            acc[i][j]);
+      xp_sched<NM, (c + 1 < NC ? NR : 0), 0>();
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    st = st + 1 == NST ? 0 : st + 1;
+  }
+
+  float* C = p.C + grp * p.gsC + split * p.slabStride;
+  const int h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = n0 + wn * 32 * NI + j * 32 + (lane & 31);
+    if (n >= p.N) continue;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 * MI + i * 32 + acc_row(r, h);
+        if (m >= p.M) continue;
+        float* c = C + (long long)m * p.ldc + n;
+        *c = (p.flags & 1) ? *c + acc[i][j][r] : acc[i][j][r];
+      }
+    }
+  }
+}
+
+template <int MI, int NI, int KT>
+int ws_launch(const XpParams& p, int nst, hipStream_t st) {
+  constexpr int BM = 64 * MI, BN = 64 * NI;
+  constexpr int SB = 3 * (BM + BN) * 2 * KT;
+  const long long blocks = (long long)rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN) * p.groups * p.splits;
+  if (blocks >= (1ll << 31)) return RK_EUNSUPPORTED;
+  const dim3 grid((unsigned)blocks), block(512);
+  if (nst == 3) {
+    if constexpr (3 * SB <= 163840)
+      hipLaunchKernelGGL((x6p_ws_kernel<MI, NI, 3, KT>), grid, block, 0, st, p);
+    else
+      return RK_EUNSUPPORTED;
+  } else {
+    if constexpr (2 * SB <= 163840)
+      hipLaunchKernelGGL((x6p_ws_kernel<MI, NI, 2, KT>), grid, block, 0, st, p);
+    else
+      return RK_EUNSUPPORTED;
+  }
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+template <int MI, int NI>
+int ws_launch_kt(const XpParams& p, int nst, int kt, hipStream_t st) {
+  return kt == 64 ? ws_launch<MI, NI, 64>(p, nst, st) : ws_launch<MI, NI, 32>(p, nst, st);
+}
+
 template <int WGM, int WGN, int MI, int NI, int KT, bool DBG = false>
 int xp_launch(const XpParams& p, int nst, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
@@ -302,15 +464,16 @@ __global__ __launch_bounds__(256) void x6p_split_kernel(const float* __restrict_
 
 // C[g] (+)= A[g] · B[g]^T for g < groups, A[g] planes [3][M][lda] (plane stride psA), B[g] planes
 // [3][N][ldb]; fp32 C[g] [M][ldc].  tile: 0 128x128 (2x2 waves), 1 128x64, 2 64x128, 3 64x64 (2x2 waves),
-// 4 64x64 (1 wave), 5 128x64 (2x1), 6 64x128 (1x2), 7 256x128 (4x2), 8 128x256 (2x4); nst: LDS ring stages
+// 4 64x64 (1 wave), 5 128x64 (2x1), 6 64x128 (1x2), 7 256x128 (4x2), 8 128x256 (2x4), 9-12 the
+// warp-specialised 128x128, 128x64, 64x128, 64x64 (2x2 compute + 4 loader waves); nst: LDS ring stages
 // (2, 3 where the LDS fits); tile + 16: 64-deep K-tiles (K % 64 == 0); flags 1: accumulate.  splits > 1: split-K, slab s of the output at
 // C + s * slabStride (raw partial sums; the consumers add the slabs).
 extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, float* C, int M, int N, int K, int lda,
                            int ldb, int ldc, long long psA, long long psB, long long gsA, long long gsB, long long gsC,
                            int groups, int flags, int splits, long long slabStride, long long bytesA, long long bytesB,
                            void* stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || groups <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 8 ||
-      tile > 24 || splits <= 0)
+  if (M <= 0 || N <= 0 || K <= 0 || groups <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 12 ||
+      tile > 28 || splits <= 0)
     return RK_EBADARG;
   if (splits > 1 && ((flags & 1) || slabStride < (long long)groups * gsC || slabStride < (long long)M * ldc))
     return RK_EBADARG;   // split-K writes raw partial slabs
@@ -351,6 +514,11 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
     // 8-wave tiles of 64x64 wave tiles (two waves per SIMD): NST 2 only (73.7 KiB per stage)
     case 7: return xp_launch_kt<4, 2, 2, 2>(p, nst, kt, st);
     case 8: return xp_launch_kt<2, 4, 2, 2>(p, nst, kt, st);
+    // warp-specialised (4 compute + 4 loader waves): 9 128x128, 10 128x64, 11 64x128, 12 64x64
+    case 9: return ws_launch_kt<2, 2>(p, nst, kt, st);
+    case 10: return ws_launch_kt<2, 1>(p, nst, kt, st);
+    case 11: return ws_launch_kt<1, 2>(p, nst, kt, st);
+    case 12: return ws_launch_kt<1, 1>(p, nst, kt, st);
   }
   return RK_EBADARG;
 }

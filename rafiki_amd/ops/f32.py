@@ -744,13 +744,15 @@ def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accu
 # transforms) instead of after every LDS read inside the K loop: the pre-transformed F(4x4) paths on
 # planes are autotune candidates next to their fp32-operand sgemm forms.  RAFIKI_X6P=0 turns them off.
 USE_X6P = USE_X6 and os.environ.get('RAFIKI_X6P', '1') != '0'
-XP_TILES = ((128, 128), (128, 64), (64, 128), (64, 64), (64, 64), (128, 64), (64, 128), (256, 128), (128, 256))
-XP_NST3 = (0, 1, 2, 3, 4, 5, 6)          # tiles 7-8 (8 waves, 72 KiB per stage) ring 2 stages only
+# tiles 9-12: warp-specialised (2x2 compute waves + 4 loader waves that alone issue the LDS-DMA pieces)
+XP_TILES = ((128, 128), (128, 64), (64, 128), (64, 64), (64, 64), (128, 64), (64, 128), (256, 128), (128, 256),
+            (128, 128), (128, 64), (64, 128), (64, 64))
+XP_NST3 = (0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12)   # tiles 7-8 (8 waves, 72 KiB per stage) ring 2 stages only
 # (tile, nst, splits) of the x6p GEMM: every tile x ring depth unsplit; the big tiles also with 2 / 4 K-splits
 # (the 4x4-map GEMMs have T = 256 rows: 288 blocks of 128x128 for 256 CUs; the slabs are summed by the
 # output transforms that read Y' / dU anyway)
 _XP_CFGS = tuple((t, n, 1) for t in range(len(XP_TILES)) for n in ((2, 3) if t in XP_NST3 else (2,))) + \
-    tuple((t, 2, s) for t in (0, 1, 2, 7, 8) for s in (2, 4))
+    tuple((t, 2, s) for t in (0, 1, 2, 7, 8) for s in (2, 4)) + tuple((t, 3, s) for t in (9, 10, 11) for s in (2, 4))
 WINO4_PTX = -15         # conv / data gradient: cfg = (-15, x6p code, splits), code = tile * 4 + nst
 WINO4_WGRAD_PTX = -16   # weight gradient: likewise
 WINO4_PTX_CFGS = tuple((WINO4_PTX, 4 * t + n, s) for t, n, s in _XP_CFGS) if USE_X6P else ()

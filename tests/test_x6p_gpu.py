@@ -37,7 +37,7 @@ def test_split_planes_sum_back_exactly():
 
 @pytest.mark.parametrize("G,M,N,K", [(1, 256, 256, 256), (3, 100, 72, 64), (4, 256, 512, 512), (2, 33, 130, 96),
                                      (5, 1, 64, 32)])
-@pytest.mark.parametrize("tile", range(9))
+@pytest.mark.parametrize("tile", range(13))
 @pytest.mark.parametrize("nst", [2, 3])
 def test_x6p_gemm_vs_fp64(G, M, N, K, tile, nst):
     from rafiki_amd.ops import f32 as S
@@ -59,7 +59,7 @@ def test_x6p_gemm_vs_fp64(G, M, N, K, tile, nst):
 
 
 @pytest.mark.parametrize("splits", [2, 3, 4])
-@pytest.mark.parametrize("tile", [0, 3, 7])
+@pytest.mark.parametrize("tile", [0, 3, 7, 9, 12])
 def test_x6p_gemm_split_k_slabs(splits, tile):
     from rafiki_amd.ops import f32 as S
     G, M, N, K = 3, 96, 160, 224
@@ -109,7 +109,7 @@ def test_weight_planes_match_fp32_sets():
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(8, 4, 4, 512, 512), (3, 8, 8, 256, 96), (16, 8, 8, 64, 128),
                                             (2, 16, 16, 32, 64), (1, 4, 4, 64, 64)])
-@pytest.mark.parametrize("tile,splits", [(0, 1), (3, 1), (4, 1), (0, 2), (7, 4)])
+@pytest.mark.parametrize("tile,splits", [(0, 1), (3, 1), (4, 1), (0, 2), (7, 4), (9, 1), (10, 2)])
 def test_wino4_conv_pt_planes_fwd_stats_bias_relu(N, H, W, Cin, Cout, tile, splits):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=50)
@@ -118,7 +118,7 @@ def test_wino4_conv_pt_planes_fwd_stats_bias_relu(N, H, W, Cin, Cout, tile, spli
     acc = torch.zeros((S.bn_slots(Cout), 2, Cout), dtype=torch.float64, device=DEV)
     y = S.wino4_conv_pt(x.to(DEV), up, stats=acc, tile=tile, nst=2, splits=splits)
     b = _rand(Cout, seed=52)
-    yb = S.wino4_conv_pt(x.to(DEV), up, bias=b.to(DEV), relu=True, tile=tile, nst=2 if tile > 6 else 3,
+    yb = S.wino4_conv_pt(x.to(DEV), up, bias=b.to(DEV), relu=True, tile=tile, nst=3 if tile in S.XP_NST3 else 2,
                          splits=splits)
     torch.cuda.synchronize()
     ref = TF.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
@@ -156,7 +156,7 @@ def test_wino4_conv_pt_planes_bn_epilogues(pool, H):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(16, 8, 8, 64, 128), (32, 4, 4, 256, 128), (8, 16, 16, 32, 64),
                                             (64, 4, 4, 40, 36)])
-@pytest.mark.parametrize("tile,splits", [(0, 1), (3, 1), (5, 1), (8, 2), (0, 4)])
+@pytest.mark.parametrize("tile,splits", [(0, 1), (3, 1), (5, 1), (8, 2), (0, 4), (11, 1), (9, 4)])
 def test_wino4_wgrad_pt_planes(N, H, W, Cin, Cout, tile, splits):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=40)
@@ -165,7 +165,7 @@ def test_wino4_wgrad_pt_planes(N, H, W, Cin, Cout, tile, splits):
     S.wino4_wgrad_pt(dy.to(DEV), x.to(DEV), dw, tile=tile, nst=2, planes=True, splits=splits)
     prev = _rand(Cout, 9 * Cin, seed=42).to(DEV)
     acc = prev.clone()
-    S.wino4_wgrad_pt(dy.to(DEV), x.to(DEV), acc, accumulate=True, tile=tile, nst=2 if tile > 6 else 3, planes=True,
+    S.wino4_wgrad_pt(dy.to(DEV), x.to(DEV), acc, accumulate=True, tile=tile, nst=3 if tile in S.XP_NST3 else 2, planes=True,
                      splits=splits)
     torch.cuda.synchronize()
     wd = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
