@@ -330,7 +330,12 @@ def test_per_model_path_is_thread_safe_on_one_replica(ensemble, monkeypatch):
         t.join(timeout=120)
     assert not errs, errs
     assert p.replicas[0].graphs is None
-    assert np.allclose(np.concatenate(out), ref, atol=1e-5)
+    got = np.concatenate(out)
+    # every row is its own query's answer (a mixed-up batch is off by ~1e-1, not by rounding) ...
+    d = np.abs(got[:, None, :] - ref[None, :, :]).max(-1)
+    assert (d.argmin(1) == np.arange(len(ref))).all()
+    # ... and the per-model kernels agree with the grouped one-graph network to fp32 rounding
+    assert np.abs(got - ref).max() < 1e-4, np.abs(got - ref).max()
 
 
 def test_pipelined_batcher_matches_direct_path(ensemble):
