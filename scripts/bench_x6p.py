@@ -18,6 +18,11 @@ PEAK = 2.5e15 / 6
 
 
 def t(fn, reps=20):
+    if os.environ.get('X6P_EAGER') == '1':   # plain launches (profiler counter passes)
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return 1.0
     fn()
     torch.cuda.synchronize()
     s = torch.cuda.Event(enable_timing=True)
@@ -49,6 +54,8 @@ def gemm(a, b, out, M, N, K, tile, nst, sp):
               0, 0, M * N, 36, 0, sp, 36 * M * N, a.numel() * 2, b.numel() * 2, torch.cuda.current_stream().cuda_stream)
 
 
+if os.environ.get('X6P_SHAPES'):
+    SHAPES = [x for x in SHAPES if x[0] in os.environ['X6P_SHAPES'].split(',')]
 for name, M, N, K in SHAPES:
     a = torch.randn(1 if SHARED else 36, 3, M, K, device='cuda').to(torch.bfloat16)
     b = torch.randn(1 if SHARED else 36, 3, N, K, device='cuda').to(torch.bfloat16)

@@ -251,10 +251,11 @@ def test_one_graph_ensemble_matches_per_model_path(ensemble, monkeypatch):
         ref = ref_p.predict_array(imgs)
         monkeypatch.setenv('RAFIKI_ENSEMBLE_GRAPH', '1')
         got = p.predict_array(imgs)
-        assert got.shape == (n, 10) and np.allclose(got, ref, atol=1e-5), n
+        # two kernel sets (grouped one-graph network vs per-model engines): fp32 rounding through 10 layers
+        assert got.shape == (n, 10) and np.abs(got - ref).max() < 5e-5, (n, np.abs(got - ref).max())
         sig = models[0][1].input_signature()
         dev = p.predict_proba_device({sig: torch.from_numpy(imgs).to(DEV)})
-        assert np.allclose(dev.cpu().numpy(), ref, atol=1e-5), n
+        assert np.abs(dev.cpu().numpy() - ref).max() < 5e-5, n
     g = p.replicas[0].graphs
     assert g is not None and g.replays >= 8 and ref_p.replicas[0].graphs is None
     assert {b for b, _ in g._graphs} >= {1, 8, 64, 512}
@@ -335,7 +336,7 @@ def test_per_model_path_is_thread_safe_on_one_replica(ensemble, monkeypatch):
     d = np.abs(got[:, None, :] - ref[None, :, :]).max(-1)
     assert (d.argmin(1) == np.arange(len(ref))).all()
     # ... and the per-model kernels agree with the grouped one-graph network to fp32 rounding
-    assert np.abs(got - ref).max() < 1e-4, np.abs(got - ref).max()
+    assert np.abs(got - ref).max() < 5e-5, np.abs(got - ref).max()
 
 
 def test_pipelined_batcher_matches_direct_path(ensemble):
