@@ -40,7 +40,8 @@ struct XpParams {
   int groups, flags;            // flags: 1 = accumulate into C
   int splits, ktPer;            // split-K: split s covers K-tiles [s ktPer, (s+1) ktPer), writes slab s
   long long slabStride;         // elements between split-K slabs of C
-  int dbg;                      // DBG builds: 1 no DMA in the K loop, 2 no MFMAs
+  int dbg;                      // DBG builds: 1 no DMA in the K loop, 2 no MFMAs, 4 per-block phase stamps
+  unsigned long long* stamps;   // DBG & 4: per block [start, first tile landed, K loop done, stored, realtime x2]
   unsigned long long bytesA, bytesB;
 };
 
@@ -119,7 +120,9 @@ RK_DEV void xp_sched() {
   }
 }
 
-// DBG: timing-diagnostic build (RAFIKI_X6P_DBG, tiles 0 and 3): p.dbg 1 = no DMA in the K loop, 2 = no MFMAs
+// DBG: timing-diagnostic build (RAFIKI_X6P_DBG, tiles 0 and 3): p.dbg 1 = no DMA in the K loop, 2 = no MFMAs,
+// 4 = per-block phase stamps (s_memtime shader clocks + s_memrealtime at 100 MHz; lane 0 of wave 0 stores them
+// with vector stores)
 template <int WGM, int WGN, int MI, int NI, int NST, int KT, bool DBG = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams p) {
   constexpr int NW = WGM * WGN;
@@ -128,6 +131,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
   constexpr int L = XOp<BM, NW, KT>::NQ + XOp<BN, NW, KT>::NQ;   // DMA wave-instructions per wave per K-tile
   __shared__ __attribute__((aligned(16))) char smem[NST * SB];
   const int tid = threadIdx.x, lane = tid & 63;
+  const bool stamp = DBG && (p.dbg & 4) && tid == 0;
+  unsigned long long t0 = 0, r0 = 0, t1 = 0, t2 = 0;
+  if (stamp) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid - (wid / WGN) * WGN;
   const int tilesN = (p.N + BN - 1) / BN;
@@ -180,6 +189,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
       s_wait_vmcnt<0>();
     }
     s_barrier_lds();   // every wave's DMA for tile kt is in LDS; every wave is done with tile kt-1
+    if (stamp && kt == 0) t1 = __builtin_amdgcn_s_memtime();
     const char* As = smem + st * SB;
     const char* Bs = As + ABYTES;
     const bool more = kt + NST - 1 < nk;
@@ -236,6 +246,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
     st = st + 1 == NST ? 0 : st + 1;
   }
   s_wait_vmcnt<0>();   // the trailing zero-DMAs land before the workgroup's LDS is released
+  if (stamp) t2 = __builtin_amdgcn_s_memtime();
 
   // epilogue: register r of block (i, j) is row acc_row(r, h), column lane & 31 — 2 x 128-B row stores
   float* C = p.C + grp * p.gsC + split * p.slabStride;
@@ -254,6 +265,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
         *c = (p.flags & 1) ? *c + acc[i][j][r] : acc[i][j][r];
       }
     }
+  }
+  if (stamp) {
+    __builtin_amdgcn_s_waitcnt(0);   // the block's stores issued (their issue cost is what is timed)
+    unsigned long long* o = p.stamps + (long long)blockIdx.x * 8;
+    o[0] = t0;
+    o[1] = t1;
+    o[2] = t2;
+    o[3] = __builtin_amdgcn_s_memtime();
+    o[4] = r0;
+    o[5] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -460,6 +481,9 @@ __global__ __launch_bounds__(256) void x6p_split_kernel(const float* __restrict_
   dst[o + 2 * ps] = l;
 }
 
+unsigned long long* g_stamps = nullptr;
+long long g_stamp_n = 0;
+
 }  // namespace
 
 // C[g] (+)= A[g] · B[g]^T for g < groups, A[g] planes [3][M][lda] (plane stride psA), B[g] planes
@@ -499,6 +523,16 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   p.slabStride = splits > 1 ? slabStride : 0;
   static const int dbg = getenv("RAFIKI_X6P_DBG") ? atoi(getenv("RAFIKI_X6P_DBG")) : 0;
   p.dbg = dbg;
+  p.stamps = nullptr;
+  if (dbg & 4) {
+    const long long need = (long long)rk_cdiv(M, 128) * rk_cdiv(N, 64) * 4 * groups * splits * 8;   // >= blocks*8 for 64x64
+    if (need > g_stamp_n) {
+      if (g_stamps) (void)hipFree(g_stamps);
+      if (hipMalloc((void**)&g_stamps, need * 8) != hipSuccess) return RK_ELAUNCH;
+      g_stamp_n = need;
+    }
+    p.stamps = g_stamps;
+  }
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   const hipStream_t st = (hipStream_t)stream;
   if (dbg && kt == 32 && (tile == 0 || tile == 3))
@@ -521,6 +555,12 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
     case 12: return ws_launch_kt<1, 1>(p, nst, kt, st);
   }
   return RK_EBADARG;
+}
+
+// DBG & 4: the per-block stamps of the last diagnostic launch (8 x u64 per block) -> host
+extern "C" int rk_x6p_stamps(void* host, long long n) {
+  if (!g_stamps || n > g_stamp_n) return RK_EBADARG;
+  return hipMemcpy(host, g_stamps, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? RK_OK : RK_ELAUNCH;
 }
 
 // planes [3][rows][ldd] (plane stride ps) of an fp32 [rows][lds] matrix

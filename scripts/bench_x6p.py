@@ -47,6 +47,26 @@ res = []
 SHARED = os.environ.get('X6P_SHARED') == '1'
 
 
+def phases(tile, M, N, sp):
+    """Per-block phase stamps of the last launch (RAFIKI_X6P_DBG & 4): median shader-clock cycles of the
+    prologue (start -> first K-tile landed), the K loop and the epilogue, the clock (MHz) and the block
+    start spread (how many rounds of blocks the grid ran in)."""
+    import numpy as np
+    bm, bn = S.XP_TILES[tile & 15]
+    nb = -(-M // bm) * -(-N // bn) * 36 * sp
+    h = np.zeros(nb * 8, dtype=np.uint64)
+    torch.cuda.synchronize()
+    _lib.call("rk_x6p_stamps", h.ctypes.data, nb * 8)
+    h = h.reshape(nb, 8).astype(np.float64)
+    pro, loop, epi = h[:, 1] - h[:, 0], h[:, 2] - h[:, 1], h[:, 3] - h[:, 2]
+    mhz = (h[:, 3] - h[:, 0]) / np.maximum(1.0, h[:, 5] - h[:, 4]) * 100.0
+    life = h[:, 3] - h[:, 0]
+    span = h[:, 3].max() - h[:, 0].min()
+    return {'blocks': nb, 'prologue': float(np.median(pro)), 'loop': float(np.median(loop)),
+            'epilogue': float(np.median(epi)), 'life': float(np.median(life)), 'mhz': float(np.median(mhz)),
+            'span_cycles': float(span), 'concurrency': float(life.sum() / max(1.0, span))}
+
+
 def gemm(a, b, out, M, N, K, tile, nst, sp):
     if not SHARED:
         return S.x6p_gemm(a, b, out, M, N, K, groups=36, tile=tile, nst=nst, splits=sp)
@@ -70,6 +90,8 @@ for name, M, N, K in SHAPES:
         sp = S.x6p_splits(K, sp)
         try:
             times[(tile, nst, sp)] = t(lambda: gemm(a, b, out[:sp], M, N, K, tile, nst, sp))
+            if int(os.environ.get('RAFIKI_X6P_DBG', '0')) & 4 and tile & 15 in (0, 3):
+                r.setdefault('phases', {})['{},{},{}'.format(tile, nst, sp)] = phases(tile, M, N, sp)
         except Exception:  # noqa: BLE001
             times[(tile, nst, sp)] = float('inf')
     best = min(times, key=times.get)
