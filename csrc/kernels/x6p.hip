@@ -463,10 +463,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_pers_kernel(const XpParams
   const int tilesN = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tilesN;
   const int total = tiles * p.groups * p.splits;
-  // this block's items: the XCD's contiguous share [lo, hi), strided by the XCD's block count
+  // this block's items: the XCD's contiguous share [lo, hi) (in proportion to the blocks it holds: block b runs
+  // on XCD b % 8), strided by the XCD's block count
   const int xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
-  const int bpx = ((int)gridDim.x - xcd + 7) >> 3;
-  const int lo = (int)((long long)total * xcd / 8), hi = (int)((long long)total * (xcd + 1) / 8);
+  const int gq = (int)gridDim.x >> 3, gr = (int)gridDim.x & 7;
+  const int bpx = gq + (xcd < gr ? 1 : 0);
+  const int before = xcd * gq + min(xcd, gr), upto = before + bpx;   // blocks on XCDs < xcd, <= xcd
+  const int lo = (int)((long long)total * before / gridDim.x), hi = (int)((long long)total * upto / gridDim.x);
   const int nk = p.ktPer;
   int wi = lo + kx;   // the item whose K-tiles the DMA cursor issues
   if (wi >= hi) return;

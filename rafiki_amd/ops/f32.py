@@ -1203,7 +1203,8 @@ def bn_bwd(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, 
     if not reduced:
         if C <= 1024 and not (C & (C - 1)):
             npix = dout.numel() // C
-            blocks = max(1, min(_BWD_BLOCKS, cdiv(npix, max(1, 256 // (C // 4)) * 8)))
+            # ~2 passes of 256 / (C / 4) pixel rows per block: enough blocks to fill the chip on small maps
+            blocks = max(1, min(_BWD_BLOCKS, cdiv(npix, max(1, 256 // (C // 4)) * 2)))
             _lib.call("rk_bnf_bwd_reduce", _p(dout), _p(y), _p(coeffs), _p(acc), acc.shape[0], blocks, Nb, H, W, C,
                       int(pool), int(act), float(slope), s)
         elif not pool and act == ACT_NONE:
