@@ -121,6 +121,32 @@ RK_DEV void xp_sched() {
   }
 }
 
+// Epilogue of one wave tile: register r of 32x32 block (i, j) is row acc_row(r, h), column lane & 31.  Buffer
+// stores with one VGPR offset per store (no 64-bit address math or per-element branches): rows >= M fall past
+// the group slab's range and are dropped by the buffer range check; columns >= N get an out-of-range offset.
+template <int MI, int NI>
+RK_DEV void xp_store(const XpParams& p, f32x16 (&acc)[MI][NI], int grp, int split, int mw, int nw, int lane) {
+  float* C = p.C + grp * p.gsC + split * p.slabStride;
+  const __amdgpu_buffer_rsrc_t rs = s_rsrc(C, (unsigned long long)p.M * p.ldc * 4);
+  const int h = lane >> 5;
+  const bool acc_in = p.flags & 1;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = nw + j * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const unsigned base = n < p.N ? (unsigned)(((mw + i * 32 + 4 * h) * p.ldc + n) * 4) : SOOB;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned o = base + (unsigned)(((r & 3) + 8 * (r >> 2)) * p.ldc * 4);
+        float v = acc[i][j][r];
+        if (acc_in) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)o, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, (int)o, 0, 0);
+      }
+    }
+  }
+}
+
 // DBG: timing-diagnostic build (RAFIKI_X6P_DBG, tiles 0 and 3): p.dbg 1 = no DMA in the K loop, 2 = no MFMAs,
 // 4 = per-block phase stamps (s_memtime shader clocks + s_memrealtime at 100 MHz; lane 0 of wave 0 stores them
 // with vector stores)
@@ -249,24 +275,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
   s_wait_vmcnt<0>();   // the trailing zero-DMAs land before the workgroup's LDS is released
   if (stamp) t2 = __builtin_amdgcn_s_memtime();
 
-  // epilogue: register r of block (i, j) is row acc_row(r, h), column lane & 31 — 2 x 128-B row stores
-  float* C = p.C + grp * p.gsC + split * p.slabStride;
-  const int h = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int n = n0 + wn * 32 * NI + j * 32 + (lane & 31);
-    if (n >= p.N) continue;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 32 * MI + i * 32 + acc_row(r, h);
-        if (m >= p.M) continue;
-        float* c = C + (long long)m * p.ldc + n;
-        *c = (p.flags & 1) ? *c + acc[i][j][r] : acc[i][j][r];
-      }
-    }
-  }
+  xp_store<MI, NI>(p, acc, grp, split, m0 + wm * 32 * MI, n0 + wn * 32 * NI, lane);
   if (stamp) {
     __builtin_amdgcn_s_waitcnt(0);   // the block's stores issued (their issue cost is what is timed)
     unsigned long long* o = p.stamps + (long long)blockIdx.x * 8;
@@ -395,23 +404,7 @@ __global__ __launch_bounds__(512) void x6p_ws_kernel(const XpParams p) {
     st = st + 1 == NST ? 0 : st + 1;
   }
 
-  float* C = p.C + grp * p.gsC + split * p.slabStride;
-  const int h = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int n = n0 + wn * 32 * NI + j * 32 + (lane & 31);
-    if (n >= p.N) continue;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 32 * MI + i * 32 + acc_row(r, h);
-        if (m >= p.M) continue;
-        float* c = C + (long long)m * p.ldc + n;
-        *c = (p.flags & 1) ? *c + acc[i][j][r] : acc[i][j][r];
-      }
-    }
-  }
+  xp_store<MI, NI>(p, acc, grp, split, m0 + wm * 32 * MI, n0 + wn * 32 * NI, lane);
 }
 
 template <int MI, int NI, int KT>
@@ -581,25 +574,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_pers_kernel(const XpParams
     if (++ktc == nk) {   // item wc done: store it while the next item's first K-tiles land
       int grp, split, m0, n0;
       coords(wc, grp, split, m0, n0);
-      float* C = p.C + grp * p.gsC + split * p.slabStride;
-      const int h = lane >> 5;
-      const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
+      xp_store<MI, NI>(p, acc, grp, split, m0 + wm * 32 * MI, n0 + wn * 32 * NI, lane);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int n = n0 + wn * 32 * NI + j * 32 + (lane & 31);
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {
+        for (int j = 0; j < NI; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = m0 + wm * 32 * MI + i * 32 + acc_row(r, h);
-            if (full || (m < p.M && n < p.N)) {
-              float* c = C + (long long)m * p.ldc + n;
-              *c = (p.flags & 1) ? *c + acc[i][j][r] : acc[i][j][r];
-            }
-            acc[i][j][r] = 0.f;
-          }
-        }
-      }
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
       ktc = 0;
       wc += bpx;
     }
@@ -704,6 +685,7 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   tile &= 15;
   if (K % kt || lda % 8 || ldb % 8 || lda < K || ldb < K) return RK_EUNSUPPORTED;
   if (psA < (long long)M * lda || psB < (long long)N * ldb || bytesA <= 0 || bytesB <= 0) return RK_EBADARG;
+  if ((long long)M * ldc * 4 >= (1ll << 31) || ldc < N) return RK_EUNSUPPORTED;   // 32-bit epilogue offsets
   // every in-group byte offset must stay below the 2 GiB buffer range
   if ((2 * psA + (long long)M * lda) * 2 >= (1ll << 31) || (2 * psB + (long long)N * ldb) * 2 >= (1ll << 31))
     return RK_EUNSUPPORTED;
