@@ -21,7 +21,6 @@
 //     XCD-aware remap (a group's tiles share their A / B panels in one XCD's L2).
 #include "common.h"
 #include <cstdlib>
-#include <algorithm>
 #include <utility>
 
 namespace {
@@ -434,189 +433,6 @@ int ws_launch_kt(const XpParams& p, int nst, int kt, hipStream_t st) {
   return kt == 64 ? ws_launch<MI, NI, 64>(p, nst, st) : ws_launch<MI, NI, 32>(p, nst, st);
 }
 
-// Persistent variant: a grid of (CUs x resident blocks) workgroups, each walking a list of output tiles
-// (the XCD's share of them, in order, so a group's tiles stay on one XCD's L2).  The LDS ring runs across
-// tile boundaries: the DMA pieces of the next tile's first K-tiles are issued during the current tile's
-// last ones, and the current tile's epilogue runs while they land.  A short-K grid GEMM (the pre-transformed
-// Winograd GEMMs have K = 128..1024: 4..32 K-tiles) otherwise pays a cold prologue and an idle epilogue per
-// tile.  Requires K / KT == splits * ktPer (equal K ranges per split).
-template <int WGM, int WGN, int MI, int NI, int NST, int KT>
-__global__ __launch_bounds__(64 * WGM * WGN) void x6p_pers_kernel(const XpParams p) {
-  constexpr int NW = WGM * WGN;
-  constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
-  constexpr int ABYTES = 3 * BM * 2 * KT, SB = 3 * (BM + BN) * 2 * KT;
-  using OA = XOp<BM, NW, KT>;
-  using OB = XOp<BN, NW, KT>;
-  constexpr int L = OA::NQ + OB::NQ;
-  constexpr int LA = OA::NQ;
-  __shared__ __attribute__((aligned(16))) char smem[NST * SB];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WGN, wn = wid - (wid / WGN) * WGN;
-  const int tilesN = (p.N + BN - 1) / BN;
-  const int tiles = ((p.M + BM - 1) / BM) * tilesN;
-  const int total = tiles * p.groups * p.splits;
-  // this block's items: the XCD's contiguous share [lo, hi) (in proportion to the blocks it holds: block b runs
-  // on XCD b % 8), strided by the XCD's block count
-  const int xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
-  const int gq = (int)gridDim.x >> 3, gr = (int)gridDim.x & 7;
-  const int bpx = gq + (xcd < gr ? 1 : 0);
-  const int before = xcd * gq + min(xcd, gr), upto = before + bpx;   // blocks on XCDs < xcd, <= xcd
-  const int lo = (int)((long long)total * before / gridDim.x), hi = (int)((long long)total * upto / gridDim.x);
-  const int nk = p.ktPer;
-  int wi = lo + kx;   // the item whose K-tiles the DMA cursor issues
-  if (wi >= hi) return;
-
-  auto coords = [&](int w, int& grp, int& split, int& m0, int& n0) {
-    const int gs = w / tiles, bid = w - gs * tiles;
-    grp = gs / p.splits;
-    split = gs - grp * p.splits;
-    const int mt = bid / tilesN;
-    m0 = mt * BM;
-    n0 = (bid - mt * tilesN) * BN;
-  };
-  OA A;
-  OB B;
-  auto init_ops = [&](int w) {
-    int grp, split, m0, n0;
-    coords(w, grp, split, m0, n0);
-    const int kt0 = split * p.ktPer;
-    const unsigned long long ka = 2ull * (unsigned long long)kt0 * KT;
-    A.init(p.A + grp * p.gsA + kt0 * KT, p.bytesA - 2ull * (unsigned long long)(grp * p.gsA) - ka, p.lda, p.psA, m0,
-           p.M, wid, lane);
-    B.init(p.B + grp * p.gsB + kt0 * KT, p.bytesB - 2ull * (unsigned long long)(grp * p.gsB) - ka, p.ldb, p.psB, n0,
-           p.N, wid, lane);
-  };
-  init_ops(wi);
-  int kti = 0;   // next K-tile of item wi to issue
-  // issue piece q of the cursor's K-tile into `stage`; the cursor advances after the last piece
-  auto issue_piece = [&](char* stage, int q) {
-    if (q < LA) A.issue_q(stage, kti, wid, true, q);
-    else B.issue_q(stage + ABYTES, kti, wid, true, q - LA);
-  };
-  auto advance = [&]() {
-    if (++kti == nk) {
-      kti = 0;
-      wi += bpx;
-      if (wi < hi) init_ops(wi);
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s) {
-    if (wi < hi) {
-#pragma unroll
-      for (int q = 0; q < L; ++q) issue_piece(smem + s * SB, q);
-      advance();
-    }
-  }
-
-  f32x16 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  constexpr int NC = KT / 16;
-  constexpr int NM = 6 * MI * NI;
-  constexpr int NR = 3 * (MI + NI);
-  int wc = lo + kx, ktc = 0, st = 0;
-  while (wc < hi) {
-    // the K-tile consumed now has landed once only the younger K-tiles' pieces are outstanding
-    if constexpr (NST == 3) {
-      const bool younger = ktc + 1 < nk || wc + bpx < hi;
-      if (younger) s_wait_vmcnt<L>();
-      else s_wait_vmcnt<0>();
-    } else {
-      s_wait_vmcnt<0>();
-    }
-    s_barrier_lds();
-    const char* As = smem + st * SB;
-    const char* Bs = As + ABYTES;
-    char* nxt = smem + (st == 0 ? NST - 1 : st - 1) * SB;
-    const bool live = wi < hi;   // uniform: is there a K-tile left to issue
-    bf16x8 fa[2][3][MI], fb[2][3][NI];
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) fa[0][pl][i] = A.frag(As, pl, wm * 32 * MI + i * 32, 0, lane);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) fb[0][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, 0, lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<NC>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      constexpr int cur = c & 1, nx = cur ^ 1;
-      if constexpr (c + 1 < NC) {
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-          for (int i = 0; i < MI; ++i) fa[nx][pl][i] = A.frag(As, pl, wm * 32 * MI + i * 32, c + 1, lane);
-#pragma unroll
-          for (int j = 0; j < NI; ++j) fb[nx][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, c + 1, lane);
-        }
-      }
-      if (live) {
-#pragma unroll
-        for (int q = L * c / NC; q < L * (c + 1) / NC; ++q) issue_piece(nxt, q);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = mfma6(fa[cur][0][i], fa[cur][1][i], fa[cur][2][i], fb[cur][0][j], fb[cur][1][j], fb[cur][2][j],
-                            acc[i][j]);
-      xp_sched<NM, (c + 1 < NC ? NR : 0), L * (c + 1) / NC - L * c / NC>();
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    if (live) advance();
-    st = st + 1 == NST ? 0 : st + 1;
-    if (++ktc == nk) {   // item wc done: store it while the next item's first K-tiles land
-      int grp, split, m0, n0;
-      coords(wc, grp, split, m0, n0);
-      xp_store<MI, NI>(p, acc, grp, split, m0 + wm * 32 * MI, n0 + wn * 32 * NI, lane);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-      ktc = 0;
-      wc += bpx;
-    }
-  }
-  s_wait_vmcnt<0>();
-}
-
-template <int WGM, int WGN, int MI, int NI, int KT>
-int pers_launch(const XpParams& p, int nst, hipStream_t st) {
-  constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
-  constexpr int SB = 3 * (BM + BN) * 2 * KT;
-  if ((p.K / KT) != p.splits * p.ktPer) return RK_EUNSUPPORTED;
-  const long long items = (long long)rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN) * p.groups * p.splits;
-  if (items >= (1ll << 31)) return RK_EUNSUPPORTED;
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  auto run = [&](auto kern) -> int {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * WGM * WGN, 0) != hipSuccess || occ <= 0) occ = 1;
-    const long long g = std::min<long long>(items, (long long)cus * occ);
-    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(64 * WGM * WGN), 0, st, p);
-    RK_LAUNCH_CHECK();
-    return RK_OK;
-  };
-  if (nst == 3) {
-    if constexpr (3 * SB <= 163840) return run(x6p_pers_kernel<WGM, WGN, MI, NI, 3, KT>);
-    return RK_EUNSUPPORTED;
-  }
-  if constexpr (2 * SB <= 163840) return run(x6p_pers_kernel<WGM, WGN, MI, NI, 2, KT>);
-  return RK_EUNSUPPORTED;
-}
-
 template <int WGM, int WGN, int MI, int NI, int KT, bool DBG = false>
 int xp_launch(const XpParams& p, int nst, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
@@ -667,18 +483,15 @@ long long g_stamp_n = 0;
 // [3][N][ldb]; fp32 C[g] [M][ldc].  tile: 0 128x128 (2x2 waves), 1 128x64, 2 64x128, 3 64x64 (2x2 waves),
 // 4 64x64 (1 wave), 5 128x64 (2x1), 6 64x128 (1x2), 7 256x128 (4x2), 8 128x256 (2x4), 9-12 the
 // warp-specialised 128x128, 128x64, 64x128, 64x64 (2x2 compute + 4 loader waves); nst: LDS ring stages
-// (2, 3 where the LDS fits); tile + 16: 64-deep K-tiles (K % 64 == 0); tile + 32 (tiles 0-3): persistent grid;
-// flags 1: accumulate.  splits > 1: split-K, slab s of the output at
+// (2, 3 where the LDS fits); tile + 16: 64-deep K-tiles (K % 64 == 0); flags 1: accumulate.  splits > 1: split-K, slab s of the output at
 // C + s * slabStride (raw partial sums; the consumers add the slabs).
 extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, float* C, int M, int N, int K, int lda,
                            int ldb, int ldc, long long psA, long long psB, long long gsA, long long gsB, long long gsC,
                            int groups, int flags, int splits, long long slabStride, long long bytesA, long long bytesB,
                            void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || groups <= 0 || (nst != 2 && nst != 3) || tile < 0 || (tile & 15) > 12 ||
-      tile >= 64 || splits <= 0 || ((tile & 32) && (tile & 15) > 3))
+      tile >= 32 || splits <= 0)
     return RK_EBADARG;
-  const bool pers = tile & 32;   // tile + 32: the persistent form of tiles 0-3
-  tile &= ~32;
   if (splits > 1 && ((flags & 1) || slabStride < (long long)groups * gsC || slabStride < (long long)M * ldc))
     return RK_EBADARG;   // split-K writes raw partial slabs
   const int kt = (tile >> 4) ? 64 : 32;   // tile + 16: 64-deep K-tiles (128-B plane rows)
@@ -716,14 +529,6 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   }
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   const hipStream_t st = (hipStream_t)stream;
-  if (pers) {
-    switch (tile) {
-      case 0: return kt == 64 ? pers_launch<2, 2, 2, 2, 64>(p, nst, st) : pers_launch<2, 2, 2, 2, 32>(p, nst, st);
-      case 1: return kt == 64 ? pers_launch<2, 2, 2, 1, 64>(p, nst, st) : pers_launch<2, 2, 2, 1, 32>(p, nst, st);
-      case 2: return kt == 64 ? pers_launch<2, 2, 1, 2, 64>(p, nst, st) : pers_launch<2, 2, 1, 2, 32>(p, nst, st);
-      case 3: return kt == 64 ? pers_launch<2, 2, 1, 1, 64>(p, nst, st) : pers_launch<2, 2, 1, 1, 32>(p, nst, st);
-    }
-  }
   if (dbg && kt == 32 && (tile == 0 || tile == 3))
     return tile == 0 ? xp_launch<2, 2, 2, 2, 32, true>(p, nst, st) : xp_launch<2, 2, 1, 1, 32, true>(p, nst, st);
   switch (tile) {

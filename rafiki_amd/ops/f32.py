@@ -748,15 +748,11 @@ USE_X6P = USE_X6 and os.environ.get('RAFIKI_X6P', '1') != '0'
 XP_TILES = ((128, 128), (128, 64), (64, 128), (64, 64), (64, 64), (128, 64), (64, 128), (256, 128), (128, 256),
             (128, 128), (128, 64), (64, 128), (64, 64))
 XP_NST3 = (0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12)   # tiles 7-8 (8 waves, 72 KiB per stage) ring 2 stages only
-# tile + XP_PERS (tiles 0-3): persistent grid (CUs x resident blocks walking the tile list; the LDS ring runs
-# across tiles, so a tile's epilogue overlaps the next tile's first loads — short-K GEMMs)
-XP_PERS = 32
 # (tile, nst, splits) of the x6p GEMM: every tile x ring depth unsplit; the big tiles also with 2 / 4 K-splits
 # (the 4x4-map GEMMs have T = 256 rows: 288 blocks of 128x128 for 256 CUs; the slabs are summed by the
 # output transforms that read Y' / dU anyway)
 _XP_CFGS = tuple((t, n, 1) for t in range(len(XP_TILES)) for n in ((2, 3) if t in XP_NST3 else (2,))) + \
-    tuple((t, 2, s) for t in (0, 1, 2, 7, 8) for s in (2, 4)) + tuple((t, 3, s) for t in (9, 10, 11) for s in (2, 4)) + \
-    tuple((XP_PERS + t, n, s) for t in (0, 1, 2, 3) for n in (2, 3) for s in (1, 2))
+    tuple((t, 2, s) for t in (0, 1, 2, 7, 8) for s in (2, 4)) + tuple((t, 3, s) for t in (9, 10, 11) for s in (2, 4))
 WINO4_PTX = -15         # conv / data gradient: cfg = (-15, x6p code, splits), code = tile * 4 + nst
 WINO4_WGRAD_PTX = -16   # weight gradient: likewise
 WINO4_PTX_CFGS = tuple((WINO4_PTX, 4 * t + n, s) for t, n, s in _XP_CFGS) if USE_X6P else ()
@@ -1203,8 +1199,8 @@ def bn_bwd(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, 
     if not reduced:
         if C <= 1024 and not (C & (C - 1)):
             npix = dout.numel() // C
-            # ~2 passes of 256 / (C / 4) pixel rows per block: enough blocks to fill the chip on small maps
-            blocks = max(1, min(_BWD_BLOCKS, cdiv(npix, max(1, 256 // (C // 4)) * 2)))
+            # 8 passes of 256 / (C / 4) pixel rows per block (2 passes: 4x the slot atomics, measured slower)
+            blocks = max(1, min(_BWD_BLOCKS, cdiv(npix, max(1, 256 // (C // 4)) * 8)))
             _lib.call("rk_bnf_bwd_reduce", _p(dout), _p(y), _p(coeffs), _p(acc), acc.shape[0], blocks, Nb, H, W, C,
                       int(pool), int(act), float(slope), s)
         elif not pool and act == ACT_NONE:
