@@ -239,6 +239,18 @@ class EnsembleGraphs:
                                    for _ in range(2)]
         return [t.numpy().reshape(-1) for t in self._stage]
 
+    def warm_staged(self):
+        """Capture every bucket's graph for both staging slots now (a lazy first capture inside the serving
+        loop stalls every queued query for its warm-up + capture: the p99 spikes of a server that meets new
+        batch sizes under load)."""
+        if self._stage is None:
+            raise RuntimeError('staging() first')
+        with self.lock:
+            for slot in (0, 1):
+                for b in BUCKETS:
+                    self._entry(b, ('stage', slot))
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
     def launch_staged(self, slot: int, B: int):
         """Replay the graph of staging slot ``slot`` for its first B images (B <= BUCKETS[-1]); returns an
         event the caller waits on before reading ``staged_out(slot)[:B]``.  No host sync here."""

@@ -140,6 +140,8 @@ class NativePredictorServer:
         self._stopped = threading.Event()
         self._pool = None
         self._base = {'python_batches': 0, 'python_errors': 0}
+        self._ready = []
+        self.ready_timeout_s = 300.0
 
     # ------------------------------------------------------------------------------ stats
     @property
@@ -154,6 +156,12 @@ class NativePredictorServer:
 
     # ------------------------------------------------------------------------------ loops
     def _batch_loop(self, idx=0):
+        try:
+            return self._batch_loop_body(idx)
+        finally:
+            self._ready[idx].set()
+
+    def _batch_loop_body(self, idx):
         fn = getattr(self.predictor, 'staged_graphs', None)
         staged = None
         if callable(fn):
@@ -164,7 +172,15 @@ class NativePredictorServer:
         if staged is not None:
             bufs = staged[1].staging(staged[2])
             if bufs is not None:
+                try:
+                    staged[1].warm_staged()   # every bucket x slot captured before the first query
+                except Exception:
+                    logger.error('replica %d: staged graphs failed:\n%s', idx, traceback.format_exc())
+                    self._ready[idx].set()
+                    return self._plain_loop()
+                self._ready[idx].set()
                 return self._staged_loop(staged[1], staged[2], bufs)
+        self._ready[idx].set()
         return self._plain_loop()
 
     def _complete(self, bid, probs, n):
@@ -323,6 +339,7 @@ class NativePredictorServer:
         self._running.set()
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self.generic_threads,
                                                            thread_name_prefix='rafiki-http-py')
+        self._ready = [threading.Event() for _ in range(self.slots)]
         for i in range(self.slots):
             t = threading.Thread(target=self._batch_loop, args=(i,), name='rafiki-http-batch-{}'.format(i),
                                  daemon=True)
@@ -331,6 +348,8 @@ class NativePredictorServer:
         t = threading.Thread(target=self._generic_loop, name='rafiki-http-generic', daemon=True)
         t.start()
         self._threads.append(t)
+        for e in self._ready:   # replicas' graphs captured (queries arriving meanwhile wait in the C++ queue)
+            e.wait(self.ready_timeout_s)
         return self
 
     def serve_forever(self):
