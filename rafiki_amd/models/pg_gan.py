@@ -843,14 +843,13 @@ class PgGan(BaseModel):
         real_l, fake_l = rf_l[:mb], rf_l[mb:]
         loss = fake_s - real_s
         alpha = self._shard(rng.rand((mb * self.world, 1, 1, 1), TrialRng.D_ALPHA))
-        mixed = (reals.float() + (fakes.float() - reals.float()) * alpha).to(reals.dtype).detach().requires_grad_(True)
+        mixed = torch.lerp(reals.float(), fakes.float(), alpha).to(reals.dtype).detach().requires_grad_(True)
         mixed_s, _ = nets.discriminator(PD, mixed, lod)
         if ar is not None:
             ar.begin()
         (grads,) = torch.autograd.grad(mixed_s.sum(), mixed, create_graph=True)
-        norms = grads.float().square().sum((1, 2, 3)).sqrt()
-        loss = loss + (norms - wgan_target).square() * (wgan_lambda / wgan_target ** 2)
-        loss = loss + real_s.square() * wgan_epsilon
+        penalty, norms = _GradPenaltyFn.apply(grads, wgan_lambda / wgan_target ** 2, wgan_target)
+        loss = torch.addcmul(loss + penalty, real_s, real_s, value=wgan_epsilon)
         if nets.label_size:
             loss = loss + _softmax_xent(real_l, labels) + _softmax_xent(fake_l, labels)
         # data-parallel rounds launch their all-reduce buckets from post-accumulate-grad hooks, so
@@ -861,8 +860,7 @@ class PgGan(BaseModel):
             ar.finish()
         if apply:
             self._apply(nets.D, opt, rng)
-        return torch.stack([loss.mean().detach(), real_s.mean().detach(), fake_s.mean().detach(),
-                            norms.mean().detach()])
+        return torch.stack([loss.detach(), real_s.detach(), fake_s.detach(), norms.detach()]).mean(1)
 
     def _g_step(self, lod, mb, labels_all, rng, opt, ar, apply=True):
         """_G_wgan_acgan (pg_gans.py:1276-1289) + G optimizer step (``apply=False``: gradients only)."""
@@ -1009,6 +1007,27 @@ class PgGan(BaseModel):
 
 
 # ============================================================================== eval helpers
+class _GradPenaltyFn(torch.autograd.Function):
+    """WGAN-GP penalty of per-sample gradients g [mb, ...]: -> (lambda (|g| - t)^2 [mb], |g| [mb]).  Forward:
+    one norm reduction; backward: one broadcast multiply, d/dg = 2 lambda (|g| - t) / |g| * g * gout (the
+    autograd chain of square / sum / sqrt / sub / square / mul was ~14 small kernels per D step)."""
+
+    @staticmethod
+    def forward(ctx, g, lam, target):
+        n = torch.linalg.vector_norm((g if g.dtype == torch.float64 else g.float()).reshape(g.shape[0], -1), dim=1)
+        ctx.save_for_backward(g, n)
+        ctx.lam, ctx.target = lam, target
+        return (n - target).square() * lam, n
+
+    @staticmethod
+    def backward(ctx, gp, gn):
+        g, n = ctx.saved_tensors
+        coef = gp * (2.0 * ctx.lam) * (n - ctx.target) / n.clamp_min(1e-30)
+        if gn is not None:
+            coef = coef + gn / n.clamp_min(1e-30)
+        return (g * coef.view((-1,) + (1,) * (g.dim() - 1)).to(g.dtype)), None, None
+
+
 def _softmax_xent(logits, onehot):
     return -(torch.log_softmax(logits.float(), 1) * onehot).sum(1)
 

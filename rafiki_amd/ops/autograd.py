@@ -263,7 +263,14 @@ class ConvDgradFn(torch.autograd.Function):
         if _needed(ctx, 0):
             g_gy = ConvFn.apply(ggx, w, None, ctx.wb, ctx.taps, None)
         if _needed(ctx, 1):
-            g_w = ConvWgradFn.apply(ggx, gy, ctx.taps)
+            # the WGAN-GP penalty's second-order weight gradient: straight into the .grad arena when the
+            # outer backward allows it (no autograd sum / AccumulateGrad add kernels)
+            buf = _param_grad_buffer(w) if gy.dtype == F32 and ggx.dtype == F32 else None
+            if buf is not None:
+                S.conv_wgrad(gy.contiguous(), ggx.contiguous(), taps=ctx.taps, out=buf.view(buf.shape[0], -1),
+                             accumulate=True)
+            else:
+                g_w = ConvWgradFn.apply(ggx, gy, ctx.taps)
         return g_gy, g_w, None, None
 
 
@@ -602,7 +609,11 @@ class DenseDxFn(torch.autograd.Function):
         if _needed(ctx, 0):
             g_gy = DenseFn.apply(ggx, w, None, ctx.wb, None)
         if _needed(ctx, 1):
-            g_w = DenseDwFn.apply(ggx, gy)
+            buf = _param_grad_buffer(w) if gy.dtype == F32 and ggx.dtype == F32 else None
+            if buf is not None:
+                S.linear_dw(gy.contiguous(), ggx.contiguous(), out=buf, accumulate=True)
+            else:
+                g_w = DenseDwFn.apply(ggx, gy)
         return g_gy, g_w, None
 
 

@@ -129,6 +129,34 @@ def test_wgan_gp_double_backward_matches_fp32(lod, dtype):
             assert cos(a.cpu(), b) > 0.97, (name, cos(a.cpu(), b))
 
 
+@pytest.mark.parametrize("lod", [0.0, 0.5])
+def test_wgan_gp_in_place_weight_grads_match_autograd(lod):
+    """accumulate_weight_grads_in_place: the first- AND second-order (penalty double backward) conv / dense
+    weight gradients go straight into the .grad arena; the result equals autograd's summed gradients,
+    and the fused penalty Function (_GradPenaltyFn) equals the square / sum / sqrt chain."""
+    from rafiki_amd.models.pg_gan import _GradPenaltyFn
+    from rafiki_amd.ops import autograd as A
+    gnet, _ = _twin_nets(dtype='fp32')
+    torch.manual_seed(0)
+    x = torch.randn(8, 8, 8, gnet.cpad)
+    x[..., 1:] = 0
+    x = x.to(DEV)
+    gnet.D.grad.zero_()
+    _, _, loss = _gp_loss(gnet, x, lod)
+    loss.backward()
+    ref = gnet.D.grad.clone()
+    gnet.D.grad.zero_()
+    P = gnet.src_D()
+    xi = x.clone().requires_grad_(True)
+    s, _ = gnet.discriminator(P, xi, lod)
+    (gr,) = torch.autograd.grad(s.sum(), xi, create_graph=True)
+    pen, _ = _GradPenaltyFn.apply(gr, 10.0, 1.0)
+    with A.accumulate_weight_grads_in_place():
+        torch.addcmul(pen, s.float(), s.float(), value=1e-3).mean().backward()
+    torch.cuda.synchronize()
+    assert frob(gnet.D.grad, ref) < 1e-5, frob(gnet.D.grad, ref)
+
+
 @pytest.mark.parametrize("dtype", ['fp32', 'bf16'])
 def test_generator_upconv_path_matches_fp32(dtype):
     gnet, cnet = _twin_nets(res=16, dtype=dtype)
