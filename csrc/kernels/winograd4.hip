@@ -1428,7 +1428,7 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
                                                             const float* __restrict__ bp, double* stats, int slotMask,
                                                             const float* __restrict__ gate, int Nb, int H, int W,
                                                             int N, int TW, int THW, int T, int flags, int nslab,
-                                                            long long slab) {
+                                                            long long slab, long long qs, long long ts) {
   constexpr int TPB = 4;                   // tiles per block: one per 64-thread group (>= 2 blocks per CU
                                            // on the 4x4 x 512 maps: T x N / 256 blocks)
   __shared__ float red[2][4][64];
@@ -1437,7 +1437,6 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
   const int lane = threadIdx.x & 63, tg = threadIdx.x >> 6;
   const int n = nb * 64 + lane;
   const bool nok = n < N;
-  const long long plane = (long long)T * N;
   const float bs = ((flags & (WF_BIAS | WF_BNB | WF_BNP)) && nok) ? bp[n] : 0.f;
   const float sh = ((flags & (WF_BNB | WF_BNP)) && nok) ? bp[N + n] : 0.f;
   float s = 0.f, ss = 0.f;
@@ -1446,10 +1445,10 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
     if (t < T && nok) {
     float m[36];
 #pragma unroll
-    for (int q = 0; q < 36; ++q) m[q] = yt[q * plane + (long long)t * N + n];
+    for (int q = 0; q < 36; ++q) m[q] = yt[q * qs + (long long)t * ts + n];
     for (int k = 1; k < nslab; ++k)   // split-K partial slabs of the GEMM
 #pragma unroll
-      for (int q = 0; q < 36; ++q) m[q] += yt[k * slab + q * plane + (long long)t * N + n];
+      for (int q = 0; q < 36; ++q) m[q] += yt[k * slab + q * qs + (long long)t * ts + n];
     float tt[6][4];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {          // M A: along columns
@@ -1522,7 +1521,7 @@ __global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restr
                                                             const float* __restrict__ bp, double* stats, int slotMask,
                                                             const float* __restrict__ gate, int Nb, int H, int W,
                                                             int N, int TW, int THW, int T, int flags, int nslab,
-                                                            long long slab) {
+                                                            long long slab, long long qs, long long ts) {
   constexpr int LPT = 64 / VW, TPB = 64 / LPT;   // lanes per tile, tiles per block
   typedef __attribute__((ext_vector_type(VW))) float fv;
   __shared__ float red[2][TPB][64];
@@ -1531,7 +1530,6 @@ __global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restr
   const int qd = threadIdx.x % LPT, tg = threadIdx.x / LPT;
   const int n = nb * 64 + VW * qd;
   const bool nok = n < N;
-  const long long plane = (long long)T * N;
   fv bs = {}, sh = {};
   if ((flags & (WF_BIAS | WF_BNB | WF_BNP)) && nok) bs = *(const fv*)(bp + n);
   if ((flags & (WF_BNB | WF_BNP)) && nok) sh = *(const fv*)(bp + N + n);
@@ -1539,12 +1537,12 @@ __global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restr
   const int t = tb * TPB + tg;
   if (t < T && nok) {
     fv m[36];
-    const float* src = yt + (long long)t * N + n;
+    const float* src = yt + (long long)t * ts + n;
 #pragma unroll
-    for (int q = 0; q < 36; ++q) m[q] = *(const fv*)(src + q * plane);
+    for (int q = 0; q < 36; ++q) m[q] = *(const fv*)(src + q * qs);
     for (int k = 1; k < nslab; ++k)   // split-K partial slabs of the GEMM
 #pragma unroll
-      for (int q = 0; q < 36; ++q) m[q] += *(const fv*)(src + k * slab + q * plane);
+      for (int q = 0; q < 36; ++q) m[q] += *(const fv*)(src + k * slab + q * qs);
     const int im = t / THW, rr = t - im * THW, ty = rr / TW;
     const int oy = 4 * ty, ox = 4 * (rr - ty * TW);
     fv res[4][4];
@@ -1637,9 +1635,11 @@ __global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restr
 }  // namespace
 
 // yt: nslab slabs of [36][T][N], slab floats apart (split-K partial sums of the GEMM), summed here
+// tmajor: Y' is tile-major [T][36][N] (the plane GEMM writes it so: each tile's 36 positions in one 36N-float
+// run instead of 36 runs a T x N plane apart), else position-major [36][T][N]
 extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias, double* stats, int slotMask,
                                     const float* gate, int Nb, int H, int W, int N, int flags, int nslab,
-                                    long long slab, void* stream) {
+                                    long long slab, int tmajor, void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || N <= 0 || nslab <= 0) return RK_EBADARG;
   if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
   if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
@@ -1649,6 +1649,7 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
   if (T * N >= (1LL << 31)) return RK_EUNSUPPORTED;
   const long long blocks = ((N + 63) / 64) * ((T + 3) / 4);
   if (nslab > 1 && slab < 36 * T * N) return RK_EBADARG;
+  const long long qs = tmajor ? N : T * N, ts = tmajor ? 36LL * N : N;
   // vector widths: RAFIKI_PT_OUT_VW = 4 (16-B) | 2 (8-B, default: fewer registers) | 1 (the scalar kernel)
   static const int vw = getenv("RAFIKI_PT_OUT_VW") ? atoi(getenv("RAFIKI_PT_OUT_VW")) : 2;
   if ((vw == 2 || vw == 4) && N % vw == 0) {
@@ -1656,15 +1657,15 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
     const long long blocksv = ((N + 63) / 64) * ((T + tpb - 1) / tpb);
     if (vw == 4)
       hipLaunchKernelGGL(w4pt_conv_outv_kernel<4>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
-                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab);
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts);
     else
       hipLaunchKernelGGL(w4pt_conv_outv_kernel<2>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
-                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab);
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts);
     RK_LAUNCH_CHECK();
     return RK_OK;
   }
   hipLaunchKernelGGL(w4pt_conv_out_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, yt, y, bias,
-                     stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab);
+                     stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -503,7 +503,10 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   if ((2 * psA + (long long)M * lda) * 2 >= (1ll << 31) || (2 * psB + (long long)N * ldb) * 2 >= (1ll << 31))
     return RK_EUNSUPPORTED;
   // gsA / gsB == 0: one operand shared by every group (broadcast)
-  if (groups > 1 && ((gsA && gsA < 3 * psA) || (gsB && gsB < 3 * psB) || gsC < (long long)M * ldc)) return RK_EBADARG;
+  // group outputs: group-major (gsC >= M ldc) or row-interleaved (gsC >= N, ldc >= groups gsC, e.g. [M][G][N])
+  if (groups > 1 && ((gsA && gsA < 3 * psA) || (gsB && gsB < 3 * psB) ||
+                     (gsC < (long long)M * ldc && (gsC < N || ldc < (long long)groups * gsC))))
+    return RK_EBADARG;
   if (2 * (gsA * (groups - 1) + 3 * psA) > bytesA || 2 * (gsB * (groups - 1) + 3 * psB) > bytesB) return RK_EBADARG;
   XpParams p;
   p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = C;

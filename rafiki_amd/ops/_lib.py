@@ -78,7 +78,7 @@ _SIGS = {
     "rk_wino4_pt_transform": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "rk_wino4_pt_output": [vp, vp, i32, i32, i32, i32, i64, vp],
     "rk_wino4_pt_input": [vp, vp, i32, i32, i32, i32, vp],
-    "rk_wino4_pt_conv_out": [vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, vp],
+    "rk_wino4_pt_conv_out": [vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, i32, vp],
     "rk_wino2s_conv_grp": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, vp],
     # fp32 path (sgemm.hip, bnf.hip)
     "rk_sgemm": [i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,

@@ -610,10 +610,11 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
     T = Nb * (H // 4) * (W // 4)
     if planes:   # pre-split X6: V planes [36][3][T][C] once, then the plane GEMM (no split in the K loop)
         splits = x6p_splits(C, splits)
-        yt = torch.empty((splits, 36, T, N), device=x.device, dtype=torch.float32)
+        # Y' tile-major [T][36][N]: the output transform reads each tile's 36 positions as one run
+        yt = torch.empty((splits, T, 36, N), device=x.device, dtype=torch.float32)
         v = torch.empty((36, 3, T, C), device=x.device, dtype=torch.bfloat16)
         _lib.call("rk_x6p_w4_input", _p(x), _p(v), Nb, H, W, C, _s())
-        x6p_gemm(v, u, yt, T, N, C, groups=36, tile=tile, nst=nst, splits=splits)
+        x6p_gemm(v, u, yt, T, N, C, groups=36, tile=tile, nst=nst, splits=splits, row_major_groups=True)
     else:
         splits = 1
         yt = torch.empty((36, T, N), device=x.device, dtype=torch.float32)
@@ -621,7 +622,7 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
         _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
         sgemm_grp(KIND_DENSE, v, u, yt, T, N, C, C, C, N, 36, T * C, N * C, T * N, tile=tile, nst=nst)
     _lib.call("rk_wino4_pt_conv_out", _p(yt), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
-              Nb, H, W, N, flags, splits, 36 * T * N, _s())
+              Nb, H, W, N, flags, splits, 36 * T * N, int(planes), _s())
     return out
 
 
@@ -769,14 +770,17 @@ def x6p_split(src: torch.Tensor, out=None) -> torch.Tensor:
 
 
 def x6p_gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, M: int, N: int, K: int, *, groups: int = 1,
-             tile: int = 0, nst: int = 2, accumulate: bool = False, splits: int = 1) -> torch.Tensor:
+             tile: int = 0, nst: int = 2, accumulate: bool = False, splits: int = 1,
+             row_major_groups: bool = False) -> torch.Tensor:
     """out[g] (+)= A[g] . B[g]^T for g < groups: A bf16 planes [G][3][M][K], B [G][3][N][K] (contiguous),
-    out fp32 [G][M][N]; K % 32 == 0.  splits > 1: out is [splits][G][M][N] raw split-K partial sums."""
+    out fp32 [G][M][N] (``row_major_groups``: [M][G][N]); K % 32 == 0.  splits > 1: out is [splits][...] raw
+    split-K partial sums."""
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and A.is_contiguous() and B.is_contiguous()
     assert A.numel() == groups * 3 * M * K and B.numel() == groups * 3 * N * K
     assert out.numel() == splits * groups * M * N and not (accumulate and splits > 1)
-    _lib.call("rk_x6p_gemm", int(tile), int(nst), _p(A), _p(B), _p(out), M, N, K, K, K, N, M * K, N * K, 3 * M * K,
-              3 * N * K, M * N, int(groups), int(bool(accumulate)), int(splits), groups * M * N, _nbytes(A),
+    ldc, gsc = (groups * N, N) if row_major_groups else (N, M * N)
+    _lib.call("rk_x6p_gemm", int(tile), int(nst), _p(A), _p(B), _p(out), M, N, K, K, K, ldc, M * K, N * K, 3 * M * K,
+              3 * N * K, gsc, int(groups), int(bool(accumulate)), int(splits), groups * M * N, _nbytes(A),
               _nbytes(B), _s())
     return out
 

@@ -11,7 +11,7 @@ mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/t -o run -- \
   python3 scripts/bench_pg_gan.py --lods $LOD --steps $STEPS --warmup 3 > $OUT/t.log 2>&1
 python3 scripts/trace_steps.py $(find $OUT/t -name '*kernel_trace.csv' | head -1) --steps $STEPS \
-  --marker lerp_kernel --csv $OUT/kernels.csv > $OUT/kernels.txt
+  --marker lerp_kernel --csv $OUT/kernels.csv --seq $OUT/seq.txt > $OUT/kernels.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES \
   SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
   --output-format csv -d $OUT/p0 -o run -- python3 scripts/bench_pg_gan.py --lods $LOD --steps 2 --warmup 1 \
