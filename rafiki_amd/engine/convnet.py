@@ -231,7 +231,9 @@ class ConvNetEngine:
     # re-measured with the current kernels, still 5-6% slower (258k -> 243-245k img/s), so it is off
     # by default (RAFIKI_OVERLAP_WGRAD=1) and kept as an option for layer shapes where it pays.
     # fp32 path (Winograd kernels, one or two LDS-heavy workgroups per CU): 2.27 -> 2.46 ms, 8% slower.
-    overlap_wgrad = os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') == '1'
+    # 'deep': only the 8x8 / 4x4 layers (grids of a few hundred workgroups that leave CUs idle)
+    overlap_wgrad = os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') in ('1', 'deep')
+    overlap_max_hw = 8 if os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') == 'deep' else 1 << 30
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
     # ... and into BN+ReLU+max-pool blocks (FLAG_BNP: argmax routing in the dgrad epilogue)
@@ -467,7 +469,7 @@ class ConvNetEngine:
             y, coeffs = saved[bi]
             dy = S.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), accs[bi][1], pool=pool, act=F.ACT_RELU,
                           dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'), reduced=reduced)
-            if side is not None:
+            if side is not None and hw <= self.overlap_max_hw:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
