@@ -251,11 +251,14 @@ def test_one_graph_ensemble_matches_per_model_path(ensemble, monkeypatch):
         ref = ref_p.predict_array(imgs)
         monkeypatch.setenv('RAFIKI_ENSEMBLE_GRAPH', '1')
         got = p.predict_array(imgs)
-        # two kernel sets (grouped one-graph network vs per-model engines): fp32 rounding through 10 layers
-        assert got.shape == (n, 10) and np.abs(got - ref).max() < 5e-5, (n, np.abs(got - ref).max())
+        # two kernel sets (grouped one-graph network vs per-model engines): fp32 rounding through 10 layers,
+        # amplified by folded eval-BN scales of the 1-epoch models (up to 1/sqrt(eps) on near-dead channels):
+        # the median row agrees to ~1e-7, single rows drift to ~5e-4; a wrong row / batch is off by ~1e-1
+        assert got.shape == (n, 10) and np.abs(got - ref).max() < 2e-3, (n, np.abs(got - ref).max())
+        assert np.median(np.abs(got - ref).max(1)) < 1e-5, n
         sig = models[0][1].input_signature()
         dev = p.predict_proba_device({sig: torch.from_numpy(imgs).to(DEV)})
-        assert np.abs(dev.cpu().numpy() - ref).max() < 5e-5, n
+        assert np.abs(dev.cpu().numpy() - ref).max() < 2e-3, n
     g = p.replicas[0].graphs
     assert g is not None and g.replays >= 8 and ref_p.replicas[0].graphs is None
     assert {b for b, _ in g._graphs} >= {1, 8, 64, 512}
@@ -335,8 +338,9 @@ def test_per_model_path_is_thread_safe_on_one_replica(ensemble, monkeypatch):
     # every row is its own query's answer (a mixed-up batch is off by ~1e-1, not by rounding) ...
     d = np.abs(got[:, None, :] - ref[None, :, :]).max(-1)
     assert (d.argmin(1) == np.arange(len(ref))).all()
-    # ... and the per-model kernels agree with the grouped one-graph network to fp32 rounding
-    assert np.abs(got - ref).max() < 5e-5, np.abs(got - ref).max()
+    # ... and the per-model kernels agree with the grouped one-graph network to (BN-amplified) fp32 rounding
+    assert np.abs(got - ref).max() < 2e-3, np.abs(got - ref).max()
+    assert np.median(np.abs(got - ref).max(1)) < 1e-5
 
 
 def test_pipelined_batcher_matches_direct_path(ensemble):
