@@ -433,206 +433,6 @@ int ws_launch_kt(const XpParams& p, int nst, int kt, hipStream_t st) {
   return kt == 64 ? ws_launch<MI, NI, 64>(p, nst, st) : ws_launch<MI, NI, 32>(p, nst, st);
 }
 
-// ---------------------------------------------------------------------------------------------------------
-// x6s: the X6 GEMM on fp32 operands split ONCE per element inside the workgroup.  fp32 K-tiles (32 deep,
-// 128-B rows) arrive by LDS-DMA into an NST-stage ring; while the MFMAs of tile kt read bf16 hi / mid / lo
-// fragments from plane buffer P[kt & 1] (the x6p layout), the same waves split tile kt+1 (one 16-B chunk
-// = 4 values per thread and step: ds_read_b128, split3v, three ds_write_b64) into P[(kt+1) & 1].  Against
-// x6p: 4 instead of 6 bytes per element from L2 and no plane-writing producers; against the sgemm X6 loop:
-// each element split once per workgroup instead of once per wave that reads it.
-template <int T, int NW>
-struct FOp {   // fp32 operand: T rows x 32 k per K-tile, 8 rows (1 KiB) per DMA wave-instruction
-  static constexpr int PI = T / 8;
-  static constexpr int NQ = PI / NW;
-  static_assert(NQ >= 1 && NQ * NW == PI, "fp32 operand tile must split evenly over the waves");
-  __amdgpu_buffer_rsrc_t rsrc;
-  unsigned off[NQ];
-  RK_DEV void init(const float* base, unsigned long long bytes, int ld, int row0, int extent, int wid, int lane) {
-    rsrc = s_rsrc(base, bytes);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int r = (wid * NQ + q) * 8 + (lane >> 3);
-      const int gr = row0 + r;
-      off[q] = gr < extent ? (unsigned)(((long long)gr * ld + (lane & 7) * 4) * 4) : SOOB;
-    }
-  }
-  RK_DEV void issue(char* tile, int kt, int wid) const {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(tile + (wid * NQ + q) * 1024), 16,
-                                               (int)(off[q] + (unsigned)kt * 128u), 0, 0, 0);
-  }
-};
-
-// split chunk ci (row ci / 8, fp32 k 4 (ci % 8) .. +3) of a T-row fp32 stage into the T-row plane image
-template <int T>
-RK_DEV void x6s_split_chunk(const char* f, char* pl, int ci) {
-  const int r = ci >> 3, c = ci & 7;
-  const f32x4 v = *(const f32x4*)(f + r * 128 + c * 16);
-  bf16x4 h, m, l;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    bf16 a, b, d;
-    split3v(v[e], a, b, d);
-    h[e] = a;
-    m[e] = b;
-    l[e] = d;
-  }
-  const int o = r * 64 + (((c >> 1) ^ xswz<32>(r)) << 4) + (c & 1) * 8;
-  *(bf16x4*)(pl + o) = h;
-  *(bf16x4*)(pl + T * 64 + o) = m;
-  *(bf16x4*)(pl + 2 * T * 64 + o) = l;
-}
-
-template <int WGM, int WGN, int MI, int NI, int NST>
-__global__ __launch_bounds__(64 * WGM * WGN) void x6s_gemm_kernel(const XpParams p) {
-  constexpr int NW = WGM * WGN, NT = 64 * NW;
-  constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
-  constexpr int FA = BM * 128, FS = (BM + BN) * 128;     // fp32 stage: A rows then B rows
-  constexpr int PA = 3 * BM * 64, PS = 3 * (BM + BN) * 64;   // plane buffer: A planes then B planes
-  using OA = FOp<BM, NW>;
-  using OB = FOp<BN, NW>;
-  constexpr int L = OA::NQ + OB::NQ;
-  constexpr int CA = BM * 8 / NT, CB = BN * 8 / NT;        // split chunks per thread per K-tile
-  static_assert(CA * NT == BM * 8 && CB * NT == BN * 8, "split chunks");
-  __shared__ __attribute__((aligned(16))) char smem[NST * FS + 2 * PS];
-  char* const pbuf = smem + NST * FS;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WGN, wn = wid - (wid / WGN) * WGN;
-  const int tilesN = (p.N + BN - 1) / BN;
-  const int tiles = ((p.M + BM - 1) / BM) * tilesN;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int gs = lin / tiles, bid = lin - gs * tiles;
-  const int grp = gs / p.splits, split = gs - grp * p.splits;
-  const int mt = bid / tilesN, nt = bid - mt * tilesN;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int kt0 = split * p.ktPer;
-  const int nk = min(p.K / 32 - kt0, p.ktPer);
-  const float* Ab = (const float*)p.A;
-  const float* Bb = (const float*)p.B;
-  OA A;
-  OB B;
-  const unsigned long long ka = 4ull * (unsigned long long)kt0 * 32;
-  A.init(Ab + grp * p.gsA + kt0 * 32, p.bytesA - 4ull * (unsigned long long)(grp * p.gsA) - ka, p.lda, m0, p.M, wid,
-         lane);
-  B.init(Bb + grp * p.gsB + kt0 * 32, p.bytesB - 4ull * (unsigned long long)(grp * p.gsB) - ka, p.ldb, n0, p.N, wid,
-         lane);
-  XOp<BM, NW, 32> FAop;   // fragment addressing of the plane images
-  XOp<BN, NW, 32> FBop;
-
-  auto split_tile = [&](const char* f, char* pl) {
-#pragma unroll
-    for (int j = 0; j < CA; ++j) x6s_split_chunk<BM>(f, pl, tid + j * NT);
-#pragma unroll
-    for (int j = 0; j < CB; ++j) x6s_split_chunk<BN>(f + FA, pl + PA, tid + j * NT);
-  };
-
-#pragma unroll
-  for (int s = 0; s < NST; ++s) {
-    if (s < nk) {
-      A.issue(smem + s * FS, s, wid);
-      B.issue(smem + s * FS + FA, s, wid);
-    }
-  }
-  // tile 0 landed: only the younger prologue tiles may be outstanding
-  if constexpr (NST == 3) {
-    if (nk >= 3) s_wait_vmcnt<2 * L>();
-    else if (nk == 2) s_wait_vmcnt<L>();
-    else s_wait_vmcnt<0>();
-  } else {
-    if (nk >= 2) s_wait_vmcnt<L>();
-    else s_wait_vmcnt<0>();
-  }
-  s_barrier_lds();
-  split_tile(smem, pbuf);
-
-  f32x16 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt+1 has landed (it is split during this tile's MFMAs) once only younger tiles are outstanding
-    if constexpr (NST == 3) {
-      if (kt + 2 < nk) s_wait_vmcnt<L>();
-      else s_wait_vmcnt<0>();
-    } else {
-      s_wait_vmcnt<0>();
-    }
-    s_barrier_lds();   // P[kt & 1] complete; P[(kt+1) & 1] and the stage of tile kt free
-    if (kt + NST < nk) {   // refill the stage tile kt used (split in the previous iteration)
-      A.issue(smem + (kt % NST) * FS, kt + NST, wid);
-      B.issue(smem + (kt % NST) * FS + FA, kt + NST, wid);
-    }
-    const char* As = pbuf + (kt & 1) * PS;
-    const char* Bs = As + PA;
-    const bool more = kt + 1 < nk;
-    const char* fn = smem + ((kt + 1) % NST) * FS;
-    char* pn = pbuf + ((kt + 1) & 1) * PS;
-    bf16x8 fa[2][3][MI], fb[2][3][NI];
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) fa[0][pl][i] = FAop.frag(As, pl, wm * 32 * MI + i * 32, 0, lane);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) fb[0][pl][j] = FBop.frag(Bs, pl, wn * 32 * NI + j * 32, 0, lane);
-    }
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) fa[1][pl][i] = FAop.frag(As, pl, wm * 32 * MI + i * 32, 1, lane);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) fb[1][pl][j] = FBop.frag(Bs, pl, wn * 32 * NI + j * 32, 1, lane);
-    }
-    // chunk 0's MFMAs beside the first half of the next tile's split, chunk 1's beside the second
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      if (more) {
-        if (c == 0) {
-#pragma unroll
-          for (int j = 0; j < CA; ++j) x6s_split_chunk<BM>(fn, pn, tid + j * NT);
-        } else {
-#pragma unroll
-          for (int j = 0; j < CB; ++j) x6s_split_chunk<BN>(fn + FA, pn + PA, tid + j * NT);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = mfma6(fa[c][0][i], fa[c][1][i], fa[c][2][i], fb[c][0][j], fb[c][1][j], fb[c][2][j], acc[i][j]);
-    }
-  }
-  s_wait_vmcnt<0>();
-  xp_store<MI, NI>(p, acc, grp, split, m0 + wm * 32 * MI, n0 + wn * 32 * NI, lane);
-}
-
-template <int MI, int NI>
-int x6s_launch(const XpParams& p, int nst, hipStream_t st) {
-  constexpr int BM = 64 * MI, BN = 64 * NI;
-  constexpr int FS = (BM + BN) * 128, PS = 3 * (BM + BN) * 64;
-  const long long blocks = (long long)rk_cdiv(p.M, BM) * rk_cdiv(p.N, BN) * p.groups * p.splits;
-  if (blocks >= (1ll << 31)) return RK_EUNSUPPORTED;
-  const dim3 grid((unsigned)blocks), block(256);
-  if (nst == 3) {
-    if constexpr (3 * FS + 2 * PS <= 163840)
-      hipLaunchKernelGGL((x6s_gemm_kernel<2, 2, MI, NI, 3>), grid, block, 0, st, p);
-    else
-      return RK_EUNSUPPORTED;
-  } else {
-    if constexpr (2 * FS + 2 * PS <= 163840)
-      hipLaunchKernelGGL((x6s_gemm_kernel<2, 2, MI, NI, 2>), grid, block, 0, st, p);
-    else
-      return RK_EUNSUPPORTED;
-  }
-  RK_LAUNCH_CHECK();
-  return RK_OK;
-}
-
 template <int WGM, int WGN, int MI, int NI, int KT, bool DBG = false>
 int xp_launch(const XpParams& p, int nst, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
@@ -750,48 +550,6 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
     case 10: return ws_launch_kt<2, 1>(p, nst, kt, st);
     case 11: return ws_launch_kt<1, 2>(p, nst, kt, st);
     case 12: return ws_launch_kt<1, 1>(p, nst, kt, st);
-  }
-  return RK_EBADARG;
-}
-
-// C[g] (+)= A[g] . B[g]^T with FP32 operands split inside the workgroup (x6s): A[g] [M][lda] (group stride
-// gsA floats), B[g] [N][ldb]; K % 32 == 0; tile 0 128x128, 1 128x64, 2 64x128, 3 64x64 (2x2 waves); nst 2 / 3
-// (where the LDS fits); C, flags, splits and slabs as rk_x6p_gemm (gsC / ldc: group-major or row-interleaved).
-extern "C" int rk_x6s_gemm(int tile, int nst, const float* A, const float* B, float* C, int M, int N, int K, int lda,
-                           int ldb, int ldc, long long gsA, long long gsB, long long gsC, int groups, int flags,
-                           int splits, long long slabStride, long long bytesA, long long bytesB, void* stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || groups <= 0 || (nst != 2 && nst != 3) || tile < 0 || tile > 3 || splits <= 0)
-    return RK_EBADARG;
-  if (splits > 1 && ((flags & 1) || slabStride < (long long)groups * gsC || slabStride < (long long)M * ldc))
-    return RK_EBADARG;
-  if (K % 32 || lda % 4 || ldb % 4 || lda < K || ldb < K || ldc < N) return RK_EUNSUPPORTED;
-  if ((long long)M * lda * 4 >= (1ll << 31) || (long long)N * ldb * 4 >= (1ll << 31) ||
-      (long long)M * ldc * 4 >= (1ll << 31))
-    return RK_EUNSUPPORTED;
-  if (groups > 1 && ((gsA && gsA < (long long)M * lda) || (gsB && gsB < (long long)N * ldb) ||
-                     (gsC < (long long)M * ldc && (gsC < N || ldc < (long long)groups * gsC))))
-    return RK_EBADARG;
-  if (4 * (gsA * (groups - 1) + (long long)M * lda) > bytesA || 4 * (gsB * (groups - 1) + (long long)N * ldb) > bytesB)
-    return RK_EBADARG;
-  XpParams p;
-  p.A = (const bf16*)(const void*)A; p.B = (const bf16*)(const void*)B; p.C = C;
-  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
-  p.psA = p.psB = 0; p.gsA = gsA; p.gsB = gsB; p.gsC = gsC;
-  p.groups = groups; p.flags = flags;
-  const int nk = K / 32;
-  p.ktPer = rk_cdiv(nk, splits);
-  p.splits = rk_cdiv(nk, p.ktPer);
-  if (p.splits != splits) return RK_EBADARG;
-  p.slabStride = splits > 1 ? slabStride : 0;
-  p.dbg = 0;
-  p.stamps = nullptr;
-  p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
-  const hipStream_t st = (hipStream_t)stream;
-  switch (tile) {
-    case 0: return x6s_launch<2, 2>(p, nst, st);
-    case 1: return x6s_launch<2, 1>(p, nst, st);
-    case 2: return x6s_launch<1, 2>(p, nst, st);
-    case 3: return x6s_launch<1, 1>(p, nst, st);
   }
   return RK_EBADARG;
 }

@@ -196,10 +196,6 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
             wino4_conv_pt(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
                           relu=act == ACT_RELU, tile=nst, nst=s)
             return
-        if tile == WINO4_PTS:
-            wino4_conv_pt(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
-                          relu=act == ACT_RELU, tile=nst // 4, nst=nst % 4, splits=s, gemm='x6s')
-            return
         if cfg in WINO4_CFGS:
             wino4_conv(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
                        relu=act == ACT_RELU, variant=_wino4_variant(cfg))
@@ -225,8 +221,6 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         cands.extend(WINO4_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
-        if Cin % 32 == 0:
-            cands.extend(WINO4_PTS_CFGS)
     if use_ptx:
         cands.extend(WINO4_PTX_CFGS)
     cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w,
@@ -280,10 +274,6 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
             wino4_conv_pt(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, tile=cfg[1],
                           nst=cfg[2])
             return
-        if cfg[0] == WINO4_PTS:
-            wino4_conv_pt(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp, tile=cfg[1] // 4,
-                          nst=cfg[1] % 4, splits=cfg[2], gemm='x6s')
-            return
         if cfg in WINO4_CFGS:
             wino4_conv(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp,
                        variant=_wino4_variant(cfg))
@@ -300,8 +290,6 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
         cands.extend(WINO4_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
-        if Cout % 32 == 0:
-            cands.extend(WINO4_PTS_CFGS)
     if use_ptx:
         cands.extend(WINO4_PTX_CFGS)
     cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w,
@@ -588,7 +576,7 @@ WINO4_PT_CFGS = tuple((WINO4_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)
 
 
 def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None,
-                  bnp=None, tile=0, nst=2, splits=1, gemm='sgemm'):
+                  bnp=None, tile=0, nst=2, splits=1):
     """wino4_conv through position-major buffers: V = B^T x B [36][T][C] (one launch), Y'[q] = V[q] u[q]^T
     as one 36-group sgemm, then A^T Y' A with the same epilogues (bias / ReLU / BN statistics / BNB / BNP).
     With bf16 X6 planes u [36][3][N][C] (WinoWeights 'u4p' / 'ut4p') the input transform writes V as planes
@@ -627,12 +615,6 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
         v = torch.empty((36, 3, T, C), device=x.device, dtype=torch.bfloat16)
         _lib.call("rk_x6p_w4_input", _p(x), _p(v), Nb, H, W, C, _s())
         x6p_gemm(v, u, yt, T, N, C, groups=36, tile=tile, nst=nst, splits=splits, row_major_groups=True)
-    elif gemm == 'x6s':   # fp32 V [36][T][C], the GEMM splits each element once per workgroup
-        splits = x6p_splits(C, splits)
-        yt = torch.empty((splits, T, 36, N), device=x.device, dtype=torch.float32)
-        v = torch.empty((36, T, C), device=x.device, dtype=torch.float32)
-        _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
-        x6s_gemm(v, u, yt, T, N, C, groups=36, tile=tile, nst=nst, splits=splits, row_major_groups=True)
     else:
         splits = 1
         yt = torch.empty((36, T, N), device=x.device, dtype=torch.float32)
@@ -640,7 +622,7 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
         _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
         sgemm_grp(KIND_DENSE, v, u, yt, T, N, C, C, C, N, 36, T * C, N * C, T * N, tile=tile, nst=nst)
     _lib.call("rk_wino4_pt_conv_out", _p(yt), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
-              Nb, H, W, N, flags, splits, 36 * T * N, int(planes or gemm == 'x6s'), _s())
+              Nb, H, W, N, flags, splits, 36 * T * N, int(planes), _s())
     return out
 
 
@@ -775,12 +757,6 @@ _XP_CFGS = tuple((t, n, 1) for t in range(len(XP_TILES)) for n in ((2, 3) if t i
 WINO4_PTX = -15         # conv / data gradient: cfg = (-15, x6p code, splits), code = tile * 4 + nst
 WINO4_WGRAD_PTX = -16   # weight gradient: likewise
 WINO4_PTX_CFGS = tuple((WINO4_PTX, 4 * t + n, s) for t, n, s in _XP_CFGS) if USE_X6P else ()
-# the fp32-operand pre-transformed path with the in-workgroup split GEMM (x6s): cfg = (-17, 4 tile + nst, splits)
-WINO4_PTS = -17
-XS_TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
-_XS_CFGS = ((0, 2, 1), (1, 2, 1), (1, 3, 1), (2, 2, 1), (2, 3, 1), (3, 2, 1), (3, 3, 1), (0, 2, 2), (1, 2, 2),
-            (2, 2, 2), (3, 2, 2))
-WINO4_PTS_CFGS = tuple((WINO4_PTS, 4 * t + n, s) for t, n, s in _XS_CFGS) if USE_X6P else ()
 
 
 def x6p_split(src: torch.Tensor, out=None) -> torch.Tensor:
@@ -814,21 +790,6 @@ def x6p_splits(K: int, s: int) -> int:
     nk = K // 32
     per = cdiv(nk, max(1, s))
     return cdiv(nk, per)
-
-
-def x6s_gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, M: int, N: int, K: int, *, groups: int = 1,
-             tile: int = 3, nst: int = 2, accumulate: bool = False, splits: int = 1,
-             row_major_groups: bool = False) -> torch.Tensor:
-    """out[g] (+)= A[g] . B[g]^T with fp32 operands A [G][M][K], B [G][N][K] (contiguous) split into bf16
-    hi / mid / lo once per element inside the workgroup (x6s, fp32-accurate); out as x6p_gemm."""
-    _check(A, 'x6s A')
-    _check(B, 'x6s B')
-    assert A.numel() == groups * M * K and B.numel() == groups * N * K
-    assert out.numel() == splits * groups * M * N and not (accumulate and splits > 1)
-    ldc, gsc = (groups * N, N) if row_major_groups else (N, M * N)
-    _lib.call("rk_x6s_gemm", int(tile), int(nst), _p(A), _p(B), _p(out), M, N, K, K, K, ldc, M * K, N * K, gsc,
-              int(groups), int(bool(accumulate)), int(splits), groups * M * N, _nbytes(A), _nbytes(B), _s())
-    return out
 
 
 def wino4_ptx_ok(H, W, C, N):

@@ -67,12 +67,7 @@ def phases(tile, M, N, sp):
             'span_cycles': float(span), 'concurrency': float(life.sum() / max(1.0, span))}
 
 
-X6S = os.environ.get('X6S') == '1'   # the fp32-operand in-workgroup split GEMM (x6s) on the same shapes
-
-
 def gemm(a, b, out, M, N, K, tile, nst, sp):
-    if X6S:
-        return S.x6s_gemm(a, b, out, M, N, K, groups=36, tile=tile, nst=nst, splits=sp)
     if not SHARED:
         return S.x6p_gemm(a, b, out, M, N, K, groups=36, tile=tile, nst=nst, splits=sp)
     _lib.call("rk_x6p_gemm", tile, nst, a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, K, K, N, M * K, N * K,
@@ -82,18 +77,13 @@ def gemm(a, b, out, M, N, K, tile, nst, sp):
 if os.environ.get('X6P_SHAPES'):
     SHAPES = [x for x in SHAPES if x[0] in os.environ['X6P_SHAPES'].split(',')]
 for name, M, N, K in SHAPES:
-    if X6S:
-        a = torch.randn(36, M, K, device='cuda')
-        b = torch.randn(36, N, K, device='cuda')
-    else:
-        a = torch.randn(1 if SHARED else 36, 3, M, K, device='cuda').to(torch.bfloat16)
-        b = torch.randn(1 if SHARED else 36, 3, N, K, device='cuda').to(torch.bfloat16)
+    a = torch.randn(1 if SHARED else 36, 3, M, K, device='cuda').to(torch.bfloat16)
+    b = torch.randn(1 if SHARED else 36, 3, N, K, device='cuda').to(torch.bfloat16)
     out = torch.empty(4, 36, M, N, device='cuda')
     fl = 2.0 * 36 * M * N * K
-    r = dict(name=name, M=M, N=N, K=K, shared=SHARED, x6s=X6S, dbg=os.environ.get('RAFIKI_X6P_DBG', '0'))
+    r = dict(name=name, M=M, N=N, K=K, shared=SHARED, dbg=os.environ.get('RAFIKI_X6P_DBG', '0'))
     times = {}
-    cfgs = list(S._XS_CFGS) if X6S else [(t + kt, n, sp) for (t, n, sp) in S._XP_CFGS for kt in (0, 16)
-                                         if not (kt and K % 64)]
+    cfgs = [(t + kt, n, sp) for (t, n, sp) in S._XP_CFGS for kt in (0, 16) if not (kt and K % 64)]
     if os.environ.get('X6P_CFGS'):   # e.g. "3,2,1;16,3,1" (timing-diagnostic runs: RAFIKI_X6P_DBG)
         cfgs = [tuple(int(v) for v in c.split(',')) for c in os.environ['X6P_CFGS'].split(';')]
     for (tile, nst, sp) in cfgs:

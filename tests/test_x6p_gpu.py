@@ -188,58 +188,3 @@ def test_conv_fwd_tuner_offers_and_runs_plane_path():
         y = torch.full_like(ref, float('nan'))
         S.wino4_conv_pt(x, up, out=y, tile=cfg[1] // 4, nst=cfg[1] % 4, splits=cfg[2])
         assert rel(y, ref) < TOL, cfg
-
-
-@pytest.mark.parametrize("G,M,N,K", [(1, 256, 256, 256), (3, 100, 72, 64), (4, 256, 512, 512), (2, 33, 130, 96),
-                                     (5, 1, 64, 32)])
-@pytest.mark.parametrize("tile,nst", [(0, 2), (1, 2), (1, 3), (2, 2), (2, 3), (3, 2), (3, 3)])
-def test_x6s_gemm_vs_fp64(G, M, N, K, tile, nst):
-    """x6s: fp32 operands split into bf16 hi / mid / lo once per element inside the workgroup."""
-    from rafiki_amd.ops import f32 as S
-    a = _rand(G, M, K, seed=60 + tile)
-    b = _rand(G, N, K, seed=70 + nst)
-    out = torch.full((G, M, N), float('nan'), device=DEV)
-    S.x6s_gemm(a.to(DEV).contiguous(), b.to(DEV).contiguous(), out, M, N, K, groups=G, tile=tile, nst=nst)
-    prev = _rand(G, M, N, seed=31).to(DEV)
-    acc = prev.clone()
-    S.x6s_gemm(a.to(DEV).contiguous(), b.to(DEV).contiguous(), acc, M, N, K, groups=G, tile=tile, nst=nst,
-               accumulate=True)
-    torch.cuda.synchronize()
-    ref = torch.einsum('gmk,gnk->gmn', a.double(), b.double())
-    assert rel(out, ref) < 2e-6
-    assert rel(acc, ref + prev.double().cpu()) < 2e-6
-
-
-@pytest.mark.parametrize("splits", [2, 4])
-@pytest.mark.parametrize("tile", [0, 3])
-def test_x6s_gemm_split_k_row_major_groups(splits, tile):
-    from rafiki_amd.ops import f32 as S
-    G, M, N, K = 3, 96, 160, 256
-    a = _rand(G, M, K, seed=5)
-    b = _rand(G, N, K, seed=6)
-    s = S.x6p_splits(K, splits)
-    out = torch.full((s, M, G, N), float('nan'), device=DEV)
-    S.x6s_gemm(a.to(DEV).contiguous(), b.to(DEV).contiguous(), out, M, N, K, groups=G, tile=tile, nst=2, splits=s,
-               row_major_groups=True)
-    torch.cuda.synchronize()
-    ref = torch.einsum('gmk,gnk->mgn', a.double(), b.double())
-    assert rel(out.sum(0), ref) < 2e-6
-
-
-@pytest.mark.parametrize("N,H,W,Cin,Cout", [(8, 4, 4, 512, 512), (3, 8, 8, 256, 96), (16, 8, 8, 64, 128)])
-@pytest.mark.parametrize("tile,nst,splits", [(3, 2, 1), (1, 3, 1), (0, 2, 2)])
-def test_wino4_conv_pt_x6s_fwd_stats_bias_relu(N, H, W, Cin, Cout, tile, nst, splits):
-    from rafiki_amd.ops import f32 as S
-    x = _rand(N, H, W, Cin, seed=80)
-    w = _rand(Cout, 3, 3, Cin, seed=81, scale=1.0 / math.sqrt(9 * Cin))
-    u = S.wino4_u(_w2(w).to(DEV))
-    acc = torch.zeros((S.bn_slots(Cout), 2, Cout), dtype=torch.float64, device=DEV)
-    y = S.wino4_conv_pt(x.to(DEV), u, stats=acc, tile=tile, nst=nst, splits=splits, gemm='x6s')
-    b = _rand(Cout, seed=82)
-    yb = S.wino4_conv_pt(x.to(DEV), u, bias=b.to(DEV), relu=True, tile=tile, nst=nst, splits=splits, gemm='x6s')
-    torch.cuda.synchronize()
-    ref = TF.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
-    assert rel(y, ref) < TOL
-    assert rel(yb, (ref + b.double()).clamp_min(0)) < TOL
-    st = acc.sum(0).cpu()
-    assert rel(st[0], ref.sum((0, 1, 2))) < 1e-5
