@@ -659,3 +659,124 @@ extern "C" int rk_lrelu_gate_colsum_f32(const float* gy, const float* y, float* 
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
+
+// ------------------------------------------------------------------------------ WGAN-GP loss head
+// The D loss of _D_wgangp_acgan (pg_gans.py:1291-1315) without labels, per sample r < mb:
+//   loss_r = fake_r - real_r + lam (|g_r| - t)^2 + eps real_r^2
+// with real_r / fake_r = column 0 of the discriminator's raw output rows r / mb + r (ld floats apart) and
+// g_r the penalty gradient row (P floats); the G loss (pg_gans.py:1276-1289) is loss_r = -s_r (P = 0).
+// Two launches forward (one block per sample row: norm + per-row terms into rows[4][mb]; one block: the
+// four means in a fixed order -> loss, acc += means) and one backward replace the ~30 small PyTorch
+// kernels of the composed loss (slices, sub, lerp-free penalty chain, addcmul, mean and their backward).
+namespace {
+
+RK_DEV float block_sum256(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();   // red may still be read by a previous call
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void wgan_rows_kernel(const float* __restrict__ s, int ld, int mb,
+                                                        const float* __restrict__ g, int P, float lam, float target,
+                                                        float eps, float* __restrict__ rows) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  float ss = 0.f;
+  if (P > 0) {
+    const float* gr = g + (long long)r * P;
+    if ((P & 3) == 0) {
+      for (int i = threadIdx.x; i < P / 4; i += 256) {
+        const f32x4 v = *(const f32x4*)(gr + 4 * i);
+        ss += (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+      }
+    } else {
+      for (int i = threadIdx.x; i < P; i += 256) ss += gr[i] * gr[i];
+    }
+  }
+  ss = block_sum256(ss, red);
+  if (threadIdx.x == 0) {
+    float loss, real = 0.f, fake = 0.f, n = 0.f;
+    if (P > 0) {
+      real = s[(long long)r * ld];
+      fake = s[(long long)(mb + r) * ld];
+      n = sqrtf(ss);
+      const float d = n - target;
+      loss = (fake - real) + lam * d * d + eps * real * real;
+    } else {
+      loss = -s[(long long)r * ld];
+    }
+    rows[r] = loss;
+    rows[mb + r] = real;
+    rows[2 * mb + r] = fake;
+    rows[3 * mb + r] = n;
+  }
+}
+
+__global__ __launch_bounds__(256) void wgan_final_kernel(const float* __restrict__ rows, int mb, int nstat,
+                                                         float* __restrict__ loss, float* __restrict__ acc) {
+  __shared__ float red[4];
+  for (int k = 0; k < nstat; ++k) {
+    float a = 0.f;
+    for (int i = threadIdx.x; i < mb; i += 256) a += rows[k * mb + i];
+    a = block_sum256(a, red) / (float)mb;
+    if (threadIdx.x == 0) {
+      if (k == 0) *loss = a;
+      if (acc) acc[k] += a;
+    }
+  }
+}
+
+// ds: d loss / d s over the whole raw output (zeros off column 0); dg = go lam 2 (n - t) / n / mb * g
+__global__ __launch_bounds__(256) void wgan_bwd_kernel(const float* __restrict__ gl, const float* __restrict__ s,
+                                                       int ld, int mb, const float* __restrict__ g, int P, float lam,
+                                                       float target, float eps, const float* __restrict__ rows,
+                                                       float* __restrict__ ds, float* __restrict__ dg) {
+  const int r = blockIdx.x;
+  const float go = *gl / (float)mb;
+  if (P > 0) {
+    const float n = rows[3 * mb + r];
+    const float c = go * lam * 2.f * (n - target) / fmaxf(n, 1e-30f);
+    const float* gr = g + (long long)r * P;
+    float* dr = dg + (long long)r * P;
+    if ((P & 3) == 0) {
+      for (int i = threadIdx.x; i < P / 4; i += 256) *(f32x4*)(dr + 4 * i) = *(const f32x4*)(gr + 4 * i) * c;
+    } else {
+      for (int i = threadIdx.x; i < P; i += 256) dr[i] = gr[i] * c;
+    }
+    for (int j = threadIdx.x; j < ld; j += 256) {
+      const float real = s[(long long)r * ld];
+      ds[(long long)r * ld + j] = j == 0 ? go * (2.f * eps * real - 1.f) : 0.f;
+      ds[(long long)(mb + r) * ld + j] = j == 0 ? go : 0.f;
+    }
+  } else {
+    for (int j = threadIdx.x; j < ld; j += 256) ds[(long long)r * ld + j] = j == 0 ? -go : 0.f;
+  }
+}
+
+}  // namespace
+
+// P > 0: D loss (s has 2 mb rows: reals then fakes; g [mb][P]); P == 0: G loss (s has mb rows).
+// rows: scratch [4][mb]; acc (optional): += the means (loss, real, fake, |g|) (nstat = 4) or loss (1).
+extern "C" int rk_wgan_loss_fwd(const float* s, int ld, int mb, const float* g, int P, float lam, float target,
+                                float eps, float* rows, float* loss, float* acc, void* stream) {
+  if (mb <= 0 || ld <= 0 || P < 0 || (P > 0 && !g) || !rows || !loss) return RK_EBADARG;
+  hipLaunchKernelGGL(wgan_rows_kernel, dim3(mb), dim3(256), 0, (hipStream_t)stream, s, ld, mb, g, P, lam, target, eps,
+                     rows);
+  RK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(wgan_final_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, rows, mb, P > 0 ? 4 : 1, loss,
+                     acc);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_wgan_loss_bwd(const float* gl, const float* s, int ld, int mb, const float* g, int P, float lam,
+                                float target, float eps, const float* rows, float* ds, float* dg, void* stream) {
+  if (mb <= 0 || ld <= 0 || P < 0 || (P > 0 && (!g || !dg)) || !ds || !gl) return RK_EBADARG;
+  hipLaunchKernelGGL(wgan_bwd_kernel, dim3(mb), dim3(256), 0, (hipStream_t)stream, gl, s, ld, mb, g, P, lam, target,
+                     eps, rows, ds, dg);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}

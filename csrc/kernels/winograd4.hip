@@ -32,7 +32,7 @@ namespace {
 #include "wino_wt.h"
 
 constexpr int KC = 8;     // input channels per K chunk
-enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_BNB = 512, WF_BNP = 1024 };
+enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_LRELU = 8, WF_BNB = 512, WF_BNP = 1024 };
 
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
@@ -1428,7 +1428,7 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
                                                             const float* __restrict__ bp, double* stats, int slotMask,
                                                             const float* __restrict__ gate, int Nb, int H, int W,
                                                             int N, int TW, int THW, int T, int flags, int nslab,
-                                                            long long slab, long long qs, long long ts) {
+                                                            long long slab, long long qs, long long ts, float slope) {
   constexpr int TPB = 4;                   // tiles per block: one per 64-thread group (>= 2 blocks per CU
                                            // on the 4x4 x 512 maps: T x N / 256 blocks)
   __shared__ float red[2][4][64];
@@ -1473,6 +1473,7 @@ __global__ __launch_bounds__(256) void w4pt_conv_out_kernel(const float* __restr
           ss += v * v;
         }
         if (flags & WF_RELU) v = fmaxf(v, 0.f);
+        if (flags & WF_LRELU) v = v > 0.f ? v : v * slope;
         if (flags & WF_BNB) {
           const float g = gate[idx];
           v = g * bs + sh > 0.f ? v : 0.f;
@@ -1521,7 +1522,8 @@ __global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restr
                                                             const float* __restrict__ bp, double* stats, int slotMask,
                                                             const float* __restrict__ gate, int Nb, int H, int W,
                                                             int N, int TW, int THW, int T, int flags, int nslab,
-                                                            long long slab, long long qs, long long ts) {
+                                                            long long slab, long long qs, long long ts,
+                                                            float slope) {
   constexpr int LPT = 64 / VW, TPB = 64 / LPT;   // lanes per tile, tiles per block
   typedef __attribute__((ext_vector_type(VW))) float fv;
   __shared__ float red[2][TPB][64];
@@ -1579,6 +1581,10 @@ __global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restr
 #pragma unroll
           for (int e = 0; e < VW; ++e) v[e] = fmaxf(v[e], 0.f);
         }
+        if (flags & WF_LRELU) {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * slope;
+        }
         if (flags & WF_BNB) {
           const fv g = *(const fv*)(gate + idx);
 #pragma unroll
@@ -1635,12 +1641,14 @@ __global__ __launch_bounds__(64) void w4pt_conv_outv_kernel(const float* __restr
 }  // namespace
 
 // yt: nslab slabs of [36][T][N], slab floats apart (split-K partial sums of the GEMM), summed here
+// slope: the leaky-ReLU slope of WF_LRELU (bias, then max(v, slope v); no statistics with it)
 // tmajor: Y' is tile-major [T][36][N] (the plane GEMM writes it so: each tile's 36 positions in one 36N-float
 // run instead of 36 runs a T x N plane apart), else position-major [36][T][N]
 extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias, double* stats, int slotMask,
                                     const float* gate, int Nb, int H, int W, int N, int flags, int nslab,
-                                    long long slab, int tmajor, void* stream) {
+                                    long long slab, int tmajor, float slope, void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || N <= 0 || nslab <= 0) return RK_EBADARG;
+  if ((flags & WF_LRELU) && (flags & (WF_RELU | WF_STATS | WF_BNB | WF_BNP))) return RK_EBADARG;
   if ((flags & (WF_STATS | WF_BNB | WF_BNP)) && !stats) return RK_EBADARG;
   if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
   if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
@@ -1657,15 +1665,15 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
     const long long blocksv = ((N + 63) / 64) * ((T + tpb - 1) / tpb);
     if (vw == 4)
       hipLaunchKernelGGL(w4pt_conv_outv_kernel<4>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
-                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts);
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
     else
       hipLaunchKernelGGL(w4pt_conv_outv_kernel<2>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
-                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts);
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
     RK_LAUNCH_CHECK();
     return RK_OK;
   }
   hipLaunchKernelGGL(w4pt_conv_out_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, yt, y, bias,
-                     stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts);
+                     stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

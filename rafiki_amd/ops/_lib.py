@@ -78,7 +78,7 @@ _SIGS = {
     "rk_wino4_pt_transform": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "rk_wino4_pt_output": [vp, vp, i32, i32, i32, i32, i64, vp],
     "rk_wino4_pt_input": [vp, vp, i32, i32, i32, i32, vp],
-    "rk_wino4_pt_conv_out": [vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, i32, vp],
+    "rk_wino4_pt_conv_out": [vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, i32, f32, vp],
     "rk_wino2s_conv_grp": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, vp],
     # fp32 path (sgemm.hip, bnf.hip)
     "rk_sgemm": [i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
@@ -91,6 +91,8 @@ _SIGS = {
     "rk_colsum_f32": [vp, i32, i32, i32, vp, i32, i32, vp],
     "rk_lrelu_gate_f32": [vp, vp, vp, i64, f32, vp],
     "rk_lrelu_gate_colsum_f32": [vp, vp, vp, i32, i32, f32, vp, i32, vp],
+    "rk_wgan_loss_fwd": [vp, i32, i32, vp, i32, f32, f32, f32, vp, vp, vp, vp],
+    "rk_wgan_loss_bwd": [vp, vp, i32, i32, vp, i32, f32, f32, f32, vp, vp, vp, vp],
     "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, i32, vp],
     "rk_sgemm_grp": [i32, i32, i32, vp, vp, vp, vp] + [i32] * 10 + [i32, i64, i32, f32, f32, i64, i64, i32, i64, i64,
                                                                      i64, i64, vp],

@@ -27,7 +27,6 @@ from __future__ import annotations
 
 import contextlib
 import os
-import threading
 from typing import Optional
 
 import torch
@@ -128,36 +127,65 @@ def sumpool2(x):
 
 
 # ------------------------------------------------------------------------------------- conv
-_direct = threading.local()
-
-
 @contextlib.contextmanager
-def accumulate_weight_grads_in_place():
-    """Within this context a plain ``loss.backward()`` (no create_graph) accumulates fp32 conv / dense
-    weight gradients straight into each leaf's persistent ``.grad`` buffer (the flat gradient arena)
-    and returns None for the weight, skipping autograd's AccumulateGrad add — one weight-sized
-    read-modify-write per use, and a weight is used several times per WGAN-GP step (real/fake, mixed,
-    the penalty's double backward).  Only for ``.backward()`` into ``.grad`` (not autograd.grad)."""
-    prev = getattr(_direct, 'on', False)
-    _direct.on = True
+def accumulate_weight_grads_in_place(params):
+    """Within this context a plain ``loss.backward()`` (no create_graph) accumulates the fp32 conv / dense
+    weight and bias gradients of the leaves in ``params`` straight into each leaf's persistent ``.grad``
+    buffer (the flat gradient arena) and returns None for them, skipping autograd's gradient sums and
+    AccumulateGrad adds — a parameter is used several times per WGAN-GP step (real/fake, mixed, the
+    penalty's double backward).  Only for ``.backward()`` into ``.grad`` (not autograd.grad).
+
+    The opt-in is a mark on the leaves themselves, not thread-local state: autograd runs a CUDA
+    backward on its own device thread, which never sees the caller's thread-locals."""
+    leaves = [p for p in params if isinstance(p, torch.Tensor)]
+    prev = [getattr(p, '_rk_direct', False) for p in leaves]
+    for p in leaves:
+        p._rk_direct = True
     try:
         yield
     finally:
-        _direct.on = prev
+        for p, v in zip(leaves, prev):
+            p._rk_direct = v
 
 
 def _param_grad_buffer(w):
-    """The persistent fp32 gradient buffer of a weight (the leaf's .grad, or the viewed leaf's, in the
-    weight's shape), inside ``accumulate_weight_grads_in_place`` and outside a create_graph backward."""
-    if not getattr(_direct, 'on', False) or torch.is_grad_enabled() or w.dtype != F32 or not w.is_cuda:
+    """The persistent fp32 gradient buffer of a parameter (the leaf's .grad, or the viewed leaf's, in
+    the parameter's shape), for a leaf marked by ``accumulate_weight_grads_in_place`` and outside a
+    create_graph backward; None otherwise (the caller returns the gradient to autograd)."""
+    if w is None or torch.is_grad_enabled() or w.dtype != F32 or not w.is_cuda:
         return None
     leaf = w if w.is_leaf else getattr(w, '_base', None)
-    if leaf is None or not leaf.is_leaf or not leaf.requires_grad:
+    if leaf is None or not leaf.is_leaf or not leaf.requires_grad or not getattr(leaf, '_rk_direct', False):
         return None
     g = leaf.grad
     if g is None or g.dtype != F32 or not g.is_contiguous() or g.numel() != w.numel() or leaf.numel() != w.numel():
         return None
+    # a reinterpreting view only (reshape of the whole contiguous leaf), never a transpose
+    if not (w.is_contiguous() and leaf.is_contiguous() and w.data_ptr() == leaf.data_ptr()):
+        return None
     return g.view(w.shape)
+
+
+def _bias_grad_into(gy, b):
+    """Bias gradient of ``gy`` for parameter ``b``: accumulated in place into b's .grad buffer when
+    ``_param_grad_buffer`` allows it (returns None), else returned for autograd."""
+    buf = _param_grad_buffer(b)
+    if buf is not None and gy.dtype in (F32, BF16) and gy.is_cuda:
+        Cc = gy.shape[-1]
+        g2 = gy.contiguous().reshape(-1, Cc)
+        (S.colsum if gy.dtype == F32 else F.colsum)(g2, buf, accumulate=True)
+        return None
+    return _bias_grad(gy)
+
+
+def _gate_colsum(ctx, gy, y, b):
+    """(gated gy, bias gradient or None): the leaky-ReLU gate and the bias column sum in one pass over
+    gy (outside a create_graph backward); the sum goes straight into b's .grad when allowed."""
+    buf = _param_grad_buffer(b)
+    if buf is not None:
+        g, _ = S.lrelu_gate_colsum(gy, y.contiguous(), float(ctx.slope), acc=buf)
+        return g, None
+    return S.lrelu_gate_colsum(gy, y.contiguous(), float(ctx.slope))
 
 
 class LReluGateFn(torch.autograd.Function):
@@ -198,7 +226,8 @@ class ConvFn(torch.autograd.Function):
             # 3x3: the fused Winograd kernels (weights transformed inside the candidate) compete in the tuner
             y = S.conv_fwd(x, wd, taps=taps, bias=bd, act=_act(slope), slope=0.2 if slope is None else slope,
                            wino=(lambda: S.wino_u(wd)) if taps == 9 else None,
-                           wino4=(lambda: S.wino4_u(wd)) if taps == 9 else None)
+                           wino4=(lambda: S.wino4_u(wd)) if taps == 9 else None,
+                           wino4p=(lambda: S.wino4_u4p(wd)) if taps == 9 else None)
         else:
             y = F.conv_fwd(x, _wshadow(w, wb), taps=taps, bias=bd, act=_act(slope),
                            slope=0.2 if slope is None else slope)
@@ -208,18 +237,20 @@ class ConvFn(torch.autograd.Function):
         else:
             ctx.save_for_backward(x, w, y)
         ctx.wb, ctx.taps, ctx.has_b, ctx.slope = wb, taps, b is not None, slope
+        ctx.b = b   # the bias leaf: its .grad takes the bias gradient in place (_param_grad_buffer)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors[:2]
-        gb = None
+        gb, b_done = None, False
         if ctx.slope is not None:
             y = ctx.saved_tensors[2]
             if (ctx.has_b and _needed(ctx, 2) and not torch.is_grad_enabled() and gy.is_cuda
                     and gy.dtype == F32 and y.dtype == F32 and gy.is_contiguous()):
                 # outside a create_graph backward: gate + bias gradient in one pass over gy
-                gy, gb = S.lrelu_gate_colsum(gy, y.contiguous(), float(ctx.slope))
+                gy, gb = _gate_colsum(ctx, gy, y, ctx.b)
+                b_done = True
             else:
                 gy = _lrelu_gate(gy, y, ctx.slope)
         gy = _as(gy, ctx.dt)
@@ -233,8 +264,8 @@ class ConvFn(torch.autograd.Function):
                              accumulate=True)
             else:
                 gw = ConvWgradFn.apply(x, gy, ctx.taps)
-        if ctx.has_b and _needed(ctx, 2) and gb is None:
-            gb = _bias_grad(gy)
+        if ctx.has_b and _needed(ctx, 2) and not b_done:
+            gb = _bias_grad_into(gy, ctx.b)
         return gx, gw, gb, None, None, None
 
 
@@ -248,7 +279,8 @@ class ConvDgradFn(torch.autograd.Function):
             wd = w.detach().contiguous()
             dx = S.conv_dgrad(gy, lambda: S.conv_wt(wd, taps), taps=taps, cin=wd.numel() // (taps * wd.shape[0]),
                               wino=(lambda: S.wino_ut(wd)) if taps == 9 else None,
-                              wino4=(lambda: S.wino4_ut(wd)) if taps == 9 else None)
+                              wino4=(lambda: S.wino4_ut(wd)) if taps == 9 else None,
+                              wino4p=(lambda: S.wino4_u4p(wd, dgrad=True)) if taps == 9 else None)
         else:
             dx = F.conv_dgrad(gy, _wshadow(w, wb), taps=taps)
         ctx.save_for_backward(gy, w)
@@ -448,7 +480,7 @@ class S2Fn(torch.autograd.Function):
         y = S.s2_conv(x, W.detach().contiguous(), bias=None if b is None else b.detach().float().contiguous(),
                       act=_act(slope), slope=0.2 if slope is None else slope)
         ctx.save_for_backward(*((x, W) if slope is None else (x, W, y)))
-        ctx.has_b, ctx.slope = b is not None, slope
+        ctx.has_b, ctx.slope, ctx.b = b is not None, slope, b
         return y
 
     @staticmethod
@@ -463,7 +495,7 @@ class S2Fn(torch.autograd.Function):
         if _needed(ctx, 1):
             gW = S2WFn.apply(x, gy)
         if ctx.has_b and _needed(ctx, 2):
-            gb = _bias_grad(gy)
+            gb = _bias_grad_into(gy, ctx.b)
         return gx, gW, gb, None
 
 
@@ -475,7 +507,7 @@ class S2TFn(torch.autograd.Function):
         y = S.s2t_conv(z, W.detach().contiguous(), bias=None if b is None else b.detach().float().contiguous(),
                        act=_act(slope), slope=0.2 if slope is None else slope)
         ctx.save_for_backward(*((z, W) if slope is None else (z, W, y)))
-        ctx.has_b, ctx.slope = b is not None, slope
+        ctx.has_b, ctx.slope, ctx.b = b is not None, slope, b
         return y
 
     @staticmethod
@@ -490,7 +522,7 @@ class S2TFn(torch.autograd.Function):
         if _needed(ctx, 1):
             gW = S2WFn.apply(gy, z)
         if ctx.has_b and _needed(ctx, 2):
-            gb = _bias_grad(gy)
+            gb = _bias_grad_into(gy, ctx.b)
         return gz, gW, gb, None
 
 
@@ -559,19 +591,20 @@ class DenseFn(torch.autograd.Function):
             ctx.save_for_backward(x, w)
         else:
             ctx.save_for_backward(x, w, y)
-        ctx.wb, ctx.has_b, ctx.slope = wb, b is not None, slope
+        ctx.wb, ctx.has_b, ctx.slope, ctx.b = wb, b is not None, slope, b
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors[:2]
-        gb = None
+        gb, b_done = None, False
         if ctx.slope is not None:
             y = ctx.saved_tensors[2]
             if (ctx.has_b and _needed(ctx, 2) and not torch.is_grad_enabled() and gy.is_cuda
                     and gy.dtype == F32 and y.dtype == F32 and gy.is_contiguous()):
                 # outside a create_graph backward: gate + bias gradient in one pass over gy
-                gy, gb = S.lrelu_gate_colsum(gy, y.contiguous(), float(ctx.slope))
+                gy, gb = _gate_colsum(ctx, gy, y, ctx.b)
+                b_done = True
             else:
                 gy = _lrelu_gate(gy, y, ctx.slope)
         gy = _as(gy, ctx.dt)
@@ -584,8 +617,8 @@ class DenseFn(torch.autograd.Function):
                 S.linear_dw(gy.contiguous(), x.contiguous(), out=buf, accumulate=True)
             else:
                 gw = DenseDwFn.apply(x, gy)
-        if ctx.has_b and _needed(ctx, 2) and gb is None:
-            gb = _bias_grad(gy)
+        if ctx.has_b and _needed(ctx, 2) and not b_done:
+            gb = _bias_grad_into(gy, ctx.b)
         return gx, gw, gb, None, None
 
 
@@ -667,7 +700,7 @@ class LReluPixelNormFn(torch.autograd.Function):
         bd = None if b is None else b.detach().float().contiguous()
         z = F.lrelu_pixelnorm(x, bd, slope=slope, eps=eps)
         ctx.save_for_backward(x)
-        ctx.bd, ctx.slope, ctx.eps, ctx.has_b = bd, slope, eps, b is not None
+        ctx.bd, ctx.slope, ctx.eps, ctx.has_b, ctx.b = bd, slope, eps, b is not None, b
         return z
 
     @staticmethod
@@ -677,7 +710,7 @@ class LReluPixelNormFn(torch.autograd.Function):
         gx = F.lrelu_pixelnorm(x, ctx.bd, slope=ctx.slope, eps=ctx.eps, dz=gz)
         gb = None
         if ctx.has_b and ctx.needs_input_grad[1]:
-            gb = _bias_grad(gx)
+            gb = _bias_grad_into(gx, ctx.b)
         return (gx if ctx.needs_input_grad[0] else None), gb, None, None
 
 

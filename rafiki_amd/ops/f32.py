@@ -182,19 +182,21 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
 
     use_w = wino is not None and taps == 9 and wino_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
-
-    use_pt = use_w4 and wino4_pt_ok(H, W, Cin, Cout)
-    use_ptx = (wino4p is not None and taps == 9 and wino4_ptx_ok(H, W, Cin, Cout) and act in (ACT_NONE, ACT_RELU))
+    # the pre-transformed paths also carry a leaky-ReLU epilogue (no statistics with it): PG-GAN's D convs
+    act_pt = act in (ACT_NONE, ACT_RELU) or (act == ACT_LRELU and stats_acc is None)
+    use_pt = (wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act_pt and wino4_pt_ok(H, W, Cin, Cout))
+    use_ptx = wino4p is not None and taps == 9 and wino4_ptx_ok(H, W, Cin, Cout) and act_pt
+    lrelu = slope if act == ACT_LRELU else None
 
     def run(cfg):
         tile, nst, s = cfg
         if tile == WINO4_PTX:
             wino4_conv_pt(x, wino4p() if callable(wino4p) else wino4p, out=out, bias=bias, stats=stats_acc,
-                          relu=act == ACT_RELU, tile=nst // 4, nst=nst % 4, splits=s)
+                          relu=act == ACT_RELU, tile=nst // 4, nst=nst % 4, splits=s, lrelu=lrelu)
             return
         if tile == WINO4_PT:
             wino4_conv_pt(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
-                          relu=act == ACT_RELU, tile=nst, nst=s)
+                          relu=act == ACT_RELU, tile=nst, nst=s, lrelu=lrelu)
             return
         if cfg in WINO4_CFGS:
             wino4_conv(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
@@ -399,7 +401,7 @@ class SConvWT:
 
 
 # -------------------------------------------------------------------- Winograd F(2x2, 3x3) convs
-WF_RELU, WF_BIAS, WF_STATS, WF_BNB, WF_BNP = 1, 2, 4, 512, 1024
+WF_RELU, WF_BIAS, WF_STATS, WF_LRELU, WF_BNB, WF_BNP = 1, 2, 4, 8, 512, 1024
 WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
 # autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1),
 # and the 16x16-wave-tile kernels of winograd4.hip: 4-wave 32x32 (variant 2), 2-wave 16x32 (variant 3),
@@ -465,6 +467,9 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
         flags |= WF_BIAS
     if relu:
         flags |= WF_RELU
+    if lrelu is not None:
+        assert not relu and stats is None and bnb is None and bnp is None
+        flags |= WF_LRELU
     if stats is not None:
         flags |= WF_STATS
     if bnb is not None:
@@ -536,6 +541,9 @@ def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=N
         flags |= WF_BIAS
     if relu:
         flags |= WF_RELU
+    if lrelu is not None:
+        assert not relu and stats is None and bnb is None and bnp is None
+        flags |= WF_LRELU
     if stats is not None:
         flags |= WF_STATS
     if bnb is not None:
@@ -576,9 +584,10 @@ WINO4_PT_CFGS = tuple((WINO4_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)
 
 
 def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None,
-                  bnp=None, tile=0, nst=2, splits=1):
+                  bnp=None, tile=0, nst=2, splits=1, lrelu=None):
     """wino4_conv through position-major buffers: V = B^T x B [36][T][C] (one launch), Y'[q] = V[q] u[q]^T
-    as one 36-group sgemm, then A^T Y' A with the same epilogues (bias / ReLU / BN statistics / BNB / BNP).
+    as one 36-group sgemm, then A^T Y' A with the same epilogues (bias / ReLU / BN statistics / BNB / BNP;
+    ``lrelu`` = slope: bias + leaky ReLU, the PG-GAN discriminator's conv epilogue).
     With bf16 X6 planes u [36][3][N][C] (WinoWeights 'u4p' / 'ut4p') the input transform writes V as planes
     too and the GEMM is the pre-split X6 one (x6p_gemm; ``tile`` / ``nst`` are its configs)."""
     _check(x, 'wino4_conv_pt x')
@@ -595,6 +604,9 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
         flags |= WF_BIAS
     if relu:
         flags |= WF_RELU
+    if lrelu is not None:
+        assert not relu and stats is None and bnb is None and bnp is None
+        flags |= WF_LRELU
     if stats is not None:
         flags |= WF_STATS
     if bnb is not None:
@@ -622,7 +634,7 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
         _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
         sgemm_grp(KIND_DENSE, v, u, yt, T, N, C, C, C, N, 36, T * C, N * C, T * N, tile=tile, nst=nst)
     _lib.call("rk_wino4_pt_conv_out", _p(yt), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
-              Nb, H, W, N, flags, splits, 36 * T * N, int(planes), _s())
+              Nb, H, W, N, flags, splits, 36 * T * N, int(planes), float(0.0 if lrelu is None else lrelu), _s())
     return out
 
 
@@ -790,6 +802,16 @@ def x6p_splits(K: int, s: int) -> int:
     nk = K // 32
     per = cdiv(nk, max(1, s))
     return cdiv(nk, per)
+
+
+def wino4_u4p(w: torch.Tensor, dgrad: bool = False) -> torch.Tensor:
+    """X6 planes of the F(4x4) weights of one conv weight [Cout, 3, 3, Cin] (fresh buffer): forward set
+    [36][3][Cout][Cin] (WinoWeights 'u4p'), ``dgrad``: the data-gradient set [36][3][Cin][Cout] ('ut4p')."""
+    Cout = w.shape[0]
+    Cin = w.numel() // (9 * Cout)
+    out = torch.empty((36, 3, Cin, Cout) if dgrad else (36, 3, Cout, Cin), device=w.device, dtype=torch.bfloat16)
+    _lib.call("rk_x6p_w4_weights", _p(w), None if dgrad else _p(out), _p(out) if dgrad else None, Cout, Cin, _s())
+    return out
 
 
 def wino4_ptx_ok(H, W, C, N):
@@ -1127,8 +1149,9 @@ def lrelu_gate(gy: torch.Tensor, y: torch.Tensor, slope: float, out=None):
     return out
 
 
-def lrelu_gate_colsum(gy: torch.Tensor, y: torch.Tensor, slope: float):
-    """(g, colsum(g)) with g = lrelu_gate(gy, y, slope) in one pass; gy / y [..., C] fp32."""
+def lrelu_gate_colsum(gy: torch.Tensor, y: torch.Tensor, slope: float, acc=None):
+    """(g, colsum(g)) with g = lrelu_gate(gy, y, slope) in one pass; gy / y [..., C] fp32.  ``acc`` (fp32
+    [C]): the column sum is added into it instead (returns (g, acc))."""
     _check(gy, 'lrelu_gate_colsum gy')
     _check(y, 'lrelu_gate_colsum y')
     assert gy.shape == y.shape
@@ -1138,6 +1161,9 @@ def lrelu_gate_colsum(gy: torch.Tensor, y: torch.Tensor, slope: float):
     chunks = max(1, min(cdiv(R, 256), cdiv(2 * NUM_CU, cdiv(Cc, 64))))
     part = torch.empty((chunks, Cc), device=gy.device, dtype=torch.float32)
     _lib.call("rk_lrelu_gate_colsum_f32", _p(gy), _p(y), _p(g), R, Cc, float(slope), _p(part), chunks, _s())
+    if acc is not None:
+        assert acc.shape == (Cc,) and acc.dtype == torch.float32 and acc.is_contiguous()
+        return g, reduce_slabs(part, acc, accumulate=True)
     if chunks == 1:
         return g, part[0]
     out = torch.empty(Cc, device=gy.device, dtype=torch.float32)

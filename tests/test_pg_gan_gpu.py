@@ -151,7 +151,7 @@ def test_wgan_gp_in_place_weight_grads_match_autograd(lod):
     s, _ = gnet.discriminator(P, xi, lod)
     (gr,) = torch.autograd.grad(s.sum(), xi, create_graph=True)
     pen, _ = _GradPenaltyFn.apply(gr, 10.0, 1.0)
-    with A.accumulate_weight_grads_in_place():
+    with A.accumulate_weight_grads_in_place(gnet.d_params.values()):
         torch.addcmul(pen, s.float(), s.float(), value=1e-3).mean().backward()
     torch.cuda.synchronize()
     assert frob(gnet.D.grad, ref) < 1e-5, frob(gnet.D.grad, ref)
@@ -436,8 +436,9 @@ def test_lrelu_gate_kernels_and_double_backward():
 
 
 def test_in_place_weight_grad_accumulation_matches_autograd():
-    """accumulate_weight_grads_in_place: conv / dense weight gradients written straight into the leaf's
-    .grad buffer equal autograd's accumulated ones (weight used twice, lrelu epilogues, bias)."""
+    """accumulate_weight_grads_in_place: conv / dense weight and bias gradients written straight into the
+    leaf's .grad buffer (from autograd's device thread: no AccumulateGrad runs for them) equal autograd's
+    accumulated ones (weight and bias used twice, lrelu epilogues with and without the fused column sum)."""
     from rafiki_amd.ops import autograd as A
     g = torch.Generator().manual_seed(4)
     x = torch.randn(8, 8, 8, 32, generator=g).to(DEV)
@@ -450,18 +451,24 @@ def test_in_place_weight_grad_accumulation_matches_autograd():
         wd = torch.nn.Parameter(base_d.clone())
         bb = torch.nn.Parameter(b.clone())
         w.grad, wd.grad, bb.grad = torch.zeros_like(w), torch.zeros_like(wd), torch.zeros_like(bb)
+        bd = torch.nn.Parameter(torch.zeros(16, device=DEV))
+        bd.grad = torch.zeros_like(bd)
+        hits = []
+        for p in (w, wd, bb, bd):   # AccumulateGrad runs these; the in-place path must bypass it
+            p.register_post_accumulate_grad_hook(lambda t: hits.append(t.shape))
         y1 = A.conv2d(x, w.reshape(48, -1), bb, lrelu=0.2)
-        y2 = A.conv2d(x * 0.5, w.reshape(48, -1), bb, lrelu=0.2)
-        z = A.dense((y1 + y2).reshape(8, -1), wd, None)
-        ctx = A.accumulate_weight_grads_in_place() if in_place else contextlib.nullcontext()
+        y2 = A.conv2d(x * 0.5, w.reshape(48, -1), bb)
+        z = A.dense((y1 + y2).reshape(8, -1), wd, bd, lrelu=0.2)
+        ctx = A.accumulate_weight_grads_in_place([w, wd, bb, bd]) if in_place else contextlib.nullcontext()
         with ctx:
             z.square().mean().backward()
         torch.cuda.synchronize()
-        return w.grad.clone(), wd.grad.clone(), bb.grad.clone()
+        return (w.grad.clone(), wd.grad.clone(), bb.grad.clone(), bd.grad.clone()), hits
 
     import contextlib
-    a = grads(False)
-    c = grads(True)
+    a, hits_a = grads(False)
+    c, hits_c = grads(True)
+    assert len(hits_a) == 4 and hits_c == [], (hits_a, hits_c)
     for u, v in zip(a, c):
         assert frob(v, u) < 1e-6, frob(v, u)
 
@@ -560,3 +567,38 @@ def test_box_weights_kernel_and_adjoints(co, cin):
         (gw2,) = torch.autograd.grad(fn(wd, cin), wd, gyd, create_graph=True)
         (dgy,) = torch.autograd.grad((gw2 * v.to(DEV)).sum(), gyd)
         assert _rel64(dgy, fn(v.double(), cin)) <= 1e-6
+
+
+@pytest.mark.parametrize("mb,gshape", [(512, (4, 4, 8)), (64, (32, 32, 8)), (6, (3, 3, 3))])
+def test_wgan_loss_head_vs_fp64(mb, gshape):
+    """WganLossFn (rk_wgan_loss_fwd / _bwd) == the composed WGAN-GP D loss and the G loss in fp64: the mean
+    loss, the device stat accumulation, d/ds over the raw output rows and d/dg."""
+    from rafiki_amd.models.pg_gan import WganLossFn
+    g0 = torch.Generator().manual_seed(mb)
+    s = torch.randn(2 * mb, 8, generator=g0)
+    g = torch.randn((mb,) + gshape, generator=g0) * 0.3
+    lam, t, eps = 10.0, 1.0, 1e-3
+    sd, gd = s.double().requires_grad_(True), g.double().requires_grad_(True)
+    n = gd.reshape(mb, -1).norm(dim=1)
+    per = sd[mb:, 0] - sd[:mb, 0] + lam * (n - t) ** 2 + eps * sd[:mb, 0] ** 2
+    per.mean().backward()
+    acc = torch.ones(4, device=DEV)
+    sg, gg = s.to(DEV).requires_grad_(True), g.to(DEV).requires_grad_(True)
+    loss = WganLossFn.apply(sg, gg, lam, t, eps, acc)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - per.mean().item()) < 1e-5 * max(1.0, abs(per.mean().item()))
+    stats = torch.stack([per.mean(), sd[:mb, 0].mean(), sd[mb:, 0].mean(), n.mean()]).detach() + 1
+    assert rel_err(acc.cpu(), stats.float()) < 1e-6
+    assert rel_err(sg.grad.cpu(), sd.grad.float()) < 1e-6
+    assert rel_err(gg.grad.cpu(), gd.grad.float()) < 1e-6
+    # G loss: mean(-s[:, 0])
+    accg = torch.zeros(1, device=DEV)
+    sg2 = s[:mb].to(DEV).requires_grad_(True)
+    lg = WganLossFn.apply(sg2, None, 0.0, 0.0, 0.0, accg)
+    lg.backward()
+    ref = -s[:mb, 0].double().mean()
+    assert abs(lg.item() - ref.item()) < 1e-6 and abs(accg.item() - ref.item()) < 1e-6
+    dref = torch.zeros(mb, 8)
+    dref[:, 0] = -1.0 / mb
+    assert torch.equal(sg2.grad.cpu(), dref)

@@ -188,3 +188,39 @@ def test_conv_fwd_tuner_offers_and_runs_plane_path():
         y = torch.full_like(ref, float('nan'))
         S.wino4_conv_pt(x, up, out=y, tile=cfg[1] // 4, nst=cfg[1] % 4, splits=cfg[2])
         assert rel(y, ref) < TOL, cfg
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout", [(8, 4, 520, 512), (4, 8, 256, 128), (2, 32, 64, 64)])
+def test_wino4_conv_pt_lrelu_epilogue(N, H, Cin, Cout, monkeypatch):
+    """bias + leaky-ReLU epilogue of the pre-transformed F(4x4) output transform (PG-GAN D convs): the fp32-U
+    path and, where K % 32 == 0, the X6 plane path, against fp64; and every tuner candidate of conv_fwd with
+    act = leaky ReLU (the direct GEMMs and the PT paths) agrees."""
+    from rafiki_amd.ops import f32 as S
+    x = _rand(N, H, H, Cin, seed=80)
+    w = _rand(Cout, 3, 3, Cin, seed=81, scale=1.0 / math.sqrt(9 * Cin))
+    b = _rand(Cout, seed=82)
+    ref = TF.leaky_relu(TF.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), padding=1)
+                        .permute(0, 2, 3, 1) + b.double(), 0.2)
+    xd, bd = x.to(DEV), b.to(DEV)
+    y = S.wino4_conv_pt(xd, S.wino4_u(_w2(w)), bias=bd, lrelu=0.2, tile=0, nst=2)
+    assert rel(y, ref) < TOL
+    if Cin % 32 == 0:
+        yp = S.wino4_conv_pt(xd, S.wino4_u4p(_w2(w)), bias=bd, lrelu=0.2, tile=0, nst=2)
+        assert rel(yp, ref) < TOL
+        assert rel(S.wino4_u4p(_w2(w), dgrad=True).double().sum(1), S.wino4_ut(_w2(w)).double()) < 1e-7
+    seen = {}
+
+    def grab(key, cands, run, protect=()):
+        seen['cands'], seen['run'] = list(cands), run
+        return cands[0]
+    monkeypatch.setattr(S, '_pick', grab)
+    yy = torch.full((N, H, H, Cout), float('nan'), device=DEV)
+    S.conv_fwd(xd, _w2(w), bias=bd, act=S.ACT_LRELU, slope=0.2, out=yy, wino4=lambda: S.wino4_u(_w2(w)),
+               wino4p=lambda: S.wino4_u4p(_w2(w)))
+    pt = [c for c in seen['cands'] if c[0] in (S.WINO4_PT, S.WINO4_PTX)]
+    assert any(c[0] == S.WINO4_PT for c in pt) and (Cin % 32 or any(c[0] == S.WINO4_PTX for c in pt))
+    for cfg in pt[:3] + pt[-2:] + [seen['cands'][0]]:
+        yy.fill_(float('nan'))
+        seen['run'](cfg)
+        torch.cuda.synchronize()
+        assert rel(yy, ref) < TOL, cfg
