@@ -379,7 +379,8 @@ __global__ __launch_bounds__(256) void sreduce_epi_kernel(const float* __restric
 // flags bit 0: uint8 source (else fp32), bit 1: source already NHWC (else NCHW)
 __global__ __launch_bounds__(256) void pack_nhwc_f32_kernel(const void* __restrict__ src, int flags, int N, int C,
                                                             int H, int W, int Cp, float scale, float shift,
-                                                            float* __restrict__ dst) {
+                                                            float* __restrict__ dst, const int* __restrict__ idx,
+                                                            int nsrc) {
   const bool is_u8 = flags & 1, nhwc = flags & 2;
   const long long total = (long long)N * H * W * Cp;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
@@ -391,7 +392,14 @@ __global__ __launch_bounds__(256) void pack_nhwc_f32_kernel(const void* __restri
     const long long n = t / H;
     float v = 0.f;
     if (c < C) {
-      const long long si = nhwc ? pix * C + c : ((n * C + c) * H + h) * W + w;
+      // idx: output image n is source image idx[n] (the minibatch gather folded in; out-of-range -> 0)
+      long long ns = n;
+      if (idx) {
+        ns = idx[n];
+        if ((unsigned long long)ns >= (unsigned long long)nsrc) ns = 0;
+      }
+      const long long sp = (ns * H + h) * W + w;
+      const long long si = nhwc ? sp * C + c : ((ns * C + c) * H + h) * W + w;
       v = (is_u8 ? (float)((const unsigned char*)src)[si] : ((const float*)src)[si]) * scale + shift;
     }
     dst[i] = v;
@@ -539,10 +547,12 @@ extern "C" int rk_sreduce_epi(const float* slab, int S, int M, int N, const floa
   return RK_OK;
 }
 
+// idx (optional, N int32 rows of a source holding nsrc images): out[n] = pack(src[idx[n]])
 extern "C" int rk_pack_nhwc_f32(const void* src, int flags, int N, int C, int H, int W, int Cp, float scale,
-                                float shift, float* out, void* stream) {
+                                float shift, float* out, const int* idx, int nsrc, void* stream) {
+  if (idx && nsrc <= 0) return RK_EBADARG;
   hipLaunchKernelGGL(pack_nhwc_f32_kernel, dim3(grid_cap((long long)N * H * W * Cp, 4096)), dim3(256), 0,
-                     (hipStream_t)stream, src, flags, N, C, H, W, Cp, scale, shift, out);
+                     (hipStream_t)stream, src, flags, N, C, H, W, Cp, scale, shift, out, idx, nsrc);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -136,6 +136,15 @@ __global__ __launch_bounds__(256) void lerp_kernel(float* __restrict__ dst, cons
   }
 }
 
+// dst[0 .. n) = 0 for any 4-byte element type: 16-B vector stores, a scalar tail
+__global__ __launch_bounds__(256) void zero32_kernel(unsigned* __restrict__ dst, long long n) {
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    ((uint4*)dst)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (long long i = 4 * n4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = 0u;
+}
+
 __global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ x, long long n, int* flag) {
   int bad = 0;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
@@ -416,6 +425,17 @@ extern "C" int rk_adam_step(float* w, void* wb, const float* g, float* m, float*
 extern "C" int rk_lerp(float* dst, const float* src, void* dstb, long long n, float t, void* stream) {
   hipLaunchKernelGGL(lerp_kernel, dim3(grid_for(n, 4096)), dim3(256), 0, (hipStream_t)stream, dst, src, (bf16*)dstb,
                      n, t);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// zero n 4-byte elements (16-B aligned base: a torch allocation or an offset multiple of 4 elements)
+extern "C" int rk_zero32(void* dst, long long n, void* stream) {
+  if (n < 0 || (n > 0 && !dst)) return RK_EBADARG;
+  if (n == 0) return RK_OK;
+  if (((unsigned long long)dst) & 15) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(zero32_kernel, dim3(grid_for((n + 3) / 4, 2048)), dim3(256), 0, (hipStream_t)stream,
+                     (unsigned*)dst, n);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -576,10 +576,13 @@ class PgGan(BaseModel):
     def _reals(self, level_u8, idx, frac):
         """uint8 [N, C, r, r] (device) rows idx -> NHWC [n, r, r, cpad] in [-1, 1] with LOD fade
         (pg_gans.py:347-369 process_reals: dynamic range, FadeLOD; UpscaleLOD is the identity here)."""
-        x = level_u8.index_select(0, idx)
         nets = self.nets
+        if (self.device.type == 'cuda' and frac <= 0 and nets.act_dtype == torch.float32 and level_u8.is_cuda
+                and idx.dtype == torch.int32):
+            # the minibatch gather folded into the pack kernel (no index_select pass)
+            return S.pack_nhwc(level_u8, nets.cpad, 2.0 / 255.0, -1.0, idx=idx)
+        x = level_u8.index_select(0, idx)
         if self.device.type == 'cuda' and frac <= 0:
-            from rafiki_amd.ops import f32 as S
             from rafiki_amd.ops import functional as F
             pack = S.pack_nhwc if nets.act_dtype == torch.float32 else F.pack_nhwc
             return pack(x.contiguous(), nets.cpad, 2.0 / 255.0, -1.0)
@@ -782,9 +785,9 @@ class PgGan(BaseModel):
         self._g_step(lod, mb, labels_all, rng, G_opt, g_ar, acc=acc)
 
     def _finite_guard(self, flat, opt):
-        opt.skip_flag.zero_()
         if self.device.type == 'cuda':
             from rafiki_amd.ops import functional as F
+            F.zero_(opt.skip_flag)
             F.nonfinite_flag(flat.grad, opt.skip_flag)
         else:
             opt.skip_flag.fill_(0 if bool(torch.isfinite(flat.grad).all()) else 1)
@@ -835,6 +838,13 @@ class PgGan(BaseModel):
         return (self.device.type == 'cuda' and self.nets.label_size == 0 and self.nets.act_dtype == torch.float32
                 and (grads is None or grads.dtype == torch.float32))
 
+    def _one(self):
+        """A resident scalar 1.0: the backward seed of a scalar loss (no ones_like kernel per step)."""
+        one = self.__dict__.get('_one_t')
+        if one is None:
+            one = self._one_t = torch.ones((), device=self.device)
+        return one
+
     def _score_seed(self, n, ld):
         """Constant [n, ld] fp32 rows with 1 in column 0: the input-gradient seed of sum(scores) taken on
         the raw discriminator output (no slice / select backward kernels)."""
@@ -854,7 +864,7 @@ class PgGan(BaseModel):
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.g_params, False)
         nets.set_requires_grad(nets.d_params, True)
-        nets.D.grad.zero_()
+        _zero(nets.D.grad)
         idx = self._shard(rng.randint(level.shape[0], mb * self.world, TrialRng.D_IDX)).to(level.device)
         reals = self._reals(level, idx, lod - math.floor(lod))
         labels = labels_all.index_select(0, idx) if nets.label_size else torch.zeros((mb, 0), device=self.device)
@@ -892,7 +902,7 @@ class PgGan(BaseModel):
         # data-parallel rounds launch their all-reduce buckets from post-accumulate-grad hooks, so
         # they keep autograd's accumulation
         with A.accumulate_weight_grads_in_place(nets.d_params.values()) if ar is None else contextlib.nullcontext():
-            loss.backward()
+            loss.backward(self._one() if loss.is_cuda else None)
         if ar is not None:
             ar.finish()
         if apply:
@@ -908,7 +918,7 @@ class PgGan(BaseModel):
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.d_params, False)
         nets.set_requires_grad(nets.g_params, True)
-        nets.G.grad.zero_()
+        _zero(nets.G.grad)
         labels = self._rand_labels(labels_all, mb, rng)
         fakes = nets.generator(PG, self._latents(mb, rng, TrialRng.G_LAT), labels, lod)
         if self._fused_loss():
@@ -927,7 +937,7 @@ class PgGan(BaseModel):
         # data-parallel rounds launch their all-reduce buckets from post-accumulate-grad hooks, so
         # they keep autograd's accumulation
         with A.accumulate_weight_grads_in_place(nets.g_params.values()) if ar is None else contextlib.nullcontext():
-            loss.backward()
+            loss.backward(self._one() if loss.is_cuda else None)
         if ar is not None:
             ar.finish()
         if apply:
@@ -1075,6 +1085,13 @@ class _GradPenaltyFn(torch.autograd.Function):
         if gn is not None:
             coef = coef + gn / n.clamp_min(1e-30)
         return (g * coef.view((-1,) + (1,) * (g.dim() - 1)).to(g.dtype)), None, None
+
+
+def _zero(t):
+    if t.is_cuda:
+        from rafiki_amd.ops import functional as F
+        return F.zero_(t)
+    return t.zero_()
 
 
 class WganLossFn(torch.autograd.Function):

@@ -50,6 +50,7 @@ _SIGS = {
     "rk_add_int": [vp, i32, vp],
     "rk_rows_reduce": [vp, i32, i64, i32, vp, vp],
     "rk_lerp": [vp, vp, vp, i64, f32, vp],
+    "rk_zero32": [vp, i64, vp],
     "rk_nonfinite": [vp, i64, vp, vp],
     "rk_reduce_slabs": [vp, i32, i64, vp, i32, f32, vp],
     "rk_colsum": [vp, i32, i32, i32, vp, i32, vp],
@@ -97,7 +98,7 @@ _SIGS = {
     "rk_sgemm_grp": [i32, i32, i32, vp, vp, vp, vp] + [i32] * 10 + [i32, i64, i32, f32, f32, i64, i64, i32, i64, i64,
                                                                      i64, i64, vp],
     "rk_bnf_eval_grp": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
-    "rk_pack_nhwc_f32": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp],
+    "rk_pack_nhwc_f32": [vp, i32, i32, i32, i32, i32, i32, f32, f32, vp, vp, i32, vp],
     "rk_softmax_xent_f32": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],
     # table-driven gathers (PG-GAN up / down convs), resampling, fp32 PG-GAN side kernels
     "rk_sgemm_g": [i32, i32, i32, vp, vp, vp, vp] + [i32] * 14 + [u32p, u32p, C.c_uint, i32, i64, i32, i64, i32, f32,

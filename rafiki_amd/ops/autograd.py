@@ -432,11 +432,12 @@ def resample_via_winograd(full_hw: int, channels: int) -> bool:
     does 2.25 per full-res pixel — 1.8x fewer MFMA cycles for the down conv, 1.8x fewer for the up conv
     — at the price of one full-resolution activation round trip (upscale / box-filter pass).  On the
     32x32x512 PG-GAN layers the resampling convs are a third of the lod-0 step
-    (profiles/pg_gan_lod0_f32_kernels_r3_direct.txt), yet measured end to end the Winograd route was
-    slower (lod 0: 73.0 vs 71.3 ms per D+G round, profiles/pg_gan_bench_r3e.jsonl): the direct gathers
-    run at high MFMA utilisation and the full-resolution round trips cost more than the saved MACs.
-    RAFIKI_PGGAN_RESAMPLE = direct (default) | wino | auto (Winograd on maps >= 16 with >= 64 channels)."""
-    mode = os.environ.get('RAFIKI_PGGAN_RESAMPLE', 'direct')
+    (profiles/pg_gan_lod0_f32_kernels_r3_direct.txt).  In round 3 the Winograd route lost end to end
+    (lod 0: 73.0 vs 71.3 ms per D+G round, profiles/pg_gan_bench_r3e.jsonl); with the pre-split X6 plane
+    GEMMs, the leaky-ReLU output-transform epilogue and the native leaky ReLU after the box filter it wins
+    (40.2 vs 46.3 ms, profiles/pg_gan_resample_ab_r4.jsonl), so it is the default.
+    RAFIKI_PGGAN_RESAMPLE = wino (default) | direct | auto (Winograd on maps >= 16 with >= 64 channels)."""
+    mode = os.environ.get('RAFIKI_PGGAN_RESAMPLE', 'wino')
     if mode == 'wino':
         return S.WINO and S.WINO4 and full_hw % 4 == 0 and channels % 8 == 0
     if mode == 'auto':
@@ -678,8 +679,27 @@ def dense(x, w, b=None, *, wb=None, lrelu=None):
 
 
 # ---------------------------------------------------------------------------- elementwise glue
+class LReluFn(torch.autograd.Function):
+    """y = max(x, slope x) on the native gate kernel (lrelu_gate(x, x) = x (x > 0 ? 1 : slope)); backward is
+    the gate read from y (LReluGateFn), itself differentiable, so WGAN-GP's double backward goes through."""
+
+    @staticmethod
+    def forward(ctx, x, slope):
+        y = S.lrelu_gate(x, x, slope)
+        ctx.save_for_backward(y)
+        ctx.slope = slope
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        return _lrelu_gate(gy.contiguous(), y, ctx.slope), None
+
+
 def leaky_relu(x, slope=0.2):
-    """max(x*a, x) (pg_gans.py:987-990); twice differentiable through torch."""
+    """max(x*a, x) (pg_gans.py:987-990); twice differentiable (native kernels on fp32 GPU tensors)."""
+    if x.is_cuda and x.dtype == F32 and x.is_contiguous() and x.numel() % 4 == 0:
+        return LReluFn.apply(x, float(slope))
     return TF.leaky_relu(x, slope)
 
 

@@ -1285,19 +1285,25 @@ def head_dw(z, dlogits, dz, *, dw, db=None, dbh=None):
     _lib.call("rk_head_dw", _p(z), _p(dlogits), _p(dz), B, D, NC, _p(dw), _p(db), _p(dbh), _s())
 
 
-def pack_nhwc(images, cpad=4, scale=1.0, shift=0.0, out=None, nhwc=False):
-    """uint8/float32 NCHW (``nhwc``: NHWC) -> fp32 NHWC with channels padded to ``cpad``, x*scale+shift."""
+def pack_nhwc(images, cpad=4, scale=1.0, shift=0.0, out=None, nhwc=False, idx=None):
+    """uint8/float32 NCHW (``nhwc``: NHWC) -> fp32 NHWC with channels padded to ``cpad``, x*scale+shift.
+    ``idx`` (int32 [n], device): pack images[idx] (the minibatch gather in the same pass)."""
     if nhwc:
         Nb, H, W, Cc = images.shape
     else:
         Nb, Cc, H, W = images.shape
+    nsrc = Nb
+    if idx is not None:
+        assert idx.dtype == torch.int32 and idx.is_cuda and idx.dim() == 1
+        idx = idx.contiguous()
+        Nb = idx.numel()
     if out is None:
         out = torch.empty((Nb, H, W, cpad), device=images.device, dtype=torch.float32)
     is_u8 = 1 if images.dtype == torch.uint8 else 0
     if not is_u8 and images.dtype != torch.float32:
         images = images.float()
     _lib.call("rk_pack_nhwc_f32", _p(images.contiguous()), is_u8 | (2 if nhwc else 0), Nb, Cc, H, W, cpad,
-              float(scale), float(shift), _p(out), _s())
+              float(scale), float(shift), _p(out), _p(idx), nsrc, _s())
     return out
 
 

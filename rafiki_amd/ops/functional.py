@@ -738,6 +738,15 @@ def lerp_(dst, src, t, dst_bf16=None):
     _lib.call("rk_lerp", _p(dst), _p(src), _p(dst_bf16), dst.numel(), float(t), _s())
 
 
+def zero_(t):
+    """t.zero_() on the native kernel (4-byte dtypes, contiguous, 16-B aligned): keeps the per-step
+    gradient-arena and flag resets out of PyTorch's fill kernels inside captured training graphs."""
+    if (t.is_cuda and t.is_contiguous() and t.element_size() == 4 and t.data_ptr() % 16 == 0):
+        _lib.call("rk_zero32", _p(t), t.numel(), _s())
+        return t
+    return t.zero_()
+
+
 def nonfinite_flag(x, flag):
     _lib.call("rk_nonfinite", _p(x), x.numel(), _p(flag), _s())
 
