@@ -467,9 +467,6 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
         flags |= WF_BIAS
     if relu:
         flags |= WF_RELU
-    if lrelu is not None:
-        assert not relu and stats is None and bnb is None and bnp is None
-        flags |= WF_LRELU
     if stats is not None:
         flags |= WF_STATS
     if bnb is not None:
@@ -541,9 +538,6 @@ def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=N
         flags |= WF_BIAS
     if relu:
         flags |= WF_RELU
-    if lrelu is not None:
-        assert not relu and stats is None and bnb is None and bnp is None
-        flags |= WF_LRELU
     if stats is not None:
         flags |= WF_STATS
     if bnb is not None:
