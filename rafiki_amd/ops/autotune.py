@@ -252,12 +252,17 @@ def _tune_locked(key, candidates, run):
                 continue
             try:
                 t = _time_graph(cfg, run, max(REPS, 5)) if use_graph else _time_eager(cfg, run, REPS)
-            except Exception:
+            except (NameError, TypeError, AttributeError, KeyError, IndexError, UnboundLocalError):
+                raise   # a bug in the candidate's Python path, never "this config does not apply here"
+            except Exception as e:   # KernelError (unsupported shape), capture / launch failures, asserts
                 try:
                     torch.cuda.synchronize()
                 except Exception:
                     pass
                 t = float('inf')
+                stats['failed'] = stats.get('failed', 0) + 1
+                if os.environ.get('RAFIKI_AUTOTUNE_VERBOSE'):
+                    print('autotune: candidate {} of {} failed: {!r}'.format(cfg, key, e), flush=True)
             times[cfg] = min(times.get(cfg, float('inf')), t)
     best = min(candidates, key=lambda c: times.get(c, float('inf')))
     best_t = times.get(best, float('inf'))

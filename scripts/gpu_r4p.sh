@@ -2,8 +2,8 @@
 # PG-GAN after the fused loss head / in-place grads / Winograd resampling: tests, census, profiles, A/B
 set -o pipefail
 O=gpurun_out/r4p; mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_pg_gan_gpu.py \
-  tests/test_x6p_gpu.py -k "not x6p_gemm_vs_fp64" > $O/tests.log 2>&1
+timeout -k 10 1200 python -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/ \
+  > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u scripts/pggan_aten_census.py --lods 3,0 > $O/census.jsonl 2> $O/census.err || exit $?
 for m in wino direct; do
