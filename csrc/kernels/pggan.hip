@@ -758,6 +758,25 @@ __global__ __launch_bounds__(256) void wgan_bwd_kernel(const float* __restrict__
 
 }  // namespace
 
+namespace {
+
+// The D step's inputs in one pass (pg_gans.py:1297-1306): rf = [reals; fakes] (one batched D evaluation) and
+// mixed_r = reals_r + (fakes_r - reals_r) alpha_r (the penalty's interpolates), P floats per sample.
+__global__ __launch_bounds__(256) void wgan_mix_kernel(const float* __restrict__ reals, const float* __restrict__ fakes,
+                                                       const float* __restrict__ alpha, float* __restrict__ rf,
+                                                       float* __restrict__ mixed, int mb, int P4) {
+  const long long n4 = (long long)mb * P4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const int r = (int)(i / P4);
+    const f32x4 a = ((const f32x4*)reals)[i], b = ((const f32x4*)fakes)[i];
+    ((f32x4*)rf)[i] = a;
+    ((f32x4*)rf)[n4 + i] = b;
+    ((f32x4*)mixed)[i] = a + (b - a) * alpha[r];
+  }
+}
+
+}  // namespace
+
 // P > 0: D loss (s has 2 mb rows: reals then fakes; g [mb][P]); P == 0: G loss (s has mb rows).
 // rows: scratch [4][mb]; acc (optional): += the means (loss, real, fake, |g|) (nstat = 4) or loss (1).
 extern "C" int rk_wgan_loss_fwd(const float* s, int ld, int mb, const float* g, int P, float lam, float target,
@@ -768,6 +787,17 @@ extern "C" int rk_wgan_loss_fwd(const float* s, int ld, int mb, const float* g, 
   RK_LAUNCH_CHECK();
   hipLaunchKernelGGL(wgan_final_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, rows, mb, P > 0 ? 4 : 1, loss,
                      acc);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_wgan_mix(const float* reals, const float* fakes, const float* alpha, float* rf, float* mixed, int mb,
+                           int P, void* stream) {
+  if (mb <= 0 || P <= 0 || (P & 3)) return RK_EUNSUPPORTED;
+  const long long n4 = (long long)mb * (P / 4);
+  const unsigned blocks = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(wgan_mix_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, reals, fakes, alpha, rf, mixed,
+                     mb, P / 4);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -859,7 +859,21 @@ class PgGan(BaseModel):
     def _d_step(self, lod, mb, level, labels_all, rng, opt, ar, wgan_lambda=10.0, wgan_epsilon=0.001,
                 wgan_target=1.0, apply=True, acc=None):
         """_D_wgangp_acgan (pg_gans.py:1291-1328) + D optimizer step (``apply=False``: gradients only).
-        acc[:4] += the step's mean (loss, real score, fake score, |grad|)."""
+        acc[:4] += the step's mean (loss, real score, fake score, |grad|).  The weights' Winograd / X6-plane
+        forms are derived once per step (A.cached_weight_transforms), not once per conv call."""
+        with A.cached_weight_transforms(self._cacheable()):
+            stats = self._d_grads(lod, mb, level, labels_all, rng, ar, wgan_lambda, wgan_epsilon, wgan_target, acc)
+        if apply:
+            self._apply(self.nets.D, opt, rng)
+        if stats is not None and acc is not None:
+            acc[:4] += stats
+        return stats
+
+    def _cacheable(self):
+        nets = self.nets
+        return list(nets.d_params.values()) + list(nets.g_params.values()) if self.device.type == 'cuda' else []
+
+    def _d_grads(self, lod, mb, level, labels_all, rng, ar, wgan_lambda, wgan_epsilon, wgan_target, acc):
         nets = self.nets
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.g_params, False)
@@ -871,11 +885,20 @@ class PgGan(BaseModel):
         with torch.no_grad():
             fakes = nets.generator(PG, self._latents(mb, rng, TrialRng.D_LAT), labels, lod)
         fused = self._fused_loss()
+        alpha = self._shard(rng.rand((mb * self.world, 1, 1, 1), TrialRng.D_ALPHA))
+        if fused and reals.dtype == torch.float32 and fakes.dtype == torch.float32 and reals[0].numel() % 4 == 0:
+            # [reals; fakes] and the interpolates in one native pass
+            rf_in = torch.empty((2 * mb,) + tuple(reals.shape[1:]), device=reals.device, dtype=torch.float32)
+            mixed = torch.empty_like(reals)
+            _lib.call("rk_wgan_mix", S._p(reals.contiguous()), S._p(fakes.contiguous()), S._p(alpha.contiguous()),
+                      S._p(rf_in), S._p(mixed), mb, reals[0].numel(), S._s())
+            mixed.requires_grad_(True)
+        else:
+            rf_in = torch.cat([reals, fakes.to(reals.dtype)], 0)
+            mixed = torch.lerp(reals.float(), fakes.float(), alpha).to(reals.dtype).detach().requires_grad_(True)
         # real and fake minibatches share one batched D evaluation (2 independent mbstd segments):
         # half the launches, twice the GEMM rows, one weight-gradient contribution instead of two
-        rf = nets.discriminator(PD, torch.cat([reals, fakes.to(reals.dtype)], 0), lod, segs=2, raw=fused)
-        alpha = self._shard(rng.rand((mb * self.world, 1, 1, 1), TrialRng.D_ALPHA))
-        mixed = torch.lerp(reals.float(), fakes.float(), alpha).to(reals.dtype).detach().requires_grad_(True)
+        rf = nets.discriminator(PD, rf_in, lod, segs=2, raw=fused)
         if fused:
             mixed_raw = nets.discriminator(PD, mixed, lod, raw=True)
             if ar is not None:
@@ -905,15 +928,21 @@ class PgGan(BaseModel):
             loss.backward(self._one() if loss.is_cuda else None)
         if ar is not None:
             ar.finish()
-        if apply:
-            self._apply(nets.D, opt, rng)
-        if stats is not None and acc is not None:
-            acc[:4] += stats
         return stats
 
     def _g_step(self, lod, mb, labels_all, rng, opt, ar, apply=True, acc=None):
         """_G_wgan_acgan (pg_gans.py:1276-1289) + G optimizer step (``apply=False``: gradients only).
         acc[4] += the step's mean loss."""
+        with A.cached_weight_transforms(self._cacheable()):
+            stat = self._g_grads(lod, mb, labels_all, rng, ar, acc)
+        if apply:
+            self._apply(self.nets.G, opt, rng)
+            self.nets.set_requires_grad(self.nets.d_params, True)
+        if stat is not None and acc is not None:
+            acc[4] += stat
+        return stat
+
+    def _g_grads(self, lod, mb, labels_all, rng, ar, acc):
         nets = self.nets
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.d_params, False)
@@ -940,11 +969,6 @@ class PgGan(BaseModel):
             loss.backward(self._one() if loss.is_cuda else None)
         if ar is not None:
             ar.finish()
-        if apply:
-            self._apply(nets.G, opt, rng)
-            nets.set_requires_grad(nets.d_params, True)
-        if stat is not None and acc is not None:
-            acc[4] += stat
         return stat
 
     # ------------------------------------------------------------------ generation

@@ -93,6 +93,7 @@ _SIGS = {
     "rk_lrelu_gate_f32": [vp, vp, vp, i64, f32, vp],
     "rk_lrelu_gate_colsum_f32": [vp, vp, vp, i32, i32, f32, vp, i32, vp],
     "rk_wgan_loss_fwd": [vp, i32, i32, vp, i32, f32, f32, f32, vp, vp, vp, vp],
+    "rk_wgan_mix": [vp, vp, vp, vp, vp, i32, i32, vp],
     "rk_wgan_loss_bwd": [vp, vp, i32, i32, vp, i32, f32, f32, f32, vp, vp, vp, vp],
     "rk_sreduce_epi": [vp, i32, i32, i32, vp, i32, f32, f32, vp, i32, vp, i32, i32, vp],
     "rk_sgemm_grp": [i32, i32, i32, vp, vp, vp, vp] + [i32] * 10 + [i32, i64, i32, f32, f32, i64, i64, i32, i64, i64,

@@ -148,6 +148,50 @@ def accumulate_weight_grads_in_place(params):
             p._rk_direct = v
 
 
+_WT = {'on': 0, 'cache': {}}
+
+
+@contextlib.contextmanager
+def cached_weight_transforms(params):
+    """Within this context the derived forms of the conv weights in ``params`` (Winograd U sets, their X6
+    planes, the data-gradient transposes) are computed once and reused by every conv / dgrad that reads the
+    same weight — a WGAN-GP step reads each discriminator weight in 4-6 convs.  The weights must not
+    change inside the context (wrap forward + backward, not the optimizer step).  Only leaves marked here
+    are cached (persistent arena storage: their addresses never name another tensor); the marks and the
+    cache are process-global because the backward runs on autograd's device thread."""
+    leaves = [p for p in params if isinstance(p, torch.Tensor)]
+    prev = [getattr(p, '_rk_wcache', False) for p in leaves]
+    for p in leaves:
+        p._rk_wcache = True
+    _WT['on'] += 1
+    try:
+        yield
+    finally:
+        _WT['on'] -= 1
+        if _WT['on'] == 0:
+            _WT['cache'].clear()
+        for p, v in zip(leaves, prev):
+            p._rk_wcache = v
+
+
+def _wt(kind, w, fn):
+    """``fn`` (a producer of a derived form of weight ``w``), cached by (kind, address, shape) when ``w`` is
+    (a reinterpreting view of) a leaf marked by ``cached_weight_transforms``; else ``fn`` itself."""
+    if not _WT['on']:
+        return fn
+    leaf = w if w.is_leaf else getattr(w, '_base', None)
+    if leaf is None or not getattr(leaf, '_rk_wcache', False) or not w.is_contiguous():
+        return fn
+    key = (kind, w.data_ptr(), tuple(w.shape))
+
+    def get():
+        t = _WT['cache'].get(key)
+        if t is None:
+            t = _WT['cache'][key] = fn()
+        return t
+    return get
+
+
 def _param_grad_buffer(w):
     """The persistent fp32 gradient buffer of a parameter (the leaf's .grad, or the viewed leaf's, in
     the parameter's shape), for a leaf marked by ``accumulate_weight_grads_in_place`` and outside a
@@ -225,9 +269,9 @@ class ConvFn(torch.autograd.Function):
             wd = w.detach().contiguous()
             # 3x3: the fused Winograd kernels (weights transformed inside the candidate) compete in the tuner
             y = S.conv_fwd(x, wd, taps=taps, bias=bd, act=_act(slope), slope=0.2 if slope is None else slope,
-                           wino=(lambda: S.wino_u(wd)) if taps == 9 else None,
-                           wino4=(lambda: S.wino4_u(wd)) if taps == 9 else None,
-                           wino4p=(lambda: S.wino4_u4p(wd)) if taps == 9 else None)
+                           wino=_wt('u2', w, lambda: S.wino_u(wd)) if taps == 9 else None,
+                           wino4=_wt('u4', w, lambda: S.wino4_u(wd)) if taps == 9 else None,
+                           wino4p=_wt('u4p', w, lambda: S.wino4_u4p(wd)) if taps == 9 else None)
         else:
             y = F.conv_fwd(x, _wshadow(w, wb), taps=taps, bias=bd, act=_act(slope),
                            slope=0.2 if slope is None else slope)
@@ -277,10 +321,11 @@ class ConvDgradFn(torch.autograd.Function):
         gy = gy.contiguous()
         if gy.dtype == F32:
             wd = w.detach().contiguous()
-            dx = S.conv_dgrad(gy, lambda: S.conv_wt(wd, taps), taps=taps, cin=wd.numel() // (taps * wd.shape[0]),
-                              wino=(lambda: S.wino_ut(wd)) if taps == 9 else None,
-                              wino4=(lambda: S.wino4_ut(wd)) if taps == 9 else None,
-                              wino4p=(lambda: S.wino4_u4p(wd, dgrad=True)) if taps == 9 else None)
+            dx = S.conv_dgrad(gy, _wt('wt%d' % taps, w, lambda: S.conv_wt(wd, taps)), taps=taps,
+                              cin=wd.numel() // (taps * wd.shape[0]),
+                              wino=_wt('ut2', w, lambda: S.wino_ut(wd)) if taps == 9 else None,
+                              wino4=_wt('ut4', w, lambda: S.wino4_ut(wd)) if taps == 9 else None,
+                              wino4p=_wt('ut4p', w, lambda: S.wino4_u4p(wd, dgrad=True)) if taps == 9 else None)
         else:
             dx = F.conv_dgrad(gy, _wshadow(w, wb), taps=taps)
         ctx.save_for_backward(gy, w)

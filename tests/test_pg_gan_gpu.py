@@ -605,3 +605,16 @@ def test_wgan_loss_head_vs_fp64(mb, gshape):
     dref = torch.zeros(mb, 8)
     dref[:, 0] = -1.0 / mb
     assert torch.equal(sg2.grad.cpu(), dref)
+
+
+def test_wgan_mix_kernel():
+    """rk_wgan_mix: [reals; fakes] and reals + (fakes - reals) * alpha per sample, exactly as torch.cat / lerp."""
+    from rafiki_amd.ops import _lib, f32 as S
+    g0 = torch.Generator().manual_seed(7)
+    r, f = torch.randn(33, 4, 4, 8, generator=g0).to(DEV), torch.randn(33, 4, 4, 8, generator=g0).to(DEV)
+    a = torch.rand(33, 1, 1, 1, generator=g0).to(DEV)
+    rf, mixed = torch.empty(66, 4, 4, 8, device=DEV), torch.empty(33, 4, 4, 8, device=DEV)
+    _lib.call("rk_wgan_mix", S._p(r), S._p(f), S._p(a), S._p(rf), S._p(mixed), 33, 128, S._s())
+    torch.cuda.synchronize()
+    assert torch.equal(rf, torch.cat([r, f]))
+    assert (mixed - (r + (f - r) * a)).abs().max().item() < 1e-6
