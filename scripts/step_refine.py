@@ -57,6 +57,7 @@ def main():
     ap.add_argument('--steps', type=int, default=40)
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--max-alts', type=int, default=3)
+    ap.add_argument('--start', default='', help='start from this database JSON instead of the shipped one')
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     log_path = os.path.join(a.out, 'cold_tune.jsonl')
@@ -77,7 +78,7 @@ def main():
     gen.manual_seed(0)
     idx = torch.randint(0, 8192, (64, 256), device=dev, generator=gen)
 
-    shipped = autotune._read(os.path.join(autotune.SHIPPED_DIR, autotune.db_name()))
+    shipped = autotune._read(a.start or os.path.join(autotune.SHIPPED_DIR, autotune.db_name()))
     # 1. cold tune (nothing loaded), recording which keys the step looks up
     autotune._loaded = True
     autotune.clear()
@@ -123,7 +124,7 @@ def main():
             autotune._cache[key] = c
             ms = build_and_time(dev, data, y_all, idx, a.steps, a.reps)
             keep = ms < best_ms * (1.0 - a.gain)
-            print(json.dumps({'key': [str(x) for x in key], 'op_us': round(best_t * 1e3, 1), 'from': list(prev),
+            print(json.dumps({'key': [str(x) for x in key], 'op_us': round(best_t, 1), 'from': list(prev),
                               'to': list(c), 'step_ms': round(ms, 4), 'best_ms': round(best_ms, 4), 'kept': keep}),
                   flush=True)
             if keep:
