@@ -137,3 +137,50 @@ def test_single_launch_refresh_table_covers_every_family(monkeypatch):
         assert torch.equal(m[base:base + fmeta.numel() // 5], fmeta.view(-1, 5))
         row += fnb
         base += fmeta.numel() // 5
+
+
+# ---- per-step weight-transform cache and in-place gradient marks (ops/autograd.py), host-side logic
+def test_cached_weight_transforms_logic():
+    """_wt caches a marked leaf's derived forms by (kind, address, shape) only inside the context, never a
+    non-leaf (gradient) tensor or an unmarked leaf, and the cache and marks are gone after the context."""
+    import torch
+    from rafiki_amd.ops import autograd as A
+    w = torch.nn.Parameter(torch.randn(4, 9, 8))
+    other = torch.nn.Parameter(torch.randn(4, 72))
+    grad_like = torch.randn(4, 72) * 2
+    calls = []
+
+    def producer(tag):
+        def f():
+            calls.append(tag)
+            return torch.full((1,), float(len(calls)))
+        return f
+    view = w.reshape(4, -1)
+    assert A._wt('u4p', view, producer('a')) is not None
+    A._wt('u4p', view, producer('a'))()
+    assert calls == ['a']                                  # no context: the producer itself, uncached
+    with A.cached_weight_transforms([w]):
+        assert getattr(w, '_rk_wcache', False)
+        r1 = A._wt('u4p', view, producer('b'))()
+        r2 = A._wt('u4p', w.reshape(4, -1), producer('b'))()   # same leaf, same form: served from the cache
+        r3 = A._wt('ut4p', view, producer('c'))()             # another form: its own entry
+        A._wt('u4p', other.reshape(4, -1), producer('d'))()   # unmarked leaf: never cached
+        A._wt('u4p', other.reshape(4, -1), producer('d'))()
+        A._wt('u4p', grad_like, producer('e'))()             # a non-leaf tensor: never cached
+        A._wt('u4p', grad_like, producer('e'))()
+        assert r1 is r2 and r3 is not r1
+    assert calls == ['a', 'b', 'c', 'd', 'd', 'e', 'e']
+    assert not getattr(w, '_rk_wcache', False) and not A._WT['cache'] and A._WT['on'] == 0
+
+
+def test_in_place_grad_marks_are_scoped():
+    import torch
+    from rafiki_amd.ops import autograd as A
+    p = torch.nn.Parameter(torch.zeros(3))
+    p.grad = torch.zeros(3)
+    with A.accumulate_weight_grads_in_place([p]):
+        assert p._rk_direct
+        with torch.no_grad():
+            # CPU tensors never take the native in-place path (the GPU kernels write the buffer)
+            assert A._param_grad_buffer(p) is None
+    assert not p._rk_direct
