@@ -973,9 +973,16 @@ class WinoWeights:
     # one launch for every family (RAFIKI_WT_ALL=0: one launch per family)
     WT_ALL = os.environ.get('RAFIKI_WT_ALL', '1') != '0'
 
-    def refresh(self):
-        tabs = self._prepare(self.live)
-        allt = self._tables.get(('all', self.live))
+    def refresh(self, part=None):
+        """Transform the live sets (one launch); ``part`` = 'fwd' / 'bwd': only the forward (u*) or the
+        data-gradient (ut*) sets — the engine runs the 'bwd' half on a side stream under the forward pass."""
+        live = self.live if part is None else frozenset(k for k in self.live if k[0].startswith('ut') == (part == 'bwd'))
+        if part != 'bwd':
+            self._fresh = set()
+        if not live:
+            return
+        tabs = self._prepare(live)
+        allt = self._tables.get(('all', live))
         if self.WT_ALL and allt is not None:
             desc, meta, nb = allt
             _lib.call("rk_wino_weights_all", _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
@@ -984,7 +991,7 @@ class WinoWeights:
                 name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi",
                         'p': "rk_x6p_w4_weights_multi"}[fam]
                 _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
-        self._fresh = set(self.live)
+        self._fresh |= set(live)
 
     def end_step(self):
         """Narrow the live sets to the ones this step's convs used (no-op inside graph capture)."""
