@@ -237,6 +237,7 @@ class ConvNetEngine:
     # RAFIKI_WT_SPLIT=1: the data-gradient Winograd weight sets are transformed on a side stream while the
     # forward pass runs (only the forward sets stay on the step's critical path)
     split_wt = os.environ.get('RAFIKI_WT_SPLIT', '0') == '1'
+    split_wt_hw = int(os.environ.get('RAFIKI_WT_SPLIT_HW', '8'))   # "deep" layers: maps <= this
 
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
@@ -390,18 +391,25 @@ class ConvNetEngine:
         if not self._acc_zeroed_by_prologue:
             self._bn_acc_flat.zero_()  # one memset node for every layer's fp64 statistic slots
         ww = self._wino_train()
-        wt_side = None
+        wt_side = late_ready = None
+        k_late = next((bi for bi, b in enumerate(self.blocks) if b[4] <= self.split_wt_hw), len(self.blocks))
         if ww is not None and self.split_wt:
-            # forward sets now; the data-gradient sets on the side stream, under the forward pass
-            ww.refresh('fwd')
+            # the early layers' forward sets now; the deep layers' forward sets (the big 256 / 512-channel
+            # ones) and every data-gradient set on a side stream, under the early layers' convs
+            ww.refresh(lambda k, l: not k.startswith('ut') and l < k_late)
             wt_side = self._side_stream()
             wt_side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(wt_side):
-                ww.refresh('bwd')
+                ww.refresh(lambda k, l: not k.startswith('ut') and l >= k_late, reset=False)
+                late_ready = torch.cuda.Event()
+                late_ready.record(wt_side)
+                ww.refresh(lambda k, l: k.startswith('ut'), reset=False)
         elif ww is not None:
             ww.refresh()   # one launch per family: the live Winograd-domain weight sets of every block
         acts, saved, h = [x], [], x
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            if late_ready is not None and bi == k_late:
+                torch.cuda.current_stream(self.device).wait_event(late_ready)
             rm, rv = self.running_stats(bi)
             y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0],
                            wino=ww.lazy('u2', bi) if ww is not None else None,

@@ -973,11 +973,12 @@ class WinoWeights:
     # one launch for every family (RAFIKI_WT_ALL=0: one launch per family)
     WT_ALL = os.environ.get('RAFIKI_WT_ALL', '1') != '0'
 
-    def refresh(self, part=None):
-        """Transform the live sets (one launch); ``part`` = 'fwd' / 'bwd': only the forward (u*) or the
-        data-gradient (ut*) sets — the engine runs the 'bwd' half on a side stream under the forward pass."""
-        live = self.live if part is None else frozenset(k for k in self.live if k[0].startswith('ut') == (part == 'bwd'))
-        if part != 'bwd':
+    def refresh(self, select=None, reset=True):
+        """Transform the live sets (one launch).  ``select(kind, layer)``: only those sets; ``reset`` starts
+        the step's freshness record (False for the later parts of a split refresh — the engine runs the
+        deep layers' forward sets and the data-gradient sets on a side stream under the early layers)."""
+        live = self.live if select is None else frozenset(k for k in self.live if select(*k))
+        if reset:
             self._fresh = set()
         if not live:
             return
