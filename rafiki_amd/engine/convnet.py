@@ -234,11 +234,6 @@ class ConvNetEngine:
     # 'deep': only the 8x8 / 4x4 layers (grids of a few hundred workgroups that leave CUs idle)
     overlap_wgrad = os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') in ('1', 'deep')
     overlap_max_hw = 8 if os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') == 'deep' else 1 << 30
-    # RAFIKI_WT_SPLIT=1: the data-gradient Winograd weight sets are transformed on a side stream while the
-    # forward pass runs (only the forward sets stay on the step's critical path)
-    split_wt = os.environ.get('RAFIKI_WT_SPLIT', '0') == '1'
-    split_wt_hw = int(os.environ.get('RAFIKI_WT_SPLIT_HW', '8'))   # "deep" layers: maps <= this
-
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
     fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
     # ... and into BN+ReLU+max-pool blocks (FLAG_BNP: argmax routing in the dgrad epilogue)
@@ -391,25 +386,10 @@ class ConvNetEngine:
         if not self._acc_zeroed_by_prologue:
             self._bn_acc_flat.zero_()  # one memset node for every layer's fp64 statistic slots
         ww = self._wino_train()
-        wt_side = late_ready = None
-        k_late = next((bi for bi, b in enumerate(self.blocks) if b[4] <= self.split_wt_hw), len(self.blocks))
-        if ww is not None and self.split_wt:
-            # the early layers' forward sets now; the deep layers' forward sets (the big 256 / 512-channel
-            # ones) and every data-gradient set on a side stream, under the early layers' convs
-            ww.refresh(lambda k, l: not k.startswith('ut') and l < k_late)
-            wt_side = self._side_stream()
-            wt_side.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(wt_side):
-                ww.refresh(lambda k, l: not k.startswith('ut') and l >= k_late, reset=False)
-                late_ready = torch.cuda.Event()
-                late_ready.record(wt_side)
-                ww.refresh(lambda k, l: k.startswith('ut'), reset=False)
-        elif ww is not None:
+        if ww is not None:
             ww.refresh()   # one launch per family: the live Winograd-domain weight sets of every block
         acts, saved, h = [x], [], x
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
-            if late_ready is not None and bi == k_late:
-                torch.cuda.current_stream(self.device).wait_event(late_ready)
             rm, rv = self.running_stats(bi)
             y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0],
                            wino=ww.lazy('u2', bi) if ww is not None else None,
@@ -475,8 +455,6 @@ class ConvNetEngine:
                      act=F.ACT_NONE, dgamma=fl.g('in_bn.gamma'), dbeta=fl.g('in_bn.beta'))
             return
         d = d.view(B, self.feat_hw, self.feat_hw, -1)
-        if wt_side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(wt_side)   # join before the first dgrad
         wt = self._conv_wt()
         if wt is not None:
             # flipped/transposed fp32 weights of every dgrad layer, refreshed (one launch) on first use

@@ -973,17 +973,9 @@ class WinoWeights:
     # one launch for every family (RAFIKI_WT_ALL=0: one launch per family)
     WT_ALL = os.environ.get('RAFIKI_WT_ALL', '1') != '0'
 
-    def refresh(self, select=None, reset=True):
-        """Transform the live sets (one launch).  ``select(kind, layer)``: only those sets; ``reset`` starts
-        the step's freshness record (False for the later parts of a split refresh — the engine runs the
-        deep layers' forward sets and the data-gradient sets on a side stream under the early layers)."""
-        live = self.live if select is None else frozenset(k for k in self.live if select(*k))
-        if reset:
-            self._fresh = set()
-        if not live:
-            return
-        tabs = self._prepare(live)
-        allt = self._tables.get(('all', live))
+    def refresh(self):
+        tabs = self._prepare(self.live)
+        allt = self._tables.get(('all', self.live))
         if self.WT_ALL and allt is not None:
             desc, meta, nb = allt
             _lib.call("rk_wino_weights_all", _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
@@ -992,7 +984,7 @@ class WinoWeights:
                 name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi",
                         'p': "rk_x6p_w4_weights_multi"}[fam]
                 _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
-        self._fresh |= set(live)
+        self._fresh = set(self.live)
 
     def end_step(self):
         """Narrow the live sets to the ones this step's convs used (no-op inside graph capture)."""
