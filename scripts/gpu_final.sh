@@ -1,8 +1,21 @@
-# final check at HEAD: full GPU suite + smoke + bench --gpus 1
+#!/bin/bash
+# Round-end evidence: full GPU suite, smoke, default bench (the driver's command), step kernels + PMC
 set -o pipefail
-mkdir -p gpurun_out/final
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/final/pytest_gpu.log 2>&1
-rc=$?; tail -3 gpurun_out/final/pytest_gpu.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1
-timeout -k 10 400 python -u bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/final/bench.log 2>&1 || exit $?
-tail -1 gpurun_out/final/bench.log | cut -c1-300
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/final; mkdir -p $O
+# bash scripts/gpu_final.sh        : suite + smoke + default bench
+# bash scripts/gpu_final.sh prof   : step kernel trace + PMC passes
+if [ "$1" != "prof" ]; then
+  bash scripts/gpu_suite.sh || exit 1
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 \
+    || { tail -5 $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
+  timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
+  tail -1 $O/bench.log | cut -c1-300
+fi
+if [ "$1" = "prof" ]; then
+  bash scripts/prof_step.sh final > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
+  head -3 gpurun_out/prof_final/durations.txt
+  bash scripts/pmc_step.sh > $O/pmc.log 2>&1 || { tail -5 $O/pmc.log; exit 1; }
+  tail -1 gpurun_out/pmc_step/summary.txt
+fi
