@@ -1,5 +1,8 @@
 """Step-level refinement of the tune database (run on the GPU box).
 
+``--workload pggan --lod L``: the same re-ranking on the captured PG-GAN D+G round at LOD L (mb from the
+reference schedule) instead of the VGG-small step.
+
 The autotuner times each candidate in isolation (a captured graph of back-to-back launches of one op);
 inside the training step the same kernel runs between other kernels, with other L2 / Infinity-Cache
 contents and clocks, and the isolated ranking of near-tied candidates does not always carry over
@@ -49,8 +52,56 @@ def build_and_time(dev, data, y_all, idx, steps, reps):
     return best
 
 
+class _PgRound:
+    """build_and_time's PG-GAN counterpart: one model, a fresh GraphedRounds per evaluation (first round
+    eager, second captured, then timed replays)."""
+
+    def __init__(self, dev, lod):
+        from rafiki_amd.engine.flat import FlatAdam
+        from rafiki_amd.models.pg_gan import PgGan, TrainingSchedule, TrialRng
+        self.m = PgGan(D_repeats=1, minibatch_base=16, G_lrate=1e-3, D_lrate=1e-3)
+        self.m.device = dev
+        self.m._build([1, 32, 32], 0)
+        nets = self.m.nets
+        self.G_opt = FlatAdam(nets.G, 1e-3, betas=(0.0, 0.99))
+        self.D_opt = FlatAdam(nets.D, 1e-3, betas=(0.0, 0.99))
+        for o in (self.G_opt, self.D_opt):
+            o.skip_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.rng = TrialRng(dev, 0)
+        self.acc = torch.zeros(6, device=dev)
+        self.lod = lod
+        r = 2 ** (5 - int(lod))
+        self.mb = TrainingSchedule.MINIBATCH_DICTS[16].get(r, 16)
+        self.level = torch.randint(0, 256, (4096, 1, r, r), dtype=torch.uint8, device=dev)
+        self.labels = torch.zeros((4096, 0), device=dev)
+
+    def __call__(self, steps, reps):
+        from rafiki_amd.models.pg_gan import GraphedRounds
+        g = GraphedRounds(True)
+
+        def rnd():
+            g.run(self.lod, lambda: self.m.train_round(self.lod, self.mb, self.level, self.labels, self.rng,
+                                                       self.G_opt, self.D_opt, self.acc))
+        for _ in range(3):
+            rnd()
+        torch.cuda.synchronize()
+        best = float('inf')
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                rnd()
+            torch.cuda.synchronize()
+            best = min(best, (time.perf_counter() - t0) / steps * 1e3)
+        del g
+        torch.cuda.empty_cache()
+        return best
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument('--workload', default='vgg', choices=('vgg', 'pggan'))
+    ap.add_argument('--lod', type=float, default=3.0)
     ap.add_argument('--out', default='gpurun_out/refine')
     ap.add_argument('--within', type=float, default=1.25)
     ap.add_argument('--gain', type=float, default=0.003)
@@ -77,6 +128,14 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(0)
     idx = torch.randint(0, 8192, (64, 256), device=dev, generator=gen)
+    if a.workload == 'pggan':
+        pg = _PgRound(dev, a.lod)
+
+        def measure():
+            return pg(a.steps, a.reps)
+    else:
+        def measure():
+            return build_and_time(dev, data, y_all, idx, a.steps, a.reps)
 
     shipped = autotune._read(a.start or os.path.join(autotune.SHIPPED_DIR, autotune.db_name()))
     # 1. cold tune (nothing loaded), recording which keys the step looks up
@@ -90,7 +149,7 @@ def main():
             used.append(key)
         return orig_lookup(key)
     autotune.lookup = rec
-    cold_ms = build_and_time(dev, data, y_all, idx, a.steps, a.reps)
+    cold_ms = measure()
     autotune.lookup = orig_lookup
     times = {}
     with open(log_path) as f:
@@ -100,7 +159,7 @@ def main():
     # 2. the shipped picks
     autotune.clear()
     autotune._cache.update(shipped)
-    base = build_and_time(dev, data, y_all, idx, a.steps, a.reps)
+    base = measure()
     print(json.dumps({'cold_tuned_ms': round(cold_ms, 4), 'shipped_ms': round(base, 4), 'keys': len(used)}),
           flush=True)
     cur = dict(autotune._cache)
@@ -122,7 +181,7 @@ def main():
         for c in alts:
             prev = cur[key]
             autotune._cache[key] = c
-            ms = build_and_time(dev, data, y_all, idx, a.steps, a.reps)
+            ms = measure()
             keep = ms < best_ms * (1.0 - a.gain)
             print(json.dumps({'key': [str(x) for x in key], 'op_us': round(best_t, 1), 'from': list(prev),
                               'to': list(c), 'step_ms': round(ms, 4), 'best_ms': round(best_ms, 4), 'kept': keep}),
@@ -133,7 +192,7 @@ def main():
                 changes.append((key, prev, c))
             else:
                 autotune._cache[key] = prev
-    final = build_and_time(dev, data, y_all, idx, a.steps, a.reps)
+    final = measure()
     out = {json.dumps(list(k)): list(v) for k, v in autotune._cache.items()}
     for k, v in shipped.items():   # keys the step does not use (trials / serving shapes) stay as shipped
         out.setdefault(json.dumps(list(k)), list(v))
