@@ -7,7 +7,7 @@ Every part of it is measured in this run, none extrapolated:
 
   phase 1  images/sec/trial (the JSON ``value`` = aggregate over all GPUs, weak scaling: per-GPU work
            is fixed): rank 0's GP-EI advisor proposes one knob set per rank (broadcast over RCCL as
-           packed fp64), every rank captures its VGG-small training step (device-side minibatch
+           packed fp64 when N > 1), every rank captures its VGG-small training step (device-side minibatch
            gather + fwd + bwd + fused SGD) into one hipGraph and replays it on a device-resident
            synthetic dataset; W untimed warmup steps, then K timed steps bracketed by barrier +
            synchronize on both sides, max over ranks.
@@ -308,6 +308,14 @@ def main():
     dev = torch.device('cuda', gpu)
     n_devices = world if info.backend in ('nccl', 'none') else min(world, ndev)
 
+    pre = None
+    if world > 1:
+        # bounded-time check of every collective and rank-0 <-> peer P2P pair before any timed work (a
+        # missing peer or unusable link ends the run with a named step instead of a hang)
+        from rafiki_amd.parallel.exchange import control_group
+        pre = D.preflight(info, timeout_s=float(os.environ.get('RAFIKI_PREFLIGHT_TIMEOUT_S', '120')),
+                          group=control_group(info))
+
     th = phase_throughput(args, info, dev)
     B = args.batch
     ms = th['elapsed'] * 1000.0 / args.steps
@@ -370,9 +378,12 @@ def main():
             out['trials_wall_s'] = round(trials['wall'], 3)
             out['trials_per_rank'] = trials['per_rank']
             out['trial_busy_s_per_rank'] = [round(b, 3) for b in trials['busy']]
-            out['trial_definition'] = ('VggSmallTrial: GP-EI knobs (lr, momentum, wd) from rank 0 over RCCL, '
+            via = ('from rank 0 over {} point-to-point'.format('RCCL' if info.backend == 'nccl' else info.backend)
+                   if world > 1 else 'from the in-process advisor (1 rank: no collective in the path)')
+            out['trial_definition'] = ('VggSmallTrial: GP-EI knobs (lr, momentum, wd) {}, '
                                        '10 epochs x 50000 synthetic CIFAR-shaped images, batch 256 + eval on '
-                                       '10000, params pickled; async scheduling; after 1 untimed warm-up trial/GPU')
+                                       '10000, params pickled; async scheduling; after 1 untimed warm-up trial/GPU'
+                                       .format(via))
             out['trial_scores'] = [round(s, 4) for s in trials['scores']]
             out['trial_breakdown_s'] = {'first_trial_rank0': trials['first'], 'steady_mean_rank0': trials['steady']}
             if trials['exchange'] is not None:
@@ -383,6 +394,8 @@ def main():
             out['probe_trials_measured'] = probe['n']
             out['probe_definition'] = 'VggSmallProbe: 2 epochs x 8192 images + eval 2048 (~64 steps; overhead probe)'
             out['probe_breakdown_s'] = probe['steady']
+        if pre is not None:
+            out['preflight'] = pre
         if serving is not None:
             out['ensemble_qps'] = serving['device_b256']['qps']
             out['ensemble'] = serving

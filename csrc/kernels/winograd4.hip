@@ -23,7 +23,13 @@
 //     loads are in flight while the current chunk's MFMAs run; XOR-swizzled column pairs keep the
 //     fragment reads bank-conflict-free (the same layout as the F(2x2) kernel);
 //   * epilogues identical to the F(2x2) kernel: bias, ReLU, BN statistics (fp64 slot atomics) and
-//     the data-gradient FLAG_BNB / FLAG_BNP fusions; grouped launches for the serving ensemble.
+//     the data-gradient FLAG_BNB / FLAG_BNP fusions; grouped launches for the serving ensemble;
+//   * blocked weights (UB): the per-step weight transform can also write U as the byte image of the
+//     kernel's LDS stage, one contiguous [36][32 co][8 ci] block (36 KiB, column swizzle applied) per
+//     (32-channel output block, 8-channel input chunk).  The weight loads then move 16 B per lane and
+//     1 KiB per wave-instruction over whole cache lines, instead of 8 B per lane scattered over a
+//     32-B segment of each (position, channel) row — those loads cost about as much time as the
+//     MFMAs on the 32x32 layers (profiles/wino4_load_breakdown_r5.jsonl).
 #include "common.h"
 #include <cstdlib>
 
@@ -122,7 +128,7 @@ RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) { w_tile
 // NS = 2: two LDS stages and two register sets — the transform of chunk c+1 (loaded during chunk c-1)
 // is written to one stage while the MFMAs of chunk c read the other, in the same wave (software
 // pipelining; one barrier per chunk; chunks past Cin load zeros, so the body is branch-free)
-template <int MO, int WM, int WN, int MINW, int FL, int NS = 1>
+template <int MO, int WM, int WN, int MINW, int FL, int NS = 1, bool UB = false>
 __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4Params p) {
   constexpr int A = MO + 2;                // window / transformed tile side
   constexpr int P = A * A;                 // Winograd positions
@@ -131,7 +137,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   constexpr int BNC = 16 * WN;             // output channels per block
   constexpr int IT = T * KC / NT;          // input windows per thread and chunk
   constexpr int UL = P * BNC * 4 / NT;    // f32x2 weight loads per thread and chunk
+  // UB: 16-B units of one blocked weight chunk, per thread (the last round masked when NT does not divide)
+  constexpr int UNITS = P * BNC * KC / 4;
+  constexpr int UBL = (UNITS + NT - 1) / NT;
+  constexpr int ULR = UB ? 1 : UL, UBR = UB ? UBL : 1;   // register arrays of the two weight paths
   static_assert(IT >= 1 && IT * NT == T * KC && UL * NT == P * BNC * 4, "tile shape");
+  static_assert(!UB || (MO == 4 && BNC == 32), "blocked weights: F(4x4), 32-channel output blocks");
   __shared__ __attribute__((aligned(16))) float Vs[NS][P][T][KC];
   __shared__ __attribute__((aligned(16))) float Us[NS][P][BNC][KC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -168,14 +179,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   constexpr int UPK = NT / (4 * BNC);
   static_assert(UPK * 4 * BNC == NT, "weight loader shape");
   const int uco = (tid >> 2) & (BNC - 1), upr = tid & 3, upos = tid / (4 * BNC);
-  const unsigned ub = cbase + uco < p.N ? (unsigned)(((upos * p.N + cbase + uco) * p.C + 2 * upr) * 4) : OOB;
+  const unsigned ub_off = cbase + uco < p.N ? (unsigned)(((upos * p.N + cbase + uco) * p.C + 2 * upr) * 4) : OOB;
   const int ustride = __builtin_amdgcn_readfirstlane(UPK * p.N * p.C * 4);
 
-  auto load = [&](int c0, float (&raw)[IT][P], f32x2 (&ur)[UL]) {
+  // UB: the block's weight chunks are consecutive 36-KiB images: chunk c of output block cb at
+  // ((cb * nch + c) * UNITS) units of 16 B
+  const int nchunk = p.C / KC;
+  auto load = [&](int c0, float (&raw)[IT][P], f32x2 (&ur)[ULR], f32x4 (&ub)[UBR]) {
     // a chunk past Cin (the pipelined tail) reads zeros: empty buffer ranges
     const bool live = c0 < p.C;
     const __amdgpu_buffer_rsrc_t xr = rsrc(gxp + c0, live ? p.xbytes - 4ull * c0 : 0ull);
-    const __amdgpu_buffer_rsrc_t urs = rsrc(gup + c0, live ? p.ubytes - 4ull * c0 : 0ull);
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
       // opaque copies: the window offsets are rebuilt per chunk from 3 registers instead of being
@@ -200,12 +213,23 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
         }
       }
     }
+    if constexpr (UB) {
+      const __amdgpu_buffer_rsrc_t urs = rsrc(gup + (long long)(cb * nchunk + c0 / KC) * (UNITS * 4),
+                                              live ? (unsigned long long)UNITS * 16 : 0ull);
 #pragma unroll
-    for (int k = 0; k < UL; ++k)
-      ur[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(urs, (int)ub,
-                                                                           __builtin_amdgcn_readfirstlane(k * ustride), 0));
+      for (int k = 0; k < UBL; ++k) {
+        const unsigned off = (tid + NT * k < UNITS) ? (unsigned)((tid + NT * k) * 16) : OOB;
+        ub[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, (int)off, 0, 0));
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t urs = rsrc(gup + c0, live ? p.ubytes - 4ull * c0 : 0ull);
+#pragma unroll
+      for (int k = 0; k < UL; ++k)
+        ur[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(urs, (int)ub_off,
+                                                                             __builtin_amdgcn_readfirstlane(k * ustride), 0));
+    }
   };
-  auto store = [&](int st, float (&raw)[IT][P], const f32x2 (&ur)[UL]) {
+  auto store = [&](int st, float (&raw)[IT][P], const f32x2 (&ur)[ULR], const f32x4 (&ub)[UBR]) {
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
       const int row = lt + NT / 8 * h, c = lc ^ swz(row);
@@ -225,8 +249,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
         for (int bb = 0; bb < A; ++bb) Vs[st][a * A + bb][row][c] = o[bb];
       }
     }
+    if constexpr (UB) {   // the global image is the LDS image: a straight 16-B copy
+      float* const us = &Us[st][0][0][0];
 #pragma unroll
-    for (int k = 0; k < UL; ++k) *(f32x2*)&Us[st][upos + UPK * k][uco][(2 * upr) ^ swz(uco)] = ur[k];
+      for (int k = 0; k < UBL; ++k)
+        if (tid + NT * k < UNITS) *(f32x4*)(us + 4 * (tid + NT * k)) = ub[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < UL; ++k) *(f32x2*)&Us[st][upos + UPK * k][uco][(2 * upr) ^ swz(uco)] = ur[k];
+    }
   };
 
   f32x4 acc[P];
@@ -254,35 +285,37 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
     }
   };
   float rA[IT][P];
-  f32x2 uA[UL];
+  f32x2 uA[ULR];
+  f32x4 bA[UBR];
   if constexpr (NS == 1) {
-    load(0, rA, uA);
-    store(0, rA, uA);
+    load(0, rA, uA, bA);
+    store(0, rA, uA, bA);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-      if (c + 1 < nch) load((c + 1) * KC, rA, uA);
+      if (c + 1 < nch) load((c + 1) * KC, rA, uA, bA);
       mfma(0);
       if (c + 1 < nch) {
         __syncthreads();                   // every wave is done reading the stage
-        store(0, rA, uA);
+        store(0, rA, uA, bA);
       }
       __syncthreads();
     }
   } else {
     float rB[IT][P];
-    f32x2 uB[UL];
-    load(0, rA, uA);
-    load(KC, rB, uB);
-    store(0, rA, uA);
+    f32x2 uB[ULR];
+    f32x4 bB[UBR];
+    load(0, rA, uA, bA);
+    load(KC, rB, uB, bB);
+    store(0, rA, uA, bA);
     __syncthreads();
     for (int c = 0; c < nch; c += 2) {
-      load((c + 2) * KC, rA, uA);
+      load((c + 2) * KC, rA, uA, bA);
       mfma(0);                             // chunk c
-      store(1, rB, uB);                    // chunk c + 1, in the MFMAs' shadow
+      store(1, rB, uB, bB);                // chunk c + 1, in the MFMAs' shadow
       __syncthreads();
-      load((c + 3) * KC, rB, uB);
+      load((c + 3) * KC, rB, uB, bB);
       mfma(1);                             // chunk c + 1 (zeros past the end)
-      store(0, rA, uA);                    // chunk c + 2
+      store(0, rA, uA, bA);                // chunk c + 2
       __syncthreads();
     }
   }
@@ -824,6 +857,60 @@ __global__ __launch_bounds__(256) void x6p_wt_multi_kernel(const float* __restri
                  (int)m[4], d.y, d.z, g);
 }
 
+// element (pos, r, c) of a set with R output rows and C input columns (C % 8 == 0) in the blocked layout of
+// the fused forward kernel's weight stage: [R / 32 rounded up][C / 8][36][32][8], column swizzled
+RK_DEV long long w4b_index(int pos, int r, int c, int C) {
+  const int rb = r >> 5, rr = r & 31, ch = c >> 3, lc = c & 7;
+  return ((((long long)rb * (C >> 3) + ch) * 36 + pos) * 32 + rr) * 8 + (lc ^ swz(rr));
+}
+
+// one 32 co x 32 ci block of filters -> the blocked forward set ub (rows co, columns ci) and / or the blocked
+// data-gradient set utb (rows ci, columns co, flipped filters); either may be null
+RK_DEV void w4b_block(const float* __restrict__ w, float* __restrict__ ub, float* __restrict__ utb, int Co, int Ci,
+                      int co0, int ci0, float (&g)[32][9][33]) {
+  float st[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    const int ci = i & 31, t = (i >> 5) % 9, co = i / (9 * 32);
+    st[k] = (co0 + co < Co && ci0 + ci < Ci) ? w[((long long)(co0 + co) * 9 + t) * Ci + ci0 + ci] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    g[i / (9 * 32)][(i >> 5) % 9][i & 31] = st[k];
+  }
+  __syncthreads();
+  if (ub != nullptr)
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+      const int ci = i & 31, co = i >> 5;
+      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
+      float gg[9], U[36];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) gg[t] = g[co][t][ci];
+      w4_transform(gg, U);
+#pragma unroll
+      for (int q = 0; q < 36; ++q) ub[w4b_index(q, co0 + co, ci0 + ci, Ci)] = U[q];
+    }
+  if (utb != nullptr)
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+      const int co = i & 31, ci = i >> 5;
+      if (co0 + co >= Co || ci0 + ci >= Ci) continue;
+      float gg[9], U[36];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) gg[t] = g[co][8 - t][ci];
+      w4_transform(gg, U);
+#pragma unroll
+      for (int q = 0; q < 36; ++q) utb[w4b_index(q, ci0 + ci, co0 + co, Co)] = U[q];
+    }
+}
+
+__global__ __launch_bounds__(256) void w4b_wt_kernel(const float* __restrict__ w, float* __restrict__ ub,
+                                                     float* __restrict__ utb, int Co, int Ci) {
+  __shared__ float g[32][9][33];
+  w4b_block(w, ub, utb, Co, Ci, blockIdx.y * 32, blockIdx.x * 32, g);
+}
+
 __global__ __launch_bounds__(256) void wt_all_kernel(const float* __restrict__ arena, float* __restrict__ dst,
                                                      const int4* __restrict__ desc, const long long* __restrict__ meta) {
   __shared__ float g[32][9][33];
@@ -835,10 +922,12 @@ __global__ __launch_bounds__(256) void wt_all_kernel(const float* __restrict__ a
   } else if (d.w == 1) {
     w4_block<false>(w, m[1] >= 0 ? dst + m[1] : nullptr, m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4], d.y,
                     d.z, g);
-  } else {
+  } else if (d.w == 2) {
     bf16* db = (bf16*)dst;
     w4_block<true>(w, m[1] >= 0 ? db + m[1] : nullptr, m[2] >= 0 ? db + m[2] : nullptr, (int)m[3], (int)m[4], d.y,
                    d.z, g);
+  } else {
+    w4b_block(w, m[1] >= 0 ? dst + m[1] : nullptr, m[2] >= 0 ? dst + m[2] : nullptr, (int)m[3], (int)m[4], d.y, d.z, g);
   }
 }
 
@@ -847,6 +936,7 @@ __global__ __launch_bounds__(256) void x6p_wt_kernel(const float* __restrict__ w
   __shared__ float g[32][9][33];
   w4_block<true>(w, u, ut, Co, Ci, blockIdx.y * 32, blockIdx.x * 32, g);
 }
+
 
 }  // namespace
 
@@ -860,7 +950,8 @@ extern "C" int rk_wino4_weights(const float* w, float* u, float* ut, int Co, int
 }
 
 // Every live Winograd weight set of a network, all families, in ONE launch: desc[block] = (meta row, co0,
-// ci0, family), family 0 F(2x2) fp32 sets, 1 F(4x4) fp32 sets, 2 F(4x4) X6 bf16 planes; meta rows as the
+// ci0, family), family 0 F(2x2) fp32 sets, 1 F(4x4) fp32 sets, 2 F(4x4) X6 bf16 planes, 3 blocked F(4x4) fp32
+// sets of the UB fused kernels; meta rows as the
 // per-family kernels' (offsets in floats of dst, bf16 elements of dst for family 2).  Replaces three
 // launches, two of them a few dozen latency-bound blocks (profiles/vgg_small_f32_step_kernels_r4*).
 extern "C" int rk_wino_weights_all(const float* arena, float* dst, const int* desc, int nblocks,
@@ -872,6 +963,17 @@ extern "C" int rk_x6p_w4_weights(const float* w, void* u, void* ut, int Co, int 
   if (108ll * Co * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
   const dim3 grid(rk_cdiv(Ci, 32), rk_cdiv(Co, 32));
   hipLaunchKernelGGL(x6p_wt_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, (bf16*)u, (bf16*)ut, Co, Ci);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// blocked forward / data-gradient sets (either nullable) of w [Co][9][Ci] for the UB fused kernels:
+// ub holds ceil(Co / 32) * 32 * Ci * 36 floats, utb ceil(Ci / 32) * 32 * Co * 36 (zero padding rows stay
+// as the caller initialised them); Ci % 8 == 0 for ub, Co % 8 == 0 for utb
+extern "C" int rk_wino4b_weights(const float* w, float* ub, float* utb, int Co, int Ci, void* stream) {
+  if (Co <= 0 || Ci <= 0 || (!ub && !utb) || (ub && Ci % 8) || (utb && Co % 8)) return RK_EBADARG;
+  const dim3 grid(rk_cdiv(Ci, 32), rk_cdiv(Co, 32));
+  hipLaunchKernelGGL(w4b_wt_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, ub, utb, Co, Ci);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -906,7 +1008,7 @@ extern "C" int rk_wino4_weights_multi(const float* arena, float* dst, const int*
 namespace {
 // shared launcher of the small-wave-tile Winograd forward kernels: MO = 4 (u [36][N][C], H, W multiples
 // of 4) or MO = 2 (u [16][N][C], even H, W); T tiles x BNC channels per block of NT threads
-template <int MO, int WM, int WN, int MINW, int NS = 1>
+template <int MO, int WM, int WN, int MINW, int NS = 1, bool UB = false>
 int launch_gfwd(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
                 const float* gate, int Nb, int H, int W, int C, int N, int flags, int groups, long long gx,
                 long long gu, long long gy, long long gbias, void* stream) {
@@ -927,7 +1029,7 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   p.ntiles = (int)nt;
   p.ncb = rk_cdiv(N, BNC);
   p.xbytes = 4ull * Nb * H * W * C;
-  p.ubytes = 4ull * P * N * C;
+  p.ubytes = UB ? 4ull * P * rk_cdiv(N, 32) * 32 * C : 4ull * P * N * C;
   p.ybytes = 4ull * Nb * H * W * N;
   const unsigned long long gbytes = (flags & WF_BNP) ? 4 * p.ybytes : p.ybytes;
   if (p.xbytes >= 0x7fffffffull || p.ubytes >= 0x7fffffffull || gbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
@@ -941,14 +1043,16 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   const dim3 grid((unsigned)blocks), block(64 * WM * WN);
   const hipStream_t st = (hipStream_t)stream;
   switch (flags) {
-    case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0, NS>), grid, block, 0, st, p); break;
-    case WF_STATS: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS, NS>), grid, block, 0, st, p); break;
-    case WF_BNB: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNB, NS>), grid, block, 0, st, p); break;
-    case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP, NS>), grid, block, 0, st, p); break;
-    case WF_BIAS | WF_RELU:
-      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU, NS>), grid, block, 0, st, p);
+    case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0, NS, UB>), grid, block, 0, st, p); break;
+    case WF_STATS:
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS, NS, UB>), grid, block, 0, st, p);
       break;
-    default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1, NS>), grid, block, 0, st, p); break;
+    case WF_BNB: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNB, NS, UB>), grid, block, 0, st, p); break;
+    case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP, NS, UB>), grid, block, 0, st, p); break;
+    case WF_BIAS | WF_RELU:
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU, NS, UB>), grid, block, 0, st, p);
+      break;
+    default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1, NS, UB>), grid, block, 0, st, p); break;
   }
   RK_LAUNCH_CHECK();
   return RK_OK;
@@ -970,6 +1074,13 @@ extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const
   if (variant == 2)   // 4 waves, 32 x 32, two LDS stages (147 KiB), software-pipelined
     return launch_gfwd<4, 2, 2, 1, 2>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu,
                                       gy, gbias, stream);
+  // blocked weights (rk_wino4b_weights layout): variant 3 = variant 0's tile, 4 = variant 1's
+  if (variant == 3)
+    return launch_gfwd<4, 4, 2, 1, 1, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx,
+                                            gu, gy, gbias, stream);
+  if (variant == 4)
+    return launch_gfwd<4, 2, 2, 2, 1, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx,
+                                            gu, gy, gbias, stream);
   return RK_EBADARG;
 }
 

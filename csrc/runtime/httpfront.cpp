@@ -299,13 +299,15 @@ bool parse_npy_u8(const char* b, long long n, long long* count, long long* shape
     dims[nd++] = v;
   }
   if (nd < 2 || nd > 9) return false;
+  // every product is checked BEFORE it is formed (dims <= 2^40, so a later multiply could wrap int64)
+  constexpr long long kMaxBytes = 1ll << 40;
   long long per = 1;
   for (int k = 1; k < nd; ++k) {
-    if (dims[k] <= 0) return false;
+    if (dims[k] <= 0 || dims[k] > kMaxBytes / per) return false;
     per *= dims[k];
-    if (per > (1ll << 40)) return false;
   }
-  if (dims[0] <= 0 || dims[0] * per != n - h0 - hl) return false;
+  const long long body = n - h0 - hl;
+  if (dims[0] <= 0 || body <= 0 || dims[0] > kMaxBytes / per || dims[0] * per != body) return false;
   *count = dims[0];
   *ndim = nd - 1;
   for (int k = 1; k < nd; ++k) shape[k - 1] = dims[k];

@@ -17,6 +17,12 @@ Per conv block (conv3x3 -> BatchNorm -> ReLU [-> maxpool2x2]) the step runs
         (epilogue: the input layer's ReLU mask / max-pool routing + BN-backward sums)
 then one fused SGD/Adam pass over the flat parameter arena.
 
+``bn=False`` builds conv3x3 + bias + ReLU blocks instead (Keras VGG16, TfVgg16.py:115-130, has no
+BatchNorm): the conv epilogue adds the bias (and applies the ReLU when no max-pool follows); the same
+backward kernels run with the constant coefficients (mean 0, rstd 1, scale 1, shift 0) and an
+infinite count, which turns the BN-backward apply into the ReLU mask / max-pool routing alone and
+its per-channel sum of dz into the bias gradient.
+
 VGG-small (the BASELINE benchmark architecture; the reference's TfVgg16.py:115-130 is 48x48x3
 VGG16 without BN — SURVEY §7.4 item 8 asks for an explicit definition):
   input 32x32x3 (zero-padded to 8 channels)
@@ -115,7 +121,7 @@ class ConvNetEngine:
                  cfg: Sequence = VGG_SMALL_CFG, fc_dims: Sequence[int] = (512,), device='cuda', seed: int = 0,
                  bn_eps: float = 1e-5, bn_momentum: float = 0.1, optimizer: str = 'sgd', lr: float = 0.05,
                  momentum: float = 0.9, weight_decay: float = 5e-4, nesterov: bool = True,
-                 betas=(0.9, 0.999), input_bn: bool = False, dtype: Optional[str] = None):
+                 betas=(0.9, 0.999), input_bn: bool = False, dtype: Optional[str] = None, bn: bool = True):
         self.device = torch.device(device)
         self.dtype = dtype or default_dtype()
         if self.dtype not in DTYPES:
@@ -131,6 +137,9 @@ class ConvNetEngine:
                       else _pad8(in_channels))
         self.ncls_p = _pad8(num_classes)
         self.bn_eps, self.bn_momentum = bn_eps, bn_momentum
+        self.bn = bool(bn)
+        if not self.bn and not self.f32:
+            raise ValueError('bn=False (conv + bias + ReLU blocks) runs on the fp32 engine')
         self.input_bn = bool(input_bn)
         if self.input_bn and not self.flat_input:
             raise ValueError('input_bn is for fully-connected nets (no conv blocks)')
@@ -147,8 +156,11 @@ class ConvNetEngine:
             name = 'conv{}'.format(i)
             zero = slice(real_cin, None) if real_cin < cin else None
             flat.add(name + '.w', (v, 3, 3, cin), init_kaiming(9 * real_cin, zero_in_slice=zero))
-            flat.add(name + '.gamma', (v,), init_const(1.0), decay=False)
-            flat.add(name + '.beta', (v,), init_const(0.0), decay=False)
+            if self.bn:
+                flat.add(name + '.gamma', (v,), init_const(1.0), decay=False)
+                flat.add(name + '.beta', (v,), init_const(0.0), decay=False)
+            else:
+                flat.add(name + '.b', (v,), init_const(0.0), decay=False)
             self.blocks.append((name, cin, v, pool, hw))
             if pool:
                 hw //= 2
@@ -179,15 +191,21 @@ class ConvNetEngine:
         self.flat = flat.build()
         self.d_last = d_in
         self.d_last_real = d_in_real
-        C = sum(b[2] for b in self.blocks) + (self.feat_dim if self.input_bn else 0)
+        C = (sum(b[2] for b in self.blocks) if self.bn else 0) + (self.feat_dim if self.input_bn else 0)
         self.running = torch.zeros((2, C), dtype=torch.float32, device=self.device)
         self.running[1].fill_(1.0)
         self._roff = []
         off = 0
         for b in self.blocks:
             self._roff.append(off)
-            off += b[2]
+            off += b[2] if self.bn else 0
         self._in_roff = off
+        # bn=False: per block the constant BN-backward coefficients [4][C] (mean 0, rstd 1, scale 1, shift 0)
+        # and a unit gamma, built once (no allocation inside a captured step)
+        self._nobn_coeffs = [] if self.bn else [
+            torch.tensor([[0.0], [1.0], [1.0], [0.0]]).expand(4, b[2]).contiguous().to(self.device)
+            for b in self.blocks]
+        self._ones = None if self.bn else torch.ones(max([b[2] for b in self.blocks] or [1]), device=self.device)
         if optimizer == 'adam':
             self.opt = FlatAdam(self.flat, lr, betas=betas, weight_decay=weight_decay, decoupled=True)
         else:
@@ -208,6 +226,24 @@ class ConvNetEngine:
         else:
             o, c = self._roff[bi], self.blocks[bi][2]
         return self.running[0, o:o + c], self.running[1, o:o + c]
+
+    def _block_coeffs(self, bi):
+        """bn=False: the [4][C] constant coefficients of block ``bi``."""
+        return self._nobn_coeffs[bi]
+
+    def real_param_count(self) -> int:
+        """Trainable parameters of the network as defined (channel / class padding excluded)."""
+        n, real_cin = 0, self.in_channels
+        for (_, cin, cout, _, _) in self.blocks:
+            n += cout * 9 * real_cin + 2 * cout if self.bn else cout * 9 * real_cin + cout
+            real_cin = cout
+        d_in = self.in_dim if self.flat_input else self.feat_hw * self.feat_hw * real_cin
+        if self.input_bn:
+            n += 2 * d_in
+        for (_, _, _, d) in self.fcs:
+            n += d * d_in + d
+            d_in = d
+        return n + self.num_classes * d_in + self.num_classes
 
     def train_flops_per_image(self) -> float:
         """Model FLOPs of one training image as a direct computation: forward + data gradient +
@@ -390,11 +426,22 @@ class ConvNetEngine:
             ww.refresh()   # one launch per family: the live Winograd-domain weight sets of every block
         acts, saved, h = [x], [], x
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
+            wk = dict(wino=ww.lazy('u2', bi) if ww is not None else None,
+                      wino4=ww.lazy('u4', bi) if ww is not None else None,
+                      wino4p=ww.lazy('u4p', bi) if ww is not None else None,
+                      wino4b=ww.lazy('u4b', bi) if ww is not None else None)
+            if not self.bn:
+                # conv + bias (+ ReLU in the epilogue when no pool follows; the saved post-ReLU output
+                # gives the same mask); a pooled block runs ReLU + max-pool in the eval-BN kernel
+                c = self._block_coeffs(bi)
+                y = S.conv_fwd(h, fl.w(name + '.w'), bias=fl.w(name + '.b'),
+                               act=F.ACT_NONE if pool else F.ACT_RELU, **wk)
+                h = S.bn_eval(y, c[2], c[3], pool=True, act=F.ACT_RELU) if pool else y
+                saved.append((y, c))
+                acts.append(h)
+                continue
             rm, rv = self.running_stats(bi)
-            y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0],
-                           wino=ww.lazy('u2', bi) if ww is not None else None,
-                           wino4=ww.lazy('u4', bi) if ww is not None else None,
-                           wino4p=ww.lazy('u4p', bi) if ww is not None else None)
+            y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0], **wk)
             h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
                                  self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
             saved.append((y, coeffs))
@@ -467,8 +514,12 @@ class ConvNetEngine:
         for bi in range(len(self.blocks) - 1, -1, -1):
             name, cin, cout, pool, hw = self.blocks[bi]
             y, coeffs = saved[bi]
-            dy = S.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), accs[bi][1], pool=pool, act=F.ACT_RELU,
-                          dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'), reduced=reduced)
+            if self.bn:
+                dy = S.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), accs[bi][1], pool=pool, act=F.ACT_RELU,
+                              dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'), reduced=reduced)
+            else:   # ReLU mask / pool routing only; sum dz -> the bias gradient
+                dy = S.bn_bwd(d, y, coeffs, self._ones[:cout], accs[bi][1], pool=pool, act=F.ACT_RELU,
+                              dbeta=fl.g(name + '.b'), reduced=reduced, count=float('inf'))
             if side is not None and hw <= self.overlap_max_hw:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
@@ -484,17 +535,19 @@ class ConvNetEngine:
             wu = ww.lazy('ut2', bi) if ww is not None else None
             wu4 = ww.lazy('ut4', bi) if ww is not None else None
             wu4p = ww.lazy('ut4p', bi) if ww is not None else None
+            wu4b = ww.lazy('ut4b', bi) if ww is not None else None
             wl = wt.lazy(bi - 1)
+            dk = dict(wino=wu, wino4=wu4, cin=cin, wino4p=wu4p, wino4b=wu4b)
             if not ppool:
                 # the input block is BN+ReLU: its mask and BN-backward sums ride in this dgrad's epilogue
-                d = S.conv_dgrad(dy, wl, bnb=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin, wino4p=wu4p)
+                d = S.conv_dgrad(dy, wl, bnb=(py, pco, accs[bi - 1][1]), **dk)
                 reduced = True
             elif phw == 2 * hw and not (hw & (hw - 1)):
                 # BN+ReLU+max-pool input (even power-of-two geometry): pool routing + sums in the epilogue
-                d = S.conv_dgrad(dy, wl, bnp=(py, pco, accs[bi - 1][1]), wino=wu, wino4=wu4, cin=cin, wino4p=wu4p)
+                d = S.conv_dgrad(dy, wl, bnp=(py, pco, accs[bi - 1][1]), **dk)
                 reduced = True
             else:
-                d = S.conv_dgrad(dy, wl, wino=wu, wino4=wu4, cin=cin, wino4p=wu4p)
+                d = S.conv_dgrad(dy, wl, **dk)
                 reduced = False
         if side is not None:
             main.wait_stream(side)
@@ -568,6 +621,10 @@ class ConvNetEngine:
         h = up(x_nhwc).permute(0, 3, 1, 2) if x_nhwc.dim() == 4 else up(x_nhwc)
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             w = rndw(P[name + '.w']).permute(0, 3, 1, 2)
+            if not self.bn:
+                h = torch.relu(TF.conv2d(h, w, P[name + '.b'], padding=1))
+                h = rnd(TF.max_pool2d(h, 2) if pool else h)
+                continue
             h = rnd(TF.conv2d(h, w, padding=1))
             rm, rv = self.running_stats(bi)
             if not update_running:
@@ -794,6 +851,10 @@ class ConvNetEngine:
         if self.input_bn:
             items.append(('in', 'in_bn'))
         for bi, name in items:
+            if bi != 'in' and not self.bn:   # conv bias as the shift (the eval conv runs without bias)
+                b = fl.w(name + '.b').detach()
+                coeffs.append(torch.stack([torch.zeros_like(b), torch.ones_like(b), torch.ones_like(b), b.clone()]))
+                continue
             rm, rv = self.running_stats(bi)
             if self.device.type == 'cuda':
                 c = F.bn_eval_coeffs(fl.w(name + '.gamma'), fl.w(name + '.beta'), rm, rv, self.bn_eps)
@@ -945,7 +1006,7 @@ class GroupedConvNets:
         if not isinstance(eng, ConvNetEngine) or not eng.f32 or eng.input_bn or eng.flat_input:
             return None
         return (tuple(eng.blocks), tuple(eng.fcs), eng.num_classes, eng.ncls_p, eng.cin_p, eng.image_size,
-                eng.feat_dim, str(eng.device))
+                eng.feat_dim, str(eng.device), eng.bn)
 
     def __init__(self, engines):
         keys = {self.arch_key(e) for e in engines}

@@ -144,6 +144,7 @@ class CorpusDataset(ModelDataset):
 
 # ------------------------------------------------------------------------------- synthetic data
 _BANKS = {}
+_BANK_BYTES = 256 << 20   # host bytes of the shared noise bank at most (default bank size)
 
 
 def _noise_bank(shape, nb):
@@ -168,7 +169,8 @@ def synthetic_images(n, size=32, channels=3, classes=10, seed=0, separable=True,
     float32 — a CIFAR-sized split (50k x 32x32x3) takes a fraction of a second instead of drawing 150M
     normals, which dominated a benchmark trial's first dataset load.  The bank is shared by all splits
     and seeds and has at least as many images as pixels (default max(4096, dim)), so every split's noise
-    has the same full-rank distribution; the seed picks the labels, pairs and angles.  (Round 3 drew a
+    has the same full-rank distribution (above 8192 values per image, e.g. 64x64x3, the bank is capped at
+    256 MB of host memory, so its rank is the bank size); the seed picks the labels, pairs and angles.  (Round 3 drew a
     1024-image bank per seed — a rank-1024 noise subspace that differed between train and test — so
     scores on this data are not comparable with that round's.)"""
     rng = np.random.default_rng(seed)
@@ -178,7 +180,10 @@ def synthetic_images(n, size=32, channels=3, classes=10, seed=0, separable=True,
     templates = templates * np.float32(0.6) + np.float32(50.0)
     labels = rng.integers(0, classes, size=n)
     std = np.float32(noise if noise is not None else (48.0 if separable else 96.0))
-    nb = int(bank) if bank is not None else max(4096, int(np.prod(shape)))
+    dim = int(np.prod(shape))
+    # full rank (>= dim images) while that fits the byte budget; large images cap the bank instead of
+    # growing it with the square of the pixel count (128x128x3 would need ~9.7 GB at full rank)
+    nb = int(bank) if bank is not None else max(1024, min(max(4096, dim), _BANK_BYTES // (4 * dim)))
     B = _noise_bank(shape, nb)
     j1, j2 = rng.integers(0, nb, size=n), rng.integers(0, nb, size=n)
     th = rng.uniform(0.0, 2.0 * np.pi, size=n)

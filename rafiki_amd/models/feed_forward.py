@@ -2,7 +2,7 @@
 -> Dense -> softmax cross-entropy, Adam.
 
 Reference: examples/models/image_classification/TfFeedForward.py:14-164 (knobs :20-28: epochs
-Fixed 2 [here a range], hidden_layer_count Int(1,2), hidden_layer_units Int(2,128),
+Fixed 2, hidden_layer_count Int(1,2), hidden_layer_units Int(2,128),
 learning_rate Float(1e-5,1e-1,exp), batch_size Cat(16..128), image_size Fixed 32).
 """
 from rafiki_amd.constants import TaskType  # noqa: F401
@@ -16,7 +16,7 @@ class FeedForward(NativeImageClassifier):
     @staticmethod
     def get_knob_config():
         return {
-            'epochs': FixedKnob(3),
+            'epochs': FixedKnob(2),
             'hidden_layer_count': IntegerKnob(1, 2),
             'hidden_layer_units': IntegerKnob(2, 128),
             'learning_rate': FloatKnob(1e-5, 1e-1, is_exp=True),
@@ -41,5 +41,5 @@ if __name__ == '__main__':
     test_model_class(__file__, 'FeedForward', TaskType.IMAGE_CLASSIFICATION, {},
                      'synthetic://image?n=4096&size=28&channels=1&classes=10&seed=0',
                      'synthetic://image?n=1024&size=28&channels=1&classes=10&seed=1',
-                     knobs={'epochs': 3, 'hidden_layer_count': 2, 'hidden_layer_units': 36, 'learning_rate': 0.01,
+                     knobs={'epochs': 2, 'hidden_layer_count': 2, 'hidden_layer_units': 36, 'learning_rate': 0.01,
                             'batch_size': 32, 'image_size': 28})

@@ -4,11 +4,12 @@ TfVgg16.py:15-130): 13 conv3x3 layers (64,64 / 128,128 / 256x3 / 512x3 / 512x3, 
 inputs are stacked to three channels (TfVgg16.py:43).  Same knobs (epochs Fixed(1), learning_rate,
 batch_size).
 
-Runs on the gfx950 static-graph engine: the 48/24/12/6/3 maps use the implicit-GEMM conv's
+Runs on the gfx950 static-graph engine as the reference's network: conv3x3 + bias + ReLU blocks,
+no BatchNorm (Keras VGG16, TfVgg16.py:115-130), 33.6 M parameters at 48x48x3 with 10 classes
+(``ConvNetEngine(bn=False)``, fp32).  The ``batch_norm`` knob (default False) opts into the engine's
+conv + BN + ReLU blocks instead.  The 48/24/12/6/3 maps use the implicit-GEMM conv's
 reciprocal-decoded pixel gather (non-power-of-two extents), the 3 -> 1 pool the floor-mode odd
-pooling path.  Deviation: each conv is followed by BatchNorm (the engine's fused conv+BN+ReLU
-block); Keras' VGG16 has none, and BN makes the Adam learning-rate range of the knob trainable from
-scratch.
+pooling path.
 """
 import numpy as np
 
@@ -28,6 +29,7 @@ class Vgg16(NativeImageClassifier):
             'epochs': FixedKnob(1),
             'learning_rate': FloatKnob(1e-5, 1e-2, is_exp=True),
             'batch_size': CategoricalKnob([16, 32, 64, 128]),
+            'batch_norm': FixedKnob(False),
         }
 
     def _load(self, uri):
@@ -37,8 +39,12 @@ class Vgg16(NativeImageClassifier):
         return images, labels, classes
 
     def _engine_kwargs(self, num_classes, channels, image_size):
-        return dict(cfg=VGG16_CFG, fc_dims=(4096, 4096), optimizer='adam',
-                    lr=float(self._knobs.get('learning_rate', 1e-3)), weight_decay=0.0)
+        bn = bool(self._knobs.get('batch_norm', False))
+        kw = dict(cfg=VGG16_CFG, fc_dims=(4096, 4096), optimizer='adam',
+                  lr=float(self._knobs.get('learning_rate', 1e-3)), weight_decay=0.0, bn=bn)
+        if not bn:
+            kw['dtype'] = 'fp32'   # the conv + bias + ReLU blocks run on the fp32 engine
+        return kw
 
 
 if __name__ == '__main__':

@@ -71,6 +71,7 @@ _SIGS = {
     "rk_wino_wgrad": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "rk_wino_conv": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "rk_wino4_weights": [vp, vp, vp, i32, i32, vp],
+    "rk_wino4b_weights": [vp, vp, vp, i32, i32, vp],
     "rk_wino4_weights_multi": [vp, vp, vp, i32, vp, vp],
     "rk_wino4_conv_grp": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, vp],
     "rk_wino4_conv": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp],

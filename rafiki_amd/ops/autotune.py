@@ -85,8 +85,7 @@ def lib_hash() -> str:
 
 # switches that change the candidate sets (not the kernels): a non-default setting tunes into its own
 # database file, so a pick made among more candidates is never replayed where they are switched off
-_CAND_SWITCHES = ('RAFIKI_X6', 'RAFIKI_PT_MAX_HW', 'RAFIKI_WINOGRAD', 'RAFIKI_WINOGRAD4',
-                  'RAFIKI_WINO_PIPE')
+_CAND_SWITCHES = ('RAFIKI_X6', 'RAFIKI_PT_MAX_HW', 'RAFIKI_WINOGRAD', 'RAFIKI_WINOGRAD4')
 
 
 def db_name() -> str:

@@ -163,7 +163,7 @@ def _slots_flags(acc):
 
 # ------------------------------------------------------------------------------------------ conv
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None, bias=None, act=ACT_NONE,
-             slope=0.2, out=None, wino=None, wino4=None, wino4p=None):
+             slope=0.2, out=None, wino=None, wino4=None, wino4p=None, wino4b=None):
     """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
     [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue.
     ``wino``: the layer's Winograd weights (WinoWeights.u), or a callable producing them (run only
@@ -182,6 +182,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
 
     use_w = wino is not None and taps == 9 and wino_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
+    use_w4b = wino4b is not None and taps == 9 and wino4_ok(H, W, Cin) and act in (ACT_NONE, ACT_RELU)
     # the pre-transformed paths also carry a leaky-ReLU epilogue (no statistics with it): PG-GAN's D convs
     act_pt = act in (ACT_NONE, ACT_RELU) or (act == ACT_LRELU and stats_acc is None)
     use_pt = (wino4 is not None and taps == 9 and wino4_ok(H, W, Cin) and act_pt and wino4_pt_ok(H, W, Cin, Cout))
@@ -202,6 +203,10 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
             wino4_conv(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
                        relu=act == ACT_RELU, variant=_wino4_variant(cfg))
             return
+        if cfg in WINO4B_CFGS:
+            wino4_conv(x, wino4b() if callable(wino4b) else wino4b, out=out, bias=bias, stats=stats_acc,
+                       relu=act == ACT_RELU, variant=_WINO4B_VARIANT[cfg[0]], n_out=Cout)
+            return
         if cfg in WINO_CFGS:
             wino_conv(x, wino() if callable(wino) else wino, out=out, bias=bias, stats=stats_acc,
                       relu=act == ACT_RELU, variant=_wino_variant(cfg))
@@ -221,12 +226,15 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         cands.extend(WINO_CFGS)
     if use_w4:
         cands.extend(WINO4_CFGS)
+    if use_w4b:
+        cands.extend(WINO4B_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
     if use_ptx:
         cands.extend(WINO4_PTX_CFGS)
     cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4, use_pt, 'lazy' if callable(wino4p) else use_ptx), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt, 'lazy' if callable(wino4p) else use_ptx)
+                + (('b', 'lazy' if callable(wino4b) else True),) * use_w4b, cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -234,7 +242,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
 
 
 def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=None, bnp=None,
-               wino=None, wino4=None, cin=None, wino4p=None):
+               wino=None, wino4=None, cin=None, wino4p=None, wino4b=None):
     """dx = data gradient of a 3x3 conv as conv3x3(dy, wt) with wt = SConvWT.view() [Cin][taps*Cout].
     Epilogue options: ``gate`` (ReLU mask of the input activation), ``bnb = (y, coeffs, acc)`` (the input
     is BN+ReLU(y): mask + BN-backward sums into acc), ``bnp = (y, coeffs, acc)`` (the input is
@@ -262,6 +270,7 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
     # ``wino``: the layer's Winograd data-gradient weights (WinoWeights.ut), one more candidate
     use_w = wino is not None and taps == 9 and wino_ok(H, W, Cout) and not (flags & F_GATE)
     use_w4 = wino4 is not None and taps == 9 and wino4_ok(H, W, Cout) and not (flags & F_GATE)
+    use_w4b = wino4b is not None and taps == 9 and wino4_ok(H, W, Cout) and not (flags & F_GATE)
 
     use_pt = use_w4 and wino4_pt_ok(H, W, Cout, Cin)
     # ``wino4p``: the X6 planes of the data-gradient set (WinoWeights 'ut4p'): the pre-split PT path
@@ -280,6 +289,10 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
             wino4_conv(dy, wino4() if callable(wino4) else wino4, out=out, bnb=bnb, bnp=bnp,
                        variant=_wino4_variant(cfg))
             return
+        if cfg in WINO4B_CFGS:
+            wino4_conv(dy, wino4b() if callable(wino4b) else wino4b, out=out, bnb=bnb, bnp=bnp,
+                       variant=_WINO4B_VARIANT[cfg[0]], n_out=Cin)
+            return
         if cfg in WINO_CFGS:
             wino_conv(dy, wino() if callable(wino) else wino, out=out, bnb=bnb, bnp=bnp, variant=_wino_variant(cfg))
             return
@@ -290,12 +303,15 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
         cands.extend(WINO_CFGS)
     if use_w4:
         cands.extend(WINO4_CFGS)
+    if use_w4b:
+        cands.extend(WINO4B_CFGS)
     if use_pt:
         cands.extend(WINO4_PT_CFGS)
     if use_ptx:
         cands.extend(WINO4_PTX_CFGS)
     cfg = _pick(('sd', M, Cin, K, H, W, Cout, taps, flags, 'lazy' if callable(wino) else use_w,
-                 'lazy' if callable(wino4) else use_w4, use_pt, 'lazy' if callable(wino4p) else use_ptx), cands, run)
+                 'lazy' if callable(wino4) else use_w4, use_pt, 'lazy' if callable(wino4p) else use_ptx)
+                + (('b', 'lazy' if callable(wino4b) else True),) * use_w4b, cands, run)
     if stats is not None and autotune.can_tune():
         stats.zero_()
     run(cfg)
@@ -407,10 +423,9 @@ WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
 # and the 16x16-wave-tile kernels of winograd4.hip: 4-wave 32x32 (variant 2), 2-wave 16x32 (variant 3),
 # 8-wave 64x32 (variant 4)
 # software-pipelined (two LDS stage) variants: the F(2x2) 8-wave one wins the 4x4-map layers and is a
-# default candidate; the F(4x4) ones (one wave per SIMD) measured 1.3-1.5x slower than the single-stage
-# kernels on every VGG-small layer (profiles/winograd_variants_r2e.jsonl) and join the candidates only
-# with RAFIKI_WINO_PIPE=1
-WINO_PIPE = os.environ.get('RAFIKI_WINO_PIPE', '0') != '0'
+# candidate; the F(4x4) ones (one wave per SIMD) measured 1.3-1.5x slower than the single-stage kernels on
+# every VGG-small layer (profiles/winograd_variants_r2e.jsonl) and are not offered to the tuner (kept
+# callable as variant 2 of rk_wino4_conv / rk_wino4_wgrad_v, exercised by tests/test_winograd4_gpu.py)
 WINO_CFGS = ((-1, 0, 1), (-2, 0, 1), (-8, 0, 1), (-9, 0, 1), (-10, 0, 1), (-12, 0, 1))
 _WINO_VARIANT = {-1: 0, -2: 1, -8: 2, -9: 3, -10: 4, -12: 5}   # -12: 8-wave 64x32, two-stage pipelined
 
@@ -491,7 +506,7 @@ def wino_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=No
 # ----------------------------------------------------------------- Winograd F(4x4, 3x3) forward
 # autotune candidates that run rk_wino4_conv: 8-wave 64 tiles x 32 channels (variant 0) / 4-wave 32 x 32
 # (variant 1) / 4-wave 32 x 32 over two LDS stages, software-pipelined (variant 2)
-WINO4_CFGS = ((-5, 0, 1), (-6, 0, 1)) + (((-11, 0, 1),) if WINO_PIPE else ())
+WINO4_CFGS = ((-5, 0, 1), (-6, 0, 1))
 _WINO4_VARIANT = {-5: 0, -6: 1, -11: 2}
 
 
@@ -523,13 +538,40 @@ def wino4_ut(w: torch.Tensor) -> torch.Tensor:
     return ut
 
 
+# blocked-weight variants of the fused F(4x4) kernel (weights as the kernel's LDS stage image, one contiguous
+# 36-KiB block per 32 output channels x 8 input channels: rk_wino4b_weights / WinoWeights 'u4b' / 'ut4b'):
+# variant 3 = variant 0's 8-wave tile, 4 = variant 1's 4-wave tile
+WINO4B_CFGS = ((-15, 0, 1), (-16, 0, 1))
+_WINO4B_VARIANT = {-15: 3, -16: 4}
+
+
+def wino4b_numel(N: int, C: int) -> int:
+    """Floats of a blocked F(4x4) set with N output rows (padded to 32) and C input columns."""
+    return 36 * cdiv(N, 32) * 32 * C
+
+
+def wino4b_u(w: torch.Tensor, dgrad: bool = False) -> torch.Tensor:
+    """Blocked F(4x4) set (forward, or the data-gradient one) of one conv weight [Cout, 3, 3, Cin]."""
+    Cout = w.shape[0]
+    Cin = w.numel() // (9 * Cout)
+    n = wino4b_numel(Cin, Cout) if dgrad else wino4b_numel(Cout, Cin)
+    ub = torch.zeros(n, device=w.device, dtype=torch.float32)
+    _lib.call("rk_wino4b_weights", _p(w), None if dgrad else _p(ub), _p(ub) if dgrad else None, Cout, Cin, _s())
+    return ub
+
+
 def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None, bnp=None,
-               variant=0):
-    """y = conv3x3(x, w) (stride 1, pad 1) by F(4x4,3x3) from u = wino4_u(w); options as wino_conv."""
+               variant=0, n_out=None):
+    """y = conv3x3(x, w) (stride 1, pad 1) by F(4x4,3x3) from u = wino4_u(w); options as wino_conv.
+    Variants 3 / 4 take the blocked set (wino4b_u / WinoWeights 'u4b'), flat, with ``n_out`` channels."""
     _check(x, 'wino4_conv x')
     Nb, H, W, C = x.shape
-    N = u.shape[1]
-    assert u.shape == (36, N, C) and u.is_contiguous(), (u.shape, x.shape)
+    if variant >= 3:
+        N = int(n_out)
+        assert u.dim() == 1 and u.numel() == wino4b_numel(N, C) and u.is_contiguous(), (u.shape, N, C)
+    else:
+        N = u.shape[1]
+        assert u.shape == (36, N, C) and u.is_contiguous(), (u.shape, x.shape)
     if out is None:
         out = torch.empty((Nb, H, W, N), device=x.device, dtype=torch.float32)
     assert out.shape == (Nb, H, W, N) and out.is_contiguous()
@@ -660,7 +702,7 @@ def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
         return []
     out = []
-    for v, bco in ((0, 32), (1, 64)) + (((2, 32),) if WINO_PIPE else ()):
+    for v, bco in ((0, 32), (1, 64)):
         if v == 1 and Cout < 64:
             continue
         base = cdiv(Cout, bco) * cdiv(Cin, 32)
@@ -895,7 +937,7 @@ class WinoWeights:
     step pays only for the transforms it needs (outside graph capture; the captured step replays the
     narrowed refresh)."""
 
-    KINDS = ('u2', 'ut2', 'u4', 'ut4', 'u4p', 'ut4p')
+    KINDS = ('u2', 'ut2', 'u4', 'ut4', 'u4p', 'ut4p', 'u4b', 'ut4b')
 
     def __init__(self, arena: torch.Tensor, weights, dgrad=True, f4=None, hw=None):
         """hw[l]: the layer's map size (F(4x4) sets only where it is a multiple of 4; None: every layer)."""
@@ -918,8 +960,18 @@ class WinoWeights:
                     kinds.append('u4p')
                 if dgrad and (hw is None or wino4_ptx_ok(hw[l], hw[l], Cout, Cin)):
                     kinds.append('ut4p')
+                # blocked sets of the UB fused kernels (input columns in multiples of 8)
+                if Cin % 8 == 0:
+                    kinds.append('u4b')
+                if dgrad and Cout % 8 == 0:
+                    kinds.append('ut4b')
             for k in kinds:
-                n = 54 * Cout * Cin if k.endswith('p') else (16 if k.endswith('2') else 36) * Cout * Cin
+                if k == 'u4b':
+                    n = wino4b_numel(Cout, Cin)
+                elif k == 'ut4b':
+                    n = wino4b_numel(Cin, Cout)
+                else:
+                    n = 54 * Cout * Cin if k.endswith('p') else (16 if k.endswith('2') else 36) * Cout * Cin
                 self._sets[(k, l)] = (off, n)
                 off += n
         dev = arena.device
@@ -935,7 +987,7 @@ class WinoWeights:
         if live in self._tables:
             return self._tables[live]
         out = []
-        for fam, (ka, kb) in (('2', ('u2', 'ut2')), ('4', ('u4', 'ut4')), ('p', ('u4p', 'ut4p'))):
+        for fam, (ka, kb) in (('2', ('u2', 'ut2')), ('4', ('u4', 'ut4')), ('p', ('u4p', 'ut4p')), ('b', ('u4b', 'ut4b'))):
             scale = 2 if fam == 'p' else 1   # plane sets: offsets in bf16 elements
             meta, desc, idx = [], [], {}
             for l, (so, Cout, Cin) in enumerate(self._layers):
@@ -955,7 +1007,7 @@ class WinoWeights:
         self._tables[live] = out
         # every family in one table for the single-launch refresh (rk_wino_weights_all): meta rows
         # concatenated, each block's desc row = (meta row, co0, ci0, family)
-        fam_id = {'2': 0, '4': 1, 'p': 2}
+        fam_id = {'2': 0, '4': 1, 'p': 2, 'b': 3}
         adesc, ameta, base = [], [], 0
         for fam, desc, meta, nb in out:
             d = desc.view(-1, 4).cpu().clone()
@@ -970,20 +1022,13 @@ class WinoWeights:
                                            sum(int(t.shape[0]) for t in adesc))
         return out
 
-    # one launch for every family (RAFIKI_WT_ALL=0: one launch per family)
-    WT_ALL = os.environ.get('RAFIKI_WT_ALL', '1') != '0'
-
     def refresh(self):
-        tabs = self._prepare(self.live)
+        """Every live set of every family in ONE launch (rk_wino_weights_all)."""
+        self._prepare(self.live)
         allt = self._tables.get(('all', self.live))
-        if self.WT_ALL and allt is not None:
+        if allt is not None:
             desc, meta, nb = allt
             _lib.call("rk_wino_weights_all", _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
-        else:
-            for fam, desc, meta, nb in tabs:
-                name = {'2': "rk_wino_weights_multi", '4': "rk_wino4_weights_multi",
-                        'p': "rk_x6p_w4_weights_multi"}[fam]
-                _lib.call(name, _p(self.arena), _p(self.buf), _p(desc), nb, _p(meta), _s())
         self._fresh = set(self.live)
 
     def end_step(self):
@@ -1002,6 +1047,8 @@ class WinoWeights:
     def _view(self, kind, l):
         off, n = self._sets[(kind, l)]
         _, Cout, Cin = self._layers[l]
+        if kind in ('u4b', 'ut4b'):
+            return self.buf[off:off + n]
         if kind.endswith('p'):
             flat = self.buf[off:off + n].view(torch.bfloat16)
             return flat.view((36, 3, Cout, Cin) if kind == 'u4p' else (36, 3, Cin, Cout))
@@ -1017,6 +1064,8 @@ class WinoWeights:
             name = "rk_wino_weights" if kind.endswith('2') else "rk_wino4_weights"
             if kind.endswith('p'):
                 name = "rk_x6p_w4_weights"
+            if kind.endswith('b'):
+                name = "rk_wino4b_weights"
             if kind.startswith('ut'):
                 _lib.call(name, _p(w), None, _p(v), Cout, Cin, _s())
             else:
@@ -1215,9 +1264,11 @@ _BWD_BLOCKS = int(os.environ.get('RAFIKI_BNF_BWD_BLOCKS', '1024'))
 
 
 def bn_bwd(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, dgamma=None, dbeta=None, dy=None,
-           accumulate=False, reduced=False):
+           accumulate=False, reduced=False, count=None):
     """Backward of out = pool?(act(BN(y))).  ``acc``: zeroed fp64 [SL][2][C] for (sum dz, sum dz*y);
-    ``reduced``: the producer of dout already accumulated them (conv_dgrad(bnb=/bnp=...))."""
+    ``reduced``: the producer of dout already accumulated them (conv_dgrad(bnb=/bnp=...)).
+    ``count`` (default the pixel count): ``inf`` with unit coefficients drops the normalisation terms
+    (dy = the act mask / pool routing of dout; ``dbeta`` = sum dz, a bias gradient)."""
     Nb, H, W, C = y.shape
     s = _s()
     if not reduced:
@@ -1233,7 +1284,8 @@ def bn_bwd(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, 
             raise ValueError('bn_bwd: unsupported channel count {} for pool/act'.format(C))
     if dy is None:
         dy = torch.empty_like(y)
-    _lib.call("rk_bnf_bwd_apply", _p(dout), _p(y), _p(coeffs), _p(acc), acc.shape[0], float(Nb * H * W), _p(gamma),
+    _lib.call("rk_bnf_bwd_apply", _p(dout), _p(y), _p(coeffs), _p(acc), acc.shape[0],
+              float(Nb * H * W) if count is None else float(count), _p(gamma),
               _p(dgamma), _p(dbeta), int(accumulate), _p(dy), Nb, H, W, C, int(pool), int(act), float(slope), s)
     return dy
 

@@ -156,3 +156,80 @@ def world_size(info: DistInfo) -> int:
 def destroy(info: DistInfo):
     if info.world_size > 1 and dist.is_initialized():
         dist.destroy_process_group()
+
+
+def preflight(info: DistInfo, timeout_s: float = 120.0, group=None) -> dict:
+    """Exercise every communication pattern a multi-rank job uses, once, before any timed or trial
+    work: barrier, all_reduce (max), broadcast, all_gather and broadcast_object on the default group,
+    then point-to-point rows rank 0 <-> every peer in both directions on ``group`` (the knob exchange's
+    control group; its communicators are created here, not lazily mid-trial).  A watchdog ends the
+    process with a message naming the step that did not complete within ``timeout_s`` (exit code 3)
+    instead of hanging the node; returns {'ok', 'seconds', 'steps': {name: ms}}."""
+    import sys
+    import threading
+    import time
+    if info.world_size <= 1:
+        return {'ok': True, 'seconds': 0.0, 'steps': {}, 'world_size': 1}
+    state = {'step': 'start'}
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(timeout_s):
+            sys.stderr.write('rafiki preflight: rank {} stuck in step {!r} for {:.0f} s (backend {}, world {}): '
+                             'a peer is missing or the interconnect is not usable; aborting\n'.format(
+                                 info.rank, state['step'], timeout_s, info.backend, info.world_size))
+            sys.stderr.flush()
+            os._exit(3)
+    threading.Thread(target=watchdog, name='rafiki-preflight-watchdog', daemon=True).start()
+    dev = comm_device(info)
+    steps = {}
+    t_all = time.perf_counter()
+
+    def step(name, fn):
+        state['step'] = name
+        t0 = time.perf_counter()
+        out = fn()
+        if dev.type == 'cuda':
+            torch.cuda.synchronize(dev)
+        steps[name] = round((time.perf_counter() - t0) * 1e3, 3)
+        return out
+    try:
+        step('barrier', lambda: barrier(info))
+        mx = step('all_reduce_max', lambda: all_reduce_max(info, float(info.rank)))
+        if mx != float(info.world_size - 1):
+            raise RuntimeError('preflight: all_reduce max {} != {}'.format(mx, info.world_size - 1))
+
+        def bcast():
+            t = torch.full((4,), float(info.rank), dtype=torch.float64, device=dev)
+            dist.broadcast(t, src=0)
+            return float(t[0].item())
+        if step('broadcast', bcast) != 0.0:
+            raise RuntimeError('preflight: broadcast from rank 0 lost')
+        table = step('all_gather', lambda: gather_floats(info, [float(info.rank)]))
+        if table[:, 0].tolist() != [float(r) for r in range(info.world_size)]:
+            raise RuntimeError('preflight: all_gather rows out of order: {}'.format(table[:, 0].tolist()))
+        if step('broadcast_object', lambda: broadcast_object(info, 'rafiki' if info.is_main else None)) != 'rafiki':
+            raise RuntimeError('preflight: broadcast_object lost')
+        g = group if group is not None else dist.group.WORLD
+
+        def p2p():
+            for peer in range(1, info.world_size):
+                if info.rank == peer:
+                    t = torch.full((8,), float(peer), dtype=torch.float64, device=dev)
+                    dist.send(t, dst=0, group=g)
+                    r = torch.empty(8, dtype=torch.float64, device=dev)
+                    dist.recv(r, src=0, group=g)
+                    if float(r[0].item()) != -float(peer):
+                        raise RuntimeError('preflight: rank 0 -> {} row corrupted'.format(peer))
+                elif info.is_main:
+                    r = torch.empty(8, dtype=torch.float64, device=dev)
+                    dist.recv(r, src=peer, group=g)
+                    if float(r[0].item()) != float(peer):
+                        raise RuntimeError('preflight: rank {} -> 0 row corrupted'.format(peer))
+                    dist.send(-r, dst=peer, group=g)
+        step('p2p_rank0_pairs', p2p)
+        step('barrier_end', lambda: barrier(info))
+    finally:
+        done.set()
+    return {'ok': True, 'seconds': round(time.perf_counter() - t_all, 4), 'steps': steps,
+            'world_size': info.world_size, 'backend': info.backend}

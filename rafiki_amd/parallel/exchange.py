@@ -33,6 +33,7 @@ from __future__ import annotations
 import datetime
 import logging
 import math
+import os
 import sys
 import threading
 import time
@@ -92,6 +93,32 @@ class _Channel:
             dist.recv(t, src=peer, group=self.group)
             return t.cpu().tolist()
 
+    def recv_bounded(self, n: int, peer: int, lock, timeout_s: float) -> List[float]:
+        """Rank 0's receive of a row whose doorbell has rung: the receive is POSTED under ``lock``
+        (a launch: never while another thread captures a graph) and waited for outside it, up to
+        ``timeout_s`` — a peer that died between its doorbell and its send leaves a TimeoutError,
+        not a server thread blocked forever while holding the capture lock."""
+        with lock:
+            with self._ctx():
+                t = torch.empty(n, dtype=torch.float64, device=self.dev)
+                work = dist.irecv(t, src=peer, group=self.group)
+        msg = 'knob exchange: rank {} rang its doorbell but sent no row within {:.0f} s'.format(peer, timeout_s)
+        if self.dev.type != 'cuda':
+            # gloo: a receive completes only inside wait(), which takes the deadline itself
+            try:
+                work.wait(timeout=datetime.timedelta(seconds=timeout_s))
+            except RuntimeError as e:
+                raise TimeoutError(msg) from e
+        else:
+            deadline = time.monotonic() + timeout_s
+            while not work.is_completed():   # RCCL: poll the completion event (no host-blocking wait)
+                if time.monotonic() > deadline:
+                    raise TimeoutError(msg)
+                time.sleep(0.0002)
+        if self.stream is not None:
+            self.stream.synchronize()
+        return t.cpu().tolist()
+
 
 class KnobExchange:
     """Rank 0: the advisor + server thread.  Other ranks: a thin client.  Same API on every rank:
@@ -117,6 +144,9 @@ class KnobExchange:
         self.advisor = None
         self._threads = []
         self._error = None
+        self._broken = False
+        # rank 0: how long a doorbell may precede its row (the peer's send follows its push at once)
+        self.recv_timeout_s = float(os.environ.get('RAFIKI_EXCHANGE_RECV_TIMEOUT_S', '120'))
         if info.world_size > 1:
             self.group = control_group(info)
             self.chan = _Channel(info, self.group)
@@ -276,8 +306,18 @@ class KnobExchange:
             if peer < 0:
                 continue   # a local kick: re-check the proposal work
             t0 = time.perf_counter()
-            with graphs.LOCK:
-                row = self.chan.recv(_HDR + len(self.names), peer)
+            try:
+                row = self.chan.recv_bounded(_HDR + len(self.names), peer, graphs.LOCK, self.recv_timeout_s)
+            except TimeoutError as e:
+                # the control group now holds a receive that will never complete: stop serving (rank 0's
+                # own requests raise from here on, so the worker exits and the launcher ends the group)
+                logger.error('%s', e)
+                with self._cv:
+                    self._error = self._error or e
+                    self._broken = True
+                    self._active.clear()
+                    self._cv.notify_all()
+                return
             op, has_prev, score, ok, secs = row[:_HDR]
             op = int(op)
             prev = (self._knobs(row[_HDR:]), score, ok > 0, secs) if has_prev > 0 else None
@@ -313,8 +353,13 @@ class KnobExchange:
             raise RuntimeError('knob exchange: rank 0 could not propose knobs (advisor failed)')
         return self._knobs(rep[1:])
 
+    def _check_broken(self):
+        if self._broken:
+            raise RuntimeError('knob exchange is down (a peer stopped mid-exchange)') from self._error
+
     def request(self, prev=None) -> dict:
         if self.info.is_main:
+            self._check_broken()
             knobs = self._handle(0, OP_REQUEST, prev)
             self._kick()
             return knobs

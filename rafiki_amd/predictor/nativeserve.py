@@ -212,6 +212,7 @@ class NativePredictorServer:
         big = None       # fallback buffer for requests the staging slot cannot hold
         while self._running.is_set():
             launched = None
+            taken = None   # a batch id handed out by rt_http_next_batch and not yet launched / completed
             try:
                 n = h.rt_http_next_batch(self._h, 0 if pending else 100, bufs[slot].ctypes.data, cap, shape,
                                          ctypes.byref(nd), ctypes.byref(bid))
@@ -224,25 +225,32 @@ class NativePredictorServer:
                     n = h.rt_http_next_batch(self._h, 0, big.ctypes.data, big.size, shape, ctypes.byref(nd),
                                              ctypes.byref(bid))
                     if n > 0:
+                        taken = bid.value
                         q = tuple(int(shape[i]) for i in range(nd.value))
                         arr = big[:n * math.prod(q)].reshape((int(n),) + q)
+                        taken = None
                         self._run_sync(bid.value, arr, n)
                     continue
                 if n > 0:
+                    taken = bid.value
                     q = tuple(int(shape[i]) for i in range(nd.value))
                     if q == tuple(img_shape):
                         try:
                             launched = (g.launch_staged(slot, int(n)), slot, bid.value, int(n))
                         except Exception as e:
                             self._fail(bid.value, e)
+                        taken = None
                         slot ^= 1
                     else:   # another image shape (resized by the models): the synchronous array path
                         pending = self._finish_staged(g, pending)
                         arr = bufs[slot][:n * math.prod(q)].reshape((int(n),) + q).copy()
+                        taken = None
                         self._run_sync(bid.value, arr, n)
-            except Exception:   # never let the replica's only batch thread die
+            except Exception as e:   # never let the replica's only batch thread die
                 self._base['python_errors'] += 1
                 logger.error('batch loop error:\n%s', traceback.format_exc())
+                if taken is not None:   # the clients of a taken batch get an error reply, not a hang
+                    self._fail(taken, e)
             pending = self._finish_staged(g, pending)
             pending = launched
         self._finish_staged(g, pending)
@@ -277,6 +285,7 @@ class NativePredictorServer:
         nd = ctypes.c_int(0)
         bid = ctypes.c_ulonglong(0)
         while self._running.is_set():
+            taken = None
             try:
                 n = h.rt_http_next_batch(self._h, 100, buf.ctypes.data, cap, shape, ctypes.byref(nd),
                                          ctypes.byref(bid))
@@ -284,17 +293,21 @@ class NativePredictorServer:
                     continue
                 if n == -1:
                     break
-                per = int(math.prod(int(shape[i]) for i in range(nd.value)))
                 if n == -3:   # the first request does not fit: grow to the bound (C++ keeps requests below it)
                     cap = max(cap, MAX_BATCH_BUF)
                     buf = np.empty(cap, dtype=np.uint8)
                     continue
-            except Exception:   # never let the replica's only batch thread die
+                if n < 0:
+                    continue
+                taken = bid.value
+                q = tuple(int(shape[i]) for i in range(nd.value))
+                arr = buf[:n * int(math.prod(q))].reshape((int(n),) + q)
+            except Exception as e:   # never let the replica's only batch thread die
                 self._base['python_errors'] += 1
                 logger.error('batch loop error:\n%s', traceback.format_exc())
+                if taken is not None:
+                    self._fail(taken, e)
                 continue
-            q = tuple(int(shape[i]) for i in range(nd.value))
-            arr = buf[:n * per].reshape((int(n),) + q)
             self._run_sync(bid.value, arr, n)
 
     def _serve_generic(self, rid, method, path, body):
@@ -348,8 +361,13 @@ class NativePredictorServer:
         t = threading.Thread(target=self._generic_loop, name='rafiki-http-generic', daemon=True)
         t.start()
         self._threads.append(t)
-        for e in self._ready:   # replicas' graphs captured (queries arriving meanwhile wait in the C++ queue)
-            e.wait(self.ready_timeout_s)
+        # replicas' graphs captured (queries arriving meanwhile wait in the C++ queue): one shared deadline
+        deadline = time.monotonic() + self.ready_timeout_s
+        late = [i for i, e in enumerate(self._ready) if not e.wait(max(0.0, deadline - time.monotonic()))]
+        if late:
+            logger.warning('native predictor server: replica(s) %s not ready after %.0f s; serving anyway '
+                           '(their batches queue until they are)', late, self.ready_timeout_s)
+        self.not_ready = late
         return self
 
     def serve_forever(self):

@@ -189,8 +189,9 @@ class Predictor:
     # ------------------------------------------------------------------ loading from the DB
     @classmethod
     def from_inference_job(cls, inference_job_id, db=None, replicas=None, devices=None, **kw):
-        """Load the job's top-k trials.  ``replicas`` (default INFERENCE_WORKER_REPLICAS_PER_TRIAL)
-        copies go round-robin over ``devices`` (default: every GPU visible to this process).  A
+        """Load the job's top-k trials.  ``replicas`` (default INFERENCE_WORKER_REPLICAS_PER_TRIAL,
+        capped at one per device unless that variable or ``replicas`` is given explicitly) copies go
+        round-robin over ``devices`` (default: every GPU visible to this process).  A
         trial trained in this process is taken from HBM (resident.STORE) for replica 0 on its own
         GPU; everything else is read from the params file once and instantiated per replica."""
         if os.environ.get('RAFIKI_INFERENCE_MODE', 'local') == 'workers':
@@ -205,6 +206,10 @@ class Predictor:
         n_rep = max(1, int(replicas if replicas is not None else config.INFERENCE_WORKER_REPLICAS_PER_TRIAL))
         if devices is None:
             devices = _serving_devices()
+        if replicas is None and 'INFERENCE_WORKER_REPLICAS_PER_TRIAL' not in os.environ:
+            # the default is at most one replica per GPU: two replicas sharing one GPU serve 0.71x of one
+            # (profiles/predictor_qps_r4_2replicas.json); an explicit count is honoured as given
+            n_rep = min(n_rep, max(1, len(devices)))
         sets = [[] for _ in range(n_rep)]
         for w in db.get_workers_of_inference_job(inference_job_id):
             trial = db.get_trial(w.trial_id)

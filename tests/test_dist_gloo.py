@@ -320,3 +320,120 @@ def test_knob_exchange_advisor_failure_does_not_hang_peers():
         res = [eval(open(os.path.join(d, 'f{}.txt'.format(r))).read()) for r in range(world)]
         assert res[0] == ['ValueError', 'close']
         assert res[1] == res[2] == ['RuntimeError']
+
+
+def _bench_control_path(rank, world, port, db_path, service_id, workdir, out_dir):
+    """bench.py's control path on ``world`` gloo ranks (no GPU work): preflight, GP-EI proposals
+    broadcast from rank 0, all_reduce_max / gather_floats of the timed window, then the async trial loop
+    (atomic budget claims + the threaded P2P knob exchange) of a CPU model."""
+    _env(rank, world, port)
+    os.environ['WORKDIR_PATH'] = workdir
+    from rafiki_amd.advisor.advisor import GpAdvisor
+    from rafiki_amd.db.database import Database
+    from rafiki_amd.model.knob import FixedKnob, FloatKnob
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.parallel.exchange import control_group
+    from rafiki_amd.worker.train import TrainWorker
+    info = D.init_distributed(backend='gloo')
+    pre = D.preflight(info, timeout_s=60, group=control_group(info))
+    kc = {'lr': FloatKnob(1e-3, 2e-1, is_exp=True), 'momentum': FloatKnob(0.8, 0.95), 'batch_size': FixedKnob(256)}
+    advisor = GpAdvisor(kc, seed=0) if info.is_main else None
+    props = D.broadcast_proposals(info, kc, advisor.propose_batch(world) if info.is_main else None)
+    elapsed = D.all_reduce_max(info, 0.5 + 0.01 * rank)
+    table = D.gather_floats(info, [float(rank), props[rank]['lr']])
+    w = TrainWorker(service_id, 'w{}'.format(rank), db=Database(db_path), dist_info=info, seed=0, scheduling='async')
+    w.start()
+    ex = getattr(w, 'exchange', None)
+    with open(os.path.join(out_dir, 'b{}.txt'.format(rank)), 'w') as f:
+        f.write(repr((pre['ok'], sorted(pre['steps']), [p['lr'] for p in props], elapsed, table.tolist(),
+                      len(w.completed_trials), dict(ex.stats) if (ex is not None and info.is_main) else None)))
+    D.destroy(info)
+
+
+def test_bench_control_path_8_ranks():
+    """The 8-rank control path of bench.py --gpus 8 rehearsed on gloo: preflight of every collective and
+    rank-0 pair, one proposal per rank (all distinct, identical on every rank), the max-over-ranks and
+    gather reductions, and 8 ranks pulling 20 trials through the async exchange with an exact budget."""
+    port = _free_port()
+    world = 8
+    with tempfile.TemporaryDirectory() as d:
+        db_path = os.path.join(d, 'db.sqlite3')
+        db, sid, sub_id = _setup_db(db_path, 'SkDt', 'SkDt', 'IMAGE_CLASSIFICATION', {'MODEL_TRIAL_COUNT': 20},
+                                    'synthetic://image?n=200&size=16&channels=1&classes=4&seed=0',
+                                    'synthetic://image?n=80&size=16&channels=1&classes=4&seed=1')
+        mp.spawn(_bench_control_path, args=(world, port, db_path, sid, d, d), nprocs=world, join=True)
+        res = [eval(open(os.path.join(d, 'b{}.txt'.format(r))).read()) for r in range(world)]
+        lrs = res[0][2]
+        assert len(set(lrs)) == world
+        for r, (ok, steps, got_lrs, elapsed, table, _n, _st) in enumerate(res):
+            assert ok and 'p2p_rank0_pairs' in steps and 'all_gather' in steps
+            assert got_lrs == lrs and elapsed == 0.5 + 0.01 * (world - 1)
+            assert [row[0] for row in table] == [float(i) for i in range(world)]
+            assert [row[1] for row in table] == lrs
+        trials = db.get_trials_of_sub_train_job(sub_id)
+        assert len(trials) == 20 and all(t.status == 'COMPLETED' for t in trials)
+        assert sum(r[5] for r in res) == 20
+        stats = res[0][6]
+        assert stats is not None and stats['remote_requests'] >= 20 - res[0][5]
+
+
+def _knobx_dead_peer(rank, world, port, out_dir):
+    """Rank 2 rings rank 0's doorbell and dies before sending its row."""
+    _env(rank, world, port)
+    os.environ['RAFIKI_EXCHANGE_RECV_TIMEOUT_S'] = '3'
+    from rafiki_amd.advisor.advisor import GpAdvisor
+    from rafiki_amd.model.knob import FloatKnob
+    from rafiki_amd.ops import graphs
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.parallel.exchange import KnobExchange
+    info = D.init_distributed(backend='gloo')
+    kc = {'x': FloatKnob(0.0, 1.0)}
+    ex = KnobExchange(info, kc, lambda: GpAdvisor(kc, seed=0), tag='dead')
+    out = []
+    if rank == 2:
+        ex.store.queue_push(ex.tag + '/q', str(rank))
+        with open(os.path.join(out_dir, 'd{}.txt'.format(rank)), 'w') as f:
+            f.write(repr(['rang']))
+        os._exit(0)   # no row, no finish: a peer lost mid-exchange
+    if rank == 1:   # a live peer that has not asked yet (the group is broken once rank 0 times out)
+        import time
+        time.sleep(1.0)
+        out.append('idle')
+    if rank == 0:
+        import time
+        t0 = time.monotonic()
+        while not ex._broken and time.monotonic() - t0 < 30:
+            time.sleep(0.05)
+        out.append('broken' if ex._broken else 'hung')
+        # the capture lock is free again (the server thread waits for the row outside it)
+        got = graphs.LOCK.acquire(timeout=1.0)
+        out.append('lock' if got else 'lock-held')
+        if got:
+            graphs.LOCK.release()
+        try:
+            ex.request(None)
+        except RuntimeError:
+            out.append('request-refused')
+        try:
+            ex.close()
+        except RuntimeError:
+            out.append('close-raised')
+    with open(os.path.join(out_dir, 'd{}.txt'.format(rank)), 'w') as f:
+        f.write(repr(out))
+    os._exit(0)   # the group is broken by design: skip destroy_process_group
+
+
+def test_knob_exchange_dead_peer_times_out_and_frees_the_capture_lock():
+    port = _free_port()
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_knobx_dead_peer, args=(world, port, d), nprocs=world, join=False,
+                                 start_method='spawn')
+        import time
+        deadline = time.monotonic() + 120
+        while not ctx.join(5) and time.monotonic() < deadline:
+            pass
+        res = {r: eval(open(os.path.join(d, 'd{}.txt'.format(r))).read()) for r in range(world)
+               if os.path.exists(os.path.join(d, 'd{}.txt'.format(r)))}
+        assert res.get(2) == ['rang']
+        assert res.get(0) == ['broken', 'lock', 'request-refused', 'close-raised'], res

@@ -242,6 +242,52 @@ def test_engine_grads_non_pow2_and_odd_pool():
     _grad_check(eng, x, y, 1e-4)
 
 
+@pytest.mark.parametrize("wino", [False, True])
+def test_engine_no_bn_grads_match_fp64_reference(wino, monkeypatch):
+    """bn=False (Keras VGG16's conv3x3 + bias + ReLU blocks, TfVgg16.py:115-130): the fp32 step against
+    fp64 autograd, after two steps so the biases are non-zero.  32x32 maps (Winograd paths, pooled and
+    pool-free blocks, the dgrad's BNB / BNP epilogues with the constant coefficients) and 48x48 -> 3x3 ->
+    1x1 (reciprocal gathers, odd pooling)."""
+    from rafiki_amd.ops import f32 as S
+    monkeypatch.setattr(S, 'WINO', wino)
+    for image_size, cfg, B in ((32, (16, 16, 'M', 32, 32, 'M', 64, 'M'), 32),
+                               (48, (16, 'M', 32, 'M', 32, 'M', 64, 'M', 64, 'M'), 16)):
+        eng = _engine(image_size=image_size, cfg=cfg, fc_dims=(64,), bn=False, optimizer='adam', lr=1e-3,
+                      weight_decay=0.0)
+        assert not any(n.endswith(('.gamma', '.beta')) for n in eng.flat.names())
+        for i in range(2):
+            x, y = _batch(B, hw=image_size, seed=20 + i)
+            eng.train_step(x, y)
+        assert all(eng.flat.w(b[0] + '.b').abs().sum().item() > 0 for b in eng.blocks)
+        eng.reset_metrics()
+        x, y = _batch(B, hw=image_size, seed=9)
+        _grad_check(eng, x, y, 1e-3 if wino else 1e-4)
+
+
+def test_engine_no_bn_eval_and_grouped_match_reference():
+    """bn=False inference: the per-model eval forward (conv without bias + the bias as the folded shift)
+    and the grouped ensemble network both match fp64 PyTorch."""
+    from rafiki_amd.engine.convnet import GroupedConvNets
+    engs = [_engine(image_size=16, bn=False, seed=s) for s in (3, 4)]
+    x, y = _batch(64, seed=5)
+    for e in engs:
+        for _ in range(2):
+            e.train_step(x, y)
+        e.prepare_eval()
+    refs = []
+    for e in engs:
+        probs = e.forward_eval_graphed(x)
+        _, ref_logits = e.reference_loss(x.double().cpu(), None, training=False,
+                                         params={n: e.flat.w(n).double().cpu() for n in e.flat.names()})
+        refs.append(torch.softmax(ref_logits, 1))
+        assert (probs.double().cpu() - refs[-1]).abs().max().item() < 1e-5
+    grp = GroupedConvNets(engs)
+    out = torch.empty((2, x.shape[0], 10), dtype=torch.float32, device=DEV)
+    grp.forward_into(x, out)
+    for g in range(2):
+        assert (out[g].double().cpu() - refs[g]).abs().max().item() < 1e-5
+
+
 def test_mlp_input_bn_grads():
     eng = _engine(cfg=(), fc_dims=(64, 64), input_bn=True, optimizer='adam', lr=1e-3, in_channels=1, image_size=28)
     g = torch.Generator().manual_seed(2)

@@ -240,3 +240,34 @@ def test_native_npy_batches_join_the_image_queue():
         assert requests.post(url + '/predict', json={'query': qs[0].tolist()}).status_code == 200
     finally:
         srv.shutdown()
+
+
+def _raw_npy_header(shape_text):
+    hd = "{'descr': '|u1', 'fortran_order': False, 'shape': %s, }" % shape_text
+    total = (10 + len(hd) + 1 + 63) // 64 * 64
+    hd = hd + ' ' * (total - 10 - len(hd) - 1) + '\n'
+    return b'\x93NUMPY\x01\x00' + bytes([len(hd) & 255, len(hd) >> 8]) + hd.encode('latin-1')
+
+
+def test_native_npy_overflowing_shape_is_rejected_and_server_keeps_serving():
+    """A .npy header whose dims multiply past int64 (and an empty data section) must not be accepted as
+    a batch: the C++ decoder rejects it (checked before every multiply), the request is answered with
+    an error, and later queries are still served (the replica's batch thread is alive)."""
+    from rafiki_amd.predictor import nativeserve
+    if not nativeserve.available():
+        pytest.skip('librafiki_runtime.so not built')
+    fake = FakePredictor()
+    srv = nativeserve.NativePredictorServer(fake, '127.0.0.1', 0, max_batch=64).start()
+    try:
+        url = 'http://127.0.0.1:{}'.format(srv.port)
+        for shape in ('(1, %d, %d)' % (2 ** 40, 2 ** 24), '(%d, %d, %d)' % (2 ** 40, 2 ** 40, 2 ** 40),
+                      '(0, 3, 4)', '(2, 3, 4)'):
+            r = requests.post(url + '/predict_batch_npy', data=_raw_npy_header(shape), timeout=30)
+            assert r.status_code in (400, 500), (shape, r.status_code)
+        q = np.arange(12, dtype=np.uint8).reshape(3, 4)
+        r = requests.post(url + '/predict', json={'query': q.tolist()}, timeout=30)
+        assert r.status_code == 200 and np.allclose(r.json()['prediction'], fake._probs(q[None])[0])
+        r = requests.post(url + '/predict_batch_npy', data=_npy(q[None].repeat(5, 0)), timeout=30)
+        assert r.status_code == 200 and np.load(io.BytesIO(r.content)).shape == (5, 3)
+    finally:
+        srv.shutdown()

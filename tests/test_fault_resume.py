@@ -52,9 +52,9 @@ def test_crash_then_resume_from_checkpoint(tmp_path, monkeypatch):
     from rafiki_amd.worker.train import TrainWorker
     db, sid, sub_id = _setup(tmp_path, {'MODEL_TRIAL_COUNT': 1})
     params = str(tmp_path / 'params')
-    monkeypatch.setenv('RAFIKI_FAULT_INJECT', 'crash:epoch=1')
+    monkeypatch.setenv('RAFIKI_FAULT_INJECT', 'crash:epoch=0')
     w = TrainWorker(sid, 'w0', db=db, seed=0, params_dir=params)
-    # FeedForward runs 3 epochs (FixedKnob); the crash fires right after epoch 1's checkpoint
+    # FeedForward runs 2 epochs (FixedKnob, the reference's); the crash fires right after epoch 0's checkpoint
     with pytest.raises(faults.WorkerCrash):
         w.start()
     (trial,) = db.get_trials_of_sub_train_job(sub_id)
@@ -70,7 +70,7 @@ def test_crash_then_resume_from_checkpoint(tmp_path, monkeypatch):
     assert not os.path.exists(os.path.join(params, trial.id + '.ckpt'))
     assert os.path.exists(t2.params_file_path)
     logs = [l.line if hasattr(l, 'line') else l for l in db.get_trial_logs(trial.id)]
-    assert any('resumed from checkpoint after epoch 1' in str(x) for x in logs)
+    assert any('resumed from checkpoint after epoch 0' in str(x) for x in logs)
 
 
 def test_heartbeat_staleness(tmp_path):

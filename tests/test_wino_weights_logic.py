@@ -25,7 +25,6 @@ def _setup(monkeypatch, capturing=False):
     monkeypatch.setattr(S, '_s', lambda: None)
     monkeypatch.setattr(S, '_p', lambda t: None if t is None else t.data_ptr())   # host tensors are fine here
     monkeypatch.setattr(torch.cuda, 'is_current_stream_capturing', lambda: capturing)
-    monkeypatch.setattr(S.WinoWeights, 'WT_ALL', False)   # one launch per family (the combined table: below)
     shapes = [(64, 32), (16, 64), (40, 24)]
     arena = torch.zeros(sum(co * 9 * ci for co, ci in shapes) + 3)
     ws, off = [], 3
@@ -56,14 +55,17 @@ def test_sets_per_layer_follow_map_size(monkeypatch):
     assert ww.has('u2', 1) and ww.has('ut2', 1) and not ww.has('u4', 1)   # 6x6 map: no F(4x4) set
     assert ww.has('u4', 0) and ww.has('ut4', 2)
     assert ww.u4(1) is None and ww.u4(0).shape == (36, 64, 32) and ww.ut(2).shape == (16, 24, 40)
+    # blocked sets of the UB fused kernels: rows padded to 32, flat
+    assert ww.has('u4b', 0) and ww.has('ut4b', 2) and not ww.has('u4b', 1)
+    assert ww._view('u4b', 2).shape == (36 * 64 * 24,) and ww._view('ut4b', 0).shape == (36 * 32 * 64,)
 
 
 def test_refresh_narrows_to_the_sets_a_step_used(monkeypatch):
     rec, ww = _setup(monkeypatch)
     ww.refresh()
-    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi', 'rk_x6p_w4_weights_multi']
+    assert rec.names() == ['rk_wino_weights_all']
     ww.end_step()                      # nothing read: keep everything
-    assert len(ww.live) == 12
+    assert len(ww.live) == 16
     ww.refresh()
     ww.lazy('u4', 0)()
     ww.lazy('ut2', 2)()
@@ -80,12 +82,15 @@ def test_refresh_narrows_to_the_sets_a_step_used(monkeypatch):
     assert t['4'] == {0: (ww._sets[('u4', 0)][0], -1)}           # forward set only
     rec.calls.clear()
     ww.refresh()
-    assert rec.names() == ['rk_wino_weights_multi', 'rk_wino4_weights_multi']
+    assert rec.names() == ['rk_wino_weights_all']
     # a set outside the live group is transformed on demand, once per step
     ww.lazy('u2', 1)()
     ww.lazy('u2', 1)()
-    assert rec.names()[2:] == ['rk_wino_weights']
-    _, args = rec.calls[2]
+    ww.lazy('ut4b', 2)()
+    assert rec.names()[1:] == ['rk_wino_weights', 'rk_wino4b_weights']
+    _, bargs = rec.calls[2]
+    assert bargs[1] is None and bargs[2] is not None and bargs[3:5] == (40, 24)   # gradient set only
+    _, args = rec.calls[1]
     assert args[1] is not None and args[2] is None                 # forward set, no gradient set
 
 
@@ -94,7 +99,7 @@ def test_no_narrowing_inside_capture(monkeypatch):
     ww.refresh()
     ww.lazy('u2', 0)()
     ww.end_step()
-    assert len(ww.live) == 12                                      # tables cannot be rebuilt in a capture
+    assert len(ww.live) == 16                                      # tables cannot be rebuilt in a capture
 
 
 def test_sconvwt_refresh_is_lazy(monkeypatch):
@@ -115,10 +120,9 @@ def test_sconvwt_refresh_is_lazy(monkeypatch):
 
 
 def test_single_launch_refresh_table_covers_every_family(monkeypatch):
-    """RAFIKI_WT_ALL (default): one rk_wino_weights_all launch whose table is the per-family tables
-    concatenated — meta rows renumbered, the family id in each block's 4th field."""
+    """One rk_wino_weights_all launch whose table is the per-family tables concatenated — meta rows
+    renumbered, the family id in each block's 4th field."""
     rec, ww = _setup(monkeypatch)
-    monkeypatch.setattr(S.WinoWeights, 'WT_ALL', True)
     ww.refresh()
     assert rec.names() == ['rk_wino_weights_all']
     fams = ww._prepare(ww.live)
@@ -126,7 +130,7 @@ def test_single_launch_refresh_table_covers_every_family(monkeypatch):
     d, m = desc.view(-1, 4), meta.view(-1, 5)
     assert nb == d.shape[0] == sum(f[3] for f in fams)
     assert m.shape[0] == sum(f[2].numel() // 5 for f in fams)
-    fam_of = {'2': 0, '4': 1, 'p': 2}
+    fam_of = {'2': 0, '4': 1, 'p': 2, 'b': 3}
     row = 0
     base = 0
     for fam, fdesc, fmeta, fnb in fams:

@@ -4,7 +4,6 @@ F(4x4,3x3)'s transforms have coefficients up to 8 (A^T) and 5 (B^T), so its fp32
 ten times F(2x2)'s (profiles/winograd_error_r2.jsonl); the gate is 3e-5 relative Frobenius error,
 against ~1e-6 measured."""
 import math
-import os
 
 import pytest
 import torch
@@ -13,9 +12,15 @@ import torch.nn.functional as TF
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 TOL = 3e-5
-# the software-pipelined variants (2) are exercised with the candidate switch that enables them
-PIPE = os.environ.get('RAFIKI_WINO_PIPE', '0') != '0'
-VARIANTS = [0, 1, 2] if PIPE else [0, 1]
+# 0 / 1: 8- / 4-wave tiles; 2: 4-wave two-stage (not a tuner candidate, kept exercised); 3 / 4: 0 / 1 on the
+# blocked weight sets (wino4b_u)
+VARIANTS = [0, 1, 2, 3, 4]
+
+
+def _u4(S, w2, variant, dgrad=False):
+    if variant >= 3:
+        return S.wino4b_u(w2, dgrad=dgrad)
+    return S.wino4_ut(w2) if dgrad else S.wino4_u(w2)
 
 
 def rel(a, b):
@@ -45,9 +50,9 @@ def test_wino4_fwd_and_stats(N, H, W, Cin, Cout, variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=1)
     w = _rand(Cout, 3, 3, Cin, seed=2, scale=1.0 / math.sqrt(9 * Cin))
-    u = S.wino4_u(_w2(w))
+    u = _u4(S, _w2(w), variant)
     acc = torch.zeros((S.bn_slots(Cout), 2, Cout), dtype=torch.float64, device=DEV)
-    y = S.wino4_conv(x.to(DEV), u, stats=acc, variant=variant)
+    y = S.wino4_conv(x.to(DEV), u, stats=acc, variant=variant, n_out=Cout)
     torch.cuda.synchronize()
     ref = _conv_ref(x, w)
     assert rel(y, ref) < TOL
@@ -56,14 +61,19 @@ def test_wino4_fwd_and_stats(N, H, W, Cin, Cout, variant):
     assert rel(s[0], r.sum(0)) < TOL and rel(s[1], (r * r).sum(0)) < TOL
 
 
-def test_wino4_bias_relu():
+@pytest.mark.parametrize("variant", [0, 4])
+def test_wino4_bias_relu(variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(3, 8, 8, 32, seed=3)
     w = _rand(48, 3, 3, 32, seed=4, scale=0.1)
     b = _rand(48, seed=5)
-    y = S.wino4_conv(x.to(DEV), S.wino4_u(_w2(w)), bias=b.to(DEV), relu=True)
+    y = S.wino4_conv(x.to(DEV), _u4(S, _w2(w), variant), bias=b.to(DEV), relu=True, variant=variant, n_out=48)
     torch.cuda.synchronize()
     assert rel(y, torch.relu(_conv_ref(x, w) + b.double())) < TOL
+    # bias without ReLU (the runtime-flag instantiation: no-BN blocks followed by a max-pool)
+    y = S.wino4_conv(x.to(DEV), _u4(S, _w2(w), variant), bias=b.to(DEV), variant=variant, n_out=48)
+    torch.cuda.synchronize()
+    assert rel(y, _conv_ref(x, w) + b.double()) < TOL
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 16, 16, 64, 64), (8, 4, 4, 512, 256),
@@ -75,7 +85,7 @@ def test_wino4_dgrad_from_flipped_set(N, H, W, Cin, Cout, variant):
     x = _rand(N, H, W, Cin, seed=6)
     w = _rand(Cout, 3, 3, Cin, seed=7, scale=0.1)
     dy = _rand(N, H, W, Cout, seed=8)
-    dx = S.wino4_conv(dy.to(DEV), S.wino4_ut(_w2(w)), variant=variant)
+    dx = S.wino4_conv(dy.to(DEV), _u4(S, _w2(w), variant, dgrad=True), variant=variant, n_out=Cin)
     torch.cuda.synchronize()
     xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
     out = TF.conv2d(xd, w.double().permute(0, 3, 1, 2), padding=1)
@@ -100,11 +110,11 @@ def test_wino4_dgrad_bn_epilogues_match_direct(pool, variant, H):
     arena = w.reshape(-1).to(DEV).contiguous()
     wt = S.SConvWT(arena, [arena.view(Cout, 3, 3, Cin)])
     wt.refresh()
-    ut = S.wino4_ut(_w2(w))
+    ut = _u4(S, _w2(w), variant, dgrad=True)
     dyo = _rand(N, H, W, Cout, seed=20).to(DEV)
     acc_w, acc_d = torch.zeros_like(acc), torch.zeros_like(acc)
     key = 'bnp' if pool else 'bnb'
-    d_w = S.wino4_conv(dyo, ut, variant=variant, **{key: (y.to(DEV), coeffs, acc_w)})
+    d_w = S.wino4_conv(dyo, ut, variant=variant, n_out=Cin, **{key: (y.to(DEV), coeffs, acc_w)})
     d_d = S.conv_dgrad(dyo, wt.view(0), **{key: (y.to(DEV), coeffs, acc_d)})
     torch.cuda.synchronize()
     assert rel(d_w, d_d) < TOL
@@ -112,7 +122,7 @@ def test_wino4_dgrad_bn_epilogues_match_direct(pool, variant, H):
 
 
 @pytest.mark.parametrize("shared", [True, False])
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_wino4_conv_grouped(shared, variant):
     """k convs in one grid (the serving ensemble's layers) == k separate convs."""
     from rafiki_amd.ops import f32 as S
@@ -132,7 +142,7 @@ def test_wino4_conv_grouped(shared, variant):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(4, 8, 8, 64, 128), (2, 32, 32, 64, 64), (16, 4, 4, 256, 512),
                                             (3, 4, 12, 24, 40), (2, 4, 4, 16, 16)])
 @pytest.mark.parametrize("splits", [1, 2, 5])
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_wino4_wgrad(N, H, W, Cin, Cout, splits, variant):
     from rafiki_amd.ops import f32 as S
     x = _rand(N, H, W, Cin, seed=30)
