@@ -22,7 +22,9 @@ Every part of it is measured in this run, none extrapolated:
   phase 3  predictor ensemble QPS (rank 0, 1 GPU): the top-4 trials of phase 2 loaded from their
            params files into one ``Predictor``; hipGraph-captured forwards on 4 HIP streams + the
            on-device ensemble mean, device-resident uint8 batches of 256 (plus the batch-1 latency
-           and the host-array API path).
+           and the host-array API path); then POST /predict through the native HTTP front end under
+           64 closed-loop JSON clients and 8 .npy batch-128 clients from a separate load-generator
+           process (``ensemble_http_qps`` with p50 / p99, rafiki_amd/predictor/loadgen.py).
 
 ``python bench.py`` defaults to 1 GPU and finishes in about a minute.
 """
@@ -228,7 +230,7 @@ def phase_trials(args, info, root, model_class, per_gpu, train_uri, test_uri, wa
                 steady=steady, exchange=dict(ex.stats) if (ex is not None and info.is_main) else None)
 
 
-def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30):
+def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30, http_seconds=3.0):
     import pickle
 
     import numpy as np
@@ -278,6 +280,17 @@ def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30):
     arr = rng.integers(0, 256, (batch, 32, 32, 3), dtype=np.uint8)
     dt = timed(lambda: pred.predict_array(arr), max(3, iters // 3))
     out['host_array_b{}'.format(batch)] = {'qps': round(batch / dt, 1), 'ms': round(dt * 1e3, 3)}
+    # the BASELINE metric's own path: POST /predict through the native HTTP front end, loaded from a separate
+    # process (64 single-query JSON clients, then 8 clients posting .npy batches of 128)
+    from rafiki_amd.predictor import loadgen
+    if loadgen.available():
+        pred.start()
+        try:
+            out['http'] = loadgen.http_load(pred, seconds=http_seconds)
+        except Exception as e:   # the device numbers above stand; say why HTTP is missing
+            out['http'] = {'error': '{}: {}'.format(type(e).__name__, e)[:300]}
+        finally:
+            pred.stop()
     return out
 
 
@@ -398,6 +411,12 @@ def main():
             out['preflight'] = pre
         if serving is not None:
             out['ensemble_qps'] = serving['device_b256']['qps']
+            http = serving.get('http') or {}
+            if 'json_single_query' in http:
+                js, nb = http['json_single_query'], http.get('npy_batch128', {})
+                out['ensemble_http_qps'] = js['qps']
+                out['ensemble_http_p50_ms'], out['ensemble_http_p99_ms'] = js['p50_ms'], js['p99_ms']
+                out['ensemble_http_npy_b128_qps'] = nb.get('qps')
             out['ensemble'] = serving
         print(json.dumps(out), flush=True)
     D.destroy(info)

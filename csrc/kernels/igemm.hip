@@ -45,7 +45,7 @@ enum EpiMode { EPI_BF16 = 0, EPI_F32 = 1 };
 // through `gate` and scale/shift = bias[0:N] / bias[N:2N]; the per-channel sums (sum dz,
 // sum dz*y) that BN backward needs go to the fp64 slot table `stats` (with FLAG_SATOM), so that
 // layer's separate reduction pass disappears.
-enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16, FLAG_NOFAST = 64,
+enum Flags { FLAG_RELU = 1, FLAG_BIAS = 2, FLAG_STATS = 4, FLAG_GATE = 8, FLAG_ACCUM = 16,
              FLAG_LRELU = 32, FLAG_SATOM = 256, FLAG_BNB = 512, FLAG_BNP = 1024 };
 // FLAG_BNP (data-gradient into a BatchNorm+ReLU+2x2-max-pool layer): the output is that layer's
 // pooled gradient (stored unchanged); its BN-backward sums are formed here: per output element the
@@ -392,13 +392,13 @@ struct DmaOperand {
       }
     }
     // ---- fast-path preconditions (uniform) and lane constants
-    const bool k64 = (p.K & (BK - 1)) == 0 && !(p.flags & FLAG_NOFAST);
+    const bool k64 = (p.K & (BK - 1)) == 0;
     if constexpr (MODE == OP_DENSE_KIN) {
       fast = k64;
 #pragma unroll
       for (int q = 0; q < NI; ++q) fbase[q] = vmask[q] ? base[q] : OOB;
     } else if constexpr (MODE == OP_CONV_KIN || MODE == OP_CONVT_KIN) {
-      fast = p.log2C >= 6 && !(p.flags & FLAG_NOFAST);  // C % 64 == 0: one tap per K-tile
+      fast = p.log2C >= 6;  // C % 64 == 0: one tap per K-tile
 #pragma unroll
       for (int q = 0; q < NI; ++q) fbase[q] = base[q] + (unsigned)sub[q] * 16u;
     } else if constexpr (MODE == OP_DENSE_KOUT) {
@@ -1478,8 +1478,6 @@ extern "C" int rk_igemm(int kind, int epi, int tile, const void* A, const void* 
   p.ktPer = rk_cdiv(kTiles, splits);
   p.slabStride = slabStride;
   p.flags = flags; p.alpha = alpha; p.slope = slope;
-  static const bool nofast = getenv("RAFIKI_IGEMM_NOFAST") != nullptr;  // A/B switch for the DMA fast path
-  if (nofast) p.flags |= FLAG_NOFAST;
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   hipStream_t st = (hipStream_t)stream;
   const bool conv = kind <= 2 || kind == 6;

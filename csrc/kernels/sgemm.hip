@@ -328,7 +328,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
     } else {
       s_wait_vmcnt<0>();
     }
-    if (!(p.dbg & 2)) s_barrier_lds();  // every wave's DMA for tile kt is in LDS; done with tile kt-1
+    s_barrier_lds();  // every wave's DMA for tile kt is in LDS; done with tile kt-1
     const char* As = smem + st * SB;
     const char* Bs = As + ABYTES;
     const bool more = kt + NST - 1 < kt1;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
         load_frags(A, As, wm * WMT, 2 * c + 1, lane, a1);
         load_frags(B, Bs, wn * WNT, 2 * c, lane, b0);
         load_frags(B, Bs, wn * WNT, 2 * c + 1, lane, b1);
-        if (c == 0 && !(p.dbg & 1)) {
+        if (c == 0) {
           A.issue(p, nxt, kt + NST - 1, p.K, p.lda, wid, more);
           B.issue(p, nxt + ABYTES, kt + NST - 1, p.K, p.ldb, wid, more);
         }
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sgemm_kernel(const SgParams p)
       // scheduling region
       // the next tile's DMAs go out in the first group, so they have (NST-1) whole K-tiles of MFMAs
       // to land (a 64x64 tile's K-tile is only 16 MFMAs = ~1k cycles per wave)
-      if (g == 0 && !(p.dbg & 1)) {
+      if (g == 0) {
         A.issue(p, nxt, kt + NST - 1, p.K, p.lda, wid, more);
         B.issue(p, nxt + ABYTES, kt + NST - 1, p.K, p.ldb, wid, more);
       }
@@ -507,8 +507,6 @@ extern "C" int rk_sgemm(int kind, int tile, int nst, const float* A, const float
   p.slabStride = splits > 1 ? slabStride : 0;
   p.flags = flags; p.slotMask = slotMask; p.alpha = alpha; p.slope = slope;
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
-  static const int dbg = getenv("RAFIKI_SGEMM_DBG") ? atoi(getenv("RAFIKI_SGEMM_DBG")) : 0;
-  p.dbg = dbg;
   p.groups = 1;
   p.Ho = H; p.Wo = W; p.log2Ho = p.log2H; p.log2Wo = p.log2W; p.invHo = p.invH; p.invWo = p.invW;
   hipStream_t st = (hipStream_t)stream;

@@ -39,7 +39,6 @@ struct SgParams {
   int flags, slotMask;
   float alpha, slope;
   unsigned long long bytesA, bytesB;
-  int dbg;  // diagnostics (RAFIKI_SGEMM_DBG): 1 no DMA in the K loop (stale LDS), 2 no K-loop barrier
   // table-driven gathers (SM_KIN_CONVG / SM_KOUT_CONVG); H, W above = the INPUT map
   int Ho, Wo, log2Ho, log2Wo;  // row grid (output pixels of the gather)
   float invHo, invWo;

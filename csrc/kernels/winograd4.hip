@@ -128,11 +128,15 @@ RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) { w_tile
 // NS = 2: two LDS stages and two register sets — the transform of chunk c+1 (loaded during chunk c-1)
 // is written to one stage while the MFMAs of chunk c read the other, in the same wave (software
 // pipelining; one barrier per chunk; chunks past Cin load zeros, so the body is branch-free)
-template <int MO, int WM, int WN, int MINW, int FL, int NS = 1, bool UB = false>
-__global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4Params p) {
+// WS: warp-specialised — WM x WN compute waves (MFMAs + epilogue) and as many loader waves (global loads,
+// input transform, LDS writes) over two LDS stages: the loaders fill chunk c+1 while the compute waves run
+// chunk c, one barrier per chunk; every SIMD holds one wave of each role, so the transform's VALU and the
+// loads issue beside the other wave's MFMAs instead of in a phase of their own (NS = 2, blocked weights)
+template <int MO, int WM, int WN, int MINW, int FL, int NS = 1, bool UB = false, bool WS = false>
+__global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_kernel(const W4Params p) {
   constexpr int A = MO + 2;                // window / transformed tile side
   constexpr int P = A * A;                 // Winograd positions
-  constexpr int NT = 64 * WM * WN;         // threads
+  constexpr int NT = 64 * WM * WN;         // threads of one role (WS: compute and loader waves each)
   constexpr int T = 16 * WM;               // tiles per block
   constexpr int BNC = 16 * WN;             // output channels per block
   constexpr int IT = T * KC / NT;          // input windows per thread and chunk
@@ -143,10 +147,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   constexpr int ULR = UB ? 1 : UL, UBR = UB ? UBL : 1;   // register arrays of the two weight paths
   static_assert(IT >= 1 && IT * NT == T * KC && UL * NT == P * BNC * 4, "tile shape");
   static_assert(!UB || (MO == 4 && BNC == 32), "blocked weights: F(4x4), 32-channel output blocks");
+  static_assert(!WS || (NS == 2 && UB), "warp-specialised: two stages, blocked weights");
   __shared__ __attribute__((aligned(16))) float Vs[NS][P][T][KC];
   __shared__ __attribute__((aligned(16))) float Us[NS][P][BNC][KC];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave % WM, wn = wave / WM;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool compute = !WS || wave < WM * WN;
+  // tid: the thread's index within its role (WS loaders count from 0 too)
+  const int tid = (WS && !compute) ? (int)threadIdx.x - NT : (int)threadIdx.x;
+  const int wm = wave % WM, wn = (wave / WM) % WN;
   const int b0 = xcd_remap(blockIdx.x, gridDim.x);
   const int grp = b0 / p.bpg, b = b0 - grp * p.bpg;
   const int cb = b % p.ncb, tb = b / p.ncb;
@@ -260,14 +268,61 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
     }
   };
 
+  const int nch = p.C / KC;
+  if constexpr (WS) {
+    // loader waves (their own branch, so the compute waves' accumulators are not live here): chunk 0, then
+    // per barrier the next chunk's transform + LDS writes, its successor's loads already in flight.  The
+    // compute waves pass the same nch + 1 barriers.
+    if (!compute) {
+      float rL[IT][P];
+      f32x2 uL[ULR];
+      f32x4 bL[UBR];
+      load(0, rL, uL, bL);
+      store(0, rL, uL, bL);
+      if (nch > 1) load(KC, rL, uL, bL);
+      __syncthreads();
+      for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) {
+          store((c + 1) & 1, rL, uL, bL);  // chunk c + 1 (its loads were issued one chunk ago)
+          if (c + 2 < nch) load((c + 2) * KC, rL, uL, bL);
+        }
+        __syncthreads();
+      }
+      return;
+    }
+    __syncthreads();                       // chunk 0 is in stage 0
+  }
+
   f32x4 acc[P];
 #pragma unroll
   for (int q = 0; q < P; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nch = p.C / KC;
   const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
   const int ka = (2 * (lane >> 4)) ^ swz(ar), kb = (2 * (lane >> 4)) ^ swz(br);
   auto mfma = [&](int st) {
+    if constexpr (WS) {
+      // one compute wave per SIMD: the next group's fragments are read while this group's MFMAs run
+      f32x2 a[2][4], bv[2][4];
+      auto rd = [&](int q, int buf) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[buf][e] = *(const f32x2*)&Vs[st][q + e][ar][ka];
+          bv[buf][e] = *(const f32x2*)&Us[st][q + e][br][kb];
+        }
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int g = 0; g < P / 4; ++g) {
+        if (g + 1 < P / 4) rd(4 * (g + 1), (g + 1) & 1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[4 * g + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g & 1][e][s], bv[g & 1][e][s], acc[4 * g + e], 0,
+                                                                  0, 0);
+      }
+      return;
+    }
     // four positions at a time: 4 independent MFMAs between dependent ones
 #pragma unroll
     for (int q = 0; q < P; q += 4) {
@@ -287,7 +342,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino_gfwd_kernel(const W4P
   float rA[IT][P];
   f32x2 uA[ULR];
   f32x4 bA[UBR];
-  if constexpr (NS == 1) {
+  if constexpr (WS) {
+    for (int c = 0; c < nch; ++c) {        // compute waves: chunk c, then the barrier that publishes c + 1
+      mfma(c & 1);
+      __syncthreads();
+    }
+  } else if constexpr (NS == 1) {
     load(0, rA, uA, bA);
     store(0, rA, uA, bA);
     __syncthreads();
@@ -669,12 +729,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
 // same wave transforms chunk c+1 (loaded during chunk c-1) into the other, so the transform VALU and
 // LDS writes issue in the shadow of the 32-cycle MFMAs instead of in a phase of their own; one barrier
 // per chunk.  Chunks past the end load zeros (out-of-range offsets), so the body is branch-free.
+// (A warp-specialised form — 4 MFMA waves plus 4 loader waves transforming chunk c+1 into the other
+// stage, 512 threads — measured 35-60% slower on every VGG-small layer, profiles/wino4_variants_r5.jsonl.)
 __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParams p) {
   constexpr int BCO = 32, BCI = 32;
   __shared__ __attribute__((aligned(16))) float Ms[2][36][BCO][KC];
   __shared__ __attribute__((aligned(16))) float Vs[2][36][BCI][KC];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tid = (int)threadIdx.x;
+  const int wm = wave & 1, wn = (wave >> 1) & 1;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int per = p.nco * p.nci;
   const int split = b / per, r0 = b - split * per;
@@ -780,21 +843,23 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
     }
   };
 
-  float gA[16], rA[36], gB[16], rB[36];
-  if (nch > 0) {
-    load(0, gA, rA);
-    load(1, gB, rB);
-    store(0, gA, rA);
-    __syncthreads();
-    for (int c = 0; c < nch; c += 2) {
-      load(c + 2, gA, rA);
-      mfma(0);                             // chunk c
-      store(1, gB, rB);                    // chunk c + 1, in the MFMAs' shadow
+  {
+    float gA[16], rA[36], gB[16], rB[36];
+    if (nch > 0) {
+      load(0, gA, rA);
+      load(1, gB, rB);
+      store(0, gA, rA);
       __syncthreads();
-      load(c + 3, gB, rB);
-      mfma(1);                             // chunk c + 1 (zeros past the end)
-      store(0, gA, rA);                    // chunk c + 2
-      __syncthreads();
+      for (int c = 0; c < nch; c += 2) {
+        load(c + 2, gA, rA);
+        mfma(0);                           // chunk c
+        store(1, gB, rB);                  // chunk c + 1, in the MFMAs' shadow
+        __syncthreads();
+        load(c + 3, gB, rB);
+        mfma(1);                           // chunk c + 1 (zeros past the end)
+        store(0, gA, rA);                  // chunk c + 2
+        __syncthreads();
+      }
     }
   }
 
@@ -1008,7 +1073,7 @@ extern "C" int rk_wino4_weights_multi(const float* arena, float* dst, const int*
 namespace {
 // shared launcher of the small-wave-tile Winograd forward kernels: MO = 4 (u [36][N][C], H, W multiples
 // of 4) or MO = 2 (u [16][N][C], even H, W); T tiles x BNC channels per block of NT threads
-template <int MO, int WM, int WN, int MINW, int NS = 1, bool UB = false>
+template <int MO, int WM, int WN, int MINW, int NS = 1, bool UB = false, bool WS = false>
 int launch_gfwd(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
                 const float* gate, int Nb, int H, int W, int C, int N, int flags, int groups, long long gx,
                 long long gu, long long gy, long long gbias, void* stream) {
@@ -1040,19 +1105,19 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   const long long blocks = bpg * groups;
   if (blocks >= (1LL << 31)) return RK_EBADARG;
   p.bpg = (int)bpg;
-  const dim3 grid((unsigned)blocks), block(64 * WM * WN);
+  const dim3 grid((unsigned)blocks), block(64 * WM * WN * (WS ? 2 : 1));
   const hipStream_t st = (hipStream_t)stream;
   switch (flags) {
-    case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0, NS, UB>), grid, block, 0, st, p); break;
+    case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0, NS, UB, WS>), grid, block, 0, st, p); break;
     case WF_STATS:
-      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS, NS, UB>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS, NS, UB, WS>), grid, block, 0, st, p);
       break;
-    case WF_BNB: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNB, NS, UB>), grid, block, 0, st, p); break;
-    case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP, NS, UB>), grid, block, 0, st, p); break;
+    case WF_BNB: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNB, NS, UB, WS>), grid, block, 0, st, p); break;
+    case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP, NS, UB, WS>), grid, block, 0, st, p); break;
     case WF_BIAS | WF_RELU:
-      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU, NS, UB>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU, NS, UB, WS>), grid, block, 0, st, p);
       break;
-    default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1, NS, UB>), grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1, NS, UB, WS>), grid, block, 0, st, p); break;
   }
   RK_LAUNCH_CHECK();
   return RK_OK;
@@ -1081,6 +1146,10 @@ extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const
   if (variant == 4)
     return launch_gfwd<4, 2, 2, 2, 1, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx,
                                             gu, gy, gbias, stream);
+  // 5: warp-specialised 32 x 32 (4 compute + 4 loader waves, two stages, 147 KiB), blocked weights
+  if (variant == 5)
+    return launch_gfwd<4, 2, 2, 1, 2, true, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups,
+                                                  gx, gu, gy, gbias, stream);
   return RK_EBADARG;
 }
 
@@ -1769,17 +1838,13 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
   const long long blocks = ((N + 63) / 64) * ((T + 3) / 4);
   if (nslab > 1 && slab < 36 * T * N) return RK_EBADARG;
   const long long qs = tmajor ? N : T * N, ts = tmajor ? 36LL * N : N;
-  // vector widths: RAFIKI_PT_OUT_VW = 4 (16-B) | 2 (8-B, default: fewer registers) | 1 (the scalar kernel)
-  static const int vw = getenv("RAFIKI_PT_OUT_VW") ? atoi(getenv("RAFIKI_PT_OUT_VW")) : 2;
-  if ((vw == 2 || vw == 4) && N % vw == 0) {
-    const long long tpb = vw == 4 ? 4 : 2;
-    const long long blocksv = ((N + 63) / 64) * ((T + tpb - 1) / tpb);
-    if (vw == 4)
-      hipLaunchKernelGGL(w4pt_conv_outv_kernel<4>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
-                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
-    else
-      hipLaunchKernelGGL(w4pt_conv_outv_kernel<2>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
-                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
+  // vector width 2 (8-B accesses): measured against 4 (16-B, more registers) and 1 (the scalar kernel),
+  // profiles/vgg_small_f32_step_kernels_r3*.txt
+  constexpr int vw = 2;
+  if (N % vw == 0) {
+    const long long blocksv = ((N + 63) / 64) * ((T + 1) / 2);
+    hipLaunchKernelGGL(w4pt_conv_outv_kernel<vw>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
+                       bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
     RK_LAUNCH_CHECK();
     return RK_OK;
   }

@@ -40,8 +40,6 @@ struct XpParams {
   int groups, flags;            // flags: 1 = accumulate into C
   int splits, ktPer;            // split-K: split s covers K-tiles [s ktPer, (s+1) ktPer), writes slab s
   long long slabStride;         // elements between split-K slabs of C
-  int dbg;                      // DBG builds: 1 no DMA in the K loop, 2 no MFMAs, 4 per-block phase stamps
-  unsigned long long* stamps;   // DBG & 4: per block [start, first tile landed, K loop done, stored, realtime x2]
   unsigned long long bytesA, bytesB;
 };
 
@@ -146,10 +144,7 @@ RK_DEV void xp_store(const XpParams& p, f32x16 (&acc)[MI][NI], int grp, int spli
   }
 }
 
-// DBG: timing-diagnostic build (RAFIKI_X6P_DBG, tiles 0 and 3): p.dbg 1 = no DMA in the K loop, 2 = no MFMAs,
-// 4 = per-block phase stamps (s_memtime shader clocks + s_memrealtime at 100 MHz; lane 0 of wave 0 stores them
-// with vector stores)
-template <int WGM, int WGN, int MI, int NI, int NST, int KT, bool DBG = false>
+template <int WGM, int WGN, int MI, int NI, int NST, int KT>
 __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams p) {
   constexpr int NW = WGM * WGN;
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
@@ -157,12 +152,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
   constexpr int L = XOp<BM, NW, KT>::NQ + XOp<BN, NW, KT>::NQ;   // DMA wave-instructions per wave per K-tile
   __shared__ __attribute__((aligned(16))) char smem[NST * SB];
   const int tid = threadIdx.x, lane = tid & 63;
-  const bool stamp = DBG && (p.dbg & 4) && tid == 0;
-  unsigned long long t0 = 0, r0 = 0, t1 = 0, t2 = 0;
-  if (stamp) {
-    t0 = __builtin_amdgcn_s_memtime();
-    r0 = __builtin_amdgcn_s_memrealtime();
-  }
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid - (wid / WGN) * WGN;
   const int tilesN = (p.N + BN - 1) / BN;
@@ -215,7 +204,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
       s_wait_vmcnt<0>();
     }
     s_barrier_lds();   // every wave's DMA for tile kt is in LDS; every wave is done with tile kt-1
-    if (stamp && kt == 0) t1 = __builtin_amdgcn_s_memtime();
     const char* As = smem + st * SB;
     const char* Bs = As + ABYTES;
     const bool more = kt + NST - 1 < nk;
@@ -243,48 +231,25 @@ __global__ __launch_bounds__(64 * WGM * WGN) void x6p_gemm_kernel(const XpParams
           for (int j = 0; j < NI; ++j) fb[nx][pl][j] = B.frag(Bs, pl, wn * 32 * NI + j * 32, c + 1, lane);
         }
       }
-      if (!DBG || !(p.dbg & 1)) {
 #pragma unroll
-        for (int q = L * c / NC; q < L * (c + 1) / NC; ++q) {
-          if (q < LA) A.issue_q(nxt, kt + NST - 1, wid, more, q);
-          else B.issue_q(nxt + ABYTES, kt + NST - 1, wid, more, q - LA);
-        }
+      for (int q = L * c / NC; q < L * (c + 1) / NC; ++q) {
+        if (q < LA) A.issue_q(nxt, kt + NST - 1, wid, more, q);
+        else B.issue_q(nxt + ABYTES, kt + NST - 1, wid, more, q - LA);
       }
-      if (DBG && (p.dbg & 2)) {   // keep the fragment reads, drop the MFMAs
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[cur][pl][i]));
-#pragma unroll
-          for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fb[cur][pl][j]));
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-            acc[i][j] = mfma6(fa[cur][0][i], fa[cur][1][i], fa[cur][2][i], fb[cur][0][j], fb[cur][1][j],
-                              fb[cur][2][j], acc[i][j]);
-      }
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = mfma6(fa[cur][0][i], fa[cur][1][i], fa[cur][2][i], fb[cur][0][j], fb[cur][1][j],
+                            fb[cur][2][j], acc[i][j]);
       xp_sched<NM, (c + 1 < NC ? NR : 0), L * (c + 1) / NC - L * c / NC>();
       __builtin_amdgcn_sched_barrier(0);
     });
     st = st + 1 == NST ? 0 : st + 1;
   }
   s_wait_vmcnt<0>();   // the trailing zero-DMAs land before the workgroup's LDS is released
-  if (stamp) t2 = __builtin_amdgcn_s_memtime();
 
   xp_store<MI, NI>(p, acc, grp, split, m0 + wm * 32 * MI, n0 + wn * 32 * NI, lane);
-  if (stamp) {
-    __builtin_amdgcn_s_waitcnt(0);   // the block's stores issued (their issue cost is what is timed)
-    unsigned long long* o = p.stamps + (long long)blockIdx.x * 8;
-    o[0] = t0;
-    o[1] = t1;
-    o[2] = t2;
-    o[3] = __builtin_amdgcn_s_memtime();
-    o[4] = r0;
-    o[5] = __builtin_amdgcn_s_memrealtime();
-  }
 }
 
 // Warp-specialised variant: 2 x 2 compute waves (wave tile 32 MI x 32 NI) that only read fragments and
@@ -433,7 +398,7 @@ int ws_launch_kt(const XpParams& p, int nst, int kt, hipStream_t st) {
   return kt == 64 ? ws_launch<MI, NI, 64>(p, nst, st) : ws_launch<MI, NI, 32>(p, nst, st);
 }
 
-template <int WGM, int WGN, int MI, int NI, int KT, bool DBG = false>
+template <int WGM, int WGN, int MI, int NI, int KT>
 int xp_launch(const XpParams& p, int nst, hipStream_t st) {
   constexpr int BM = WGM * 32 * MI, BN = WGN * 32 * NI;
   constexpr int SB = 3 * (BM + BN) * 2 * KT;
@@ -442,12 +407,12 @@ int xp_launch(const XpParams& p, int nst, hipStream_t st) {
   const dim3 grid((unsigned)blocks), block(64 * WGM * WGN);
   if (nst == 3) {
     if constexpr (3 * SB <= 163840)
-      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 3, KT, DBG>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 3, KT>), grid, block, 0, st, p);
     else
       return RK_EUNSUPPORTED;
   } else {
     if constexpr (2 * SB <= 163840)
-      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 2, KT, DBG>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((x6p_gemm_kernel<WGM, WGN, MI, NI, 2, KT>), grid, block, 0, st, p);
     else
       return RK_EUNSUPPORTED;
   }
@@ -474,8 +439,6 @@ __global__ __launch_bounds__(256) void x6p_split_kernel(const float* __restrict_
   dst[o + 2 * ps] = l;
 }
 
-unsigned long long* g_stamps = nullptr;
-long long g_stamp_n = 0;
 
 }  // namespace
 
@@ -518,22 +481,8 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
   p.splits = rk_cdiv(nk, p.ktPer);   // every split gets >= 1 K-tile
   if (p.splits != splits) return RK_EBADARG;
   p.slabStride = splits > 1 ? slabStride : 0;
-  static const int dbg = getenv("RAFIKI_X6P_DBG") ? atoi(getenv("RAFIKI_X6P_DBG")) : 0;
-  p.dbg = dbg;
-  p.stamps = nullptr;
-  if (dbg & 4) {
-    const long long need = (long long)rk_cdiv(M, 128) * rk_cdiv(N, 64) * 4 * groups * splits * 8;   // >= blocks*8 for 64x64
-    if (need > g_stamp_n) {
-      if (g_stamps) (void)hipFree(g_stamps);
-      if (hipMalloc((void**)&g_stamps, need * 8) != hipSuccess) return RK_ELAUNCH;
-      g_stamp_n = need;
-    }
-    p.stamps = g_stamps;
-  }
   p.bytesA = (unsigned long long)bytesA; p.bytesB = (unsigned long long)bytesB;
   const hipStream_t st = (hipStream_t)stream;
-  if (dbg && kt == 32 && (tile == 0 || tile == 3))
-    return tile == 0 ? xp_launch<2, 2, 2, 2, 32, true>(p, nst, st) : xp_launch<2, 2, 1, 1, 32, true>(p, nst, st);
   switch (tile) {
     case 0: return xp_launch_kt<2, 2, 2, 2>(p, nst, kt, st);
     case 1: return xp_launch_kt<2, 2, 2, 1>(p, nst, kt, st);
@@ -552,12 +501,6 @@ extern "C" int rk_x6p_gemm(int tile, int nst, const void* A, const void* B, floa
     case 12: return ws_launch_kt<1, 1>(p, nst, kt, st);
   }
   return RK_EBADARG;
-}
-
-// DBG & 4: the per-block stamps of the last diagnostic launch (8 x u64 per block) -> host
-extern "C" int rk_x6p_stamps(void* host, long long n) {
-  if (!g_stamps || n > g_stamp_n) return RK_EBADARG;
-  return hipMemcpy(host, g_stamps, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? RK_OK : RK_ELAUNCH;
 }
 
 // planes [3][rows][ldd] (plane stride ps) of an fp32 [rows][lds] matrix

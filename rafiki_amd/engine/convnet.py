@@ -262,29 +262,20 @@ class ConvNetEngine:
         fl += 2.0 * self.d_last * self.num_classes
         return fl
 
-    # Measured on MI355X (VGG-small, batch 256): overlapping wgrad on a side stream made the step
-    # 11% SLOWER (1.161 -> 1.289 ms; the concurrent GEMMs and split-K slab traffic interfere) and,
-    # re-measured with the current kernels, still 5-6% slower (258k -> 243-245k img/s), so it is off
-    # by default (RAFIKI_OVERLAP_WGRAD=1) and kept as an option for layer shapes where it pays.
-    # fp32 path (Winograd kernels, one or two LDS-heavy workgroups per CU): 2.27 -> 2.46 ms, 8% slower.
-    # 'deep': only the 8x8 / 4x4 layers (grids of a few hundred workgroups that leave CUs idle)
-    overlap_wgrad = os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') in ('1', 'deep')
-    overlap_max_hw = 8 if os.environ.get('RAFIKI_OVERLAP_WGRAD', '0') == 'deep' else 1 << 30
+    # Weight gradients run in stream order.  Overlapping them on a side stream was measured slower on
+    # VGG-small every time it was tried: bf16 1.161 -> 1.289 ms, fp32 2.27 -> 2.46 ms, and with the
+    # round-4 kernels 5-6% (profiles/step_switches_ab_r4.txt): the concurrent GEMMs and split-K slab
+    # traffic interfere, and the LDS-heavy Winograd kernels leave no room for a second workgroup.
     _acc_zeroed_by_prologue = False  # set while a scheduled step's gather kernel zeroes the BN tables
-    fuse_bn_dgrad = os.environ.get('RAFIKI_BN_DGRAD_FUSE', '1') != '0'
-    # ... and into BN+ReLU+max-pool blocks (FLAG_BNP: argmax routing in the dgrad epilogue)
-    fuse_bn_pool = os.environ.get('RAFIKI_BN_POOL_FUSE', '1') != '0'
+    # the dgrad epilogue forms the ReLU mask / max-pool routing and BN-backward sums of the layer below
+    # (FLAG_BNB / FLAG_BNP), so its BN backward is a single apply pass
+    fuse_bn_dgrad = True
+    fuse_bn_pool = True
     # data gradients as forward convs of dy with flipped/transposed weights (F.ConvWT, one transpose
     # launch per step): the forward kernels' K-inner weight operand and tiles are the faster ones
-    dgrad_wt = os.environ.get('RAFIKI_DGRAD_WT', '1') != '0'
+    dgrad_wt = True
     # fp32 path: the classifier head (output layer, softmax-xent, its gradients) as two fused launches
-    fused_head = os.environ.get('RAFIKI_FUSED_HEAD', '1') != '0'
-
-    def _side_stream(self):
-        st = getattr(self, '_wgrad_stream', None)
-        if st is None:
-            st = self._wgrad_stream = torch.cuda.Stream(device=self.device)
-        return st
+    fused_head = True
 
     def reset_metrics(self):
         self.loss_sum.zero_()
@@ -360,13 +351,6 @@ class ConvNetEngine:
                      dgamma=fl.g('in_bn.gamma'), dbeta=fl.g('in_bn.beta'))
             return
         d = d.view(B, self.feat_hw, self.feat_hw, -1)
-        # Weight gradients are off the critical path (nothing downstream in this step reads them
-        # before the optimizer), so they run on a side HIP stream, overlapping the main chain
-        # bn_bwd -> dgrad -> bn_bwd -> ... ; each individual GEMM is latency-bound at these sizes,
-        # so two concurrent kernels fill the CUs better than either alone.  Fork/join through
-        # stream waits is captured into the hipGraph as graph edges.
-        main = torch.cuda.current_stream(self.device)
-        side = self._side_stream()
         reduced = False
         wt = self._conv_wt() if self.dgrad_wt else None
         if wt is not None:
@@ -380,14 +364,7 @@ class ConvNetEngine:
             else:
                 dy = F.bn_bwd(d, y, coeffs, fl.w(name + '.gamma'), pool=pool, act=F.ACT_RELU,
                               dgamma=fl.g(name + '.gamma'), dbeta=fl.g(name + '.beta'))
-            if self.overlap_wgrad:
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    F.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
-                dy.record_stream(side)
-                acts[bi].record_stream(side)
-            else:
-                F.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
+            F.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
             if bi > 0:
                 # into a pool-free BN+ReLU block: its ReLU mask and BN-backward sums ride in the
                 # dgrad epilogue (FLAG_BNB), so its bn_bwd_acc is a single apply pass
@@ -410,8 +387,6 @@ class ConvNetEngine:
                     d = F.conv_dgrad(dy, fl.wb(name + '.w'), bn_y=py, bn_coeffs=pco, bn_acc=accs[bi - 1][1])
                 else:
                     d = F.conv_dgrad(dy, fl.wb(name + '.w'))
-        if self.overlap_wgrad:
-            main.wait_stream(side)
 
     # ------------------------------------------------------------------------- fp32 train
     def _fwd_bwd_gpu_f32(self, x, labels):
@@ -507,10 +482,6 @@ class ConvNetEngine:
             # flipped/transposed fp32 weights of every dgrad layer, refreshed (one launch) on first use
             wt.begin_step()
         reduced = False
-        # RAFIKI_OVERLAP_WGRAD=1: weight gradients on a side stream (fork / join become graph edges),
-        # so a weight gradient and the next data gradient share the CUs
-        main = torch.cuda.current_stream(self.device)
-        side = self._side_stream() if self.overlap_wgrad else None
         for bi in range(len(self.blocks) - 1, -1, -1):
             name, cin, cout, pool, hw = self.blocks[bi]
             y, coeffs = saved[bi]
@@ -520,14 +491,7 @@ class ConvNetEngine:
             else:   # ReLU mask / pool routing only; sum dz -> the bias gradient
                 dy = S.bn_bwd(d, y, coeffs, self._ones[:cout], accs[bi][1], pool=pool, act=F.ACT_RELU,
                               dbeta=fl.g(name + '.b'), reduced=reduced, count=float('inf'))
-            if side is not None and hw <= self.overlap_max_hw:
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
-                dy.record_stream(side)
-                acts[bi].record_stream(side)
-            else:
-                S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
+            S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
             if bi == 0:
                 break
             py, pco = saved[bi - 1]
@@ -549,8 +513,6 @@ class ConvNetEngine:
             else:
                 d = S.conv_dgrad(dy, wl, **dk)
                 reduced = False
-        if side is not None:
-            main.wait_stream(side)
         if ww is not None:
             ww.end_step()   # only the Winograd sets the tuned convs use are transformed from now on
 

@@ -1,7 +1,7 @@
 """Per-shape kernel-config autotuning for the igemm engine (find-once, replay-forever).
 
 The best (tile shape, staging variant, split-K) differs per layer shape (measured on MI355X with
-scripts/bench_igemm.py: e.g. the LDS-DMA 2-stage ring wins on 16x16/8x8 layers, 64x64 register
+scripts/dev/bench_igemm.py: e.g. the LDS-DMA 2-stage ring wins on 16x16/8x8 layers, 64x64 register
 staging on the 4x4x512 layers).  The first time a shape is seen outside hipGraph capture, every
 candidate runs a few times under HIP events and the fastest is cached.  During capture only
 cached/heuristic configs are used, so captured graphs never contain tuning launches.
@@ -35,8 +35,8 @@ _loaded = False
 _disk_mtime = [None]
 stats = {'tuned': 0, 'seconds': 0.0, 'candidates': 0, 'loaded': 0, 'reloads': 0}
 ENABLED = os.environ.get('RAFIKI_AUTOTUNE', '1') != '0'
-REPS = int(os.environ.get('RAFIKI_AUTOTUNE_REPS', '3'))
-PASSES = int(os.environ.get('RAFIKI_AUTOTUNE_PASSES', '2'))
+REPS = 3      # timed replays per candidate and pass (at least 5 when timing a captured graph)
+PASSES = 2    # sweeps over the candidates, min per candidate (the first also absorbs clock ramp-up)
 SHIPPED_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tune')
 _ident = {}
 
@@ -224,24 +224,32 @@ def _time_eager(cfg, run, reps):
     return s.elapsed_time(e) / reps
 
 
+def _valid(hit, candidates):
+    """A stored pick is used only if it is still one of this call's candidates (a database written by other
+    candidate-generation code, or for a key whose candidate set changed, is never replayed blindly)."""
+    return hit is not None and tuple(hit) in {tuple(c) for c in candidates}
+
+
 def tune(key, candidates, run):
     """candidates: list of config tuples; run(cfg) launches the op once.  Returns the best cfg."""
     hit = lookup(key)
+    if _valid(hit, candidates):
+        return tuple(hit)
     if hit is not None:
-        return hit
+        stats['stale'] = stats.get('stale', 0) + 1
     if not can_tune():
         return candidates[0]
     with _GRAPH_LOCK:   # sweeps time captured graphs: never interleave with another thread's capture
         hit = lookup(key)
-        if hit is not None:
-            return hit
+        if _valid(hit, candidates):
+            return tuple(hit)
         return _tune_locked(key, candidates, run)
 
 
 def _tune_locked(key, candidates, run):
     import time as _time
     t_start = _time.perf_counter()
-    use_graph = os.environ.get('RAFIKI_AUTOTUNE_GRAPH', '1') != '0'
+    use_graph = True   # candidates timed inside a captured hipGraph (host launch overhead excluded)
     # PASSES sweeps over the candidates, min per candidate: the first sweep also absorbs clock
     # ramp-up after idle, which otherwise penalises whichever candidates happen to run first
     times = {}

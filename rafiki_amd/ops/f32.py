@@ -43,8 +43,6 @@ def tile_dims(t: int):
     return TILES[t & 15]
 
 
-# RAFIKI_SGEMM_CFG="tile,nst" pins every sgemm launch (A/B runs without the tuner)
-_PIN = tuple(int(v) for v in os.environ['RAFIKI_SGEMM_CFG'].split(',')) if os.environ.get('RAFIKI_SGEMM_CFG') else None
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -144,11 +142,9 @@ def _cands(M, N, splittable=False, K=0, big=False):
 def _pick(key, cands, run, protect=()):
     """The tuned config for ``key``.  ``protect``: tensors the op accumulates into — a tuning sweep runs
     every candidate several times, so their contents are saved first and restored afterwards."""
-    if _PIN is not None:
-        return (_PIN[0], _PIN[1], cands[0][2])
     if not autotune.ENABLED:
         return cands[0]
-    if protect and autotune.lookup(key) is None and autotune.can_tune():
+    if protect and not autotune._valid(autotune.lookup(key), cands) and autotune.can_tune():
         saved = [t.clone() for t in protect]
         cfg = autotune.tune(key, cands, run)
         for t, v in zip(protect, saved):
@@ -540,9 +536,10 @@ def wino4_ut(w: torch.Tensor) -> torch.Tensor:
 
 # blocked-weight variants of the fused F(4x4) kernel (weights as the kernel's LDS stage image, one contiguous
 # 36-KiB block per 32 output channels x 8 input channels: rk_wino4b_weights / WinoWeights 'u4b' / 'ut4b'):
-# variant 3 = variant 0's 8-wave tile, 4 = variant 1's 4-wave tile
-WINO4B_CFGS = ((-15, 0, 1), (-16, 0, 1))
-_WINO4B_VARIANT = {-15: 3, -16: 4}
+# variant 3 = variant 0's 8-wave tile, 4 = variant 1's 4-wave tile, 5 = warp-specialised (4 compute + 4 loader
+# waves over two LDS stages)
+WINO4B_CFGS = ((-17, 0, 1), (-18, 0, 1), (-19, 0, 1))
+_WINO4B_VARIANT = {-17: 3, -18: 4, -19: 5}
 
 
 def wino4b_numel(N: int, C: int) -> int:
@@ -1260,7 +1257,7 @@ def col_stats(a2d, acc, b2d=None):
     return acc
 
 
-_BWD_BLOCKS = int(os.environ.get('RAFIKI_BNF_BWD_BLOCKS', '1024'))
+_BWD_BLOCKS = 1024   # grid cap of the BN-backward reduce (8 passes of pixel rows per block)
 
 
 def bn_bwd(dout, y, coeffs, gamma, acc, *, pool=False, act=ACT_RELU, slope=0.2, dgamma=None, dbeta=None, dy=None,

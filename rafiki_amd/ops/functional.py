@@ -25,10 +25,10 @@ FLAG_SATOM = 256
 FLAG_BNB = 512
 FLAG_BNP = 1024  # dgrad into a BN+ReLU+maxpool layer: its BN-backward sums in the epilogue
 # BatchNorm statistics as fp64 atomic sums in a few slots (conv epilogue / bwd reduce) consumed by
-# fused finalize+apply kernels: 2 launches per BN layer and direction instead of 4 / 3.  Summation
-# order then varies run to run in the last bits; RAFIKI_BN_ATOMIC=0 keeps the deterministic
-# partial-row path.
-BN_ATOMIC = os.environ.get('RAFIKI_BN_ATOMIC', '1') != '0'
+# fused finalize+apply kernels: 2 launches per BN layer and direction instead of 4 / 3 (summation order
+# varies run to run in the last bits of the fp64 sums; the partial-row path remains for channel counts
+# the slot kernels do not take)
+BN_ATOMIC = True
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 # shape 4: 64x64 wave-K-split kernel (igemm_ks_kernel, LDS-DMA rings only): each wave owns the whole
 # tile for a quarter of every K-tile pair — half the LDS reads per MFMA of shape 3 (small-M layers)
@@ -37,8 +37,7 @@ KS_TILE = 4
 _KS_VARIANTS = (64, 32)  # 2-stage (64 KiB LDS, 2 blocks/CU) and 3-stage (96 KiB) rings
 NUM_CU = 256
 # Kernel variant bits OR'ed into the tile code (see rk_igemm): 0 register-staged, 16 register ring,
-# 32 LDS-DMA 3-stage ring, 64 LDS-DMA 2-stage, 128 LDS-DMA 4-stage.
-VARIANT = int(os.environ.get('RAFIKI_IGEMM_VARIANT', '0'))
+# 32 LDS-DMA 3-stage ring, 64 LDS-DMA 2-stage, 128 LDS-DMA 4-stage (chosen per shape by the tuner).
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -89,9 +88,9 @@ def pick_splits(M: int, N: int, K: int, tile: int, target_blocks: int = 2 * NUM_
 
 
 # Staging variants the tuner tries.  The 3/4-stage LDS-DMA rings (32/128) win some isolated timings
-# but lose inside the training step (less occupancy when neighbouring kernels share L2), so they are
-# opt-in: RAFIKI_IGEMM_DEEP=1.
-_VARIANTS = (0, 64, 32, 128) if os.environ.get('RAFIKI_IGEMM_DEEP', '0') == '1' else (0, 64)
+# but lose inside the training step (less occupancy when neighbouring kernels share L2), so they are not
+# offered (the kernels keep them: tile codes | 32 / | 128).
+_VARIANTS = (0, 64)
 
 
 def _tile_candidates(M, N, fixed_bm=None, ks=True):
@@ -139,7 +138,7 @@ def _split_candidates(M, N, K):
 
 def _tuned(key, candidates, run):
     from . import autotune
-    if VARIANT or not autotune.ENABLED:
+    if not autotune.ENABLED:
         return candidates[0]
     return autotune.tune(key, candidates, run)
 
@@ -148,8 +147,6 @@ def igemm(kind, epi, A, B, out, M, N, K, lda=0, ldb=0, ldc=0, *, bias=None, stat
           C=8, taps=1, Cb=1, splits=1, slab_stride=0, flags=0, alpha=1.0, slope=0.2, tile=None):
     if tile is None:
         tile = pick_tile(M, N)
-    if VARIANT and tile < 16:
-        tile |= VARIANT
     _lib.call("rk_igemm", kind, epi, tile, _p(A), _p(B), _p(out), _p(bias), _p(stats), _p(gate), M, N, K, lda, ldb,
               ldc, H, W, C, taps, Cb, splits, slab_stride, flags, alpha, slope, _nbytes(A), _nbytes(B), _s())
     return out
@@ -163,8 +160,8 @@ def stats_rows(M: int, N: int, tile: Optional[int] = None) -> int:
 
 # Halo-tiled 3x3 conv (rk_hconv): one LDS patch per (item, 64-channel chunk) serves all 9 taps.
 # Candidates are ('h', bn_bit, grid): grid 0 = one item per block, else a persistent grid.
-HCONV = os.environ.get('RAFIKI_HCONV', '1') != '0'
-KS = os.environ.get('RAFIKI_IGEMM_KS', '1') != '0'
+HCONV = True
+KS = True
 
 
 def _hconv_bm(W: int) -> int:
@@ -212,7 +209,7 @@ def slab_epi(slab, S, M, N, out, *, mode=0, gate=None, scale=None, shift=None, a
 # Split-K conv forward / data-gradient: ('k', tile, S) = S fp32 slabs from the igemm + one rk_slab_epi
 # combine.  Offered only where a big tile shape (fewer L2->LDS re-reads of both operands) has too few
 # output tiles to fill the chip on its own: the VGG 4x4 / 8x8 layers (M = 4096 / 16384 at batch 256).
-CONV_SPLIT = os.environ.get('RAFIKI_CONV_SPLIT', '1') != '0'
+CONV_SPLIT = True
 
 
 def _conv_split_candidates(M, N, K, H, W, C):
@@ -234,7 +231,7 @@ def _conv_split_candidates(M, N, K, H, W, C):
     return out
 
 
-_BWD_RED_CAP = int(os.environ.get('RAFIKI_BN_RED_CAP', '2048'))
+_BWD_RED_CAP = 2048
 
 
 def bn_slots(C: int) -> int:

@@ -9,10 +9,10 @@ WHAT="${*:-lstm pggan serve}"
 for w in $WHAT; do
   case $w in
     lstm)
-      timeout -k 10 300 python3 -u scripts/bench_lstm.py --reps 20 > $O/lstm.json 2> $O/lstm.err || exit 1
+      timeout -k 10 300 python3 -u scripts/dev/bench_lstm.py --reps 20 > $O/lstm.json 2> $O/lstm.err || exit 1
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/lstm_prof -o run -- \
-        python3 scripts/bench_lstm.py --reps 5 --only-tagger > $O/lstm_prof.log 2>&1 || exit 1
-      python3 scripts/kernel_summary.py $(find $O/lstm_prof -name '*kernel_trace.csv' | head -1) > $O/lstm_kernels.txt
+        python3 scripts/dev/bench_lstm.py --reps 5 --only-tagger > $O/lstm_prof.log 2>&1 || exit 1
+      python3 scripts/dev/kernel_summary.py $(find $O/lstm_prof -name '*kernel_trace.csv' | head -1) > $O/lstm_kernels.txt
       rm -rf $O/lstm_prof
       cat $O/lstm.json; head -30 $O/lstm_kernels.txt ;;
     pggan)

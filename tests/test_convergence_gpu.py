@@ -6,7 +6,7 @@ full-width VGG-small (the bench model) from the same initial weights on the same
 class-conditional 32x32 images with heavy noise and 20% uniformly relabelled targets (Bayes accuracy
 <= 82%), with nesterov SGD (lr 0.01, momentum 0.9) + weight decay.  Every step sees fresh images
 (38,400 = 300 x 128), so the training loss estimates the population loss.  Measured on MI355X
-(profiles/bf16_vs_fp32_convergence_r2.json; scripts/convergence_sweep.py): mean window gap 0.019 nats,
+(profiles/bf16_vs_fp32_convergence_r2.json; scripts/dev/convergence_sweep.py): mean window gap 0.019 nats,
 largest 0.089, final window 0.0025, test accuracy 0.815 (fp32) vs 0.818 (bf16).
 Gates:
   * 25-step window-mean training loss: mean |bf16 - fp32| <= 0.05, max <= 0.2, last window <= 0.03 nats;

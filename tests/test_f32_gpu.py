@@ -221,7 +221,7 @@ def test_engine_grads_match_fp64_reference():
 @pytest.mark.parametrize("wino", [False, True])
 def test_engine_grads_vgg_small_full_width(wino, monkeypatch):
     """Direct convs: 1e-4 (or 2x torch fp32).  With the fused Winograd convs as autotune candidates
-    the conv outputs are as accurate (scripts/wino_error.py: 2.6e-7..7.4e-7 vs fp64, direct
+    the conv outputs are as accurate (scripts/dev/wino_error.py: 2.6e-7..7.4e-7 vs fp64, direct
     4.2e-7..5.9e-7) but round differently from torch, so a ReLU-boundary sign in the 4x4 layers can
     flip where torch's does not — one flipped element moves a BN dgamma by ~1e-4 relative: gate 1e-3."""
     from rafiki_amd.ops import f32 as S
@@ -260,7 +260,10 @@ def test_engine_no_bn_grads_match_fp64_reference(wino, monkeypatch):
             eng.train_step(x, y)
         assert all(eng.flat.w(b[0] + '.b').abs().sum().item() > 0 for b in eng.blocks)
         eng.reset_metrics()
-        x, y = _batch(B, hw=image_size, seed=9)
+        # (seed 9 on the 48x48 net with the direct stem puts one stem max-pool window within fp32 rounding of
+        # a tie, whose flipped argmax moves conv0.w's gradient by 1.8e-3 while every other gradient and the
+        # stem's dy sum stay at 1e-7: scripts/dev/nobn_diag3.py; seed 11 has no such window)
+        x, y = _batch(B, hw=image_size, seed=11)
         _grad_check(eng, x, y, 1e-3 if wino else 1e-4)
 
 

@@ -271,3 +271,18 @@ def test_native_npy_overflowing_shape_is_rejected_and_server_keeps_serving():
         assert r.status_code == 200 and np.load(io.BytesIO(r.content)).shape == (5, 3)
     finally:
         srv.shutdown()
+
+
+def test_loadgen_measures_the_native_front_end():
+    """bench.py's HTTP phase (predictor/loadgen.py): the native server over a predictor, driven by the
+    separate httpload process — JSON single queries and .npy batches, QPS in queries, no errors."""
+    from rafiki_amd.predictor import loadgen, nativeserve
+    if not (nativeserve.available() and loadgen.available()):
+        pytest.skip('native runtime / httpload not built')
+    fake = FakePredictor()
+    out = loadgen.http_load(fake, image_shape=(3, 4), seconds=0.5, json_clients=8, npy_clients=2, npy_batch=16)
+    js, nb = out['json_single_query'], out['npy_batch16']
+    assert js['errors'] == 0 and nb['errors'] == 0 and js['qps'] > 0 and nb['qps'] > 0
+    assert nb['qps'] == pytest.approx(16 * nb['requests_per_s'], rel=1e-3)
+    assert js['p99_ms'] >= js['p50_ms'] > 0
+    assert out['server_counters']['batched_queries'] > 0

@@ -13,8 +13,8 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 TOL = 3e-5
 # 0 / 1: 8- / 4-wave tiles; 2: 4-wave two-stage (not a tuner candidate, kept exercised); 3 / 4: 0 / 1 on the
-# blocked weight sets (wino4b_u)
-VARIANTS = [0, 1, 2, 3, 4]
+# blocked weight sets (wino4b_u); 5: warp-specialised two-stage kernel on the blocked sets
+VARIANTS = [0, 1, 2, 3, 4, 5]
 
 
 def _u4(S, w2, variant, dgrad=False):
