@@ -19,7 +19,8 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
                                                            int ignore_index, float grad_scale,
                                                            DT* __restrict__ dlogits, int ldd,
                                                            float* __restrict__ probs, float* loss_sum,
-                                                           int* correct, int* counted) {
+                                                           int* correct, int* counted,
+                                                           const float* __restrict__ scale_ptr) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -43,6 +44,10 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   const float lse = mx + __logf(se);
   const int y = labels ? labels[row] : -1;
   const bool valid = labels && y != ignore_index && y >= 0 && y < ncls;
+  // scale_ptr: a device factor on the gradient and the loss (the tagger's 1 / #valid tokens of a batch,
+  // written with the batch, so a replayed graph takes each batch's mean)
+  const float sc = scale_ptr ? scale_ptr[0] : 1.f;
+  grad_scale *= sc;
   if (dlogits) {
     DT* dr = dlogits + (long long)row * ldd;
     for (int c = lane; c < ldd; c += 64) {
@@ -56,7 +61,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
     for (int c = lane; c < ncls; c += 64) pr[c] = __expf(lr[c] - lse);
   }
   if (lane == 0 && valid) {
-    if (loss_sum) atomicAdd(loss_sum, lse - lr[y]);
+    if (loss_sum) atomicAdd(loss_sum, (lse - lr[y]) * sc);
     if (correct) atomicAdd(correct, amax == y ? 1 : 0);
     if (counted) atomicAdd(counted, 1);
   }
@@ -386,7 +391,8 @@ extern "C" int rk_softmax_xent(const float* logits, int ldl, const int* labels, 
                                int* counted, void* stream) {
   if (B <= 0) return RK_OK;
   hipLaunchKernelGGL(softmax_xent_kernel<bf16>, dim3(rk_cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, logits, ldl,
-                     labels, B, ncls, ignore_index, grad_scale, (bf16*)dlogits, ldd, probs, loss_sum, correct, counted);
+                     labels, B, ncls, ignore_index, grad_scale, (bf16*)dlogits, ldd, probs, loss_sum, correct, counted,
+                     nullptr);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -397,7 +403,20 @@ extern "C" int rk_softmax_xent_f32(const float* logits, int ldl, const int* labe
                                    int* correct, int* counted, void* stream) {
   if (B <= 0) return RK_OK;
   hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(rk_cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, logits, ldl,
-                     labels, B, ncls, ignore_index, grad_scale, dlogits, ldd, probs, loss_sum, correct, counted);
+                     labels, B, ncls, ignore_index, grad_scale, dlogits, ldd, probs, loss_sum, correct, counted,
+                     nullptr);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// fp32 d(logits) with a device scale factor: gradient and loss both times *scale (mean over a
+// data-dependent count, e.g. the non-ignored tokens of a tagger batch)
+extern "C" int rk_softmax_xent_f32s(const float* logits, int ldl, const int* labels, int B, int ncls,
+                                    int ignore_index, const float* scale, float* dlogits, int ldd, float* loss_sum,
+                                    void* stream) {
+  if (B <= 0) return RK_OK;
+  hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(rk_cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, logits, ldl,
+                     labels, B, ncls, ignore_index, 1.0f, dlogits, ldd, nullptr, loss_sum, nullptr, nullptr, scale);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -22,12 +22,12 @@
 //      bwd2:  gg_out = [ggx, H_j, 0],  H_j = sum_{k,pc} ggx_k (x_k - mu) / (g s P C)
 //             g_x_k = G_j / (g P C s) * (ggx_k - mean(ggx) - u_k * mean(ggx * u)),  u = (x - mu) / s
 #include "common.h"
+#include "philox.h"
 
 #include <algorithm>
 
 namespace {
 
-struct U4 { uint32_t v[4]; };
 
 // 8 consecutive channels of a bf16 or fp32 NHWC row <-> 8 floats (the PG-GAN ops run in either
 // precision: bf16 for the opt-in fast path, fp32 — the reference's precision — by default)
@@ -44,25 +44,6 @@ template <> RK_DEV void st8<float>(float* p, const float (&f)[8]) {
   *(f32x4*)p = f32x4{f[0], f[1], f[2], f[3]};
   *(f32x4*)(p + 4) = f32x4{f[4], f[5], f[6], f[7]};
 }
-
-RK_DEV U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
-  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
-    const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
-    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-    k0 += W0; k1 += W1;
-  }
-  U4 o;
-  o.v[0] = c0; o.v[1] = c1; o.v[2] = c2; o.v[3] = c3;
-  return o;
-}
-
-// [0, 1) with 24 random mantissa bits; (0, 1] variant for the Box-Muller log
-RK_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
-RK_DEV float u01_open(uint32_t x) { return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f); }
 
 // dist 0: a + b*U[0,1) (fp32)   1: a + b*N(0,1) (fp32)   2: floor(U*hi) (int32)
 __global__ __launch_bounds__(256) void philox_kernel(void* __restrict__ out, long long n, int dist, int hi, float a,

@@ -669,10 +669,14 @@ class PgGan(BaseModel):
         # group rehearses capture of the DP round on a single GPU)
         if self.world > 1 or bool(knobs.get('force_grad_allreduce', False)):
             force = self.world == 1
+            # 4 MiB buckets: at lod 3 only a third of the arena receives gradients, and the finer buckets
+            # both skip more of the untouched blocks and start reducing earlier in the backward
+            # (docs/architecture.md, comm model); RAFIKI_GRAD_BUCKET_MB / the knob override it
+            bmb = knobs.get('grad_bucket_mb', os.environ.get('RAFIKI_GRAD_BUCKET_MB', 4))
             g_ar = FlatGradAllReduce(nets.G.grad, nets.G.param_ranges(), list(nets.g_params.values()), self.world,
-                                     force=force)
+                                     force=force, bucket_mb=float(bmb))
             d_ar = FlatGradAllReduce(nets.D.grad, nets.D.param_ranges(), list(nets.d_params.values()), self.world,
-                                     force=force)
+                                     force=force, bucket_mb=float(bmb))
         rng = TrialRng(dev, self.seed * 7919)   # one stream for all ranks; each keeps its shard
         # RCCL collectives are graph-capturable, gloo ones are not (a gloo group on GPUs is the
         # one-box multi-rank rehearsal: eager)
@@ -688,7 +692,8 @@ class PgGan(BaseModel):
         # collective segments a gloo group (the one-box multi-rank rehearsal) is capturable too.
         whole = g_ar is not None and (self.ctx.dist.backend == 'nccl'
                                       and os.environ.get('RAFIKI_PGGAN_GRAPH_COLLECTIVES', '0') == '1')
-        segmented = g_ar is not None and not whole
+        # dp_segmented=False (tests): the unsegmented round — hooks launch the buckets, finish() waits
+        segmented = g_ar is not None and not whole and bool(knobs.get('dp_segmented', True))
         capturable = g_ar is None or whole or segmented
         graphs = GraphedRounds(dev.type == 'cuda' and capturable and bool(knobs.get('cuda_graph', True))
                                and os.environ.get('RAFIKI_PGGAN_GRAPH', '1') != '0', collectives=whole)
@@ -715,6 +720,9 @@ class PgGan(BaseModel):
             if lod_int not in level_cache:
                 level_cache.clear()
                 graphs.clear()
+                for ar in (g_ar, d_ar):
+                    if ar is not None:
+                        ar.clear_plans()
                 level_cache[lod_int] = torch.as_tensor(ds.images[lod_int]).to(dev)
             level = level_cache[lod_int]
             if np.floor(sched.lod) != np.floor(prev_lod) or np.ceil(sched.lod) != np.ceil(prev_lod):
@@ -734,7 +742,8 @@ class PgGan(BaseModel):
                 self.train_round(sched.lod, mb, level, labels_all, rng, G_opt, D_opt, acc, D_repeats=D_repeats,
                                  G_smoothing=G_smoothing, d_ar=d_ar, g_ar=g_ar)
             segs = (self.round_segments(sched.lod, mb, level, labels_all, rng, G_opt, D_opt, acc,
-                                        D_repeats=D_repeats, G_smoothing=G_smoothing, d_ar=d_ar, g_ar=g_ar)
+                                        D_repeats=D_repeats, G_smoothing=G_smoothing, d_ar=d_ar, g_ar=g_ar,
+                                        tag=key)
                     if segmented else None)
             for _ in range(minibatch_repeats):
                 if frac == 0 and segs is not None:
@@ -793,10 +802,14 @@ class PgGan(BaseModel):
             opt.skip_flag.fill_(0 if bool(torch.isfinite(flat.grad).all()) else 1)
 
     def round_segments(self, lod, mb, level, labels_all, rng, G_opt, D_opt, acc, *, D_repeats=1, G_smoothing=0.99,
-                       d_ar=None, g_ar=None):
+                       d_ar=None, g_ar=None, tag=None):
         """train_round as segments for GraphedRounds.run_segments: per D step gradients ('g'), the
         bucketed all-reduce of D.grad ('e'), then mean + finite guard + Adam + Gs EMA ('g'); likewise
-        the G step.  Adjacent compute segments are merged (D_repeats + 2 graphs per round)."""
+        the G step.  Adjacent compute segments are merged (D_repeats + 2 graphs per round).  The
+        all-reduce segments come from FlatGradAllReduce.overlapped: in a replayed round each bucket's
+        all-reduce starts as soon as the captured backward has written its last gradient (external
+        event per bucket), and buckets no contribution reached (blocks above the current LOD) are
+        skipped."""
         nets = self.nets
 
         def d_grads():
@@ -816,9 +829,11 @@ class PgGan(BaseModel):
             nets.set_requires_grad(nets.d_params, True)
 
         raw = []
-        for _ in range(D_repeats):
-            raw += [('g', d_grads), ('e', d_ar.allreduce_now), ('g', d_apply)]
-        raw += [('g', g_grads), ('e', g_ar.allreduce_now), ('g', g_apply)]
+        for r in range(D_repeats):
+            d_gr, d_red = d_ar.overlapped(d_grads, (tag, 'D', r))
+            raw += [('g', d_gr), ('e', d_red), ('g', d_apply)]
+        g_gr, g_red = g_ar.overlapped(g_grads, (tag, 'G'))
+        raw += [('g', g_gr), ('e', g_red), ('g', g_apply)]
         segs = []
         for kind, fn in raw:
             if segs and kind == 'g' and segs[-1][0] == 'g':

@@ -5,8 +5,10 @@ and PyBiLstm.py:19-274 (Embedding -> Dropout -> BiLSTM -> Linear; knobs :24-32).
 
 Task I/O (tasks.rst): a query is a list of tokens, a prediction is a list of integer tags.
 Differences: Viterbi runs vectorised in numpy log-space; the BiLSTM applies cross-entropy to
-logits (the reference applies it to softmax outputs, bug (k)), batches sentences bucketed by
-length, and runs on the trial's device (PyTorch-ROCm LSTM on GPU).
+logits (the reference applies it to softmax outputs, bug (k)) and batches sentences bucketed by
+length.  On a GPU the BiLSTM's training step and prediction run on the native tagger engine
+(engine/tagger.py: in-tree kernels only, one hipGraph per bucket shape, any knob value); on the CPU
+the same network runs as torch modules.
 """
 import math
 
@@ -131,6 +133,7 @@ class PyBiLstm(BaseModel):
         super().__init__(**knobs)
         self._knobs = knobs
         self._net = None
+        self._engine = None
         self._word_dict = {}
         self._tag_count = 0
         self.device = trial_context().device
@@ -167,8 +170,8 @@ class PyBiLstm(BaseModel):
     def _encode(self, sents_tokens):
         return [[self._word_dict.get(w, 1) for w in s] for s in sents_tokens]
 
-    def _batches(self, ids, tags, bs, shuffle, rng):
-        import torch
+    @staticmethod
+    def _batches_np(ids, tags, bs, shuffle, rng):
         order = np.argsort([len(s) for s in ids], kind='stable')  # bucket by length
         chunks = [order[i:i + bs] for i in range(0, len(order), bs)]
         if shuffle:
@@ -181,7 +184,17 @@ class PyBiLstm(BaseModel):
                 x[r, :len(ids[i])] = ids[i]
                 if tags is not None:
                     y[r, :len(tags[i])] = tags[i]
+            yield ch, x, y
+
+    def _batches(self, ids, tags, bs, shuffle, rng):
+        import torch
+        for ch, x, y in self._batches_np(ids, tags, bs, shuffle, rng):
             yield ch, torch.from_numpy(x).to(self.device), torch.from_numpy(y).to(self.device)
+
+    def _native(self) -> bool:
+        """The native engine runs the GPU step for every knob value of the search space (hidden <= 128)."""
+        return (self.device.type == 'cuda' and int(self._knobs.get('word_rnn_hidden_size', 64)) <= 128
+                and (self._knobs.get('dtype') or default_dtype()) != 'bf16')
 
     def train(self, dataset_uri):
         import torch
@@ -194,15 +207,17 @@ class PyBiLstm(BaseModel):
                 self._word_dict.setdefault(tok[0], len(self._word_dict) + 2)
         self._tag_count = ds.tag_num_classes[0]
         self._net = self._create()
-        opt = torch.optim.Adam(self._net.parameters(), lr=float(self._knobs.get('learning_rate', 0.05)))
         ids = self._encode([[t[0] for t in s] for s in sents])
         tags = [[t[1] for t in s] for s in sents]
         rng = np.random.default_rng(0)
         logger.define_loss_plot()
         epochs = int(self._knobs.get('epochs', 10))
         ck = trial_context().checkpoint
-        start = 0
         saved = ck.load() if ck is not None else None
+        if self._native():
+            return self._train_native(ids, tags, rng, epochs, ck, saved)
+        opt = torch.optim.Adam(self._net.parameters(), lr=float(self._knobs.get('learning_rate', 0.05)))
+        start = 0
         if saved is not None:
             self._restore_ckpt(saved['state'], opt, rng)
             start = int(saved['epoch']) + 1
@@ -223,6 +238,40 @@ class PyBiLstm(BaseModel):
             if ck is not None and ck.due(ep) and ep + 1 < epochs:
                 ck.save(self._ckpt_state(opt, rng), ep)
             faults.maybe_fail('crash', epoch=ep, rank=0)
+
+    def _train_native(self, ids, tags, rng, epochs, ck, saved):
+        """The GPU training loop on the native engine: Adam over the padded arena, dropout from the
+        engine's Philox stream (seeded from the trial's numpy generator), one graph per bucket shape."""
+        from rafiki_amd.engine.tagger import TaggerEngine
+        eng = TaggerEngine(self._net, float(self._knobs.get('learning_rate', 0.05)),
+                           float(self._knobs.get('word_dropout', 0.1)), seed=int(rng.integers(1 << 62)))
+        start = 0
+        if saved is not None:
+            st = saved['state']
+            if 'engine' in st:
+                eng.load_state(st['engine'])
+            else:   # a checkpoint of the torch path: weights carry over, Adam restarts
+                self._net.load_state_dict(st['net'])
+                eng.load_module(self._net)
+            rng.bit_generator.state = st['np_rng']
+            start = int(saved['epoch']) + 1
+            logger.log('resumed from checkpoint after epoch {}'.format(saved['epoch']))
+        bs = int(self._knobs.get('batch_size', 32))
+        eng.take_loss()
+        for ep in range(start, epochs):
+            n = 0
+            for _, x, y in self._batches_np(ids, tags, bs, True, rng):
+                eng.step(x, y)
+                n += 1
+            logger.log_loss(loss=eng.take_loss() / max(1, n), epoch=ep)   # one host sync per epoch
+            if ck is not None and ck.due(ep) and ep + 1 < epochs:
+                eng.store_module(self._net)
+                ck.save({'engine': eng.state(), 'np_rng': rng.bit_generator.state,
+                         'net': _to_cpu(self._net.state_dict())}, ep)
+            faults.maybe_fail('crash', epoch=ep, rank=0)
+        eng.store_module(self._net)
+        eng.close()   # the step graphs are done; the engine stays for predict
+        self._engine = eng
 
     # ----------------------------------------------------------------- checkpoint / resume
     def _ckpt_state(self, opt, rng):
@@ -249,9 +298,19 @@ class PyBiLstm(BaseModel):
         self._net.eval()
         ids = self._encode(sents_tokens)
         out = [None] * len(ids)
+        eng = None
+        if self._native():
+            from rafiki_amd.engine.tagger import TaggerEngine
+            eng = getattr(self, '_engine', None)
+            if eng is None:
+                eng = self._engine = TaggerEngine(self._net, 0.0, 0.0)
         with torch.no_grad():
-            for ch, x, _ in self._batches(ids, None, 256, False, None):
-                pred = self._net(x).argmax(-1).cpu().numpy()
+            for ch, x, _ in self._batches_np(ids, None, 256, False, None):
+                if eng is not None:
+                    logits = eng.logits(x)
+                else:
+                    logits = self._net(torch.from_numpy(x).to(self.device))
+                pred = logits.argmax(-1).cpu().numpy()
                 for r, i in enumerate(ch):
                     out[i] = [int(t) for t in pred[r, :len(ids[i])]]
         return out
@@ -273,3 +332,4 @@ class PyBiLstm(BaseModel):
         self._tag_count = params['tag_count']
         self._net = self._create()
         self._net.load_state_dict(params['net_state_dict'])
+        self._engine = None

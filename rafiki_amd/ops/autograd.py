@@ -192,6 +192,13 @@ def _wt(kind, w, fn):
     return get
 
 
+# Observer of in-place gradient writes: GRAD_WATCH[0](leaf) is called right before a backward enqueues a
+# contribution into a leaf's persistent .grad buffer (parallel/grad_bucket.py places each bucket's
+# all-reduce event after the bucket's last contribution).  Process-global: the backward of a CUDA graph
+# runs on autograd's device thread.
+GRAD_WATCH = [None]
+
+
 def _param_grad_buffer(w):
     """The persistent fp32 gradient buffer of a parameter (the leaf's .grad, or the viewed leaf's, in
     the parameter's shape), for a leaf marked by ``accumulate_weight_grads_in_place`` and outside a
@@ -207,6 +214,9 @@ def _param_grad_buffer(w):
     # a reinterpreting view only (reshape of the whole contiguous leaf), never a transpose
     if not (w.is_contiguous() and leaf.is_contiguous() and w.data_ptr() == leaf.data_ptr()):
         return None
+    watch = GRAD_WATCH[0]
+    if watch is not None:
+        watch(leaf)
     return g.view(w.shape)
 
 

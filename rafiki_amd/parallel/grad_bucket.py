@@ -13,7 +13,16 @@ all-reduces over contiguous slices of the FlatParams gradient buffer:
   stream, overlapping the rest of the backward;
 * ``finish()`` launches whatever did not fire (parameters outside the active graph, e.g. PG-GAN
   blocks above the current level of detail, still hold zeros and must be reduced to keep the
-  replicas identical) and waits, then applies the 1/world mean (pg_gans.py:1175-1179).
+  replicas identical) and waits, then applies the 1/world mean (pg_gans.py:1175-1179);
+* ``overlapped(grads_fn, tag)`` is the form for CAPTURED data-parallel rounds (GraphedRounds'
+  segments): while the gradient segment is traced / captured, every gradient contribution is
+  observed (ops.autograd.GRAD_WATCH for the in-place weight-gradient writes, the post-accumulate
+  hooks for autograd's), which gives each bucket's last contribution.  Inside the capture an
+  external event is recorded right after it, so a replay fires one event per bucket as the backward
+  passes it; the eager reduce segment then issues each bucket's all-reduce from a side stream that
+  waits on that bucket's event only — RCCL reduces bucket b while the replay still computes the
+  earlier layers' gradients.  Buckets that received no contribution (PG-GAN blocks above the current
+  level of detail: zero on every rank, so their sum is zero) are not reduced at all.
 
 Gradients are summed in fp32 (they live in fp32 in the arena), so the reduction is exact up to
 fp32 association order — identical across ranks, which keeps the replicated Adam states in sync.
@@ -24,6 +33,8 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+
+from ..ops import autograd as _ag
 
 
 class FlatGradAllReduce:
@@ -81,13 +92,20 @@ class FlatGradAllReduce:
         self._launched = [False] * len(self.buckets)
         self._works = []
         self._hooks = []
+        self._idx = {id(p): i for i, p in enumerate(params)}
+        self._note = None        # the gradient-contribution observer of a traced segment (overlapped())
+        self._plans = {}
+        self._side = None
         if self.overlap:
             for i, p in enumerate(params):
                 if p.requires_grad:
                     self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
 
     def _make_hook(self, i):
-        def hook(_p):
+        def hook(p):
+            note = self._note
+            if note is not None:
+                note(p)
             if not self.active:
                 return
             b = self.bucket_of[i]
@@ -131,6 +149,86 @@ class FlatGradAllReduce:
             return
         works = [dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                  for a, e in self.buckets]
+        for w in works:
+            w.wait()
+
+    # ------------------------------------------------------------ overlapped reduce of a captured segment
+    def overlapped(self, grads_fn, tag):
+        """(grads, reduce) callables for a data-parallel round's segments: ``grads`` runs ``grads_fn``
+        watching where its gradient contributions land (and, while a graph is being captured, records
+        one external event per bucket after its last contribution); ``reduce`` all-reduces (sum) the
+        buckets that received any contribution — each from a side stream waiting on its own event when
+        the segment was captured, so the reductions overlap the replay's remaining backward — and makes
+        the current stream wait for them.  ``tag`` names the segment across rounds (its graph key and
+        position): the captured events belong to that graph."""
+        plan = self._plans.get(tag)
+        if plan is None:
+            plan = self._plans[tag] = {'last': None, 'events': None}
+        return (lambda: self._watched(plan, grads_fn)), (lambda: self._reduce_plan(plan))
+
+    def clear_plans(self):
+        self._plans.clear()
+
+    def _watched(self, plan, fn):
+        capturing = self.grad.is_cuda and torch.cuda.is_current_stream_capturing()
+        last = plan['last']
+        order = sorted(last, key=last.get) if (capturing and last) else []
+        seq, events, k = [], {}, [0]
+
+        def close_before(pos):
+            while k[0] < len(order) and last[order[k[0]]] < pos:
+                ev = torch.cuda.Event(external=True)
+                ev.record()
+                events[order[k[0]]] = ev
+                k[0] += 1
+
+        def note(leaf):
+            i = self._idx.get(id(leaf))
+            if i is None:
+                return
+            if order:
+                close_before(len(seq))
+            seq.append(self.bucket_of[i])
+
+        prev = _ag.GRAD_WATCH[0]
+        _ag.GRAD_WATCH[0] = note
+        self._note = note
+        try:
+            fn()
+        finally:
+            _ag.GRAD_WATCH[0] = prev
+            self._note = None
+        if order:
+            close_before(1 << 62)
+        traced = {}
+        for pos, b in enumerate(seq):
+            traced[b] = pos
+        if capturing and last is not None and traced != last:
+            events = {}   # the captured segment differs from its trace: reduce after the segment instead
+        plan['last'] = traced
+        plan['events'] = events if (capturing and events) else None
+
+    def _reduce_plan(self, plan):
+        if self.world <= 1 and not self.force:
+            return
+        last = plan['last'] or {}
+        live = sorted(last, key=last.get)      # buckets in the order the backward completes them
+        events = plan['events']
+        works = []
+        if events is not None:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self.grad.device)
+            for b in live:
+                a, e = self.buckets[b]
+                self._side.wait_event(events[b])
+                with torch.cuda.stream(self._side):
+                    works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group,
+                                                 async_op=True))
+        else:
+            for b in live:
+                a, e = self.buckets[b]
+                works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group,
+                                             async_op=True))
         for w in works:
             w.wait()
 

@@ -73,7 +73,7 @@ def main():
         def step():
             if a.force_allreduce:
                 graphs.run_segments(lod, m.round_segments(lod, mb, level, labels, rng, G_opt, D_opt, acc,
-                                                          d_ar=d_ar, g_ar=g_ar))
+                                                          d_ar=d_ar, g_ar=g_ar, tag=lod))
             else:
                 graphs.run(lod, lambda: m.train_round(lod, mb, level, labels, rng, G_opt, D_opt, acc))
         for _ in range(max(2, a.warmup)):

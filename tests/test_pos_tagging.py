@@ -66,3 +66,21 @@ def test_pybilstm_crash_resume_matches_uninterrupted(tmp_path, monkeypatch):
     wa, wb = _weights(a), _weights(b)
     for k in wa:
         assert torch.equal(wa[k], wb[k]), k
+
+
+def test_tagger_pack_batch_layout():
+    """Host packing of a tagger batch (engine/tagger.py): time-major ids / labels, stable-sorted runs
+    with the padding id marked -1, and 1/#labelled tokens as float bits."""
+    import numpy as np
+    from rafiki_amd.engine.tagger import pack_batch
+    x = np.array([[3, 1, 0], [1, 3, 2]])
+    y = np.array([[5, 6, -100], [7, 8, 9]])
+    w = pack_batch(x, y)
+    n = 6
+    assert w[:n].tolist() == [3, 1, 1, 3, 0, 2]
+    assert w[n:2 * n].tolist() == [5, 7, 6, 8, -100, 9]
+    assert w[2 * n:3 * n].tolist() == [4, 1, 2, 5, 0, 3]
+    assert w[3 * n:3 * n + 4].tolist() == [-1, 1, 2, 3]
+    assert w[4 * n:4 * n + 5].tolist() == [0, 1, 3, 4, 6]
+    assert w[5 * n + 1] == 4
+    assert w[5 * n + 2:].view(np.float32)[0] == np.float32(0.2)
