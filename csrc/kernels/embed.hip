@@ -15,19 +15,22 @@ namespace {
 
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const long long* __restrict__ ids,
                                                             const float* __restrict__ w, float* __restrict__ out,
-                                                            int n, int E4) {
+                                                            int n, int E4, int V) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long long)n * E4) return;
   const int tok = (int)(i / E4), c = (int)(i - (long long)tok * E4);
-  ((f32x4*)out)[i] = ((const f32x4*)w)[ids[tok] * E4 + c];
+  long long id = ids[tok];
+  id = id < 0 || id >= V ? 0 : id;   // an out-of-range id reads row 0 (the padding row) instead of past W
+  ((f32x4*)out)[i] = ((const f32x4*)w)[id * E4 + c];
 }
 
 __global__ __launch_bounds__(256) void iota_kernel(int* __restrict__ v, const long long* __restrict__ ids,
-                                                   int* __restrict__ keys, int n) {
+                                                   int* __restrict__ keys, int n, int V) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   v[i] = i;
-  keys[i] = (int)ids[i];
+  const long long id = ids[i];
+  keys[i] = id < 0 || id >= V ? 0 : (int)id;   // as the forward: out-of-range ids are row 0
 }
 
 // zero every row no token touches: rows v with no entry in the sorted ids (binary search), padding row too
@@ -66,13 +69,13 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int* __restric
 
 }  // namespace
 
-// out [n][E] = W[ids] (E % 4 == 0)
-extern "C" int rk_embedding_fwd(const long long* ids, const float* w, float* out, int n, int E, void* stream) {
+// out [n][E] = W[ids] (E % 4 == 0, V rows of W)
+extern "C" int rk_embedding_fwd(const long long* ids, const float* w, float* out, int n, int E, int V, void* stream) {
   if (n <= 0) return RK_OK;
   if (E <= 0 || (E & 3)) return RK_EUNSUPPORTED;
   const long long t = (long long)n * (E / 4);
   hipLaunchKernelGGL(embedding_fwd_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ids,
-                     w, out, n, E / 4);
+                     w, out, n, E / 4, V);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -97,7 +100,7 @@ extern "C" int rk_embedding_bwd(const long long* ids, const float* dy, float* dw
   int* perm = skeys + n;
   void* tmp = (void*)(((uintptr_t)(perm + n) + 255) & ~(uintptr_t)255);
   size_t tmp_bytes = (size_t)(ws_bytes - ((char*)tmp - (char*)ws));
-  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, vals, ids, keys, n);
+  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, vals, ids, keys, n, V);
   RK_LAUNCH_CHECK();
   int bits = 1;
   while (bits < 31 && (1 << bits) < V) ++bits;

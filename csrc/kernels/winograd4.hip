@@ -567,7 +567,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   const int t_begin = split * p.tps;
   const int t_end = min(t_begin + p.tps, p.ntiles);
   const int nch = (t_end - t_begin + KC - 1) / KC;
-  const int tt = tid & 7, ch = tid >> 3;   // tile within the chunk, channel (+ NT/8 h) within the block
+  // (tile, channel) item of the thread: a wave covers 2 tiles x 32 consecutive channels, so every buffer
+  // load of dy / x moves two whole 128-B lines (lanes = 8 tiles x 8 channels touched 8 lines for 32 B
+  // each, 4x the cache-line traffic through the texture path for the same bytes).  The LDS stores stay
+  // at most 2-way bank-conflicted under the column swizzle (free for ds_write_b32).
+  static_assert(PY == 1 && PX == 1, "one dy patch and at most one x window per thread and chunk");
+  const int tt = (tid >> 5) & 7, ch = (tid & 31) + 32 * (tid >> 8);
   const __amdgpu_buffer_rsrc_t dyr = rsrc(p.dy, p.dybytes), xr = rsrc(p.x, p.xbytes);
 
   float gy[PY][16], raw[PX][36];

@@ -144,6 +144,17 @@ class FlatParams:
     def param_ranges(self):
         return [(s.offset, s.numel) for s in self.specs]
 
+    def ranges_of(self, names):
+        """Merged contiguous arena ranges [(a, b)] (aligned extents) of the named parameters."""
+        rs = sorted((self._by_name[n].offset, self._by_name[n].offset + _align(self._by_name[n].numel)) for n in names)
+        out = []
+        for a, b in rs:
+            if out and out[-1][1] == a:
+                out[-1] = (out[-1][0], b)
+            else:
+                out.append((a, b))
+        return out
+
     def num_params(self):
         return sum(s.numel for s in self.specs)
 
@@ -226,11 +237,17 @@ class FlatAdam:
         self.v.zero_()
         self.t.zero_()
 
-    def step(self):
+    def step(self, live=None):
+        """``live``: arena ranges [(a, b)] to update (None: the whole arena).  Only exact for ranges
+        left out whose gradient AND first moment are zero (an untouched parameter with beta1 = 0, or
+        one never touched since reset_state): Adam then leaves the weight unchanged."""
         f = self.flat
         # Equalized LR (pg_gans.py:1006-1013) is applied by re-parameterisation: the arena holds the
         # EFFECTIVE weights c*w, stepped with lr*c and eps*c — algebraically identical to Adam on w.
         segs = f.segments(self.wd)
+        if live is not None:
+            segs = [(max(a, c), min(b, d), wd, mult) for a, b, wd, mult in segs for c, d in live
+                    if min(b, d) > max(a, c)]
         if f.device.type == 'cuda':
             F.add_int_(self.t, 1)
             for a, b, wd, mult in segs:

@@ -196,6 +196,22 @@ class PgNetworks:
         w = P.w(name + '/weight')
         return A.dense(x, w, P.w(name + '/bias') if bias else None, wb=P.wb(name + '/weight'), lrelu=lrelu)
 
+    def live_names(self, lod):
+        """(G names, D names): the parameters the generator / discriminator use at ``lod`` (the layers
+        ``generator`` / ``discriminator`` below evaluate); the others get no gradient that round."""
+        cur = self.L - int(math.floor(lod))
+        frac = lod - math.floor(lod)
+        g = ['4x4/Dense', '4x4/Conv', 'ToRGB_lod%d' % (self.L - cur)]
+        d = ['FromRGB_lod%d' % (self.L - cur), '4x4/Conv', '4x4/Dense0', '4x4/Dense1']
+        for res in range(3, cur + 1):
+            tag = '%dx%d' % (2 ** res, 2 ** res)
+            g += [tag + '/Conv0_up', tag + '/Conv1']
+            d += [tag + '/Conv0', tag + '/Conv1_down']
+        if frac > 0 and cur > 2:
+            g.append('ToRGB_lod%d' % (self.L - cur + 1))
+            d.append('FromRGB_lod%d' % (self.L - cur + 1))
+        return ([n + s for n in g for s in ('/weight', '/bias')], [n + s for n in d for s in ('/weight', '/bias')])
+
     def generator(self, P, latents, labels, lod):
         """latents [N, latent] fp32, labels [N, label_size] -> images NHWC [N, r, r, cpad] (bf16 on GPU)
         at r = 2 ** (L - floor(lod)), in [-1, 1] drange (pg_gans.py:803-880, 'recursive' structure)."""
@@ -728,6 +744,9 @@ class PgGan(BaseModel):
             if np.floor(sched.lod) != np.floor(prev_lod) or np.ceil(sched.lod) != np.ceil(prev_lod):
                 G_opt.reset_state()
                 D_opt.reset_state()
+                _zero(nets.G.grad)   # ranges that leave the live set keep zero gradients
+                _zero(nets.D.grad)
+            self.set_lod_live(sched.lod)
             prev_lod = sched.lod
             G_opt.lr, D_opt.lr = sched.G_lrate, sched.D_lrate
             mb = sched.minibatch // self.world
@@ -793,13 +812,41 @@ class PgGan(BaseModel):
             self.nets.update_Gs(G_smoothing)
         self._g_step(lod, mb, labels_all, rng, G_opt, g_ar, acc=acc)
 
+    # -- live arena ranges: at a given LOD only the layers up to its resolution receive gradients (at the
+    # reference schedule's lod 3 a third of each arena).  Zeroing, the finite check and Adam then run over
+    # those ranges only; the others hold zero gradient (the whole arenas are zeroed at every LOD change)
+    # and zero Adam moments (reset_state at the same points), where Adam would leave the weights
+    # unchanged anyway — the trimmed round gives bit-identical weights (tests/test_pg_gan.py).
+    _live = None
+
+    def set_lod_live(self, lod):
+        if not bool(self._knobs.get('live_ranges', True)):
+            self._live = None
+            return
+        g, d = self.nets.live_names(lod)
+        self._live = {id(self.nets.G): self.nets.G.ranges_of(g), id(self.nets.D): self.nets.D.ranges_of(d)}
+
+    def _live_of(self, flat):
+        return None if self._live is None else self._live.get(id(flat))
+
+    def _zero_grad(self, flat):
+        live = self._live_of(flat)
+        if live is None:
+            _zero(flat.grad)
+            return
+        for a, b in live:
+            _zero(flat.grad[a:b])
+
     def _finite_guard(self, flat, opt):
+        live = self._live_of(flat)
+        views = [flat.grad] if live is None else [flat.grad[a:b] for a, b in live]
         if self.device.type == 'cuda':
             from rafiki_amd.ops import functional as F
             F.zero_(opt.skip_flag)
-            F.nonfinite_flag(flat.grad, opt.skip_flag)
+            for v in views:
+                F.nonfinite_flag(v, opt.skip_flag)
         else:
-            opt.skip_flag.fill_(0 if bool(torch.isfinite(flat.grad).all()) else 1)
+            opt.skip_flag.fill_(0 if all(bool(torch.isfinite(v).all()) for v in views) else 1)
 
     def round_segments(self, lod, mb, level, labels_all, rng, G_opt, D_opt, acc, *, D_repeats=1, G_smoothing=0.99,
                        d_ar=None, g_ar=None, tag=None):
@@ -845,7 +892,7 @@ class PgGan(BaseModel):
 
     def _apply(self, flat, opt, rng):
         self._finite_guard(flat, opt)
-        opt.step()
+        opt.step(live=self._live_of(flat))
         rng.advance()
 
     def _fused_loss(self, grads=None):
@@ -893,7 +940,7 @@ class PgGan(BaseModel):
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.g_params, False)
         nets.set_requires_grad(nets.d_params, True)
-        _zero(nets.D.grad)
+        self._zero_grad(nets.D)
         idx = self._shard(rng.randint(level.shape[0], mb * self.world, TrialRng.D_IDX)).to(level.device)
         reals = self._reals(level, idx, lod - math.floor(lod))
         labels = labels_all.index_select(0, idx) if nets.label_size else torch.zeros((mb, 0), device=self.device)
@@ -962,7 +1009,7 @@ class PgGan(BaseModel):
         PG, PD = nets.src_G(), nets.src_D()
         nets.set_requires_grad(nets.d_params, False)
         nets.set_requires_grad(nets.g_params, True)
-        _zero(nets.G.grad)
+        self._zero_grad(nets.G)
         labels = self._rand_labels(labels_all, mb, rng)
         fakes = nets.generator(PG, self._latents(mb, rng, TrialRng.G_LAT), labels, lod)
         if self._fused_loss():

@@ -112,7 +112,7 @@ _SIGS = {
     "rk_mbstd_f32": [i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "rk_lrelu_pixelnorm_f32": [vp, vp, vp, i32, i32, f32, f32, vp, vp],
     # embedding gather / deterministic scatter-sum gradient (embed.hip)
-    "rk_embedding_fwd": [vp, vp, vp, i32, i32, vp],
+    "rk_embedding_fwd": [vp, vp, vp, i32, i32, i32, vp],
     "rk_embedding_bwd": [vp, vp, vp, i32, i32, i32, i32, vp, i64, vp],
     # native tagger step (tagger.hip): embedding + dropout, run-sum embedding gradient, W_hh^T, bias add
     "rk_tag_embed_fwd": [vp, vp, vp, vp, i32, i32, i32, f32, C.c_ulonglong, i32, vp, vp],

@@ -41,7 +41,7 @@ class EmbeddingFn(torch.autograd.Function):
         ids = ids.contiguous().to(torch.int64)
         n, (V, E) = ids.numel(), w.shape
         out = torch.empty(ids.shape + (E,), device=w.device, dtype=torch.float32)
-        _lib.call("rk_embedding_fwd", _p(ids), _p(w.contiguous()), _p(out), n, E, _s())
+        _lib.call("rk_embedding_fwd", _p(ids), _p(w.contiguous()), _p(out), n, E, V, _s())
         ctx.save_for_backward(ids)
         ctx.dims = (V, E, -1 if padding_idx is None else int(padding_idx))
         return out

@@ -69,6 +69,7 @@ def main():
         labels = torch.zeros((4096, 0), device=dev)
 
         graphs = GraphedRounds(not a.no_graph)
+        m.set_lod_live(lod)
 
         def step():
             if a.force_allreduce:

@@ -70,6 +70,7 @@ class _PgRound:
         self.rng = TrialRng(dev, 0)
         self.acc = torch.zeros(6, device=dev)
         self.lod = lod
+        self.m.set_lod_live(lod)
         r = 2 ** (5 - int(lod))
         self.mb = TrainingSchedule.MINIBATCH_DICTS[16].get(r, 16)
         self.level = torch.randint(0, 256, (4096, 1, r, r), dtype=torch.uint8, device=dev)

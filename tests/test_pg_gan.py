@@ -404,3 +404,37 @@ def test_flat_grad_allreduce_traces_and_skips_untouched_buckets():
 class _Done:
     def wait(self):
         return True
+
+
+def test_pg_gan_live_ranges_bit_identical():
+    """Zeroing, the finite check and Adam over the LOD's live arena ranges only (PgGan.set_lod_live) give
+    bit-identical G / D / Gs to the whole-arena round, through a 4x4 -> 8x8 fade and the stable 8x8 LOD."""
+    from rafiki_amd.models.pg_gan import PgGan
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    out = []
+    for live in (True, False):
+        with use_context(TrialContext(device=torch.device('cpu'))):
+            m = PgGan(**dict(EQUIV, live_ranges=live))
+            m.train(DATA)
+            out.append((m.nets.G.master.clone(), m.nets.D.master.clone(), m.nets.Gs_master.clone(), m._live))
+    (g1, d1, s1, l1), (g0, d0, s0, l0) = out
+    assert l1 is not None and l0 is None
+    assert torch.equal(g1, g0) and torch.equal(d1, d0) and torch.equal(s1, s0)
+
+
+def test_pg_gan_live_names_cover_the_lod():
+    from rafiki_amd.models.pg_gan import PgGan, load_gan_dataset
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    with use_context(TrialContext(device=torch.device('cpu'))):
+        m = PgGan(**EQUIV)
+        m._build(load_gan_dataset(DATA).shape, 0)
+    nets = m.nets
+    g3, d3 = nets.live_names(float(nets.L - 2))     # 4x4 only
+    gall, dall = nets.live_names(0.0)
+    assert set(g3) < set(nets.G.names()) and set(d3) < set(nets.D.names())
+    # the layers live at 4x4 stay live at full resolution, except the 4x4 RGB adapters
+    assert {n for n in g3 if 'RGB' not in n} <= set(gall) and {n for n in d3 if 'RGB' not in n} <= set(dall)
+    assert all(n in nets.G.names() for n in gall) and all(n in nets.D.names() for n in dall)
+    # at full resolution every conv / dense layer is live; only the coarser RGB adapters are not
+    assert all('RGB' in n for n in set(nets.G.names()) - set(gall))
+    assert all('RGB' in n for n in set(nets.D.names()) - set(dall))
