@@ -96,24 +96,28 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, bf16* _
   }
 }
 
+// omb1 / omb2: 1 - beta as computed on the host in double (torch's Adam adds (1 - beta) * g the same
+// way); forming 1 - b2 from the fp32 b2 here would cancel to 1.3e-5 relative error at b2 = 0.999
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* __restrict__ wb,
                                                    const float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, long long n, float lr, float b1, float b2,
-                                                   float eps, float wd, int decoupled, float c1, float c2,
-                                                   float gscale, const int* skip, const int* step_ptr) {
+                                                   float omb1, float omb2, float eps, float wd, int decoupled,
+                                                   float c1, float c2, float gscale, const int* skip,
+                                                   const int* step_ptr) {
   if (skip && skip[0] != 0) return;  // non-finite gradients: skip the update (pg_gans.py:1180-1191)
-  if (step_ptr) {  // device-side step counter: bias corrections survive hipGraph replay
-    const float t = (float)step_ptr[0];
-    c1 = 1.f / (1.f - __powf(b1, t));
-    c2 = 1.f / (1.f - __powf(b2, t));
+  if (step_ptr) {  // device-side step counter: bias corrections survive hipGraph replay (in double:
+                   // 1 - beta^t cancels at small t)
+    const int t = step_ptr[0];
+    c1 = omb1 < 1.f ? (float)(1.0 / (1.0 - pow(1.0 - (double)omb1, t))) : 1.f;
+    c2 = (float)(1.0 / (1.0 - pow(1.0 - (double)omb2, t)));
   }
   const long long n4 = n >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     f32x4 wv = ((const f32x4*)w)[i];
     f32x4 gv = ((const f32x4*)g)[i] * gscale;
     if (!decoupled) gv += wd * wv;
-    f32x4 mv = ((const f32x4*)m)[i] * b1 + (1.f - b1) * gv;
-    f32x4 vv = ((const f32x4*)v)[i] * b2 + (1.f - b2) * gv * gv;
+    f32x4 mv = ((const f32x4*)m)[i] * b1 + omb1 * gv;
+    f32x4 vv = ((const f32x4*)v)[i] * b2 + omb2 * gv * gv;
     ((f32x4*)m)[i] = mv;
     ((f32x4*)v)[i] = vv;
     f32x4 upd;
@@ -432,11 +436,11 @@ extern "C" int rk_sgd_step(float* w, void* wb, const float* g, float* mom, long 
 }
 
 extern "C" int rk_adam_step(float* w, void* wb, const float* g, float* m, float* v, long long n, float lr, float b1,
-                            float b2, float eps, float wd, int decoupled, float c1, float c2, float gscale,
-                            const int* skip, const int* step_ptr, void* stream) {
+                            float b2, float omb1, float omb2, float eps, float wd, int decoupled, float c1, float c2,
+                            float gscale, const int* skip, const int* step_ptr, void* stream) {
   if (n % 4) return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4, 4096)), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wb, g, m,
-                     v, n, lr, b1, b2, eps, wd, decoupled, c1, c2, gscale, skip, step_ptr);
+                     v, n, lr, b1, b2, omb1, omb2, eps, wd, decoupled, c1, c2, gscale, skip, step_ptr);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -214,7 +214,7 @@ class TaggerEngine:
         if update:
             b1, b2 = self.betas
             _lib.call("rk_adam_step", _p(self.w), None, _p(self.g), _p(self.m), _p(self.v), self.numel, self.lr, b1, b2,
-                      self.eps, 0.0, 0, 1.0, 1.0, 1.0, None, _p(self.ctr), s)
+                      1.0 - b1, 1.0 - b2, self.eps, 0.0, 0, 1.0, 1.0, 1.0, None, _p(self.ctr), s)
 
     def _upload(self, words: np.ndarray, key) -> torch.Tensor:
         """Async copy of a packed batch into the shape's device input buffer (pinned, double-buffered)."""

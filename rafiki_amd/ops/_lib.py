@@ -46,7 +46,7 @@ _SIGS = {
     "rk_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "rk_softmax_xent": [vp, i32, vp, i32, i32, i32, f32, vp, i32, vp, vp, vp, vp, vp],
     "rk_sgd_step": [vp, vp, vp, vp, i64, f32, f32, f32, i32, f32, vp, i64, vp, vp],
-    "rk_adam_step": [vp, vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, f32, f32, vp, vp, vp],
+    "rk_adam_step": [vp, vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, f32, i32, f32, f32, f32, vp, vp, vp],
     "rk_add_int": [vp, i32, vp],
     "rk_rows_reduce": [vp, i32, i64, i32, vp, vp],
     "rk_lerp": [vp, vp, vp, i64, f32, vp],

@@ -723,8 +723,8 @@ def adam_step(w, g, m, v, *, wb=None, lr, beta1=0.9, beta2=0.999, eps=1e-8, weig
     c1 = 1.0 / (1.0 - beta1 ** step) if beta1 > 0 else 1.0
     c2 = 1.0 / (1.0 - beta2 ** step)
     _lib.call("rk_adam_step", _p(w), _p(wb), _p(g), _p(m), _p(v), w.numel(), float(lr), float(beta1), float(beta2),
-              float(eps), float(weight_decay), int(decoupled), float(c1), float(c2), float(grad_scale),
-              _p(skip_flag), _p(step_tensor), _s())
+              1.0 - float(beta1), 1.0 - float(beta2), float(eps), float(weight_decay), int(decoupled), float(c1),
+              float(c2), float(grad_scale), _p(skip_flag), _p(step_tensor), _s())
 
 
 def add_int_(t, v=1):

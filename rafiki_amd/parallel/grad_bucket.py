@@ -35,6 +35,24 @@ import torch
 import torch.distributed as dist
 
 from ..ops import autograd as _ag
+from ..ops import graphs as _graphs
+
+
+_EV_OK = {}
+
+
+def _events_ok(device) -> bool:
+    """ops.graphs.external_events_ok, decided before the first capture (it runs a small graph of its
+    own, which cannot happen inside another capture)."""
+    return _EV_OK.get(device.index, False)
+
+
+def prepare_events(device):
+    """Run the external-event check for ``device`` (outside any capture); GraphedRounds calls it."""
+    if device.type == 'cuda' and device.index not in _EV_OK:
+        from ..ops.graphs import external_events_ok
+        _EV_OK[device.index] = external_events_ok(device)
+    return _EV_OK.get(device.index, False)
 
 
 class FlatGradAllReduce:
@@ -171,13 +189,15 @@ class FlatGradAllReduce:
 
     def _watched(self, plan, fn):
         capturing = self.grad.is_cuda and torch.cuda.is_current_stream_capturing()
+        if capturing and not _events_ok(self.grad.device):
+            capturing = False            # no per-bucket events: the reduce runs after the whole segment
         last = plan['last']
         order = sorted(last, key=last.get) if (capturing and last) else []
         seq, events, k = [], {}, [0]
 
         def close_before(pos):
             while k[0] < len(order) and last[order[k[0]]] < pos:
-                ev = torch.cuda.Event(external=True)
+                ev = _graphs.HipExternalEvent()
                 ev.record()
                 events[order[k[0]]] = ev
                 k[0] += 1
@@ -220,7 +240,7 @@ class FlatGradAllReduce:
                 self._side = torch.cuda.Stream(device=self.grad.device)
             for b in live:
                 a, e = self.buckets[b]
-                self._side.wait_event(events[b])
+                events[b].wait_on(self._side)
                 with torch.cuda.stream(self._side):
                     works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group,
                                                  async_op=True))

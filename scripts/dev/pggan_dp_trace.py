@@ -9,6 +9,8 @@ import os
 import socket
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
 os.environ.setdefault('RAFIKI_GRAD_BUCKET_MB', '2')
 
 import torch  # noqa: E402

@@ -6,7 +6,7 @@ cd /root/repo
 export TMPDIR=/tmp
 O=gpurun_out/r5m; mkdir -p $O
 fatal() { case $1 in 124|137|134|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
-timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_tagger_gpu.py tests/test_lstm_gpu.py tests/test_lstm_native_gpu.py tests/test_pg_gan_gpu.py -k "tagger or lstm or bilstm or embedding or dp_round" > $O/pytest_tagger.log 2>&1
+timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_graph_events_gpu.py tests/test_tagger_gpu.py tests/test_lstm_gpu.py tests/test_lstm_native_gpu.py tests/test_pg_gan_gpu.py -k "events or overlapped or tagger or lstm or bilstm or embedding or dp_round" > $O/pytest_tagger.log 2>&1
 rc=$?; echo "pytest tagger rc=$rc"; tail -25 $O/pytest_tagger.log; fatal $rc pytest_tagger
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_winograd4_gpu.py tests/test_f32_gpu.py > $O/pytest_wino.log 2>&1
 rc=$?; echo "pytest wino rc=$rc"; tail -3 $O/pytest_wino.log; fatal $rc pytest_wino
