@@ -337,7 +337,10 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
   const int t_begin = split * p.tps;
   const int t_end = min(t_begin + p.tps, p.ntiles);
   const int nch = (t_end - t_begin + WKC - 1) / WKC;
-  const int tt = tid & 7, ch = tid >> 3;   // tile within the chunk, channel within the block
+  // tile within the chunk, channel within the block: a wave covers 2 tiles x 32 consecutive channels, so
+  // each buffer load moves two whole 128-B lines (the F(4x4) weight gradient measured 1.19-1.29x from the
+  // same remap, profiles/wino4_wgrad_remap_r5.jsonl); LDS stores stay at most 2-way conflicted
+  const int tt = (tid >> 5) & 7, ch = (tid & 31) + 32 * (tid >> 8);
   const bool cok = co0 + ch < p.Co, iok = ci0 + ch < p.Ci;
   const __amdgpu_buffer_rsrc_t dyr = w_rsrc(p.dy, p.dybytes), xr = w_rsrc(p.x, p.xbytes);
 

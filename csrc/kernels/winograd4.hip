@@ -750,7 +750,7 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
   const int t_begin = split * p.tps;
   const int t_end = min(t_begin + p.tps, p.ntiles);
   const int nch = (t_end - t_begin + KC - 1) / KC;
-  const int tt = tid & 7, ch = tid >> 3;
+  const int tt = (tid >> 5) & 7, ch = tid & 31;   // a wave: 2 tiles x 32 channels (whole 128-B lines)
   const __amdgpu_buffer_rsrc_t dyr = rsrc(p.dy, p.dybytes), xr = rsrc(p.x, p.xbytes);
   const int co = co0 + ch, ci = ci0 + ch;
 

@@ -498,10 +498,6 @@ class GraphedRounds:
                 fn()
             return
         device_sync()
-        # per-bucket all-reduce events inside the captured gradient segments need the runtime's external
-        # graph events to order the side stream's reduce; checked once, before the first capture
-        from rafiki_amd.parallel.grad_bucket import prepare_events
-        prepare_events(torch.device('cuda', torch.cuda.current_device()))
         pool = torch.cuda.graph_pool_handle()
         gs = []
         for kind, fn in segs:

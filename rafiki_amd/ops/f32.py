@@ -699,7 +699,7 @@ def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     if nt >= (1 << 22) or 4 * Nb * H * W * max(Cin, Cout) >= 0x7fffffff:
         return []
     out = []
-    for v, bco in ((0, 32), (1, 64)):
+    for v, bco in ((0, 32), (1, 64)):   # 2 (software-pipelined) measured 1.2-1.3x slower, wino4_variants_r5
         if v == 1 and Cout < 64:
             continue
         base = cdiv(Cout, bco) * cdiv(Cin, 32)

@@ -62,115 +62,3 @@ def capture(graph: "torch.cuda.CUDAGraph", pool=None, stream=None):
                 gc.enable()
 
 
-
-_HIP = {}
-
-
-def _hip():
-    """The HIP runtime library this process already uses (the copy torch loaded, found in the process
-    map, so no second runtime instance is ever opened)."""
-    if 'lib' not in _HIP:
-        import ctypes
-        path = None
-        try:
-            with open('/proc/self/maps') as f:
-                for line in f:
-                    if 'libamdhip64.so' in line:
-                        path = line.split()[-1]
-                        break
-        except OSError:
-            pass
-        lib = ctypes.CDLL(path or 'libamdhip64.so')
-        vp, u32 = ctypes.c_void_p, ctypes.c_uint
-        lib.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), u32]
-        lib.hipEventRecordWithFlags.argtypes = [vp, vp, u32]
-        lib.hipStreamWaitEvent.argtypes = [vp, vp, u32]
-        lib.hipEventDestroy.argtypes = [vp]
-        for fn in (lib.hipEventCreateWithFlags, lib.hipEventRecordWithFlags, lib.hipStreamWaitEvent,
-                   lib.hipEventDestroy):
-            fn.restype = ctypes.c_int
-        _HIP['lib'] = lib
-    return _HIP['lib']
-
-
-class HipExternalEvent:
-    """A HIP event recorded with the external flag: inside a stream capture it becomes an event-record
-    node of the graph, so a stream outside the graph can wait on that point of every replay
-    (hipStreamWaitEvent after the replay is enqueued).  torch.cuda.Event(external=True) is refused on
-    ROCm builds of torch, so this calls the runtime directly; ``external_events_ok`` verifies the
-    ordering on the device before anything relies on it."""
-    DISABLE_TIMING, RECORD_EXTERNAL = 0x2, 0x1
-
-    def __init__(self):
-        import ctypes
-        self._h = ctypes.c_void_p()
-        rc = _hip().hipEventCreateWithFlags(ctypes.byref(self._h), self.DISABLE_TIMING)
-        if rc != 0:
-            raise RuntimeError('hipEventCreateWithFlags failed: {}'.format(rc))
-
-    def record(self, stream=None):
-        st = stream if stream is not None else torch.cuda.current_stream()
-        rc = _hip().hipEventRecordWithFlags(self._h, st.cuda_stream, self.RECORD_EXTERNAL)
-        if rc != 0:
-            raise RuntimeError('hipEventRecordWithFlags(external) failed: {}'.format(rc))
-
-    def wait_on(self, stream):
-        rc = _hip().hipStreamWaitEvent(stream.cuda_stream, self._h, 0)
-        if rc != 0:
-            raise RuntimeError('hipStreamWaitEvent failed: {}'.format(rc))
-
-    def __del__(self):
-        h = getattr(self, '_h', None)
-        if h is not None and h.value:
-            try:
-                _hip().hipEventDestroy(h)
-            except Exception:
-                pass
-
-
-_EXT_EVENTS = {}
-
-
-def external_events_ok(device=None) -> bool:
-    """Whether an external event recorded inside a captured graph orders work that another stream
-    issues after the replay (``side.wait_event(ev)``) behind the graph's work before the event — what
-    FlatGradAllReduce.overlapped relies on.  Checked once per process and device with a sentinel: the
-    graph copies a 64 MiB source (refilled with a new value before every replay) and records the
-    event; a side stream waiting on it must read the new value, every time.  False (the reduce then
-    runs after the whole segment) if the runtime lacks the feature or the check fails."""
-    dev = torch.device('cuda', torch.cuda.current_device()) if device is None else torch.device(device)
-    key = dev.index
-    if key in _EXT_EVENTS:
-        return _EXT_EVENTS[key]
-    ok = False
-    try:
-        with LOCK:
-            n = 16 << 20
-            src = torch.zeros(n, device=dev)
-            dst = torch.zeros(n, device=dev)
-            tail = torch.zeros(n, device=dev)
-            seen = torch.zeros(8, device=dev)
-            ev = HipExternalEvent()
-            side = torch.cuda.Stream(device=dev)
-            g = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize(dev)
-            with capture(g):
-                dst.copy_(src)
-                ev.record()
-                tail.copy_(dst)          # more graph work after the event
-                tail.copy_(src)
-            ok = True
-            for k in range(1, 9):
-                src.fill_(float(k))
-                g.replay()
-                ev.wait_on(side)
-                with torch.cuda.stream(side):
-                    seen[k - 1:k].copy_(dst[n - 1:n])
-                torch.cuda.current_stream(dev).wait_stream(side)
-            torch.cuda.synchronize(dev)
-            ok = bool((seen == torch.arange(1, 9, device=dev, dtype=seen.dtype)).all())
-            del g
-    except Exception:
-        ok = False
-    _EXT_EVENTS[key] = ok
-    return ok

@@ -15,17 +15,17 @@ all-reduces over contiguous slices of the FlatParams gradient buffer:
   blocks above the current level of detail, still hold zeros and must be reduced to keep the
   replicas identical) and waits, then applies the 1/world mean (pg_gans.py:1175-1179);
 * ``overlapped(grads_fn, tag)`` is the form for CAPTURED data-parallel rounds (GraphedRounds'
-  segments): while the gradient segment is traced / captured, every gradient contribution is
-  observed (ops.autograd.GRAD_WATCH for the in-place weight-gradient writes, the post-accumulate
-  hooks for autograd's), which gives each bucket's last contribution.  Inside the capture an
-  external event is recorded right after it, so a replay fires one event per bucket as the backward
-  passes it; the eager reduce segment then issues each bucket's all-reduce from a side stream that
-  waits on that bucket's event only — RCCL reduces bucket b while the replay still computes the
-  earlier layers' gradients.  Buckets that received no contribution (PG-GAN blocks above the current
-  level of detail: zero on every rank, so their sum is zero) are not reduced at all.
-
-Gradients are summed in fp32 (they live in fp32 in the arena), so the reduction is exact up to
-fp32 association order — identical across ranks, which keeps the replicated Adam states in sync.
+  segments): while the gradient segment runs (eagerly, the first time a round shape is seen) every
+  gradient contribution is observed (ops.autograd.GRAD_WATCH for the in-place weight-gradient
+  writes, the post-accumulate hooks for autograd's), and the reduce segment that follows the
+  segment's replays all-reduces only the buckets that received any — PG-GAN blocks above the
+  current level of detail hold zero gradient on every rank, so their sum is zero and they are not
+  reduced at all (two thirds of the arena at the reference schedule's 4x4 LOD).  Starting each
+  bucket's reduce while the replay still runs the earlier layers' backward would need an event
+  recorded inside the capture that a stream outside the graph can wait on; HIP refuses external
+  event records during stream capture (hipErrorInvalidValue, ROCm 7.2; torch refuses
+  Event(external=True) on ROCm), and an internal event does not order the other stream, so the
+  reduce runs between the replays.
 """
 from __future__ import annotations
 
@@ -35,24 +35,6 @@ import torch
 import torch.distributed as dist
 
 from ..ops import autograd as _ag
-from ..ops import graphs as _graphs
-
-
-_EV_OK = {}
-
-
-def _events_ok(device) -> bool:
-    """ops.graphs.external_events_ok, decided before the first capture (it runs a small graph of its
-    own, which cannot happen inside another capture)."""
-    return _EV_OK.get(device.index, False)
-
-
-def prepare_events(device):
-    """Run the external-event check for ``device`` (outside any capture); GraphedRounds calls it."""
-    if device.type == 'cuda' and device.index not in _EV_OK:
-        from ..ops.graphs import external_events_ok
-        _EV_OK[device.index] = external_events_ok(device)
-    return _EV_OK.get(device.index, False)
 
 
 class FlatGradAllReduce:
@@ -173,42 +155,25 @@ class FlatGradAllReduce:
     # ------------------------------------------------------------ overlapped reduce of a captured segment
     def overlapped(self, grads_fn, tag):
         """(grads, reduce) callables for a data-parallel round's segments: ``grads`` runs ``grads_fn``
-        watching where its gradient contributions land (and, while a graph is being captured, records
-        one external event per bucket after its last contribution); ``reduce`` all-reduces (sum) the
-        buckets that received any contribution — each from a side stream waiting on its own event when
-        the segment was captured, so the reductions overlap the replay's remaining backward — and makes
-        the current stream wait for them.  ``tag`` names the segment across rounds (its graph key and
-        position): the captured events belong to that graph."""
+        recording which buckets its gradient contributions land in; ``reduce`` all-reduces (sum) those
+        buckets, in the order the backward completed them, and makes the current stream wait for
+        them.  ``tag`` names the segment across rounds (its graph key and position): a replayed
+        segment keeps the buckets traced when it first ran."""
         plan = self._plans.get(tag)
         if plan is None:
-            plan = self._plans[tag] = {'last': None, 'events': None}
+            plan = self._plans[tag] = {'last': None}
         return (lambda: self._watched(plan, grads_fn)), (lambda: self._reduce_plan(plan))
 
     def clear_plans(self):
         self._plans.clear()
 
     def _watched(self, plan, fn):
-        capturing = self.grad.is_cuda and torch.cuda.is_current_stream_capturing()
-        if capturing and not _events_ok(self.grad.device):
-            capturing = False            # no per-bucket events: the reduce runs after the whole segment
-        last = plan['last']
-        order = sorted(last, key=last.get) if (capturing and last) else []
-        seq, events, k = [], {}, [0]
-
-        def close_before(pos):
-            while k[0] < len(order) and last[order[k[0]]] < pos:
-                ev = _graphs.HipExternalEvent()
-                ev.record()
-                events[order[k[0]]] = ev
-                k[0] += 1
+        seq = []
 
         def note(leaf):
             i = self._idx.get(id(leaf))
-            if i is None:
-                return
-            if order:
-                close_before(len(seq))
-            seq.append(self.bucket_of[i])
+            if i is not None:
+                seq.append(self.bucket_of[i])
 
         prev = _ag.GRAD_WATCH[0]
         _ag.GRAD_WATCH[0] = note
@@ -218,37 +183,20 @@ class FlatGradAllReduce:
         finally:
             _ag.GRAD_WATCH[0] = prev
             self._note = None
-        if order:
-            close_before(1 << 62)
         traced = {}
         for pos, b in enumerate(seq):
             traced[b] = pos
-        if capturing and last is not None and traced != last:
-            events = {}   # the captured segment differs from its trace: reduce after the segment instead
-        plan['last'] = traced
-        plan['events'] = events if (capturing and events) else None
+        if traced or plan['last'] is None:
+            plan['last'] = traced
 
     def _reduce_plan(self, plan):
         if self.world <= 1 and not self.force:
             return
         last = plan['last'] or {}
-        live = sorted(last, key=last.get)      # buckets in the order the backward completes them
-        events = plan['events']
         works = []
-        if events is not None:
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=self.grad.device)
-            for b in live:
-                a, e = self.buckets[b]
-                events[b].wait_on(self._side)
-                with torch.cuda.stream(self._side):
-                    works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group,
-                                                 async_op=True))
-        else:
-            for b in live:
-                a, e = self.buckets[b]
-                works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group,
-                                             async_op=True))
+        for b in sorted(last, key=last.get):   # buckets in the order the backward completed them
+            a, e = self.buckets[b]
+            works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         for w in works:
             w.wait()
 

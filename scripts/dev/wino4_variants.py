@@ -37,7 +37,7 @@ for (N, H, Ci, Co) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128
         r['v%d_diff' % v] = float((y - ref).abs().max())
     print(json.dumps(r), flush=True)
 
-# weight gradient: variants 0 (32x32), 1 (64x32), best split each
+# weight gradient: variants 0 (32x32), 1 (64x32), 2 (32x32 software-pipelined), best split each
 for (N, H, Ci, Co) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128), (256, 8, 128, 256),
                        (256, 32, 8, 64)]:
     x = torch.randn(N, H, H, Ci, device='cuda')
@@ -47,7 +47,7 @@ for (N, H, Ci, Co) in [(256, 32, 64, 64), (256, 16, 64, 128), (256, 16, 128, 128
     S.wino4_wgrad(dy, x, ref, splits=1, variant=0)
     r = dict(kind='wgrad', N=N, H=H, Ci=Ci, Co=Co)
     cands = S._wino4_wgrad_cands(N, H, H, Co, Ci)
-    for v in (0, 1):
+    for v in (0, 1, 2):
         ts = {}
         for c in cands:
             if c[1] != v:
