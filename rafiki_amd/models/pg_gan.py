@@ -18,7 +18,8 @@ predict contract ([grid_w, grid_h, n_images] -> JPEG file paths).  Re-designed f
 * equalized learning rate by re-parameterisation (arena holds c*w, Adam steps with lr*c, eps*c);
 * data parallel (``DATA_PARALLEL = True``): when the worker group has N ranks the trial's minibatch
   is split across them (pg_gans.py:290-293) and gradients are averaged by bucketed RCCL
-  all-reduces over the flat gradient arena, overlapped with backward
+  all-reduces over the flat gradient arena (launched from backward hooks in eager rounds, after the
+  captured gradient segment in graphed rounds, untouched buckets skipped)
   (``parallel.grad_bucket``; replaces the per-variable NCCL all-sum at pg_gans.py:1164-1171);
 * every rank draws the GLOBAL minibatch's indices / latents / mixing factors from one shared Philox
   stream and keeps its strided shard (the columns of the [group, N/group] minibatch-stddev layout),
@@ -853,10 +854,9 @@ class PgGan(BaseModel):
         """train_round as segments for GraphedRounds.run_segments: per D step gradients ('g'), the
         bucketed all-reduce of D.grad ('e'), then mean + finite guard + Adam + Gs EMA ('g'); likewise
         the G step.  Adjacent compute segments are merged (D_repeats + 2 graphs per round).  The
-        all-reduce segments come from FlatGradAllReduce.overlapped: in a replayed round each bucket's
-        all-reduce starts as soon as the captured backward has written its last gradient (external
-        event per bucket), and buckets no contribution reached (blocks above the current LOD) are
-        skipped."""
+        all-reduce segments come from FlatGradAllReduce.traced: each reduces only the buckets the
+        segment's backward wrote (untouched blocks above the current LOD are skipped exactly).
+        """
         nets = self.nets
 
         def d_grads():
@@ -877,9 +877,9 @@ class PgGan(BaseModel):
 
         raw = []
         for r in range(D_repeats):
-            d_gr, d_red = d_ar.overlapped(d_grads, (tag, 'D', r))
+            d_gr, d_red = d_ar.traced(d_grads, (tag, 'D', r))
             raw += [('g', d_gr), ('e', d_red), ('g', d_apply)]
-        g_gr, g_red = g_ar.overlapped(g_grads, (tag, 'G'))
+        g_gr, g_red = g_ar.traced(g_grads, (tag, 'G'))
         raw += [('g', g_gr), ('e', g_red), ('g', g_apply)]
         segs = []
         for kind, fn in raw:

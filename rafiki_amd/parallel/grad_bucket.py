@@ -1,4 +1,4 @@
-"""Bucketed, backward-overlapped gradient all-reduce over a flat fp32 gradient arena.
+"""Bucketed gradient all-reduce over a flat fp32 gradient arena (overlapped with an eager backward).
 
 Replaces the reference's per-variable ``tf.contrib.nccl.all_sum`` (pg_gans.py:1164-1171: ~25 calls
 per network per step, several of them on tiny bias tensors) with a handful of large RCCL
@@ -14,7 +14,7 @@ all-reduces over contiguous slices of the FlatParams gradient buffer:
 * ``finish()`` launches whatever did not fire (parameters outside the active graph, e.g. PG-GAN
   blocks above the current level of detail, still hold zeros and must be reduced to keep the
   replicas identical) and waits, then applies the 1/world mean (pg_gans.py:1175-1179);
-* ``overlapped(grads_fn, tag)`` is the form for CAPTURED data-parallel rounds (GraphedRounds'
+* ``traced(grads_fn, tag)`` is the form for CAPTURED data-parallel rounds (GraphedRounds'
   segments): while the gradient segment runs (eagerly, the first time a round shape is seen) every
   gradient contribution is observed (ops.autograd.GRAD_WATCH for the in-place weight-gradient
   writes, the post-accumulate hooks for autograd's), and the reduce segment that follows the
@@ -93,7 +93,7 @@ class FlatGradAllReduce:
         self._works = []
         self._hooks = []
         self._idx = {id(p): i for i, p in enumerate(params)}
-        self._note = None        # the gradient-contribution observer of a traced segment (overlapped())
+        self._note = None        # the gradient-contribution observer of a traced segment (traced())
         self._plans = {}
         self._side = None
         if self.overlap:
@@ -152,8 +152,8 @@ class FlatGradAllReduce:
         for w in works:
             w.wait()
 
-    # ------------------------------------------------------------ overlapped reduce of a captured segment
-    def overlapped(self, grads_fn, tag):
+    # ------------------------------------------------------------ traced reduce of a captured segment
+    def traced(self, grads_fn, tag):
         """(grads, reduce) callables for a data-parallel round's segments: ``grads`` runs ``grads_fn``
         recording which buckets its gradient contributions land in; ``reduce`` all-reduces (sum) those
         buckets, in the order the backward completed them, and makes the current stream wait for

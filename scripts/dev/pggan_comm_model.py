@@ -1,7 +1,7 @@
 """Communication model of the data-parallel PG-GAN round (docs/architecture.md): parameter bytes of G
 and D at the reference configuration (fmap_base 8192, fmap_max 512, latent 512, 32x32x1), their
 all-reduce buckets, and which buckets a round at lod 3 (4x4) / lod 0 (32x32) actually touches —
-traced on the CPU through FlatGradAllReduce.overlapped — then the ring all-reduce time per round at
+traced on the CPU through FlatGradAllReduce.traced — then the ring all-reduce time per round at
 N = 2, 4, 8 over xGMI."""
 import json
 import os

@@ -1,4 +1,4 @@
-"""One-GPU rehearsal of the overlapped data-parallel PG-GAN round for a kernel trace.
+"""One-GPU rehearsal of the segmented data-parallel PG-GAN round for a kernel trace.
 
 A 1-rank RCCL group with the bucketed all-reduce forced on (force_grad_allreduce), small buckets
 (RAFIKI_GRAD_BUCKET_MB, default here 2 MiB) so the D / G arenas split into several buckets: the

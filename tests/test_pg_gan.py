@@ -354,8 +354,8 @@ def _dp_seg_worker(rank, world, port, out_dir):
     D.destroy(info)
 
 
-def test_pg_gan_dp_overlapped_segments_match_unsegmented_gloo():
-    """2 ranks: the segmented round (bucket all-reduces from FlatGradAllReduce.overlapped — traced
+def test_pg_gan_dp_traced_segments_match_unsegmented_gloo():
+    """2 ranks: the segmented round (bucket all-reduces from FlatGradAllReduce.traced — traced
     gradient contributions, untouched buckets skipped) gives bit-identical weights to the unsegmented
     round (hook-launched buckets over the whole arena), through a LOD fade."""
     port = _free_port()
@@ -369,7 +369,7 @@ def test_pg_gan_dp_overlapped_segments_match_unsegmented_gloo():
 
 
 def test_flat_grad_allreduce_traces_and_skips_untouched_buckets():
-    """overlapped(): the trace records each bucket's last contribution; buckets with none are never
+    """traced(): the trace records each bucket's last contribution; buckets with none are never
     reduced (their gradients are zero on every rank)."""
     from rafiki_amd.engine.flat import FlatParams, init_const
     from rafiki_amd.parallel.grad_bucket import FlatGradAllReduce
@@ -388,7 +388,7 @@ def test_flat_grad_allreduce_traces_and_skips_untouched_buckets():
     orig = dist.all_reduce
     dist.all_reduce = lambda t, **kw: calls.append(t.data_ptr()) or _Done()
     try:
-        gr, red = ar.overlapped(lambda: sum((p * (i + 1)).sum() for i, p in enumerate(params[:2])).backward(),
+        gr, red = ar.traced(lambda: sum((p * (i + 1)).sum() for i, p in enumerate(params[:2])).backward(),
                                 ('k', 0))
         gr()
         red()
