@@ -177,11 +177,15 @@ def test_grads_match_reference_non_pow2_vgg16_layout():
         assert fro < 0.2 and cos > 0.98, (n, fro, cos)
 
 
-def test_vgg16_model_trains():
+@pytest.mark.parametrize("bn", [False, True])
+def test_vgg16_model_trains(bn):
+    """Vgg16 trains end to end: the default Keras-VGG16 network (conv + bias + ReLU, no BatchNorm, fp32)
+    at Adam 1e-4 — plain 16-layer VGG from scratch needs the smaller step Keras users give it — and the
+    batch_norm knob's conv + BN + ReLU blocks at 1e-3."""
     import numpy as np
     from rafiki_amd.models.vgg16 import Vgg16
-    m = Vgg16(epochs=1, learning_rate=1e-3, batch_size=32, dtype='bf16')
-    m._knobs['epochs'] = 6
+    m = Vgg16(epochs=1, learning_rate=1e-3 if bn else 1e-4, batch_size=32, batch_norm=bn)
+    m._knobs['epochs'] = 6 if bn else 10
     m.train('synthetic://image?n=512&size=28&channels=1&classes=4&seed=0')
     acc = m.evaluate('synthetic://image?n=256&size=28&channels=1&classes=4&seed=1')
     assert acc > 0.5, acc
