@@ -137,7 +137,8 @@ def test_tagger_graph_replay_matches_eager():
     torch.cuda.synchronize()
     assert len(a._graphs) == 3
     assert torch.equal(a.w, b.w) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
-    assert a.take_loss() == b.take_loss()
+    la, lb = a.take_loss(), b.take_loss()   # summed with float atomics: order-dependent in the last bits
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
     a.close()
 
 
