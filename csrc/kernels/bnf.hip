@@ -26,7 +26,8 @@ RK_DEV float act_d(float z, int act, float slope) {
 // y = conv output (pre-BN) [Nb,H,W,C]; out = pool?(act(y*scale+shift)).  Train mode: the batch
 // statistics come from `slots`; block 0 writes coeffs [4][C] = mean, rstd, scale, shift and updates the
 // running statistics (PyTorch semantics: unbiased variance in the running estimate).  Eval mode
-// (slots == null): scale/shift given.
+// (slots == null): scale/shift given.  out == null (train mode, no pool): finalize only, one block —
+// the next conv applies scale / shift + ReLU on its input loads (normalise-on-load, winograd4.hip).
 template <bool POOL>
 __global__ __launch_bounds__(256) void bnf_fwd_kernel(const float* __restrict__ y, const double* __restrict__ slots,
                                                       int SL, double count, const float* __restrict__ gamma,
@@ -68,6 +69,7 @@ __global__ __launch_bounds__(256) void bnf_fwd_kernel(const float* __restrict__ 
     s_sc[c] = sc;
     s_sh[c] = sh;
   }
+  if (!out) return;   // finalize only: the consumers apply scale / shift + ReLU while loading y
   __syncthreads();
   const int G = C >> 2;
   const int Ho = POOL ? H >> 1 : H, Wo = POOL ? W >> 1 : W;
@@ -460,9 +462,10 @@ extern "C" int rk_bnf_fwd(const float* y, const double* slots, int SL, double co
   if (C % 4 || C > BN_MAX_C || (pool && (H < 2 || W < 2))) return RK_EUNSUPPORTED;
   if (slots && (!gamma || !beta || !coeffs)) return RK_EBADARG;
   if (!slots && (!scale || !shift)) return RK_EBADARG;
+  if (!out && (!slots || pool)) return RK_EBADARG;   // out == null: train-mode finalize only (one block)
   const long long work = (long long)Nb * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   if ((long long)Nb * H * W * C >= (1ll << 31)) return RK_EUNSUPPORTED;   // 32-bit element offsets
-  const dim3 grid(grid_cap(work, 2048));
+  const dim3 grid(out ? grid_cap(work, 2048) : 1);
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = 2 * (size_t)C * sizeof(float);
   if (pool)

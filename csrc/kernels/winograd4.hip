@@ -54,6 +54,9 @@ struct W4Params {
   unsigned long long xbytes, ubytes, ybytes;
   int bpg;
   long long gx, gu, gy, gbias;
+  // normalise-on-load: the input is the pre-BN output y of the previous conv; scale [C] then shift [C] of its
+  // BatchNorm, applied with the ReLU to every in-image element as it is loaded (null: x is used as is)
+  const float* pro;
 };
 
 constexpr unsigned OOB = 0x80000000u;
@@ -132,7 +135,9 @@ RK_DEV void w4_tile(const W4Params& p, int t, int& n, int& oy, int& ox) { w_tile
 // input transform, LDS writes) over two LDS stages: the loaders fill chunk c+1 while the compute waves run
 // chunk c, one barrier per chunk; every SIMD holds one wave of each role, so the transform's VALU and the
 // loads issue beside the other wave's MFMAs instead of in a phase of their own (NS = 2, blocked weights)
-template <int MO, int WM, int WN, int MINW, int FL, int NS = 1, bool UB = false, bool WS = false>
+// PRO: normalise-on-load (p.pro = the producer's BN scale / shift; compile-time, so the kernels without it
+// keep their register allocation)
+template <int MO, int WM, int WN, int MINW, int FL, int NS = 1, bool UB = false, bool WS = false, bool PRO = false>
 __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_kernel(const W4Params p) {
   constexpr int A = MO + 2;                // window / transformed tile side
   constexpr int P = A * A;                 // Winograd positions
@@ -193,9 +198,14 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
   // UB: the block's weight chunks are consecutive 36-KiB images: chunk c of output block cb at
   // ((cb * nch + c) * UNITS) units of 16 B
   const int nchunk = p.C / KC;
-  auto load = [&](int c0, float (&raw)[IT][P], f32x2 (&ur)[ULR], f32x4 (&ub)[UBR]) {
+  auto load = [&](int c0, float (&raw)[IT][P], f32x2 (&ur)[ULR], f32x4 (&ub)[UBR], float (&pc)[2]) {
     // a chunk past Cin (the pipelined tail) reads zeros: empty buffer ranges
     const bool live = c0 < p.C;
+    if constexpr (PRO) {                   // this thread's input channel: BN scale / shift of the producer
+      const bool ok = live && c0 + lc < p.C;
+      pc[0] = ok ? p.pro[c0 + lc] : 0.f;
+      pc[1] = ok ? p.pro[p.C + c0 + lc] : 0.f;
+    }
     const __amdgpu_buffer_rsrc_t xr = rsrc(gxp + c0, live ? p.xbytes - 4ull * c0 : 0ull);
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
@@ -237,11 +247,22 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
                                                                              __builtin_amdgcn_readfirstlane(k * ustride), 0));
     }
   };
-  auto store = [&](int st, float (&raw)[IT][P], const f32x2 (&ur)[ULR], const f32x4 (&ub)[UBR]) {
+  auto store = [&](int st, float (&raw)[IT][P], const f32x2 (&ur)[ULR], const f32x4 (&ub)[UBR],
+                   const float (&pc)[2]) {
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
       const int row = lt + NT / 8 * h, c = lc ^ swz(row);
       float* const r = raw[h];
+      if constexpr (PRO) {                 // BN + ReLU of the producer on the in-image elements; padding stays 0
+        const unsigned rm = rmk[h], cm = cmk[h];
+#pragma unroll
+        for (int a = 0; a < A; ++a)
+#pragma unroll
+          for (int bb = 0; bb < A; ++bb) {
+            const bool in = (rm >> a) & (cm >> bb) & 1u;
+            r[a * A + bb] = in ? fmaxf(fmaf(r[a * A + bb], pc[0], pc[1]), 0.f) : 0.f;
+          }
+      }
 #pragma unroll
       for (int bb = 0; bb < A; ++bb) {     // B^T d along rows, in place
         float o[A];
@@ -277,14 +298,15 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
       float rL[IT][P];
       f32x2 uL[ULR];
       f32x4 bL[UBR];
-      load(0, rL, uL, bL);
-      store(0, rL, uL, bL);
-      if (nch > 1) load(KC, rL, uL, bL);
+      float pL[2];
+      load(0, rL, uL, bL, pL);
+      store(0, rL, uL, bL, pL);
+      if (nch > 1) load(KC, rL, uL, bL, pL);
       __syncthreads();
       for (int c = 0; c < nch; ++c) {
         if (c + 1 < nch) {
-          store((c + 1) & 1, rL, uL, bL);  // chunk c + 1 (its loads were issued one chunk ago)
-          if (c + 2 < nch) load((c + 2) * KC, rL, uL, bL);
+          store((c + 1) & 1, rL, uL, bL, pL);  // chunk c + 1 (its loads were issued one chunk ago)
+          if (c + 2 < nch) load((c + 2) * KC, rL, uL, bL, pL);
         }
         __syncthreads();
       }
@@ -342,21 +364,22 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
   float rA[IT][P];
   f32x2 uA[ULR];
   f32x4 bA[UBR];
+  float pA[2];
   if constexpr (WS) {
     for (int c = 0; c < nch; ++c) {        // compute waves: chunk c, then the barrier that publishes c + 1
       mfma(c & 1);
       __syncthreads();
     }
   } else if constexpr (NS == 1) {
-    load(0, rA, uA, bA);
-    store(0, rA, uA, bA);
+    load(0, rA, uA, bA, pA);
+    store(0, rA, uA, bA, pA);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-      if (c + 1 < nch) load((c + 1) * KC, rA, uA, bA);
+      if (c + 1 < nch) load((c + 1) * KC, rA, uA, bA, pA);
       mfma(0);
       if (c + 1 < nch) {
         __syncthreads();                   // every wave is done reading the stage
-        store(0, rA, uA, bA);
+        store(0, rA, uA, bA, pA);
       }
       __syncthreads();
     }
@@ -364,18 +387,19 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
     float rB[IT][P];
     f32x2 uB[ULR];
     f32x4 bB[UBR];
-    load(0, rA, uA, bA);
-    load(KC, rB, uB, bB);
-    store(0, rA, uA, bA);
+    float pB[2];
+    load(0, rA, uA, bA, pA);
+    load(KC, rB, uB, bB, pB);
+    store(0, rA, uA, bA, pA);
     __syncthreads();
     for (int c = 0; c < nch; c += 2) {
-      load((c + 2) * KC, rA, uA, bA);
+      load((c + 2) * KC, rA, uA, bA, pA);
       mfma(0);                             // chunk c
-      store(1, rB, uB, bB);                // chunk c + 1, in the MFMAs' shadow
+      store(1, rB, uB, bB, pB);            // chunk c + 1, in the MFMAs' shadow
       __syncthreads();
-      load((c + 3) * KC, rB, uB, bB);
+      load((c + 3) * KC, rB, uB, bB, pB);
       mfma(1);                             // chunk c + 1 (zeros past the end)
-      store(0, rA, uA, bA);                // chunk c + 2
+      store(0, rA, uA, bA, pA);            // chunk c + 2
       __syncthreads();
     }
   }
@@ -524,6 +548,7 @@ struct W4wParams {
   float invTW, invTHW;
   unsigned long long dybytes, xbytes;
   long long slab;       // floats per split
+  const float* xpro;    // normalise-on-load of x (BN scale [Ci], shift [Ci] + ReLU of its producer) or null
 };
 
 // A y of a 4-vector -> 6 values (the adjoint of A^T)
@@ -576,6 +601,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   const __amdgpu_buffer_rsrc_t dyr = rsrc(p.dy, p.dybytes), xr = rsrc(p.x, p.xbytes);
 
   float gy[PY][16], raw[PX][36];
+  unsigned xv[PX];                          // in-image rows (bits 0-5) / columns (bits 8-13) of each x window
+  float xpc[PX][2];                         // normalise-on-load coefficients of the thread's input channel
   auto load = [&](int c) {
     const int t = t_begin + c * KC + tt;
     const unsigned okm = t < t_end ? 1u : 0u;
@@ -608,6 +635,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
       const unsigned xm = okm & (ci < p.Ci ? 1u : 0u);
       const unsigned xb = (unsigned)((pix * p.Ci + ci) * 4);
       const unsigned cl = cm & 1u, cr = (cm >> 5) & 1u;
+      if (p.xpro) {
+        xv[h] = (xm ? (rm & 63u) : 0u) | ((cm & 63u) << 8);
+        xpc[h][0] = ci < p.Ci ? p.xpro[ci] : 0.f;
+        xpc[h][1] = ci < p.Ci ? p.xpro[p.Ci + ci] : 0.f;
+      }
 #pragma unroll
       for (int a = 0; a < 6; ++a) {        // row / edge-column vector offsets, column step in soffset
         const unsigned r = xb + (unsigned)((a - 1) * p.W * p.Ci * 4);
@@ -649,6 +681,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
     for (int h = 0; h < PX && xact; ++h) {
       const int row = ch + NT / 8 * h, c = tt ^ swz(row);
       float* const r = raw[h];
+      if (p.xpro) {                         // BN + ReLU of x's producer on the in-image elements
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int bb = 0; bb < 6; ++bb) {
+            const bool in = (xv[h] >> a) & (xv[h] >> (8 + bb)) & 1u;
+            r[a * 6 + bb] = in ? fmaxf(fmaf(r[a * 6 + bb], xpc[h][0], xpc[h][1]), 0.f) : 0.f;
+          }
+      }
 #pragma unroll
       for (int bb = 0; bb < 6; ++bb) {
         float o[6];
@@ -1078,10 +1119,11 @@ extern "C" int rk_wino4_weights_multi(const float* arena, float* dst, const int*
 namespace {
 // shared launcher of the small-wave-tile Winograd forward kernels: MO = 4 (u [36][N][C], H, W multiples
 // of 4) or MO = 2 (u [16][N][C], even H, W); T tiles x BNC channels per block of NT threads
-template <int MO, int WM, int WN, int MINW, int NS = 1, bool UB = false, bool WS = false>
+// PRO: normalise-on-load instantiations (flags 0 / WF_STATS only: the conv after a BN + ReLU block)
+template <int MO, int WM, int WN, int MINW, int NS = 1, bool UB = false, bool WS = false, bool PRO = false>
 int launch_gfwd(const float* x, const float* u, float* y, const float* bias, double* stats, int slotMask,
                 const float* gate, int Nb, int H, int W, int C, int N, int flags, int groups, long long gx,
-                long long gu, long long gy, long long gbias, void* stream) {
+                long long gu, long long gy, long long gbias, void* stream, const float* pro = nullptr) {
   constexpr int T = 16 * WM, BNC = 16 * WN, P = (MO + 2) * (MO + 2);
   if (Nb <= 0 || H <= 0 || W <= 0 || (H % MO) || (W % MO) || C <= 0 || (C % KC) || N <= 0 || groups <= 0)
     return RK_EBADARG;
@@ -1089,8 +1131,11 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   if ((flags & (WF_BNB | WF_BNP)) && (!gate || !bias)) return RK_EBADARG;
   if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
   if (groups > 1 && (flags & (WF_STATS | WF_BNB | WF_BNP))) return RK_EUNSUPPORTED;
+  if (PRO != (pro != nullptr)) return RK_EBADARG;
+  if (PRO && (groups > 1 || (flags & ~WF_STATS))) return RK_EUNSUPPORTED;
   W4Params p;
   p.x = x; p.u = u; p.y = y; p.bias = bias; p.stats = stats; p.gate = gate;
+  p.pro = pro;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.N = N;
   p.TW = W / MO;
   p.THW = (H / MO) * (W / MO);
@@ -1112,6 +1157,14 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   p.bpg = (int)bpg;
   const dim3 grid((unsigned)blocks), block(64 * WM * WN * (WS ? 2 : 1));
   const hipStream_t st = (hipStream_t)stream;
+  if constexpr (PRO) {
+    if (flags == WF_STATS)
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_STATS, NS, UB, WS, true>), grid, block, 0, st, p);
+    else
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0, NS, UB, WS, true>), grid, block, 0, st, p);
+    RK_LAUNCH_CHECK();
+    return RK_OK;
+  }
   switch (flags) {
     case 0: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, 0, NS, UB, WS>), grid, block, 0, st, p); break;
     case WF_STATS:
@@ -1131,10 +1184,22 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
 
 // y = conv3x3(x, w) via F(4x4,3x3) with u = rk_wino4_weights(w); flags / grouping as rk_wino_conv_grp.
 // variant 0: 8 waves, 64 tiles x 32 channels (1 block per CU); 1: 4 waves, 32 x 32 (2 per CU)
-extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const float* bias, double* stats,
-                                 int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
-                                 int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
-                                 void* stream) {
+static int wino4_conv_dispatch(const float* x, const float* u, float* y, const float* bias, double* stats,
+                               int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
+                               int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
+                               void* stream, const float* pro) {
+  if (pro) {   // normalise-on-load: the blocked-weight tiles only (the training path's weight sets)
+    if (variant == 3)
+      return launch_gfwd<4, 4, 2, 1, 1, true, false, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N,
+                                                           flags, groups, gx, gu, gy, gbias, stream, pro);
+    if (variant == 4)
+      return launch_gfwd<4, 2, 2, 2, 1, true, false, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N,
+                                                           flags, groups, gx, gu, gy, gbias, stream, pro);
+    if (variant == 5)
+      return launch_gfwd<4, 2, 2, 1, 2, true, true, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N,
+                                                          flags, groups, gx, gu, gy, gbias, stream, pro);
+    return RK_EUNSUPPORTED;
+  }
   if (variant == 0)
     return launch_gfwd<4, 4, 2, 1>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups, gx, gu, gy,
                                    gbias, stream);
@@ -1156,6 +1221,24 @@ extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const
     return launch_gfwd<4, 2, 2, 1, 2, true, true>(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, groups,
                                                   gx, gu, gy, gbias, stream);
   return RK_EBADARG;
+}
+
+extern "C" int rk_wino4_conv_grp(const float* x, const float* u, float* y, const float* bias, double* stats,
+                                 int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
+                                 int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
+                                 void* stream) {
+  return wino4_conv_dispatch(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, variant, groups, gx, gu,
+                             gy, gbias, stream, nullptr);
+}
+
+// normalise-on-load: x is the pre-BN output of the previous conv and pro = its BN scale [C], shift [C]; every
+// in-image input element is loaded as relu(x * scale + shift) (the consumer of a materialised BN + ReLU pass)
+extern "C" int rk_wino4_conv_pro(const float* x, const float* u, float* y, const float* bias, double* stats,
+                                 int slotMask, const float* gate, int Nb, int H, int W, int C, int N, int flags,
+                                 int variant, const float* pro, void* stream) {
+  if (!pro) return RK_EBADARG;
+  return wino4_conv_dispatch(x, u, y, bias, stats, slotMask, gate, Nb, H, W, C, N, flags, variant, 1, 0, 0, 0, 0,
+                             stream, pro);
 }
 
 // F(2x2,3x3) with u = rk_wino_weights(w) [16][N][C] on small wave tiles (many blocks for small grids):
@@ -1193,14 +1276,16 @@ extern "C" int rk_wino4_conv(const float* x, const float* u, float* y, const flo
 // (A position-split variant — each wave 9 of the 36 positions for a whole 32x32 tile on 32x32x2 MFMAs,
 // half the LDS reads per MFMA cycle — measured 5-8% SLOWER than variant 1 on every VGG-small layer,
 // profiles/wgrad4_variants_r3.jsonl, and was removed: the LDS-write / transform phase bounds it.)
-extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
-                                int splits, int accumulate, int variant, void* stream) {
+static int wino4_wgrad_dispatch(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
+                                int splits, int accumulate, int variant, void* stream, const float* xpro) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0 || splits <= 0) return RK_EBADARG;
   if (splits > 1 && accumulate) return RK_EBADARG;
   if (variant < 0 || variant > 2) return RK_EBADARG;
+  if (xpro && variant == 2) return RK_EUNSUPPORTED;
   const int BCO = variant == 1 ? 64 : 32, BCI = 32;
   W4wParams p;
   p.dy = dy; p.x = x; p.out = out;
+  p.xpro = xpro;
   p.Nb = Nb; p.H = H; p.W = W; p.Co = Co; p.Ci = Ci;
   p.TW = W / 4;
   p.THW = (H / 4) * (W / 4);
@@ -1228,6 +1313,18 @@ extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int
     hipLaunchKernelGGL((wino4_wgrad_kernel<2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p);
   RK_LAUNCH_CHECK();
   return RK_OK;
+}
+
+extern "C" int rk_wino4_wgrad_v(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
+                                int splits, int accumulate, int variant, void* stream) {
+  return wino4_wgrad_dispatch(dy, x, out, Nb, H, W, Co, Ci, splits, accumulate, variant, stream, nullptr);
+}
+
+// normalise-on-load: x is the pre-BN output of its producer, xpro = that BN's scale [Ci], shift [Ci] (+ ReLU)
+extern "C" int rk_wino4_wgrad_pro(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
+                                  int splits, int accumulate, int variant, const float* xpro, void* stream) {
+  if (!xpro) return RK_EBADARG;
+  return wino4_wgrad_dispatch(dy, x, out, Nb, H, W, Co, Ci, splits, accumulate, variant, stream, xpro);
 }
 
 extern "C" int rk_wino4_wgrad(const float* dy, const float* x, float* out, int Nb, int H, int W, int Co, int Ci,
@@ -1287,24 +1384,36 @@ __global__ __launch_bounds__(256) void w4pt_dy_kernel(const float* __restrict__ 
 }
 
 // PL: bf16 X6 planes v [36][3][T][C] (hi, mid, lo) instead of fp32 v [36][T][C]
+// pro (nullable): normalise-on-load — x is the pre-BN output of its producer; relu(x * scale + shift) with
+// scale = pro[0 .. C), shift = pro[C .. 2C) on every in-image element (the padding stays 0)
 template <bool PL = false>
 __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x, void* __restrict__ v, int H,
-                                                     int W, int C, int TW, int THW, int total4, int T) {
+                                                     int W, int C, int TW, int THW, int total4, int T,
+                                                     const float* __restrict__ pro) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total4) return;
   const int C4 = C >> 2;
   const int c4 = i % C4, t = i / C4;
   const int n = t / THW, r = t - n * THW, ty = r / TW;
   const int oy = 4 * ty - 1, ox = 4 * (r - ty * TW) - 1;
+  f32x4 psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f};
+  if (pro) {
+    psc = *(const f32x4*)(pro + 4 * c4);
+    psh = *(const f32x4*)(pro + C + 4 * c4);
+  }
   f32x4 d[36];
 #pragma unroll
   for (int a = 0; a < 6; ++a)
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
       const int yy = oy + a, xx = ox + b;
-      d[a * 6 + b] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
-                         ? *(const f32x4*)(x + ((n * H + yy) * W + xx) * C + 4 * c4)
-                         : f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      f32x4 val = in ? *(const f32x4*)(x + ((n * H + yy) * W + xx) * C + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (pro && in) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) val[e] = fmaxf(fmaf(val[e], psc[e], psh[e]), 0.f);
+      }
+      d[a * 6 + b] = val;
     }
 #pragma unroll
   for (int b = 0; b < 6; ++b)
@@ -1572,8 +1681,8 @@ __global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__
 }  // namespace
 
 // M [36][T][Co] and V [36][T][Ci] (T = Nb * H/4 * W/4 tiles) of dy / x (NHWC, H and W multiples of 4)
-extern "C" int rk_wino4_pt_transform(const float* dy, const float* x, float* m, float* v, int Nb, int H, int W,
-                                     int Co, int Ci, void* stream) {
+static int wino4_pt_transform(const float* dy, const float* x, float* m, float* v, int Nb, int H, int W, int Co,
+                              int Ci, void* stream, const float* xpro) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || Co <= 0 || Ci <= 0) return RK_EBADARG;
   if ((Co & 3) || (Ci & 3)) return RK_EUNSUPPORTED;
   const int TW = W / 4, THW = (H / 4) * (W / 4);
@@ -1584,9 +1693,21 @@ extern "C" int rk_wino4_pt_transform(const float* dy, const float* x, float* m, 
                      W, Co, TW, THW, (int)ty, (int)T);
   RK_LAUNCH_CHECK();
   hipLaunchKernelGGL(w4pt_x_kernel<false>, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
-                     v, H, W, Ci, TW, THW, (int)tx, (int)T);
+                     v, H, W, Ci, TW, THW, (int)tx, (int)T, xpro);
   RK_LAUNCH_CHECK();
   return RK_OK;
+}
+
+extern "C" int rk_wino4_pt_transform(const float* dy, const float* x, float* m, float* v, int Nb, int H, int W,
+                                     int Co, int Ci, void* stream) {
+  return wino4_pt_transform(dy, x, m, v, Nb, H, W, Co, Ci, stream, nullptr);
+}
+
+// the same with x normalised on load (xpro: its producer's BN scale [Ci], shift [Ci], + ReLU)
+extern "C" int rk_wino4_pt_transform_pro(const float* dy, const float* x, float* m, float* v, int Nb, int H, int W,
+                                         int Co, int Ci, const float* xpro, void* stream) {
+  if (!xpro) return RK_EBADARG;
+  return wino4_pt_transform(dy, x, m, v, Nb, H, W, Co, Ci, stream, xpro);
 }
 
 // du: nslab slabs of [36][Co][Ci], slab floats apart (split-K partial sums), summed here
@@ -1860,7 +1981,8 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
 }
 
 // V = B^T x B of every 6x6 window: [36][T][C] (the x half of rk_wino4_pt_transform)
-extern "C" int rk_wino4_pt_input(const float* x, float* v, int Nb, int H, int W, int C, void* stream) {
+extern "C" int rk_wino4_pt_input_pro(const float* x, float* v, int Nb, int H, int W, int C, const float* pro,
+                                     void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || C <= 0) return RK_EBADARG;
   if (C & 3) return RK_EUNSUPPORTED;
   const int TW = W / 4, THW = (H / 4) * (W / 4);
@@ -1868,13 +1990,18 @@ extern "C" int rk_wino4_pt_input(const float* x, float* v, int Nb, int H, int W,
   if (36 * T * C >= (1ll << 31)) return RK_EUNSUPPORTED;
   const long long tx = T * C / 4;
   hipLaunchKernelGGL(w4pt_x_kernel<false>, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
-                     v, H, W, C, TW, THW, (int)tx, (int)T);
+                     v, H, W, C, TW, THW, (int)tx, (int)T, pro);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
 
-// V planes [36][3][T][C] (bf16 hi, mid, lo of B^T x B) for the pre-split X6 GEMM (x6p.hip)
-extern "C" int rk_x6p_w4_input(const float* x, void* v, int Nb, int H, int W, int C, void* stream) {
+extern "C" int rk_wino4_pt_input(const float* x, float* v, int Nb, int H, int W, int C, void* stream) {
+  return rk_wino4_pt_input_pro(x, v, Nb, H, W, C, nullptr, stream);
+}
+
+// V planes [36][3][T][C] (bf16 hi, mid, lo of B^T x B) for the pre-split X6 GEMM (x6p.hip); pro as above
+extern "C" int rk_x6p_w4_input_pro(const float* x, void* v, int Nb, int H, int W, int C, const float* pro,
+                                   void* stream) {
   if (Nb <= 0 || H <= 0 || W <= 0 || (H & 3) || (W & 3) || C <= 0) return RK_EBADARG;
   if (C & 3) return RK_EUNSUPPORTED;
   const int TW = W / 4, THW = (H / 4) * (W / 4);
@@ -1882,9 +2009,13 @@ extern "C" int rk_x6p_w4_input(const float* x, void* v, int Nb, int H, int W, in
   if (108 * T * C >= (1ll << 31) || (long long)Nb * H * W * C >= (1ll << 31)) return RK_EUNSUPPORTED;
   const long long tx = T * C / 4;
   hipLaunchKernelGGL(w4pt_x_kernel<true>, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
-                     v, H, W, C, TW, THW, (int)tx, (int)T);
+                     v, H, W, C, TW, THW, (int)tx, (int)T, pro);
   RK_LAUNCH_CHECK();
   return RK_OK;
+}
+
+extern "C" int rk_x6p_w4_input(const float* x, void* v, int Nb, int H, int W, int C, void* stream) {
+  return rk_x6p_w4_input_pro(x, v, Nb, H, W, C, nullptr, stream);
 }
 
 // M^T planes [36][3][Co][T] of dy and V^T planes [36][3][Ci][T] of x (bf16), the weight-gradient operands

@@ -389,6 +389,16 @@ class ConvNetEngine:
                     d = F.conv_dgrad(dy, fl.wb(name + '.w'))
 
     # ------------------------------------------------------------------------- fp32 train
+    def _bn_on_load(self, bi, B, ww):
+        """Block bi's BN + ReLU is applied by its consumer's loads (normalise-on-load): a non-pooled block
+        followed by another conv block whose F(4x4) kernels (blocked weights) take pre-BN input."""
+        if ww is None or bi + 1 >= len(self.blocks):
+            return False
+        name, cin, cout, pool, hw = self.blocks[bi]
+        nxt = self.blocks[bi + 1]
+        return (not pool and nxt[1] == cout and nxt[4] == hw and ww.lazy('u4b', bi + 1) is not None
+                and S.bn_on_load_ok(B, hw, hw, cout, nxt[2]))
+
     def _fwd_bwd_gpu_f32(self, x, labels):
         """The fp32 step: x [B, H, W, cin_p] fp32 NHWC, labels [B] int32; every GEMM on the f32 MFMA."""
         fl = self.flat
@@ -400,6 +410,7 @@ class ConvNetEngine:
         if ww is not None:
             ww.refresh()   # one launch per family: the live Winograd-domain weight sets of every block
         acts, saved, h = [x], [], x
+        pros, hpro = [None], None   # normalise-on-load: the BN coeffs acts[bi] still needs applied (or None)
         for bi, (name, cin, cout, pool, hw) in enumerate(self.blocks):
             wk = dict(wino=ww.lazy('u2', bi) if ww is not None else None,
                       wino4=ww.lazy('u4', bi) if ww is not None else None,
@@ -416,11 +427,20 @@ class ConvNetEngine:
                 acts.append(h)
                 continue
             rm, rv = self.running_stats(bi)
-            y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0], **wk)
-            h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
-                                 self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
+            y = S.conv_fwd(h, fl.w(name + '.w'), stats_acc=accs[bi][0], pro=hpro, **wk)
+            if self._bn_on_load(bi, B, ww):
+                # BN + ReLU never materialised: the next conv's forward and weight-gradient kernels apply
+                # scale / shift + ReLU to y as they load it (bn_finalize = the coefficient half, one block)
+                coeffs = S.bn_finalize(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
+                                       self.bn_eps, rm, rv, self.bn_momentum)
+                h, hpro = y, coeffs
+            else:
+                h, coeffs = S.bn_fwd(y, accs[bi][0], B * hw * hw, fl.w(name + '.gamma'), fl.w(name + '.beta'),
+                                     self.bn_eps, rm, rv, self.bn_momentum, pool=pool, act=F.ACT_RELU)
+                hpro = None
             saved.append((y, coeffs))
             acts.append(h)
+            pros.append(hpro)
         in_saved = None
         if self.input_bn:
             raw = h.reshape(B, 1, 1, self.feat_dim)
@@ -491,7 +511,8 @@ class ConvNetEngine:
             else:   # ReLU mask / pool routing only; sum dz -> the bias gradient
                 dy = S.bn_bwd(d, y, coeffs, self._ones[:cout], accs[bi][1], pool=pool, act=F.ACT_RELU,
                               dbeta=fl.g(name + '.b'), reduced=reduced, count=float('inf'))
-            S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1))
+            S.conv_wgrad(dy, acts[bi], out=fl.g(name + '.w').view(cout, -1),
+                         xpro=pros[bi] if self.bn else None)
             if bi == 0:
                 break
             py, pco = saved[bi - 1]

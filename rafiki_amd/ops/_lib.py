@@ -75,6 +75,11 @@ _SIGS = {
     "rk_wino4_weights_multi": [vp, vp, vp, i32, vp, vp],
     "rk_wino4_conv_grp": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, vp],
     "rk_wino4_conv": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "rk_wino4_conv_pro": [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp],
+    "rk_wino4_wgrad_pro": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp],
+    "rk_wino4_pt_transform_pro": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp],
+    "rk_wino4_pt_input_pro": [vp, vp, i32, i32, i32, i32, vp, vp],
+    "rk_x6p_w4_input_pro": [vp, vp, i32, i32, i32, i32, vp, vp],
     "rk_wino4_wgrad": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "rk_wino4_wgrad_v": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "rk_wino4_pt_transform": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],

@@ -159,13 +159,16 @@ def _slots_flags(acc):
 
 # ------------------------------------------------------------------------------------------ conv
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None, bias=None, act=ACT_NONE,
-             slope=0.2, out=None, wino=None, wino4=None, wino4p=None, wino4b=None):
+             slope=0.2, out=None, wino=None, wino4=None, wino4p=None, wino4b=None, pro=None):
     """y = conv3x3(x, w) (stride 1, pad 1; taps=1: 1x1) [+bias][act]; with ``stats_acc`` (zeroed fp64
     [SL][2][Cout]) the per-channel (sum y, sum y^2) BatchNorm statistics ride in the epilogue.
     ``wino``: the layer's Winograd weights (WinoWeights.u), or a callable producing them (run only
     when a Winograd candidate runs, so the tuner times transform + conv) -> the fused F(2x2,3x3)
     kernels are more autotune candidates; ``wino4`` likewise for the F(4x4,3x3) kernels (WinoWeights.u4),
-    ``wino4p`` the X6 weight planes (WinoWeights 'u4p') of the pre-split pre-transformed F(4x4) path."""
+    ``wino4p`` the X6 weight planes (WinoWeights 'u4p') of the pre-split pre-transformed F(4x4) path.
+    ``pro``: normalise-on-load — x is the pre-BN output y of the previous conv, pro = its coeffs
+    (bn_finalize): every candidate loads relu(y * scale + shift) (the F(4x4) kernels with blocked weights
+    and the pre-transformed paths; see bn_on_load_ok)."""
     _check(x, 'conv_fwd x')
     Nb, H, W, Cin = x.shape
     Cout = w.shape[0]
@@ -189,11 +192,11 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         tile, nst, s = cfg
         if tile == WINO4_PTX:
             wino4_conv_pt(x, wino4p() if callable(wino4p) else wino4p, out=out, bias=bias, stats=stats_acc,
-                          relu=act == ACT_RELU, tile=nst // 4, nst=nst % 4, splits=s, lrelu=lrelu)
+                          relu=act == ACT_RELU, tile=nst // 4, nst=nst % 4, splits=s, lrelu=lrelu, pro=pro)
             return
         if tile == WINO4_PT:
             wino4_conv_pt(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
-                          relu=act == ACT_RELU, tile=nst, nst=s, lrelu=lrelu)
+                          relu=act == ACT_RELU, tile=nst, nst=s, lrelu=lrelu, pro=pro)
             return
         if cfg in WINO4_CFGS:
             wino4_conv(x, wino4() if callable(wino4) else wino4, out=out, bias=bias, stats=stats_acc,
@@ -201,7 +204,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
             return
         if cfg in WINO4B_CFGS:
             wino4_conv(x, wino4b() if callable(wino4b) else wino4b, out=out, bias=bias, stats=stats_acc,
-                       relu=act == ACT_RELU, variant=_WINO4B_VARIANT[cfg[0]], n_out=Cout)
+                       relu=act == ACT_RELU, variant=_WINO4B_VARIANT[cfg[0]], n_out=Cout, pro=pro)
             return
         if cfg in WINO_CFGS:
             wino_conv(x, wino() if callable(wino) else wino, out=out, bias=bias, stats=stats_acc,
@@ -217,7 +220,12 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         sgemm(KIND_CONV, x, w, slab, M, Cout, K, Cin, K, Cout, tile=tile, nst=nst, splits=s, slab_stride=M * Cout,
               H=H, W=W, C=Cin, taps=taps)
         sreduce_epi(slab, M, Cout, out.view(M, Cout), bias=bias, act=act, slope=slope)
-    cands = _cands(M, Cout, splittable=stats_acc is None and Cout % 4 == 0, K=K, big=Cin % 32 == 0)
+    if pro is not None:   # only the kernels that normalise on load are candidates
+        assert bias is None and act == ACT_NONE and pro.shape == (4, Cin)
+        use_w = use_w4 = False
+        cands = []
+    else:
+        cands = _cands(M, Cout, splittable=stats_acc is None and Cout % 4 == 0, K=K, big=Cin % 32 == 0)
     if use_w:
         cands.extend(WINO_CFGS)
     if use_w4:
@@ -228,9 +236,12 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, *, taps: int = 9, stats_acc=None,
         cands.extend(WINO4_PT_CFGS)
     if use_ptx:
         cands.extend(WINO4_PTX_CFGS)
+    if not cands:
+        raise ValueError('conv_fwd(pro=...): no normalise-on-load kernel for this shape (see bn_on_load_ok)')
     cfg = _pick(('sf', M, Cout, K, H, W, Cin, taps, flags, 'lazy' if callable(wino) else use_w,
                  'lazy' if callable(wino4) else use_w4, use_pt, 'lazy' if callable(wino4p) else use_ptx)
-                + (('b', 'lazy' if callable(wino4b) else True),) * use_w4b, cands, run)
+                + (('b', 'lazy' if callable(wino4b) else True),) * use_w4b + (('pro',) if pro is not None else ()),
+                cands, run)
     if stats_acc is not None and autotune.can_tune():
         stats_acc.zero_()  # tuning runs accumulated into it
     run(cfg)
@@ -314,8 +325,10 @@ def conv_dgrad(dy: torch.Tensor, wt, *, taps: int = 9, out=None, gate=None, bnb=
     return out
 
 
-def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, accumulate=False):
-    """dW[co][tap][ci] (fp32 [Cout][taps*Cin]) = sum over pixels of dy[p][co] * x[shift_tap(p)][ci]."""
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, accumulate=False, xpro=None):
+    """dW[co][tap][ci] (fp32 [Cout][taps*Cin]) = sum over pixels of dy[p][co] * x[shift_tap(p)][ci].
+    ``xpro``: x is the pre-BN output of its producer and xpro that BN's coeffs (bn_finalize): the F(4x4)
+    kernels normalise + ReLU it on load (the only candidates then; see bn_on_load_ok)."""
     _check(dy, 'conv_wgrad dy')
     _check(x, 'conv_wgrad x')
     Nb, H, W, Cout = dy.shape
@@ -330,10 +343,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
             wino_wgrad(dy, x, out, splits=s, accumulate=accumulate)
             return
         if tile == WINO4_WGRAD:
-            wino4_wgrad(dy, x, out, splits=s, accumulate=accumulate, variant=nst)
+            wino4_wgrad(dy, x, out, splits=s, accumulate=accumulate, variant=nst, xpro=xpro)
             return
         if tile == WINO4_WGRAD_PT:
-            wino4_wgrad_pt(dy, x, out, accumulate=accumulate, tile=nst, nst=s)
+            wino4_wgrad_pt(dy, x, out, accumulate=accumulate, tile=nst, nst=s, xpro=xpro)
             return
         if tile == WINO4_WGRAD_PTX:
             wino4_wgrad_pt(dy, x, out, accumulate=accumulate, tile=nst // 4, nst=nst % 4, planes=True, splits=s)
@@ -356,9 +369,16 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, *, taps: int = 9, out=None, ac
     w4cands = _wino4_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
     ptcands = _wino4_pt_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
     ptxcands = _wino4_ptx_wgrad_cands(Nb, H, W, Cout, Cin) if taps == 9 else []
-    cands += wcands + w4cands + ptcands + ptxcands
+    if xpro is not None:
+        assert taps == 9 and xpro.shape == (4, Cin)
+        cands, wcands, ptxcands = w4cands + ptcands, [], []
+        if not cands:
+            raise ValueError('conv_wgrad(xpro=...): no normalise-on-load kernel for this shape (see bn_on_load_ok)')
+    else:
+        cands += wcands + w4cands + ptcands + ptxcands
     cfg = _pick(('sw', M, N, K, H, W, Cin, taps, bool(accumulate), bool(wcands), bool(w4cands), bool(ptcands),
-                 bool(ptxcands)), cands, run, protect=(out,) if accumulate else ())
+                 bool(ptxcands)) + (('pro',) if xpro is not None else ()), cands, run,
+                protect=(out,) if accumulate else ())
     run(cfg)
     return out
 
@@ -516,6 +536,18 @@ def wino4_ok(H: int, W: int, C: int) -> bool:
     return WINO and WINO4 and H % 4 == 0 and W % 4 == 0 and C % 8 == 0 and C > 0
 
 
+# normalise-on-load (the non-pooled BN + ReLU blocks of the fp32 engine): RAFIKI_BN_ON_LOAD=0 materialises
+# every BN output instead
+BN_ON_LOAD = os.environ.get('RAFIKI_BN_ON_LOAD', '1') != '0'
+
+
+def bn_on_load_ok(Nb: int, H: int, W: int, Cin: int, Cout: int) -> bool:
+    """Whether a 3x3 conv of Cin -> Cout channels on [Nb, H, W] can take its input as the previous conv's
+    pre-BN output (conv_fwd(pro=...) with blocked F(4x4) weights, conv_wgrad(xpro=...))."""
+    return (BN_ON_LOAD and wino4_ok(H, W, Cin) and Cin % 4 == 0
+            and bool(_wino4_wgrad_cands(Nb, H, W, Cout, Cin) or _wino4_pt_cands(Nb, H, W, Cout, Cin)))
+
+
 def wino4_u(w: torch.Tensor) -> torch.Tensor:
     """Forward F(4x4) weights [36][Cout][Cin] of one conv weight [Cout, 3, 3, Cin] (fresh buffer)."""
     Cout = w.shape[0]
@@ -558,9 +590,11 @@ def wino4b_u(w: torch.Tensor, dgrad: bool = False) -> torch.Tensor:
 
 
 def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None, bnp=None,
-               variant=0, n_out=None):
+               variant=0, n_out=None, pro=None):
     """y = conv3x3(x, w) (stride 1, pad 1) by F(4x4,3x3) from u = wino4_u(w); options as wino_conv.
-    Variants 3 / 4 take the blocked set (wino4b_u / WinoWeights 'u4b'), flat, with ``n_out`` channels."""
+    Variants 3 / 4 take the blocked set (wino4b_u / WinoWeights 'u4b'), flat, with ``n_out`` channels.
+    ``pro``: normalise-on-load — x is the pre-BN output of the previous conv and pro its BN coeffs [4][C]
+    (bn_finalize): the kernel loads relu(x * scale + shift) (blocked variants 3-5, no bias / activation)."""
     _check(x, 'wino4_conv x')
     Nb, H, W, C = x.shape
     if variant >= 3:
@@ -589,6 +623,11 @@ def wino4_conv(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=N
         bias, flags = coeffs[2:4].reshape(-1), WF_BNP
     if stats is not None:
         assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
+    if pro is not None:
+        assert variant >= 3 and flags in (0, WF_STATS) and pro.shape == (4, C) and pro.is_contiguous()
+        _lib.call("rk_wino4_conv_pro", _p(x), _p(u), _p(out), None, _p(stats), _slots_flags(stats), None,
+                  Nb, H, W, C, N, flags, int(variant), _p(pro[2]), _s())
+        return out
     _lib.call("rk_wino4_conv", _p(x), _p(u), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
               Nb, H, W, C, N, flags, int(variant), _s())
     return out
@@ -617,7 +656,7 @@ WINO4_PT_CFGS = tuple((WINO4_PT, t + x, n) for x in ((0, X6) if USE_X6 else (0,)
 
 
 def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stats=None, relu=False, bnb=None,
-                  bnp=None, tile=0, nst=2, splits=1, lrelu=None):
+                  bnp=None, tile=0, nst=2, splits=1, lrelu=None, pro=None):
     """wino4_conv through position-major buffers: V = B^T x B [36][T][C] (one launch), Y'[q] = V[q] u[q]^T
     as one 36-group sgemm, then A^T Y' A with the same epilogues (bias / ReLU / BN statistics / BNB / BNP;
     ``lrelu`` = slope: bias + leaky ReLU, the PG-GAN discriminator's conv epilogue).
@@ -653,18 +692,26 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
     if stats is not None:
         assert stats.dtype == torch.float64 and stats.is_contiguous() and stats.shape[-1] == N
     T = Nb * (H // 4) * (W // 4)
+    if pro is not None:   # normalise-on-load in the input transform (pro = the producer's BN coeffs [4][C])
+        assert pro.shape == (4, C) and pro.is_contiguous()
     if planes:   # pre-split X6: V planes [36][3][T][C] once, then the plane GEMM (no split in the K loop)
         splits = x6p_splits(C, splits)
         # Y' tile-major [T][36][N]: the output transform reads each tile's 36 positions as one run
         yt = torch.empty((splits, T, 36, N), device=x.device, dtype=torch.float32)
         v = torch.empty((36, 3, T, C), device=x.device, dtype=torch.bfloat16)
-        _lib.call("rk_x6p_w4_input", _p(x), _p(v), Nb, H, W, C, _s())
+        if pro is None:
+            _lib.call("rk_x6p_w4_input", _p(x), _p(v), Nb, H, W, C, _s())
+        else:
+            _lib.call("rk_x6p_w4_input_pro", _p(x), _p(v), Nb, H, W, C, _p(pro[2]), _s())
         x6p_gemm(v, u, yt, T, N, C, groups=36, tile=tile, nst=nst, splits=splits, row_major_groups=True)
     else:
         splits = 1
         yt = torch.empty((36, T, N), device=x.device, dtype=torch.float32)
         v = torch.empty((36, T, C), device=x.device, dtype=torch.float32)
-        _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
+        if pro is None:
+            _lib.call("rk_wino4_pt_input", _p(x), _p(v), Nb, H, W, C, _s())
+        else:
+            _lib.call("rk_wino4_pt_input_pro", _p(x), _p(v), Nb, H, W, C, _p(pro[2]), _s())
         sgemm_grp(KIND_DENSE, v, u, yt, T, N, C, C, C, N, 36, T * C, N * C, T * N, tile=tile, nst=nst)
     _lib.call("rk_wino4_pt_conv_out", _p(yt), _p(out), _p(bias), _p(stats), _slots_flags(stats), _p(gate),
               Nb, H, W, N, flags, splits, 36 * T * N, int(planes), float(0.0 if lrelu is None else lrelu), _s())
@@ -716,20 +763,25 @@ def _wino4_wgrad_cands(Nb, H, W, Cout, Cin):
     return out
 
 
-def wino4_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1, accumulate=False, variant=0):
+def wino4_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1, accumulate=False, variant=0,
+                xpro=None):
     """out [Cout][9*Cin] (+)= weight gradient of a 3x3 stride-1 conv by F(4x4,3x3); splits > 1: per-split
-    slabs summed by reduce_slabs."""
+    slabs summed by reduce_slabs.  ``xpro``: x is pre-BN, normalised + ReLU'd on load (variants 0 / 1)."""
     _check(dy, 'wino4_wgrad dy')
     _check(x, 'wino4_wgrad x')
     Nb, H, W, Cout = dy.shape
     Cin = x.shape[-1]
     assert x.shape[:3] == dy.shape[:3] and out.numel() == Cout * 9 * Cin and out.is_contiguous()
+    if xpro is not None:
+        assert xpro.shape == (4, Cin) and xpro.is_contiguous() and variant in (0, 1)
+        fn, tail = "rk_wino4_wgrad_pro", (_p(xpro[2]), _s())
+    else:
+        fn, tail = "rk_wino4_wgrad_v", (_s(),)
     if splits == 1:
-        _lib.call("rk_wino4_wgrad_v", _p(dy), _p(x), _p(out), Nb, H, W, Cout, Cin, 1, int(bool(accumulate)),
-                  int(variant), _s())
+        _lib.call(fn, _p(dy), _p(x), _p(out), Nb, H, W, Cout, Cin, 1, int(bool(accumulate)), int(variant), *tail)
         return out
     slab = torch.empty((splits, Cout, 9 * Cin), device=dy.device, dtype=torch.float32)
-    _lib.call("rk_wino4_wgrad_v", _p(dy), _p(x), _p(slab), Nb, H, W, Cout, Cin, int(splits), 0, int(variant), _s())
+    _lib.call(fn, _p(dy), _p(x), _p(slab), Nb, H, W, Cout, Cin, int(splits), 0, int(variant), *tail)
     reduce_slabs(slab, out.view(Cout, 9 * Cin), accumulate=accumulate)
     return out
 
@@ -754,7 +806,7 @@ def _wino4_pt_cands(Nb, H, W, Cout, Cin):
 
 
 def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accumulate=False, tile=0, nst=2,
-                   planes=False, splits=1):
+                   planes=False, splits=1, xpro=None):
     """out [Cout][9*Cin] (+)= the F(4x4,3x3) weight gradient through position-major transformed buffers:
     M [36][T][Cout], V [36][T][Cin] (one transform launch each), dU[q] = M[q]^T V[q] as ONE sgemm with
     36 K-splits (slab q = dU[q]), then dW = G^T dU G.  ``planes``: the operands as X6 planes transposed to
@@ -766,6 +818,7 @@ def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accu
     T = Nb * (H // 4) * (W // 4)
     assert H % 4 == 0 and W % 4 == 0 and T % 32 == 0 and x.shape[:3] == dy.shape[:3], (dy.shape, x.shape)
     assert out.numel() == Cout * 9 * Cin and out.is_contiguous()
+    assert xpro is None or (not planes and xpro.shape == (4, Cin) and xpro.is_contiguous())
     if planes:   # pre-split X6: M^T / V^T planes [36][3][C][T] (K = tiles inner), 36-group plane GEMM
         splits = x6p_splits(T, splits)
         du = torch.empty((splits, 36, Cout, Cin), device=dy.device, dtype=torch.float32)
@@ -778,7 +831,11 @@ def wino4_wgrad_pt(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, accu
         du = torch.empty((36, Cout, Cin), device=dy.device, dtype=torch.float32)
         m = torch.empty((36 * T, Cout), device=dy.device, dtype=torch.float32)
         v = torch.empty((36 * T, Cin), device=dy.device, dtype=torch.float32)
-        _lib.call("rk_wino4_pt_transform", _p(dy), _p(x), _p(m), _p(v), Nb, H, W, Cout, Cin, _s())
+        if xpro is None:
+            _lib.call("rk_wino4_pt_transform", _p(dy), _p(x), _p(m), _p(v), Nb, H, W, Cout, Cin, _s())
+        else:
+            _lib.call("rk_wino4_pt_transform_pro", _p(dy), _p(x), _p(m), _p(v), Nb, H, W, Cout, Cin, _p(xpro[2]),
+                      _s())
         sgemm(KIND_DENSE_DW, m, v, du, Cout, Cin, 36 * T, Cout, Cin, Cin, tile=tile, nst=nst, splits=36,
               slab_stride=Cout * Cin)
     _lib.call("rk_wino4_pt_output", _p(du), _p(out), Cout, Cin, int(bool(accumulate)), splits, 36 * Cout * Cin, _s())
@@ -1238,6 +1295,19 @@ def bn_fwd(y, acc, count, gamma, beta, eps, running_mean=None, running_var=None,
               _p(running_mean), _p(running_var), float(momentum), None, None, _p(coeffs), _p(out), Nb, H, W, C,
               int(pool), int(act), float(slope), _s())
     return out, coeffs
+
+
+def bn_finalize(y, acc, count, gamma, beta, eps, running_mean=None, running_var=None, momentum=0.1, *, coeffs=None):
+    """The coefficient half of bn_fwd (one block): coeffs [4][C] = mean, rstd, scale, shift and the
+    running-statistics update, no output pass — the consumer conv normalises + ReLUs y on its loads
+    (conv_fwd(pro=coeffs), conv_wgrad(xpro=coeffs))."""
+    Nb, H, W, C = y.shape
+    if coeffs is None:
+        coeffs = torch.empty((4, C), device=y.device, dtype=torch.float32)
+    _lib.call("rk_bnf_fwd", _p(y), _p(acc), acc.shape[0], float(count), _p(gamma), _p(beta), float(eps),
+              _p(running_mean), _p(running_var), float(momentum), None, None, _p(coeffs), None, Nb, H, W, C,
+              0, int(ACT_RELU), 0.2, _s())
+    return coeffs
 
 
 def bn_eval(y, scale, shift, *, pool=False, act=ACT_RELU, slope=0.2, out=None):
