@@ -60,6 +60,7 @@ struct W4Params {
 };
 
 constexpr unsigned OOB = 0x80000000u;
+constexpr int W4_PRO_MAXC = 512;   // normalise-on-load: input channels whose BN coefficients are staged in LDS
 
 RK_DEV int swz(int row) { return ((row >> 2) & 3) << 1; }
 
@@ -155,6 +156,14 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
   static_assert(!WS || (NS == 2 && UB), "warp-specialised: two stages, blocked weights");
   __shared__ __attribute__((aligned(16))) float Vs[NS][P][T][KC];
   __shared__ __attribute__((aligned(16))) float Us[NS][P][BNC][KC];
+  // PRO: the producer's BN scale [0, C) and shift [W4_PRO_MAXC, +C), staged once (4 KiB): read per chunk
+  // from LDS at transform time instead of riding in registers across the MFMA phase
+  __shared__ float Ps[PRO ? 2 * W4_PRO_MAXC : 1];
+  if constexpr (PRO) {
+    for (int i = threadIdx.x; i < 2 * p.C; i += (int)blockDim.x)
+      Ps[i < p.C ? i : W4_PRO_MAXC + i - p.C] = p.pro[i];
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool compute = !WS || wave < WM * WN;
   // tid: the thread's index within its role (WS loaders count from 0 too)
@@ -198,14 +207,9 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
   // UB: the block's weight chunks are consecutive 36-KiB images: chunk c of output block cb at
   // ((cb * nch + c) * UNITS) units of 16 B
   const int nchunk = p.C / KC;
-  auto load = [&](int c0, float (&raw)[IT][P], f32x2 (&ur)[ULR], f32x4 (&ub)[UBR], float (&pc)[2]) {
+  auto load = [&](int c0, float (&raw)[IT][P], f32x2 (&ur)[ULR], f32x4 (&ub)[UBR]) {
     // a chunk past Cin (the pipelined tail) reads zeros: empty buffer ranges
     const bool live = c0 < p.C;
-    if constexpr (PRO) {                   // this thread's input channel: BN scale / shift of the producer
-      const bool ok = live && c0 + lc < p.C;
-      pc[0] = ok ? p.pro[c0 + lc] : 0.f;
-      pc[1] = ok ? p.pro[p.C + c0 + lc] : 0.f;
-    }
     const __amdgpu_buffer_rsrc_t xr = rsrc(gxp + c0, live ? p.xbytes - 4ull * c0 : 0ull);
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
@@ -247,21 +251,36 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
                                                                              __builtin_amdgcn_readfirstlane(k * ustride), 0));
     }
   };
-  auto store = [&](int st, float (&raw)[IT][P], const f32x2 (&ur)[ULR], const f32x4 (&ub)[UBR],
-                   const float (&pc)[2]) {
+  // c0: the chunk's first input channel (PRO: its BN coefficients; chunks past C stay zero)
+  auto store = [&](int st, float (&raw)[IT][P], const f32x2 (&ur)[ULR], const f32x4 (&ub)[UBR], int c0) {
+    float psc = 0.f, psh = 0.f;
+    if constexpr (PRO) {
+      const bool ok = c0 + lc < p.C;
+      psc = Ps[ok ? c0 + lc : 0];
+      psh = Ps[W4_PRO_MAXC + (ok ? c0 + lc : 0)];
+      psc = ok ? psc : 0.f;
+      psh = ok ? psh : 0.f;
+    }
 #pragma unroll
     for (int h = 0; h < IT; ++h) {
       const int row = lt + NT / 8 * h, c = lc ^ swz(row);
       float* const r = raw[h];
-      if constexpr (PRO) {                 // BN + ReLU of the producer on the in-image elements; padding stays 0
+      if constexpr (PRO) {
+        // BN + ReLU of the producer on the in-image elements; the padding (loaded as 0) must stay 0, so its
+        // shift is 0: only the edge rows / columns of a window can leave the map (H, W multiples of 4), and
+        // a tile past the end has no row in it
         const unsigned rm = rmk[h], cm = cmk[h];
+        const float shT = rm ? psh : 0.f;
+        const float shTop = (rm & 1u) ? shT : 0.f, shBot = ((rm >> (A - 1)) & 1u) ? shT : 0.f;
+        const bool lin = cm & 1u, rin = (cm >> (A - 1)) & 1u;
 #pragma unroll
-        for (int a = 0; a < A; ++a)
+        for (int a = 0; a < A; ++a) {
+          const float shA = a == 0 ? shTop : a == A - 1 ? shBot : shT;
+          const float shL = lin ? shA : 0.f, shR = rin ? shA : 0.f;
 #pragma unroll
-          for (int bb = 0; bb < A; ++bb) {
-            const bool in = (rm >> a) & (cm >> bb) & 1u;
-            r[a * A + bb] = in ? fmaxf(fmaf(r[a * A + bb], pc[0], pc[1]), 0.f) : 0.f;
-          }
+          for (int bb = 0; bb < A; ++bb)
+            r[a * A + bb] = fmaxf(fmaf(r[a * A + bb], psc, bb == 0 ? shL : bb == A - 1 ? shR : shA), 0.f);
+        }
       }
 #pragma unroll
       for (int bb = 0; bb < A; ++bb) {     // B^T d along rows, in place
@@ -298,15 +317,14 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
       float rL[IT][P];
       f32x2 uL[ULR];
       f32x4 bL[UBR];
-      float pL[2];
-      load(0, rL, uL, bL, pL);
-      store(0, rL, uL, bL, pL);
-      if (nch > 1) load(KC, rL, uL, bL, pL);
+      load(0, rL, uL, bL);
+      store(0, rL, uL, bL, 0);
+      if (nch > 1) load(KC, rL, uL, bL);
       __syncthreads();
       for (int c = 0; c < nch; ++c) {
         if (c + 1 < nch) {
-          store((c + 1) & 1, rL, uL, bL, pL);  // chunk c + 1 (its loads were issued one chunk ago)
-          if (c + 2 < nch) load((c + 2) * KC, rL, uL, bL, pL);
+          store((c + 1) & 1, rL, uL, bL, (c + 1) * KC);  // chunk c + 1 (its loads were issued one chunk ago)
+          if (c + 2 < nch) load((c + 2) * KC, rL, uL, bL);
         }
         __syncthreads();
       }
@@ -364,22 +382,21 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
   float rA[IT][P];
   f32x2 uA[ULR];
   f32x4 bA[UBR];
-  float pA[2];
   if constexpr (WS) {
     for (int c = 0; c < nch; ++c) {        // compute waves: chunk c, then the barrier that publishes c + 1
       mfma(c & 1);
       __syncthreads();
     }
   } else if constexpr (NS == 1) {
-    load(0, rA, uA, bA, pA);
-    store(0, rA, uA, bA, pA);
+    load(0, rA, uA, bA);
+    store(0, rA, uA, bA, 0);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-      if (c + 1 < nch) load((c + 1) * KC, rA, uA, bA, pA);
+      if (c + 1 < nch) load((c + 1) * KC, rA, uA, bA);
       mfma(0);
       if (c + 1 < nch) {
         __syncthreads();                   // every wave is done reading the stage
-        store(0, rA, uA, bA, pA);
+        store(0, rA, uA, bA, (c + 1) * KC);
       }
       __syncthreads();
     }
@@ -387,19 +404,18 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
     float rB[IT][P];
     f32x2 uB[ULR];
     f32x4 bB[UBR];
-    float pB[2];
-    load(0, rA, uA, bA, pA);
-    load(KC, rB, uB, bB, pB);
-    store(0, rA, uA, bA, pA);
+    load(0, rA, uA, bA);
+    load(KC, rB, uB, bB);
+    store(0, rA, uA, bA, 0);
     __syncthreads();
     for (int c = 0; c < nch; c += 2) {
-      load((c + 2) * KC, rA, uA, bA, pA);
+      load((c + 2) * KC, rA, uA, bA);
       mfma(0);                             // chunk c
-      store(1, rB, uB, bB, pB);            // chunk c + 1, in the MFMAs' shadow
+      store(1, rB, uB, bB, (c + 1) * KC);  // chunk c + 1, in the MFMAs' shadow
       __syncthreads();
-      load((c + 3) * KC, rB, uB, bB, pB);
+      load((c + 3) * KC, rB, uB, bB);
       mfma(1);                             // chunk c + 1 (zeros past the end)
-      store(0, rA, uA, bA, pA);            // chunk c + 2
+      store(0, rA, uA, bA, (c + 2) * KC);  // chunk c + 2
       __syncthreads();
     }
   }
@@ -1132,7 +1148,7 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
   if (groups > 1 && (flags & (WF_STATS | WF_BNB | WF_BNP))) return RK_EUNSUPPORTED;
   if (PRO != (pro != nullptr)) return RK_EBADARG;
-  if (PRO && (groups > 1 || (flags & ~WF_STATS))) return RK_EUNSUPPORTED;
+  if (PRO && (groups > 1 || (flags & ~WF_STATS) || C > W4_PRO_MAXC)) return RK_EUNSUPPORTED;
   W4Params p;
   p.x = x; p.u = u; p.y = y; p.bias = bias; p.stats = stats; p.gate = gate;
   p.pro = pro;
