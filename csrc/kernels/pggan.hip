@@ -336,29 +336,31 @@ __global__ __launch_bounds__(256) void mbstd_h_kernel(const T* __restrict__ x, c
 // statistics and writes every member's output, one thread per (group, 8-channel vector).
 // part[J][chunk][2]: mode 0 {sum s, -}; mode 1 {sum gout[.., C], -}; mode 2 {G sum, H sum}.
 template <int G, class T>
-RK_DEV void mb_load(const T* __restrict__ base, const long long (&smp)[MB_MAXG], long long stride, long long off,
-                    int g, float (&v)[MB_MAXG][8]) {
+RK_DEV void mb_load(const T* __restrict__ base, const long long (&smp)[G], long long stride, long long off,
+                    int g, float (&v)[G][8]) {
 #pragma unroll
   for (int k = 0; k < G; ++k)
     if (k < g) ld8(base + smp[k] * stride + off, v[k]);
 }
 
-RK_DEV void mb_vstats(const float (&xv)[MB_MAXG][8], int g, float (&mu)[8], float (&rs)[8]) {
+template <int G>
+RK_DEV void mb_vstats(const float (&xv)[G][8], int g, float (&mu)[8], float (&rs)[8]) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     float m = 0.f;
 #pragma unroll
-    for (int k = 0; k < MB_MAXG; ++k) if (k < g) m += xv[k][c];
+    for (int k = 0; k < G; ++k) if (k < g) m += xv[k][c];
     m /= (float)g;
     float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < MB_MAXG; ++k) if (k < g) { const float d = xv[k][c] - m; v += d * d; }
+    for (int k = 0; k < G; ++k) if (k < g) { const float d = xv[k][c] - m; v += d * d; }
     mu[c] = m;
     rs[c] = rsqrtf(v / (float)g + 1e-8f);
   }
 }
 
-template <class T>
+// G: the compile-time group-size bound (4 for the usual group of 4: half the registers of G)
+template <int G, class T>
 __global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const T* __restrict__ x,
                                                           const T* __restrict__ a, const T* __restrict__ gout,
                                                           int N, int P, int C, int Cp, int g, int segs, int chunks,
@@ -366,24 +368,24 @@ __global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const T* __r
   __shared__ float red[4];
   const int J = blockIdx.x, ch = blockIdx.y;
   const int C8 = C >> 3, V = P * C8;
-  long long smp[MB_MAXG];
+  long long smp[G];
 #pragma unroll
-  for (int k = 0; k < MB_MAXG; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
+  for (int k = 0; k < G; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
   const int per = (V + chunks - 1) / chunks, v0 = ch * per, v1 = min(V, v0 + per);
   float s0 = 0.f, s1 = 0.f;
   if (mode != 1) {
     for (int v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-      float xv[MB_MAXG][8], mu[8], rs[8];
-      mb_load<MB_MAXG>(x, smp, (long long)P * C, (long long)v * 8, g, xv);
+      float xv[G][8], mu[8], rs[8];
+      mb_load<G>(x, smp, (long long)P * C, (long long)v * 8, g, xv);
       mb_vstats(xv, g, mu, rs);
       if (mode == 0) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) s0 += 1.0f / rs[c];
       } else {
-        float av[MB_MAXG][8];
-        mb_load<MB_MAXG>(a, smp, (long long)P * C, (long long)v * 8, g, av);
+        float av[G][8];
+        mb_load<G>(a, smp, (long long)P * C, (long long)v * 8, g, av);
 #pragma unroll
-        for (int k = 0; k < MB_MAXG; ++k)
+        for (int k = 0; k < G; ++k)
           if (k < g)
 #pragma unroll
             for (int c = 0; c < 8; ++c) s1 += av[k][c] * (xv[k][c] - mu[c]) * rs[c];
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const T* __r
       const int k = t / (p1 - p0), p = p0 + t - k * (p1 - p0);
       long long sk = 0;
 #pragma unroll
-      for (int q = 0; q < MB_MAXG; ++q) if (q == k) sk = smp[q];
+      for (int q = 0; q < G; ++q) if (q == k) sk = smp[q];
       s0 += (float)gout[(sk * P + p) * Cp + C];
     }
   }
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(256) void mbstd_vec_a_kernel(int mode, const T* __r
   }
 }
 
-template <class T>
+template <int G, class T>
 __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __restrict__ x,
                                                           const T* __restrict__ a, const T* __restrict__ gout,
                                                           int N, int P, int C, int Cp, int g, int segs, int chunks,
@@ -418,9 +420,9 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __r
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int J = (int)(t / V), v = (int)(t - (long long)J * V);
   if (J >= N / g) return;
-  long long smp[MB_MAXG];
+  long long smp[G];
 #pragma unroll
-  for (int k = 0; k < MB_MAXG; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
+  for (int k = 0; k < G; ++k) smp[k] = k < g ? mb_sample(J, k, N, g, segs) : 0;
   float S0 = 0.f, S1 = 0.f;
   for (int c = 0; c < chunks; ++c) {
     S0 += part[((long long)J * chunks + c) * 2];
@@ -429,11 +431,11 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __r
   const long long PC = (long long)P * C, PCp = (long long)P * Cp;
   const int p = v / C8, c8 = v - p * C8;
   const float inv = 1.0f / ((float)g * (float)PC);
-  float xv[MB_MAXG][8], mu[8], rs[8];
+  float xv[G][8], mu[8], rs[8];
   if (mode == 0) {
-    mb_load<MB_MAXG>(x, smp, PC, (long long)v * 8, g, xv);
+    mb_load<G>(x, smp, PC, (long long)v * 8, g, xv);
 #pragma unroll
-    for (int k = 0; k < MB_MAXG; ++k) {
+    for (int k = 0; k < G; ++k) {
       if (k >= g) break;
       st8(out + smp[k] * PCp + (long long)p * Cp + c8 * 8, xv[k]);
       if (c8 == 0) {
@@ -443,13 +445,13 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __r
     }
     return;
   }
-  mb_load<MB_MAXG>(x, smp, PC, (long long)v * 8, g, xv);
+  mb_load<G>(x, smp, PC, (long long)v * 8, g, xv);
   mb_vstats(xv, g, mu, rs);
   if (mode == 1) {
-    float go[MB_MAXG][8];
-    mb_load<MB_MAXG>(gout, smp, PCp, (long long)p * Cp + c8 * 8, g, go);
+    float go[G][8];
+    mb_load<G>(gout, smp, PCp, (long long)p * Cp + c8 * 8, g, go);
 #pragma unroll
-    for (int k = 0; k < MB_MAXG; ++k) {
+    for (int k = 0; k < G; ++k) {
       if (k >= g) break;
       float o[8];
 #pragma unroll
@@ -459,20 +461,20 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __r
     return;
   }
   // mode 2: g_x -> out, gg_out -> out2
-  float av[MB_MAXG][8];
-  mb_load<MB_MAXG>(a, smp, PC, (long long)v * 8, g, av);
+  float av[G][8];
+  mb_load<G>(a, smp, PC, (long long)v * 8, g, av);
   float m1[8], m2[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < MB_MAXG; ++k)
+    for (int k = 0; k < G; ++k)
       if (k < g) { s1 += av[k][c]; s2 += av[k][c] * (xv[k][c] - mu[c]) * rs[c]; }
     m1[c] = s1 / (float)g;
     m2[c] = s2 / (float)g;
   }
 #pragma unroll
-  for (int k = 0; k < MB_MAXG; ++k) {
+  for (int k = 0; k < G; ++k) {
     if (k >= g) break;
     float o[8];
 #pragma unroll
@@ -520,11 +522,19 @@ int mbstd_launch(int mode, const void* x, const void* a, const void* b, int N, i
     const int groups = N / g;
     const int chunks = std::max(1, std::min(16, 1024 / groups));
     const T* gout = (const T*)(mode == 1 ? a : b);
-    hipLaunchKernelGGL(mbstd_vec_a_kernel<T>, dim3(groups, chunks), block, 0, s, mode, (const T*)x, (const T*)a,
-                       gout, N, P, C, Cp, g, segs, chunks, part);
     const long long threads = (long long)groups * P * (C / 8);
-    hipLaunchKernelGGL(mbstd_vec_b_kernel<T>, dim3((unsigned)((threads + 255) / 256)), block, 0, s, mode,
-                       (const T*)x, (const T*)a, gout, N, P, C, Cp, g, segs, chunks, part, (T*)out, (T*)out2);
+    if (g <= 4) {
+      hipLaunchKernelGGL((mbstd_vec_a_kernel<4, T>), dim3(groups, chunks), block, 0, s, mode, (const T*)x,
+                         (const T*)a, gout, N, P, C, Cp, g, segs, chunks, part);
+      hipLaunchKernelGGL((mbstd_vec_b_kernel<4, T>), dim3((unsigned)((threads + 255) / 256)), block, 0, s, mode,
+                         (const T*)x, (const T*)a, gout, N, P, C, Cp, g, segs, chunks, part, (T*)out, (T*)out2);
+    } else {
+      hipLaunchKernelGGL((mbstd_vec_a_kernel<MB_MAXG, T>), dim3(groups, chunks), block, 0, s, mode, (const T*)x,
+                         (const T*)a, gout, N, P, C, Cp, g, segs, chunks, part);
+      hipLaunchKernelGGL((mbstd_vec_b_kernel<MB_MAXG, T>), dim3((unsigned)((threads + 255) / 256)), block, 0, s,
+                         mode, (const T*)x, (const T*)a, gout, N, P, C, Cp, g, segs, chunks, part, (T*)out,
+                         (T*)out2);
+    }
     RK_LAUNCH_CHECK();
     return RK_OK;
   }
@@ -632,9 +642,13 @@ extern "C" int rk_lrelu_gate_f32(const float* gy, const float* y, float* out, lo
   return RK_OK;
 }
 
+extern "C" int rk_lrelu_gate_colsum4_f32(const float* gy, const float* y, float* g, int R, int C, float slope,
+                                         float* part, int chunks, void* stream);   // bnf.hip (vectorised)
+
 extern "C" int rk_lrelu_gate_colsum_f32(const float* gy, const float* y, float* out, int R, int C, float slope,
                                         float* part, int chunks, void* stream) {
   if (R <= 0 || C <= 0 || chunks < 1) return RK_EBADARG;
+  if (rk_lrelu_gate_colsum4_f32(gy, y, out, R, C, slope, part, chunks, stream) == RK_OK) return RK_OK;
   hipLaunchKernelGGL(lrelu_gate_colsum_kernel, dim3(rk_cdiv(C, 64), chunks), dim3(256), 0, (hipStream_t)stream, gy, y,
                      out, R, C, slope, part);
   RK_LAUNCH_CHECK();

@@ -1255,11 +1255,13 @@ def lrelu_gate_colsum(gy: torch.Tensor, y: torch.Tensor, slope: float, acc=None)
     Cc = gy.shape[-1]
     R = gy.numel() // Cc
     g = torch.empty_like(gy)
-    chunks = max(1, min(cdiv(R, 256), cdiv(2 * NUM_CU, cdiv(Cc, 64))))
+    chunks = _colsum_chunks(R, Cc) if Cc % 4 == 0 else 1
     part = torch.empty((chunks, Cc), device=gy.device, dtype=torch.float32)
     _lib.call("rk_lrelu_gate_colsum_f32", _p(gy), _p(y), _p(g), R, Cc, float(slope), _p(part), chunks, _s())
     if acc is not None:
         assert acc.shape == (Cc,) and acc.dtype == torch.float32 and acc.is_contiguous()
+        if Cc % 4:   # odd width (the slab fold takes whole float4s)
+            return g, acc.add_(part.sum(0))
         return g, reduce_slabs(part, acc, accumulate=True)
     if chunks == 1:
         return g, part[0]
@@ -1267,16 +1269,26 @@ def lrelu_gate_colsum(gy: torch.Tensor, y: torch.Tensor, slope: float, acc=None)
     return g, reduce_slabs(part, out)
 
 
+def _colsum_chunks(R, Cc):
+    """Row chunks of the column-sum kernels: ~2 blocks per CU over the column blocks (256 columns per
+    block on the vectorised path, C % 4 == 0; 64 otherwise), >= 64 rows per chunk."""
+    cols = min(Cc // 4, 64) * 4 if Cc % 4 == 0 else 64
+    return max(1, min(cdiv(R, 64), cdiv(2 * NUM_CU, cdiv(Cc, cols))))
+
+
 def colsum(x2d, out, *, accumulate=False):
     """out[c] (+)= sum_r x2d[r, c] (fp32).  Tall inputs split the rows over ~2 blocks per CU, then fold
     the partial rows with reduce_slabs."""
     R, Cc = x2d.shape
-    chunks = max(1, min(cdiv(R, 256), cdiv(2 * NUM_CU, cdiv(Cc, 64))))
+    chunks = _colsum_chunks(R, Cc)
     if chunks == 1:
         _lib.call("rk_colsum_f32", _p(x2d), R, Cc, x2d.stride(0), _p(out), int(accumulate), 1, _s())
         return out
     part = torch.empty((chunks, Cc), device=x2d.device, dtype=torch.float32)
     _lib.call("rk_colsum_f32", _p(x2d), R, Cc, x2d.stride(0), _p(part), 0, chunks, _s())
+    if Cc % 4:   # the slab fold takes whole float4s; an odd width (not on the engines' padded paths) folds here
+        s = part.sum(0)
+        return out.add_(s) if accumulate else out.copy_(s)
     return reduce_slabs(part, out, accumulate=accumulate)
 
 

@@ -398,3 +398,35 @@ def test_grouped_conv_linear_bn_match_per_group(shared):
     for g in range(G):
         ref = torch.relu((xa if shared else xa[g]).double().cpu() @ wl[g].double().cpu().t() + bl[g].double().cpu())
         assert rel(o[g], ref) < 1e-5
+
+
+@pytest.mark.parametrize("R,C,ld", [(8192, 512, 512), (8192 + 37, 520, 520), (4099, 12, 16), (300, 3, 3),
+                                    (65536, 64, 64), (777, 1000, 1004), (5, 256, 256)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_colsum_vectorised_and_scalar_paths(R, C, ld, accumulate):
+    """bnf.hip column sums (bias gradients): the float4 kernel (C % 4 == 0, 16-B rows, row chunks + slab
+    fold) and the scalar one, strided rows, accumulate — vs fp64."""
+    from rafiki_amd.ops import f32 as S
+    g = torch.Generator().manual_seed(R + C)
+    full = torch.randn(R, ld, generator=g).to(DEV)
+    x = full[:, :C]
+    base = torch.randn(C, generator=g).to(DEV)
+    out = base.clone() if accumulate else torch.empty(C, device=DEV)
+    S.colsum(x, out, accumulate=accumulate)
+    ref = x.double().sum(0) + (base.double() if accumulate else 0)
+    assert rel(out, ref) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [(512, 4, 4, 512), (64, 8, 8, 256), (37, 3, 5, 12), (9, 7, 7, 3)])
+def test_lrelu_gate_colsum_vectorised(shape):
+    from rafiki_amd.ops import f32 as S
+    g = torch.Generator().manual_seed(sum(shape))
+    gy = torch.randn(*shape, generator=g).to(DEV)
+    y = torch.randn(*shape, generator=g).to(DEV)
+    ref = torch.where(y > 0, gy, gy * 0.2)
+    out, cs = S.lrelu_gate_colsum(gy, y, 0.2)
+    assert torch.equal(out, ref)
+    assert rel(cs, ref.reshape(-1, shape[-1]).double().sum(0)) < 1e-6
+    acc = torch.ones(shape[-1], device=DEV)
+    _, acc2 = S.lrelu_gate_colsum(gy, y, 0.2, acc=acc)
+    assert rel(acc2, ref.reshape(-1, shape[-1]).double().sum(0) + 1) < 1e-6
