@@ -544,7 +544,8 @@ BN_ON_LOAD = os.environ.get('RAFIKI_BN_ON_LOAD', '1') != '0'
 def bn_on_load_ok(Nb: int, H: int, W: int, Cin: int, Cout: int) -> bool:
     """Whether a 3x3 conv of Cin -> Cout channels on [Nb, H, W] can take its input as the previous conv's
     pre-BN output (conv_fwd(pro=...) with blocked F(4x4) weights, conv_wgrad(xpro=...))."""
-    return (BN_ON_LOAD and wino4_ok(H, W, Cin) and Cin % 4 == 0
+    # Cin <= 512: the fused forward stages the 2 x Cin coefficients in 4 KiB of LDS (W4_PRO_MAXC)
+    return (BN_ON_LOAD and wino4_ok(H, W, Cin) and Cin % 4 == 0 and Cin <= 512
             and bool(_wino4_wgrad_cands(Nb, H, W, Cout, Cin) or _wino4_pt_cands(Nb, H, W, Cout, Cin)))
 
 
