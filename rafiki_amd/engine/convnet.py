@@ -1013,6 +1013,15 @@ class GroupedConvNets:
             return torch.stack([fn(e) for e in self.engines]).contiguous()
         self.conv_w = [stack(lambda e, n=name: e.flat.w(n + '.w').reshape(e.flat.w(n + '.w').shape[0], -1))
                        for (name, _, _, _, _) in e0.blocks]
+        self.scale = [stack(lambda e, i=bi: e._eval_coeffs[i][2]) for bi in range(len(e0.blocks))]
+        self.shift = [stack(lambda e, i=bi: e._eval_coeffs[i][3]) for bi in range(len(e0.blocks))]
+        # non-pooled blocks: the eval BN folded into the conv (weights x scale per output channel, shift as
+        # the bias, ReLU in the conv epilogue) — no separate BN pass over the activation; a pooled block
+        # keeps its one BN + ReLU + 2x2 max pass
+        self.folded = [not b[3] for b in e0.blocks]
+        for bi in range(len(e0.blocks)):
+            if self.folded[bi]:
+                self.conv_w[bi] = (self.conv_w[bi] * self.scale[bi].unsqueeze(-1)).contiguous()
         # Winograd-domain weights [k, 16, Cout, Cin] of the 3x3 layers the fused kernel takes
         self.conv_u = [None] * len(e0.blocks)
         self.conv_u4 = [None] * len(e0.blocks)   # F(4x4) sets [k, 36, Cout, Cin] (maps in multiples of 4)
@@ -1023,8 +1032,6 @@ class GroupedConvNets:
                     self.conv_u[bi] = torch.stack([S.wino_u(w[g]) for g in range(self.k)]).contiguous()
                     if S.WINO4 and hw % 4 == 0:
                         self.conv_u4[bi] = torch.stack([S.wino4_u(w[g]) for g in range(self.k)]).contiguous()
-        self.scale = [stack(lambda e, i=bi: e._eval_coeffs[i][2]) for bi in range(len(e0.blocks))]
-        self.shift = [stack(lambda e, i=bi: e._eval_coeffs[i][3]) for bi in range(len(e0.blocks))]
         self.fc_w = [stack(lambda e, n=name: e.flat.w(n + '.w')) for (name, _, _, _) in e0.fcs]
         self.fc_b = [stack(lambda e, n=name: e.flat.w(n + '.b')) for (name, _, _, _) in e0.fcs]
         self.out_w = stack(lambda e: e.flat.w('out.w'))
@@ -1037,6 +1044,10 @@ class GroupedConvNets:
         B = x.shape[0]
         h = x
         for bi, (name, cin, cout, pool, hw) in enumerate(e0.blocks):
+            if self.folded[bi]:
+                h = S.conv_fwd_grp(h, self.conv_w[bi], bias=self.shift[bi], act=F.ACT_RELU, wino=self.conv_u[bi],
+                                   wino4=self.conv_u4[bi])
+                continue
             y = S.conv_fwd_grp(h, self.conv_w[bi], wino=self.conv_u[bi], wino4=self.conv_u4[bi])
             h = S.bn_eval_grp(y, self.scale[bi], self.shift[bi], pool=pool, act=F.ACT_RELU)
         z = h.reshape(k, B, e0.feat_dim)

@@ -430,3 +430,27 @@ def test_lrelu_gate_colsum_vectorised(shape):
     acc = torch.ones(shape[-1], device=DEV)
     _, acc2 = S.lrelu_gate_colsum(gy, y, 0.2, acc=acc)
     assert rel(acc2, ref.reshape(-1, shape[-1]).double().sum(0) + 1) < 1e-6
+
+
+def test_grouped_ensemble_with_folded_bn_matches_reference():
+    """BN engines: the grouped ensemble folds each non-pooled block's eval BN into its conv (weights x
+    scale, shift as the bias, ReLU epilogue) and keeps the pooled blocks' BN + ReLU + max pass — vs fp64
+    PyTorch eval and each engine's own (unfolded) eval forward."""
+    from rafiki_amd.engine.convnet import GroupedConvNets
+    engs = [_engine(image_size=16, cfg=(16, 16, 'M', 32, 32, 'M'), seed=s) for s in (3, 4, 5)]
+    x, y = _batch(64, seed=6)
+    for e in engs:
+        for _ in range(3):
+            e.train_step(x, y)
+        e.prepare_eval()
+    grp = GroupedConvNets(engs)
+    assert grp.folded == [True, False, True, False]
+    out = torch.empty((3, x.shape[0], 10), dtype=torch.float32, device=DEV)
+    grp.forward_into(x, out)
+    for g, e in enumerate(engs):
+        own = e.forward_eval(x)
+        _, ref_logits = e.reference_loss(x.double().cpu(), None, training=False,
+                                         params={n: e.flat.w(n).double().cpu() for n in e.flat.names()})
+        ref = torch.softmax(ref_logits, 1)
+        assert (out[g].double().cpu() - ref).abs().max().item() < 1e-5
+        assert (out[g] - own).abs().max().item() < 1e-5
