@@ -559,6 +559,7 @@ extern "C" int rk_wino_conv_grp(const float* x, const float* u, float* y, const 
                                 int variant, int groups, long long gx, long long gu, long long gy, long long gbias,
                                 void* stream) {
   if (variant != 0 && variant != 1) return RK_EBADARG;
+  if (flags & 2048) return RK_EUNSUPPORTED;   // WF_POOL: the winograd4.hip launcher's pooled epilogue only
   const int BNC = variant ? 64 : 32;
   if (Nb <= 0 || (H & 1) || (W & 1) || H <= 0 || W <= 0 || C <= 0 || (C % WKC) || N <= 0 || groups <= 0)
     return RK_EBADARG;

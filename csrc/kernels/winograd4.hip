@@ -38,7 +38,11 @@ namespace {
 #include "wino_wt.h"
 
 constexpr int KC = 8;     // input channels per K chunk
-enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_LRELU = 8, WF_BNB = 512, WF_BNP = 1024 };
+enum { WF_RELU = 1, WF_BIAS = 2, WF_STATS = 4, WF_LRELU = 8, WF_BNB = 512, WF_BNP = 1024, WF_POOL = 2048 };
+// WF_POOL (fused forward, with exactly WF_BIAS | WF_RELU): the 2x2 max-pool of relu(conv + bias) written
+// from the epilogue, y [Nb, H/2, W/2, N] — the serving network's pooled blocks with their eval BN folded
+// into the weights / bias (each 2x2 window lies inside one output tile)
+constexpr int WF_POOLED = WF_BIAS | WF_RELU | WF_POOL;
 
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
@@ -482,12 +486,29 @@ __global__ __launch_bounds__(64 * WM * WN * (WS ? 2 : 1), MINW) void wino_gfwd_k
     }
     if (tok && nok) {
       const int pix = (im * p.H + oy) * p.W + ox;
+      [[maybe_unused]] float pm[MO / 2];   // FL == WF_POOLED: row-pair maxima of the current column pair
 #pragma unroll
       for (int j = 0; j < MO; ++j) {
         float m[A], o[MO];                 // A^T (M A): along rows
 #pragma unroll
         for (int a = 0; a < A; ++a) m[a] = tt[a][j];
         at_line<MO>(m, o);
+        if constexpr (FL == WF_POOLED) {
+#pragma unroll
+          for (int k = 0; k < MO / 2; ++k) {
+            const float mx = fmaxf(fmaxf(o[2 * k] + bs, 0.f), fmaxf(o[2 * k + 1] + bs, 0.f));
+            pm[k] = (j & 1) ? fmaxf(pm[k], mx) : mx;
+          }
+          if (j & 1) {
+            const int H2 = p.H >> 1, W2 = p.W >> 1;
+#pragma unroll
+            for (int k = 0; k < MO / 2; ++k) {
+              const int pidx = ((im * H2 + (oy >> 1) + k) * W2 + (ox >> 1) + (j >> 1)) * p.N + n;
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, pm[k]), yr, pidx * 4, 0, 0);
+            }
+          }
+          continue;
+        }
 #pragma unroll
         for (int i = 0; i < MO; ++i) {
           float v = o[i];
@@ -1148,6 +1169,7 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   if ((flags & WF_BIAS) && !bias) return RK_EBADARG;
   if (groups > 1 && (flags & (WF_STATS | WF_BNB | WF_BNP))) return RK_EUNSUPPORTED;
   if (PRO != (pro != nullptr)) return RK_EBADARG;
+  if ((flags & WF_POOL) && (flags != WF_POOLED || PRO || (H & 1) || (W & 1))) return RK_EUNSUPPORTED;
   if (PRO && (groups > 1 || (flags & ~WF_STATS) || C > W4_PRO_MAXC)) return RK_EUNSUPPORTED;
   W4Params p;
   p.x = x; p.u = u; p.y = y; p.bias = bias; p.stats = stats; p.gate = gate;
@@ -1161,7 +1183,7 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
   p.ncb = rk_cdiv(N, BNC);
   p.xbytes = 4ull * Nb * H * W * C;
   p.ubytes = UB ? 4ull * P * rk_cdiv(N, 32) * 32 * C : 4ull * P * N * C;
-  p.ybytes = 4ull * Nb * H * W * N;
+  p.ybytes = (flags & WF_POOL) ? 4ull * Nb * (H / 2) * (W / 2) * N : 4ull * Nb * H * W * N;
   const unsigned long long gbytes = (flags & WF_BNP) ? 4 * p.ybytes : p.ybytes;
   if (p.xbytes >= 0x7fffffffull || p.ubytes >= 0x7fffffffull || gbytes >= 0x7fffffffull) return RK_EUNSUPPORTED;
   p.slotMask = slotMask;
@@ -1190,6 +1212,9 @@ int launch_gfwd(const float* x, const float* u, float* y, const float* bias, dou
     case WF_BNP: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BNP, NS, UB, WS>), grid, block, 0, st, p); break;
     case WF_BIAS | WF_RELU:
       hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_BIAS | WF_RELU, NS, UB, WS>), grid, block, 0, st, p);
+      break;
+    case WF_POOLED:
+      hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, WF_POOLED, NS, UB, WS>), grid, block, 0, st, p);
       break;
     default: hipLaunchKernelGGL((wino_gfwd_kernel<MO, WM, WN, MINW, -1, NS, UB, WS>), grid, block, 0, st, p); break;
   }

@@ -433,7 +433,7 @@ class SConvWT:
 
 
 # -------------------------------------------------------------------- Winograd F(2x2, 3x3) convs
-WF_RELU, WF_BIAS, WF_STATS, WF_LRELU, WF_BNB, WF_BNP = 1, 2, 4, 8, 512, 1024
+WF_RELU, WF_BIAS, WF_STATS, WF_LRELU, WF_BNB, WF_BNP, WF_POOL = 1, 2, 4, 8, 512, 1024, 2048
 WINO = os.environ.get('RAFIKI_WINOGRAD', '1') != '0'
 # autotune candidates that run rk_wino_conv: 4-wave 64x32 tiles (variant 0) / 8-wave 64x64 (variant 1),
 # and the 16x16-wave-tile kernels of winograd4.hip: 4-wave 32x32 (variant 2), 2-wave 16x32 (variant 3),
@@ -719,18 +719,25 @@ def wino4_conv_pt(x: torch.Tensor, u: torch.Tensor, *, out=None, bias=None, stat
     return out
 
 
-def wino4_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
-    """k F(4x4) convs in one grid: x [G, Nb, H, W, C] (or shared [Nb, H, W, C]), u [G, 36, N, C]."""
+def wino4_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0, pool=False):
+    """k F(4x4) convs in one grid: x [G, Nb, H, W, C] (or shared [Nb, H, W, C]), u [G, 36, N, C].
+    ``pool`` (with bias + relu): the 2x2 max-pool from the epilogue, out [G, Nb, H/2, W/2, N]."""
     G, _, N, C = u.shape
     shared = x.dim() == 4
     Nb, H, W, Cx = x.shape[-4:]
     assert Cx == C and (shared or x.shape[0] == G) and u.is_contiguous() and x.is_contiguous()
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
     if out is None:
-        out = torch.empty((G, Nb, H, W, N), device=x.device, dtype=torch.float32)
+        out = torch.empty((G, Nb, Ho, Wo, N), device=x.device, dtype=torch.float32)
+    assert out.shape == (G, Nb, Ho, Wo, N) and out.is_contiguous()
     M = Nb * H * W
     flags = (WF_BIAS if bias is not None else 0) | (WF_RELU if relu else 0)
+    if pool:
+        assert bias is not None and relu
+        flags |= WF_POOL
     _lib.call("rk_wino4_conv_grp", _p(x), _p(u), _p(out), _p(bias), None, 0, None, Nb, H, W, C, N, flags,
-              int(variant), G, 0 if shared else M * C, 36 * N * C, M * N, N if bias is not None else 0, _s())
+              int(variant), G, 0 if shared else M * C, 36 * N * C, Nb * Ho * Wo * N, N if bias is not None else 0,
+              _s())
     return out
 
 
@@ -963,20 +970,26 @@ def wino_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, *, splits=1
     return out
 
 
-def wino_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0):
+def wino_conv_grp(x, u, *, out=None, bias=None, relu=False, variant=0, pool=False):
     """k Winograd convs in one grid: x [G, Nb, H, W, C] (or [Nb, H, W, C] shared), u [G, 16, N, C],
-    bias [G, N] -> out [G, Nb, H, W, N]."""
+    bias [G, N] -> out [G, Nb, H, W, N].  ``pool`` (with bias + relu, variants >= 2): the 2x2 max-pool of
+    the output from the epilogue, out [G, Nb, H/2, W/2, N]."""
     G, _, N, C = u.shape
     shared = x.dim() == 4
     Nb, H, W, Cx = x.shape[-4:]
     assert Cx == C and (shared or x.shape[0] == G) and u.is_contiguous() and x.is_contiguous()
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
     if out is None:
-        out = torch.empty((G, Nb, H, W, N), device=x.device, dtype=torch.float32)
+        out = torch.empty((G, Nb, Ho, Wo, N), device=x.device, dtype=torch.float32)
+    assert out.shape == (G, Nb, Ho, Wo, N) and out.is_contiguous()
     M = Nb * H * W
     flags = (WF_BIAS if bias is not None else 0) | (WF_RELU if relu else 0)
+    if pool:
+        assert bias is not None and relu and variant >= 2 and H % 2 == 0 and W % 2 == 0
+        flags |= WF_POOL
     name, v = ("rk_wino2s_conv_grp", int(variant) - 2) if variant >= 2 else ("rk_wino_conv_grp", int(variant))
     _lib.call(name, _p(x), _p(u), _p(out), _p(bias), None, 0, None, Nb, H, W, C, N, flags,
-              v, G, 0 if shared else M * C, 16 * N * C, M * N, N if bias is not None else 0, _s())
+              v, G, 0 if shared else M * C, 16 * N * C, Nb * Ho * Wo * N, N if bias is not None else 0, _s())
     return out
 
 
@@ -1643,11 +1656,19 @@ def _grp_run(kind, A, B, out, M, N, K, lda, ldb, G, gsa, key, *, bias=None, act=
     return out
 
 
-def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=None, wino4=None):
+def conv_fwd_grp_pool_ok(H, W, Cin, wino, wino4):
+    """conv_fwd_grp(pool=True) has a fused candidate for this shape (F(4x4) or the small-tile F(2x2))."""
+    return ((wino4 is not None and wino4_ok(H, W, Cin))
+            or (wino is not None and wino_ok(H, W, Cin) and any(_wino_variant(c) >= 2 for c in WINO_CFGS)))
+
+
+def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=None, wino4=None, pool=False):
     """k convs in one launch: x [G, Nb, H, W, Cin] (or [Nb, H, W, Cin] shared by every group),
     W [G, Cout, taps*Cin], bias [G, Cout] -> [G, Nb, H, W, Cout] (3x3 stride-1 or 1x1).
     ``wino``: stacked Winograd weights [G, 16, Cout, Cin] -> grouped fused F(2x2,3x3) candidates;
-    ``wino4``: [G, 36, Cout, Cin] -> grouped F(4x4,3x3) candidates."""
+    ``wino4``: [G, 36, Cout, Cin] -> grouped F(4x4,3x3) candidates.  ``pool`` (bias + ReLU): the 2x2
+    max-pool written by the fused kernels' epilogue -> [G, Nb, H/2, W/2, Cout] (only they are candidates;
+    see conv_fwd_grp_pool_ok)."""
     G, Cout, K = W.shape
     shared = x.dim() == 4
     Nb, H, Wd, Cin = x.shape[-4:]
@@ -1655,6 +1676,8 @@ def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=Non
     assert taps in (1, 9) and K == taps * Cin and (shared or x.shape[0] == G), (x.shape, W.shape)
     _check(x, 'conv_fwd_grp x')
     M = Nb * H * Wd
+    if pool:
+        return _conv_fwd_grp_pooled(x, W, bias, act, out, wino, wino4)
     if out is None:
         out = torch.empty((G, Nb, H, Wd, Cout), device=x.device, dtype=torch.float32)
     extra = None
@@ -1673,6 +1696,27 @@ def conv_fwd_grp(x, W, *, bias=None, act=ACT_NONE, slope=0.2, out=None, wino=Non
     return _grp_run(0, x, W, out, M, Cout, K, Cin, K, G, 0 if shared else M * Cin,
                     ('sfg', G, M, Cout, K, H, Wd, Cin, shared, bias is not None, act, w2, w4), bias=bias,
                     act=act, slope=slope, geo=dict(H=H, W=Wd, C=Cin, taps=taps), extra=extra)
+
+
+def _conv_fwd_grp_pooled(x, W, bias, act, out, wino, wino4):
+    G, Cout, K = W.shape
+    Nb, H, Wd, Cin = x.shape[-4:]
+    assert bias is not None and act == ACT_RELU and K == 9 * Cin and H % 2 == 0 and Wd % 2 == 0
+    if out is None:
+        out = torch.empty((G, Nb, H // 2, Wd // 2, Cout), device=x.device, dtype=torch.float32)
+    w4 = wino4 is not None and wino4_ok(H, Wd, Cin)
+    w2 = wino is not None and wino_ok(H, Wd, Cin)
+    cands = ([c for c in WINO4_CFGS] if w4 else []) + ([c for c in WINO_CFGS if _wino_variant(c) >= 2] if w2 else [])
+    if not cands:
+        raise ValueError('conv_fwd_grp(pool=True): no fused candidate (see conv_fwd_grp_pool_ok)')
+
+    def run(cfg):
+        if cfg in WINO4_CFGS:
+            wino4_conv_grp(x, wino4, out=out, bias=bias, relu=True, variant=_wino4_variant(cfg), pool=True)
+        else:
+            wino_conv_grp(x, wino, out=out, bias=bias, relu=True, variant=_wino_variant(cfg), pool=True)
+    run(_pick(('sfgp', G, Nb * H * Wd, Cout, K, H, Wd, Cin, x.dim() == 4, w2, w4), cands, run))
+    return out
 
 
 def linear_grp(x, w, bias=None, *, act=ACT_NONE, slope=0.2, out=None):

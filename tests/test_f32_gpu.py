@@ -433,9 +433,9 @@ def test_lrelu_gate_colsum_vectorised(shape):
 
 
 def test_grouped_ensemble_with_folded_bn_matches_reference():
-    """BN engines: the grouped ensemble folds each non-pooled block's eval BN into its conv (weights x
-    scale, shift as the bias, ReLU epilogue) and keeps the pooled blocks' BN + ReLU + max pass — vs fp64
-    PyTorch eval and each engine's own (unfolded) eval forward."""
+    """BN engines: the grouped ensemble folds every block's eval BN into its conv (weights x scale, shift
+    as the bias, ReLU epilogue; pooled blocks with the 2x2 max-pool written by the fused kernel's
+    epilogue) — vs fp64 PyTorch eval and each engine's own (unfolded) eval forward."""
     from rafiki_amd.engine.convnet import GroupedConvNets
     engs = [_engine(image_size=16, cfg=(16, 16, 'M', 32, 32, 'M'), seed=s) for s in (3, 4, 5)]
     x, y = _batch(64, seed=6)
@@ -444,9 +444,13 @@ def test_grouped_ensemble_with_folded_bn_matches_reference():
             e.train_step(x, y)
         e.prepare_eval()
     grp = GroupedConvNets(engs)
-    assert grp.folded == [True, False, True, False]
+    assert grp.folded == [True, True, True, True]   # the pooled blocks through the pooled epilogue
     out = torch.empty((3, x.shape[0], 10), dtype=torch.float32, device=DEV)
     grp.forward_into(x, out)
+    small = torch.empty((3, 4, 10), dtype=torch.float32, device=DEV)
+    grp.forward_into(x[:4].contiguous(), small)   # below POOL_EPILOGUE_MIN_PIXELS: conv + ReLU / max pass
+    assert 4 * 16 * 16 < grp.POOL_EPILOGUE_MIN_PIXELS <= 64 * 8 * 8
+    assert (small - out[:, :4]).abs().max().item() < 1e-5
     for g, e in enumerate(engs):
         own = e.forward_eval(x)
         _, ref_logits = e.reference_loss(x.double().cpu(), None, training=False,
@@ -454,3 +458,31 @@ def test_grouped_ensemble_with_folded_bn_matches_reference():
         ref = torch.softmax(ref_logits, 1)
         assert (out[g].double().cpu() - ref).abs().max().item() < 1e-5
         assert (out[g] - own).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("H,Cin,Cout", [(16, 16, 32), (8, 64, 64), (4, 128, 96), (12, 24, 40)])
+@pytest.mark.parametrize("kind,variant", [('w4', 0), ('w4', 1), ('w4', 2), ('w2', 2), ('w2', 3), ('w2', 4),
+                                          ('w2', 5)])
+def test_grouped_winograd_pooled_epilogue(H, Cin, Cout, kind, variant):
+    """rk_wino4_conv_grp / rk_wino2s_conv_grp with WF_POOL: maxpool2(relu(conv + bias)) from the epilogue
+    == the same kernel unpooled then pooled by PyTorch (bitwise), and vs fp64."""
+    from rafiki_amd.ops import f32 as S
+    if kind == 'w4' and H % 4:
+        pytest.skip('F(4x4) maps in multiples of 4')
+    G, Nb = 3, 5
+    g = torch.Generator().manual_seed(H * 1000 + Cin)
+    x = torch.randn(G, Nb, H, H, Cin, generator=g).to(DEV)
+    w = (torch.randn(G, Cout, 3, 3, Cin, generator=g) / math.sqrt(9 * Cin)).to(DEV)
+    b = (torch.randn(G, Cout, generator=g) * 0.1).to(DEV)
+    fn = S.wino4_u if kind == 'w4' else S.wino_u
+    u = torch.stack([fn(w[k].reshape(Cout, -1).contiguous()) for k in range(G)]).contiguous()
+    conv = S.wino4_conv_grp if kind == 'w4' else S.wino_conv_grp
+    full = conv(x, u, bias=b, relu=True, variant=variant)
+    pooled = conv(x, u, bias=b, relu=True, variant=variant, pool=True)
+    torch.cuda.synchronize()
+    ref = TF.max_pool2d(full.reshape(G * Nb, H, H, Cout).permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    assert torch.equal(pooled.reshape(G * Nb, H // 2, H // 2, Cout), ref)
+    r64 = torch.stack([TF.conv2d(x[k].double().permute(0, 3, 1, 2), w[k].double().permute(0, 3, 1, 2),
+                                 b[k].double(), padding=1) for k in range(G)])
+    r64 = TF.max_pool2d(torch.relu(r64).reshape(G * Nb, Cout, H, H), 2).permute(0, 2, 3, 1)
+    assert rel(pooled.reshape(G * Nb, H // 2, H // 2, Cout), r64) < 3e-5
