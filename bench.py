@@ -25,8 +25,17 @@ Every part of it is measured in this run, none extrapolated:
            and the host-array API path); then POST /predict through the native HTTP front end under
            64 closed-loop JSON clients and 8 .npy batch-128 clients from a separate load-generator
            process (``ensemble_http_qps`` with p50 / p99, rafiki_amd/predictor/loadgen.py).
+  phase 4  the other BASELINE.json configs (rafiki_amd/utils/benchmarks.py), each with its own config and
+           dtype in the JSON (``baseline_configs``):
+             #5 PG-GAN train rounds, reference architecture, fp32, graphed: lod 3 (4x4, mb 512, the
+                reference's total_kimg=2 schedule) and lod 0 (32x32, mb 64, whole network).  N = 1:
+                in-process; N > 1: rank 0 starts N fresh ranks (their own RCCL group, bounded by a
+                timeout) running the DATA-PARALLEL round over all N GPUs (global minibatch split, bucketed
+                all-reduce overlapped with the graphed backward) while the bench's ranks wait;
+             #2 FeedForward (TfFeedForward-style MLP) trial on 1 GPU (N = 1 only);
+             #1 SkDt random-search trials on the CPU (N = 1 only).
 
-``python bench.py`` defaults to 1 GPU and finishes in about a minute.
+``python bench.py`` defaults to 1 GPU and finishes in a few minutes.
 """
 from __future__ import annotations
 
@@ -63,6 +72,9 @@ def parse():
     ap.add_argument('--trials', type=int, default=2, help='timed VggSmallTrial trials per GPU in phase 2 (0: skip)')
     ap.add_argument('--probe-trials', type=int, default=4, help='timed overhead-probe trials per GPU (0: skip)')
     ap.add_argument('--no-serving', action='store_true', help='skip phase 3')
+    ap.add_argument('--configs', default='auto',
+                    help="phase 4: comma list of pggan,mlp,skdt (auto: all at N = 1, pggan at N > 1; none: skip)")
+    ap.add_argument('--skdt-trials', type=int, default=3)
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--dtype', default=os.environ.get('RAFIKI_DTYPE', 'fp32'), choices=('fp32', 'bf16'),
@@ -294,6 +306,62 @@ def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30, http_seconds=3.0):
     return out
 
 
+def _configs(args, world):
+    if args.configs == 'none':
+        return []
+    if args.configs == 'auto':
+        return ['pggan', 'mlp', 'skdt'] if world == 1 else ['pggan']
+    return [c for c in args.configs.split(',') if c]
+
+
+def phase_pg_gan(args, info, dev):
+    """BASELINE #5 (see the module docstring).  Returns the phase's JSON dict (or an error record)."""
+    from rafiki_amd.utils.benchmarks import pg_gan_rounds
+    if info.world_size == 1:
+        try:
+            return pg_gan_rounds(dev, lods=(3.0, 0.0), steps=20, warmup=3, dtype='fp32')
+        except Exception as e:   # the other phases' numbers stand; say why this one is missing
+            return {'error': '{}: {}'.format(type(e).__name__, e)[:300]}
+    # N > 1: N fresh ranks (own process group) so a hung collective is bounded by the spawn timeout and
+    # the bench's own ranks are untouched; they wait on the rendezvous store, not in a collective
+    import io
+    from torch.distributed import distributed_c10d as c10d
+
+    from rafiki_amd.parallel import launch as L
+    store = c10d._get_default_store()
+    key = 'rafiki/bench/pggan_dp_done'
+    res = None
+    if info.is_main:
+        buf = io.StringIO()
+        timeout = float(os.environ.get('RAFIKI_BENCH_PGGAN_DP_TIMEOUT_S', '420'))
+        t0 = time.perf_counter()
+        rc = L.spawn([sys.executable, '-u', os.path.join(ROOT, 'scripts', 'bench_pg_gan.py'), '--lods', '3,0',
+                      '--steps', '20', '--warmup', '3'], info.world_size, out=buf, timeout_s=timeout)
+        lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith('{')]
+        res = json.loads(lines[-1]) if (rc == 0 and lines) else {'error': 'rc={} after {:.0f} s'.format(
+            rc, time.perf_counter() - t0), 'tail': buf.getvalue()[-500:]}
+        store.set(key, '1')
+    else:
+        store.wait([key], __import__('datetime').timedelta(seconds=900))
+    return res
+
+
+def phase_small_configs(args, dev, which):
+    from rafiki_amd.utils.benchmarks import mlp_trial, skdt_trials
+    out = {}
+    if 'mlp' in which:
+        try:
+            out['mlp'] = mlp_trial(dev)
+        except Exception as e:
+            out['mlp'] = {'error': '{}: {}'.format(type(e).__name__, e)[:300]}
+    if 'skdt' in which and args.skdt_trials > 0:
+        try:
+            out['skdt'] = skdt_trials(trials=args.skdt_trials)
+        except Exception as e:
+            out['skdt'] = {'error': '{}: {}'.format(type(e).__name__, e)[:300]}
+    return out
+
+
 def main():
     args = parse()
     from rafiki_amd.config import NodeConfig
@@ -349,6 +417,14 @@ def main():
     src = probe or trials
     if src is not None and info.is_main and not args.no_serving:
         serving = phase_serving(src['db'], src['sub'], dev)
+
+    which = _configs(args, world)
+    cfgs = {}
+    if 'pggan' in which and n_devices == world:
+        D.barrier(info)
+        cfgs['pg_gan'] = phase_pg_gan(args, info, dev)
+    if info.is_main and world == 1:
+        cfgs.update(phase_small_configs(args, dev, which))
 
     if info.is_main:
         out = {
@@ -418,6 +494,16 @@ def main():
                 out['ensemble_http_p50_ms'], out['ensemble_http_p99_ms'] = js['p50_ms'], js['p99_ms']
                 out['ensemble_http_npy_b128_qps'] = nb.get('qps')
             out['ensemble'] = serving
+        if cfgs:
+            pg = cfgs.get('pg_gan') or {}
+            for lod, k in (('3.0', 'pg_gan_lod3_img_s'), ('0.0', 'pg_gan_lod0_img_s')):
+                if lod in pg.get('lods', {}):
+                    out[k] = pg['lods'][lod]['images_per_sec']
+            if 'value' in cfgs.get('mlp', {}):
+                out['mlp_img_s'] = cfgs['mlp']['value']
+            if 'value' in cfgs.get('skdt', {}):
+                out['skdt_trials_per_hour'] = cfgs['skdt']['value']
+            out['baseline_configs'] = cfgs
         print(json.dumps(out), flush=True)
     D.destroy(info)
 

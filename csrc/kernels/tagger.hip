@@ -50,12 +50,12 @@ __global__ __launch_bounds__(256) void tag_embed_bwd_kernel(const int* __restric
                                                             const int* __restrict__ start, const int* __restrict__ nruns,
                                                             const float* __restrict__ dy,
                                                             const float* __restrict__ mask, float* __restrict__ dw,
-                                                            int maxruns, int E) {
+                                                            int maxruns, int E, int V) {
   const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (u >= maxruns || u >= nruns[0]) return;
   const long long v = uniq[u];
-  if (v < 0) return;                 // the padding id's run: no gradient
+  if (v < 0 || v >= V) return;       // the padding id's run (and, like the forward's clamp, any id out of range)
   const int k0 = start[u], k1 = start[u + 1];
   for (int c = lane; c < E; c += 64) {
     float s = 0.f;
@@ -108,11 +108,11 @@ extern "C" int rk_tag_embed_fwd(const int* ids, const float* w, float* out, floa
 
 // dW rows of the runs (uniq, start [maxruns + 1], nruns on the device); mask nullable (no dropout)
 extern "C" int rk_tag_embed_bwd(const int* perm, const int* uniq, const int* start, const int* nruns, const float* dy,
-                                const float* mask, float* dw, int maxruns, int E, void* stream) {
+                                const float* mask, float* dw, int maxruns, int E, int V, void* stream) {
   if (maxruns <= 0) return RK_OK;
-  if (E <= 0) return RK_EBADARG;
+  if (E <= 0 || V <= 0) return RK_EBADARG;
   hipLaunchKernelGGL(tag_embed_bwd_kernel, dim3((unsigned)((maxruns + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                     perm, uniq, start, nruns, dy, mask, dw, maxruns, E);
+                     perm, uniq, start, nruns, dy, mask, dw, maxruns, E, V);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -67,6 +67,12 @@ constexpr unsigned OOB = 0x80000000u;
 constexpr int W4_PRO_MAXC = 512;   // normalise-on-load: input channels whose BN coefficients are staged in LDS
 
 RK_DEV int swz(int row) { return ((row >> 2) & 3) << 1; }
+// the weight-gradient kernels' column swizzle: a wave stores 32 rows (channels) x 2 tiles, so the four rows
+// of each bank group (r, r + 8, r + 16, r + 24) take four different even offsets and the two tiles fill the
+// odd ones (conflict-free ds_write_b32; swz left those rows pairwise equal: 2-way, 21.8 % of the LDS cycles
+// in profiles/vgg_small_f32_step_pmc_r5.txt); the 16-row fragment reads stay conflict-free (rows r and
+// r + 8 differ by 4 in the offset)
+RK_DEV int swzw(int row) { return (((row >> 3) & 1) << 2) | (((row >> 4) & 1) << 1); }
 
 RK_DEV __amdgpu_buffer_rsrc_t rsrc(const float* base, unsigned long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)(unsigned)bytes, 0x00020000);
@@ -697,7 +703,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
     const bool yact = YALL || threadIdx.x < BCO * KC, xact = XALL || threadIdx.x < BCI * KC;
 #pragma unroll
     for (int h = 0; h < PY && yact; ++h) {
-      const int row = ch + NT / 8 * h, c = tt ^ swz(row);
+      const int row = ch + NT / 8 * h, c = tt ^ swzw(row);
       float m[6][4];                       // A dY: along rows
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -716,7 +722,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
     }
 #pragma unroll
     for (int h = 0; h < PX && xact; ++h) {
-      const int row = ch + NT / 8 * h, c = tt ^ swz(row);
+      const int row = ch + NT / 8 * h, c = tt ^ swzw(row);
       float* const r = raw[h];
       if (p.xpro) {                         // BN + ReLU of x's producer on the in-image elements
 #pragma unroll
@@ -753,7 +759,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   }
   __syncthreads();
   const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
-  const int ka = (2 * (lane >> 4)) ^ swz(ar), kb = (2 * (lane >> 4)) ^ swz(br);
+  const int ka = (2 * (lane >> 4)) ^ swzw(ar), kb = (2 * (lane >> 4)) ^ swzw(br);
   for (int c = 0; c < nch; ++c) {
     if (c + 1 < nch) load(c + 1);
 #pragma unroll
@@ -871,7 +877,7 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
       }
     }
   };
-  const int srow = ch, scol = tt ^ swz(ch);
+  const int srow = ch, scol = tt ^ swzw(ch);
   auto store = [&](int st, const float (&gy)[16], float (&raw)[36]) {
     float m[6][4];
 #pragma unroll
@@ -908,7 +914,7 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
 #pragma unroll
   for (int q = 0; q < 36; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
-  const int ka = (2 * (lane >> 4)) ^ swz(ar), kb = (2 * (lane >> 4)) ^ swz(br);
+  const int ka = (2 * (lane >> 4)) ^ swzw(ar), kb = (2 * (lane >> 4)) ^ swzw(br);
   auto mfma = [&](int st) {
 #pragma unroll
     for (int q = 0; q < 36; q += 4) {

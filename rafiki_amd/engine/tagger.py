@@ -27,6 +27,8 @@ fresh masks.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import numpy as np
 import torch
 
@@ -43,15 +45,18 @@ def _cdiv(a: int, b: int) -> int:
     return -(-a // b)
 
 
-def pack_batch(x_bl: np.ndarray, y_bl, padding_idx: int = 0) -> np.ndarray:
+def pack_batch(x_bl: np.ndarray, y_bl, padding_idx: int = 0, vocab: Optional[int] = None) -> np.ndarray:
     """One batch as the int32 words the step reads: x_bl / y_bl are [B, L] (batch-first, like the
     reference's batches; labels IGNORE where no token).  Layout, with n = L*B tokens in time-major
     order (t, b): [ids n | labels n | perm n | run ids n | run starts n+1 | #runs | 1/#labelled as
     float bits].  perm is the stable argsort of the ids; run u covers perm[start[u]:start[u+1]] and
-    has id uniq[u] (-1 for the padding id: no gradient)."""
+    has id uniq[u] (-1 for the padding id: no gradient).  With ``vocab``, ids outside [0, vocab) become
+    the padding id, as the forward's gather treats them (no gradient row is written for them)."""
     B, L = x_bl.shape
     n = B * L
     ids = np.ascontiguousarray(x_bl.T, dtype=np.int32).reshape(-1)
+    if vocab is not None:
+        ids = np.where((ids < 0) | (ids >= vocab), np.int32(padding_idx), ids)
     if y_bl is None:
         labels = np.full(n, IGNORE, np.int32)
     else:
@@ -210,7 +215,7 @@ class TaggerEngine:
         g_emb = self.seg(G, 'emb')
         _lib.call("rk_zero32", _p(g_emb), g_emb.numel(), s)
         _lib.call("rk_tag_embed_bwd", _p(perm), _p(uniq), _p(starts), _p(nruns), _p(gx), _p(mask), _p(g_emb), n, EP,
-                  s)
+                  self.V, s)
         if update:
             b1, b2 = self.betas
             _lib.call("rk_adam_step", _p(self.w), None, _p(self.g), _p(self.m), _p(self.v), self.numel, self.lr, b1, b2,
@@ -240,7 +245,7 @@ class TaggerEngine:
         """One training step on a batch-first [B, L] batch (ids int, labels IGNORE-padded)."""
         B, L = x_bl.shape
         key = (L, B)
-        ib = self._upload(pack_batch(x_bl, y_bl, self.padding_idx), key)
+        ib = self._upload(pack_batch(x_bl, y_bl, self.padding_idx, self.V), key)
         g = self._graphs.get(key) if graph and update else None
         if g is not None:
             g.replay()

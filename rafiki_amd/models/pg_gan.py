@@ -476,11 +476,13 @@ class GraphedRounds:
         self.seen.clear()
 
     def run_segments(self, key, segs):
-        """A round as a list of ('g', fn) compute segments and ('e', fn) eager collective segments
-        (data-parallel rounds: gradients -> all-reduce -> optimizer).  Each compute segment becomes its
-        own graph (one memory pool per key, segments replayed in capture order); the collectives run
-        eagerly between replays, so no collective is ever inside a capture and the process group's
-        watchdog has nothing of ours to race (no sleep, deterministic)."""
+        """A round as a list of ('g', fn) compute segments, ('s', BucketedGrads) gradient segments and
+        ('e', fn) eager collective segments (data-parallel rounds: gradients -> all-reduce -> optimizer).
+        Each compute segment becomes its own graph; a gradient segment becomes a SEQUENCE of graphs
+        cut where a gradient bucket completes, and its bucket all-reduces are launched eagerly between
+        their replays, so they run on RCCL's stream while the rest of the backward replays (one memory
+        pool per key, everything replayed in capture order).  No collective is ever inside a capture
+        and the process group's watchdog has nothing of ours to race (no sleep, deterministic)."""
         if not self.enabled:
             for _, fn in segs:
                 fn()
@@ -488,7 +490,9 @@ class GraphedRounds:
         gs = self.graphs.get(key)
         if gs is not None:
             for (kind, fn), g in zip(segs, gs):
-                if g is None:
+                if kind == 's':
+                    fn.replay(g)
+                elif g is None:
                     fn()
                 else:
                     g.replay()
@@ -505,6 +509,12 @@ class GraphedRounds:
             if kind == 'e':
                 fn()
                 gs.append(None)
+                continue
+            if kind == 's':
+                parts = fn.capture(pool)
+                fn.replay(parts)   # a capture records, it does not execute: run it (and its reduces) now
+                gs.append(parts)
+                self.captures += len(parts)
                 continue
             g = torch.cuda.CUDAGraph()
             with _capture(g, pool=pool):
@@ -851,11 +861,12 @@ class PgGan(BaseModel):
 
     def round_segments(self, lod, mb, level, labels_all, rng, G_opt, D_opt, acc, *, D_repeats=1, G_smoothing=0.99,
                        d_ar=None, g_ar=None, tag=None):
-        """train_round as segments for GraphedRounds.run_segments: per D step gradients ('g'), the
-        bucketed all-reduce of D.grad ('e'), then mean + finite guard + Adam + Gs EMA ('g'); likewise
-        the G step.  Adjacent compute segments are merged (D_repeats + 2 graphs per round).  The
-        all-reduce segments come from FlatGradAllReduce.traced: each reduces only the buckets the
-        segment's backward wrote (untouched blocks above the current LOD are skipped exactly).
+        """train_round as segments for GraphedRounds.run_segments: per D step the gradients ('s': a
+        BucketedGrads whose bucket all-reduces start while its backward still runs), the wait for
+        those reduces ('e'), then mean + finite guard + Adam + Gs EMA ('g'); likewise the G step.  An
+        optimizer segment is merged into the first graph of the next gradient segment.  The reduces
+        cover only the buckets the segment's backward wrote (untouched blocks above the current LOD
+        are skipped exactly).
         """
         nets = self.nets
 
@@ -878,14 +889,18 @@ class PgGan(BaseModel):
         raw = []
         for r in range(D_repeats):
             d_gr, d_red = d_ar.traced(d_grads, (tag, 'D', r))
-            raw += [('g', d_gr), ('e', d_red), ('g', d_apply)]
+            raw += [('s', d_gr), ('e', d_red), ('g', d_apply)]
         g_gr, g_red = g_ar.traced(g_grads, (tag, 'G'))
-        raw += [('g', g_gr), ('e', g_red), ('g', g_apply)]
+        raw += [('s', g_gr), ('e', g_red), ('g', g_apply)]
         segs = []
         for kind, fn in raw:
-            if segs and kind == 'g' and segs[-1][0] == 'g':
-                prev = segs[-1][1]
-                segs[-1] = ('g', (lambda a, b: (lambda: (a(), b())))(prev, fn))
+            if segs and kind in ('g', 's') and segs[-1][0] == 'g':
+                prev = segs.pop()[1]
+                if kind == 's':
+                    fn.pre.append(prev)   # the previous step's optimizer runs in the first graph of this one
+                    segs.append((kind, fn))
+                else:
+                    segs.append(('g', (lambda a, b: (lambda: (a(), b())))(prev, fn)))
             else:
                 segs.append((kind, fn))
         return segs

@@ -121,7 +121,7 @@ _SIGS = {
     "rk_embedding_bwd": [vp, vp, vp, i32, i32, i32, i32, vp, i64, vp],
     # native tagger step (tagger.hip): embedding + dropout, run-sum embedding gradient, W_hh^T, bias add
     "rk_tag_embed_fwd": [vp, vp, vp, vp, i32, i32, i32, f32, C.c_ulonglong, i32, vp, vp],
-    "rk_tag_embed_bwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, vp],
+    "rk_tag_embed_bwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
     "rk_tag_transpose": [vp, vp, i32, i32, i32, vp],
     "rk_tag_add": [vp, vp, vp, i64, vp],
     "rk_softmax_xent_f32s": [vp, i32, vp, i32, i32, i32, vp, vp, i32, vp, vp],

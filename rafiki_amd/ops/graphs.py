@@ -62,3 +62,58 @@ def capture(graph: "torch.cuda.CUDAGraph", pool=None, stream=None):
                 gc.enable()
 
 
+class SplitCapture:
+    """One capture region recorded as a SEQUENCE of graphs on one stream and one memory pool.
+
+    ``cut(mark)`` ends the current graph and begins the next one where the stream's work stands; the
+    caller replays the graphs in order and may enqueue other work between them (the data-parallel
+    gradient segments start each bucket's all-reduce after the graph that finished the bucket, so the
+    reduce runs on RCCL's stream while the next graph replays the rest of the backward).  Cuts are
+    made from inside a backward, i.e. on autograd's device thread, whose current stream is the
+    capture stream there; so the graphs are captured in ``relaxed`` mode (a graph may end on another
+    thread than the one that began it).  LOCK is held and the cyclic GC is off for the whole region,
+    as in ``capture``; the graphs share ``pool`` and are replayed in capture order, so memory reuse
+    across them is stream-ordered exactly as inside one graph."""
+
+    def __init__(self, pool=None):
+        self.pool = pool if pool is not None else torch.cuda.graph_pool_handle()
+        self.parts = []            # [(graph, mark)]
+        self.tail_mark = None      # the mark of the last graph (set before the region ends)
+        self._cur = None
+        self._stream = None
+
+    def _begin(self):
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self.pool, capture_error_mode='relaxed')
+        self._cur = g
+
+    def cut(self, mark=None):
+        """End the current graph (its replay is followed by ``mark``'s work) and begin the next."""
+        assert torch.cuda.current_stream() == self._stream, 'SplitCapture.cut off the capture stream'
+        self._cur.capture_end()
+        self.parts.append((self._cur, mark))
+        self._begin()
+
+    @contextlib.contextmanager
+    def region(self):
+        with LOCK:
+            if _depth[0] == 0:
+                _depth[1] = gc.isenabled()
+                gc.disable()
+            _depth[0] += 1
+            try:
+                torch.cuda.synchronize()
+                self._stream = torch.cuda.Stream()
+                with torch.cuda.stream(self._stream):
+                    self._begin()
+                    try:
+                        yield self
+                    finally:
+                        self._cur.capture_end()
+                        self.parts.append((self._cur, self.tail_mark))
+                        self._cur = None
+            finally:
+                _depth[0] -= 1
+                if _depth[0] == 0 and _depth[1]:
+                    gc.enable()
+

@@ -110,14 +110,22 @@ class _Channel:
             except RuntimeError as e:
                 raise TimeoutError(msg) from e
         else:
+            # RCCL: poll the completion event.  Each poll is an event query on the GPU, so it runs
+            # under ``lock`` (never mid-capture of another thread); the deadline check and the sleep
+            # between polls stay outside it, so a capture waits at most one poll.
             deadline = time.monotonic() + timeout_s
-            while not work.is_completed():   # RCCL: poll the completion event (no host-blocking wait)
+            while True:
+                with lock:
+                    done = work.is_completed()
+                if done:
+                    break
                 if time.monotonic() > deadline:
                     raise TimeoutError(msg)
                 time.sleep(0.0002)
-        if self.stream is not None:
-            self.stream.synchronize()
-        return t.cpu().tolist()
+        with lock:   # the stream sync and the D2H copy are GPU calls too
+            if self.stream is not None:
+                self.stream.synchronize()
+            return t.cpu().tolist()
 
 
 class KnobExchange:

@@ -1,4 +1,4 @@
-"""Bucketed gradient all-reduce over a flat fp32 gradient arena (overlapped with an eager backward).
+"""Bucketed gradient all-reduce over a flat fp32 gradient arena, overlapped with the backward.
 
 Replaces the reference's per-variable ``tf.contrib.nccl.all_sum`` (pg_gans.py:1164-1171: ~25 calls
 per network per step, several of them on tiny bias tensors) with a handful of large RCCL
@@ -15,21 +15,30 @@ all-reduces over contiguous slices of the FlatParams gradient buffer:
   blocks above the current level of detail, still hold zeros and must be reduced to keep the
   replicas identical) and waits, then applies the 1/world mean (pg_gans.py:1175-1179);
 * ``traced(grads_fn, tag)`` is the form for CAPTURED data-parallel rounds (GraphedRounds'
-  segments): while the gradient segment runs (eagerly, the first time a round shape is seen) every
-  gradient contribution is observed (ops.autograd.GRAD_WATCH for the in-place weight-gradient
-  writes, the post-accumulate hooks for autograd's), and the reduce segment that follows the
-  segment's replays all-reduces only the buckets that received any — PG-GAN blocks above the
-  current level of detail hold zero gradient on every rank, so their sum is zero and they are not
-  reduced at all (two thirds of the arena at the reference schedule's 4x4 LOD).  Starting each
-  bucket's reduce while the replay still runs the earlier layers' backward would need an event
-  recorded inside the capture that a stream outside the graph can wait on; HIP refuses external
-  event records during stream capture (hipErrorInvalidValue, ROCm 7.2; torch refuses
-  Event(external=True) on ROCm), and an internal event does not order the other stream, so the
-  reduce runs between the replays.
+  segments).  The first time a round shape runs (eagerly), every gradient contribution of the
+  segment is observed in order (ops.autograd.GRAD_WATCH for the in-place weight-gradient writes,
+  the post-accumulate hooks for autograd's) and becomes the segment's PLAN: the sequence of buckets
+  the contributions land in.  Buckets that receive none are never reduced: PG-GAN blocks above the
+  current level of detail hold zero gradient on every rank, so their sum is zero (two thirds of the
+  arena at the reference schedule's 4x4 LOD).  From then on each bucket's all-reduce starts as soon
+  as its last contribution is enqueued, while the rest of the backward still runs:
+    - eager rounds launch it from the observer, at the next contribution after the bucket's last;
+    - captured rounds CUT the capture there (``ops.graphs.SplitCapture``): the gradient segment
+      becomes a sequence of graphs, and each bucket's all-reduce is launched on RCCL's stream
+      between the replay of the graph that finished the bucket and the replay of the next one, so
+      the reduce overlaps the later layers' backward on the GPU (pg_gans.py:1164-1171 starts each
+      per-variable nccl all_sum as soon as its gradient exists).  No collective is ever inside a
+      capture, and no event crosses a graph boundary (HIP refuses external event records during
+      capture: ``profiles/graph_external_events_r5.txt``).
+  The reduce segment that follows waits for every launched bucket (the current stream waits on
+  RCCL's), so the mean + optimizer graph starts only after all of them.  Every rank must launch the
+  same buckets in the same order: the first reduce of each plan compares a digest of it across the
+  group and raises on a mismatch instead of hanging in mismatched collectives.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+import zlib
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -152,53 +161,41 @@ class FlatGradAllReduce:
         for w in works:
             w.wait()
 
-    # ------------------------------------------------------------ traced reduce of a captured segment
+    # ------------------------------------------------------------ traced, overlapped gradient segments
     def traced(self, grads_fn, tag):
-        """(grads, reduce) callables for a data-parallel round's segments: ``grads`` runs ``grads_fn``
-        recording which buckets its gradient contributions land in; ``reduce`` all-reduces (sum) those
-        buckets, in the order the backward completed them, and makes the current stream wait for
-        them.  ``tag`` names the segment across rounds (its graph key and position): a replayed
-        segment keeps the buckets traced when it first ran."""
+        """(grads, reduce) for a data-parallel round's segments: ``grads`` (a ``BucketedGrads``: callable
+        eagerly, or captured as a graph sequence) runs ``grads_fn`` and starts each bucket's all-reduce
+        once the bucket is complete; ``reduce`` launches whatever has not started (the whole plan on the
+        tracing run) and makes the current stream wait for all of them.  ``tag`` names the segment
+        across rounds (its graph key and position): a replayed segment keeps the plan traced when it
+        first ran."""
         plan = self._plans.get(tag)
         if plan is None:
-            plan = self._plans[tag] = {'last': None}
-        return (lambda: self._watched(plan, grads_fn)), (lambda: self._reduce_plan(plan))
+            plan = self._plans[tag] = {'seq': None, 'cuts': {}, 'tail': [], 'order': [], 'checked': False}
+        seg = BucketedGrads(self, plan, grads_fn)
+        return seg, seg.reduce
 
     def clear_plans(self):
         self._plans.clear()
 
-    def _watched(self, plan, fn):
-        seq = []
+    def _launch_slice(self, b, works):
+        a, e = self.buckets[b]
+        works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
-        def note(leaf):
-            i = self._idx.get(id(leaf))
-            if i is not None:
-                seq.append(self.bucket_of[i])
-
-        prev = _ag.GRAD_WATCH[0]
-        _ag.GRAD_WATCH[0] = note
-        self._note = note
-        try:
-            fn()
-        finally:
-            _ag.GRAD_WATCH[0] = prev
-            self._note = None
-        traced = {}
-        for pos, b in enumerate(seq):
-            traced[b] = pos
-        if traced or plan['last'] is None:
-            plan['last'] = traced
-
-    def _reduce_plan(self, plan):
-        if self.world <= 1 and not self.force:
-            return
-        last = plan['last'] or {}
-        works = []
-        for b in sorted(last, key=last.get):   # buckets in the order the backward completed them
-            a, e = self.buckets[b]
-            works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
-        for w in works:
-            w.wait()
+    def _check_plan(self, plan):
+        """Every rank must reduce the same buckets in the same order (a rank-dependent branch or a stale
+        plan would otherwise mismatch the collectives and hang): all_gather (count, crc32 of the order)."""
+        order = plan['order']
+        crc = zlib.crc32(','.join(str(b) for b in order).encode())
+        mine = torch.tensor([len(order), crc], dtype=torch.int64, device=self.grad.device)
+        world = dist.get_world_size(self.group)
+        outs = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(outs, mine, group=self.group)
+        got = [tuple(int(v) for v in o.tolist()) for o in outs]
+        if any(g != got[0] for g in got):
+            raise RuntimeError('data-parallel gradient buckets differ across ranks (count, crc32 per rank): '
+                               '{}'.format(got))
+        plan['checked'] = True
 
     def scale(self):
         """grad *= 1/world (the all-reduce mean, pg_gans.py:1175-1179)."""
@@ -215,3 +212,124 @@ def broadcast_flat(t: torch.Tensor, src: int = 0, group=None, world_size: int = 
     """Make a replicated flat buffer identical on every rank (initial weights)."""
     if world_size > 1:
         dist.broadcast(t, src=src, group=group)
+
+
+class BucketedGrads:
+    """One data-parallel gradient segment (forward + backward of a D or G step) whose bucket
+    all-reduces overlap its own backward; see the module docstring.  Made by
+    ``FlatGradAllReduce.traced``; run eagerly by calling it, or captured with ``capture(pool)`` and
+    replayed with ``replay(parts)`` (GraphedRounds.run_segments)."""
+
+    def __init__(self, ar: FlatGradAllReduce, plan: dict, fn):
+        self.ar, self.plan, self.fn = ar, plan, fn
+        self.pre = []            # compute run before ``fn`` in the same (first) graph: a merged prelude
+        self.works = []
+        self.launched = set()
+
+    @property
+    def live(self) -> bool:
+        return self.ar.world > 1 or self.ar.force
+
+    def _body(self):
+        for f in self.pre:
+            f()
+        self.fn()
+
+    def _observe(self, on_cut):
+        """Run the segment with an observer over its gradient contributions; ``on_cut(b)`` is called at
+        the first contribution after bucket b's last one (the plan's cut points), before it."""
+        ar, plan = self.ar, self.plan
+        seq: List[int] = []
+        cuts = plan['cuts'] if plan['seq'] is not None else {}
+
+        def note(leaf):
+            i = ar._idx.get(id(leaf))
+            if i is None:
+                return
+            b = cuts.get(len(seq))
+            if b is not None:
+                on_cut(b)
+            seq.append(ar.bucket_of[i])
+
+        prev = _ag.GRAD_WATCH[0]
+        _ag.GRAD_WATCH[0] = note
+        ar._note = note
+        try:
+            self._body()
+        finally:
+            _ag.GRAD_WATCH[0] = prev
+            ar._note = None
+        return seq
+
+    def _set_plan(self, seq):
+        last: Dict[int, int] = {}
+        for pos, b in enumerate(seq):
+            last[b] = pos
+        order = sorted(last, key=last.get)   # buckets in the order the backward completed them
+        n = len(seq)
+        self.plan.update(seq=list(seq), order=order, tail=[b for b in order if last[b] == n - 1],
+                         cuts={last[b] + 1: b for b in order if last[b] + 1 < n})
+
+    def _verify(self, seq):
+        if seq != self.plan['seq']:
+            raise RuntimeError('data-parallel gradient segment changed since it was traced ({} contributions, '
+                               'traced {}): its bucket reduces would start early'.format(len(seq),
+                                                                                        len(self.plan['seq'])))
+
+    def _launch(self, b):
+        if b not in self.launched:
+            self.launched.add(b)
+            self.ar._launch_slice(b, self.works)
+
+    def __call__(self):
+        """Eager run: trace the plan on the first run; later runs launch each bucket at its cut."""
+        self.works, self.launched = [], set()
+        if self.plan['seq'] is None or not self.live:
+            seq = self._observe(lambda b: None)
+            if self.plan['seq'] is None and (seq or not self.live):
+                self._set_plan(seq)
+            return
+        seq = self._observe(self._launch)
+        self._verify(seq)
+        for b in self.plan['tail']:
+            self._launch(b)
+
+    def capture(self, pool):
+        """Capture the segment as a graph sequence cut at the plan's points; returns the parts
+        [(graph, bucket to launch after it or None)] (the last part's mark is the tail list)."""
+        from ..ops.graphs import SplitCapture
+        sc = SplitCapture(pool)
+        if not self.live or self.plan['seq'] is None:
+            with sc.region():
+                self._observe(lambda b: None)
+            return sc.parts
+        with sc.region():
+            sc.tail_mark = list(self.plan['tail'])
+            seq = self._observe(lambda b: sc.cut(b))
+        self._verify(seq)
+        return sc.parts
+
+    def replay(self, parts):
+        self.works, self.launched = [], set()
+        for g, mark in parts:
+            g.replay()
+            if not self.live or mark is None:
+                continue
+            for b in (mark if isinstance(mark, list) else [mark]):
+                self._launch(b)
+
+    def reduce(self):
+        """The reduce segment: launch what has not started (the tracing run's buckets), then make the
+        current stream wait for every bucket of the round."""
+        if not self.live:
+            return
+        if not self.plan['checked'] and self.ar.world > 1:
+            self._check_plan_once()
+        for b in self.plan['order']:
+            self._launch(b)
+        for w in self.works:
+            w.wait()
+        self.works, self.launched = [], set()
+
+    def _check_plan_once(self):
+        self.ar._check_plan(self.plan)

@@ -39,6 +39,10 @@ def under_launcher() -> bool:
 
 def rank_env(rank: int, world: int, port: int, base: Optional[Dict[str, str]] = None) -> Dict[str, str]:
     env = dict(os.environ if base is None else base)
+    # a parent started by torchrun: its elastic-agent variables would make the children's rendezvous
+    # look for the agent's store (TORCHELASTIC_USE_AGENT_STORE) on a port nobody serves
+    for k in [k for k in env if k.startswith('TORCHELASTIC_')]:
+        del env[k]
     env.update({
         'RANK': str(rank), 'LOCAL_RANK': str(rank), 'WORLD_SIZE': str(world),
         'LOCAL_WORLD_SIZE': str(world), 'GROUP_RANK': '0',
@@ -62,11 +66,12 @@ def _pump(stream, rank: int, out, lock: threading.Lock):
 
 
 def spawn(cmd: Sequence[str], world: int, port: Optional[int] = None, out=None,
-          poll_s: float = 0.05, env: Optional[Dict[str, str]] = None) -> int:
+          poll_s: float = 0.05, env: Optional[Dict[str, str]] = None, timeout_s: Optional[float] = None) -> int:
     """Run ``cmd`` as ``world`` ranks; return 0 iff every rank exited 0.
 
     On the first failing rank the others are terminated (then killed after 10 s) and that rank's
-    exit code is returned (1 for a signal).
+    exit code is returned (1 for a signal).  With ``timeout_s``, ranks still running at the deadline
+    are terminated the same way and 124 is returned (a hung collective ends the call, not the caller).
     """
     out = out or sys.stdout
     port = port or free_port()
@@ -82,6 +87,7 @@ def spawn(cmd: Sequence[str], world: int, port: Optional[int] = None, out=None,
         pumps.append(t)
     rc = 0
     failed = None
+    deadline_all = None if timeout_s is None else time.time() + timeout_s
     while True:
         alive = 0
         for r, p in enumerate(procs):
@@ -93,10 +99,16 @@ def spawn(cmd: Sequence[str], world: int, port: Optional[int] = None, out=None,
                 rc = code if code > 0 else 1
         if failed is not None or alive == 0:
             break
+        if deadline_all is not None and time.time() > deadline_all:
+            failed, rc = -1, 124
+            break
         time.sleep(poll_s)
     if failed is not None:
-        sys.stderr.write('launch: rank {} exited with {}; terminating the other ranks\n'.format(
-            failed, procs[failed].returncode))
+        if failed < 0:
+            sys.stderr.write('launch: ranks still running after {:.0f} s; terminating them\n'.format(timeout_s))
+        else:
+            sys.stderr.write('launch: rank {} exited with {}; terminating the other ranks\n'.format(
+                failed, procs[failed].returncode))
         for p in procs:
             if p.poll() is None:
                 p.terminate()

@@ -8,7 +8,8 @@
      synthetic CIFAR-shaped images, batch 256, width 1.0) -> evaluate (10k) -> dump_parameters ->
      feedback, timed per trial (measured trials/hour; bench.py reports the steady-state step rate)
 
-#3 is bench.py, #4 scripts/bench_predictor.py, #5 scripts/bench_pg_gan.py.
+bench.py measures #1-#5 itself (#1, #2, #5 through rafiki_amd/utils/benchmarks.py); this script runs them
+stand-alone.
 """
 import argparse
 import json
@@ -24,56 +25,15 @@ TEST = 'synthetic://image?n={n}&size=28&channels=1&classes=10&seed=1'
 
 
 def config1(n_train, n_test, trials):
-    from rafiki_amd.advisor.advisor import make_advisor
-    from rafiki_amd.constants import AdvisorType
-    from rafiki_amd.model.model import load_model_class
-    from rafiki_amd.models import model_file
-    from rafiki_amd.parallel.context import TrialContext, use_context
-    import torch
-    clazz = load_model_class(open(model_file('SkDt'), 'rb').read(), 'SkDt')
-    adv = make_advisor(clazz.get_knob_config(), AdvisorType.RANDOM, seed=0)
-    times, scores = [], []
-    with use_context(TrialContext(device=torch.device('cpu'))):
-        for _ in range(trials):
-            t0 = time.perf_counter()
-            knobs = adv.propose()
-            m = clazz(**knobs)
-            m.train(TRAIN.format(n=n_train))
-            s = m.evaluate(TEST.format(n=n_test))
-            pickle.dumps(m.dump_parameters())
-            adv.feedback(knobs, s)
-            times.append(time.perf_counter() - t0)
-            scores.append(s)
-    per = sum(times) / len(times)
-    return {'config': 'SkDt single-trial random-search advisor, CPU', 'metric': 'trials/hour',
-            'value': round(3600.0 / per, 1), 'seconds_per_trial': round(per, 3), 'trials': trials,
-            'best_score': max(scores), 'data': 'synthetic Fashion-MNIST-shaped {}+{} 28x28'.format(n_train, n_test)}
+    from rafiki_amd.utils.benchmarks import skdt_trials
+    return skdt_trials(n_train, n_test, trials)
 
 
 def config2(n_train, n_test, epochs):
     import torch
-    from rafiki_amd.model.model import load_model_class
-    from rafiki_amd.models import model_file
-    from rafiki_amd.parallel.context import TrialContext, use_context
+    from rafiki_amd.utils.benchmarks import mlp_trial
     dev = torch.device('cuda', 0) if torch.cuda.is_available() else torch.device('cpu')
-    clazz = load_model_class(open(model_file('FeedForward'), 'rb').read(), 'FeedForward')
-    knobs = {'epochs': epochs, 'hidden_layer_count': 2, 'hidden_layer_units': 128, 'learning_rate': 0.001,
-             'batch_size': 128, 'image_size': 28}
-    with use_context(TrialContext(device=dev)):
-        m = clazz(**knobs)
-        from rafiki_amd.model import dataset_utils
-        dataset_utils.load_dataset_of_image_files(TRAIN.format(n=n_train), image_size=28)  # warm generator
-        t0 = time.perf_counter()
-        m.train(TRAIN.format(n=n_train))
-        if dev.type == 'cuda':
-            torch.cuda.synchronize()
-        t_train = time.perf_counter() - t0
-        s = m.evaluate(TEST.format(n=n_test))
-        t_trial = time.perf_counter() - t0
-    return {'config': 'TfFeedForward-style MLP, 1 trial on 1 {}'.format('MI355X' if dev.type == 'cuda' else 'CPU'),
-            'metric': 'training images/s (incl. data decode + upload)', 'value': round(n_train * epochs / t_train, 1),
-            'trial_seconds': round(t_trial, 3), 'score': s, 'knobs': knobs, 'dtype': m._meta.get('dtype', 'fp32'),
-            'data': 'synthetic Fashion-MNIST-shaped {}+{} 28x28'.format(n_train, n_test)}
+    return mlp_trial(dev, n_train, n_test, epochs)
 
 
 def config3(trials, epochs):
@@ -129,7 +89,7 @@ if __name__ == '__main__':
     ap.add_argument('--n_train', type=int, default=60000)
     ap.add_argument('--n_test', type=int, default=10000)
     ap.add_argument('--trials', type=int, default=3)
-    ap.add_argument('--epochs', type=int, default=3)
+    ap.add_argument('--epochs', type=int, default=2)
     ap.add_argument('--vgg_trials', type=int, default=4)
     ap.add_argument('--vgg_epochs', type=int, default=10)
     a = ap.parse_args()

@@ -80,3 +80,22 @@ def test_bench_world_size_mismatch_fails():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert 'WORLD_SIZE=2 but --gpus 4' in (r.stderr + r.stdout)
+
+
+def test_spawn_timeout_terminates_hung_ranks(tmp_path, monkeypatch):
+    """A hung child group (e.g. a collective that never completes) ends at the deadline with 124, and a
+    torchrun parent's elastic-agent variables are not passed to the children (their rendezvous would
+    look for the agent's store)."""
+    import time
+    p = tmp_path / 'hang.py'
+    p.write_text('import json, os, sys, time\n'
+                 'print(json.dumps(sorted(k for k in os.environ if k.startswith("TORCHELASTIC_"))), flush=True)\n'
+                 'time.sleep(60)\n')
+    monkeypatch.setenv('TORCHELASTIC_USE_AGENT_STORE', 'True')
+    out = io.StringIO()
+    t = time.time()
+    rc = L.spawn([sys.executable, str(p)], 2, out=out, timeout_s=3)
+    assert rc == 124
+    assert time.time() - t < 30
+    r0 = [ln for ln in out.getvalue().splitlines() if ln.startswith('[')and not ln.startswith('[rank')]
+    assert r0 and all(json.loads(ln) == [] for ln in r0), out.getvalue()

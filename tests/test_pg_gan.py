@@ -370,7 +370,9 @@ def test_pg_gan_dp_traced_segments_match_unsegmented_gloo():
 
 def test_flat_grad_allreduce_traces_and_skips_untouched_buckets():
     """traced(): the trace records each bucket's last contribution; buckets with none are never
-    reduced (their gradients are zero on every rank)."""
+    reduced (their gradients are zero on every rank).  After the tracing run, each bucket's all-reduce
+    starts INSIDE the backward, at the first contribution after the bucket's last one (the overlap the
+    captured rounds get by cutting their graphs there), in backward-completion order."""
     from rafiki_amd.engine.flat import FlatParams, init_const
     from rafiki_amd.parallel.grad_bucket import FlatGradAllReduce
     flat = FlatParams('cpu')
@@ -384,21 +386,35 @@ def test_flat_grad_allreduce_traces_and_skips_untouched_buckets():
         params.append(p)
     ar = FlatGradAllReduce(flat.grad, flat.param_ranges(), params, 1, bucket_mb=0.001, force=True)
     calls = []
+    state = {'bwd': False}
     import torch.distributed as dist
     orig = dist.all_reduce
-    dist.all_reduce = lambda t, **kw: calls.append(t.data_ptr()) or _Done()
+    dist.all_reduce = lambda t, **kw: calls.append((t.data_ptr(), state['bwd'])) or _Done()
+
+    def grads():
+        state['bwd'] = True
+        # params 0, 1 and 3 receive gradients (in the order autograd accumulates them); 2, 4, 5 do not
+        sum((p * (i + 1)).sum() for i, p in ((0, params[0]), (1, params[1]), (3, params[3]))).backward()
+        state['bwd'] = False
     try:
-        gr, red = ar.traced(lambda: sum((p * (i + 1)).sum() for i, p in enumerate(params[:2])).backward(),
-                                ('k', 0))
+        gr, red = ar.traced(grads, ('k', 0))
         gr()
+        red()
+        first = list(calls)
+        calls.clear()
+        gr()          # planned run: launches from inside the backward
         red()
     finally:
         dist.all_reduce = orig
         ar.remove()
     plan = ar._plans[('k', 0)]
-    touched = {ar.bucket_of[0], ar.bucket_of[1]}
-    assert set(plan['last']) == touched
-    assert len(calls) == len(touched) < len(ar.buckets)
+    touched = {ar.bucket_of[0], ar.bucket_of[1], ar.bucket_of[3]}
+    assert set(plan['order']) == touched and len(plan['order']) == 3
+    assert len(first) == len(touched) < len(ar.buckets)
+    assert not any(inside for _, inside in first)              # tracing run: reduce segment only
+    assert [p for p, _ in calls] == [p for p, _ in first]      # same buckets, same order
+    assert sum(inside for _, inside in calls) == len(touched) - 1   # all but the last start mid-backward
+    assert plan['tail'] == plan['order'][-1:]
 
 
 class _Done:
@@ -438,3 +454,30 @@ def test_pg_gan_live_names_cover_the_lod():
     # at full resolution every conv / dense layer is live; only the coarser RGB adapters are not
     assert all('RGB' in n for n in set(nets.G.names()) - set(gall))
     assert all('RGB' in n for n in set(nets.D.names()) - set(dall))
+
+
+def _rounds_worker(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rafiki_amd.parallel import dist as D
+    from rafiki_amd.utils.benchmarks import pg_gan_rounds
+    info = D.init_distributed(backend='gloo')
+    res = pg_gan_rounds(torch.device('cpu'), lods=(3.0,), steps=1, warmup=2, minibatch=16, info=info)
+    if rank == 0:
+        import json as _json
+        with open(os.path.join(out_dir, 'res.json'), 'w') as f:
+            _json.dump(res, f)
+    D.destroy(info)
+
+
+def test_bench_pg_gan_rounds_data_parallel_gloo():
+    """bench.py's PG-GAN phase at N > 1 (BASELINE #5 data parallel): 2 ranks split the global minibatch,
+    the overlapped bucketed all-reduce round runs, and rank 0 reports the global rate."""
+    import json as _json
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rounds_worker, args=(2, port, d), nprocs=2, join=True)
+        with open(os.path.join(d, 'res.json')) as f:
+            res = _json.load(f)
+    r = res['lods']['3.0']
+    assert res['world_size'] == 2 and r['global_minibatch'] == 16 and r['minibatch_per_rank'] == 8
+    assert r['images_per_sec'] > 0 and 'data parallel x2' in res['parallelism']
