@@ -298,7 +298,8 @@ def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30, http_seconds=3.0):
     if loadgen.available():
         pred.start()
         try:
-            out['http'] = loadgen.http_load(pred, seconds=http_seconds)
+            out['http'] = loadgen.http_load(pred, seconds=http_seconds, json_sweep=(16, 256), npy_sweep=(16,),
+                                            sweep_seconds=2.0)
         except Exception as e:   # the device numbers above stand; say why HTTP is missing
             out['http'] = {'error': '{}: {}'.format(type(e).__name__, e)[:300]}
         finally:
@@ -493,6 +494,11 @@ def main():
                 out['ensemble_http_qps'] = js['qps']
                 out['ensemble_http_p50_ms'], out['ensemble_http_p99_ms'] = js['p50_ms'], js['p99_ms']
                 out['ensemble_http_npy_b128_qps'] = nb.get('qps')
+                for key, rows in (('json', [js] + http.get('json_sweep', [])), ('npy_b128', [nb] + http.get('npy_sweep', []))):
+                    out['ensemble_http_{}_sweep'.format(key)] = sorted(
+                        ({'clients': r.get('clients'), 'qps': r.get('qps'), 'p50_ms': r.get('p50_ms'),
+                          'p99_ms': r.get('p99_ms'), 'mean_batch': r.get('mean_batch')} for r in rows if r),
+                        key=lambda r: r['clients'] or 0)
             out['ensemble'] = serving
         if cfgs:
             pg = cfgs.get('pg_gan') or {}

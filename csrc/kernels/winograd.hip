@@ -59,6 +59,9 @@ constexpr unsigned WOOB = 0x80000000u;
 // rows x one pair of a ds_read2st64_b64 lane group (banks mod 32) and the 16 rows x two pairs of a
 // ds_read_b64 group (banks mod 64) then hit distinct banks
 RK_DEV int w_swz(int row) { return ((row >> 2) & 3) << 1; }
+// the weight gradient's stores (a wave: 32 channel rows x 2 tiles): rows r, r + 8, r + 16, r + 24 of a bank
+// group take four different even offsets (conflict-free ds_write_b32; see winograd4.hip swzw)
+RK_DEV int w_swzw(int row) { return (((row >> 3) & 1) << 2) | (((row >> 4) & 1) << 1); }
 
 RK_DEV __amdgpu_buffer_rsrc_t w_rsrc(const float* base, unsigned long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)(unsigned)bytes, 0x00020000);
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
     }
   };
   auto store = [&](int st) {
-    const int c = tt ^ w_swz(ch);
+    const int c = tt ^ w_swzw(ch);
     // A dY A^T (4x4 from 2x2): rows (y0, y0 + y1, y0 - y1, -y1), then the same on columns
     float rw[4][2];
 #pragma unroll
@@ -420,7 +423,8 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
   }
   __syncthreads();
   const int ar = wm * 16 + (lane & 15), br = wn * 32 + (lane & 15);
-  const int ka = (2 * (lane >> 4)) ^ w_swz(ar), kb = (2 * (lane >> 4)) ^ w_swz(br);
+  const int ka = (2 * (lane >> 4)) ^ w_swzw(ar), kb = (2 * (lane >> 4)) ^ w_swzw(br);
+  const int kb16 = (2 * (lane >> 4)) ^ w_swzw(br + 16);   // rows br + 16: bit 4 of the row is in w_swzw
   for (int c = 0; c < nch; ++c) {
     const int st = c & 1;
     if (c + 1 < nch) load(c + 1);
@@ -431,7 +435,7 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
       for (int e = 0; e < 2; ++e) {
         a[e] = *(const f32x2*)&Ms[st][q + e][ar][ka];
         bv[e][0] = *(const f32x2*)&Vs[st][q + e][br][kb];
-        bv[e][1] = *(const f32x2*)&Vs[st][q + e][br + 16][kb];
+        bv[e][1] = *(const f32x2*)&Vs[st][q + e][br + 16][kb16];
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s)

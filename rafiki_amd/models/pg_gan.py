@@ -497,7 +497,8 @@ class GraphedRounds:
                 else:
                     g.replay()
             return
-        if key not in self.seen:
+        if key not in self.seen or any(kind == 's' and not fn.planned for kind, fn in segs):
+            # eager until every gradient segment's bucket plan is traced (BucketedGrads.TRACES runs)
             self.seen.add(key)
             for _, fn in segs:
                 fn()

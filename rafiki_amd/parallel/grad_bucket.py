@@ -15,25 +15,28 @@ all-reduces over contiguous slices of the FlatParams gradient buffer:
   blocks above the current level of detail, still hold zeros and must be reduced to keep the
   replicas identical) and waits, then applies the 1/world mean (pg_gans.py:1175-1179);
 * ``traced(grads_fn, tag)`` is the form for CAPTURED data-parallel rounds (GraphedRounds'
-  segments).  The first time a round shape runs (eagerly), every gradient contribution of the
-  segment is observed in order (ops.autograd.GRAD_WATCH for the in-place weight-gradient writes,
-  the post-accumulate hooks for autograd's) and becomes the segment's PLAN: the sequence of buckets
-  the contributions land in.  Buckets that receive none are never reduced: PG-GAN blocks above the
-  current level of detail hold zero gradient on every rank, so their sum is zero (two thirds of the
-  arena at the reference schedule's 4x4 LOD).  From then on each bucket's all-reduce starts as soon
-  as its last contribution is enqueued, while the rest of the backward still runs:
-    - eager rounds launch it from the observer, at the next contribution after the bucket's last;
+  segments).  The first eager runs of a round shape observe every gradient contribution of the
+  segment (ops.autograd.GRAD_WATCH for the in-place weight-gradient writes, the post-accumulate hooks
+  for autograd's) and record the segment's PLAN: how many contributions each bucket receives.
+  Buckets that receive none are never reduced: PG-GAN blocks above the current level of detail hold
+  zero gradient on every rank, so their sum is zero (two thirds of the arena at the reference
+  schedule's 4x4 LOD).  From then on each bucket's all-reduce starts as soon as it is complete, while
+  the rest of the backward still runs:
+    - eager rounds launch it from the observer, at the first contribution after the bucket's last;
     - captured rounds CUT the capture there (``ops.graphs.SplitCapture``): the gradient segment
       becomes a sequence of graphs, and each bucket's all-reduce is launched on RCCL's stream
-      between the replay of the graph that finished the bucket and the replay of the next one, so
+      between the replay of the graph that completed the bucket and the replay of the next one, so
       the reduce overlaps the later layers' backward on the GPU (pg_gans.py:1164-1171 starts each
       per-variable nccl all_sum as soon as its gradient exists).  No collective is ever inside a
       capture, and no event crosses a graph boundary (HIP refuses external event records during
       capture: ``profiles/graph_external_events_r5.txt``).
-  The reduce segment that follows waits for every launched bucket (the current stream waits on
-  RCCL's), so the mean + optimizer graph starts only after all of them.  Every rank must launch the
-  same buckets in the same order: the first reduce of each plan compares a digest of it across the
-  group and raises on a mismatch instead of hanging in mismatched collectives.
+  Every rank reduces the live buckets in ascending bucket order (reverse parameter order, roughly
+  the order the backward completes them), a bucket as soon as it and every lower one are complete:
+  the order the collectives are issued in never depends on a rank's own autograd order, which a
+  per-rank autotuner pick can change.  The reduce segment that follows waits for every launched
+  bucket (the current stream waits on RCCL's), so the mean + optimizer graph starts after all of
+  them.  The first reduce of each plan compares a digest of it across the group and raises on a
+  mismatch instead of hanging in mismatched collectives.
 """
 from __future__ import annotations
 
@@ -171,7 +174,7 @@ class FlatGradAllReduce:
         first ran."""
         plan = self._plans.get(tag)
         if plan is None:
-            plan = self._plans[tag] = {'seq': None, 'cuts': {}, 'tail': [], 'order': [], 'checked': False}
+            plan = self._plans[tag] = {'count': None, 'order': [], 'traces': 0, 'ready': False}
         seg = BucketedGrads(self, plan, grads_fn)
         return seg, seg.reduce
 
@@ -183,11 +186,11 @@ class FlatGradAllReduce:
         works.append(dist.all_reduce(self.grad[a:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def _check_plan(self, plan):
-        """Every rank must reduce the same buckets in the same order (a rank-dependent branch or a stale
-        plan would otherwise mismatch the collectives and hang): all_gather (count, crc32 of the order)."""
-        order = plan['order']
-        crc = zlib.crc32(','.join(str(b) for b in order).encode())
-        mine = torch.tensor([len(order), crc], dtype=torch.int64, device=self.grad.device)
+        """Every rank must reduce the same buckets (a rank-dependent branch would otherwise mismatch the
+        collectives and hang): all_gather (live buckets, crc32 of (bucket, contributions)) and compare."""
+        live = sorted(plan['count'] or {})
+        crc = zlib.crc32(','.join('{}:{}'.format(b, plan['count'][b]) for b in live).encode())
+        mine = torch.tensor([len(live), crc], dtype=torch.int64, device=self.grad.device)
         world = dist.get_world_size(self.group)
         outs = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(outs, mine, group=self.group)
@@ -195,7 +198,16 @@ class FlatGradAllReduce:
         if any(g != got[0] for g in got):
             raise RuntimeError('data-parallel gradient buckets differ across ranks (count, crc32 per rank): '
                                '{}'.format(got))
-        plan['checked'] = True
+
+    def _agree_order(self, order):
+        """Rank 0's bucket completion order, the same list on every rank (the order collectives are issued in)."""
+        t = torch.full((len(self.buckets) + 1,), -1, dtype=torch.int64, device=self.grad.device)
+        t[0] = len(order)
+        if order:
+            t[1:1 + len(order)] = torch.tensor(order, dtype=torch.int64)
+        dist.broadcast(t, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
+        v = t.tolist()
+        return [int(b) for b in v[1:1 + int(v[0])]]
 
     def scale(self):
         """grad *= 1/world (the all-reduce mean, pg_gans.py:1175-1179)."""
@@ -218,38 +230,68 @@ class BucketedGrads:
     """One data-parallel gradient segment (forward + backward of a D or G step) whose bucket
     all-reduces overlap its own backward; see the module docstring.  Made by
     ``FlatGradAllReduce.traced``; run eagerly by calling it, or captured with ``capture(pool)`` and
-    replayed with ``replay(parts)`` (GraphedRounds.run_segments)."""
+    replayed with ``replay(parts)`` (GraphedRounds.run_segments).
+
+    The plan is the number of gradient contributions each live bucket receives (``count``) and the ORDER the
+    buckets are reduced in, traced on the first TRACES eager runs (the first one also autotunes, and a
+    tuned pick may reorder the backward).  The order is rank 0's completion order of the last tracing run,
+    broadcast, so every rank issues the collectives in the same order whatever its own autograd order (a
+    per-rank tuner pick can change it; the WGAN-GP double backward completes the output layers' buckets
+    last, so bucket index order would leave nothing to overlap).  A bucket becomes ready at the first
+    contribution after its count is reached (its last write is enqueued by then) once every bucket
+    before it in the order is ready.  Tracing runs reduce everything after the backward, in bucket order."""
+
+    TRACES = 2
 
     def __init__(self, ar: FlatGradAllReduce, plan: dict, fn):
         self.ar, self.plan, self.fn = ar, plan, fn
         self.pre = []            # compute run before ``fn`` in the same (first) graph: a merged prelude
         self.works = []
         self.launched = set()
+        self._traced = False     # this round's gradient pass was a tracing run (its reduce finalises)
 
     @property
     def live(self) -> bool:
         return self.ar.world > 1 or self.ar.force
+
+    @property
+    def planned(self) -> bool:
+        return self.plan['ready']
 
     def _body(self):
         for f in self.pre:
             f()
         self.fn()
 
-    def _observe(self, on_cut):
-        """Run the segment with an observer over its gradient contributions; ``on_cut(b)`` is called at
-        the first contribution after bucket b's last one (the plan's cut points), before it."""
+    def _observe(self, on_ready, extra=None):
+        """Run the segment with an observer over its gradient contributions.  Planned: ``on_ready(bs)`` is
+        called with the buckets that just became ready (in order), before the contribution that found
+        them so; returns (per-bucket contribution counts, buckets not yet ready at the end)."""
         ar, plan = self.ar, self.plan
-        seq: List[int] = []
-        cuts = plan['cuts'] if plan['seq'] is not None else {}
+        planned = self.planned
+        order = plan['order'] if planned else []
+        count = plan['count'] if planned else {}
+        seen: Dict[int, int] = {}
+        nxt = [0]
 
         def note(leaf):
             i = ar._idx.get(id(leaf))
             if i is None:
                 return
-            b = cuts.get(len(seq))
-            if b is not None:
-                on_cut(b)
-            seq.append(ar.bucket_of[i])
+            if planned:
+                ready = []
+                while nxt[0] < len(order) and seen.get(order[nxt[0]], 0) == count[order[nxt[0]]]:
+                    ready.append(order[nxt[0]])
+                    nxt[0] += 1
+                if ready:
+                    on_ready(ready)
+            b = ar.bucket_of[i]
+            if planned and b in order[:nxt[0]]:
+                raise RuntimeError('data-parallel bucket {} received a gradient after its all-reduce was '
+                                   'started (the segment changed since it was traced)'.format(b))
+            seen[b] = seen.get(b, 0) + 1
+            if extra is not None:
+                extra(leaf)
 
         prev = _ag.GRAD_WATCH[0]
         _ag.GRAD_WATCH[0] = note
@@ -259,77 +301,82 @@ class BucketedGrads:
         finally:
             _ag.GRAD_WATCH[0] = prev
             ar._note = None
-        return seq
+        if planned and seen != count:
+            raise RuntimeError('data-parallel gradient segment changed since it was traced: contributions per '
+                               'bucket {} vs traced {}'.format(seen, count))
+        return seen, order[nxt[0]:]
 
-    def _set_plan(self, seq):
+    def _trace(self):
+        ar = self.ar
         last: Dict[int, int] = {}
-        for pos, b in enumerate(seq):
-            last[b] = pos
-        order = sorted(last, key=last.get)   # buckets in the order the backward completed them
-        n = len(seq)
-        self.plan.update(seq=list(seq), order=order, tail=[b for b in order if last[b] == n - 1],
-                         cuts={last[b] + 1: b for b in order if last[b] + 1 < n})
+        pos = [0]
 
-    def _verify(self, seq):
-        if seq != self.plan['seq']:
-            raise RuntimeError('data-parallel gradient segment changed since it was traced ({} contributions, '
-                               'traced {}): its bucket reduces would start early'.format(len(seq),
-                                                                                        len(self.plan['seq'])))
+        def note(leaf):   # the order the backward completes the buckets in (position of the last contribution)
+            i = ar._idx.get(id(leaf))
+            if i is not None:
+                last[ar.bucket_of[i]] = pos[0]
+                pos[0] += 1
+        seen, _ = self._observe(None, extra=note)
+        if seen or self.plan['count'] is None:
+            self.plan.update(count=dict(seen), order=sorted(seen, key=lambda b: last[b]))
+        self.plan['traces'] += 1
+        self._traced = True
 
     def _launch(self, b):
         if b not in self.launched:
             self.launched.add(b)
             self.ar._launch_slice(b, self.works)
 
-    def __call__(self):
-        """Eager run: trace the plan on the first run; later runs launch each bucket at its cut."""
-        self.works, self.launched = [], set()
-        if self.plan['seq'] is None or not self.live:
-            seq = self._observe(lambda b: None)
-            if self.plan['seq'] is None and (seq or not self.live):
-                self._set_plan(seq)
-            return
-        seq = self._observe(self._launch)
-        self._verify(seq)
-        for b in self.plan['tail']:
+    def _launch_all(self, bs):
+        for b in bs:
             self._launch(b)
 
+    def __call__(self):
+        """Eager run: trace until the plan is settled; then launch each bucket as it becomes ready."""
+        self.works, self.launched = [], set()
+        self._traced = False
+        if not self.planned or not self.live:
+            self._trace()
+            return
+        _, tail = self._observe(self._launch_all)
+        self._launch_all(tail)
+
     def capture(self, pool):
-        """Capture the segment as a graph sequence cut at the plan's points; returns the parts
-        [(graph, bucket to launch after it or None)] (the last part's mark is the tail list)."""
+        """Capture the segment as a graph sequence cut where buckets become ready; returns the parts
+        [(graph, buckets to launch after it)]."""
         from ..ops.graphs import SplitCapture
+        if not self.planned:
+            raise RuntimeError('BucketedGrads.capture before the plan is traced ({} eager runs needed)'.format(
+                self.TRACES))
         sc = SplitCapture(pool)
-        if not self.live or self.plan['seq'] is None:
-            with sc.region():
-                self._observe(lambda b: None)
-            return sc.parts
         with sc.region():
-            sc.tail_mark = list(self.plan['tail'])
-            seq = self._observe(lambda b: sc.cut(b))
-        self._verify(seq)
+            _, tail = self._observe(lambda bs: sc.cut(list(bs)) if self.live else None)
+            sc.tail_mark = list(tail) if self.live else None
         return sc.parts
 
     def replay(self, parts):
         self.works, self.launched = [], set()
         for g, mark in parts:
             g.replay()
-            if not self.live or mark is None:
-                continue
-            for b in (mark if isinstance(mark, list) else [mark]):
-                self._launch(b)
+            if self.live and mark:
+                self._launch_all(mark)
 
     def reduce(self):
-        """The reduce segment: launch what has not started (the tracing run's buckets), then make the
-        current stream wait for every bucket of the round."""
+        """The reduce segment: after a tracing run, check the plan across the ranks and reduce every live
+        bucket in bucket order (and, after the last tracing run, agree on rank 0's completion order); then
+        make the current stream wait for every bucket of the round."""
         if not self.live:
             return
-        if not self.plan['checked'] and self.ar.world > 1:
-            self._check_plan_once()
-        for b in self.plan['order']:
-            self._launch(b)
+        if self._traced:
+            self._traced = False
+            if self.ar.world > 1:
+                self.ar._check_plan(self.plan)
+            self._launch_all(sorted(self.plan['count'] or {}))
+            if self.plan['traces'] >= self.TRACES and not self.plan['ready']:
+                if self.ar.world > 1:
+                    self.plan['order'] = self.ar._agree_order(self.plan['order'])
+                self.plan['ready'] = True
+        self._launch_all(self.plan['order'])   # none left on a planned round: each started when ready
         for w in self.works:
             w.wait()
         self.works, self.launched = [], set()
-
-    def _check_plan_once(self):
-        self.ar._check_plan(self.plan)

@@ -41,8 +41,11 @@ def run_httpload(port, path, body: bytes, connections, threads, seconds, per_req
 
 
 def http_load(pred, image_shape=(32, 32, 3), seconds=3.0, json_clients=64, npy_clients=8, npy_batch=128,
-              seed=0):
-    """Serve ``pred`` on the native front end and measure it with httpload; returns a dict of phases."""
+              seed=0, json_sweep=(), npy_sweep=(), sweep_seconds=2.0):
+    """Serve ``pred`` on the native front end and measure it with httpload; returns a dict of phases.
+    ``json_sweep`` / ``npy_sweep``: further client counts, each its own closed-loop phase (where the front end
+    saturates against the device rate).  Every phase carries the server's own per-batch timeline
+    (NativePredictorServer.batch_timing) next to the client's latencies."""
     from ..container.container_manager import free_port
     from .nativeserve import NativePredictorServer
     if not available():
@@ -57,12 +60,26 @@ def http_load(pred, image_shape=(32, 32, 3), seconds=3.0, json_clients=64, npy_c
     try:
         warm = json.dumps({'query': one}).encode()
         run_httpload(port, '/predict', warm, 8, 2, 0.5)   # graphs / buckets warm before the timed phases
+        npy = buf.getvalue()
+
+        def phase(path, body, clients, secs, per_request=1):
+            srv.reset_timing()
+            c0 = srv.counters
+            r = dict(run_httpload(port, path, body, clients, 4, secs, per_request=per_request), clients=clients)
+            c1 = srv.counters
+            nb = c1.get('batches', 0) - c0.get('batches', 0)
+            r['mean_batch'] = round((c1.get('batched_queries', 0) - c0.get('batched_queries', 0)) / max(1, nb), 1)
+            r['server_batches'] = srv.batch_timing()
+            return r
         out = {'server': 'native', 'client': 'httpload (separate process, keep-alive, closed loop)',
-               'json_single_query': dict(run_httpload(port, '/predict', warm, json_clients, 4, seconds),
-                                         clients=json_clients),
-               'npy_batch{}'.format(npy_batch): dict(run_httpload(port, '/predict_batch_npy', buf.getvalue(),
-                                                                  npy_clients, 4, seconds, per_request=npy_batch),
-                                                     clients=npy_clients)}
+               'json_single_query': phase('/predict', warm, json_clients, seconds),
+               'npy_batch{}'.format(npy_batch): phase('/predict_batch_npy', npy, npy_clients, seconds,
+                                                      per_request=npy_batch)}
+        if json_sweep:
+            out['json_sweep'] = [phase('/predict', warm, k, sweep_seconds) for k in json_sweep]
+        if npy_sweep:
+            out['npy_sweep'] = [phase('/predict_batch_npy', npy, k, sweep_seconds, per_request=npy_batch)
+                                for k in npy_sweep]
         c = getattr(srv, 'counters', {})
         out['server_counters'] = {k: c[k] for k in ('requests', 'batches', 'batched_queries') if k in c}
         return out

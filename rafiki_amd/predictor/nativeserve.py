@@ -127,6 +127,8 @@ def route(predictor, counters, method: str, path: str, body: bytes):
 class NativePredictorServer:
     """Drop-in for ``FastPredictorServer``: ``start()`` / ``serve_forever()`` / ``shutdown()`` / ``port``."""
 
+    TIMING_RING = 1 << 16
+
     def __init__(self, predictor, host='0.0.0.0', port=3003, max_batch=512, io_threads=4, generic_threads=4):
         self.predictor = predictor
         self.host, self.port = host, int(port)
@@ -141,6 +143,11 @@ class NativePredictorServer:
         self._pool = None
         self._base = {'python_batches': 0, 'python_errors': 0}
         self._ready = []
+        # per-batch timeline of the staged loop (ring of the last TIMING_RING batches): queries, then the
+        # seconds from the batch leaving the C++ queue to its launch, to its graph finishing, and to its
+        # responses being handed back (batch_timing() summarises; the p99 analysis of docs/serving.md)
+        self._timing = np.zeros((self.TIMING_RING, 4), dtype=np.float64)
+        self._timing_n = 0
         self.ready_timeout_s = 300.0
 
     # ------------------------------------------------------------------------------ stats
@@ -152,6 +159,27 @@ class NativePredictorServer:
             buf = (ctypes.c_longlong * 8)()
             h.rt_http_stats(self._h, buf)
             out.update({k: int(v) for k, v in zip(_STAT_KEYS, buf)})
+        return out
+
+    def reset_timing(self):
+        self._timing_n = 0
+
+    def batch_timing(self) -> dict:
+        """Percentiles (ms) of the staged batches since ``reset_timing``: ``launch`` = C++ queue -> graph
+        launched, ``device`` = launch -> graph done (includes waiting behind the previous batch on the
+        stream), ``complete`` = done -> responses handed to C++; plus the batch-size distribution."""
+        n = min(self._timing_n, self.TIMING_RING)
+        if n == 0:
+            return {}
+        t = self._timing[:n]
+        out = {'batches': int(n), 'batch_queries_p50': float(np.percentile(t[:, 0], 50)),
+               'batch_queries_max': float(t[:, 0].max())}
+        for j, k in ((1, 'launch'), (2, 'device'), (3, 'complete')):
+            for q in (50, 99):
+                out['{}_p{}_ms'.format(k, q)] = round(float(np.percentile(t[:, j], q)) * 1e3, 3)
+        tot = t[:, 1:].sum(1)
+        out['total_p50_ms'] = round(float(np.percentile(tot, 50)) * 1e3, 3)
+        out['total_p99_ms'] = round(float(np.percentile(tot, 99)) * 1e3, 3)
         return out
 
     # ------------------------------------------------------------------------------ loops
@@ -233,10 +261,12 @@ class NativePredictorServer:
                     continue
                 if n > 0:
                     taken = bid.value
+                    t_take = time.perf_counter()
                     q = tuple(int(shape[i]) for i in range(nd.value))
                     if q == tuple(img_shape):
                         try:
-                            launched = (g.launch_staged(slot, int(n)), slot, bid.value, int(n))
+                            launched = (g.launch_staged(slot, int(n)), slot, bid.value, int(n), t_take,
+                                        time.perf_counter())
                         except Exception as e:
                             self._fail(bid.value, e)
                         taken = None
@@ -259,14 +289,18 @@ class NativePredictorServer:
         """Wait for a launched staged batch and complete it; returns None (the new 'pending')."""
         if pending is None:
             return None
-        ev, slot, bid, n = pending
+        ev, slot, bid, n, t_take, t_launch = pending
         try:
             ev.synchronize()
         except Exception as e:
             self._fail(bid, e)
             return None
+        t_done = time.perf_counter()
         self.predictor.stats['queries'] = self.predictor.stats.get('queries', 0) + n
         self._complete(bid, g.staged_out(slot), n)
+        i = self._timing_n % self.TIMING_RING
+        self._timing[i] = (n, t_launch - t_take, t_done - t_launch, time.perf_counter() - t_done)
+        self._timing_n += 1
         return None
 
     def _run_sync(self, bid, arr, n):
