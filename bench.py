@@ -494,6 +494,8 @@ def main():
                 out['ensemble_http_qps'] = js['qps']
                 out['ensemble_http_p50_ms'], out['ensemble_http_p99_ms'] = js['p50_ms'], js['p99_ms']
                 out['ensemble_http_npy_b128_qps'] = nb.get('qps')
+                best = max([nb] + http.get('npy_sweep', []), key=lambda r: r.get('qps') or 0)
+                out['ensemble_http_npy_b128_qps_max'] = {'qps': best.get('qps'), 'clients': best.get('clients')}
                 for key, rows in (('json', [js] + http.get('json_sweep', [])), ('npy_b128', [nb] + http.get('npy_sweep', []))):
                     out['ensemble_http_{}_sweep'.format(key)] = sorted(
                         ({'clients': r.get('clients'), 'qps': r.get('qps'), 'p50_ms': r.get('p50_ms'),

@@ -439,6 +439,57 @@ __global__ __launch_bounds__(256) void x6p_split_kernel(const float* __restrict_
   dst[o + 2 * ps] = l;
 }
 
+// fp32 src [rows][lds] -> three bf16 planes [3][cols][ldd] of its TRANSPOSE (plane stride ps): the K-inner
+// operand of a GEMM that reduces over src's rows (the dense weight gradient dW = dY^T X reduces over the
+// batch; the dense data gradient dX = dY W takes W^T).  The plane columns rows .. ldd-1 (the K padding to a
+// 32-deep K-tile) are written as zeros.  64 x 64 tiles through LDS; each thread stores 4 consecutive plane
+// elements per plane (8-B stores).
+__global__ __launch_bounds__(256) void x6p_split_t_kernel(const float* __restrict__ src, bf16* __restrict__ dst,
+                                                          int rows, int cols, int lds, int ldd, long long ps) {
+  __shared__ float t[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  const int lc = (tid & 15) * 4, lr = tid >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r0 + lr + 16 * k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + lc + e;
+      t[lr + 16 * k][lc + e] = (r < rows && c < cols) ? src[(long long)r * lds + c] : 0.f;
+    }
+  }
+  __syncthreads();
+  const int sr = (tid & 15) * 4, sc = tid >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + sc + 16 * k, r = r0 + sr;
+    if (c >= cols || r >= ldd) continue;
+    bf16 h[4], m[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3v(t[sr + e][sc + 16 * k], h[e], m[e], l[e]);
+    const long long o = (long long)c * ldd + r;
+    if (r + 3 < ldd) {   // ldd % 4 == 0: an aligned 8-B store per plane
+      typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+      u16x4 vh, vm, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        vh[e] = __builtin_bit_cast(unsigned short, h[e]);
+        vm[e] = __builtin_bit_cast(unsigned short, m[e]);
+        vl[e] = __builtin_bit_cast(unsigned short, l[e]);
+      }
+      *(u16x4*)(dst + o) = vh;
+      *(u16x4*)(dst + o + ps) = vm;
+      *(u16x4*)(dst + o + 2 * ps) = vl;
+    } else {
+      for (int e = 0; e < 4 && r + e < ldd; ++e) {
+        dst[o + e] = h[e];
+        dst[o + e + ps] = m[e];
+        dst[o + e + 2 * ps] = l[e];
+      }
+    }
+  }
+}
 
 }  // namespace
 
@@ -510,6 +561,19 @@ extern "C" int rk_x6p_split(const float* src, void* dst, int rows, int cols, int
   const long long n = (long long)rows * cols;
   hipLaunchKernelGGL(x6p_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, src,
                      (bf16*)dst, rows, cols, lds, ldd, ps);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// planes [3][cols][ldd] (plane stride ps) of the transpose of an fp32 [rows][lds] matrix; plane columns
+// rows .. ldd-1 zero; ldd % 4 == 0
+extern "C" int rk_x6p_split_t(const float* src, void* dst, int rows, int cols, int lds, int ldd, long long ps,
+                              void* stream) {
+  if (rows <= 0 || cols <= 0 || lds < cols || ldd < rows || (ldd & 3) || ps < (long long)cols * ldd)
+    return RK_EBADARG;
+  const dim3 grid((unsigned)rk_cdiv(cols, 64), (unsigned)rk_cdiv(ldd, 64));
+  hipLaunchKernelGGL(x6p_split_t_kernel, grid, dim3(256), 0, (hipStream_t)stream, src, (bf16*)dst, rows, cols, lds,
+                     ldd, ps);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -708,16 +708,14 @@ class PgGan(BaseModel):
         rng = TrialRng(dev, self.seed * 7919)   # one stream for all ranks; each keeps its shard
         # RCCL collectives are graph-capturable, gloo ones are not (a gloo group on GPUs is the
         # one-box multi-rank rehearsal: eager)
-        # Capturing rounds WITH collectives is opt-in (RAFIKI_PGGAN_GRAPH_COLLECTIVES=1): the process
-        # group's watchdog thread polls the events of the eager rounds' completed works on its own
-        # schedule, and torch exposes no hook to wait until it has retired them, so a capture could
-        # still overlap such a poll (GraphedRounds.run waits 0.3 s, ~3 watchdog periods: a residual
-        # race, not a guarantee).  Default: data-parallel rounds run eager, single-GPU ones captured.
-        # Data-parallel rounds are captured by SEGMENTS: gradients (captured) -> bucketed all-reduce
-        # (eager, between replays) -> optimizer (captured), so no collective is inside a capture.  The
-        # older whole-round capture with the collectives inside stays an opt-in
-        # (RAFIKI_PGGAN_GRAPH_COLLECTIVES=1, nccl only: it waits 0.3 s for the watchdog).  With eager
-        # collective segments a gloo group (the one-box multi-rank rehearsal) is capturable too.
+        # Data-parallel rounds are captured by SEGMENTS (round_segments): each gradient pass as a sequence
+        # of graphs cut where a gradient bucket completes, its bucket all-reduces launched eagerly between
+        # those replays (overlapping the rest of the backward), then the optimizer graph — no collective
+        # is ever inside a capture, so the process group's watchdog has nothing of ours to race, and a
+        # gloo group (the one-box multi-rank rehearsal) is capturable too.  The older whole-round capture
+        # with the collectives inside stays an opt-in (RAFIKI_PGGAN_GRAPH_COLLECTIVES=1, nccl only): the
+        # watchdog polls the eager rounds' completed works on its own schedule, so that capture waits
+        # 0.3 s (~3 watchdog periods) first — a residual race, not a guarantee.
         whole = g_ar is not None and (self.ctx.dist.backend == 'nccl'
                                       and os.environ.get('RAFIKI_PGGAN_GRAPH_COLLECTIVES', '0') == '1')
         # dp_segmented=False (tests): the unsegmented round — hooks launch the buckets, finish() waits

@@ -132,6 +132,7 @@ _SIGS = {
     "rk_x6p_gemm": [i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i32, i32, i32, i64,
                     i64, i64, vp],
     "rk_x6p_split": [vp, vp, i32, i32, i32, i32, i64, vp],
+    "rk_x6p_split_t": [vp, vp, i32, i32, i32, i32, i64, vp],
     "rk_x6p_w4_weights": [vp, vp, vp, i32, i32, vp],
     "rk_x6p_w4_weights_multi": [vp, vp, vp, i32, vp, vp],
     "rk_wino_weights_all": [vp, vp, vp, i32, vp, vp],

@@ -879,6 +879,18 @@ def x6p_split(src: torch.Tensor, out=None) -> torch.Tensor:
     return out
 
 
+def x6p_split_t(src: torch.Tensor, ldd: Optional[int] = None, out=None) -> torch.Tensor:
+    """bf16 X6 planes [3][cols][ldd] of the TRANSPOSE of an fp32 [rows][cols] matrix (row stride any), the
+    plane columns rows .. ldd-1 zero (ldd: rows rounded up to 32, the x6p GEMM's K granularity)."""
+    rows, cols = src.shape
+    assert src.dtype == torch.float32 and src.stride(1) == 1, (src.dtype, src.stride())
+    ldd = ldd or cdiv(rows, 32) * 32
+    if out is None:
+        out = torch.empty((3, cols, ldd), dtype=torch.bfloat16, device=src.device)
+    _lib.call("rk_x6p_split_t", _p(src), _p(out), rows, cols, src.stride(0), ldd, cols * ldd, _s())
+    return out
+
+
 def x6p_gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, M: int, N: int, K: int, *, groups: int = 1,
              tile: int = 0, nst: int = 2, accumulate: bool = False, splits: int = 1,
              row_major_groups: bool = False) -> torch.Tensor:
@@ -1169,6 +1181,32 @@ class WinoWeights:
 
 
 # ----------------------------------------------------------------------------------------- dense
+# Pre-split X6 dense candidates (cfg = (XP_DENSE, x6p tile * 4 + nst, splits)): both operands split into bf16
+# planes by one pass each (x6p_split / x6p_split_t, inside the timed candidate), then the x6p GEMM — its K
+# loop is LDS reads + MFMAs only, where the sgemm X6 loop re-splits every fragment after its LDS read and runs
+# VALU-bound (the PG-GAN dense layers: 512 x 8192 at mb 512, profiles/pg_gan_lod3_f32_kernels_r5.txt); the
+# bias / activation / gate epilogue and the split-K combine ride in sreduce_epi / reduce_slabs
+XP_DENSE = -21
+XPD_MIN_MN = 1 << 20   # output elements below which the two split passes cannot pay (tiny / head layers)
+XPD_CFGS = tuple((XP_DENSE, 4 * t + n, s) for t in (0, 1, 2, 3) for n in (2, 3) for s in (1, 2, 4)) + \
+    tuple((XP_DENSE, 4 * t + 2, s) for t in (7, 8) for s in (1, 2, 4)) if USE_X6P else ()
+
+
+def _xpd(cfg):
+    return cfg[0] == XP_DENSE
+
+
+def _xp_gemm_into(A, B, M, N, K, code, s, out=None, accumulate=False):
+    """x6p GEMM of planes A [3][M][K] . B [3][N][K]^T: into ``out`` (s == 1) or a fresh [s][M][N] slab."""
+    s = x6p_splits(K, s)
+    if s == 1 and out is not None:
+        x6p_gemm(A, B, out, M, N, K, tile=code // 4, nst=code % 4, accumulate=accumulate)
+        return out, 1
+    slab = torch.empty((s, M, N), device=A.device, dtype=torch.float32)
+    x6p_gemm(A, B, slab, M, N, K, tile=code // 4, nst=code % 4, splits=s)
+    return slab, s
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0.2, out=None, alpha=1.0):
     """out = act(alpha * x @ w.T + bias), fp32; small-M layers autotune split-K + a fused combine."""
     M, K = x.shape
@@ -1179,6 +1217,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0
 
     def run(cfg):
         tile, nst, s = cfg
+        if _xpd(cfg):
+            slab, _ = _xp_gemm_into(x6p_split(x), x6p_split(w), M, N, K, nst, s)
+            sreduce_epi(slab, M, N, out, bias=bias, act=act, slope=slope, alpha=alpha)
+            return
         if s == 1:
             sgemm(KIND_DENSE, x, w, out, M, N, K, x.stride(0), w.stride(0), out.stride(0), tile=tile, nst=nst,
                   bias=bias, flags=flags, slope=slope, alpha=alpha)
@@ -1188,7 +1230,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0
               slab_stride=M * N)
         sreduce_epi(slab, M, N, out, bias=bias, act=act, slope=slope, alpha=alpha)
     cands = _cands(M, N, splittable=N % 4 == 0 and out.stride(0) % 4 == 0, K=K)
-    run(_pick(('sl', M, N, K, act, bias is not None, float(alpha)), cands, run))
+    xp = K % 32 == 0 and x.is_contiguous() and w.is_contiguous() and M * N >= XPD_MIN_MN
+    if xp:
+        cands = cands + list(XPD_CFGS)
+    run(_pick(('sl', M, N, K, act, bias is not None, float(alpha)) + (('xp',) if xp else ()), cands, run))
     return out
 
 
@@ -1201,6 +1246,10 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, *, gate=None, out=None):
 
     def run(cfg):
         tile, nst, s = cfg
+        if _xpd(cfg):
+            slab, _ = _xp_gemm_into(x6p_split(dy), x6p_split_t(w), M, Nin, Nout, nst, s)
+            sreduce_epi(slab, M, Nin, out, gate=gate)
+            return
         if s == 1:
             sgemm(KIND_DENSE_DX, dy, w, out, M, Nin, Nout, dy.stride(0), w.stride(0), out.stride(0), tile=tile,
                   nst=nst, gate=gate, flags=F_GATE if gate is not None else 0)
@@ -1210,7 +1259,10 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, *, gate=None, out=None):
               splits=s, slab_stride=M * Nin)
         sreduce_epi(slab, M, Nin, out, gate=gate)
     cands = _cands(M, Nin, splittable=Nin % 4 == 0, K=Nout)
-    run(_pick(('sx', M, Nin, Nout, gate is not None), cands, run))
+    xp = Nout % 32 == 0 and dy.is_contiguous() and w.is_contiguous() and M * Nin >= XPD_MIN_MN
+    if xp:
+        cands = cands + list(XPD_CFGS)
+    run(_pick(('sx', M, Nin, Nout, gate is not None) + (('xp',) if xp else ()), cands, run))
     return out
 
 
@@ -1223,6 +1275,13 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, *, out=None, accumulate=False):
 
     def run(cfg):
         tile, nst, s = cfg
+        if _xpd(cfg):
+            Mp = cdiv(M, 32) * 32
+            res, k = _xp_gemm_into(x6p_split_t(dy, Mp), x6p_split_t(x, Mp), Nout, Nin, Mp, nst, s,
+                                   out=out if out.is_contiguous() else None, accumulate=accumulate)
+            if k > 1 or res is not out:
+                reduce_slabs(res, out, accumulate=accumulate)
+            return
         if s == 1:
             sgemm(KIND_DENSE_DW, dy, x, out, Nout, Nin, M, dy.stride(0), x.stride(0), Nin, tile=tile, nst=nst,
                   flags=F_ACCUM if accumulate else 0)
@@ -1232,7 +1291,11 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, *, out=None, accumulate=False):
               splits=s, slab_stride=Nout * Nin)
         reduce_slabs(slab, out, accumulate=accumulate)
     cands = _cands(Nout, Nin, splittable=True, K=M)
-    run(_pick(('sdw', M, Nout, Nin, bool(accumulate)), cands, run, protect=(out,) if accumulate else ()))
+    xp = Nout * Nin >= XPD_MIN_MN
+    if xp:
+        cands = cands + list(XPD_CFGS)
+    run(_pick(('sdw', M, Nout, Nin, bool(accumulate)) + (('xp',) if xp else ()), cands, run,
+              protect=(out,) if accumulate else ()))
     return out
 
 

@@ -31,7 +31,10 @@ import torch
 from ..ops.graphs import LOCK as _GRAPH_LOCK
 from ..ops.graphs import capture as _capture
 
-BUCKETS = (1, 8, 32, 64, 128, 256, 512)
+# batch buckets: above 64 the ensemble's graph time grows about linearly with the bucket, so the steps are
+# at most 1.5x (a 84-query batch of 256 closed-loop JSON clients ran the 128 graph: 66 % of it useful,
+# bench.py ensemble_http_json_sweep)
+BUCKETS = (1, 8, 16, 32, 64, 96, 128, 192, 256, 384, 512)
 
 
 def supports(models: Sequence[object]) -> bool:
