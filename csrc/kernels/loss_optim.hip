@@ -134,6 +134,63 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* 
   }
 }
 
+// Multi-segment forms (one launch over a LOD's live arena ranges instead of one per range: at the PG-GAN
+// reference schedule's 4x4 LOD the live set is 3-4 ranges per arena, several of them a few hundred
+// elements, and Adam splits further by the per-layer equalized-LR multiplier — 11 Adam, 9 zeroing and 7
+// finite-check launches per round, profiles/pg_gan_lod3_f32_kernels_r5.txt).  blk [nblk][3] int64 =
+// (segment, first element, end element) of each block's chunk, built on the host once per live set;
+// every bound a multiple of 4 (16-B vectors).
+__global__ __launch_bounds__(256) void adam_multi_kernel(float* __restrict__ w, bf16* __restrict__ wb,
+                                                         const float* __restrict__ g, float* __restrict__ m,
+                                                         float* __restrict__ v, const long long* __restrict__ blk,
+                                                         const float* __restrict__ segp, float b1, float b2,
+                                                         float omb1, float omb2, int decoupled, float gscale,
+                                                         const int* skip, const int* step_ptr) {
+  if (skip && skip[0] != 0) return;
+  const int t = step_ptr[0];
+  const float c1 = omb1 < 1.f ? (float)(1.0 / (1.0 - pow(1.0 - (double)omb1, t))) : 1.f;
+  const float c2 = (float)(1.0 / (1.0 - pow(1.0 - (double)omb2, t)));
+  const long long* e = blk + 3 * (long long)blockIdx.x;
+  const int sg = (int)e[0];
+  const float lr = segp[4 * sg], eps = segp[4 * sg + 1], wd = segp[4 * sg + 2];
+  for (long long i = (e[1] >> 2) + threadIdx.x; i < (e[2] >> 2); i += 256) {
+    f32x4 wv = ((const f32x4*)w)[i];
+    f32x4 gv = ((const f32x4*)g)[i] * gscale;
+    if (!decoupled) gv += wd * wv;
+    f32x4 mv = ((const f32x4*)m)[i] * b1 + omb1 * gv;
+    f32x4 vv = ((const f32x4*)v)[i] * b2 + omb2 * gv * gv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
+    f32x4 upd;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) upd[q] = (mv[q] * c1) / (sqrtf(vv[q] * c2) + eps);
+    if (decoupled) upd += wd * wv;
+    wv -= lr * upd;
+    ((f32x4*)w)[i] = wv;
+    if (wb) {
+      bf16x4 o;
+      o[0] = (bf16)wv[0]; o[1] = (bf16)wv[1]; o[2] = (bf16)wv[2]; o[3] = (bf16)wv[3];
+      ((bf16x4*)wb)[i] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void zero_multi_kernel(unsigned* __restrict__ dst, const long long* __restrict__ blk) {
+  const long long* e = blk + 3 * (long long)blockIdx.x;
+  for (long long i = (e[1] >> 2) + threadIdx.x; i < (e[2] >> 2); i += 256) ((uint4*)dst)[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+__global__ __launch_bounds__(256) void nonfinite_multi_kernel(const float* __restrict__ x,
+                                                              const long long* __restrict__ blk, int* flag) {
+  const long long* e = blk + 3 * (long long)blockIdx.x;
+  int bad = 0;
+  for (long long i = (e[1] >> 2) + threadIdx.x; i < (e[2] >> 2); i += 256) {
+    const f32x4 q = ((const f32x4*)x)[i];
+    bad |= !isfinite(q[0]) | !isfinite(q[1]) | !isfinite(q[2]) | !isfinite(q[3]);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 __global__ __launch_bounds__(256) void lerp_kernel(float* __restrict__ dst, const float* __restrict__ src,
                                                    bf16* __restrict__ dstb, long long n, float t) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -723,6 +780,35 @@ extern "C" int rk_rows_reduce(const float* in, int R, long long W, int G, float*
   if (G <= 0 || G > 65535) return RK_EBADARG;
   dim3 grid((unsigned)((W + 255) / 256), (unsigned)G);
   hipLaunchKernelGGL(rows_reduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, R, W, out);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+// the multi-segment launches: nblk blocks over the chunk table blk (see adam_multi_kernel)
+extern "C" int rk_adam_multi(float* w, void* wb, const float* g, float* m, float* v, const long long* blk, int nblk,
+                             const float* segp, float b1, float b2, float omb1, float omb2, int decoupled, float gscale,
+                             const int* skip, const int* step_ptr, void* stream) {
+  if (nblk <= 0 || !blk || !segp || !step_ptr) return RK_EBADARG;
+  if ((((unsigned long long)w) | ((unsigned long long)g) | ((unsigned long long)m) | ((unsigned long long)v)) & 15)
+    return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wb, g, m, v,
+                     blk, segp, b1, b2, omb1, omb2, decoupled, gscale, skip, step_ptr);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_zero_multi(void* dst, const long long* blk, int nblk, void* stream) {
+  if (nblk <= 0 || !blk || !dst) return RK_EBADARG;
+  if (((unsigned long long)dst) & 15) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(zero_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, (unsigned*)dst, blk);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_nonfinite_multi(const float* x, const long long* blk, int nblk, int* flag, void* stream) {
+  if (nblk <= 0 || !blk || !x || !flag) return RK_EBADARG;
+  if (((unsigned long long)x) & 15) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(nonfinite_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, blk, flag);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

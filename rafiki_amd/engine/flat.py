@@ -250,6 +250,18 @@ class FlatAdam:
                     if min(b, d) > max(a, c)]
         if f.device.type == 'cuda':
             F.add_int_(self.t, 1)
+            if live is not None and len(segs) > 1 and F.seg_table_ok([(a, b) for a, b, _, _ in segs]):
+                # every live segment in one launch (per-segment lr / eps / wd from a cached device table)
+                key = (tuple(segs), self.lr, self.eps)
+                tabs = self.__dict__.setdefault('_seg_tables', {})
+                tab = tabs.get(key)
+                if tab is None and not F._capturing():
+                    tab = tabs[key] = F.SegTable(f.device, [(a, b) for a, b, _, _ in segs],
+                                                 [(self.lr * mult, self.eps * mult, wd, 0.0) for _, _, wd, mult in segs])
+                if tab is not None:
+                    F.adam_multi(f.master, f.grad, self.m, self.v, tab, wb=f.bf16, beta1=self.b1, beta2=self.b2,
+                                 decoupled=self.decoupled, step_tensor=self.t, skip_flag=self.skip_flag)
+                    return
             for a, b, wd, mult in segs:
                 if b > a:
                     F.adam_step(f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b],

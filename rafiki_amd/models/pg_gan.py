@@ -452,6 +452,13 @@ class TrialRng:
             F.add_int_(self.step, 1)
 
 
+def grad_bucket_mb() -> float:
+    """PG-GAN's data-parallel bucket size: 4 MiB (RAFIKI_GRAD_BUCKET_MB overrides) — each 3x3x512x512 conv
+    is a bucket of its own, so the lod-3 rounds skip every untouched block exactly and start reducing early
+    (docs/architecture.md, comm model; profiles/pggan_comm_model_r6.json)."""
+    return float(os.environ.get('RAFIKI_GRAD_BUCKET_MB', 4))
+
+
 class GraphedRounds:
     """hipGraph cache of training rounds (D_repeats D steps + Gs EMA + one G step).
 
@@ -700,7 +707,7 @@ class PgGan(BaseModel):
             # 4 MiB buckets: at lod 3 only a third of the arena receives gradients, and the finer buckets
             # both skip more of the untouched blocks and start reducing earlier in the backward
             # (docs/architecture.md, comm model); RAFIKI_GRAD_BUCKET_MB / the knob override it
-            bmb = knobs.get('grad_bucket_mb', os.environ.get('RAFIKI_GRAD_BUCKET_MB', 4))
+            bmb = knobs.get('grad_bucket_mb', grad_bucket_mb())
             g_ar = FlatGradAllReduce(nets.G.grad, nets.G.param_ranges(), list(nets.g_params.values()), self.world,
                                      force=force, bucket_mb=float(bmb))
             d_ar = FlatGradAllReduce(nets.D.grad, nets.D.param_ranges(), list(nets.d_params.values()), self.world,
@@ -839,10 +846,30 @@ class PgGan(BaseModel):
     def _live_of(self, flat):
         return None if self._live is None else self._live.get(id(flat))
 
+    def _seg_table(self, flat, live):
+        """The cached multi-segment chunk table of ``live`` (None: per-range launches — on the CPU, for
+        unaligned ranges, or when the table would have to be built inside a capture)."""
+        if self.device.type != 'cuda' or live is None or len(live) < 2:
+            return None
+        from rafiki_amd.ops import functional as F
+        if not F.seg_table_ok(live):
+            return None
+        tabs = self.__dict__.setdefault('_seg_tables', {})
+        key = (id(flat), tuple(live))
+        tab = tabs.get(key)
+        if tab is None and not F._capturing():
+            tab = tabs[key] = F.SegTable(self.device, live)
+        return tab
+
     def _zero_grad(self, flat):
         live = self._live_of(flat)
         if live is None:
             _zero(flat.grad)
+            return
+        tab = self._seg_table(flat, live)
+        if tab is not None:
+            from rafiki_amd.ops import functional as F
+            F.zero_multi(flat.grad, tab)
             return
         for a, b in live:
             _zero(flat.grad[a:b])
@@ -853,6 +880,10 @@ class PgGan(BaseModel):
         if self.device.type == 'cuda':
             from rafiki_amd.ops import functional as F
             F.zero_(opt.skip_flag)
+            tab = self._seg_table(flat, live)
+            if tab is not None:
+                F.nonfinite_multi(flat.grad, tab, opt.skip_flag)
+                return
             for v in views:
                 F.nonfinite_flag(v, opt.skip_flag)
         else:

@@ -1187,7 +1187,7 @@ class WinoWeights:
 # VALU-bound (the PG-GAN dense layers: 512 x 8192 at mb 512, profiles/pg_gan_lod3_f32_kernels_r5.txt); the
 # bias / activation / gate epilogue and the split-K combine ride in sreduce_epi / reduce_slabs
 XP_DENSE = -21
-XPD_MIN_MN = 1 << 20   # output elements below which the two split passes cannot pay (tiny / head layers)
+XPD_MIN_MACS = 1 << 28   # GEMM size below which the split passes cannot pay (VGG / MLP heads, tiny layers)
 XPD_CFGS = tuple((XP_DENSE, 4 * t + n, s) for t in (0, 1, 2, 3) for n in (2, 3) for s in (1, 2, 4)) + \
     tuple((XP_DENSE, 4 * t + 2, s) for t in (7, 8) for s in (1, 2, 4)) if USE_X6P else ()
 
@@ -1230,7 +1230,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, *, act=ACT_NONE, slope=0
               slab_stride=M * N)
         sreduce_epi(slab, M, N, out, bias=bias, act=act, slope=slope, alpha=alpha)
     cands = _cands(M, N, splittable=N % 4 == 0 and out.stride(0) % 4 == 0, K=K)
-    xp = K % 32 == 0 and x.is_contiguous() and w.is_contiguous() and M * N >= XPD_MIN_MN
+    xp = K % 32 == 0 and x.is_contiguous() and w.is_contiguous() and M * N * K >= XPD_MIN_MACS
     if xp:
         cands = cands + list(XPD_CFGS)
     run(_pick(('sl', M, N, K, act, bias is not None, float(alpha)) + (('xp',) if xp else ()), cands, run))
@@ -1259,7 +1259,7 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, *, gate=None, out=None):
               splits=s, slab_stride=M * Nin)
         sreduce_epi(slab, M, Nin, out, gate=gate)
     cands = _cands(M, Nin, splittable=Nin % 4 == 0, K=Nout)
-    xp = Nout % 32 == 0 and dy.is_contiguous() and w.is_contiguous() and M * Nin >= XPD_MIN_MN
+    xp = Nout % 32 == 0 and dy.is_contiguous() and w.is_contiguous() and M * Nin * Nout >= XPD_MIN_MACS
     if xp:
         cands = cands + list(XPD_CFGS)
     run(_pick(('sx', M, Nin, Nout, gate is not None) + (('xp',) if xp else ()), cands, run))
@@ -1291,7 +1291,7 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, *, out=None, accumulate=False):
               splits=s, slab_stride=Nout * Nin)
         reduce_slabs(slab, out, accumulate=accumulate)
     cands = _cands(Nout, Nin, splittable=True, K=M)
-    xp = Nout * Nin >= XPD_MIN_MN
+    xp = Nout * Nin * M >= XPD_MIN_MACS
     if xp:
         cands = cands + list(XPD_CFGS)
     run(_pick(('sdw', M, Nout, Nin, bool(accumulate)) + (('xp',) if xp else ()), cands, run,

@@ -727,6 +727,58 @@ def adam_step(w, g, m, v, *, wb=None, lr, beta1=0.9, beta2=0.999, eps=1e-8, weig
               float(c2), float(grad_scale), _p(skip_flag), _p(step_tensor), _s())
 
 
+# ---- multi-segment updates (one launch over a set of arena ranges; loss_optim.hip adam_multi_kernel)
+SEG_CHUNK = 16384   # elements per block
+
+
+class SegTable:
+    """The device chunk table [nblk][3] (segment, begin, end) of arena ranges segs [(a, b)] (+ per-segment
+    Adam parameters [nseg][4] = lr, eps, wd, 0), built once on the host.  Tables are device tensors that a
+    captured graph reads by address, so callers cache them for as long as the graphs live."""
+
+    def __init__(self, device, segs, params=None):
+        rows = []
+        for i, (a, b) in enumerate(segs):
+            assert a % 4 == 0 and b % 4 == 0 and b > a, (a, b)
+            for c in range(a, b, SEG_CHUNK):
+                rows.append((i, c, min(b, c + SEG_CHUNK)))
+        self.nblk = len(rows)
+        self.blk = torch.tensor(rows, dtype=torch.int64).to(device)
+        self.params = None if params is None else torch.tensor(params, dtype=torch.float32).to(device)
+
+
+MULTISEG = os.environ.get('RAFIKI_MULTISEG', '1') != '0'
+
+
+def seg_table_ok(segs) -> bool:
+    """Multi-segment launches apply (RAFIKI_MULTISEG=0: one launch per range): 16-B aligned bounds."""
+    return MULTISEG and bool(segs) and all(a % 4 == 0 and b % 4 == 0 and b > a for a, b in segs)
+
+
+def adam_multi(w, g, m, v, table: SegTable, *, wb=None, beta1, beta2, decoupled=False, grad_scale=1.0,
+               skip_flag=None, step_tensor):
+    """Adam over every segment of ``table`` (per-segment lr / eps / wd in table.params) in one launch; same
+    arithmetic per element as adam_step."""
+    _lib.call("rk_adam_multi", _p(w), _p(wb), _p(g), _p(m), _p(v), _p(table.blk), table.nblk, _p(table.params),
+              float(beta1), float(beta2), 1.0 - float(beta1), 1.0 - float(beta2), int(decoupled), float(grad_scale),
+              _p(skip_flag), _p(step_tensor), _s())
+
+
+def zero_multi(t, table: SegTable):
+    _lib.call("rk_zero_multi", _p(t), _p(table.blk), table.nblk, _s())
+
+
+def nonfinite_multi(x, table: SegTable, flag):
+    _lib.call("rk_nonfinite_multi", _p(x), _p(table.blk), table.nblk, _p(flag), _s())
+
+
+def _capturing() -> bool:
+    try:
+        return torch.cuda.is_current_stream_capturing()
+    except Exception:
+        return False
+
+
 def add_int_(t, v=1):
     _lib.call("rk_add_int", _p(t), int(v), _s())
 

@@ -107,7 +107,7 @@ def pg_gan_rounds(dev: torch.device, lods: Sequence[float] = (3.0, 0.0), steps: 
     backward still replays (parallel/grad_bucket.py BucketedGrads), then mean + Adam + EMA.  Timed
     windows are bracketed by barrier + synchronize; the reported time is the max over ranks."""
     from rafiki_amd.engine.flat import FlatAdam
-    from rafiki_amd.models.pg_gan import GraphedRounds, PgGan, TrainingSchedule, TrialRng
+    from rafiki_amd.models.pg_gan import GraphedRounds, PgGan, TrainingSchedule, TrialRng, grad_bucket_mb
     from rafiki_amd.ops import _lib
     from rafiki_amd.parallel import dist as D
     from rafiki_amd.parallel.context import TrialContext, use_context
@@ -128,8 +128,7 @@ def pg_gan_rounds(dev: torch.device, lods: Sequence[float] = (3.0, 0.0), steps: 
     rng = TrialRng(dev, 0)
     g_ar = d_ar = None
     if dp:
-        from rafiki_amd.config import NodeConfig
-        bmb = float(bucket_mb if bucket_mb is not None else NodeConfig().grad_bucket_mb)
+        bmb = float(bucket_mb if bucket_mb is not None else grad_bucket_mb())
         g_ar = FlatGradAllReduce(nets.G.grad, nets.G.param_ranges(), list(nets.g_params.values()), world,
                                  force=world == 1, bucket_mb=bmb)
         d_ar = FlatGradAllReduce(nets.D.grad, nets.D.param_ranges(), list(nets.d_params.values()), world,

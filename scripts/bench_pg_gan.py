@@ -39,7 +39,9 @@ def main():
         os.environ['MASTER_PORT'] = str(free_port())
         dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda', 0))
         info = D.DistInfo(0, 1, 0, 'nccl')
-    local = info.local_rank if info is not None else 0
+    # one GPU per rank over RCCL; a gloo group (the one-box rehearsal of the data-parallel path) may put
+    # several ranks on one GPU
+    local = info.local_rank % max(1, torch.cuda.device_count()) if info is not None else 0
     torch.cuda.set_device(local)
     res = pg_gan_rounds(torch.device('cuda', local), lods=[float(x) for x in a.lods.split(',')], steps=a.steps,
                         warmup=a.warmup, minibatch=a.minibatch, graph=not a.no_graph, dtype=a.dtype,

@@ -1,0 +1,79 @@
+"""Multi-segment optimizer / zeroing / finite-check launches (loss_optim.hip adam_multi_kernel, zero_multi,
+nonfinite_multi): one launch over a set of arena ranges gives bit-identical results to one launch per range
+(the PG-GAN live ranges, per-layer equalized-LR multipliers), and leaves everything outside the ranges alone."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def _flat():
+    from rafiki_amd.engine.flat import FlatParams, init_const
+    f = FlatParams(torch.device(DEV))
+    for i, n in enumerate((70000, 33, 4096, 517, 123457, 8)):
+        f.add('p{}'.format(i), (n,), init_const(0.5 + 0.1 * i), decay=i % 2 == 0, lr_mult=1.0 + 0.37 * i)
+    f.build()
+    g = torch.Generator().manual_seed(0)
+    f.master.copy_(torch.randn(f.master.shape, generator=g).to(DEV))
+    f.grad.copy_(torch.randn(f.grad.shape, generator=g).to(DEV))
+    return f
+
+
+def test_adam_multi_matches_per_segment_launches():
+    from rafiki_amd.engine.flat import FlatAdam
+    from rafiki_amd.ops import functional as F
+    out = []
+    for multi in (False, True):
+        f = _flat()
+        opt = FlatAdam(f, 1e-3, betas=(0.0, 0.99), eps=1e-8, weight_decay=1e-4)
+        opt.skip_flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+        specs = {s.name: s for s in f.specs}
+        live = f.ranges_of(['p0', 'p1', 'p4', 'p5'])
+        if not multi:   # the per-segment path: hide the table builder
+            opt._seg_tables = {}
+            orig = F.seg_table_ok
+            F.seg_table_ok = lambda segs: False
+        try:
+            for _ in range(3):
+                opt.step(live=live)
+        finally:
+            if not multi:
+                F.seg_table_ok = orig
+        torch.cuda.synchronize()
+        assert (multi and opt.__dict__.get('_seg_tables')) or not multi
+        out.append((f.master.clone(), opt.m.clone(), opt.v.clone(), specs))
+    (w0, m0, v0, sp), (w1, m1, v1, _) = out
+    assert torch.equal(w0, w1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+    # the ranges left out are untouched (p2, p3: zero moments)
+    for n in ('p2', 'p3'):
+        a, b = sp[n].offset, sp[n].offset + sp[n].numel
+        assert torch.count_nonzero(m1[a:b]) == 0
+
+
+def test_zero_and_nonfinite_multi():
+    from rafiki_amd.ops import functional as F
+    f = _flat()
+    live = f.ranges_of(['p0', 'p1', 'p4'])
+    tab = F.SegTable(f.device, live)
+    before = f.grad.clone()
+    F.zero_multi(f.grad, tab)
+    mask = torch.zeros_like(f.grad, dtype=torch.bool)
+    for a, b in live:
+        mask[a:b] = True
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(f.grad[mask]) == 0 and torch.equal(f.grad[~mask], before[~mask])
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    F.nonfinite_multi(f.grad, tab, flag)
+    assert int(flag.item()) == 0
+    a, b = live[-1]
+    f.grad[b - 1] = float('nan')     # the last element of the last range
+    F.nonfinite_multi(f.grad, tab, flag)
+    assert int(flag.item()) == 1
+    flag.zero_()
+    f.grad[b - 1] = 0.0
+    s2 = f.specs[2]
+    f.grad[s2.offset] = float('inf')  # outside the ranges: not seen
+    F.nonfinite_multi(f.grad, tab, flag)
+    assert int(flag.item()) == 0

@@ -23,7 +23,7 @@ def _rand(*shape, seed=0, scale=1.0):
 def _force(monkeypatch, key, cfg):
     from rafiki_amd.ops import autotune
     from rafiki_amd.ops import f32 as S
-    monkeypatch.setattr(S, 'XPD_MIN_MN', 0)
+    monkeypatch.setattr(S, 'XPD_MIN_MACS', 0)
     monkeypatch.setitem(autotune._cache, key, cfg)
 
 
