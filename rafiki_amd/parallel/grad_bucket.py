@@ -318,7 +318,9 @@ class BucketedGrads:
                 pos[0] += 1
         seen, _ = self._observe(None, extra=note)
         if seen or self.plan['count'] is None:
-            self.plan.update(count=dict(seen), order=sorted(seen, key=lambda b: last[b]))
+            # 'at': where in the pass each bucket completed (fraction of the contributions; the comm model)
+            self.plan.update(count=dict(seen), order=sorted(seen, key=lambda b: last[b]),
+                             at={b: (last[b] + 1) / max(1, pos[0]) for b in last})
         self.plan['traces'] += 1
         self._traced = True
 

@@ -5,10 +5,11 @@ total_kimg=2 schedule) and lod 0 (32x32, whole network) and in which order the b
 (FlatGradAllReduce.traced, the plan the overlapped rounds run), for several bucket sizes.  Then, per
 rank count N = 2 / 4 / 8, it models one round:
 
-  compute   the per-rank round shrinks with the per-rank minibatch: T(N) = T1 * (mb/N) / mb (T1 = the
-            measured 1-GPU round, --t1-lod3 / --t1-lod0 ms; linear scaling is optimistic for compute at
-            small per-rank batches, so the comm SHARE below is an upper bound); the D step is ~70 % of a
-            round, its backward ~60 % of the step, likewise for G;
+  compute   the MEASURED 1-GPU round at the per-rank minibatch mb / N (scripts/bench_pg_gan.py --minibatch,
+            profiles/pg_gan_dp_rank_shapes_r6.jsonl: lod 3 at mb 512 / 256 / 128 / 64 = 3.70 / 2.72 / 2.01 /
+            1.67 ms, lod 0 at mb 64 / 32 / 16 / 8 = 37.0 / 21.8 / 13.2 / 8.8 ms — far from linear in mb:
+            small per-rank batches leave the GPU underused); the D step is ~70 % of a round, its backward
+            ~60 % of the step, likewise for G;
   buckets   bucket i completes at a point of its step's backward proportional to the position of its
             last gradient contribution in the traced order;
   reduce    a ring all-reduce moves 2 (N-1)/N of the bucket over one xGMI link per hop: ~100 GB/s
@@ -17,7 +18,8 @@ rank count N = 2 / 4 / 8, it models one round:
             stream); what is left after the step's backward is EXPOSED (the optimizer waits for it).
             Serialised = every reduce after the backward (the round-5 design).
 
-Prints one JSON document: exposed comm ms and its share of the per-rank round, per LOD, N and bucket size.
+Prints one JSON document: exposed comm ms and its share of the per-rank round, and the round's speedup over one
+GPU, per LOD, N and bucket size.
 """
 import argparse
 import json
@@ -62,9 +64,7 @@ def trace(bucket_mb):
             res = {}
             for name, ar in ars.items():
                 plan = [p for t, p in ar._plans.items() if t[0] == lod][0]
-                n = len(plan['seq'])
-                last = {b: i for i, b in enumerate(plan['seq'])}
-                res[name] = [{'mib': 4 * (ar.buckets[b][1] - ar.buckets[b][0]) / 2 ** 20, 'at': (last[b] + 1) / n}
+                res[name] = [{'mib': 4 * (ar.buckets[b][1] - ar.buckets[b][0]) / 2 ** 20, 'at': plan['at'][b]}
                              for b in plan['order']]
             out['lod{}'.format(int(lod))] = res
         for ar in ars.values():
@@ -86,13 +86,14 @@ def model(buckets, t_bwd, t_after, n, bw_gbs, lat_us):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--buckets', default='4,8,16,32')
-    ap.add_argument('--t1-lod3', type=float, default=3.82, help='measured 1-GPU round, ms (mb 512)')
-    ap.add_argument('--t1-lod0', type=float, default=37.5, help='measured 1-GPU round, ms (mb 64)')
+    ap.add_argument('--t-lod3', default='3.70,2.717,2.012,1.666', help='measured rounds (ms) at mb 512/N, N=1,2,4,8')
+    ap.add_argument('--t-lod0', default='37.0,21.75,13.203,8.834', help='measured rounds (ms) at mb 64/N, N=1,2,4,8')
     ap.add_argument('--bw-gbs', type=float, default=100.0)
     ap.add_argument('--latency-us', type=float, default=25.0)
     a = ap.parse_args()
-    t1 = {'lod3': a.t1_lod3, 'lod0': a.t1_lod0}
-    out = {'assumptions': {'t1_ms': t1, 'ring_bw_gbs': a.bw_gbs, 'latency_us': a.latency_us,
+    rt = {lod: dict(zip((1, 2, 4, 8), [float(x) for x in v.split(',')])) for lod, v in (('lod3', a.t_lod3),
+                                                                                       ('lod0', a.t_lod0))}
+    out = {'assumptions': {'per_rank_round_ms': rt, 'ring_bw_gbs': a.bw_gbs, 'latency_us': a.latency_us,
                            'D_share_of_round': 0.7, 'backward_share_of_step': 0.6}, 'bucket_mb': {}}
     for bmb in [float(x) for x in a.buckets.split(',')]:
         tr = trace(bmb)
@@ -102,7 +103,7 @@ def main():
             rows = {'live_buckets': {k: len(v) for k, v in tr[lod].items()},
                     'live_mib': {k: round(sum(b['mib'] for b in v), 1) for k, v in tr[lod].items()}}
             for n in (2, 4, 8):
-                rnd = t1[lod] / n
+                rnd = rt[lod][n]
                 exp = ser = 0.0
                 for name, share in (('D', 0.7), ('G', 0.3)):
                     step = rnd * share
@@ -111,7 +112,8 @@ def main():
                     ser += s
                 rows['N{}'.format(n)] = {'per_rank_round_ms': round(rnd, 3), 'exposed_ms': round(exp, 3),
                                          'exposed_share': round(exp / (rnd + exp), 3), 'serialised_ms': round(ser, 3),
-                                         'serialised_share': round(ser / (rnd + ser), 3)}
+                                         'serialised_share': round(ser / (rnd + ser), 3),
+                                         'speedup_vs_1gpu': round(rt[lod][1] / (rnd + exp), 2)}
             per[lod] = rows
         out['bucket_mb'][str(bmb)] = per
     print(json.dumps(out, indent=1))
