@@ -10,7 +10,7 @@ if [ "$1" != "prof" ]; then
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 \
     || { tail -5 $O/smoke.log; exit 1; }
   tail -1 $O/smoke.log
-  timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
+  timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
   tail -1 $O/bench.log | cut -c1-300
 fi
 if [ "$1" = "prof" ]; then
