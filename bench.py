@@ -307,6 +307,16 @@ def phase_serving(db, sub_id, dev, k=4, batch=256, iters=30, http_seconds=3.0):
     return out
 
 
+def _progress(info, msg):
+    """A progress line on stderr (rank 0; stdout carries only the final JSON line)."""
+    if info.is_main:
+        sys.stderr.write('[bench {:.0f}s] {}\n'.format(time.perf_counter() - _T0, msg))
+        sys.stderr.flush()
+
+
+_T0 = time.perf_counter()
+
+
 def _configs(args, world):
     if args.configs == 'none':
         return []
@@ -398,7 +408,10 @@ def main():
         pre = D.preflight(info, timeout_s=float(os.environ.get('RAFIKI_PREFLIGHT_TIMEOUT_S', '120')),
                           group=control_group(info))
 
+    _progress(info, 'phase 1: VGG-small training step (capture + {} warmup + {} timed)'.format(args.warmup,
+                                                                                               args.steps))
     th = phase_throughput(args, info, dev)
+    _progress(info, 'phase 1 done: {:.4f} ms/step'.format(th['elapsed'] * 1000.0 / args.steps))
     B = args.batch
     ms = th['elapsed'] * 1000.0 / args.steps
     ips_trial = B * args.steps / th['elapsed']
@@ -411,21 +424,27 @@ def main():
     tag = os.environ.get('MASTER_PORT', '0') if world > 1 else str(os.getpid())
     root = os.path.join(tempfile.gettempdir(), 'rafiki_bench_{}'.format(tag))
     if args.trials > 0:
+        _progress(info, 'phase 2: VggSmallTrial trials')
         trials = phase_trials(args, info, root, 'VggSmallTrial', args.trials, TRAIN_URI, TEST_URI)
     if args.probe_trials > 0:
+        _progress(info, 'phase 2b: overhead-probe trials')
         probe = phase_trials(args, info, root, 'VggSmallProbe', args.probe_trials, PROBE_TRAIN_URI, PROBE_TEST_URI,
                              warm=False)
     src = probe or trials
     if src is not None and info.is_main and not args.no_serving:
+        _progress(info, 'phase 3: ensemble serving (device, then HTTP)')
         serving = phase_serving(src['db'], src['sub'], dev)
 
     which = _configs(args, world)
     cfgs = {}
     if 'pggan' in which and n_devices == world:
         D.barrier(info)
+        _progress(info, 'phase 4: PG-GAN rounds' + (' (data parallel x{})'.format(world) if world > 1 else ''))
         cfgs['pg_gan'] = phase_pg_gan(args, info, dev)
-    if info.is_main and world == 1:
+    if info.is_main and world == 1 and ('mlp' in which or 'skdt' in which):
+        _progress(info, 'phase 4: FeedForward trial, SkDt trials')
         cfgs.update(phase_small_configs(args, dev, which))
+    _progress(info, 'done')
 
     if info.is_main:
         out = {

@@ -23,6 +23,7 @@ import fcntl
 import hashlib
 import json
 import os
+import sys
 import threading
 
 import torch
@@ -34,6 +35,7 @@ _cache = {}
 _loaded = False
 _disk_mtime = [None]
 stats = {'tuned': 0, 'seconds': 0.0, 'candidates': 0, 'loaded': 0, 'reloads': 0}
+_last_note = [0.0]
 ENABLED = os.environ.get('RAFIKI_AUTOTUNE', '1') != '0'
 REPS = 3      # timed replays per candidate and pass (at least 5 when timing a captured graph)
 PASSES = 2    # sweeps over the candidates, min per candidate (the first also absorbs clock ramp-up)
@@ -288,6 +290,11 @@ def _tune_locked(key, candidates, run):
         stats['tuned'] += 1
         stats['candidates'] += len(candidates)
         stats['seconds'] += _time.perf_counter() - t_start
+        now = _time.perf_counter()
+        if now - _last_note[0] > 30.0:   # a long in-process tuning pass says it is alive (stderr)
+            _last_note[0] = now
+            sys.stderr.write('[autotune] {} shapes tuned in {:.0f} s\n'.format(stats['tuned'], stats['seconds']))
+            sys.stderr.flush()
     return best
 
 
