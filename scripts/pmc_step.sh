@@ -11,10 +11,10 @@ OUT=gpurun_out/pmc_step
 mkdir -p $OUT
 export RAFIKI_TUNE_CACHE=$PWD/$OUT/tune.json
 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $OUT/t -o run -- \
-  python3 bench.py --steps 20 --warmup 5 --trials 0 --probe-trials 0 --no-serving > $OUT/t.log 2>&1
+  python3 bench.py --steps 20 --warmup 5 --trials 0 --probe-trials 0 --no-serving --configs none > $OUT/t.log 2>&1
 python3 scripts/trace_steps.py $(find $OUT/t -name '*kernel_trace.csv' | head -1) --steps 20 \
   --csv $OUT/durations.csv > $OUT/durations.txt
-ARGS="bench.py --steps 2 --warmup 1 --trials 0 --probe-trials 0 --no-serving"
+ARGS="bench.py --steps 2 --warmup 1 --trials 0 --probe-trials 0 --no-serving --configs none"
 timeout -k 10 180 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA \
   SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY GRBM_GUI_ACTIVE \
   --output-format csv -d $OUT/p0 -o run -- python3 $ARGS > $OUT/p0.log 2>&1

@@ -7,7 +7,7 @@ TAG=$1; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/t -o run -- \
-  python3 bench.py --steps 20 --warmup 5 --trials 0 --probe-trials 0 --no-serving "$@" > $OUT/t.log 2>&1
+  python3 bench.py --steps 20 --warmup 5 --trials 0 --probe-trials 0 --no-serving --configs none "$@" > $OUT/t.log 2>&1
 python3 scripts/trace_steps.py $(find $OUT/t -name '*kernel_trace.csv' | head -1) --steps 20 \
   --csv $OUT/durations.csv --seq $OUT/seq.txt > $OUT/durations.txt
 rm -rf $OUT/t
