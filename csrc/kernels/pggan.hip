@@ -438,9 +438,9 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __r
     for (int k = 0; k < G; ++k) {
       if (k >= g) break;
       st8(out + smp[k] * PCp + (long long)p * Cp + c8 * 8, xv[k]);
-      if (c8 == 0) {
+      if (c8 == 0) {                        // [f, 0 ...] over the padded tail C .. Cp-1 (8 per store)
         float f[8] = {S0 / (float)PC, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        st8(out + smp[k] * PCp + (long long)p * Cp + C, f);
+        for (int t = C; t < Cp; t += 8, f[0] = 0.f) st8(out + smp[k] * PCp + (long long)p * Cp + t, f);
       }
     }
     return;
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void mbstd_vec_b_kernel(int mode, const T* __r
     st8(out2 + smp[k] * PCp + (long long)p * Cp + c8 * 8, av[k]);
     if (c8 == 0) {
       float f[8] = {S1 * inv, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      st8(out2 + smp[k] * PCp + (long long)p * Cp + C, f);
+      for (int t = C; t < Cp; t += 8, f[0] = 0.f) st8(out2 + smp[k] * PCp + (long long)p * Cp + t, f);
     }
   }
 }
@@ -518,7 +518,7 @@ int mbstd_launch(int mode, const void* x, const void* a, const void* b, int N, i
   if (g < 1 || g > MB_MAXG || segs < 1 || N % segs || (N / segs) % g || Cp <= C || mode < 0 || mode > 2)
     return RK_EBADARG;
   const dim3 grid(N / g), block(256);
-  if (part && C % 8 == 0 && Cp == C + 8) {
+  if (part && C % 8 == 0 && (Cp - C) % 8 == 0 && Cp - C <= 64) {   // the feature + zero tail in 8-wide stores
     const int groups = N / g;
     const int chunks = std::max(1, std::min(16, 1024 / groups));
     const T* gout = (const T*)(mode == 1 ? a : b);

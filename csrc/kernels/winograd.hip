@@ -25,6 +25,7 @@
 //   * epilogues as in the direct kernels (csrc/kernels/sgemm.hip): bias, ReLU, BN statistics
 //     (fp64 slot atomics), and for the data gradient FLAG_BNB / FLAG_BNP (ReLU mask + BN-backward
 //     sums of the BN+ReLU(+2x2 max-pool) layer below).
+#include <type_traits>
 #include "common.h"
 
 namespace {
@@ -59,9 +60,10 @@ constexpr unsigned WOOB = 0x80000000u;
 // rows x one pair of a ds_read2st64_b64 lane group (banks mod 32) and the 16 rows x two pairs of a
 // ds_read_b64 group (banks mod 64) then hit distinct banks
 RK_DEV int w_swz(int row) { return ((row >> 2) & 3) << 1; }
-// the weight gradient's stores (a wave: 32 channel rows x 2 tiles): rows r, r + 8, r + 16, r + 24 of a bank
-// group take four different even offsets (conflict-free ds_write_b32; see winograd4.hip swzw)
-RK_DEV int w_swzw(int row) { return (((row >> 3) & 1) << 2) | (((row >> 4) & 1) << 1); }
+// the weight gradient's column swizzle (winograd4.hip swzw: stores conflict-free under the (a/4) mod 32
+// banking of ds_write2st64_b32, 16-row fragment reads under that of ds_read2st64_b64; row bit 4 swaps the
+// two columns of a pair, undone in registers by the reading wave)
+RK_DEV int w_swzw(int row) { return (((row >> 2) & 1) << 1) | (((row >> 3) & 1) << 2) | ((row >> 4) & 1); }
 
 RK_DEV __amdgpu_buffer_rsrc_t w_rsrc(const float* base, unsigned long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)(unsigned)bytes, 0x00020000);
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
   const int nch = (t_end - t_begin + WKC - 1) / WKC;
   // tile within the chunk, channel within the block: a wave covers 2 tiles x 32 consecutive channels, so
   // each buffer load moves two whole 128-B lines (the F(4x4) weight gradient measured 1.19-1.29x from the
-  // same remap, profiles/wino4_wgrad_remap_r5.jsonl); LDS stores stay at most 2-way conflicted
+  // same remap, profiles/wino4_wgrad_remap_r5.jsonl); LDS stores conflict-free under w_swzw
   const int tt = (tid >> 5) & 7, ch = (tid & 31) + 32 * (tid >> 8);
   const bool cok = co0 + ch < p.Co, iok = ci0 + ch < p.Ci;
   const __amdgpu_buffer_rsrc_t dyr = w_rsrc(p.dy, p.dybytes), xr = w_rsrc(p.x, p.xbytes);
@@ -423,11 +425,13 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
   }
   __syncthreads();
   const int ar = wm * 16 + (lane & 15), br = wn * 32 + (lane & 15);
-  const int ka = (2 * (lane >> 4)) ^ w_swzw(ar), kb = (2 * (lane >> 4)) ^ w_swzw(br);
-  const int kb16 = (2 * (lane >> 4)) ^ w_swzw(br + 16);   // rows br + 16: bit 4 of the row is in w_swzw
-  for (int c = 0; c < nch; ++c) {
-    const int st = c & 1;
-    if (c + 1 < nch) load(c + 1);
+  const int ka = (2 * (lane >> 4)) ^ (w_swzw(ar) & 6), kb = (2 * (lane >> 4)) ^ (w_swzw(br) & 6);
+  const int kb16 = (2 * (lane >> 4)) ^ (w_swzw(br + 16) & 6);
+  // pair swap of the B fragment relative to A: row bit 4 of ar is wm's (wave-uniform), of br / br + 16 it is
+  // 0 / 1, so the rows br swap when wm is odd and the rows br + 16 when it is even
+  const bool swodd = (wm & 1) != 0;
+  auto mfma = [&](int st, auto swc) __attribute__((always_inline)) {
+    constexpr int SWO = decltype(swc)::value;   // rows br (nb 0) swap iff SWO, rows br + 16 iff !SWO
 #pragma unroll
     for (int q = 0; q < 16; q += 2) {
       f32x2 a[2], bv[2][2];
@@ -443,11 +447,23 @@ __global__ __launch_bounds__(512, 1) void wino_wgrad_kernel(const WwParams p) {
         for (int e = 0; e < 2; ++e)
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb)
-            acc[q + e][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][nb][s], acc[q + e][nb], 0, 0, 0);
+            acc[q + e][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][nb][s ^ nb ^ SWO], acc[q + e][nb],
+                                                                0, 0, 0);
     }
-    if (c + 1 < nch) store(st ^ 1);
-    __syncthreads();
-  }
+  };
+  auto chunks = [&](auto swc) __attribute__((always_inline)) {   // per SWO, chosen once per wave
+    for (int c = 0; c < nch; ++c) {
+      const int st = c & 1;
+      if (c + 1 < nch) load(c + 1);
+      mfma(st, swc);
+      if (c + 1 < nch) store(st ^ 1);
+      __syncthreads();
+    }
+  };
+  if (swodd)
+    chunks(std::integral_constant<int, 1>{});
+  else
+    chunks(std::integral_constant<int, 0>{});
 
   // G^T dU G per (co, ci) in registers -> the 9 taps
   float* outp = p.out + (long long)split * p.slab;

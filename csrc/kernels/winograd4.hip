@@ -30,6 +30,7 @@
 //     1 KiB per wave-instruction over whole cache lines, instead of 8 B per lane scattered over a
 //     32-B segment of each (position, channel) row — those loads cost about as much time as the
 //     MFMAs on the 32x32 layers (profiles/wino4_load_breakdown_r5.jsonl).
+#include <type_traits>
 #include "common.h"
 #include <cstdlib>
 
@@ -67,12 +68,19 @@ constexpr unsigned OOB = 0x80000000u;
 constexpr int W4_PRO_MAXC = 512;   // normalise-on-load: input channels whose BN coefficients are staged in LDS
 
 RK_DEV int swz(int row) { return ((row >> 2) & 3) << 1; }
-// the weight-gradient kernels' column swizzle: a wave stores 32 rows (channels) x 2 tiles, so the four rows
-// of each bank group (r, r + 8, r + 16, r + 24) take four different even offsets and the two tiles fill the
-// odd ones (conflict-free ds_write_b32; swz left those rows pairwise equal: 2-way, 21.8 % of the LDS cycles
-// in profiles/vgg_small_f32_step_pmc_r5.txt); the 16-row fragment reads stay conflict-free (rows r and
-// r + 8 differ by 4 in the offset)
-RK_DEV int swzw(int row) { return (((row >> 3) & 1) << 2) | (((row >> 4) & 1) << 1); }
+// the weight-gradient kernels' column swizzle (tile column t of channel row r is stored at t ^ swzw(r)).
+// The compiler pairs the stores into ds_write2st64_b32 and the fragment reads into ds_read2st64_b64, both
+// banked (a/4) mod 32 (MI355X_MICROARCH.md §LDS): a store wave-half writes 32 consecutive rows of one
+// tile, so the 8 rows of a bank group (equal r mod 4) need 8 different columns -> swzw is a bijection of
+// row bits 2-4; a 16-lane read group takes 16 consecutive rows x one column pair, so the 4 rows of a bank
+// group need 4 different pairs -> bits 2 and 3 land on the pair bits (2, 4).  Bit 4 lands on bit 0: it
+// swaps the two columns of a pair, which is uniform over a wave's 16-row fragment (rows w*16 + 0..15), so a
+// wave whose A and B fragments differ in it swaps its B pair in registers (wswap).  Round 5's swz (bits
+// 2-3) left the stores 2-way (21.8 % of the LDS cycles, profiles/vgg_small_f32_step_pmc_r5.txt); a swizzle
+// on bits 3-4 priced for 64 banks made both 2-way (49.5 %, the first round-6 build).
+RK_DEV int swzw(int row) { return (((row >> 2) & 1) << 1) | (((row >> 3) & 1) << 2) | ((row >> 4) & 1); }
+// the pair-aligned column offset of a fragment read of row r (the pair-swap bit dropped)
+RK_DEV int swzp(int row) { return swzw(row) & 6; }
 
 RK_DEV __amdgpu_buffer_rsrc_t rsrc(const float* base, unsigned long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)(unsigned)bytes, 0x00020000);
@@ -637,8 +645,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   const int nch = (t_end - t_begin + KC - 1) / KC;
   // (tile, channel) item of the thread: a wave covers 2 tiles x 32 consecutive channels, so every buffer
   // load of dy / x moves two whole 128-B lines (lanes = 8 tiles x 8 channels touched 8 lines for 32 B
-  // each, 4x the cache-line traffic through the texture path for the same bytes).  The LDS stores stay
-  // at most 2-way bank-conflicted under the column swizzle (free for ds_write_b32).
+  // each, 4x the cache-line traffic through the texture path for the same bytes).  The LDS stores and the
+  // fragment reads are bank-conflict-free under the column swizzle swzw.
   static_assert(PY == 1 && PX == 1, "one dy patch and at most one x window per thread and chunk");
   const int tt = (tid >> 5) & 7, ch = (tid & 31) + 32 * (tid >> 8);
   const __amdgpu_buffer_rsrc_t dyr = rsrc(p.dy, p.dybytes), xr = rsrc(p.x, p.xbytes);
@@ -646,7 +654,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   float gy[PY][16], raw[PX][36];
   unsigned xv[PX];                          // in-image rows (bits 0-5) / columns (bits 8-13) of each x window
   float xpc[PX][2];                         // normalise-on-load coefficients of the thread's input channel
-  auto load = [&](int c) {
+  auto load = [&](int c) __attribute__((always_inline)) {
     const int t = t_begin + c * KC + tt;
     const unsigned okm = t < t_end ? 1u : 0u;
     const int n = (int)(((float)t + 0.5f) * p.invTHW);   // exact below 2^22 tiles
@@ -699,7 +707,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
       }
     }
   };
-  auto store = [&]() {
+  auto store = [&]() __attribute__((always_inline)) {
     const bool yact = YALL || threadIdx.x < BCO * KC, xact = XALL || threadIdx.x < BCI * KC;
 #pragma unroll
     for (int h = 0; h < PY && yact; ++h) {
@@ -759,9 +767,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
   }
   __syncthreads();
   const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
-  const int ka = (2 * (lane >> 4)) ^ swzw(ar), kb = (2 * (lane >> 4)) ^ swzw(br);
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) load(c + 1);
+  const int ka = (2 * (lane >> 4)) ^ swzp(ar), kb = (2 * (lane >> 4)) ^ swzp(br);
+  const bool wswap = ((swzw(ar) ^ swzw(br)) & 1) != 0;   // wave-uniform (row bit 4 = wm / wn parity)
+  // the chunk's MFMAs; SW (= wswap, wave-uniform) pairs A's column s with B's column s ^ 1
+  auto mfma = [&](auto swc) __attribute__((always_inline)) {
+    constexpr int SW = decltype(swc)::value;
 #pragma unroll
     for (int q = 0; q < 36; q += 4) {
       f32x2 a[4], bv[4];
@@ -774,14 +784,25 @@ __global__ __launch_bounds__(64 * WM * WN, MINW) void wino4_wgrad_kernel(const W
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s], acc[q + e], 0, 0, 0);
+          acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s ^ SW], acc[q + e], 0, 0, 0);
     }
-    if (c + 1 < nch) {
+  };
+  // the chunk loop is instantiated per SW and chosen once per wave (a choice per chunk costs registers)
+  auto chunks = [&](auto swc) __attribute__((always_inline)) {
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) load(c + 1);
+      mfma(swc);
+      if (c + 1 < nch) {
+        __syncthreads();
+        store();
+      }
       __syncthreads();
-      store();
     }
-    __syncthreads();
-  }
+  };
+  if (wswap)
+    chunks(std::integral_constant<int, 1>{});
+  else
+    chunks(std::integral_constant<int, 0>{});
 
   // G^T dU G per (co, ci) in registers -> the 9 taps
   float* outp = p.out + (long long)split * p.slab;
@@ -914,8 +935,10 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
 #pragma unroll
   for (int q = 0; q < 36; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int ar = wm * 16 + (lane & 15), br = wn * 16 + (lane & 15);
-  const int ka = (2 * (lane >> 4)) ^ swzw(ar), kb = (2 * (lane >> 4)) ^ swzw(br);
-  auto mfma = [&](int st) {
+  const int ka = (2 * (lane >> 4)) ^ swzp(ar), kb = (2 * (lane >> 4)) ^ swzp(br);
+  const bool wswap = ((swzw(ar) ^ swzw(br)) & 1) != 0;   // wave-uniform (row bit 4 = wm / wn parity)
+  auto mfma_sw = [&](int st, auto swc) __attribute__((always_inline)) {
+    constexpr int SW = decltype(swc)::value;
 #pragma unroll
     for (int q = 0; q < 36; q += 4) {
       f32x2 a[4], bv[4];
@@ -928,7 +951,7 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s], acc[q + e], 0, 0, 0);
+          acc[q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e][s], bv[e][s ^ SW], acc[q + e], 0, 0, 0);
     }
   };
 
@@ -939,16 +962,22 @@ __global__ __launch_bounds__(256, 1) void wino4_wgrad_pipe_kernel(const W4wParam
       load(1, gB, rB);
       store(0, gA, rA);
       __syncthreads();
-      for (int c = 0; c < nch; c += 2) {
-        load(c + 2, gA, rA);
-        mfma(0);                           // chunk c
-        store(1, gB, rB);                  // chunk c + 1, in the MFMAs' shadow
-        __syncthreads();
-        load(c + 3, gB, rB);
-        mfma(1);                           // chunk c + 1 (zeros past the end)
-        store(0, gA, rA);                  // chunk c + 2
-        __syncthreads();
-      }
+      auto chunks = [&](auto swc) __attribute__((always_inline)) {   // per SW, chosen once per wave
+        for (int c = 0; c < nch; c += 2) {
+          load(c + 2, gA, rA);
+          mfma_sw(0, swc);                 // chunk c
+          store(1, gB, rB);                // chunk c + 1, in the MFMAs' shadow
+          __syncthreads();
+          load(c + 3, gB, rB);
+          mfma_sw(1, swc);                 // chunk c + 1 (zeros past the end)
+          store(0, gA, rA);                // chunk c + 2
+          __syncthreads();
+        }
+      };
+      if (wswap)
+        chunks(std::integral_constant<int, 1>{});
+      else
+        chunks(std::integral_constant<int, 0>{});
     }
   }
 

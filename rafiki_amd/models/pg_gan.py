@@ -14,7 +14,9 @@ predict contract ([grid_w, grid_h, n_images] -> JPEG file paths).  Re-designed f
   transposed-conv launch reading the half-resolution input, ``Conv1_down`` (conv3x3 + downscale2d)
   one 4x4 stride-2 gather conv — 1/2.25 of the full-resolution MACs, no 2x tensor, and their
   backward passes are the same family; the LOD blends' upscale2d / downscale2d are native kernels;
-  the 513-channel minibatch-stddev conv runs on the non-power-of-two channel path (padded to 520);
+  the 513-channel minibatch-stddev conv is zero-padded to 520 input channels (MBSTD_PAD = 8; 32 -> 544
+  makes its three passes eligible for the pre-split X6 GEMMs too, which measured no faster:
+  profiles/pg_gan_mbstd_pad_ab_r6.txt);
 * equalized learning rate by re-parameterisation (arena holds c*w, Adam steps with lr*c, eps*c);
 * data parallel (``DATA_PARALLEL = True``): when the worker group has N ranks the trial's minibatch
   is split across them (pg_gans.py:290-293) and gradients are averaged by bucketed RCCL
@@ -64,6 +66,12 @@ from rafiki_amd.parallel.context import current as trial_context
 
 def _pad8(n):
     return (int(n) + 7) // 8 * 8
+
+
+# input channels of the minibatch-stddev conv (512 + 1) are zero-padded to a multiple of this (the
+# Winograd paths need C % 8 == 0; 32 would also admit the pre-split X6 GEMMs, whose K step is 32: same-box
+# lod 3 3.90 / 3.91 ms at 32 vs 3.88 / 3.89 at 8, profiles/pg_gan_mbstd_pad_ab_r6.txt)
+MBSTD_PAD = int(os.environ.get('RAFIKI_MBSTD_PAD', '8'))
 
 
 # ============================================================================== networks
@@ -144,7 +152,7 @@ class PgNetworks:
             self._w(D, '%dx%d/Conv1_down' % (2 ** res, 2 ** res), (c1, 9 * c0), 9 * c0)
         n1, n0 = self.nf(1), self.nf(0)
         cm = n1 + 1 if self.mbstd_group_size > 1 else n1
-        cm_p = _pad8(cm)
+        cm_p = (cm + MBSTD_PAD - 1) // MBSTD_PAD * MBSTD_PAD
         self.mbstd_cp = cm_p
         # [Cout][tap][Cin_p] with the padded input channels zeroed
         D.add('4x4/Conv/weight', (n1, 9, cm_p), _zero_tail_init(math.sqrt(2) / math.sqrt(9 * cm), cm),
@@ -260,7 +268,7 @@ class PgNetworks:
                 y = self._conv(P, 'FromRGB_lod%d' % (self.L - res + 1), A.downscale2d(img), taps=1, lrelu=0.2)
                 x = x + (y - x) * frac
         if self.mbstd_group_size > 1:
-            x = A.minibatch_stddev(x, self.mbstd_group_size, pad_to=8, segs=segs)
+            x = A.minibatch_stddev(x, self.mbstd_group_size, pad_to=MBSTD_PAD, segs=segs)
         x = self._conv(P, '4x4/Conv', x, lrelu=0.2)
         N = x.shape[0]
         x = self._dense(P, '4x4/Dense0', x.reshape(N, -1), lrelu=0.2)

@@ -533,20 +533,22 @@ def _mbstd64(x, g, segs, extra):
     return torch.cat(out, 0)
 
 
-@pytest.mark.parametrize("N,H,C,segs", [(64, 4, 512, 1), (16, 4, 512, 2), (8, 4, 24, 1), (12, 2, 40, 3),
-                                        (32, 4, 128, 2)])
-def test_minibatch_stddev_fp32_vs_fp64(N, H, C, segs):
+@pytest.mark.parametrize("N,H,C,segs,pad", [(64, 4, 512, 1, 8), (16, 4, 512, 2, 8), (8, 4, 24, 1, 8),
+                                            (12, 2, 40, 3, 8), (32, 4, 128, 2, 8), (64, 4, 512, 1, 32),
+                                            (16, 4, 512, 2, 32), (12, 2, 40, 3, 32)])
+def test_minibatch_stddev_fp32_vs_fp64(N, H, C, segs, pad):
     """mbstd_vec_a / _b kernels (fp32 instantiation, pg_gans.py:1070-1082): forward, backward and
-    backward-of-backward (the WGAN-GP penalty differentiates through it) <= 1e-5 against fp64."""
+    backward-of-backward (the WGAN-GP penalty differentiates through it) <= 1e-5 against fp64; pad 32 =
+    the model's 544-channel conv input (feature + 31 zero channels written by the vector kernels)."""
     from rafiki_amd.ops import autograd as A
     g = torch.Generator().manual_seed(N * H + C)
     x = torch.randn(N, H, H, C, generator=g)
-    cp = C + 1 + (-(C + 1)) % 8
+    cp = C + 1 + (-(C + 1)) % pad
     Wt = torch.randn(N, H, H, cp, generator=g)
     V = torch.randn(N, H, H, C, generator=g)
     xd = x.to(DEV).requires_grad_(True)
     Wd = Wt.to(DEV).requires_grad_(True)
-    out = A.minibatch_stddev(xd, 4, pad_to=8, segs=segs)
+    out = A.minibatch_stddev(xd, 4, pad_to=pad, segs=segs)
     (gx,) = torch.autograd.grad((out * Wd).sum(), xd, create_graph=True)
     (gx * V.to(DEV)).sum().backward()
     x64 = x.double().requires_grad_(True)
