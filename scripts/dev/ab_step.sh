@@ -10,7 +10,7 @@ export RAFIKI_TUNE_CACHE=$PWD/$O/tune_db.json
 run() {
   local spec="$1" i="$2"
   [ "$spec" = "-" ] && spec=""
-  env $spec timeout -k 10 400 python -u bench.py --steps 30 --warmup 5 --trials 0 --probe-trials 0 --no-serving \
+  env $spec timeout -k 10 400 python -u bench.py --steps 30 --warmup 5 --trials 0 --probe-trials 0 --no-serving --configs none \
     > $O/run$i.log 2>&1 || { tail -5 $O/run$i.log; return 1; }
   python3 -c "import json,sys; d=json.loads(open('$O/run$i.log').read().strip().splitlines()[-1]); print('%-40s %.4f ms  %.0f img/s' % ('$spec' or 'baseline', d['ms_per_step'], d['value']))" >> $O/results.txt
 }
