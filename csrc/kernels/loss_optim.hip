@@ -340,6 +340,35 @@ __global__ __launch_bounds__(256) void rows_reduce_kernel(const float* __restric
   out[(long long)g * W + c] = (a0 + a1) + (a2 + a3);
 }
 
+// out (+)= scale * sum_r in[r] for in [R][n], R > 16, in ONE pass (replaces rows_reduce + reduce_slabs): a
+// block owns 64 columns (16 float4 lanes) x 16 row lanes; row lane l sums rows l, l + 16, ... (two chains),
+// then lane 0 of each column folds the 16 lane sums in order — deterministic, no cross-block dependence.
+__global__ __launch_bounds__(256) void fold_rows_kernel(const float* __restrict__ in, int R, long long n,
+                                                        float* __restrict__ out, int accumulate, float scale) {
+  const int q = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const long long c = (long long)blockIdx.x * 64 + 4 * q;
+  __shared__ f32x4 red[16][16];
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  if (c < n) {
+    int r = rl;
+    for (; r + 16 < R; r += 32) {
+      a += *(const f32x4*)(in + (long long)r * n + c);
+      b += *(const f32x4*)(in + (long long)(r + 16) * n + c);
+    }
+    if (r < R) a += *(const f32x4*)(in + (long long)r * n + c);
+  }
+  red[rl][q] = a + b;
+  __syncthreads();
+  if (rl == 0 && c < n) {
+    f32x4 s = red[0][q];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) s += red[k][q];
+    s *= scale;
+    if (accumulate) s += *(const f32x4*)(out + c);
+    *(f32x4*)(out + c) = s;
+  }
+}
+
 // column sums of a bf16 [R][C] matrix into fp32 out[C] (bias gradients)
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16* __restrict__ x, int R, int C, int ld,
                                                      float* __restrict__ out, int accumulate) {
@@ -780,6 +809,18 @@ extern "C" int rk_rows_reduce(const float* in, int R, long long W, int G, float*
   if (G <= 0 || G > 65535) return RK_EBADARG;
   dim3 grid((unsigned)((W + 255) / 256), (unsigned)G);
   hipLaunchKernelGGL(rows_reduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, R, W, out);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_fold_rows(const float* in, int R, long long n, float* out, int accumulate, float scale,
+                            void* stream) {
+  if (R <= 0 || n <= 0) return RK_EBADARG;
+  if (n % 4) return RK_EUNSUPPORTED;
+  const long long blocks = (n + 63) / 64;
+  if (blocks > 0x7fffffffLL) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(fold_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in, R, n, out,
+                     accumulate, scale);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -49,6 +49,7 @@ _SIGS = {
     "rk_adam_step": [vp, vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, f32, i32, f32, f32, f32, vp, vp, vp],
     "rk_add_int": [vp, i32, vp],
     "rk_rows_reduce": [vp, i32, i64, i32, vp, vp],
+    "rk_fold_rows": [vp, i32, i64, vp, i32, f32, vp],
     "rk_lerp": [vp, vp, vp, i64, f32, vp],
     "rk_zero32": [vp, i64, vp],
     "rk_adam_multi": [vp, vp, vp, vp, vp, vp, i32, vp, f32, f32, f32, f32, i32, f32, vp, vp, vp],

@@ -800,11 +800,20 @@ def nonfinite_flag(x, flag):
     _lib.call("rk_nonfinite", _p(x), x.numel(), _p(flag), _s())
 
 
+# more than 16 slabs: one block-cooperative pass (rk_fold_rows) instead of rows_reduce + reduce_slabs
+FOLD_ROWS = os.environ.get('RAFIKI_FOLD_ROWS', '1') != '0'
+
+
 def reduce_slabs(slab, out, *, accumulate=False, scale=1.0):
-    if slab.shape[0] > 16:
-        slab = rows_reduce(slab, min(16, cdiv(slab.shape[0], 16)))
+    """out (+)= scale * sum_s slab[s] (slab [S][...] with out.numel() elements per slab)."""
     S = slab.shape[0]
     n = out.numel()
+    if S > 16:
+        if FOLD_ROWS and n % 4 == 0 and slab.is_contiguous() and out.is_contiguous():
+            _lib.call("rk_fold_rows", _p(slab), S, n, _p(out), int(accumulate), float(scale), _s())
+            return out
+        slab = rows_reduce(slab, min(16, cdiv(S, 16)))
+        S = slab.shape[0]
     _lib.call("rk_reduce_slabs", _p(slab), S, n, _p(out), int(accumulate), float(scale), _s())
     return out
 
