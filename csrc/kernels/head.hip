@@ -9,7 +9,7 @@
 //   head_fwd_bwd (one wave per row b):  logits = z W^T + bias; log-softmax; loss / #correct;
 //     dlogits = (softmax - onehot(y)) * grad_scale over the ncls real classes (0 in the padding);
 //     dz = (dlogits W) gated by z > 0 (the hidden layer's ReLU; ungated without a gate)
-//   head_dw (one block per 32 columns k):  dW[c][k] = sum_b dlogits[b][c] z[b][k], db[c] = sum_b dlogits[b][c]
+//   head_dw (one block per 8 columns k):  dW[c][k] = sum_b dlogits[b][c] z[b][k], db[c] = sum_b dlogits[b][c]
 //     and, for the hidden layer, dbh[k] = sum_b dz[b][k] (its bias gradient)
 // Reference: TfFeedForward.py / TfVgg16.py Dense(softmax) + categorical cross-entropy.
 #include "common.h"
@@ -87,23 +87,26 @@ __global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const float* __restri
   }
 }
 
-// 256 threads = 8 row groups x 32 columns; rows b = rg, rg + 8, ... ; the 8 partial sums per output are
-// combined through LDS in a fixed order
+// 256 threads = 32 row groups x 8 columns (D / 8 blocks: 64 at D = 512, so the 32-step row loop of the
+// 32-column form — 16 blocks, 18 us in profiles/vgg_small_f32_step_kernels_r6.txt — becomes 8 steps over
+// four times the CUs); rows b = rg, rg + 32, ... ; the 32 partial sums per output are combined through LDS
+// in a fixed order
 template <int NC>
 __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ z, const float* __restrict__ dlogits,
                                                       const float* __restrict__ dz, int B, int D,
                                                       float* __restrict__ dw, float* __restrict__ db,
                                                       float* __restrict__ dbh) {
-  __shared__ float red[8][NC + 1][32];
-  __shared__ float dbr[8][NC];
-  const int kk = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int k = blockIdx.x * 32 + kk;
+  constexpr int CB = 8, RG = 256 / CB;
+  __shared__ float red[RG][NC + 1][CB];
+  __shared__ float dbr[RG][NC];
+  const int kk = threadIdx.x % CB, rg = threadIdx.x / CB;
+  const int k = blockIdx.x * CB + kk;
   const bool dbl = blockIdx.x == 0 && kk == 0 && db;   // block 0 also sums dlogits' columns (the bias gradient)
   float acc[NC], dba[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[c] = dba[c] = 0.f;
   float hs = 0.f;
-  for (int b = rg; b < B; b += 8) {
+  for (int b = rg; b < B; b += RG) {
     const float zv = z[(long long)b * D + k];
     const float* gr = dlogits + (long long)b * NC;
 #pragma unroll
@@ -122,19 +125,19 @@ __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ 
     for (int c = 0; c < NC; ++c) dbr[rg][c] = dba[c];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < (NC + 1) * 32; i += 256) {
-    const int c = i >> 5, col = i & 31;
+  for (int i = threadIdx.x; i < (NC + 1) * CB; i += 256) {
+    const int c = i / CB, col = i % CB;
     float s = 0.f;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) s += red[r][c][col];
-    const int kc = blockIdx.x * 32 + col;
+    for (int r = 0; r < RG; ++r) s += red[r][c][col];
+    const int kc = blockIdx.x * CB + col;
     if (c < NC) dw[(long long)c * D + kc] = s;
     else if (dbh) dbh[kc] = s;
   }
-  if (blockIdx.x == 0 && db && threadIdx.x < NC) {   // 8 row-group partials of the bias gradient, in order
+  if (blockIdx.x == 0 && db && threadIdx.x < NC) {   // the row-group partials of the bias gradient, in order
     float s = 0.f;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) s += dbr[r][threadIdx.x];
+    for (int r = 0; r < RG; ++r) s += dbr[r][threadIdx.x];
     db[threadIdx.x] = s;
   }
 }
@@ -163,11 +166,11 @@ extern "C" int rk_head_fwd_bwd(const float* z, int B, int D, const float* w, con
 }
 
 // dw [NC][D] = dlogits^T z, db [NC] = column sums of dlogits (nullable), dbh [D] = column sums of dz
-// (nullable: the hidden layer's bias gradient); D % 32 == 0.
+// (nullable: the hidden layer's bias gradient); D % 8 == 0.
 extern "C" int rk_head_dw(const float* z, const float* dlogits, const float* dz, int B, int D, int NC, float* dw,
                           float* db, float* dbh, void* stream) {
-  if (B <= 0 || D <= 0 || (D & 31) || !dw || (dbh && !dz)) return RK_EBADARG;
-  const dim3 grid(D / 32), block(256);
+  if (B <= 0 || D <= 0 || (D & 7) || !dw || (dbh && !dz)) return RK_EBADARG;
+  const dim3 grid(D / 8), block(256);
   const hipStream_t st = (hipStream_t)stream;
   switch (NC) {
     case 8: hipLaunchKernelGGL(head_dw_kernel<8>, grid, block, 0, st, z, dlogits, dz, B, D, dw, db, dbh); break;
