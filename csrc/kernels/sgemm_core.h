@@ -97,18 +97,31 @@ RK_DEV void s_hw(int k, int H, int W, int log2H, int log2W, float invH, float in
 }
 
 // x = hi + mid + lo for 8 fp32 values (two 4-value fragments): bf16 round-to-nearest of x, then of
-// the residuals (x - hi and x - hi - mid are exact in fp32)
+// the residuals (x - hi and x - hi - mid are exact in fp32).  Written pairwise so every step is one packed
+// instruction per two values — v_cvt_pk_bf16_f32 rounds a pair, the pair's fp32 values come back with one
+// shift and one mask, v_pk_add_f32 forms both residuals: 36 VALU per 8 values (the per-element form
+// compiled to 44)
+typedef __attribute__((ext_vector_type(2))) float x6_f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 x6_bf16x2;
+typedef __attribute__((ext_vector_type(4))) unsigned x6_u32x4;
+RK_DEV x6_f32x2 x6_unpack(unsigned w) {
+  return (x6_f32x2){__builtin_bit_cast(float, w << 16), __builtin_bit_cast(float, w & 0xffff0000u)};
+}
 RK_DEV void split3(const f32x4& v0, const f32x4& v1, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+  unsigned hw[4], mw[4], lw[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float x = e < 4 ? v0[e] : v1[e - 4];
-    const bf16 h = (bf16)x;
-    const float r = x - (float)h;
-    const bf16 m = (bf16)r;
-    hi[e] = h;
-    mid[e] = m;
-    lo[e] = (bf16)(r - (float)m);
+  for (int p = 0; p < 4; ++p) {
+    const x6_f32x2 x = p < 2 ? (x6_f32x2){v0[2 * p], v0[2 * p + 1]} : (x6_f32x2){v1[2 * p - 4], v1[2 * p - 3]};
+    const unsigned h = __builtin_bit_cast(unsigned, __builtin_convertvector(x, x6_bf16x2));
+    const x6_f32x2 r = x - x6_unpack(h);
+    const unsigned m = __builtin_bit_cast(unsigned, __builtin_convertvector(r, x6_bf16x2));
+    lw[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(r - x6_unpack(m), x6_bf16x2));
+    hw[p] = h;
+    mw[p] = m;
   }
+  hi = __builtin_bit_cast(bf16x8, (x6_u32x4){hw[0], hw[1], hw[2], hw[3]});
+  mid = __builtin_bit_cast(bf16x8, (x6_u32x4){mw[0], mw[1], mw[2], mw[3]});
+  lo = __builtin_bit_cast(bf16x8, (x6_u32x4){lw[0], lw[1], lw[2], lw[3]});
 }
 
 RK_DEV f32x16 mfma6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh, const bf16x8& bm,
