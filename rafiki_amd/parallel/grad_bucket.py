@@ -7,7 +7,11 @@ all-reduces over contiguous slices of the FlatParams gradient buffer:
 * buckets are contiguous ranges of the arena in REVERSE parameter order (backward produces the
   last layers' gradients first), each ~``bucket_mb`` MiB.  On xGMI a ring all-reduce is bound by
   one 153 GB/s link per hop, so a 16-32 MiB bucket amortises the ~10-20 us launch/latency to <5%
-  while still giving several buckets to overlap with the remaining backward (SURVEY §2.5 C1);
+  while still giving several buckets to overlap with the remaining backward; PG-GAN
+  runs 4 MiB (models/pg_gan.py grad_bucket_mb): one 3x3x512x512 conv per bucket, so the untouched
+  blocks above the current LOD are skipped exactly and the first reduces start early — the measured
+  per-rank rounds and the traced completion points put that ahead of 16-32 MiB at N = 2-8
+  (profiles/pggan_comm_model_r6.json);
 * a ``register_post_accumulate_grad_hook`` per parameter counts arrivals; when a bucket is
   complete its all-reduce is launched asynchronously (``async_op=True``) on RCCL's internal
   stream, overlapping the rest of the backward;
@@ -30,10 +34,11 @@ all-reduces over contiguous slices of the FlatParams gradient buffer:
       per-variable nccl all_sum as soon as its gradient exists).  No collective is ever inside a
       capture, and no event crosses a graph boundary (HIP refuses external event records during
       capture: ``profiles/graph_external_events_r5.txt``).
-  Every rank reduces the live buckets in ascending bucket order (reverse parameter order, roughly
-  the order the backward completes them), a bucket as soon as it and every lower one are complete:
-  the order the collectives are issued in never depends on a rank's own autograd order, which a
-  per-rank autotuner pick can change.  The reduce segment that follows waits for every launched
+  Every rank reduces the live buckets in ONE order: rank 0's completion order of its last tracing
+  run, broadcast (``_agree_order``), a bucket as soon as it and every bucket before it in that order
+  are complete — so the order the collectives are issued in never depends on a rank's own autograd
+  order, which a per-rank autotuner pick can change (ascending bucket order would not do: WGAN-GP's
+  double backward completes the output layers' buckets last, leaving nothing to overlap).  The reduce segment that follows waits for every launched
   bucket (the current stream waits on RCCL's), so the mean + optimizer graph starts after all of
   them.  The first reduce of each plan compares a digest of it across the group and raises on a
   mismatch instead of hanging in mismatched collectives.
