@@ -202,6 +202,26 @@ __global__ __launch_bounds__(256) void lerp_kernel(float* __restrict__ dst, cons
   }
 }
 
+// lerp_kernel over the chunk table's ranges (16-B aligned): the same per-element arithmetic, 16-B vectors
+__global__ __launch_bounds__(256) void lerp_multi_kernel(float* __restrict__ dst, const float* __restrict__ src,
+                                                         bf16* __restrict__ dstb, const long long* __restrict__ blk,
+                                                         float t) {
+  const long long* e = blk + 3 * (long long)blockIdx.x;
+  for (long long i = (e[1] >> 2) + threadIdx.x; i < (e[2] >> 2); i += 256) {
+    const f32x4 s = ((const f32x4*)src)[i], d = ((const f32x4*)dst)[i];
+    f32x4 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = s[k] + (d[k] - s[k]) * t;
+    ((f32x4*)dst)[i] = r;
+    if (dstb) {
+      bf16x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (bf16)r[k];
+      ((bf16x4*)dstb)[i] = o;
+    }
+  }
+}
+
 // dst[0 .. n) = 0 for any 4-byte element type: 16-B vector stores, a scalar tail
 __global__ __launch_bounds__(256) void zero32_kernel(unsigned* __restrict__ dst, long long n) {
   const long long n4 = n >> 2;
@@ -842,6 +862,16 @@ extern "C" int rk_zero_multi(void* dst, const long long* blk, int nblk, void* st
   if (nblk <= 0 || !blk || !dst) return RK_EBADARG;
   if (((unsigned long long)dst) & 15) return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(zero_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, (unsigned*)dst, blk);
+  RK_LAUNCH_CHECK();
+  return RK_OK;
+}
+
+extern "C" int rk_lerp_multi(float* dst, const float* src, void* dstb, const long long* blk, int nblk, float t,
+                             void* stream) {
+  if (nblk <= 0 || !blk || !dst || !src) return RK_EBADARG;
+  if ((((unsigned long long)dst) | ((unsigned long long)src) | ((unsigned long long)dstb)) & 15) return RK_EUNSUPPORTED;
+  hipLaunchKernelGGL(lerp_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, dst, src, (bf16*)dstb,
+                     blk, t);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

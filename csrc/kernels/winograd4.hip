@@ -2040,13 +2040,21 @@ extern "C" int rk_wino4_pt_conv_out(const float* yt, float* y, const float* bias
   const long long blocks = ((N + 63) / 64) * ((T + 3) / 4);
   if (nslab > 1 && slab < 36 * T * N) return RK_EBADARG;
   const long long qs = tmajor ? N : T * N, ts = tmajor ? 36LL * N : N;
-  // vector width 2 (8-B accesses): measured against 4 (16-B, more registers) and 1 (the scalar kernel),
-  // profiles/vgg_small_f32_step_kernels_r3*.txt
-  constexpr int vw = 2;
+  // vector width 2 (8-B accesses, 2 tiles x 64 channels per block) by default; RAFIKI_PT_OUT_VW=4 selects the
+  // 16-B form: -4 us per VGG-small step but +45 us per PG-GAN lod-3 round and +0.23 ms at lod 0 on the same
+  // box (profiles/pt_out_vw_ab_r6.txt)
+  static const int vw = [] {
+    const char* e = std::getenv("RAFIKI_PT_OUT_VW");
+    return e && std::atoi(e) == 4 ? 4 : 2;
+  }();
   if (N % vw == 0) {
-    const long long blocksv = ((N + 63) / 64) * ((T + 1) / 2);
-    hipLaunchKernelGGL(w4pt_conv_outv_kernel<vw>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
-                       bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
+    const long long blocksv = ((N + 63) / 64) * ((T + vw - 1) / vw);   // vw tiles x 64 channels per block
+    if (vw == 4)
+      hipLaunchKernelGGL(w4pt_conv_outv_kernel<4>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
+    else
+      hipLaunchKernelGGL(w4pt_conv_outv_kernel<2>, dim3((unsigned)blocksv), dim3(64), 0, (hipStream_t)stream, yt, y,
+                         bias, stats, slotMask, gate, Nb, H, W, N, TW, THW, (int)T, flags, nslab, slab, qs, ts, slope);
     RK_LAUNCH_CHECK();
     return RK_OK;
   }

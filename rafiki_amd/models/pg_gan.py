@@ -72,6 +72,8 @@ def _pad8(n):
 # Winograd paths need C % 8 == 0; 32 would also admit the pre-split X6 GEMMs, whose K step is 32: same-box
 # lod 3 3.90 / 3.91 ms at 32 vs 3.88 / 3.89 at 8, profiles/pg_gan_mbstd_pad_ab_r6.txt)
 MBSTD_PAD = int(os.environ.get('RAFIKI_MBSTD_PAD', '8'))
+# the Gs EMA over the G ranges that ever trained only (bit-identical; RAFIKI_GS_TRIM=0: the whole arena)
+GS_TRIM = os.environ.get('RAFIKI_GS_TRIM', '1') != '0'
 
 
 # ============================================================================== networks
@@ -103,6 +105,9 @@ class PgNetworks:
         self.D.build()
         self.Gs_master = self.G.master.clone()
         self.Gs_bf16 = self.Gs_master.to(torch.bfloat16) if bf else None
+        # G parameters whose Gs may differ from G (None: any): Gs starts as a bit copy of G, and a weight
+        # Adam never touched keeps Gs == G exactly under the EMA, so update_Gs may skip it
+        self.gs_moved = set()
         self.g_params = self._leaves(self.G)
         self.d_params = self._leaves(self.D)
 
@@ -278,9 +283,15 @@ class PgNetworks:
         return out[:, 0], out[:, 1:1 + self.label_size]
 
     # -- Gs moving average (pg_gans.py:1247 setup_as_moving_average_of, beta = G_smoothing)
-    def update_Gs(self, beta):
+    def update_Gs(self, beta, table=None):
+        """Gs <- G + (Gs - G) * beta; ``table`` (a SegTable over the G ranges that ever trained, see
+        PgGan._gs_table): the same update over those ranges only — bit-identical, since everywhere else
+        G - Gs is exactly zero."""
         if self.device.type == 'cuda':
             from rafiki_amd.ops import functional as F
+            if table is not None:
+                F.lerp_multi(self.Gs_master, self.G.master, beta, table, dst_bf16=self.Gs_bf16)
+                return
             F.lerp_(self.Gs_master, self.G.master, beta, dst_bf16=self.Gs_bf16)
         else:
             self.Gs_master.copy_(self.G.master + (self.Gs_master - self.G.master) * beta)
@@ -293,6 +304,7 @@ class PgNetworks:
                 'Gs': {s.name: _view(self.Gs_master, s).detach().cpu().numpy().copy() for s in self.G.specs}}
 
     def load_state(self, st):
+        self.gs_moved = None   # a restored Gs may differ from G anywhere
         self.G.load_state_dict(st['G'])
         self.D.load_state_dict(st['D'])
         for s in self.G.specs:
@@ -834,7 +846,7 @@ class PgGan(BaseModel):
         round is captured whole by GraphedRounds."""
         for _ in range(D_repeats):
             self._d_step(lod, mb, level, labels_all, rng, D_opt, d_ar, acc=acc)
-            self.nets.update_Gs(G_smoothing)
+            self._update_Gs(G_smoothing)
         self._g_step(lod, mb, labels_all, rng, G_opt, g_ar, acc=acc)
 
     # -- live arena ranges: at a given LOD only the layers up to its resolution receive gradients (at the
@@ -850,11 +862,33 @@ class PgGan(BaseModel):
             return
         g, d = self.nets.live_names(lod)
         self._live = {id(self.nets.G): self.nets.G.ranges_of(g), id(self.nets.D): self.nets.D.ranges_of(d)}
+        if self.nets.gs_moved is not None:
+            self.nets.gs_moved |= set(g)
+
+    def _update_Gs(self, beta):
+        """The Gs EMA over the G ranges whose Gs may differ from G (every range Adam has stepped since Gs
+        was a copy of G: at the reference schedule's lod 3 a third of the arena), or the whole arena (live
+        ranges off, a restored state, the CPU)."""
+        nets = self.nets
+        if self.device.type != 'cuda' or self._live is None or nets.gs_moved is None or not GS_TRIM:
+            nets.update_Gs(beta)
+            return
+        rng = nets.G.ranges_of(sorted(nets.gs_moved))
+        tab = self._seg_table(nets.G, rng, key='Gs')
+        if tab is not None:
+            nets.update_Gs(beta, tab)
+        elif len(rng) == 1:
+            from rafiki_amd.ops import functional as F
+            a, b = rng[0]
+            F.lerp_(nets.Gs_master[a:b], nets.G.master[a:b], beta,
+                    dst_bf16=None if nets.Gs_bf16 is None else nets.Gs_bf16[a:b])
+        else:
+            nets.update_Gs(beta)
 
     def _live_of(self, flat):
         return None if self._live is None else self._live.get(id(flat))
 
-    def _seg_table(self, flat, live):
+    def _seg_table(self, flat, live, key=None):
         """The cached multi-segment chunk table of ``live`` (None: per-range launches — on the CPU, for
         unaligned ranges, or when the table would have to be built inside a capture)."""
         if self.device.type != 'cuda' or live is None or len(live) < 2:
@@ -863,7 +897,7 @@ class PgGan(BaseModel):
         if not F.seg_table_ok(live):
             return None
         tabs = self.__dict__.setdefault('_seg_tables', {})
-        key = (id(flat), tuple(live))
+        key = (id(flat), key, tuple(live))
         tab = tabs.get(key)
         if tab is None and not F._capturing():
             tab = tabs[key] = F.SegTable(self.device, live)
@@ -914,7 +948,7 @@ class PgGan(BaseModel):
         def d_apply():
             d_ar.scale()
             self._apply(nets.D, D_opt, rng)
-            nets.update_Gs(G_smoothing)
+            self._update_Gs(G_smoothing)
 
         def g_grads():
             self._g_step(lod, mb, labels_all, rng, G_opt, None, apply=False, acc=acc)

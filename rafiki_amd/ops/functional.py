@@ -768,6 +768,11 @@ def zero_multi(t, table: SegTable):
     _lib.call("rk_zero_multi", _p(t), _p(table.blk), table.nblk, _s())
 
 
+def lerp_multi(dst, src, t, table: SegTable, dst_bf16=None):
+    """lerp_ (dst <- src + (dst - src) * t, + the bf16 copy) over the segments of ``table`` only."""
+    _lib.call("rk_lerp_multi", _p(dst), _p(src), _p(dst_bf16), _p(table.blk), table.nblk, float(t), _s())
+
+
 def nonfinite_multi(x, table: SegTable, flag):
     _lib.call("rk_nonfinite_multi", _p(x), _p(table.blk), table.nblk, _p(flag), _s())
 

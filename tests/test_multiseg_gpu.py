@@ -77,3 +77,49 @@ def test_zero_and_nonfinite_multi():
     f.grad[s2.offset] = float('inf')  # outside the ranges: not seen
     F.nonfinite_multi(f.grad, tab, flag)
     assert int(flag.item()) == 0
+
+
+def test_lerp_multi_matches_lerp():
+    """lerp_multi_kernel: the Gs EMA over chunk-table ranges, bit-identical to lerp_ on those ranges (fp32
+    and the bf16 copy), everything outside untouched."""
+    from rafiki_amd.ops import functional as F
+    f = _flat()
+    g = torch.Generator().manual_seed(3)
+    dst = torch.randn(f.master.shape, generator=g).to(DEV)
+    live = f.ranges_of(['p0', 'p1', 'p4'])
+    tab = F.SegTable(f.device, live)
+    a, ab = dst.clone(), torch.zeros(dst.shape, dtype=torch.bfloat16, device=DEV)
+    b, bb = dst.clone(), ab.clone()
+    F.lerp_multi(a, f.master, 0.99, tab, dst_bf16=ab)
+    for lo, hi in live:
+        F.lerp_(b[lo:hi], f.master[lo:hi], 0.99, dst_bf16=bb[lo:hi])
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(ab, bb)
+
+
+def test_pg_gan_trimmed_gs_ema_bit_identical():
+    """PgGan._update_Gs at lod 3 (only the G ranges Adam stepped, one multi-segment launch) == the whole-arena
+    EMA, bit for bit: outside those ranges G - Gs is exactly zero.  A restored state falls back to the full
+    EMA (its Gs may differ from G anywhere)."""
+    from rafiki_amd.models.pg_gan import PgGan
+    from rafiki_amd.ops import functional as F
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    with use_context(TrialContext(device=torch.device(DEV))):
+        m = PgGan(D_repeats=1, minibatch_base=16)
+        m._build([1, 32, 32], 0)
+    nets = m.nets
+    m.set_lod_live(3.0)
+    rng = nets.G.ranges_of(sorted(nets.gs_moved))
+    assert sum(b - a for a, b in rng) < nets.G.master.numel() // 2
+    gen = torch.Generator().manual_seed(5)
+    for _ in range(3):
+        for a, b in m._live[id(nets.G)]:      # what Adam changes at this LOD
+            nets.G.master[a:b] += 1e-3 * torch.randn(b - a, generator=gen).to(DEV)
+        ref = nets.Gs_master.clone()
+        F.lerp_(ref, nets.G.master, 0.99)     # the whole-arena EMA
+        m._update_Gs(0.99)
+        torch.cuda.synchronize()
+        assert torch.equal(nets.Gs_master, ref)
+    assert any(k[1] == 'Gs' for k in m._seg_tables) or len(rng) == 1
+    nets.load_state(nets.state())
+    assert nets.gs_moved is None
