@@ -175,13 +175,19 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(float* __restrict__ w, 
   }
 }
 
-__global__ __launch_bounds__(256) void zero_multi_kernel(unsigned* __restrict__ dst, const long long* __restrict__ blk) {
+// flag (nullable): also zeroed (the step's finite-check flag, so the check needs no launch of its own)
+__global__ __launch_bounds__(256) void zero_multi_kernel(unsigned* __restrict__ dst, const long long* __restrict__ blk,
+                                                         int* __restrict__ flag) {
+  if (flag && blockIdx.x == 0 && threadIdx.x == 0) *flag = 0;
   const long long* e = blk + 3 * (long long)blockIdx.x;
   for (long long i = (e[1] >> 2) + threadIdx.x; i < (e[2] >> 2); i += 256) ((uint4*)dst)[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
+// bump (nullable): block 0 also advances this int32 step counter (the optimizer's, read by the next launch)
 __global__ __launch_bounds__(256) void nonfinite_multi_kernel(const float* __restrict__ x,
-                                                              const long long* __restrict__ blk, int* flag) {
+                                                              const long long* __restrict__ blk, int* flag,
+                                                              int* __restrict__ bump) {
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
   const long long* e = blk + 3 * (long long)blockIdx.x;
   int bad = 0;
   for (long long i = (e[1] >> 2) + threadIdx.x; i < (e[2] >> 2); i += 256) {
@@ -858,10 +864,11 @@ extern "C" int rk_adam_multi(float* w, void* wb, const float* g, float* m, float
   return RK_OK;
 }
 
-extern "C" int rk_zero_multi(void* dst, const long long* blk, int nblk, void* stream) {
+extern "C" int rk_zero_multi(void* dst, const long long* blk, int nblk, int* flag, void* stream) {
   if (nblk <= 0 || !blk || !dst) return RK_EBADARG;
   if (((unsigned long long)dst) & 15) return RK_EUNSUPPORTED;
-  hipLaunchKernelGGL(zero_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, (unsigned*)dst, blk);
+  hipLaunchKernelGGL(zero_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, (unsigned*)dst, blk,
+                     flag);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
@@ -876,10 +883,12 @@ extern "C" int rk_lerp_multi(float* dst, const float* src, void* dstb, const lon
   return RK_OK;
 }
 
-extern "C" int rk_nonfinite_multi(const float* x, const long long* blk, int nblk, int* flag, void* stream) {
+extern "C" int rk_nonfinite_multi(const float* x, const long long* blk, int nblk, int* flag, int* bump,
+                                  void* stream) {
   if (nblk <= 0 || !blk || !x || !flag) return RK_EBADARG;
   if (((unsigned long long)x) & 15) return RK_EUNSUPPORTED;
-  hipLaunchKernelGGL(nonfinite_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, blk, flag);
+  hipLaunchKernelGGL(nonfinite_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, blk, flag,
+                     bump);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

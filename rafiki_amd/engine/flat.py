@@ -237,10 +237,11 @@ class FlatAdam:
         self.v.zero_()
         self.t.zero_()
 
-    def step(self, live=None):
+    def step(self, live=None, bumped=False):
         """``live``: arena ranges [(a, b)] to update (None: the whole arena).  Only exact for ranges
         left out whose gradient AND first moment are zero (an untouched parameter with beta1 = 0, or
-        one never touched since reset_state): Adam then leaves the weight unchanged."""
+        one never touched since reset_state): Adam then leaves the weight unchanged.  ``bumped``: the
+        device step counter was already advanced for this step (by the finite-check launch)."""
         f = self.flat
         # Equalized LR (pg_gans.py:1006-1013) is applied by re-parameterisation: the arena holds the
         # EFFECTIVE weights c*w, stepped with lr*c and eps*c — algebraically identical to Adam on w.
@@ -249,7 +250,8 @@ class FlatAdam:
             segs = [(max(a, c), min(b, d), wd, mult) for a, b, wd, mult in segs for c, d in live
                     if min(b, d) > max(a, c)]
         if f.device.type == 'cuda':
-            F.add_int_(self.t, 1)
+            if not bumped:
+                F.add_int_(self.t, 1)
             if live is not None and len(segs) > 1 and F.seg_table_ok([(a, b) for a, b, _, _ in segs]):
                 # every live segment in one launch (per-segment lr / eps / wd from a cached device table)
                 key = (tuple(segs), self.lr, self.eps)

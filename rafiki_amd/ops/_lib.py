@@ -54,8 +54,8 @@ _SIGS = {
     "rk_zero32": [vp, i64, vp],
     "rk_adam_multi": [vp, vp, vp, vp, vp, vp, i32, vp, f32, f32, f32, f32, i32, f32, vp, vp, vp],
     "rk_lerp_multi": [vp, vp, vp, vp, i32, f32, vp],
-    "rk_zero_multi": [vp, vp, i32, vp],
-    "rk_nonfinite_multi": [vp, vp, i32, vp, vp],
+    "rk_zero_multi": [vp, vp, i32, vp, vp],
+    "rk_nonfinite_multi": [vp, vp, i32, vp, vp, vp],
     "rk_nonfinite": [vp, i64, vp, vp],
     "rk_reduce_slabs": [vp, i32, i64, vp, i32, f32, vp],
     "rk_colsum": [vp, i32, i32, i32, vp, i32, vp],

@@ -764,8 +764,9 @@ def adam_multi(w, g, m, v, table: SegTable, *, wb=None, beta1, beta2, decoupled=
               _p(skip_flag), _p(step_tensor), _s())
 
 
-def zero_multi(t, table: SegTable):
-    _lib.call("rk_zero_multi", _p(t), _p(table.blk), table.nblk, _s())
+def zero_multi(t, table: SegTable, flag=None):
+    """Zero ``t`` over the table's ranges (and the int32 ``flag``) in one launch."""
+    _lib.call("rk_zero_multi", _p(t), _p(table.blk), table.nblk, _p(flag), _s())
 
 
 def lerp_multi(dst, src, t, table: SegTable, dst_bf16=None):
@@ -773,8 +774,10 @@ def lerp_multi(dst, src, t, table: SegTable, dst_bf16=None):
     _lib.call("rk_lerp_multi", _p(dst), _p(src), _p(dst_bf16), _p(table.blk), table.nblk, float(t), _s())
 
 
-def nonfinite_multi(x, table: SegTable, flag):
-    _lib.call("rk_nonfinite_multi", _p(x), _p(table.blk), table.nblk, _p(flag), _s())
+def nonfinite_multi(x, table: SegTable, flag, bump=None):
+    """flag |= any non-finite element over the table's ranges; ``bump``: an int32 step counter the same launch
+    advances (for the optimizer launch that follows)."""
+    _lib.call("rk_nonfinite_multi", _p(x), _p(table.blk), table.nblk, _p(flag), _p(bump), _s())
 
 
 def _capturing() -> bool:

@@ -123,3 +123,36 @@ def test_pg_gan_trimmed_gs_ema_bit_identical():
     assert any(k[1] == 'Gs' for k in m._seg_tables) or len(rng) == 1
     nets.load_state(nets.state())
     assert nets.gs_moved is None
+
+
+def test_pg_gan_fused_flag_and_counter_bitwise(monkeypatch):
+    """The finite-check flag zeroed by the gradient-zeroing launch and the Adam step counter advanced by the
+    finite-check launch (PgGan._zero_grad / _finite_guard) give the same weights, bit for bit, as the
+    per-range launches with their own zeroing and counter kernels; the counters advance once per step."""
+    from rafiki_amd.engine.flat import FlatAdam
+    from rafiki_amd.models.pg_gan import PgGan, TrialRng
+    from rafiki_amd.ops import functional as F
+    from rafiki_amd.parallel.context import TrialContext, use_context
+    out = []
+    for multi in (True, False):
+        monkeypatch.setattr(F, 'MULTISEG', multi)
+        with use_context(TrialContext(device=torch.device(DEV))):
+            m = PgGan(D_repeats=1, minibatch_base=16)
+            m._build([1, 32, 32], 0)
+        nets = m.nets
+        G_opt = FlatAdam(nets.G, 1e-3, betas=(0.0, 0.99))
+        D_opt = FlatAdam(nets.D, 1e-3, betas=(0.0, 0.99))
+        for o in (G_opt, D_opt):
+            o.skip_flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+        rng = TrialRng(torch.device(DEV), 0)
+        level = torch.randint(0, 256, (64, 1, 4, 4), dtype=torch.uint8, generator=torch.Generator().manual_seed(1))
+        acc = torch.zeros(6, device=DEV)
+        m.set_lod_live(3.0)
+        for _ in range(3):
+            m.train_round(3.0, 16, level.to(DEV), torch.zeros((64, 0), device=DEV), rng, G_opt, D_opt, acc)
+        torch.cuda.synchronize()
+        assert int(G_opt.t.item()) == 3 and int(D_opt.t.item()) == 3
+        assert int(G_opt.skip_flag.item()) == 0 and int(D_opt.skip_flag.item()) == 0
+        out.append((nets.G.master.clone(), nets.D.master.clone(), nets.Gs_master.clone()))
+    (g1, d1, s1), (g0, d0, s0) = out
+    assert torch.equal(g1, g0) and torch.equal(d1, d0) and torch.equal(s1, s0)
