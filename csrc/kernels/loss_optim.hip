@@ -145,7 +145,10 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(float* __restrict__ w, 
                                                          float* __restrict__ v, const long long* __restrict__ blk,
                                                          const float* __restrict__ segp, float b1, float b2,
                                                          float omb1, float omb2, int decoupled, float gscale,
-                                                         const int* skip, const int* step_ptr) {
+                                                         const int* skip, const int* step_ptr, int* bump) {
+  // bump (nullable): another int32 step counter (the trial's random stream) advanced by block 0 whether or not
+  // the update is skipped, read by later launches only
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
   if (skip && skip[0] != 0) return;
   const int t = step_ptr[0];
   const float c1 = omb1 < 1.f ? (float)(1.0 / (1.0 - pow(1.0 - (double)omb1, t))) : 1.f;
@@ -854,12 +857,12 @@ extern "C" int rk_fold_rows(const float* in, int R, long long n, float* out, int
 // the multi-segment launches: nblk blocks over the chunk table blk (see adam_multi_kernel)
 extern "C" int rk_adam_multi(float* w, void* wb, const float* g, float* m, float* v, const long long* blk, int nblk,
                              const float* segp, float b1, float b2, float omb1, float omb2, int decoupled, float gscale,
-                             const int* skip, const int* step_ptr, void* stream) {
+                             const int* skip, const int* step_ptr, int* bump, void* stream) {
   if (nblk <= 0 || !blk || !segp || !step_ptr) return RK_EBADARG;
   if ((((unsigned long long)w) | ((unsigned long long)g) | ((unsigned long long)m) | ((unsigned long long)v)) & 15)
     return RK_EUNSUPPORTED;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, w, (bf16*)wb, g, m, v,
-                     blk, segp, b1, b2, omb1, omb2, decoupled, gscale, skip, step_ptr);
+                     blk, segp, b1, b2, omb1, omb2, decoupled, gscale, skip, step_ptr, bump);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }

@@ -237,11 +237,13 @@ class FlatAdam:
         self.v.zero_()
         self.t.zero_()
 
-    def step(self, live=None, bumped=False):
+    def step(self, live=None, bumped=False, bump=None):
         """``live``: arena ranges [(a, b)] to update (None: the whole arena).  Only exact for ranges
         left out whose gradient AND first moment are zero (an untouched parameter with beta1 = 0, or
         one never touched since reset_state): Adam then leaves the weight unchanged.  ``bumped``: the
-        device step counter was already advanced for this step (by the finite-check launch)."""
+        device step counter was already advanced for this step (by the finite-check launch).  ``bump``:
+        another int32 device counter to advance in the same launch when the step runs as one
+        multi-segment launch; returns True when it did (the caller advances it otherwise)."""
         f = self.flat
         # Equalized LR (pg_gans.py:1006-1013) is applied by re-parameterisation: the arena holds the
         # EFFECTIVE weights c*w, stepped with lr*c and eps*c — algebraically identical to Adam on w.
@@ -262,8 +264,8 @@ class FlatAdam:
                                                  [(self.lr * mult, self.eps * mult, wd, 0.0) for _, _, wd, mult in segs])
                 if tab is not None:
                     F.adam_multi(f.master, f.grad, self.m, self.v, tab, wb=f.bf16, beta1=self.b1, beta2=self.b2,
-                                 decoupled=self.decoupled, step_tensor=self.t, skip_flag=self.skip_flag)
-                    return
+                                 decoupled=self.decoupled, step_tensor=self.t, skip_flag=self.skip_flag, bump=bump)
+                    return bump is not None
             for a, b, wd, mult in segs:
                 if b > a:
                     F.adam_step(f.master[a:b], f.grad[a:b], self.m[a:b], self.v[a:b],

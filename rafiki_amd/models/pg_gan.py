@@ -993,8 +993,11 @@ class PgGan(BaseModel):
 
     def _apply(self, flat, opt, rng):
         bumped = self._finite_guard(flat, opt)
-        opt.step(live=self._live_of(flat), bumped=bumped)
-        rng.advance()
+        # the multi-segment Adam launch also advances the random stream's step counter (else its own launch)
+        bump = rng.step if self.device.type == 'cuda' and isinstance(getattr(rng, 'step', None), torch.Tensor) \
+            else None
+        if not opt.step(live=self._live_of(flat), bumped=bumped, bump=bump):
+            rng.advance()
 
     def _fused_loss(self, grads=None):
         """The fused WGAN loss head (WganLossFn) applies: fp32 on the GPU, no label logits."""

@@ -52,7 +52,7 @@ _SIGS = {
     "rk_fold_rows": [vp, i32, i64, vp, i32, f32, vp],
     "rk_lerp": [vp, vp, vp, i64, f32, vp],
     "rk_zero32": [vp, i64, vp],
-    "rk_adam_multi": [vp, vp, vp, vp, vp, vp, i32, vp, f32, f32, f32, f32, i32, f32, vp, vp, vp],
+    "rk_adam_multi": [vp, vp, vp, vp, vp, vp, i32, vp, f32, f32, f32, f32, i32, f32, vp, vp, vp, vp],
     "rk_lerp_multi": [vp, vp, vp, vp, i32, f32, vp],
     "rk_zero_multi": [vp, vp, i32, vp, vp],
     "rk_nonfinite_multi": [vp, vp, i32, vp, vp, vp],

@@ -756,12 +756,12 @@ def seg_table_ok(segs) -> bool:
 
 
 def adam_multi(w, g, m, v, table: SegTable, *, wb=None, beta1, beta2, decoupled=False, grad_scale=1.0,
-               skip_flag=None, step_tensor):
+               skip_flag=None, step_tensor, bump=None):
     """Adam over every segment of ``table`` (per-segment lr / eps / wd in table.params) in one launch; same
-    arithmetic per element as adam_step."""
+    arithmetic per element as adam_step.  ``bump``: an int32 counter the launch also advances (always)."""
     _lib.call("rk_adam_multi", _p(w), _p(wb), _p(g), _p(m), _p(v), _p(table.blk), table.nblk, _p(table.params),
               float(beta1), float(beta2), 1.0 - float(beta1), 1.0 - float(beta2), int(decoupled), float(grad_scale),
-              _p(skip_flag), _p(step_tensor), _s())
+              _p(skip_flag), _p(step_tensor), _p(bump), _s())
 
 
 def zero_multi(t, table: SegTable, flag=None):

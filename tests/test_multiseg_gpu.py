@@ -126,9 +126,10 @@ def test_pg_gan_trimmed_gs_ema_bit_identical():
 
 
 def test_pg_gan_fused_flag_and_counter_bitwise(monkeypatch):
-    """The finite-check flag zeroed by the gradient-zeroing launch and the Adam step counter advanced by the
-    finite-check launch (PgGan._zero_grad / _finite_guard) give the same weights, bit for bit, as the
-    per-range launches with their own zeroing and counter kernels; the counters advance once per step."""
+    """The finite-check flag zeroed by the gradient-zeroing launch, the Adam step counter advanced by the
+    finite-check launch and the random stream's counter by the Adam launch (PgGan._zero_grad / _finite_guard /
+    _apply) give the same weights, bit for bit, as the per-range launches with their own zeroing and counter
+    kernels; every counter advances once per step."""
     from rafiki_amd.engine.flat import FlatAdam
     from rafiki_amd.models.pg_gan import PgGan, TrialRng
     from rafiki_amd.ops import functional as F
@@ -152,6 +153,7 @@ def test_pg_gan_fused_flag_and_counter_bitwise(monkeypatch):
             m.train_round(3.0, 16, level.to(DEV), torch.zeros((64, 0), device=DEV), rng, G_opt, D_opt, acc)
         torch.cuda.synchronize()
         assert int(G_opt.t.item()) == 3 and int(D_opt.t.item()) == 3
+        assert int(rng.step.item()) == 6     # advanced once per optimizer step (by the Adam launch when fused)
         assert int(G_opt.skip_flag.item()) == 0 and int(D_opt.skip_flag.item()) == 0
         out.append((nets.G.master.clone(), nets.D.master.clone(), nets.Gs_master.clone()))
     (g1, d1, s1), (g0, d0, s0) = out
