@@ -954,6 +954,8 @@ class PgGan(BaseModel):
         cover only the buckets the segment's backward wrote (untouched blocks above the current LOD
         are skipped exactly).
         """
+        if tag is None:   # plans are per segment shape: never reuse one traced at another LOD / minibatch
+            tag = (float(lod), int(mb))
         nets = self.nets
 
         def d_grads():

@@ -293,7 +293,9 @@ class BucketedGrads:
             b = ar.bucket_of[i]
             if planned and b in order[:nxt[0]]:
                 raise RuntimeError('data-parallel bucket {} received a gradient after its all-reduce was '
-                                   'started (the segment changed since it was traced)'.format(b))
+                                   'started (the segment changed since it was traced: contribution {} of a '
+                                   'traced {}, leaf {})'.format(b, seen.get(b, 0) + 1, count.get(b),
+                                                               tuple(leaf.shape)))
             seen[b] = seen.get(b, 0) + 1
             if extra is not None:
                 extra(leaf)

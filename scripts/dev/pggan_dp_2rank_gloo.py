@@ -57,10 +57,11 @@ def main():
         level = torch.randint(0, 256, (4096, 1, r, r), dtype=torch.uint8, generator=gen).to(dev)
         labels = torch.zeros((4096, 0), device=dev)
         graphs = GraphedRounds(True)
+        m.set_lod_live(lod)   # as PgGan.train / utils.benchmarks.pg_gan_rounds run a level of detail
 
         def rnd():
             graphs.run_segments(lod, m.round_segments(lod, mb, level, labels, rng, G_opt, D_opt, acc, d_ar=d_ar,
-                                                      g_ar=g_ar))
+                                                      g_ar=g_ar, tag=lod))
         for _ in range(3):
             rnd()
         torch.cuda.synchronize()
