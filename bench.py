@@ -437,7 +437,8 @@ def main():
 
     which = _configs(args, world)
     cfgs = {}
-    if 'pggan' in which and n_devices == world:
+    # ranks sharing a GPU (gloo rehearsal) skip it unless RAFIKI_BENCH_PGGAN_REHEARSAL=1 (the spawn / store path)
+    if 'pggan' in which and (n_devices == world or os.environ.get('RAFIKI_BENCH_PGGAN_REHEARSAL') == '1'):
         D.barrier(info)
         _progress(info, 'phase 4: PG-GAN rounds' + (' (data parallel x{})'.format(world) if world > 1 else ''))
         cfgs['pg_gan'] = phase_pg_gan(args, info, dev)
