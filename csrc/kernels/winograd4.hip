@@ -1539,14 +1539,16 @@ __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x
 // window).  One thread per (tile, 4-channel group), tiles fastest, so every bf16 store of a wave writes
 // 64 consecutive tiles of one (position, plane, channel) row.
 // LDS-staged form (T % 32 == 0, C % 8 == 0): one wave per 32 tiles x 8 channels.  Lane (tile tl, 4-channel
-// group g) transforms its window, splits the 36 x 4 values and writes them as bf16 into an LDS image
-// [36][3][8][32 tiles]; the wave then stores 16-B pieces of its 864 (position, plane, channel) rows of 32
-// tiles — 54 vector stores per lane instead of 432 two-byte ones (the T-fastest kernels were store-issue
-// bound: 29.7 / 22.5 us for the 8x8x256 layer, profiles/vgg_small_f32_step_kernels_r4*).
+// group g) transforms its window, splits the 36 x 4 values and writes them as bf16 into an LDS image of 12
+// positions at a time [12][3][8][32 tiles]; the wave then stores 16-B pieces of those 288 (position, plane,
+// channel) rows of 32 tiles — 54 vector stores per lane instead of 432 two-byte ones (the T-fastest kernels
+// were store-issue bound: 29.7 / 22.5 us for the 8x8x256 layer, profiles/vgg_small_f32_step_kernels_r4*).
+// Three 18-KiB rounds instead of one 54-KiB image: 8 waves per CU can be resident instead of 2.
 template <bool DY>
 __global__ __launch_bounds__(64) void w4pt_planesT_kernel(const float* __restrict__ src, bf16* __restrict__ dst,
                                                           int H, int W, int C, int TW, int THW, int T) {
-  __shared__ __attribute__((aligned(16))) bf16 sm[36 * 3 * 8 * 32];
+  constexpr int QG = 12;                   // positions per LDS round
+  __shared__ __attribute__((aligned(16))) bf16 sm[QG * 3 * 8 * 32];
   const int lane = threadIdx.x;
   const int g = lane & 1, tl = lane >> 1;
   const int t = blockIdx.x * 32 + tl, c0 = blockIdx.y * 8 + 4 * g;
@@ -1609,26 +1611,30 @@ __global__ __launch_bounds__(64) void w4pt_planesT_kernel(const float* __restric
         for (int b = 0; b < 6; ++b) res[a * 6 + b][e] = o[b];
       }
   }
-#pragma unroll
-  for (int q = 0; q < 36; ++q)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      bf16 hh, mi, lo;
-      split3v(res[q][e], hh, mi, lo);
-      const int row = (q * 3) * 8 + 4 * g + e;   // (q, plane 0, channel)
-      sm[row * 32 + tl] = hh;
-      sm[(row + 8) * 32 + tl] = mi;
-      sm[(row + 16) * 32 + tl] = lo;
-    }
-  __syncthreads();
-  // 864 rows x 64 B = 3456 pieces of 16 B; row (q, p, c) -> dst[((q * 3 + p) * C + cbase + c) * T + tbase ..]
   const uint4* sv = (const uint4*)sm;
   const int tbase = blockIdx.x * 32, cbase = blockIdx.y * 8;
-  for (int i = lane; i < 864 * 4; i += 64) {
-    const int row = i >> 2, piece = i & 3;
-    const int qp = row >> 3, c = row & 7;
-    bf16* d = dst + ((long long)qp * C + cbase + c) * T + tbase + piece * 8;
-    *(uint4*)d = sv[i];
+#pragma unroll
+  for (int q0 = 0; q0 < 36; q0 += QG) {
+    if (q0) __syncthreads();                 // the previous round's rows are stored
+#pragma unroll
+    for (int qq = 0; qq < QG; ++qq)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bf16 hh, mi, lo;
+        split3v(res[q0 + qq][e], hh, mi, lo);
+        const int row = (qq * 3) * 8 + 4 * g + e;   // (q, plane 0, channel) of this round
+        sm[row * 32 + tl] = hh;
+        sm[(row + 8) * 32 + tl] = mi;
+        sm[(row + 16) * 32 + tl] = lo;
+      }
+    __syncthreads();
+    // 288 rows x 64 B = 1152 pieces of 16 B; row (q, p, c) -> dst[((q * 3 + p) * C + cbase + c) * T + tbase ..]
+    for (int i = lane; i < QG * 3 * 8 * 4; i += 64) {
+      const int row = i >> 2, piece = i & 3;
+      const int qp = q0 * 3 + (row >> 3), c = row & 7;
+      bf16* d = dst + ((long long)qp * C + cbase + c) * T + tbase + piece * 8;
+      *(uint4*)d = sv[i];
+    }
   }
 }
 
