@@ -1719,24 +1719,27 @@ __global__ __launch_bounds__(256) void w4pt_xT_kernel(const float* __restrict__ 
 }
 
 // dU [36][Co][Ci] -> dW [Co][9][Ci] (+= with accumulate); one thread per (co, 4-channel group)
+// VW = 2 channels per thread (72 accumulator registers; the 4-channel form needed all 256 VGPRs, one wave
+// per SIMD, and ran latency-bound on the PG-GAN lod-3 weight gradients)
 __global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__ du, float* __restrict__ out, int Co,
                                                        int Ci, int accumulate, int nslab, long long slab) {
-  const int i = blockIdx.x * 256 + threadIdx.x;   // 4-channel group index in [Co][Ci/4]
+  typedef __attribute__((ext_vector_type(2))) float fv2;
+  const int i = blockIdx.x * 256 + threadIdx.x;   // 2-channel group index in [Co][Ci/2]
   const int plane = Co * Ci;
-  if (i * 4 >= plane) return;
-  const int C4 = Ci >> 2;
-  const int co = i / C4, ci = 4 * (i - co * C4);
+  if (i * 2 >= plane) return;
+  const int C2 = Ci >> 1;
+  const int co = i / C2, ci = 2 * (i - co * C2);
   const float* src = du + co * Ci + ci;
-  f32x4 u[36];
+  fv2 u[36];
 #pragma unroll
-  for (int q = 0; q < 36; ++q) u[q] = *(const f32x4*)(src + q * plane);
+  for (int q = 0; q < 36; ++q) u[q] = *(const fv2*)(src + q * plane);
   for (int k = 1; k < nslab; ++k)   // split-K partial slabs of the GEMM
 #pragma unroll
-    for (int q = 0; q < 36; ++q) u[q] += *(const f32x4*)(src + k * slab + q * plane);
+    for (int q = 0; q < 36; ++q) u[q] += *(const fv2*)(src + k * slab + q * plane);
   float* o = out + co * 9 * Ci + ci;
-  f32x4 w[9];
+  fv2 w[9];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < 2; ++e) {
     float tq[3][6];
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
@@ -1755,7 +1758,7 @@ __global__ __launch_bounds__(256) void w4pt_out_kernel(const float* __restrict__
   }
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    f32x4* d = (f32x4*)(o + k * Ci);
+    fv2* d = (fv2*)(o + k * Ci);
     *d = accumulate ? *d + w[k] : w[k];
   }
 }
@@ -1797,8 +1800,8 @@ extern "C" int rk_wino4_pt_output(const float* du, float* out, int Co, int Ci, i
                                   long long slab, void* stream) {
   if (Co <= 0 || Ci <= 0 || nslab <= 0 || (nslab > 1 && slab < 36ll * Co * Ci)) return RK_EBADARG;
   if ((Ci & 3) || 36ll * Co * Ci >= (1ll << 31)) return RK_EUNSUPPORTED;
-  const long long g4 = (long long)Co * Ci / 4;
-  hipLaunchKernelGGL(w4pt_out_kernel, dim3((unsigned)((g4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, du,
+  const long long g2 = (long long)Co * Ci / 2;
+  hipLaunchKernelGGL(w4pt_out_kernel, dim3((unsigned)((g2 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, du,
                      out, Co, Ci, accumulate, nslab, slab);
   RK_LAUNCH_CHECK();
   return RK_OK;
