@@ -1462,39 +1462,50 @@ __global__ __launch_bounds__(256) void w4pt_dy_kernel(const float* __restrict__ 
 // PL: bf16 X6 planes v [36][3][T][C] (hi, mid, lo) instead of fp32 v [36][T][C]
 // pro (nullable): normalise-on-load — x is the pre-BN output of its producer; relu(x * scale + shift) with
 // scale = pro[0 .. C), shift = pro[C .. 2C) on every in-image element (the padding stays 0)
-template <bool PL = false>
+// VW channels per thread (4 or 2: half the 144 window registers, twice the resident waves)
+template <bool PL = false, int VW = 4>
 __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x, void* __restrict__ v, int H,
                                                      int W, int C, int TW, int THW, int total4, int T,
                                                      const float* __restrict__ pro) {
+  typedef __attribute__((ext_vector_type(VW))) float fvec;
+  typedef __attribute__((ext_vector_type(VW))) __bf16 bvec;
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= total4) return;
-  const int C4 = C >> 2;
-  const int c4 = i % C4, t = i / C4;
+  if (i >= total4) return;            // total4: T * C / VW items
+  const int CV = C / VW;
+  const int cv = i % CV, t = i / CV;
   const int n = t / THW, r = t - n * THW, ty = r / TW;
   const int oy = 4 * ty - 1, ox = 4 * (r - ty * TW) - 1;
-  f32x4 psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f};
+  fvec psc, psh;
+#pragma unroll
+  for (int e = 0; e < VW; ++e) psc[e] = 1.f, psh[e] = 0.f;
   if (pro) {
-    psc = *(const f32x4*)(pro + 4 * c4);
-    psh = *(const f32x4*)(pro + C + 4 * c4);
+    psc = *(const fvec*)(pro + VW * cv);
+    psh = *(const fvec*)(pro + C + VW * cv);
   }
-  f32x4 d[36];
+  fvec d[36];
 #pragma unroll
   for (int a = 0; a < 6; ++a)
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
       const int yy = oy + a, xx = ox + b;
       const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-      f32x4 val = in ? *(const f32x4*)(x + ((n * H + yy) * W + xx) * C + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      fvec val;
+      if (in) {
+        val = *(const fvec*)(x + ((n * H + yy) * W + xx) * C + VW * cv);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VW; ++e) val[e] = 0.f;
+      }
       if (pro && in) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) val[e] = fmaxf(fmaf(val[e], psc[e], psh[e]), 0.f);
+        for (int e = 0; e < VW; ++e) val[e] = fmaxf(fmaf(val[e], psc[e], psh[e]), 0.f);
       }
       d[a * 6 + b] = val;
     }
 #pragma unroll
   for (int b = 0; b < 6; ++b)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < VW; ++e) {
       float o[6];
       bt6(d[b][e], d[6 + b][e], d[12 + b][e], d[18 + b][e], d[24 + b][e], d[30 + b][e], o);
 #pragma unroll
@@ -1503,9 +1514,9 @@ __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x
   const int ps = T * C;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    f32x4 o4[6];
+    fvec o4[6];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < VW; ++e) {
       float o[6];
       bt6(d[a * 6 + 0][e], d[a * 6 + 1][e], d[a * 6 + 2][e], d[a * 6 + 3][e], d[a * 6 + 4][e], d[a * 6 + 5][e], o);
 #pragma unroll
@@ -1514,21 +1525,21 @@ __global__ __launch_bounds__(256) void w4pt_x_kernel(const float* __restrict__ x
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
       if constexpr (PL) {
-        bf16x4 h4, m4, l4;
+        bvec h4, m4, l4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < VW; ++e) {
           bf16 hh, mm, ll;
           split3v(o4[b][e], hh, mm, ll);
           h4[e] = hh;
           m4[e] = mm;
           l4[e] = ll;
         }
-        bf16x4* dst = (bf16x4*)((bf16*)v + (long long)(a * 6 + b) * 3 * ps + t * C + 4 * c4);
+        bvec* dst = (bvec*)((bf16*)v + (long long)(a * 6 + b) * 3 * ps + t * C + VW * cv);
         dst[0] = h4;
-        dst[ps / 4] = m4;
-        dst[ps / 2] = l4;
+        dst[ps / VW] = m4;
+        dst[2 * (ps / VW)] = l4;
       } else {
-        *(f32x4*)((float*)v + (long long)(a * 6 + b) * ps + t * C + 4 * c4) = o4[b];
+        *(fvec*)((float*)v + (long long)(a * 6 + b) * ps + t * C + VW * cv) = o4[b];
       }
     }
   }
@@ -2100,9 +2111,19 @@ extern "C" int rk_x6p_w4_input_pro(const float* x, void* v, int Nb, int H, int W
   const int TW = W / 4, THW = (H / 4) * (W / 4);
   const long long T = (long long)Nb * THW;
   if (108 * T * C >= (1ll << 31) || (long long)Nb * H * W * C >= (1ll << 31)) return RK_EUNSUPPORTED;
-  const long long tx = T * C / 4;
-  hipLaunchKernelGGL(w4pt_x_kernel<true>, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
-                     v, H, W, C, TW, THW, (int)tx, (int)T, pro);
+  // 4 channels per thread by default; RAFIKI_PT_X_VW=2: 2 channels (83 instead of 159 VGPRs, 5 waves per SIMD
+  // instead of 3) — +6 us per VGG-small step, -0.1 ms per PG-GAN lod-0 round (profiles/pt_x_vw_ab_r6.txt)
+  static const int vw = [] {
+    const char* e = std::getenv("RAFIKI_PT_X_VW");
+    return e && std::atoi(e) == 2 ? 2 : 4;
+  }();
+  const long long tx = T * C / vw;
+  if (vw == 4)
+    hipLaunchKernelGGL((w4pt_x_kernel<true, 4>), dim3((unsigned)((tx + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, v, H, W, C, TW, THW, (int)tx, (int)T, pro);
+  else
+    hipLaunchKernelGGL((w4pt_x_kernel<true, 2>), dim3((unsigned)((tx + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, v, H, W, C, TW, THW, (int)tx, (int)T, pro);
   RK_LAUNCH_CHECK();
   return RK_OK;
 }
